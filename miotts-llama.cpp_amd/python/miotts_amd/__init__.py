@@ -1,0 +1,216 @@
+"""ctypes binding over libmiotts.so's C-ABI (include/mio_hip.h).
+
+This is the Python-side mirror used by tests/ and bench.py. The product path is the
+HIP library; there is no CPU fallback here: if libmiotts.so is missing or no GPU is
+visible, every call raises (the driver checks that native code is what ran).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional
+
+import numpy as np
+
+PKG_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+REPO_ROOT = os.path.dirname(PKG_ROOT)
+BUILD_DIR = os.path.join(PKG_ROOT, "build")
+LIB_PATH = os.path.join(BUILD_DIR, "libmiotts.so")
+INCLUDE_DIR = os.path.join(REPO_ROOT, "include")
+
+MIO_IN_DEVICE = 1
+MIO_OUT_DEVICE = 2
+
+_lib: Optional[ctypes.CDLL] = None
+
+_f32p = ctypes.POINTER(ctypes.c_float)
+_i32p = ctypes.POINTER(ctypes.c_int32)
+_vp = ctypes.c_void_p
+
+
+class HipError(RuntimeError):
+    pass
+
+
+def lib() -> ctypes.CDLL:
+    """Load libmiotts.so (built in-tree by __graft_entry__.build / `make`)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"{LIB_PATH} not built: run `make -C miotts-llama.cpp_amd` "
+                "(or __graft_entry__.build()); there is no CPU fallback")
+        L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        _declare(L)
+        _lib = L
+    return _lib
+
+
+def _declare(L: ctypes.CDLL) -> None:
+    c_int, c_size = ctypes.c_int, ctypes.c_size_t
+    sig = {
+        "mio_hip_last_error": (ctypes.c_char_p, []),
+        "mio_hip_device_count": (c_int, [ctypes.POINTER(c_int)]),
+        "mio_hip_device_open": (c_int, [c_int, ctypes.POINTER(_vp)]),
+        "mio_hip_device_close": (None, [_vp]),
+        "mio_hip_device_sync": (c_int, [_vp]),
+        "mio_hip_device_cu_count": (c_int, [_vp, ctypes.POINTER(c_int)]),
+        "mio_hip_malloc": (c_int, [_vp, c_size, ctypes.POINTER(_vp)]),
+        "mio_hip_free": (c_int, [_vp, _vp]),
+        "mio_hip_memcpy_h2d": (c_int, [_vp, _vp, _vp, c_size]),
+        "mio_hip_memcpy_d2h": (c_int, [_vp, _vp, _vp, c_size]),
+        "mio_hip_memset": (c_int, [_vp, _vp, c_int, c_size]),
+        "mio_hip_timer_mark": (c_int, [_vp, _vp, c_int]),
+        "mio_hip_timer_elapsed": (c_int, [_vp, c_int, c_int, _f32p]),
+        "mio_hip_istft_create": (c_int, [_vp, c_int, c_int, ctypes.POINTER(_vp)]),
+        "mio_hip_istft_destroy": (None, [_vp]),
+        "mio_hip_istft_out_len": (c_int, [_vp, c_int, c_int, ctypes.POINTER(c_int)]),
+        "mio_hip_istft_run": (c_int, [_vp, _vp, c_int, c_int, _vp, ctypes.POINTER(c_int),
+                                      ctypes.c_uint, _vp]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+
+
+def check(rc: int) -> None:
+    if rc != 0:
+        msg = lib().mio_hip_last_error()
+        raise HipError(f"rc={rc}: {msg.decode() if msg else ''}")
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    check(lib().mio_hip_device_count(ctypes.byref(n)))
+    return n.value
+
+
+class Device:
+    """One opened GPU (mio_hip_device)."""
+
+    def __init__(self, dev: int = 0):
+        h = _vp()
+        check(lib().mio_hip_device_open(dev, ctypes.byref(h)))
+        self.h = h
+        self.dev = dev
+
+    def close(self) -> None:
+        if self.h:
+            lib().mio_hip_device_close(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def sync(self) -> None:
+        check(lib().mio_hip_device_sync(self.h))
+
+    def cu_count(self) -> int:
+        n = ctypes.c_int(0)
+        check(lib().mio_hip_device_cu_count(self.h, ctypes.byref(n)))
+        return n.value
+
+    # --- device buffers ---
+    def malloc(self, nbytes: int) -> int:
+        p = _vp()
+        check(lib().mio_hip_malloc(self.h, nbytes, ctypes.byref(p)))
+        return p.value
+
+    def free(self, p: int) -> None:
+        check(lib().mio_hip_free(self.h, p))
+
+    def upload(self, a: np.ndarray) -> "DeviceArray":
+        a = np.ascontiguousarray(a)
+        buf = DeviceArray(self, a.nbytes, a.dtype, a.shape)
+        check(lib().mio_hip_memcpy_h2d(self.h, buf.ptr, _ptr(a), a.nbytes))
+        return buf
+
+    def empty(self, shape, dtype) -> "DeviceArray":
+        dtype = np.dtype(dtype)
+        n = int(np.prod(shape)) * dtype.itemsize
+        return DeviceArray(self, n, dtype, tuple(shape) if not isinstance(shape, int) else (shape,))
+
+    # --- event timers ---
+    def mark(self, slot: int, stream: int = 0) -> None:
+        check(lib().mio_hip_timer_mark(self.h, stream or None, slot))
+
+    def elapsed_ms(self, a: int, b: int) -> float:
+        ms = ctypes.c_float(0)
+        check(lib().mio_hip_timer_elapsed(self.h, a, b, ctypes.byref(ms)))
+        return ms.value
+
+
+class DeviceArray:
+    def __init__(self, dev: Device, nbytes: int, dtype, shape):
+        self.dev = dev
+        self.nbytes = nbytes
+        self.dtype = np.dtype(dtype)
+        self.shape = tuple(shape)
+        self.ptr = dev.malloc(nbytes)
+
+    def numpy(self) -> np.ndarray:
+        out = np.empty(self.shape, self.dtype)
+        if self.nbytes:
+            check(lib().mio_hip_memcpy_d2h(self.dev.h, _ptr(out), self.ptr, self.nbytes))
+        return out
+
+    def free(self) -> None:
+        if self.ptr:
+            self.dev.free(self.ptr)
+            self.ptr = 0
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class Istft:
+    """HIP iSTFT: mirror of istft_cache + istft() (istft.h:6-42)."""
+
+    def __init__(self, dev: Device, n_fft: int = 392, win_length: Optional[int] = None):
+        self.dev = dev
+        self.n_fft = n_fft
+        self.win = n_fft if win_length is None else win_length
+        h = _vp()
+        check(lib().mio_hip_istft_create(dev.h, n_fft, self.win, ctypes.byref(h)))
+        self.h = h
+
+    def __del__(self):
+        try:
+            if self.h:
+                lib().mio_hip_istft_destroy(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+    def out_len(self, n_frames: int, hop: int) -> int:
+        n = ctypes.c_int(0)
+        check(lib().mio_hip_istft_out_len(self.h, n_frames, hop, ctypes.byref(n)))
+        return n.value
+
+    def __call__(self, spec: np.ndarray, hop: int = 98) -> np.ndarray:
+        """spec: [n_frames][n_freq][2] float32 (host). Returns the trimmed PCM."""
+        spec = np.ascontiguousarray(spec, dtype=np.float32)
+        n_frames = spec.shape[0] if spec.size else 0
+        out = np.empty(max(self.out_len(n_frames, hop), 1), np.float32)
+        n = ctypes.c_int(0)
+        check(lib().mio_hip_istft_run(self.h, _ptr(spec) if spec.size else None, n_frames, hop,
+                                      _ptr(out), ctypes.byref(n), 0, None))
+        return out[: n.value]
+
+    def run_device(self, spec: DeviceArray, n_frames: int, hop: int, out: DeviceArray,
+                   stream: int = 0) -> int:
+        n = ctypes.c_int(0)
+        check(lib().mio_hip_istft_run(self.h, spec.ptr, n_frames, hop, out.ptr, ctypes.byref(n),
+                                      MIO_IN_DEVICE | MIO_OUT_DEVICE, stream or None))
+        return n.value

@@ -1,0 +1,97 @@
+"""GPU parity: HIP iSTFT (csrc/hip/istft.hip) vs the reference iSTFT.
+
+Oracle = reference istft.cpp (committed fixtures) and its C restatement
+(oracle/istft_ref.c, bit-exact with the reference). The HIP kernel reorders only
+the DFT inner sum (MFMA fma chain), so the bound is float summation error of a
+196-term sum of O(|X|) terms divided by N: we require max |diff| <= 2e-5 * max|X|
+(absolute) and RMS <= 1e-6 * max|X|, far inside the north-star 1e-4 RMS PCM budget.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import miotts_amd as m
+import pyoracle
+
+pytestmark = pytest.mark.gpu
+
+ATOL_REL = 2e-5
+RMS_REL = 1e-6
+
+
+@pytest.fixture(scope="module")
+def ist(device):
+    return m.Istft(device, 392)
+
+
+def _check(out, ref, scale):
+    assert out.shape == ref.shape
+    if ref.size == 0:
+        return
+    d = out.astype(np.float64) - ref.astype(np.float64)
+    assert np.abs(d).max() <= ATOL_REL * scale, np.abs(d).max()
+    assert np.sqrt(np.mean(d * d)) <= RMS_REL * scale
+
+
+def test_istft_golden_fixtures(ist, golden_dir):
+    z = np.load(os.path.join(golden_dir, "istft_cases.npz"))
+    for key in z.files:
+        if key.startswith("spec_"):
+            n = key.split("_")[1]
+            spec = z[key]
+            scale = max(float(np.abs(spec).max()) if spec.size else 1.0, 1.0)
+            _check(ist(spec), z[f"pcm_{n}"], scale)
+
+
+def test_istft_kat(ist, golden_dir):
+    z = np.load(os.path.join(golden_dir, "istft_kat.npz"))
+    for name in ("dc", "nyq", "dc_im"):
+        _check(ist(z[f"spec_{name}"]), z[f"pcm_{name}"], 392.0)
+    dc = ist(z["spec_dc"])
+    assert np.allclose(dc[400:-400], 4.0 / 3.0, atol=1e-5)
+
+
+@pytest.mark.parametrize("n_frames", [0, 1, 2, 3, 4, 60, 61, 62, 63, 64, 65, 121, 122, 500])
+def test_istft_tile_edges_vs_oracle(ist, n_frames):
+    rng = np.random.default_rng(n_frames)
+    spec = (rng.standard_normal((n_frames, 197, 2)) * 5).astype(np.float32)
+    out = ist(spec)
+    ref = pyoracle.istft(spec)
+    _check(out, ref, 5.0 * 5)
+
+
+def test_istft_full_size_T700(ist):
+    """BASELINE size: T=700 codes -> 12,600 frames -> 1,234,800 samples."""
+    rng = np.random.default_rng(700)
+    F = 18 * 700
+    logmag = rng.normal(-1.0, 1.5, size=(F, 197)).astype(np.float32)
+    phase = rng.uniform(-np.pi, np.pi, size=(F, 197)).astype(np.float32)
+    mag = np.clip(np.exp(logmag), 0, 100).astype(np.float32)
+    spec = np.stack([mag * np.cos(phase), mag * np.sin(phase)], -1).astype(np.float32)
+    out = ist(spec)
+    assert out.size == 1234800
+    ref = pyoracle.istft(spec)
+    _check(out, ref, float(mag.max()))
+
+
+def test_istft_linearity_large(ist):
+    """Size-independent property: istft(a*x + y) == a*istft(x) + istft(y)."""
+    rng = np.random.default_rng(5)
+    F = 4000
+    x = rng.standard_normal((F, 197, 2)).astype(np.float32)
+    y = rng.standard_normal((F, 197, 2)).astype(np.float32)
+    lhs = ist((2.0 * x + y).astype(np.float32))
+    rhs = 2.0 * ist(x) + ist(y)
+    assert np.abs(lhs - rhs).max() < 1e-4
+
+
+def test_istft_device_buffers(ist, device):
+    rng = np.random.default_rng(11)
+    spec = rng.standard_normal((90, 197, 2)).astype(np.float32)
+    d_in = device.upload(spec)
+    d_out = device.empty((90 * 98,), np.float32)
+    n = ist.run_device(d_in, 90, 98, d_out)
+    device.sync()
+    assert n == 90 * 98
+    _check(d_out.numpy(), pyoracle.istft(spec), 5.0)
