@@ -37,6 +37,7 @@ extern "C" {
 
 typedef struct mio_hip_device mio_hip_device;
 typedef struct mio_hip_istft mio_hip_istft;
+typedef struct mio_hip_codec mio_hip_codec;
 
 /* ---------------- device / memory ---------------- */
 const char *mio_hip_last_error(void);
@@ -70,6 +71,40 @@ void mio_hip_istft_destroy(mio_hip_istft *h);
 int mio_hip_istft_out_len(const mio_hip_istft *h, int n_frames, int hop_length, int *out_len);
 int mio_hip_istft_run(mio_hip_istft *h, const float *spec, int n_frames, int hop_length,
                       float *out, int *out_len, unsigned flags, void *stream);
+
+/* ---------------- MioCodec decoder ----------------
+ * Replaces miocodec_load (miocodec.h:10, miocodec.cpp:426-504): weights are read once
+ * and uploaded once to the handle's GPU. */
+int mio_hip_codec_load(mio_hip_device *d, const char *gguf_path, mio_hip_codec **out);
+void mio_hip_codec_free(mio_hip_codec *c);
+/* info[8] = {sample_rate, n_fft, hop_length, samples_per_token, n_freq, upsampler_stages,
+ *            frames_per_code, n_codes}  (miocodec.h:38-41 accessors) */
+int mio_hip_codec_info(const mio_hip_codec *c, int *info);
+/* Replaces miocodec_decode (miocodec.h:28-34, miocodec.cpp:519-810): codes[n_codes] int32,
+ * global_emb[128] f32 -> out_spec [frames][n_freq][2] f32 with frames = n_codes *
+ * frames_per_code (*out_frames). MIO_IN_DEVICE: codes/emb are device pointers (codes are
+ * then not range-checked on the host); MIO_OUT_DEVICE: out_spec is a device pointer. */
+int mio_hip_codec_decode(mio_hip_codec *c, const int32_t *codes, int n_codes,
+                         const float *global_emb, float *out_spec, int *out_frames,
+                         unsigned flags, void *stream);
+/* codec + fused iSTFT (test-to-speech.cpp:264-287 without the host round trip):
+ * out_pcm receives n_codes * samples_per_token samples (*out_len). */
+int mio_hip_codec_decode_pcm(mio_hip_codec *c, const int32_t *codes, int n_codes,
+                             const float *global_emb, float *out_pcm, int *out_len,
+                             unsigned flags, void *stream);
+/* Debug/parity: run up to `stage` and copy that activation to host `out` (stage list as
+ * in oracle/mio_oracle.h: 0 embed .. 7+U spectrogram). rows/cols receive its shape. */
+int mio_hip_codec_decode_stage(mio_hip_codec *c, const int32_t *codes, int n_codes,
+                               const float *global_emb, int stage, float *out, int *rows,
+                               int *cols);
+
+/* ---------------- synthetic model files ----------------
+ * No GGUF model files exist offline. These write files with the
+ * reference's tensor names and KV keys (miocodec.cpp:448-481, 599-728;
+ * create_voice_emb.py:125-129) filled with seeded N(0, s) weights.
+ * preset 0 = MioCodec-25Hz-44.1kHz shapes, 1 = tiny test codec. */
+int mio_synth_codec_gguf(const char *path, int preset, uint64_t seed);
+int mio_synth_voice_gguf(const char *path, uint64_t seed);
 
 #ifdef __cplusplus
 }

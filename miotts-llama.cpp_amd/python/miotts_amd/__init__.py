@@ -67,6 +67,17 @@ def _declare(L: ctypes.CDLL) -> None:
         "mio_hip_istft_out_len": (c_int, [_vp, c_int, c_int, ctypes.POINTER(c_int)]),
         "mio_hip_istft_run": (c_int, [_vp, _vp, c_int, c_int, _vp, ctypes.POINTER(c_int),
                                       ctypes.c_uint, _vp]),
+        "mio_hip_codec_load": (c_int, [_vp, ctypes.c_char_p, ctypes.POINTER(_vp)]),
+        "mio_hip_codec_free": (None, [_vp]),
+        "mio_hip_codec_info": (c_int, [_vp, _i32p]),
+        "mio_hip_codec_decode": (c_int, [_vp, _vp, c_int, _vp, _vp, ctypes.POINTER(c_int),
+                                         ctypes.c_uint, _vp]),
+        "mio_hip_codec_decode_pcm": (c_int, [_vp, _vp, c_int, _vp, _vp, ctypes.POINTER(c_int),
+                                             ctypes.c_uint, _vp]),
+        "mio_hip_codec_decode_stage": (c_int, [_vp, _vp, c_int, _vp, c_int, _vp,
+                                               ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),
+        "mio_synth_codec_gguf": (c_int, [ctypes.c_char_p, c_int, ctypes.c_uint64]),
+        "mio_synth_voice_gguf": (c_int, [ctypes.c_char_p, ctypes.c_uint64]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -214,3 +225,84 @@ class Istft:
         check(lib().mio_hip_istft_run(self.h, spec.ptr, n_frames, hop, out.ptr, ctypes.byref(n),
                                       MIO_IN_DEVICE | MIO_OUT_DEVICE, stream or None))
         return n.value
+
+
+# ---------------------------------------------------------------- synthetic files
+def synth_codec(path: str, preset: int = 0, seed: int = 1) -> str:
+    check(lib().mio_synth_codec_gguf(path.encode(), preset, seed))
+    return path
+
+
+def synth_voice(path: str, seed: int = 7) -> str:
+    check(lib().mio_synth_voice_gguf(path.encode(), seed))
+    return path
+
+
+def read_voice(path: str) -> np.ndarray:
+    """First tensor of a .emb.gguf, F32 (mirror of load_voice_embedding, miocodec.cpp:816-853)."""
+    from . import gguf_np
+    g = gguf_np.GGUFReader(path)
+    t = g.tensors[0]
+    assert t.type == 0, "voice embedding must be F32"
+    return t.array().astype(np.float32)
+
+
+# ---------------------------------------------------------------- codec
+class Codec:
+    """HIP MioCodec decoder (mirror of miocodec.h: miocodec_load / miocodec_decode)."""
+
+    def __init__(self, dev: Device, path: str):
+        self.dev = dev
+        h = _vp()
+        check(lib().mio_hip_codec_load(dev.h, path.encode(), ctypes.byref(h)))
+        self.h = h
+        info = np.zeros(8, np.int32)
+        check(lib().mio_hip_codec_info(h, info.ctypes.data_as(_i32p)))
+        (self.sample_rate, self.n_fft, self.hop_length, self.samples_per_token, self.n_freq,
+         self.up_stages, self.frames_per_code, self.n_codes) = [int(x) for x in info]
+
+    def close(self):
+        if self.h:
+            lib().mio_hip_codec_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def decode(self, codes, emb) -> np.ndarray:
+        codes = np.ascontiguousarray(codes, dtype=np.int32)
+        emb = np.ascontiguousarray(emb, dtype=np.float32)
+        out = np.empty((len(codes) * self.frames_per_code, self.n_freq, 2), np.float32)
+        nf = ctypes.c_int(0)
+        check(lib().mio_hip_codec_decode(self.h, _ptr(codes), len(codes), _ptr(emb), _ptr(out),
+                                         ctypes.byref(nf), 0, None))
+        return out[: nf.value]
+
+    def decode_pcm(self, codes, emb) -> np.ndarray:
+        codes = np.ascontiguousarray(codes, dtype=np.int32)
+        emb = np.ascontiguousarray(emb, dtype=np.float32)
+        out = np.empty(len(codes) * self.frames_per_code * self.hop_length + self.n_fft, np.float32)
+        n = ctypes.c_int(0)
+        check(lib().mio_hip_codec_decode_pcm(self.h, _ptr(codes), len(codes), _ptr(emb), _ptr(out),
+                                             ctypes.byref(n), 0, None))
+        return out[: n.value]
+
+    def decode_pcm_device(self, codes: DeviceArray, n_codes: int, emb: DeviceArray,
+                          out: DeviceArray, stream: int = 0) -> int:
+        n = ctypes.c_int(0)
+        check(lib().mio_hip_codec_decode_pcm(self.h, codes.ptr, n_codes, emb.ptr, out.ptr,
+                                             ctypes.byref(n), MIO_IN_DEVICE | MIO_OUT_DEVICE,
+                                             stream or None))
+        return n.value
+
+    def decode_stage(self, codes, emb, stage: int, max_elems: int) -> np.ndarray:
+        codes = np.ascontiguousarray(codes, dtype=np.int32)
+        emb = np.ascontiguousarray(emb, dtype=np.float32)
+        out = np.empty(max_elems, np.float32)
+        r, c = ctypes.c_int(0), ctypes.c_int(0)
+        check(lib().mio_hip_codec_decode_stage(self.h, _ptr(codes), len(codes), _ptr(emb), stage,
+                                               _ptr(out), ctypes.byref(r), ctypes.byref(c)))
+        return out[: r.value * c.value].reshape(r.value, c.value)

@@ -1,0 +1,100 @@
+"""Small read-only GGUF v2/v3 parser (numpy, memory-mapped) for harness code.
+
+Reads KV metadata and tensor descriptors; tensor data is returned as raw bytes or,
+for F32/F16/I32, as numpy arrays in ggml order reversed (numpy shape = ne[::-1]).
+Nothing in the file is executed (no pickle).
+"""
+from __future__ import annotations
+
+import struct
+from dataclasses import dataclass, field
+from typing import Any, Dict, List
+
+import numpy as np
+
+_SCALAR = {0: "<B", 1: "<b", 2: "<H", 3: "<h", 4: "<I", 5: "<i", 6: "<f", 7: "<?",
+           10: "<Q", 11: "<q", 12: "<d"}
+_TYPE_BLOCK = {0: (1, 4), 1: (1, 2), 30: (1, 2), 24: (1, 1), 25: (1, 2), 26: (1, 4),
+               2: (32, 18), 8: (32, 34), 12: (256, 144), 14: (256, 210), 15: (256, 292)}
+
+
+@dataclass
+class Tensor:
+    name: str
+    ne: List[int]
+    type: int
+    offset: int
+    reader: "GGUFReader" = field(repr=False)
+
+    @property
+    def nbytes(self) -> int:
+        be, bb = _TYPE_BLOCK[self.type]
+        n = int(np.prod(self.ne))
+        return n // be * bb
+
+    def raw(self) -> np.ndarray:
+        start = self.reader.data_offset + self.offset
+        return self.reader.mm[start:start + self.nbytes]
+
+    def array(self) -> np.ndarray:
+        dt = {0: np.float32, 1: np.float16, 26: np.int32, 24: np.int8, 25: np.int16}[self.type]
+        return self.raw().view(dt).reshape(self.ne[::-1])
+
+
+class GGUFReader:
+    def __init__(self, path: str):
+        self.mm = np.memmap(path, dtype=np.uint8, mode="r")
+        b = self.mm
+        self.pos = 0
+        magic, ver = struct.unpack_from("<II", b, 0)
+        if magic != 0x46554747 or ver not in (2, 3):
+            raise ValueError(f"{path}: not GGUF v2/v3")
+        n_t, n_kv = struct.unpack_from("<QQ", b, 8)
+        self.pos = 24
+        self.kv: Dict[str, Any] = {}
+        for _ in range(n_kv):
+            k = self._str()
+            t = self._u32()
+            self.kv[k] = self._val(t)
+        self.tensors: List[Tensor] = []
+        for _ in range(n_t):
+            name = self._str()
+            nd = self._u32()
+            ne = [self._u64() for _ in range(nd)]
+            ty = self._u32()
+            off = self._u64()
+            self.tensors.append(Tensor(name, ne, ty, off, self))
+        align = int(self.kv.get("general.alignment", 32))
+        self.data_offset = (self.pos + align - 1) // align * align
+        self.by_name = {t.name: t for t in self.tensors}
+
+    def _u32(self) -> int:
+        v = struct.unpack_from("<I", self.mm, self.pos)[0]
+        self.pos += 4
+        return v
+
+    def _u64(self) -> int:
+        v = struct.unpack_from("<Q", self.mm, self.pos)[0]
+        self.pos += 8
+        return v
+
+    def _str(self) -> str:
+        n = self._u64()
+        s = bytes(self.mm[self.pos:self.pos + n]).decode("utf-8", errors="replace")
+        self.pos += n
+        return s
+
+    def _val(self, t: int):
+        if t == 8:
+            return self._str()
+        if t == 9:
+            at = self._u32()
+            n = self._u64()
+            return [self._val(at) for _ in range(n)]
+        fmt = _SCALAR[t]
+        v = struct.unpack_from(fmt, self.mm, self.pos)[0]
+        self.pos += struct.calcsize(fmt)
+        return v
+
+    def tensor(self, name: str) -> Tensor:
+        return self.by_name[name]

@@ -30,6 +30,22 @@ void mo_istft_tables(int n_fft, int win_length, float *cos_tbl, float *sin_tbl, 
 int mo_istft(const float *spec, int n_frames, int n_fft, int win_length, int hop_length,
              float *out);
 
+/* ---- codec forward (miocodec.cpp:519-810) ----
+ * Stages for mo_codec_decode_stage (activation copied out after the stage):
+ *   0 embed [T][Dp]          1 prenet+proj [T][Dd]   2 ConvT x2 [2T][Dd]
+ *   3 wave_prior [2T][Dd]    4 decoder+final AdaLN   5 wave_post [2T][Dd]
+ *   6..5+U upsampler stage s [L_s][C_s]               6+U out_proj+snake [L][Dd]
+ *   7+U spectrogram [L][n_freq*2]   (U = upsampler stages) */
+typedef struct mo_codec mo_codec;
+mo_codec *mo_codec_load(const char *path);
+void mo_codec_free(mo_codec *c);
+void mo_codec_info(const mo_codec *c, int *info /* [8] */);
+int mo_codec_n_stages(const mo_codec *c);
+int mo_codec_decode_stage(mo_codec *c, const int *codes, int T, const float *emb, int stop_stage,
+                          float *out, int *out_rows, int *out_cols);
+int mo_codec_decode(mo_codec *c, const int *codes, int T, const float *emb, float *spec);
+float mo_f16_round(float f);
+
 #ifdef __cplusplus
 }
 #endif

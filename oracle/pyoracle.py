@@ -34,6 +34,17 @@ def oracle() -> ctypes.CDLL:
         _o.mo_istft.restype = ctypes.c_int
         _o.mo_istft.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                 ctypes.c_int, ctypes.c_void_p]
+        vp, ci = ctypes.c_void_p, ctypes.c_int
+        _o.mo_codec_load.restype = vp
+        _o.mo_codec_load.argtypes = [ctypes.c_char_p]
+        _o.mo_codec_free.argtypes = [vp]
+        _o.mo_codec_info.argtypes = [vp, vp]
+        _o.mo_codec_n_stages.argtypes = [vp]
+        _o.mo_codec_decode_stage.argtypes = [vp, vp, ci, vp, ci, vp, ctypes.POINTER(ci),
+                                             ctypes.POINTER(ci)]
+        _o.mo_codec_decode.argtypes = [vp, vp, ci, vp, vp]
+        _o.mo_f16_round.restype = ctypes.c_float
+        _o.mo_f16_round.argtypes = [ctypes.c_float]
     return _o
 
 
@@ -65,3 +76,50 @@ def istft(spec: np.ndarray, n_fft: int = 392, win: int = 392, hop: int = 98,
     fn = ref().ref_istft if use_ref else oracle().mo_istft
     n = fn(spec.ctypes.data if spec.size else None, n_frames, n_fft, win, hop, out.ctypes.data)
     return out[:n].copy()
+
+
+class Codec:
+    """Oracle MioCodec forward (oracle/codec_ref.c)."""
+
+    def __init__(self, path: str):
+        self.h = oracle().mo_codec_load(path.encode())
+        if not self.h:
+            raise RuntimeError(f"oracle: cannot load codec {path}")
+        info = np.zeros(8, np.int32)
+        oracle().mo_codec_info(self.h, info.ctypes.data)
+        (self.sample_rate, self.n_fft, self.hop_length, self.samples_per_token, self.n_freq,
+         self.up_stages, self.frames_per_code, self.n_codes) = [int(x) for x in info]
+        self.n_stages = oracle().mo_codec_n_stages(self.h)
+
+    def __del__(self):
+        try:
+            if self.h:
+                oracle().mo_codec_free(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+    def decode(self, codes, emb) -> np.ndarray:
+        codes = np.ascontiguousarray(codes, dtype=np.int32)
+        emb = np.ascontiguousarray(emb, dtype=np.float32)
+        out = np.zeros((len(codes) * self.frames_per_code, self.n_freq, 2), np.float32)
+        n = oracle().mo_codec_decode(self.h, codes.ctypes.data, len(codes), emb.ctypes.data,
+                                     out.ctypes.data)
+        if n < 0:
+            raise RuntimeError(f"oracle codec decode failed: {n}")
+        return out[:n]
+
+    def decode_stage(self, codes, emb, stage: int, max_elems: int) -> np.ndarray:
+        codes = np.ascontiguousarray(codes, dtype=np.int32)
+        emb = np.ascontiguousarray(emb, dtype=np.float32)
+        out = np.zeros(max_elems, np.float32)
+        r, c = ctypes.c_int(0), ctypes.c_int(0)
+        rc = oracle().mo_codec_decode_stage(self.h, codes.ctypes.data, len(codes), emb.ctypes.data,
+                                            stage, out.ctypes.data, ctypes.byref(r), ctypes.byref(c))
+        if rc != 0:
+            raise RuntimeError(f"oracle stage {stage} failed: {rc}")
+        return out[: r.value * c.value].reshape(r.value, c.value)
+
+    def decode_pcm(self, codes, emb) -> np.ndarray:
+        spec = self.decode(codes, emb)
+        return istft(spec, self.n_fft, self.n_fft, self.hop_length)
