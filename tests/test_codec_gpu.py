@@ -1,10 +1,16 @@
 """GPU parity: HIP MioCodec decoder (csrc/host/codec.cpp + csrc/hip/codec_kernels.hip)
 vs the C oracle (oracle/codec_ref.c), stage by stage and end to end through the iSTFT.
 
-Tolerances (float32 path; the GPU reorders sums — MFMA fma chains, tree reductions —
-and rounds the conv operands to f16 exactly like ggml's conv_1d):
-  * per stage     : RMS(diff) <= 2e-4 * RMS(ref) and max|diff| <= 2e-3 * max|ref|
-  * PCM (north star): RMS(diff) <= 1e-4 * max(1, RMS(ref))
+Tolerances. The path is float32 except where the reference itself rounds to f16
+(ggml conv_1d casts the kernel AND the im2col input to f16, miocodec.cpp:382-386).
+The GPU reorders f32 sums (MFMA fma chains, tree reductions): pure-f32 stages agree to
+~2e-6 relative (measured, tools/codec_err_profile.py). At each f16 rounding point an
+ulp-level f32 difference flips ~0.2% of the f16 roundings (one f16 ulp = 4.9e-4), so
+after the first ResNet the stage agreement is ~7e-5 and grows to ~4e-4 at the
+spectrogram (exp() of the log-magnitude). Hence:
+  * per stage : RMS(diff) <= 1e-3 * RMS(ref) and max|diff| <= 5e-3 * max|ref|
+  * PCM       : RMS(diff) <= 1e-4 absolute (north star) and <= 1e-3 * RMS(ref)
+                (measured: 5.5e-5 absolute at ref RMS 0.13, T = 20..700)
 """
 import numpy as np
 import pytest
@@ -37,7 +43,7 @@ def _stage_close(g, o, name):
     rms_ref = np.sqrt(np.mean(o.astype(np.float64) ** 2)) + 1e-30
     rel_rms = np.sqrt(np.mean(d * d)) / rms_ref
     rel_max = np.abs(d).max() / (np.abs(o).max() + 1e-30)
-    assert rel_rms <= 2e-4 and rel_max <= 2e-3, f"{name}: rel_rms={rel_rms:.3g} rel_max={rel_max:.3g}"
+    assert rel_rms <= 1e-3 and rel_max <= 5e-3, f"{name}: rel_rms={rel_rms:.3g} rel_max={rel_max:.3g}"
 
 
 def _pcm_close(g, o):
@@ -45,7 +51,7 @@ def _pcm_close(g, o):
     d = g.astype(np.float64) - o.astype(np.float64)
     rms = np.sqrt(np.mean(d * d))
     rms_ref = np.sqrt(np.mean(o.astype(np.float64) ** 2))
-    assert rms <= 1e-4 * max(1.0, rms_ref), f"PCM rms diff {rms:.3g} (ref rms {rms_ref:.3g})"
+    assert rms <= 1e-4 and rms <= 1e-3 * rms_ref, f"PCM rms diff {rms:.3g} (ref rms {rms_ref:.3g})"
     return rms
 
 
