@@ -38,6 +38,7 @@ extern "C" {
 typedef struct mio_hip_device mio_hip_device;
 typedef struct mio_hip_istft mio_hip_istft;
 typedef struct mio_hip_codec mio_hip_codec;
+typedef struct mio_hip_llm mio_hip_llm;
 
 /* ---------------- device / memory ---------------- */
 const char *mio_hip_last_error(void);
@@ -98,6 +99,39 @@ int mio_hip_codec_decode_stage(mio_hip_codec *c, const int32_t *codes, int n_cod
                                const float *global_emb, int stage, float *out, int *rows,
                                int *cols);
 
+/* ---------------- LLM decode ----------------
+ * Replaces llama_model_load_from_file + llama_init_from_model (test-to-speech.cpp:47-49,
+ * :103-108): GGUF "llama" / "qwen2" / "qwen3" with Q8_0 / Q4_K / Q6_K matrices (Q4_K_M),
+ * F16 KV cache of n_ctx positions (0 -> 2048, :104). */
+int mio_hip_llm_load(mio_hip_device *d, const char *gguf_path, int n_ctx, mio_hip_llm **out);
+void mio_hip_llm_free(mio_hip_llm *m);
+/* info[8] = {n_vocab, n_embd, n_layer, n_head, n_head_kv, head_dim, n_ff, n_ctx} */
+int mio_hip_llm_info(const mio_hip_llm *m, int *info);
+/* Algorithmic HBM bytes streamed per decode step (all matrices incl. lm_head, norms;
+ * one embedding row), the numerator of the decode-step roofline. */
+int mio_hip_llm_weight_bytes(const mio_hip_llm *m, uint64_t *bytes);
+/* Teacher-forced llama_decode of `token` at `pos` (KV cache of positions < pos must hold
+ * earlier evals); logits[n_vocab] to host (NULL = skip). Parity entry point. */
+int mio_hip_llm_eval(mio_hip_llm *m, int32_t token, int pos, float *logits);
+/* Copies the logits of the last step to host. */
+int mio_hip_llm_logits(mio_hip_llm *m, float *logits);
+/* run_llm (test-to-speech.cpp:94-199): prefill prompt[n_prompt], then up to max_tokens
+ * sampled tokens with temperature + seeded sampling restricted to ids [allow_lo, allow_hi)
+ * (-1 = whole vocab); stops at eos0/eos1 (checked every check_interval tokens on the host,
+ * the end token itself is not returned). Sampling is on the device (Gumbel-max over a
+ * counter-based hash of (seed, step, id)); temperature <= 0 is greedy. */
+int mio_hip_llm_generate(mio_hip_llm *m, const int32_t *prompt, int n_prompt, int max_tokens,
+                         float temperature, uint64_t seed, int32_t allow_lo, int32_t allow_hi,
+                         int32_t eos0, int32_t eos1, int32_t check_interval,
+                         int32_t *out_tokens, int *n_out);
+
+/* Parity helpers: y[rows] = W x for a GGUF-layout quantized matrix (gguf_rows, ggml type
+ * 8/12/14) with x re-quantized to the ggml vec_dot_type, on the GPU matvec kernels; and
+ * the host quantizer used to build synthetic models (ggml block layout out). */
+int mio_hip_debug_matvec(mio_hip_device *d, uint32_t type, const void *gguf_rows, int rows, int k,
+                         const float *x, float *y);
+int mio_quantize_rows(uint32_t type, const float *x, int rows, int k, void *out);
+
 /* ---------------- synthetic model files ----------------
  * No GGUF model files exist offline. These write files with the
  * reference's tensor names and KV keys (miocodec.cpp:448-481, 599-728;
@@ -105,6 +139,9 @@ int mio_hip_codec_decode_stage(mio_hip_codec *c, const int32_t *codes, int n_cod
  * preset 0 = MioCodec-25Hz-44.1kHz shapes, 1 = tiny test codec. */
 int mio_synth_codec_gguf(const char *path, int preset, uint64_t seed);
 int mio_synth_voice_gguf(const char *path, uint64_t seed);
+/* Synthetic LLM (llama.cpp GGUF conventions, byte-level vocab + 12,800 speech tokens):
+ * preset 0 tiny Q8_0, 1 tiny Q4_K_M, 2 "0.1B" Q8_0, 3 "1.7B" Q4_K_M, 4 "2.6B" Q8_0. */
+int mio_synth_llm_gguf(const char *path, int preset, uint64_t seed);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,72 @@
+// Launch interface of the LLM decode-step kernels (csrc/hip/llm_kernels.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace mio {
+
+// One quantized matrix in the split layout (csrc/host/quant.h), rows x k.
+struct QMat {
+    int type;  // ggml type id: 8 Q8_0, 12 Q4_K, 14 Q6_K
+    int rows, k;
+    const uint8_t *p0, *p1, *p2, *p3;
+};
+
+// Device-resident decode state (read by every kernel of a step; advanced by the sampler),
+// so one captured hipGraph replays every token without host involvement.
+struct StepState {
+    int pos;     // position of the token being decoded
+    int step;    // step counter (sampler RNG counter, output slot)
+    int token;   // token being decoded
+    int done;    // set once an end token was sampled
+};
+
+struct SampleCfg {
+    float temp;
+    uint32_t seed_lo, seed_hi;
+    int lo, hi;          // sampled ids restricted to [lo, hi)
+    int eos0, eos1;      // end tokens (-1 = none)
+    const int *force;    // force[step] >= 0: next token is forced (prompt prefill), or null
+    int n_force;
+    int *out_tokens;     // [max_steps] sampled/forced next token per step
+    int max_steps;
+};
+
+struct LayerW {
+    const float *attn_norm, *q_norm, *k_norm, *ffn_norm;
+    QMat wq, wk, wv, wo, gate, up, down;
+};
+
+struct LlmDims {
+    int n_embd, n_head, n_kv, hd, n_ff, n_vocab, n_ctx;
+    float eps, scale;
+    int neox, qk_norm;
+    int split;        // attention positions per split
+    int max_splits;
+};
+
+struct LlmBuffers {
+    float *x;          // [n_embd] residual stream
+    float *qkv;        // [(H + 2 Hkv) hd]
+    float *part;       // [H][max_splits][hd + 2] attention partials
+    float *h;          // [n_ff] ffn activation
+    float *logits;     // [n_vocab]
+    float *act;        // quantized final-norm activation (global)
+    float *smp;        // sampler partials [2 * n_lm_blocks]
+    const float2 *rope;  // [n_ctx][hd/2] (cos, sin)
+    StepState *st;
+};
+
+// Launch one decode step (all layers + head + sampler) on stream s.
+void launch_decode_step(const LlmDims &d, const LayerW *layers, int n_layer, _Float16 *kcache,
+                        _Float16 *vcache, const float *out_norm, const QMat &lm, const QMat &tok_embd,
+                        const LlmBuffers &b, const SampleCfg &sc, hipStream_t s);
+// Embedding of `token` (row of token_embd) -> b.x, and state reset to (pos, token).
+void launch_embed_token(const LlmDims &d, const QMat &tok_embd, const LlmBuffers &b, hipStream_t s);
+int lm_head_blocks(const LlmDims &d);
+// y = W x with x re-quantized to the vec_dot_type (parity test of the matvec kernels).
+void launch_debug_matvec(const QMat &W, const float *x, float *y, hipStream_t s);
+
+}  // namespace mio

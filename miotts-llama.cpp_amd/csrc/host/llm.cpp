@@ -1,0 +1,428 @@
+// LLM decode runner (see llm.h): GGUF load -> split-layout weights in HBM, F16 KV cache,
+// one hipGraph per decode step, device-side sampling, C-ABI (include/mio_hip.h).
+//
+// Replaces, for the MioTTS path: llama_model_load_from_file (test-to-speech.cpp:47-49),
+// llama_init_from_model (:103-108), the prefill llama_decode (:132-148), the decode loop
+// llama_sampler_sample / llama_decode (:164-192) and the temp+dist sampler chain (:127-130).
+#include "llm.h"
+
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "common.h"
+#include "gguf.h"
+#include "llm_kernels.h"
+#include "quant.h"
+
+struct mio_hip_llm {
+    mio_hip_device *d = nullptr;
+    mio::LlmDims dims{};
+    int n_layer = 0;
+    std::vector<mio::LayerW> layers;
+    mio::QMat tok{}, lm{};
+    float *out_norm = nullptr;
+    _Float16 *kc = nullptr, *vc = nullptr;
+    mio::LlmBuffers buf{};
+    int *d_tokens = nullptr, *d_force = nullptr;
+    int max_steps = 0;
+    std::vector<void *> allocs;
+    uint64_t weight_bytes = 0;
+
+    hipGraphExec_t graph = nullptr;
+    mio::SampleCfg graph_cfg{};
+    // generation state
+    int n_prompt = 0, max_new = 0, steps_total = 0, steps_issued = 0;
+    mio::SampleCfg cfg{};
+
+    ~mio_hip_llm() {
+        if (d) hipSetDevice(d->dev);
+        if (graph) hipGraphExecDestroy(graph);
+        for (void *p : allocs) hipFree(p);
+    }
+};
+
+namespace {
+
+template <class T>
+T *dalloc(mio_hip_llm *m, size_t n) {
+    void *p = nullptr;
+    if (hipMalloc(&p, n * sizeof(T) + 16) != hipSuccess) return nullptr;
+    m->allocs.push_back(p);
+    hipMemset(p, 0, n * sizeof(T) + 16);
+    return (T *)p;
+}
+
+bool upload_qmat(mio_hip_llm *m, const mio::GgufTensor *t, mio::QMat &q) {
+    if (!t || t->n_dims != 2) {
+        mio::set_error("llm: matrix tensor %s missing or not 2-D", t ? t->name.c_str() : "?");
+        return false;
+    }
+    if (t->type != mio::GGML_Q8_0 && t->type != mio::GGML_Q4_K && t->type != mio::GGML_Q6_K) {
+        mio::set_error("llm: tensor %s has type %s; supported: q8_0, q4_K, q6_K", t->name.c_str(),
+                       mio::ggml_type_name(t->type));
+        return false;
+    }
+    const mio::SplitLayout L = mio::split_layout(t->type, t->ne[1], t->ne[0]);
+    std::vector<uint8_t> host(L.bytes);
+    if (!mio::to_split(t->type, t->data, t->ne[1], t->ne[0], host.data())) {
+        mio::set_error("llm: re-layout of %s failed", t->name.c_str());
+        return false;
+    }
+    uint8_t *dp = dalloc<uint8_t>(m, L.bytes);
+    if (!dp || hipMemcpy(dp, host.data(), L.bytes, hipMemcpyHostToDevice) != hipSuccess) {
+        mio::set_error("llm: upload of %s failed", t->name.c_str());
+        return false;
+    }
+    q.type = (int)t->type;
+    q.rows = (int)t->ne[1];
+    q.k = (int)t->ne[0];
+    q.p0 = dp + L.off[0];
+    q.p1 = dp + L.off[1];
+    q.p2 = dp + L.off[2];
+    q.p3 = dp + L.off[3];
+    m->weight_bytes += t->nbytes;
+    return true;
+}
+
+float *upload_f32(mio_hip_llm *m, const mio::GgufTensor *t, int64_t n) {
+    if (!t || t->type != mio::GGML_F32 || t->nelements() != n) {
+        mio::set_error("llm: norm tensor %s missing or not f32[%lld]", t ? t->name.c_str() : "?", (long long)n);
+        return nullptr;
+    }
+    float *p = dalloc<float>(m, n);
+    if (p) hipMemcpy(p, t->data, n * 4, hipMemcpyHostToDevice);
+    m->weight_bytes += n * 4;
+    return p;
+}
+
+bool same_cfg(const mio::SampleCfg &a, const mio::SampleCfg &b) { return std::memcmp(&a, &b, sizeof(a)) == 0; }
+
+int ensure_graph(mio_hip_llm *m, const mio::SampleCfg &cfg) {
+    if (m->graph && same_cfg(cfg, m->graph_cfg)) return MIO_OK;
+    if (m->graph) {
+        hipGraphExecDestroy(m->graph);
+        m->graph = nullptr;
+    }
+    hipStream_t s = m->d->stream;
+    hipGraph_t g = nullptr;
+    MIO_HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+    mio::launch_decode_step(m->dims, m->layers.data(), m->n_layer, m->kc, m->vc, m->out_norm, m->lm, m->tok,
+                            m->buf, cfg, s);
+    MIO_HIP_CHECK(hipStreamEndCapture(s, &g));
+    MIO_HIP_CHECK(hipGraphInstantiate(&m->graph, g, nullptr, nullptr, 0));
+    hipGraphDestroy(g);
+    m->graph_cfg = cfg;
+    return MIO_OK;
+}
+
+int set_state(mio_hip_llm *m, int pos, int token) {
+    mio::StepState st{pos, 0, token, 0};
+    MIO_HIP_CHECK(hipMemcpyAsync(m->buf.st, &st, sizeof(st), hipMemcpyHostToDevice, m->d->stream));
+    mio::launch_embed_token(m->dims, m->tok, m->buf, m->d->stream);
+    MIO_HIP_CHECK(hipGetLastError());
+    return MIO_OK;
+}
+
+}  // namespace
+
+namespace mio {
+
+LlmInfo llm_info(const mio_hip_llm *m) {
+    return LlmInfo{m->dims.n_vocab, m->dims.n_embd, m->n_layer, m->dims.n_head, m->dims.n_kv,
+                   m->dims.hd, m->dims.n_ff, m->dims.n_ctx};
+}
+
+uint64_t llm_step_weight_bytes(const mio_hip_llm *m) { return m->weight_bytes; }
+
+int llm_begin(mio_hip_llm *m, const int32_t *prompt, int n_prompt, int max_new, const SamplingParams &sp) {
+    MIO_REQUIRE(m && prompt && n_prompt >= 1 && max_new >= 1, MIO_ERR_INVALID, "llm_begin: bad args");
+    MIO_REQUIRE(n_prompt - 1 + max_new <= m->max_steps && n_prompt + max_new <= m->dims.n_ctx,
+                MIO_ERR_INVALID, "llm_begin: %d prompt + %d new tokens exceed n_ctx %d", n_prompt,
+                max_new, m->dims.n_ctx);
+    for (int i = 0; i < n_prompt; ++i)
+        MIO_REQUIRE(prompt[i] >= 0 && prompt[i] < m->dims.n_vocab, MIO_ERR_INVALID,
+                    "llm_begin: token %d out of vocab", prompt[i]);
+    int rc = mio::bind(m->d);
+    if (rc) return rc;
+    std::vector<int> force(m->max_steps, -1);
+    for (int j = 0; j + 1 < n_prompt; ++j) force[j] = prompt[j + 1];
+    MIO_HIP_CHECK(hipMemcpyAsync(m->d_force, force.data(), force.size() * 4, hipMemcpyHostToDevice, m->d->stream));
+    SampleCfg c{};
+    c.temp = sp.temperature;
+    c.seed_lo = (uint32_t)sp.seed, c.seed_hi = (uint32_t)(sp.seed >> 32);
+    c.lo = sp.allow_lo < 0 ? 0 : sp.allow_lo;
+    c.hi = (sp.allow_hi < 0 || sp.allow_hi > m->dims.n_vocab) ? m->dims.n_vocab : sp.allow_hi;
+    c.eos0 = sp.eos0, c.eos1 = sp.eos1;
+    c.force = m->d_force, c.n_force = m->max_steps;
+    c.out_tokens = m->d_tokens, c.max_steps = m->max_steps;
+    if ((rc = ensure_graph(m, c))) return rc;
+    m->cfg = c;
+    m->n_prompt = n_prompt;
+    m->max_new = max_new;
+    m->steps_total = n_prompt - 1 + max_new;
+    m->steps_issued = 0;
+    return set_state(m, 0, prompt[0]);
+}
+
+int llm_run(mio_hip_llm *m, int n_steps) {
+    int rc = mio::bind(m->d);
+    if (rc) return rc;
+    for (int i = 0; i < n_steps && m->steps_issued < m->steps_total; ++i, ++m->steps_issued)
+        MIO_HIP_CHECK(hipGraphLaunch(m->graph, m->d->stream));
+    return MIO_OK;
+}
+
+int llm_poll(mio_hip_llm *m, std::vector<int32_t> &out, bool *done) {
+    int rc = mio::bind(m->d);
+    if (rc) return rc;
+    StepState st{};
+    MIO_HIP_CHECK(hipMemcpyAsync(&st, m->buf.st, sizeof(st), hipMemcpyDeviceToHost, m->d->stream));
+    MIO_HIP_CHECK(hipStreamSynchronize(m->d->stream));
+    const int first = m->n_prompt - 1;
+    const int n = st.step > first ? st.step - first : 0;
+    out.resize(n);
+    if (n) MIO_HIP_CHECK(hipMemcpy(out.data(), m->d_tokens + first, (size_t)n * 4, hipMemcpyDeviceToHost));
+    bool d = false;
+    for (int i = 0; i < n; ++i)
+        if (out[i] == m->cfg.eos0 || out[i] == m->cfg.eos1) {
+            out.resize(i);  // the reference stops before appending the end token (:168-170)
+            d = true;
+            break;
+        }
+    if (done) *done = d || m->steps_issued >= m->steps_total;
+    return MIO_OK;
+}
+
+}  // namespace mio
+
+extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, mio_hip_llm **out) {
+    MIO_REQUIRE(d && path && out, MIO_ERR_INVALID, "llm_load: null argument");
+    if (n_ctx <= 0) n_ctx = 2048;  // test-to-speech.cpp:104
+    int rc = mio::bind(d);
+    if (rc) return rc;
+    mio::GgufFile g;
+    if (!g.open(path)) return MIO_ERR_IO;
+    const std::string arch = g.get_str("general.architecture");
+    MIO_REQUIRE(arch == "llama" || arch == "qwen3" || arch == "qwen2" || arch == "mistral",
+                MIO_ERR_UNSUPPORTED, "llm_load: architecture '%s' not supported (llama, qwen2, qwen3)",
+                arch.c_str());
+    auto *m = new mio_hip_llm();
+    m->d = d;
+    auto fail = [&](int code) {
+        delete m;
+        return code;
+    };
+    mio::LlmDims &D = m->dims;
+    D.n_embd = (int)g.get_int(arch + ".embedding_length", 0);
+    m->n_layer = (int)g.get_int(arch + ".block_count", 0);
+    D.n_ff = (int)g.get_int(arch + ".feed_forward_length", 0);
+    D.n_head = (int)g.get_int(arch + ".attention.head_count", 0);
+    D.n_kv = (int)g.get_int(arch + ".attention.head_count_kv", D.n_head);
+    D.hd = (int)g.get_int(arch + ".attention.key_length", D.n_head ? D.n_embd / D.n_head : 0);
+    D.eps = (float)g.get_float(arch + ".attention.layer_norm_rms_epsilon", 1e-6);
+    const float base = (float)g.get_float(arch + ".rope.freq_base", 10000.0);
+    D.neox = (arch == "qwen3" || arch == "qwen2") ? 1 : 0;
+    D.qk_norm = arch == "qwen3" ? 1 : 0;
+    D.n_ctx = n_ctx;
+    D.scale = 1.0f / sqrtf((float)D.hd);
+    D.split = 64;
+    D.max_splits = (n_ctx + D.split - 1) / D.split;
+    const int G = D.n_kv ? D.n_head / D.n_kv : 0;
+    if (D.n_embd <= 0 || m->n_layer <= 0 || D.n_head <= 0 || D.n_kv <= 0 || D.n_head % D.n_kv ||
+        !(G == 1 || G == 2 || G == 3 || G == 4 || G == 8) || !(D.hd == 64 || D.hd == 128) ||
+        D.n_embd % 256 != 0 && D.n_embd % 32 != 0) {
+        mio::set_error("llm_load: unsupported dims (n_embd %d, heads %d/%d, head_dim %d)", D.n_embd, D.n_head,
+                       D.n_kv, D.hd);
+        return fail(MIO_ERR_UNSUPPORTED);
+    }
+    const mio::GgufTensor *te = g.tensor("token_embd.weight");
+    if (!te || te->ne[0] != D.n_embd) {
+        mio::set_error("llm_load: token_embd.weight missing");
+        return fail(MIO_ERR_FORMAT);
+    }
+    D.n_vocab = (int)te->ne[1];
+    if (!upload_qmat(m, te, m->tok)) return fail(MIO_ERR_FORMAT);
+    const uint64_t embd_bytes = te->nbytes;
+    m->weight_bytes -= embd_bytes;  // one embedding row per step, not the whole table
+    const mio::GgufTensor *to = g.tensor("output.weight");
+    if (to) {
+        if (!upload_qmat(m, to, m->lm)) return fail(MIO_ERR_FORMAT);
+    } else {
+        m->lm = m->tok;  // tied embeddings: the table is streamed as the lm_head every step
+        m->weight_bytes += embd_bytes;
+    }
+    if (!(m->out_norm = upload_f32(m, g.tensor("output_norm.weight"), D.n_embd))) return fail(MIO_ERR_FORMAT);
+    auto fam = [](int t) { return t == mio::GGML_Q8_0 ? 0 : 1; };
+    for (int i = 0; i < m->n_layer; ++i) {
+        const std::string p = "blk." + std::to_string(i) + ".";
+        mio::LayerW L{};
+        if (!(L.attn_norm = upload_f32(m, g.tensor(p + "attn_norm.weight"), D.n_embd)) ||
+            !(L.ffn_norm = upload_f32(m, g.tensor(p + "ffn_norm.weight"), D.n_embd)))
+            return fail(MIO_ERR_FORMAT);
+        if (D.qk_norm) {
+            if (!(L.q_norm = upload_f32(m, g.tensor(p + "attn_q_norm.weight"), D.hd)) ||
+                !(L.k_norm = upload_f32(m, g.tensor(p + "attn_k_norm.weight"), D.hd)))
+                return fail(MIO_ERR_FORMAT);
+        }
+        if (!upload_qmat(m, g.tensor(p + "attn_q.weight"), L.wq) || !upload_qmat(m, g.tensor(p + "attn_k.weight"), L.wk) ||
+            !upload_qmat(m, g.tensor(p + "attn_v.weight"), L.wv) ||
+            !upload_qmat(m, g.tensor(p + "attn_output.weight"), L.wo) ||
+            !upload_qmat(m, g.tensor(p + "ffn_gate.weight"), L.gate) ||
+            !upload_qmat(m, g.tensor(p + "ffn_up.weight"), L.up) || !upload_qmat(m, g.tensor(p + "ffn_down.weight"), L.down))
+            return fail(MIO_ERR_FORMAT);
+        if (L.wq.rows != D.n_head * D.hd || L.wk.rows != D.n_kv * D.hd || L.wv.rows != D.n_kv * D.hd ||
+            L.gate.rows != D.n_ff || L.down.k != D.n_ff || fam(L.wq.type) != fam(L.wk.type) ||
+            fam(L.wq.type) != fam(L.wv.type) || fam(L.gate.type) != fam(L.up.type)) {
+            mio::set_error("llm_load: layer %d shapes / quant families not supported", i);
+            return fail(MIO_ERR_UNSUPPORTED);
+        }
+        m->layers.push_back(L);
+    }
+    // buffers
+    const int qkv = (D.n_head + 2 * D.n_kv) * D.hd;
+    const size_t kv = (size_t)m->n_layer * D.n_kv * n_ctx * D.hd;
+    m->kc = dalloc<_Float16>(m, kv);
+    m->vc = dalloc<_Float16>(m, kv);
+    m->buf.x = dalloc<float>(m, D.n_embd);
+    m->buf.qkv = dalloc<float>(m, qkv);
+    m->buf.part = dalloc<float>(m, (size_t)D.n_head * D.max_splits * (D.hd + 2));
+    m->buf.h = dalloc<float>(m, D.n_ff);
+    m->buf.logits = dalloc<float>(m, D.n_vocab);
+    m->buf.act = dalloc<float>(m, D.n_embd * 2 + 1024);
+    m->buf.smp = dalloc<float>(m, 2 * mio::lm_head_blocks(D) + 16);
+    m->buf.st = dalloc<mio::StepState>(m, 1);
+    m->max_steps = n_ctx;
+    m->d_tokens = dalloc<int>(m, m->max_steps);
+    m->d_force = dalloc<int>(m, m->max_steps);
+    // RoPE table, ggml rope-cache recurrence (theta = p; theta *= base^(-2/hd) per pair)
+    std::vector<float2> rope((size_t)n_ctx * (D.hd / 2));
+    const float theta_scale = powf(base, -2.0f / D.hd);
+    for (int p = 0; p < n_ctx; ++p) {
+        float theta = (float)p;
+        for (int i = 0; i < D.hd / 2; ++i) {
+            rope[(size_t)p * (D.hd / 2) + i] = make_float2(cosf(theta), sinf(theta));
+            theta *= theta_scale;
+        }
+    }
+    float2 *dr = dalloc<float2>(m, rope.size());
+    if (!m->kc || !m->vc || !m->buf.x || !m->buf.qkv || !m->buf.part || !m->buf.h || !m->buf.logits ||
+        !m->buf.act || !m->buf.smp || !m->buf.st || !m->d_tokens || !m->d_force || !dr) {
+        mio::set_error("llm_load: device allocation failed");
+        return fail(MIO_ERR_OOM);
+    }
+    hipMemcpy(dr, rope.data(), rope.size() * sizeof(float2), hipMemcpyHostToDevice);
+    m->buf.rope = dr;
+    *out = m;
+    return MIO_OK;
+}
+
+extern "C" void mio_hip_llm_free(mio_hip_llm *m) { delete m; }
+
+extern "C" int mio_hip_llm_info(const mio_hip_llm *m, int *info) {
+    MIO_REQUIRE(m && info, MIO_ERR_INVALID, "llm_info: null");
+    mio::LlmInfo i = mio::llm_info(m);
+    info[0] = i.n_vocab, info[1] = i.n_embd, info[2] = i.n_layer, info[3] = i.n_head;
+    info[4] = i.n_kv, info[5] = i.head_dim, info[6] = i.n_ff, info[7] = i.n_ctx;
+    return MIO_OK;
+}
+
+extern "C" int mio_hip_llm_weight_bytes(const mio_hip_llm *m, uint64_t *bytes) {
+    MIO_REQUIRE(m && bytes, MIO_ERR_INVALID, "llm_weight_bytes: null");
+    *bytes = m->weight_bytes;
+    return MIO_OK;
+}
+
+extern "C" int mio_hip_llm_eval(mio_hip_llm *m, int32_t token, int pos, float *logits) {
+    MIO_REQUIRE(m && token >= 0 && token < m->dims.n_vocab && pos >= 0 && pos < m->dims.n_ctx,
+                MIO_ERR_INVALID, "llm_eval: bad token/pos");
+    int rc = mio::bind(m->d);
+    if (rc) return rc;
+    mio::SampleCfg c{};
+    c.temp = 0.0f, c.lo = 0, c.hi = m->dims.n_vocab, c.eos0 = c.eos1 = -1;
+    c.force = m->d_force, c.n_force = m->max_steps, c.out_tokens = m->d_tokens, c.max_steps = m->max_steps;
+    if ((rc = ensure_graph(m, c))) return rc;
+    const int zero = 0;
+    MIO_HIP_CHECK(hipMemcpyAsync(m->d_force, &zero, 4, hipMemcpyHostToDevice, m->d->stream));
+    if ((rc = set_state(m, pos, token))) return rc;
+    MIO_HIP_CHECK(hipGraphLaunch(m->graph, m->d->stream));
+    if (logits)
+        MIO_HIP_CHECK(hipMemcpyAsync(logits, m->buf.logits, (size_t)m->dims.n_vocab * 4, hipMemcpyDeviceToHost,
+                                     m->d->stream));
+    MIO_HIP_CHECK(hipStreamSynchronize(m->d->stream));
+    return MIO_OK;
+}
+
+extern "C" int mio_hip_llm_generate(mio_hip_llm *m, const int32_t *prompt, int n_prompt, int max_tokens,
+                                    float temperature, uint64_t seed, int32_t allow_lo, int32_t allow_hi,
+                                    int32_t eos0, int32_t eos1, int32_t check_interval, int32_t *out_tokens,
+                                    int *n_out) {
+    MIO_REQUIRE(m && out_tokens && n_out, MIO_ERR_INVALID, "llm_generate: null argument");
+    mio::SamplingParams sp;
+    sp.temperature = temperature, sp.seed = seed, sp.allow_lo = allow_lo, sp.allow_hi = allow_hi;
+    sp.eos0 = eos0, sp.eos1 = eos1;
+    int rc = mio::llm_begin(m, prompt, n_prompt, max_tokens, sp);
+    if (rc) return rc;
+    const int total = n_prompt - 1 + max_tokens;
+    if (check_interval <= 0) check_interval = total;
+    std::vector<int32_t> toks;
+    bool done = false;
+    // prefill (forced prompt tokens) + check every `check_interval` generated tokens (the
+    // streaming cadence, test-to-speech.cpp:499,608) for an end token
+    if ((rc = mio::llm_run(m, n_prompt - 1))) return rc;
+    while (!done) {
+        if ((rc = mio::llm_run(m, check_interval))) return rc;
+        if ((rc = mio::llm_poll(m, toks, &done))) return rc;
+    }
+    const int n = (int)toks.size() < max_tokens ? (int)toks.size() : max_tokens;
+    std::memcpy(out_tokens, toks.data(), (size_t)n * 4);
+    *n_out = n;
+    return MIO_OK;
+}
+
+extern "C" int mio_hip_llm_logits(mio_hip_llm *m, float *logits) {
+    MIO_REQUIRE(m && logits, MIO_ERR_INVALID, "llm_logits: null");
+    int rc = mio::bind(m->d);
+    if (rc) return rc;
+    MIO_HIP_CHECK(hipMemcpyAsync(logits, m->buf.logits, (size_t)m->dims.n_vocab * 4, hipMemcpyDeviceToHost,
+                                 m->d->stream));
+    MIO_HIP_CHECK(hipStreamSynchronize(m->d->stream));
+    return MIO_OK;
+}
+
+extern "C" int mio_hip_debug_matvec(mio_hip_device *d, uint32_t type, const void *gguf_rows, int rows, int k,
+                                    const float *x, float *y) {
+    MIO_REQUIRE(d && gguf_rows && x && y && rows > 0 && k > 0, MIO_ERR_INVALID, "debug_matvec: bad args");
+    MIO_REQUIRE(type == mio::GGML_Q8_0 || type == mio::GGML_Q4_K || type == mio::GGML_Q6_K, MIO_ERR_UNSUPPORTED,
+                "debug_matvec: type %u", type);
+    MIO_REQUIRE(k % (type == mio::GGML_Q8_0 ? 32 : 256) == 0, MIO_ERR_INVALID, "debug_matvec: k %d", k);
+    int rc = mio::bind(d);
+    if (rc) return rc;
+    const mio::SplitLayout L = mio::split_layout(type, rows, k);
+    std::vector<uint8_t> host(L.bytes);
+    mio::to_split(type, gguf_rows, rows, k, host.data());
+    uint8_t *dw = nullptr;
+    float *dx = nullptr, *dy = nullptr;
+    MIO_HIP_CHECK(hipMalloc(&dw, L.bytes));
+    MIO_HIP_CHECK(hipMalloc(&dx, (size_t)k * 4));
+    MIO_HIP_CHECK(hipMalloc(&dy, (size_t)rows * 4));
+    hipMemcpy(dw, host.data(), L.bytes, hipMemcpyHostToDevice);
+    hipMemcpy(dx, x, (size_t)k * 4, hipMemcpyHostToDevice);
+    mio::QMat q{(int)type, rows, k, dw + L.off[0], dw + L.off[1], dw + L.off[2], dw + L.off[3]};
+    mio::launch_debug_matvec(q, dx, dy, d->stream);
+    hipError_t e = hipStreamSynchronize(d->stream);
+    if (e == hipSuccess) e = hipMemcpy(y, dy, (size_t)rows * 4, hipMemcpyDeviceToHost);
+    hipFree(dw), hipFree(dx), hipFree(dy);
+    MIO_HIP_CHECK(e);
+    return MIO_OK;
+}
+
+extern "C" int mio_quantize_rows(uint32_t type, const float *x, int rows, int k, void *out) {
+    MIO_REQUIRE(x && out && rows > 0 && k > 0, MIO_ERR_INVALID, "quantize_rows: bad args");
+    const size_t rb = mio::ggml_row_bytes(type, k);
+    MIO_REQUIRE(rb, MIO_ERR_UNSUPPORTED, "quantize_rows: type %u / k %d", type, k);
+    for (int r = 0; r < rows; ++r)
+        if (!mio::quantize_row(type, x + (size_t)r * k, (uint8_t *)out + r * rb, k)) return MIO_ERR_UNSUPPORTED;
+    return MIO_OK;
+}

@@ -1,0 +1,61 @@
+// ggml block quant formats (public ggml spec) on the host:
+// fp16 conversion, row quantizers (used to make synthetic Q8_0 / Q4_K_M models),
+// row dequantizers (embedding get_rows), and the re-layout of a GGUF quantized matrix
+// into the "split" layout the gfx950 matvec kernels stream:
+//
+//   Q8_0 : qs [R][K]      int8          | d  [R][K/32]  f16
+//   Q4_K : qs [R][K/2]    u8 nibbles    | hd [R][K/256] 16 B = {d, dmin, scales[12]}
+//   Q6_K : ql [R][K/2]    u8            | qh [R][K/4] u8 | sc [R][K/16] i8 | d [R][K/256] f16
+//
+// Same bytes per weight as GGUF (algorithmic bytes unchanged); each row's quant payload
+// becomes one contiguous, 16-B aligned run, so one wave reads a row with 16 B per lane.
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+#include <vector>
+
+namespace mio {
+
+#pragma pack(push, 1)
+struct BlockQ8_0 {
+    uint16_t d;
+    int8_t qs[32];
+};
+struct BlockQ4_K {
+    uint16_t d, dmin;
+    uint8_t scales[12];
+    uint8_t qs[128];
+};
+struct BlockQ6_K {
+    uint8_t ql[128];
+    uint8_t qh[64];
+    int8_t scales[16];
+    uint16_t d;
+};
+#pragma pack(pop)
+static_assert(sizeof(BlockQ8_0) == 34, "q8_0");
+static_assert(sizeof(BlockQ4_K) == 144, "q4_K");
+static_assert(sizeof(BlockQ6_K) == 210, "q6_K");
+
+float fp16_to_f32(uint16_t h);
+uint16_t f32_to_fp16(float f);  // round to nearest even
+
+void quantize_row_q8_0(const float *x, void *y, int64_t k);
+void quantize_row_q4_K(const float *x, void *y, int64_t k);
+void quantize_row_q6_K(const float *x, void *y, int64_t k);
+bool quantize_row(uint32_t type, const float *x, void *y, int64_t k);
+bool dequantize_row(uint32_t type, const void *x, float *y, int64_t k);
+
+// Split layout of one [R][K] matrix (offsets in bytes from the tensor's base).
+struct SplitLayout {
+    uint32_t type = 0;
+    int64_t rows = 0, k = 0;
+    size_t off[4] = {0, 0, 0, 0};
+    size_t bytes = 0;
+};
+SplitLayout split_layout(uint32_t type, int64_t rows, int64_t k);
+// GGUF rows -> split layout (dst has layout.bytes). Returns false on unsupported type.
+bool to_split(uint32_t type, const void *src, int64_t rows, int64_t k, uint8_t *dst);
+
+}  // namespace mio

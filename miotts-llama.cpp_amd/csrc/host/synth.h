@@ -22,8 +22,31 @@ SynthCodecCfg synth_codec_preset(int preset);
 bool synth_write_codec(const std::string &path, const SynthCodecCfg &cfg);
 bool synth_write_voice(const std::string &path, uint64_t seed, int dim = 128);
 
+// Synthetic LLM in llama.cpp GGUF conventions (arch "llama" or "qwen3"), with a
+// byte-level "gpt2" vocabulary containing the chat-template specials and the 12,800
+// speech tokens <|s_0|>..<|s_12799|> (test-to-speech.cpp:91; miocodec.h:16).
+struct SynthLlmCfg {
+    const char *name = "tiny";
+    const char *arch = "llama";  // "llama" (rope NORM) | "qwen3" (rope NEOX + q/k RMSNorm)
+    int n_embd = 256, n_layer = 2, n_head = 4, n_head_kv = 2, head_dim = 64, n_ff = 512;
+    int n_vocab = 13312, n_ctx = 4096;
+    float rope_base = 10000.f, rms_eps = 1e-6f, w_std = 0.02f;
+    int qtype = 8;   // 8 = all Q8_0; 15 = Q4_K_M mix (Q4_K + Q6_K)
+    bool tied = true;
+    uint64_t seed = 1;
+};
+// preset: 0 tiny Q8_0 (llama), 1 tiny Q4_K_M (qwen3), 2 "0.1B" Q8_0, 3 "1.7B" Q4_K_M,
+//         4 "2.6B" Q8_0  (shapes sized to the published file sizes, README.md:189-196)
+SynthLlmCfg synth_llm_preset(int preset);
+bool synth_write_llm(const std::string &path, const SynthLlmCfg &cfg);
+// Token ids of the synthetic vocabulary.
+constexpr int kSynthTokStartOfText = 256, kSynthTokImStart = 257, kSynthTokImEnd = 258,
+              kSynthTokEndOfText = 259, kSynthTokSpeech0 = 260, kSynthNumSpeech = 12800;
+
 // Deterministic N(0,1) stream: element i of stream `key` (order-independent).
 float synth_normal(uint64_t key, uint64_t i);
+// Fast approximate N(0,1) (Irwin-Hall, 4 uniforms from one hash) for large LLM tensors.
+float synth_normal_fast(uint64_t key, uint64_t i);
 uint64_t synth_key(uint64_t seed, const std::string &name);
 
 }  // namespace mio

@@ -1,0 +1,171 @@
+// Synthetic LLM GGUF writer (see synth.h). Tensor names / KV keys follow llama.cpp's
+// GGUF conventions; quant types follow llama.cpp's Q4_K_M recipe: Q4_K everywhere,
+// Q6_K for attn_v / ffn_down on "use_more_bits" layers and for the (tied) output.
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "common.h"
+#include "gguf.h"
+#include "quant.h"
+#include "synth.h"
+
+namespace mio {
+
+static inline uint64_t mix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+float synth_normal_fast(uint64_t key, uint64_t i) {
+    const uint64_t h = mix64(key ^ mix64(i));
+    const float s = (float)(h & 0xFFFF) + (float)((h >> 16) & 0xFFFF) + (float)((h >> 32) & 0xFFFF) +
+                    (float)(h >> 48);
+    return (s * (1.0f / 65536.0f) - 2.0f) * 1.7320508f;  // var(sum of 4 U(0,1)) = 1/3
+}
+
+SynthLlmCfg synth_llm_preset(int p) {
+    SynthLlmCfg c;
+    switch (p) {
+        case 0: break;
+        case 1:
+            c.name = "tiny-q4km", c.arch = "qwen3", c.n_layer = 3, c.n_ff = 768, c.qtype = 15;
+            c.rope_base = 1000000.f;
+            break;
+        case 2:
+            c.name = "MioTTS-0.1B-synthetic", c.n_embd = 576, c.n_layer = 24, c.n_head = 9,
+            c.n_head_kv = 3, c.head_dim = 64, c.n_ff = 1536, c.n_vocab = 49152 + 12800;
+            break;
+        case 3:
+            c.name = "MioTTS-1.7B-synthetic", c.arch = "qwen3", c.n_embd = 2048, c.n_layer = 28,
+            c.n_head = 16, c.n_head_kv = 8, c.head_dim = 128, c.n_ff = 6144,
+            c.n_vocab = 151936 + 12800, c.qtype = 15, c.rope_base = 1000000.f;
+            break;
+        case 4:
+            c.name = "MioTTS-2.6B-synthetic", c.n_embd = 2048, c.n_layer = 32, c.n_head = 32,
+            c.n_head_kv = 8, c.head_dim = 64, c.n_ff = 10752, c.n_vocab = 65536 + 12800;
+            break;
+        default: break;
+    }
+    return c;
+}
+
+// GPT-2 byte-level unicode for byte b (bytes_to_unicode), UTF-8 encoded
+static std::string byte_token(int b) {
+    int cp;
+    if ((b >= 33 && b <= 126) || (b >= 161 && b <= 172) || (b >= 174 && b <= 255)) {
+        cp = b;
+    } else {
+        int n = 0;
+        for (int x = 0; x < b; ++x)
+            if (!((x >= 33 && x <= 126) || (x >= 161 && x <= 172) || (x >= 174 && x <= 255))) ++n;
+        cp = 256 + n;
+    }
+    std::string s;
+    if (cp < 0x80) {
+        s += (char)cp;
+    } else {
+        s += (char)(0xC0 | (cp >> 6));
+        s += (char)(0x80 | (cp & 0x3F));
+    }
+    return s;
+}
+
+static bool use_more_bits(int i, int n) { return i < n / 8 || i >= 7 * n / 8 || (i - n / 8) % 3 == 2; }
+
+bool synth_write_llm(const std::string &path, const SynthLlmCfg &c) {
+    GgufWriter w;
+    const std::string a = c.arch;
+    w.kv_str("general.architecture", a);
+    w.kv_str("general.name", c.name);
+    w.kv_u32("general.file_type", c.qtype == 15 ? 15 : 7);
+    w.kv_u32(a + ".context_length", c.n_ctx);
+    w.kv_u32(a + ".embedding_length", c.n_embd);
+    w.kv_u32(a + ".block_count", c.n_layer);
+    w.kv_u32(a + ".feed_forward_length", c.n_ff);
+    w.kv_u32(a + ".attention.head_count", c.n_head);
+    w.kv_u32(a + ".attention.head_count_kv", c.n_head_kv);
+    w.kv_u32(a + ".attention.key_length", c.head_dim);
+    w.kv_u32(a + ".attention.value_length", c.head_dim);
+    w.kv_f32(a + ".rope.freq_base", c.rope_base);
+    w.kv_f32(a + ".attention.layer_norm_rms_epsilon", c.rms_eps);
+    // vocabulary
+    std::vector<std::string> toks;
+    std::vector<int32_t> types;
+    for (int b = 0; b < 256; ++b) toks.push_back(byte_token(b)), types.push_back(1);
+    for (const char *sp : {"<|startoftext|>", "<|im_start|>", "<|im_end|>", "<|endoftext|>"})
+        toks.push_back(sp), types.push_back(3);
+    for (int i = 0; i < kSynthNumSpeech; ++i) toks.push_back("<|s_" + std::to_string(i) + "|>"), types.push_back(4);
+    for (int i = (int)toks.size(); i < c.n_vocab; ++i)
+        toks.push_back("<|x_" + std::to_string(i) + "|>"), types.push_back(5);
+    w.kv_str("tokenizer.ggml.model", "gpt2");
+    w.kv_str("tokenizer.ggml.pre", "default");
+    w.kv_arr_str("tokenizer.ggml.tokens", toks);
+    w.kv_arr_i32("tokenizer.ggml.token_type", types);
+    w.kv_arr_str("tokenizer.ggml.merges", {});
+    w.kv_u32("tokenizer.ggml.bos_token_id", kSynthTokStartOfText);
+    w.kv_u32("tokenizer.ggml.eos_token_id", kSynthTokEndOfText);
+    w.kv_bool("tokenizer.ggml.add_bos_token", false);
+
+    struct T {
+        std::string name;
+        uint32_t type;
+        int64_t k, rows;
+        bool ones;
+    };
+    std::vector<T> ts;
+    const uint32_t base = c.qtype == 15 ? GGML_Q4_K : GGML_Q8_0;
+    const uint32_t more = c.qtype == 15 ? GGML_Q6_K : GGML_Q8_0;
+    const int q_dim = c.n_head * c.head_dim, kv_dim = c.n_head_kv * c.head_dim;
+    ts.push_back({"token_embd.weight", c.qtype == 15 ? GGML_Q6_K : GGML_Q8_0, c.n_embd, c.n_vocab, false});
+    for (int i = 0; i < c.n_layer; ++i) {
+        const std::string p = "blk." + std::to_string(i) + ".";
+        const bool mb = use_more_bits(i, c.n_layer);
+        ts.push_back({p + "attn_norm.weight", GGML_F32, c.n_embd, 1, true});
+        ts.push_back({p + "attn_q.weight", base, c.n_embd, q_dim, false});
+        ts.push_back({p + "attn_k.weight", base, c.n_embd, kv_dim, false});
+        ts.push_back({p + "attn_v.weight", mb ? more : base, c.n_embd, kv_dim, false});
+        ts.push_back({p + "attn_output.weight", base, q_dim, c.n_embd, false});
+        if (a == "qwen3") {
+            ts.push_back({p + "attn_q_norm.weight", GGML_F32, c.head_dim, 1, true});
+            ts.push_back({p + "attn_k_norm.weight", GGML_F32, c.head_dim, 1, true});
+        }
+        ts.push_back({p + "ffn_norm.weight", GGML_F32, c.n_embd, 1, true});
+        ts.push_back({p + "ffn_gate.weight", base, c.n_embd, c.n_ff, false});
+        ts.push_back({p + "ffn_up.weight", base, c.n_embd, c.n_ff, false});
+        ts.push_back({p + "ffn_down.weight", mb ? more : base, c.n_ff, c.n_embd, false});
+    }
+    ts.push_back({"output_norm.weight", GGML_F32, c.n_embd, 1, true});
+    if (!c.tied) ts.push_back({"output.weight", more, c.n_embd, c.n_vocab, false});
+    for (auto &t : ts) {
+        if (t.rows == 1)
+            w.add_tensor(t.name, t.type, {t.k});
+        else
+            w.add_tensor(t.name, t.type, {t.k, t.rows});
+    }
+    return w.write(path, [&](size_t idx, uint8_t *dst, size_t nbytes) {
+        const T &t = ts[idx];
+        if (t.ones) {
+            float *f = (float *)dst;
+            for (int64_t i = 0; i < t.k; ++i) f[i] = 1.0f;
+            return;
+        }
+        const size_t rb = ggml_row_bytes(t.type, t.k);
+        const uint64_t key = synth_key(c.seed, t.name);
+#pragma omp parallel
+        {
+            std::vector<float> row(t.k);
+#pragma omp for schedule(static)
+            for (int64_t r = 0; r < t.rows; ++r) {
+                for (int64_t j = 0; j < t.k; ++j) row[j] = c.w_std * synth_normal_fast(key, (uint64_t)r * t.k + j);
+                quantize_row(t.type, row.data(), dst + (size_t)r * rb, t.k);
+            }
+        }
+        (void)nbytes;
+    });
+}
+
+}  // namespace mio

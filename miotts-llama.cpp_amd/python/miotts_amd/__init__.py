@@ -78,6 +78,19 @@ def _declare(L: ctypes.CDLL) -> None:
                                                ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),
         "mio_synth_codec_gguf": (c_int, [ctypes.c_char_p, c_int, ctypes.c_uint64]),
         "mio_synth_voice_gguf": (c_int, [ctypes.c_char_p, ctypes.c_uint64]),
+        "mio_synth_llm_gguf": (c_int, [ctypes.c_char_p, c_int, ctypes.c_uint64]),
+        "mio_hip_llm_load": (c_int, [_vp, ctypes.c_char_p, c_int, ctypes.POINTER(_vp)]),
+        "mio_hip_llm_free": (None, [_vp]),
+        "mio_hip_debug_matvec": (c_int, [_vp, ctypes.c_uint32, _vp, c_int, c_int, _vp, _vp]),
+        "mio_quantize_rows": (c_int, [ctypes.c_uint32, _vp, c_int, c_int, _vp]),
+        "mio_hip_llm_info": (c_int, [_vp, _i32p]),
+        "mio_hip_llm_weight_bytes": (c_int, [_vp, ctypes.POINTER(ctypes.c_uint64)]),
+        "mio_hip_llm_eval": (c_int, [_vp, ctypes.c_int32, c_int, _vp]),
+        "mio_hip_llm_logits": (c_int, [_vp, _vp]),
+        "mio_hip_llm_generate": (c_int, [_vp, _vp, c_int, c_int, ctypes.c_float, ctypes.c_uint64,
+                                         ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                         ctypes.c_int32, ctypes.c_int32, _vp,
+                                         ctypes.POINTER(c_int)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -306,3 +319,85 @@ class Codec:
         check(lib().mio_hip_codec_decode_stage(self.h, _ptr(codes), len(codes), _ptr(emb), stage,
                                                _ptr(out), ctypes.byref(r), ctypes.byref(c)))
         return out[: r.value * c.value].reshape(r.value, c.value)
+
+
+# ---------------------------------------------------------------- LLM
+SYNTH_SPEECH0 = 260      # id of <|s_0|> in the synthetic vocabulary (csrc/host/synth.h)
+SYNTH_IM_END = 258
+SYNTH_EOT = 259
+
+
+def synth_llm(path: str, preset: int = 0, seed: int = 1) -> str:
+    check(lib().mio_synth_llm_gguf(path.encode(), preset, seed))
+    return path
+
+
+class Llm:
+    """HIP LLM decode (mirror of the llama.cpp calls in test-to-speech.cpp:44-196)."""
+
+    def __init__(self, dev: Device, path: str, n_ctx: int = 2048):
+        self.dev = dev
+        h = _vp()
+        check(lib().mio_hip_llm_load(dev.h, path.encode(), n_ctx, ctypes.byref(h)))
+        self.h = h
+        info = np.zeros(8, np.int32)
+        check(lib().mio_hip_llm_info(h, info.ctypes.data_as(_i32p)))
+        (self.n_vocab, self.n_embd, self.n_layer, self.n_head, self.n_kv, self.head_dim,
+         self.n_ff, self.n_ctx) = [int(x) for x in info]
+
+    def close(self):
+        if self.h:
+            lib().mio_hip_llm_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def weight_bytes(self) -> int:
+        b = ctypes.c_uint64(0)
+        check(lib().mio_hip_llm_weight_bytes(self.h, ctypes.byref(b)))
+        return b.value
+
+    def eval(self, token: int, pos: int) -> np.ndarray:
+        out = np.empty(self.n_vocab, np.float32)
+        check(lib().mio_hip_llm_eval(self.h, token, pos, _ptr(out)))
+        return out
+
+    def logits(self) -> np.ndarray:
+        out = np.empty(self.n_vocab, np.float32)
+        check(lib().mio_hip_llm_logits(self.h, _ptr(out)))
+        return out
+
+    def generate(self, prompt, max_tokens: int, temperature: float = 0.8, seed: int = 42,
+                 allow=(-1, -1), eos=(-1, -1), check_interval: int = 20) -> np.ndarray:
+        prompt = np.ascontiguousarray(prompt, dtype=np.int32)
+        out = np.empty(max_tokens, np.int32)
+        n = ctypes.c_int(0)
+        check(lib().mio_hip_llm_generate(self.h, _ptr(prompt), len(prompt), max_tokens,
+                                         temperature, seed, allow[0], allow[1], eos[0], eos[1],
+                                         check_interval, _ptr(out), ctypes.byref(n)))
+        return out[: n.value]
+
+
+GGML_BLOCK = {8: (32, 34), 12: (256, 144), 14: (256, 210)}
+
+
+def quantize_rows(qtype: int, x: np.ndarray) -> np.ndarray:
+    """Host quantizer (csrc/host/quant.cpp) -> GGUF block bytes [rows][row_bytes]."""
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    rows, k = x.shape
+    be, bb = GGML_BLOCK[qtype]
+    out = np.zeros((rows, k // be * bb), np.uint8)
+    check(lib().mio_quantize_rows(qtype, _ptr(x), rows, k, _ptr(out)))
+    return out
+
+
+def debug_matvec(dev: Device, qtype: int, w_rows: np.ndarray, k: int, x: np.ndarray) -> np.ndarray:
+    w_rows = np.ascontiguousarray(w_rows)
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    y = np.empty(w_rows.shape[0], np.float32)
+    check(lib().mio_hip_debug_matvec(dev.h, qtype, _ptr(w_rows), w_rows.shape[0], k, _ptr(x), _ptr(y)))
+    return y

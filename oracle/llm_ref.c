@@ -1,0 +1,304 @@
+/*
+ * ORACLE — TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement of one llama_decode step (test-to-speech.cpp:178-185, :589-596) for the
+ * GGUF architectures the synthetic models use ("llama": RoPE NORM; "qwen3": RoPE NEOX +
+ * per-head q/k RMSNorm), in llama.cpp / ggml CPU semantics [upstream; parity unpinned]:
+ *   rms_norm : sum x^2 in double, scale = 1/sqrtf(mean + eps), then * weight
+ *   matvec   : activation re-quantized to the weight's vec_dot_type (quant_ref.c)
+ *   rope     : theta = pos * base^(-2i/hd) by repeated float multiplication (ggml rope cache)
+ *   KV cache : F16 (llama.cpp default cache type); q rounded to f16 for Q.K^T (ggml converts
+ *              src1 to the F16 vec_dot_type), f32 accumulation; softmax(s * 1/sqrt(hd)) with the
+ *              sum in double; out = sum_t p_t * v_t in f32
+ *   ffn      : down(silu(gate x) * up x)
+ * Sampler: temperature + Gumbel-max over a counter-based hash (mo_sample). llama.cpp's
+ * dist sampler draws from the same softmax(logits/T) distribution with mt19937; bit parity
+ * of the RNG across backends is not attainable, so the GPU and this oracle
+ * share this counter-based sampler and parity is defined on logits and sampled ids.
+ */
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "gguf_ref.h"
+#include "mio_oracle.h"
+
+float mo_fp16_to_f32(uint16_t h);
+uint16_t mo_f32_to_fp16(float f);
+void mo_quantize_q8_0(const float *x, int64_t k, uint16_t *d, int8_t *qs);
+void mo_quantize_q8_K(const float *x, int64_t k, float *d, int8_t *qs, int16_t *bsums);
+float mo_vec_dot_q8_0(const uint8_t *row, int64_t k, const uint16_t *ad, const int8_t *aq);
+float mo_vec_dot_q4_K(const uint8_t *row, int64_t k, const float *ad, const int8_t *aq, const int16_t *bsums);
+float mo_vec_dot_q6_K(const uint8_t *row, int64_t k, const float *ad, const int8_t *aq);
+int mo_dequantize_row(uint32_t type, const uint8_t *row, int64_t k, float *y);
+
+typedef struct {
+    const mo_tensor *attn_norm, *wq, *wk, *wv, *wo, *q_norm, *k_norm, *ffn_norm, *gate, *up, *down;
+} mo_layer;
+
+struct mo_llm {
+    mo_gguf *g;
+    int qwen3;
+    int n_embd, n_layer, n_head, n_kv, hd, n_ff, n_vocab, n_ctx;
+    float base, eps;
+    mo_layer *L;
+    const mo_tensor *tok, *out_norm, *out;
+    uint16_t *kc, *vc;
+    /* activation scratch */
+    float *x, *h, *q, *k, *v, *att, *g1, *u1, *q8kd;
+    int8_t *q8qs;
+    int16_t *q8bs;
+    uint16_t *q80d;
+};
+
+static const mo_tensor *T(mo_gguf *g, const char *fmt, int i) {
+    char n[128];
+    snprintf(n, sizeof n, fmt, i);
+    return mo_gguf_tensor(g, n);
+}
+
+mo_llm *mo_llm_load(const char *path, int n_ctx) {
+    mo_gguf *g = mo_gguf_open(path);
+    if (!g) return NULL;
+    const mo_kv *ak = mo_gguf_kv(g, "general.architecture");
+    if (!ak || !ak->str) { mo_gguf_close(g); return NULL; }
+    mo_llm *m = (mo_llm *)calloc(1, sizeof(mo_llm));
+    m->g = g;
+    const char *a = ak->str;
+    m->qwen3 = strcmp(a, "qwen3") == 0;
+    char key[128];
+#define KI(s, def) (snprintf(key, sizeof key, "%s." s, a), (int)mo_gguf_int(g, key, def))
+#define KF(s, def) (snprintf(key, sizeof key, "%s." s, a), (float)mo_gguf_float(g, key, def))
+    m->n_embd = KI("embedding_length", 0);
+    m->n_layer = KI("block_count", 0);
+    m->n_ff = KI("feed_forward_length", 0);
+    m->n_head = KI("attention.head_count", 0);
+    m->n_kv = KI("attention.head_count_kv", m->n_head);
+    m->hd = KI("attention.key_length", m->n_head ? m->n_embd / m->n_head : 0);
+    m->base = KF("rope.freq_base", 10000.0f);
+    m->eps = KF("attention.layer_norm_rms_epsilon", 1e-6f);
+#undef KI
+#undef KF
+    m->tok = mo_gguf_tensor(g, "token_embd.weight");
+    m->out_norm = mo_gguf_tensor(g, "output_norm.weight");
+    m->out = mo_gguf_tensor(g, "output.weight");
+    if (!m->out) m->out = m->tok;
+    if (!m->tok || !m->out_norm || m->n_layer <= 0) { mo_gguf_close(g); free(m); return NULL; }
+    m->n_vocab = (int)m->tok->ne[1];
+    m->n_ctx = n_ctx;
+    m->L = (mo_layer *)calloc(m->n_layer, sizeof(mo_layer));
+    for (int i = 0; i < m->n_layer; i++) {
+        mo_layer *l = &m->L[i];
+        l->attn_norm = T(g, "blk.%d.attn_norm.weight", i);
+        l->wq = T(g, "blk.%d.attn_q.weight", i);
+        l->wk = T(g, "blk.%d.attn_k.weight", i);
+        l->wv = T(g, "blk.%d.attn_v.weight", i);
+        l->wo = T(g, "blk.%d.attn_output.weight", i);
+        l->q_norm = T(g, "blk.%d.attn_q_norm.weight", i);
+        l->k_norm = T(g, "blk.%d.attn_k_norm.weight", i);
+        l->ffn_norm = T(g, "blk.%d.ffn_norm.weight", i);
+        l->gate = T(g, "blk.%d.ffn_gate.weight", i);
+        l->up = T(g, "blk.%d.ffn_up.weight", i);
+        l->down = T(g, "blk.%d.ffn_down.weight", i);
+        if (!l->attn_norm || !l->wq || !l->wk || !l->wv || !l->wo || !l->ffn_norm || !l->gate ||
+            !l->up || !l->down) {
+            mo_gguf_close(g);
+            free(m->L);
+            free(m);
+            return NULL;
+        }
+    }
+    const size_t kv = (size_t)m->n_layer * m->n_kv * n_ctx * m->hd;
+    m->kc = (uint16_t *)calloc(kv, 2);
+    m->vc = (uint16_t *)calloc(kv, 2);
+    int big = m->n_embd > m->n_ff ? m->n_embd : m->n_ff;
+    if (m->n_head * m->hd > big) big = m->n_head * m->hd;
+    m->x = (float *)calloc(m->n_embd, 4);
+    m->h = (float *)calloc(big, 4);
+    m->q = (float *)calloc(m->n_head * m->hd, 4);
+    m->k = (float *)calloc(m->n_kv * m->hd, 4);
+    m->v = (float *)calloc(m->n_kv * m->hd, 4);
+    m->att = (float *)calloc(big, 4);
+    m->g1 = (float *)calloc(m->n_ff, 4);
+    m->u1 = (float *)calloc(m->n_ff, 4);
+    m->q8kd = (float *)calloc(big / 256 + 1, 4);
+    m->q8qs = (int8_t *)calloc(big, 1);
+    m->q8bs = (int16_t *)calloc(big / 16 + 1, 2);
+    m->q80d = (uint16_t *)calloc(big / 32 + 1, 2);
+    return m;
+}
+
+void mo_llm_free(mo_llm *m) {
+    if (!m) return;
+    mo_gguf_close(m->g);
+    free(m->L); free(m->kc); free(m->vc);
+    free(m->x); free(m->h); free(m->q); free(m->k); free(m->v); free(m->att);
+    free(m->g1); free(m->u1); free(m->q8kd); free(m->q8qs); free(m->q8bs); free(m->q80d);
+    free(m);
+}
+
+void mo_llm_info(const mo_llm *m, int *info) {
+    info[0] = m->n_vocab; info[1] = m->n_embd; info[2] = m->n_layer; info[3] = m->n_head;
+    info[4] = m->n_kv; info[5] = m->hd; info[6] = m->n_ff; info[7] = m->n_ctx;
+}
+
+void mo_llm_reset(mo_llm *m) {
+    const size_t kv = (size_t)m->n_layer * m->n_kv * m->n_ctx * m->hd;
+    memset(m->kc, 0, kv * 2);
+    memset(m->vc, 0, kv * 2);
+}
+
+/* y = W x for all rows of W (ggml mul_mat semantics incl. activation re-quantization) */
+static void matvec(mo_llm *m, const mo_tensor *W, const float *x, float *y) {
+    const int64_t K = W->ne[0], R = W->ne[1];
+    const size_t rb = W->nbytes / (size_t)R;
+    if (W->type == 8) {
+        mo_quantize_q8_0(x, K, m->q80d, m->q8qs);
+#pragma omp parallel for schedule(static)
+        for (int64_t r = 0; r < R; r++) y[r] = mo_vec_dot_q8_0(W->data + r * rb, K, m->q80d, m->q8qs);
+    } else if (W->type == 12 || W->type == 14) {
+        mo_quantize_q8_K(x, K, m->q8kd, m->q8qs, m->q8bs);
+#pragma omp parallel for schedule(static)
+        for (int64_t r = 0; r < R; r++)
+            y[r] = W->type == 12 ? mo_vec_dot_q4_K(W->data + r * rb, K, m->q8kd, m->q8qs, m->q8bs)
+                                 : mo_vec_dot_q6_K(W->data + r * rb, K, m->q8kd, m->q8qs);
+    } else if (W->type == 0) {
+#pragma omp parallel for schedule(static)
+        for (int64_t r = 0; r < R; r++) {
+            const float *w = (const float *)(W->data + r * rb);
+            float s = 0;
+            for (int64_t i = 0; i < K; i++) s += w[i] * x[i];
+            y[r] = s;
+        }
+    } else {
+        fprintf(stderr, "oracle: unsupported weight type %u\n", W->type);
+        abort();
+    }
+}
+
+static void rms_norm(const float *x, int n, const float *w, float eps, float *y) {
+    double sum = 0.0;
+    for (int i = 0; i < n; i++) sum += (double)(x[i] * x[i]);
+    const float mean = (float)(sum / n);
+    const float scale = 1.0f / sqrtf(mean + eps);
+    for (int i = 0; i < n; i++) {
+        const float v = x[i] * scale;
+        y[i] = v * w[i];
+    }
+}
+
+static void rope(float *x, int hd, int pos, float base, int neox) {
+    const float theta_scale = powf(base, -2.0f / hd);
+    float theta = (float)pos;
+    for (int i = 0; i < hd / 2; i++) {
+        const float c = cosf(theta), s = sinf(theta);
+        const int i0 = neox ? i : 2 * i, i1 = neox ? i + hd / 2 : 2 * i + 1;
+        const float x0 = x[i0], x1 = x[i1];
+        x[i0] = x0 * c - x1 * s;
+        x[i1] = x0 * s + x1 * c;
+        theta *= theta_scale;
+    }
+}
+
+static inline float silu(float x) { return x / (1.0f + expf(-x)); }
+
+int mo_llm_eval(mo_llm *m, int token, int pos, float *logits) {
+    if (token < 0 || token >= m->n_vocab || pos < 0 || pos >= m->n_ctx) return -1;
+    const int D = m->n_embd, H = m->n_head, Hk = m->n_kv, hd = m->hd, F = m->n_ff;
+    const size_t rb = m->tok->nbytes / (size_t)m->n_vocab;
+    if (mo_dequantize_row(m->tok->type, m->tok->data + (size_t)token * rb, D, m->x)) return -2;
+    const float scale = 1.0f / sqrtf((float)hd);
+    for (int il = 0; il < m->n_layer; il++) {
+        const mo_layer *l = &m->L[il];
+        rms_norm(m->x, D, (const float *)l->attn_norm->data, m->eps, m->h);
+        matvec(m, l->wq, m->h, m->q);
+        matvec(m, l->wk, m->h, m->k);
+        matvec(m, l->wv, m->h, m->v);
+        for (int h = 0; h < H; h++) {
+            if (m->qwen3 && l->q_norm) rms_norm(m->q + h * hd, hd, (const float *)l->q_norm->data, m->eps, m->q + h * hd);
+            rope(m->q + h * hd, hd, pos, m->base, m->qwen3);
+        }
+        for (int h = 0; h < Hk; h++) {
+            if (m->qwen3 && l->k_norm) rms_norm(m->k + h * hd, hd, (const float *)l->k_norm->data, m->eps, m->k + h * hd);
+            rope(m->k + h * hd, hd, pos, m->base, m->qwen3);
+            uint16_t *kd = m->kc + (((size_t)il * Hk + h) * m->n_ctx + pos) * hd;
+            uint16_t *vd = m->vc + (((size_t)il * Hk + h) * m->n_ctx + pos) * hd;
+            for (int d = 0; d < hd; d++) {
+                kd[d] = mo_f32_to_fp16(m->k[h * hd + d]);
+                vd[d] = mo_f32_to_fp16(m->v[h * hd + d]);
+            }
+        }
+#pragma omp parallel for schedule(static)
+        for (int h = 0; h < H; h++) {
+            const int kvh = h / (H / Hk);
+            float qh[512];
+            for (int d = 0; d < hd; d++) qh[d] = mo_fp16_to_f32(mo_f32_to_fp16(m->q[h * hd + d]));
+            float *s = (float *)malloc(sizeof(float) * (pos + 1));
+            float mx = -INFINITY;
+            for (int t = 0; t <= pos; t++) {
+                const uint16_t *kr = m->kc + (((size_t)il * Hk + kvh) * m->n_ctx + t) * hd;
+                float a = 0;
+                for (int d = 0; d < hd; d++) a += qh[d] * mo_fp16_to_f32(kr[d]);
+                s[t] = a * scale;
+                if (s[t] > mx) mx = s[t];
+            }
+            double sum = 0;
+            for (int t = 0; t <= pos; t++) {
+                s[t] = expf(s[t] - mx);
+                sum += (double)s[t];
+            }
+            const float inv = (float)(1.0 / sum);
+            for (int d = 0; d < hd; d++) {
+                float o = 0;
+                for (int t = 0; t <= pos; t++) {
+                    const uint16_t *vr = m->vc + (((size_t)il * Hk + kvh) * m->n_ctx + t) * hd;
+                    o += (s[t] * inv) * mo_fp16_to_f32(vr[d]);
+                }
+                m->att[h * hd + d] = o;
+            }
+            free(s);
+        }
+        matvec(m, l->wo, m->att, m->h);
+        for (int i = 0; i < D; i++) m->x[i] = m->h[i] + m->x[i];
+        rms_norm(m->x, D, (const float *)l->ffn_norm->data, m->eps, m->h);
+        matvec(m, l->gate, m->h, m->g1);
+        matvec(m, l->up, m->h, m->u1);
+        for (int i = 0; i < F; i++) m->g1[i] = silu(m->g1[i]) * m->u1[i];
+        matvec(m, l->down, m->g1, m->h);
+        for (int i = 0; i < D; i++) m->x[i] = m->h[i] + m->x[i];
+    }
+    if (logits) {
+        rms_norm(m->x, D, (const float *)m->out_norm->data, m->eps, m->h);
+        matvec(m, m->out, m->h, logits);
+    }
+    return 0;
+}
+
+/* ---- counter-based Gumbel-max sampler shared with the GPU (llm_kernels.hip) ---- */
+static inline uint64_t mix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+float mo_gumbel(uint64_t seed, int step, int idx) {
+    const uint64_t h = mix64(seed ^ mix64(((uint64_t)(uint32_t)step << 32) | (uint32_t)idx));
+    const float u = ((float)(h >> 40) + 0.5f) * (1.0f / 16777216.0f);
+    return -logf(-logf(u));
+}
+
+/* temperature + Gumbel-max over ids [lo, hi); temp <= 0 -> greedy; ties -> lowest id */
+int mo_sample(const float *logits, float temp, uint64_t seed, int step, int lo, int hi) {
+    int arg = lo;
+    float best = -INFINITY;
+    for (int i = lo; i < hi; i++) {
+        const float s = temp > 0.0f ? logits[i] / temp + mo_gumbel(seed, step, i) : logits[i];
+        if (s > best) {
+            best = s;
+            arg = i;
+        }
+    }
+    return arg;
+}

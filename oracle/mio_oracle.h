@@ -46,6 +46,24 @@ int mo_codec_decode_stage(mo_codec *c, const int *codes, int T, const float *emb
 int mo_codec_decode(mo_codec *c, const int *codes, int T, const float *emb, float *spec);
 float mo_f16_round(float f);
 
+/* ---- LLM decode step (llama_decode, test-to-speech.cpp:178-185) and sampler ---- */
+typedef struct mo_llm mo_llm;
+mo_llm *mo_llm_load(const char *path, int n_ctx);
+void mo_llm_free(mo_llm *m);
+/* info[8] = {n_vocab, n_embd, n_layer, n_head, n_head_kv, head_dim, n_ff, n_ctx} */
+void mo_llm_info(const mo_llm *m, int *info);
+void mo_llm_reset(mo_llm *m);
+int mo_llm_eval(mo_llm *m, int token, int pos, float *logits /* [n_vocab] or NULL */);
+float mo_gumbel(uint64_t seed, int step, int idx);
+int mo_sample(const float *logits, float temp, uint64_t seed, int step, int lo, int hi);
+/* ggml block helpers (quant_ref.c) */
+float mo_fp16_to_f32(uint16_t h);
+uint16_t mo_f32_to_fp16(float f);
+void mo_quantize_q8_0(const float *x, int64_t k, uint16_t *d, int8_t *qs);
+void mo_quantize_q8_K(const float *x, int64_t k, float *d, int8_t *qs, int16_t *bsums);
+int mo_dequantize_row(uint32_t type, const uint8_t *row, int64_t k, float *y);
+int mo_matvec(uint32_t type, const uint8_t *w, int rows, int64_t k, const float *x, float *y);
+
 #ifdef __cplusplus
 }
 #endif

@@ -45,6 +45,17 @@ def oracle() -> ctypes.CDLL:
         _o.mo_codec_decode.argtypes = [vp, vp, ci, vp, vp]
         _o.mo_f16_round.restype = ctypes.c_float
         _o.mo_f16_round.argtypes = [ctypes.c_float]
+        _o.mo_llm_load.restype = vp
+        _o.mo_llm_load.argtypes = [ctypes.c_char_p, ci]
+        _o.mo_llm_free.argtypes = [vp]
+        _o.mo_llm_info.argtypes = [vp, vp]
+        _o.mo_llm_reset.argtypes = [vp]
+        _o.mo_llm_eval.argtypes = [vp, ci, ci, vp]
+        _o.mo_gumbel.restype = ctypes.c_float
+        _o.mo_gumbel.argtypes = [ctypes.c_uint64, ci, ci]
+        _o.mo_sample.restype = ci
+        _o.mo_sample.argtypes = [vp, ctypes.c_float, ctypes.c_uint64, ci, ci, ci]
+        _o.mo_dequantize_row.argtypes = [ctypes.c_uint32, vp, ctypes.c_int64, vp]
     return _o
 
 
@@ -123,3 +134,60 @@ class Codec:
     def decode_pcm(self, codes, emb) -> np.ndarray:
         spec = self.decode(codes, emb)
         return istft(spec, self.n_fft, self.n_fft, self.hop_length)
+
+
+class Llm:
+    """Oracle decode step (oracle/llm_ref.c) + shared counter-based sampler."""
+
+    def __init__(self, path: str, n_ctx: int = 512):
+        self.h = oracle().mo_llm_load(path.encode(), n_ctx)
+        if not self.h:
+            raise RuntimeError(f"oracle: cannot load llm {path}")
+        info = np.zeros(8, np.int32)
+        oracle().mo_llm_info(self.h, info.ctypes.data)
+        (self.n_vocab, self.n_embd, self.n_layer, self.n_head, self.n_kv, self.head_dim,
+         self.n_ff, self.n_ctx) = [int(x) for x in info]
+
+    def __del__(self):
+        try:
+            if self.h:
+                oracle().mo_llm_free(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+    def reset(self):
+        oracle().mo_llm_reset(self.h)
+
+    def eval(self, token: int, pos: int) -> np.ndarray:
+        out = np.zeros(self.n_vocab, np.float32)
+        rc = oracle().mo_llm_eval(self.h, token, pos, out.ctypes.data)
+        if rc:
+            raise RuntimeError(f"oracle eval failed {rc}")
+        return out
+
+    def generate(self, prompt, max_tokens, temperature=0.8, seed=42, allow=(-1, -1), eos=(-1, -1)):
+        lo = 0 if allow[0] < 0 else allow[0]
+        hi = self.n_vocab if allow[1] < 0 else allow[1]
+        self.reset()
+        logits = None
+        for i, t in enumerate(prompt):
+            logits = self.eval(int(t), i)
+        pos = len(prompt)
+        out = []
+        # step counter of the GPU sampler = decode steps so far (prefill steps included)
+        step = len(prompt) - 1
+        for _ in range(max_tokens):
+            tok = sample(logits, temperature, seed, step, lo, hi)
+            if tok in eos:
+                break
+            out.append(tok)
+            logits = self.eval(tok, pos)
+            pos += 1
+            step += 1
+        return np.array(out, np.int32)
+
+
+def sample(logits: np.ndarray, temperature: float, seed: int, step: int, lo: int, hi: int) -> int:
+    logits = np.ascontiguousarray(logits, dtype=np.float32)
+    return int(oracle().mo_sample(logits.ctypes.data, temperature, seed, step, lo, hi))

@@ -1,0 +1,120 @@
+"""CPU: LLM oracle (oracle/llm_ref.c, quant_ref.c), quantizers and the shared sampler.
+
+The decode-step oracle is "parity unpinned" (llama.cpp/ggml absent). What is
+pinned here without ggml: the public block layouts (quantize -> dequantize round trips
+within the format's resolution), the activation quantizers against a numpy restatement
+of quantize_row_q8_K_ref / quantize_row_q8_0_ref, and the sampler's distribution
+(temperature + Gumbel-max draws from softmax(logits / T), the distribution llama.cpp's
+temp -> dist chain samples, test-to-speech.cpp:127-130).
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+import miotts_amd as m
+from miotts_amd import gguf_np
+import pyoracle
+
+
+def _dequant(qtype, rows_bytes, k):
+    o = pyoracle.oracle()
+    out = np.zeros((rows_bytes.shape[0], k), np.float32)
+    for r in range(rows_bytes.shape[0]):
+        rb = np.ascontiguousarray(rows_bytes[r])
+        assert o.mo_dequantize_row(qtype, rb.ctypes.data, k, out[r].ctypes.data) == 0
+    return out
+
+
+@pytest.mark.parametrize("qtype,tol", [(8, 1.0 / 127), (12, 1.0 / 15 * 1.2), (14, 1.0 / 31 * 1.2)])
+def test_quantize_dequantize_roundtrip(qtype, tol):
+    rng = np.random.default_rng(qtype)
+    x = (rng.standard_normal((6, 512)) * 0.02).astype(np.float32)
+    q = m.quantize_rows(qtype, x)
+    y = _dequant(qtype, q, 512)
+    # error bounded by the format's step relative to the (sub)block range
+    assert np.abs(y - x).max() <= tol * np.abs(x).max() + 1e-6
+
+
+def _np_q8k(x):
+    """numpy restatement of ggml quantize_row_q8_K_ref."""
+    nb = len(x) // 256
+    d = np.zeros(nb, np.float32)
+    qs = np.zeros(len(x), np.int8)
+    bs = np.zeros(nb * 16, np.int16)
+    for i in range(nb):
+        blk = x[i * 256:(i + 1) * 256]
+        j = int(np.argmax(np.abs(blk)))
+        if blk[j] == 0:
+            continue
+        iscale = np.float32(-127.0) / blk[j]
+        q = np.rint((iscale * blk).astype(np.float32)).astype(np.int32)
+        q = np.minimum(q, 127)
+        qs[i * 256:(i + 1) * 256] = q
+        bs[i * 16:(i + 1) * 16] = q.reshape(16, 16).sum(1)
+        d[i] = np.float32(1.0) / iscale
+    return d, qs, bs
+
+
+def test_q8k_activation_quantizer_matches_numpy():
+    o = pyoracle.oracle()
+    o.mo_quantize_q8_K.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
+                                   ctypes.c_void_p]
+    rng = np.random.default_rng(1)
+    x = rng.standard_normal(2048).astype(np.float32)
+    x[5] = -7.5  # signed max
+    d = np.zeros(8, np.float32)
+    qs = np.zeros(2048, np.int8)
+    bs = np.zeros(128, np.int16)
+    o.mo_quantize_q8_K(x.ctypes.data, 2048, d.ctypes.data, qs.ctypes.data, bs.ctypes.data)
+    d2, qs2, bs2 = _np_q8k(x)
+    assert np.array_equal(qs, qs2) and np.array_equal(bs, bs2) and np.array_equal(d, d2)
+
+
+@pytest.fixture(scope="module")
+def tiny_llms(tmp_path_factory):
+    d = tmp_path_factory.mktemp("llm")
+    return {p: m.synth_llm(str(d / f"llm{p}.gguf"), p, 1) for p in (0, 1)}
+
+
+def test_synth_llm_format(tiny_llms):
+    g = gguf_np.GGUFReader(tiny_llms[1])
+    assert g.kv["general.architecture"] == "qwen3"
+    toks = g.kv["tokenizer.ggml.tokens"]
+    assert toks[256] == "<|startoftext|>" and toks[258] == "<|im_end|>"
+    assert toks[m.SYNTH_SPEECH0] == "<|s_0|>" and toks[m.SYNTH_SPEECH0 + 12799] == "<|s_12799|>"
+    types = {t.name: t.type for t in g.tensors}
+    assert types["blk.0.attn_q.weight"] == 12 and types["token_embd.weight"] == 14
+    assert types["blk.2.ffn_down.weight"] == 14  # use_more_bits layer (Q4_K_M recipe)
+    assert types["blk.0.attn_q_norm.weight"] == 0
+
+
+@pytest.mark.parametrize("preset", [0, 1])
+def test_oracle_llm_deterministic_and_in_range(tiny_llms, preset):
+    o = pyoracle.Llm(tiny_llms[preset], 128)
+    prompt = [256, 257, 72, 105, 258, 257]
+    allow = (m.SYNTH_SPEECH0, m.SYNTH_SPEECH0 + 12800)
+    a = o.generate(prompt, 24, 0.8, 42, allow=allow)
+    b = o.generate(prompt, 24, 0.8, 42, allow=allow)
+    assert np.array_equal(a, b) and len(a) == 24
+    assert ((a >= allow[0]) & (a < allow[1])).all()
+    g = o.generate(prompt, 8, 0.0, 0)  # greedy
+    o.reset()
+    for i, t in enumerate(prompt):
+        lg = o.eval(t, i)
+    assert g[0] == int(np.argmax(lg))
+
+
+def test_sampler_distribution_matches_softmax():
+    """Gumbel-max with temperature samples softmax(logits/T) (llama.cpp temp -> dist)."""
+    logits = np.array([1.0, 2.0, 0.5, -1.0, 1.5], np.float32)
+    T = 0.8
+    n = 20000
+    counts = np.zeros(5)
+    for step in range(n):
+        counts[pyoracle.sample(logits, T, 42, step, 0, 5)] += 1
+    p = np.exp(logits / T - (logits / T).max())
+    p /= p.sum()
+    assert np.abs(counts / n - p).max() < 0.015
+    assert pyoracle.sample(logits, 0.0, 42, 0, 0, 5) == 1
+    assert pyoracle.sample(logits, 0.8, 42, 3, 2, 4) in (2, 3)
