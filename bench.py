@@ -1,0 +1,231 @@
+#!/usr/bin/env python3
+"""bench.py — BASELINE metric of the MI355X-native MioTTS path.
+
+Metric (BASELINE.json): realtime factor (audio s / wall s) + stage ms llm/codec/istft on
+MioTTS-1.7B Q4_K_M (configs[2]): one "step" = one whole utterance of the reference
+pipeline (test-to-speech.cpp:94-246): chat-template prompt -> prefill -> 700 sampled
+speech tokens (temp 0.8, device sampler, speech ids only so synthetic weights yield
+exactly 700 codes: flagged harness deviation) -> MioCodec decode -> iSTFT ->
+PCM in host memory. Weights are synthetic (no checkpoints offline) with the
+published shapes; "data": "synthetic".
+
+Multi-GPU: one process per GPU (torchrun), each rank synthesizes its own utterances
+(utterances are independent: no collective on the data path, "scaling": "weak"); a gloo
+barrier brackets the timed region and the max elapsed over ranks is used.
+
+roofline: the decode-step kernel with the largest per-token time, timed live with HIP
+events on the runner's stream (mio_hip_llm_time_kernel) after the timed region;
+achieved = its algorithmic bytes per launch / mean launch time; peak = 8 TB/s HBM3E.
+cpu_baseline: the C oracle (oracle/, "port") on rank 0 at N=1 only, timed on a bounded
+sample (decode steps + codec/iSTFT of a few codes) and extrapolated to one utterance.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "miotts-llama.cpp_amd", "python"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+KERNEL_NAMES = {0: "k_attn_in", 1: "k_attention", 2: "k_attn_out", 3: "k_ffn_in", 4: "k_ffn_down",
+                6: "k_lm_head"}
+PRESETS = {2: "MioTTS-0.1B Q8_0", 3: "MioTTS-1.7B Q4_K_M", 4: "MioTTS-2.6B Q8_0"}
+PROMPT = "こんにちは、今日はいい天気ですね。"  # README.md:83, SURVEY 8(d)
+
+
+def parse_args():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=3)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--preset", type=int, default=3, choices=sorted(PRESETS))
+    p.add_argument("--tokens", type=int, default=700)
+    p.add_argument("--utts-per-step", type=int, default=1)
+    p.add_argument("--workdir", default=os.environ.get("MIOTTS_BENCH_DIR", "/tmp/miotts_bench"))
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-tokens", type=int, default=12)
+    p.add_argument("--cpu-codes", type=int, default=40)
+    return p.parse_args()
+
+
+def prompt_tokens(text: str):
+    """normalize_tts_text + build_prompt + tokenize with the synthetic byte-level vocab
+    (test-to-speech.cpp:90-92,114-125): specials -> ids 256/257/258, bytes -> ids 0..255."""
+    import miotts_amd as m
+    norm = m.normalize_text(text)
+    toks = [256, 257] + list("user\n".encode()) + list(norm.encode("utf-8")) + [258]
+    toks += list("\n".encode()) + [257] + list("assistant\n".encode())
+    return toks
+
+
+def ensure_files(workdir, preset, rank, barrier):
+    import miotts_amd as m
+    os.makedirs(workdir, exist_ok=True)
+    llm = os.path.join(workdir, f"llm_preset{preset}.gguf")
+    codec = os.path.join(workdir, "miocodec_synth.gguf")
+    voice = os.path.join(workdir, "voice_synth.emb.gguf")
+    if rank == 0:
+        for path, fn in ((llm, lambda p: m.synth_llm(p, preset, 1)), (codec, lambda p: m.synth_codec(p, 0, 1)),
+                         (voice, lambda p: m.synth_voice(p, 7))):
+            if not os.path.exists(path):
+                tmp = path + ".tmp"
+                fn(tmp)
+                os.replace(tmp, path)
+    barrier()
+    return llm, codec, voice
+
+
+def cpu_baseline(llm_path, codec_path, voice_path, n_tok, n_codes, utt_tokens):
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import numpy as np
+    import miotts_amd as m
+    import pyoracle
+    o = pyoracle.Llm(llm_path, 256)
+    t0 = time.perf_counter()
+    for pos in range(n_tok):
+        o.eval(m.SYNTH_SPEECH0 + (pos * 97) % 12800, pos)
+    t_tok = (time.perf_counter() - t0) / n_tok
+    c = pyoracle.Codec(codec_path)
+    emb = m.read_voice(voice_path)
+    codes = (np.arange(n_codes) * 7919) % 12800
+    t0 = time.perf_counter()
+    c.decode_pcm(codes, emb)
+    t_code = (time.perf_counter() - t0) / n_codes
+    wall = utt_tokens * t_tok + utt_tokens * t_code
+    audio = utt_tokens * 1764 / 44100.0
+    cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    return {"value": round(audio / wall, 4), "unit": "x realtime (audio s / wall s)", "cores": cores,
+            "kind": "port",
+            "sample": f"oracle decode of {n_tok} tokens ({t_tok * 1e3:.1f} ms/token) + codec+iSTFT of "
+                      f"{n_codes} codes ({t_code * 1e3:.2f} ms/code), extrapolated to {utt_tokens} tokens"}
+
+
+def main():
+    a = parse_args()
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local_rank = int(os.environ.get("LOCAL_RANK", 0))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    import numpy as np
+    import miotts_amd as m
+
+    llm_path, codec_path, voice_path = ensure_files(a.workdir, a.preset, rank, barrier)
+    dev = m.Device(local_rank)
+    llm = m.Llm(dev, llm_path, 2048)
+    codec = m.Codec(dev, codec_path)
+    emb = m.read_voice(voice_path)
+    prompt = prompt_tokens(PROMPT)
+    allow = (m.SYNTH_SPEECH0, m.SYNTH_SPEECH0 + 12800)
+
+    stage = {"llm_ms": 0.0, "codec_ms": 0.0, "istft_ms": 0.0, "codec_wall_ms": 0.0}
+    audio_samples = 0
+
+    def utterance(seed, record):
+        nonlocal audio_samples
+        t0 = time.perf_counter()
+        toks = llm.generate(prompt, a.tokens, 0.8, seed, allow=allow, check_interval=20)
+        t1 = time.perf_counter()
+        pcm = codec.decode_pcm(toks - m.SYNTH_SPEECH0, emb)
+        t2 = time.perf_counter()
+        if record:
+            c_ms, i_ms = codec.last_timings()
+            stage["llm_ms"] += (t1 - t0) * 1e3
+            stage["codec_wall_ms"] += (t2 - t1) * 1e3
+            stage["codec_ms"] += c_ms
+            stage["istft_ms"] += i_ms
+            audio_samples += len(pcm)
+        if len(toks) != a.tokens or len(pcm) != a.tokens * codec.samples_per_token:
+            raise RuntimeError(f"utterance produced {len(toks)} tokens / {len(pcm)} samples")
+
+    for w in range(a.warmup):
+        for u in range(a.utts_per_step):
+            utterance(42 + 7919 * rank + 104729 * (w * a.utts_per_step + u), False)
+    dev.sync()
+    barrier()
+    t_start = time.perf_counter()
+    for s in range(a.steps):
+        for u in range(a.utts_per_step):
+            utterance(42 + 7919 * rank + 104729 * (1000 + s * a.utts_per_step + u), True)
+    dev.sync()
+    barrier()
+    elapsed = time.perf_counter() - t_start
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        n = torch.tensor([audio_samples], dtype=torch.float64)
+        dist.all_reduce(n, op=dist.ReduceOp.SUM)
+        total_samples = float(n.item())
+    else:
+        total_samples = float(audio_samples)
+    audio_s = total_samples / codec.sample_rate
+    value = audio_s / elapsed
+
+    # roofline of the dominant decode-step kernel, timed live on the runner's stream
+    per_token = {}
+    for which in (0, 1, 2, 3, 4, 6):
+        ms, by = llm.time_kernel(which, 40)
+        count = 1 if which == 6 else llm.n_layer
+        per_token[which] = (ms * count, ms, by)
+    dom = max((w for w in per_token if per_token[w][2] > 0), key=lambda w: per_token[w][0])
+    _, dom_ms, dom_bytes = per_token[dom]
+    achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
+    traffic = None
+    tfile = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    if os.path.exists(tfile):
+        try:
+            tj = json.load(open(tfile))
+            if tj.get("preset") == a.preset:
+                traffic = tj.get("per_launch_bytes", {}).get(KERNEL_NAMES[dom])
+        except Exception:
+            traffic = None
+
+    steps_total = a.steps * a.utts_per_step
+    out = {
+        "metric": "realtime factor (audio s / wall s) + stage ms llm/codec/istft, 1.7B Q4_K_M",
+        "value": round(value, 3),
+        "unit": "x realtime (audio s / wall s)",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(elapsed / a.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int8-dot (q4_K/q6_K x q8_K) + f32/f16 codec",
+        "data": "synthetic",
+        "config": {"workload": f"{PRESETS[a.preset]} single utterance, {a.tokens} speech tokens -> "
+                               f"MioCodec -> iSTFT ({a.tokens * 1764 / 44100:.1f} s audio) per GPU",
+                   "model": PRESETS[a.preset], "global_batch": world * a.utts_per_step,
+                   "seq_len": a.tokens, "parallelism": f"utterance-sharded x{world} (no collective)"},
+        "stage_ms": {k: round(v / steps_total, 3) for k, v in stage.items()},
+        "llm_ms_per_token": round(stage["llm_ms"] / steps_total / a.tokens, 4),
+        "roofline": {"bound": "hbm", "kernel": KERNEL_NAMES[dom], "achieved": round(achieved, 1),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": traffic, "bytes_per_launch": dom_bytes,
+                     "avg_launch_us": round(dom_ms * 1e3, 3),
+                     "step_weight_bytes": llm.weight_bytes(),
+                     "per_token_ms": {KERNEL_NAMES[w]: round(v[0], 4) for w, v in per_token.items()}},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(llm_path, codec_path, voice_path, a.cpu_tokens, a.cpu_codes, a.tokens)
+    if rank == 0:
+        print(json.dumps(out, ensure_ascii=False), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

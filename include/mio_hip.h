@@ -125,12 +125,27 @@ int mio_hip_llm_generate(mio_hip_llm *m, const int32_t *prompt, int n_prompt, in
                          int32_t eos0, int32_t eos1, int32_t check_interval,
                          int32_t *out_tokens, int *n_out);
 
+/* Live timing of one decode-step kernel (which: 0 attn_in, 1 attention, 2 attn_out,
+ * 3 ffn_in, 4 ffn_down of layer n_layer/2; 6 lm_head): `iters` back-to-back launches on
+ * the runner's stream between HIP events (state/buffers of the last generate/eval).
+ * *avg_ms = mean duration; *bytes = algorithmic HBM bytes per launch. */
+int mio_hip_llm_time_kernel(mio_hip_llm *m, int which, int iters, float *avg_ms, uint64_t *bytes);
+/* Stage times (ms, HIP events) of the last mio_hip_codec_decode_pcm: [0] codec, [1] iSTFT. */
+int mio_hip_codec_last_timings(const mio_hip_codec *c, float *ms2);
+
 /* Parity helpers: y[rows] = W x for a GGUF-layout quantized matrix (gguf_rows, ggml type
  * 8/12/14) with x re-quantized to the ggml vec_dot_type, on the GPU matvec kernels; and
  * the host quantizer used to build synthetic models (ggml block layout out). */
 int mio_hip_debug_matvec(mio_hip_device *d, uint32_t type, const void *gguf_rows, int rows, int k,
                          const float *x, float *y);
 int mio_quantize_rows(uint32_t type, const float *x, int rows, int k, void *out);
+
+/* ---------------- host text / file utilities ----------------
+ * normalize_tts_text (text-normalize.h:7), parse_speech_tokens (token-parser.h:8) and the
+ * WAV image wav_write writes (wav-writer.h:6), for FFI callers and tests. */
+int mio_normalize_tts_text(const char *text, char *out, int cap, int *out_len);
+int mio_parse_speech_tokens(const char *text, int32_t *codes, int cap, int *n);
+int mio_wav_encode(const float *samples, int n, int sample_rate, uint8_t *out, int cap, int *out_len);
 
 /* ---------------- synthetic model files ----------------
  * No GGUF model files exist offline. These write files with the

@@ -63,6 +63,9 @@ struct LlmBuffers {
 void launch_decode_step(const LlmDims &d, const LayerW *layers, int n_layer, _Float16 *kcache,
                         _Float16 *vcache, const float *out_norm, const QMat &lm, const QMat &tok_embd,
                         const LlmBuffers &b, const SampleCfg &sc, hipStream_t s);
+void launch_step_kernel(int which, const LlmDims &d, const LayerW *layers, int il, _Float16 *kcache,
+                        _Float16 *vcache, const float *out_norm, const QMat &lm, const QMat &tok_embd,
+                        const LlmBuffers &b, const SampleCfg &sc, hipStream_t s);
 // Embedding of `token` (row of token_embd) -> b.x, and state reset to (pos, token).
 void launch_embed_token(const LlmDims &d, const QMat &tok_embd, const LlmBuffers &b, hipStream_t s);
 int lm_head_blocks(const LlmDims &d);

@@ -824,35 +824,68 @@ void launch_embed_token(const LlmDims &d, const QMat &tok_embd, const LlmBuffers
     hipLaunchKernelGGL(k_embed, dim3(1), dim3(NT), 0, s, d, tok_embd, b);
 }
 
-void launch_decode_step(const LlmDims &d, const LayerW *layers, int n_layer, _Float16 *kcache,
+// Launch one kernel of the step: which = 0 attn_in, 1 attention, 2 attn_out, 3 ffn_in,
+// 4 ffn_down (layer il), 5 final_norm, 6 lm_head, 7 sample.
+void launch_step_kernel(int which, const LlmDims &d, const LayerW *layers, int il, _Float16 *kcache,
                         _Float16 *vcache, const float *out_norm, const QMat &lm, const QMat &tok_embd,
                         const LlmBuffers &b, const SampleCfg &sc, hipStream_t s) {
     const size_t layer_kv = (size_t)d.n_kv * d.n_ctx * d.hd;
     const int G = d.n_head / d.n_kv;
     const int ns = NT / (d.hd / 8);
     const size_t att_lds = (size_t)ns * G * (d.hd + 2) * 4;
-    for (int il = 0; il < n_layer; ++il) {
-        const LayerW &L = layers[il];
-        const int qkv_rows = L.wq.rows + L.wk.rows + L.wv.rows;
-        hipLaunchKernelGGL(k_attn_in, dim3((qkv_rows + QKV_ROWS - 1) / QKV_ROWS), dim3(NT), smem_bytes(d.n_embd), s,
-                           d, L.attn_norm, L.wq, L.wk, L.wv, b);
-        if (d.hd == 128)
-            launch_attention<128>(G, dim3(d.max_splits, d.n_kv), att_lds, s, d, L.q_norm, L.k_norm,
-                                  kcache + il * layer_kv, vcache + il * layer_kv, b);
-        else
-            launch_attention<64>(G, dim3(d.max_splits, d.n_kv), att_lds, s, d, L.q_norm, L.k_norm,
-                                 kcache + il * layer_kv, vcache + il * layer_kv, b);
-        hipLaunchKernelGGL(k_attn_out, dim3((L.wo.rows + RES_ROWS - 1) / RES_ROWS), dim3(NT),
-                           smem_bytes(d.n_head * d.hd), s, d, L.wo, b);
-        hipLaunchKernelGGL(k_ffn_in, dim3((L.gate.rows + FFN_PAIRS - 1) / FFN_PAIRS), dim3(NT), smem_bytes(d.n_embd), s,
-                           d, L.ffn_norm, L.gate, L.up, b);
-        hipLaunchKernelGGL(k_ffn_down, dim3((L.down.rows + RES_ROWS - 1) / RES_ROWS), dim3(NT), smem_bytes(d.n_ff), s,
-                           d, L.down, b);
-    }
-    hipLaunchKernelGGL(k_final_norm, dim3(1), dim3(NT), smem_bytes(d.n_embd), s, d, out_norm, lm.type != 8 ? 1 : 0, b);
     const int nblk = lm_head_blocks(d);
-    hipLaunchKernelGGL(k_lm_head, dim3(nblk), dim3(NT), smem_bytes(d.n_embd), s, d, lm, sc, b);
-    hipLaunchKernelGGL(k_sample, dim3(1), dim3(NT), 0, s, d, sc, tok_embd, nblk, b);
+    switch (which) {
+        case 0: {
+            const LayerW &L = layers[il];
+            const int qkv_rows = L.wq.rows + L.wk.rows + L.wv.rows;
+            hipLaunchKernelGGL(k_attn_in, dim3((qkv_rows + QKV_ROWS - 1) / QKV_ROWS), dim3(NT), smem_bytes(d.n_embd),
+                               s, d, L.attn_norm, L.wq, L.wk, L.wv, b);
+            break;
+        }
+        case 1: {
+            const LayerW &L = layers[il];
+            if (d.hd == 128)
+                launch_attention<128>(G, dim3(d.max_splits, d.n_kv), att_lds, s, d, L.q_norm, L.k_norm,
+                                      kcache + il * layer_kv, vcache + il * layer_kv, b);
+            else
+                launch_attention<64>(G, dim3(d.max_splits, d.n_kv), att_lds, s, d, L.q_norm, L.k_norm,
+                                     kcache + il * layer_kv, vcache + il * layer_kv, b);
+            break;
+        }
+        case 2: {
+            const LayerW &L = layers[il];
+            hipLaunchKernelGGL(k_attn_out, dim3((L.wo.rows + RES_ROWS - 1) / RES_ROWS), dim3(NT),
+                               smem_bytes(d.n_head * d.hd), s, d, L.wo, b);
+            break;
+        }
+        case 3: {
+            const LayerW &L = layers[il];
+            hipLaunchKernelGGL(k_ffn_in, dim3((L.gate.rows + FFN_PAIRS - 1) / FFN_PAIRS), dim3(NT),
+                               smem_bytes(d.n_embd), s, d, L.ffn_norm, L.gate, L.up, b);
+            break;
+        }
+        case 4: {
+            const LayerW &L = layers[il];
+            hipLaunchKernelGGL(k_ffn_down, dim3((L.down.rows + RES_ROWS - 1) / RES_ROWS), dim3(NT),
+                               smem_bytes(d.n_ff), s, d, L.down, b);
+            break;
+        }
+        case 5:
+            hipLaunchKernelGGL(k_final_norm, dim3(1), dim3(NT), smem_bytes(d.n_embd), s, d, out_norm,
+                               lm.type != 8 ? 1 : 0, b);
+            break;
+        case 6: hipLaunchKernelGGL(k_lm_head, dim3(nblk), dim3(NT), smem_bytes(d.n_embd), s, d, lm, sc, b); break;
+        case 7: hipLaunchKernelGGL(k_sample, dim3(1), dim3(NT), 0, s, d, sc, tok_embd, nblk, b); break;
+        default: break;
+    }
+}
+
+void launch_decode_step(const LlmDims &d, const LayerW *layers, int n_layer, _Float16 *kcache,
+                        _Float16 *vcache, const float *out_norm, const QMat &lm, const QMat &tok_embd,
+                        const LlmBuffers &b, const SampleCfg &sc, hipStream_t s) {
+    for (int il = 0; il < n_layer; ++il)
+        for (int k = 0; k < 5; ++k) launch_step_kernel(k, d, layers, il, kcache, vcache, out_norm, lm, tok_embd, b, sc, s);
+    for (int k = 5; k < 8; ++k) launch_step_kernel(k, d, layers, 0, kcache, vcache, out_norm, lm, tok_embd, b, sc, s);
 }
 
 }  // namespace mio

@@ -73,6 +73,9 @@ struct mio_hip_codec {
     size_t ws_cap = 0;
     mio_hip_istft *ist = nullptr;
     std::vector<void *> allocs;
+    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+    float last_ms[2] = {0, 0};
+    bool timed = false;
 
     ~mio_hip_codec() {
         if (d) hipSetDevice(d->dev);
@@ -80,6 +83,8 @@ struct mio_hip_codec {
         if (rope) hipFree(rope);
         if (ws) hipFree(ws);
         if (ist) mio_hip_istft_destroy(ist);
+        for (auto e : ev)
+            if (e) hipEventDestroy(e);
     }
 };
 
@@ -705,10 +710,16 @@ extern "C" int mio_hip_codec_decode_pcm(mio_hip_codec *c, const int32_t *codes, 
     if ((rc = prepare_inputs(c, w, codes, n_codes, emb, flags, s))) return rc;
     const float *buf = nullptr;
     int r = 0, cc = 0;
+    if (!c->ev[0])
+        for (auto &e : c->ev) MIO_HIP_CHECK(hipEventCreate(&e));
+    MIO_HIP_CHECK(hipEventRecord(c->ev[0], s));
     if ((rc = run_decode(c, w, s, 1 << 20, &buf, &r, &cc))) return rc;
+    MIO_HIP_CHECK(hipEventRecord(c->ev[1], s));
     int len = 0;
     if ((rc = mio_hip_istft_out_len(c->ist, w.Lf, c->hop, &len))) return rc;
     if ((rc = mio_istft_launch_device(c->ist, w.spec, w.Lf, c->hop, w.pcm, s))) return rc;
+    MIO_HIP_CHECK(hipEventRecord(c->ev[2], s));
+    c->timed = true;
     MIO_HIP_CHECK(hipGetLastError());
     if (out_len) *out_len = len;
     if (flags & MIO_OUT_DEVICE) {
@@ -717,5 +728,13 @@ extern "C" int mio_hip_codec_decode_pcm(mio_hip_codec *c, const int32_t *codes, 
         MIO_HIP_CHECK(hipMemcpyAsync(out_pcm, w.pcm, (size_t)len * 4, hipMemcpyDeviceToHost, s));
         MIO_HIP_CHECK(hipStreamSynchronize(s));
     }
+    return MIO_OK;
+}
+
+extern "C" int mio_hip_codec_last_timings(const mio_hip_codec *c, float *ms2) {
+    MIO_REQUIRE(c && ms2 && c->timed, MIO_ERR_INVALID, "codec_last_timings: no timed decode yet");
+    MIO_HIP_CHECK(hipEventSynchronize(c->ev[2]));
+    MIO_HIP_CHECK(hipEventElapsedTime(&ms2[0], c->ev[0], c->ev[1]));
+    MIO_HIP_CHECK(hipEventElapsedTime(&ms2[1], c->ev[1], c->ev[2]));
     return MIO_OK;
 }

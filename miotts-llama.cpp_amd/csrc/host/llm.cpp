@@ -426,3 +426,50 @@ extern "C" int mio_quantize_rows(uint32_t type, const float *x, int rows, int k,
         if (!mio::quantize_row(type, x + (size_t)r * k, (uint8_t *)out + r * rb, k)) return MIO_ERR_UNSUPPORTED;
     return MIO_OK;
 }
+
+// Live timing of one kernel of the decode step (bench.py roofline): launches kernel
+// `which` (0 attn_in, 1 attention, 2 attn_out, 3 ffn_in, 4 ffn_down, 6 lm_head) of layer
+// n_layer/2 `iters` times on the runner's stream between HIP events, with the buffers and
+// device state left by the last generate/eval. Returns the mean duration and the
+// algorithmic HBM bytes of one launch (weights of the matrices it streams + activations).
+extern "C" int mio_hip_llm_time_kernel(mio_hip_llm *m, int which, int iters, float *avg_ms, uint64_t *bytes) {
+    MIO_REQUIRE(m && avg_ms && bytes && iters > 0 && m->graph, MIO_ERR_INVALID,
+                "llm_time_kernel: run generate/eval first");
+    MIO_REQUIRE(which >= 0 && which <= 6 && which != 5, MIO_ERR_INVALID, "llm_time_kernel: which %d", which);
+    int rc = mio::bind(m->d);
+    if (rc) return rc;
+    const int il = m->n_layer / 2;
+    const mio::LayerW &L = m->layers[il];
+    auto qbytes = [](const mio::QMat &q) {
+        return (uint64_t)mio::ggml_row_bytes(q.type, q.k) * (uint64_t)q.rows;
+    };
+    const mio::LlmDims &D = m->dims;
+    uint64_t b = 0;
+    switch (which) {
+        case 0: b = qbytes(L.wq) + qbytes(L.wk) + qbytes(L.wv) + 4ull * D.n_embd * 2; break;
+        case 1: b = 0; break;
+        case 2: b = qbytes(L.wo) + 4ull * D.n_embd * 2; break;
+        case 3: b = qbytes(L.gate) + qbytes(L.up) + 4ull * (D.n_embd * 2 + D.n_ff); break;
+        case 4: b = qbytes(L.down) + 4ull * (D.n_ff + 2 * D.n_embd); break;
+        case 6: b = qbytes(m->lm) + 4ull * D.n_vocab; break;
+    }
+    hipEvent_t e0, e1;
+    MIO_HIP_CHECK(hipEventCreate(&e0));
+    MIO_HIP_CHECK(hipEventCreate(&e1));
+    hipStream_t s = m->d->stream;
+    // warm
+    mio::launch_step_kernel(which, D, m->layers.data(), il, m->kc, m->vc, m->out_norm, m->lm, m->tok, m->buf,
+                            m->graph_cfg, s);
+    MIO_HIP_CHECK(hipEventRecord(e0, s));
+    for (int i = 0; i < iters; ++i)
+        mio::launch_step_kernel(which, D, m->layers.data(), il, m->kc, m->vc, m->out_norm, m->lm, m->tok, m->buf,
+                                m->graph_cfg, s);
+    MIO_HIP_CHECK(hipEventRecord(e1, s));
+    MIO_HIP_CHECK(hipEventSynchronize(e1));
+    float ms = 0;
+    MIO_HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+    hipEventDestroy(e0), hipEventDestroy(e1);
+    *avg_ms = ms / iters;
+    *bytes = b;
+    return MIO_OK;
+}

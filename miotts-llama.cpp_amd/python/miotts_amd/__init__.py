@@ -81,6 +81,11 @@ def _declare(L: ctypes.CDLL) -> None:
         "mio_synth_llm_gguf": (c_int, [ctypes.c_char_p, c_int, ctypes.c_uint64]),
         "mio_hip_llm_load": (c_int, [_vp, ctypes.c_char_p, c_int, ctypes.POINTER(_vp)]),
         "mio_hip_llm_free": (None, [_vp]),
+        "mio_normalize_tts_text": (c_int, [ctypes.c_char_p, _vp, c_int, ctypes.POINTER(c_int)]),
+        "mio_parse_speech_tokens": (c_int, [ctypes.c_char_p, _vp, c_int, ctypes.POINTER(c_int)]),
+        "mio_wav_encode": (c_int, [_vp, c_int, c_int, _vp, c_int, ctypes.POINTER(c_int)]),
+        "mio_hip_llm_time_kernel": (c_int, [_vp, c_int, c_int, _f32p, ctypes.POINTER(ctypes.c_uint64)]),
+        "mio_hip_codec_last_timings": (c_int, [_vp, _f32p]),
         "mio_hip_debug_matvec": (c_int, [_vp, ctypes.c_uint32, _vp, c_int, c_int, _vp, _vp]),
         "mio_quantize_rows": (c_int, [ctypes.c_uint32, _vp, c_int, c_int, _vp]),
         "mio_hip_llm_info": (c_int, [_vp, _i32p]),
@@ -311,6 +316,11 @@ class Codec:
                                              stream or None))
         return n.value
 
+    def last_timings(self):
+        ms = np.zeros(2, np.float32)
+        check(lib().mio_hip_codec_last_timings(self.h, ms.ctypes.data_as(_f32p)))
+        return float(ms[0]), float(ms[1])
+
     def decode_stage(self, codes, emb, stage: int, max_elems: int) -> np.ndarray:
         codes = np.ascontiguousarray(codes, dtype=np.int32)
         emb = np.ascontiguousarray(emb, dtype=np.float32)
@@ -371,6 +381,12 @@ class Llm:
         check(lib().mio_hip_llm_logits(self.h, _ptr(out)))
         return out
 
+    def time_kernel(self, which: int, iters: int = 50):
+        ms = ctypes.c_float(0)
+        b = ctypes.c_uint64(0)
+        check(lib().mio_hip_llm_time_kernel(self.h, which, iters, ctypes.byref(ms), ctypes.byref(b)))
+        return ms.value, b.value
+
     def generate(self, prompt, max_tokens: int, temperature: float = 0.8, seed: int = 42,
                  allow=(-1, -1), eos=(-1, -1), check_interval: int = 20) -> np.ndarray:
         prompt = np.ascontiguousarray(prompt, dtype=np.int32)
@@ -401,3 +417,33 @@ def debug_matvec(dev: Device, qtype: int, w_rows: np.ndarray, k: int, x: np.ndar
     y = np.empty(w_rows.shape[0], np.float32)
     check(lib().mio_hip_debug_matvec(dev.h, qtype, _ptr(w_rows), w_rows.shape[0], k, _ptr(x), _ptr(y)))
     return y
+
+
+# ---------------------------------------------------------------- host text utilities
+def normalize_text(text: str) -> str:
+    """normalize_tts_text (text-normalize.h:7) via the C-ABI."""
+    b = text.encode("utf-8")
+    cap = 4 * len(b) + 16
+    out = ctypes.create_string_buffer(cap)
+    n = ctypes.c_int(0)
+    check(lib().mio_normalize_tts_text(b, out, cap, ctypes.byref(n)))
+    return out.raw[: n.value].decode("utf-8")
+
+
+def parse_speech_tokens(text: str) -> np.ndarray:
+    b = text.encode("utf-8")
+    n = ctypes.c_int(0)
+    check(lib().mio_parse_speech_tokens(b, None, 0, ctypes.byref(n)))
+    out = np.zeros(max(n.value, 1), np.int32)
+    check(lib().mio_parse_speech_tokens(b, _ptr(out), len(out), ctypes.byref(n)))
+    return out[: n.value]
+
+
+def wav_bytes(samples: np.ndarray, sample_rate: int = 44100) -> bytes:
+    s = np.ascontiguousarray(samples, dtype=np.float32)
+    cap = 44 + 2 * len(s)
+    out = np.zeros(cap, np.uint8)
+    n = ctypes.c_int(0)
+    check(lib().mio_wav_encode(_ptr(s) if len(s) else None, len(s), sample_rate, _ptr(out), cap,
+                               ctypes.byref(n)))
+    return out[: n.value].tobytes()
