@@ -54,6 +54,7 @@ struct LlmBuffers {
     float *h;          // [n_ff] ffn activation
     float *logits;     // [n_vocab]
     float *act;        // quantized final-norm activation (global)
+    float *act2;       // quantized attention output (global, written by k_attn_combine)
     float *smp;        // sampler partials [2 * n_lm_blocks]
     const float2 *rope;  // [n_ctx][hd/2] (cos, sin)
     StepState *st;

@@ -176,6 +176,9 @@ __device__ inline void quantize(const float *xs, int K, bool kquant, const ActL 
 }
 
 // ------------------------------------------------------------------ row dots (one wave)
+// A row's quant payload for one "pass" (8 superblocks = 2048 weights for K-quants, 64
+// blocks = 2048 weights for Q8_0) is one 16-B-per-lane load (+ headers); loads are issued
+// into Frags BEFORE the activation prologue so HBM latency overlaps the RMSNorm/quantize.
 __device__ inline int sbyte(const uint4 &h, int i) {
     const uint32_t w = i < 4 ? h.y : (i < 8 ? h.z : h.w);
     return (int)((w >> ((i & 3) * 8)) & 0xFF);
@@ -199,203 +202,261 @@ __device__ inline float wave_sum(float v) {
 
 constexpr uint32_t M4 = 0x0F0F0F0Fu, M2 = 0x03030303u;
 
-template <int NR>
-__device__ void dot_q4k(const QMat &W, const int (&rows)[NR], const ActL &a, float (&out)[NR]) {
+struct Frag {
+    uint4 a, b;
+    int c, d;
+    uint32_t e;
+};
+
+__device__ inline int npass_of(const QMat &W) {
+    return W.type == 8 ? ((W.k >> 5) + 63) / 64 : ((W.k >> 8) + 7) / 8;
+}
+
+__device__ inline Frag load_frag(const QMat &W, int row, int pass) {
     const int lane = threadIdx.x & 63;
-    const int nsb = W.k >> 8;
-    const int pc = lane & 7, jj = pc >> 1, hh = pc & 1;
-    float acc[NR];
-#pragma unroll
-    for (int r = 0; r < NR; ++r) acc[r] = 0.0f;
-    for (int sb0 = 0; sb0 < nsb; sb0 += 8) {
-        const int sb = sb0 + (lane >> 3);
-        const bool ok = sb < nsb;
-        uint4 q[NR], hd[NR];
-#pragma unroll
-        for (int r = 0; r < NR; ++r) {
-            if (ok && rows[r] >= 0) {
-                q[r] = ld16(W.p0 + (size_t)rows[r] * (W.k / 2) + sb * 128 + pc * 16);
-                hd[r] = ld16(W.p1 + ((size_t)rows[r] * nsb + sb) * 16);
-            } else {
-                q[r] = make_uint4(0, 0, 0, 0);
-                hd[r] = make_uint4(0, 0, 0, 0);
-            }
+    Frag f;
+    f.a = f.b = make_uint4(0, 0, 0, 0);
+    f.c = f.d = 0;
+    f.e = 0;
+    if (row < 0) return f;
+    if (W.type == 12) {
+        const int nsb = W.k >> 8, sb = pass * 8 + (lane >> 3), pc = lane & 7;
+        if (sb < nsb) {
+            f.a = ld16(W.p0 + (size_t)row * (W.k / 2) + sb * 128 + pc * 16);
+            f.b = ld16(W.p1 + ((size_t)row * nsb + sb) * 16);
         }
+    } else if (W.type == 14) {
+        const int nsb = W.k >> 8, sb = pass * 8 + (lane >> 3), pc = lane & 7;
+        if (sb < nsb) {
+            const int n = pc >> 2, qq = pc & 3, gl = qq >> 1, l0 = 16 * (qq & 1);
+            f.a = ld16(W.p0 + (size_t)row * (W.k / 2) + sb * 128 + pc * 16);
+            f.b = ld16(W.p1 + (size_t)row * (W.k / 4) + sb * 64 + 32 * n + l0);
+            const int8_t *sc = (const int8_t *)W.p2 + (size_t)row * (W.k / 16) + sb * 16 + 8 * n + 2 * gl + (l0 >> 4);
+            f.c = sc[0];
+            f.d = sc[4];
+            f.e = ((const uint16_t *)W.p3)[(size_t)row * nsb + sb];
+        }
+    } else {
+        const int nb = W.k >> 5, b = pass * 64 + lane;
+        if (b < nb) {
+            const uint8_t *p = W.p0 + (size_t)row * W.k + 32 * b;
+            f.a = ld16(p);
+            f.b = ld16(p + 16);
+            f.e = ((const uint16_t *)W.p1)[(size_t)row * nb + b];
+        }
+    }
+    return f;
+}
+
+// This lane's share of the row dot for one pass (summed over lanes by the caller).
+// Integer parts per superblock / block are exact (ggml vec_dot semantics).
+__device__ inline float compute_frag(const QMat &W, const Frag &f, int pass, const ActL &a) {
+    const int lane = threadIdx.x & 63;
+    if (W.type == 12) {
+        const int nsb = W.k >> 8, sb = pass * 8 + (lane >> 3), pc = lane & 7, jj = pc >> 1, hh = pc & 1;
+        const bool ok = sb < nsb;
         const int sbc = ok ? sb : 0;
         const int e_lo = sbc * 256 + 64 * jj + 16 * hh;
         const int4 alo = *reinterpret_cast<const int4 *>(a.qs + e_lo);
         const int4 ahi = *reinterpret_cast<const int4 *>(a.qs + e_lo + 32);
-        const int bslo = a.bs[e_lo >> 4], bshi = a.bs[(e_lo + 32) >> 4];
+        int dlo = 0, dhi = 0;
+        dlo = sdot4((int)(f.a.x & M4), alo.x, dlo);
+        dlo = sdot4((int)(f.a.y & M4), alo.y, dlo);
+        dlo = sdot4((int)(f.a.z & M4), alo.z, dlo);
+        dlo = sdot4((int)(f.a.w & M4), alo.w, dlo);
+        dhi = sdot4((int)((f.a.x >> 4) & M4), ahi.x, dhi);
+        dhi = sdot4((int)((f.a.y >> 4) & M4), ahi.y, dhi);
+        dhi = sdot4((int)((f.a.z >> 4) & M4), ahi.z, dhi);
+        dhi = sdot4((int)((f.a.w >> 4) & M4), ahi.w, dhi);
+        int sc0, m0, sc1, m1;
+        scale_min_k4(2 * jj, f.b, sc0, m0);
+        scale_min_k4(2 * jj + 1, f.b, sc1, m1);
+        int isum = sc0 * dlo + sc1 * dhi;
+        int imin = m0 * a.bs[e_lo >> 4] + m1 * a.bs[(e_lo + 32) >> 4];
+        isum += __shfl_xor(isum, 1);
+        isum += __shfl_xor(isum, 2);
+        isum += __shfl_xor(isum, 4);
+        imin += __shfl_xor(imin, 1);
+        imin += __shfl_xor(imin, 2);
+        imin += __shfl_xor(imin, 4);
+        if (!(ok && pc == 0)) return 0.0f;
         const float da = a.d[sbc];
-#pragma unroll
-        for (int r = 0; r < NR; ++r) {
-            int dlo = 0, dhi = 0;
-            dlo = sdot4((int)(q[r].x & M4), alo.x, dlo);
-            dlo = sdot4((int)(q[r].y & M4), alo.y, dlo);
-            dlo = sdot4((int)(q[r].z & M4), alo.z, dlo);
-            dlo = sdot4((int)(q[r].w & M4), alo.w, dlo);
-            dhi = sdot4((int)((q[r].x >> 4) & M4), ahi.x, dhi);
-            dhi = sdot4((int)((q[r].y >> 4) & M4), ahi.y, dhi);
-            dhi = sdot4((int)((q[r].z >> 4) & M4), ahi.z, dhi);
-            dhi = sdot4((int)((q[r].w >> 4) & M4), ahi.w, dhi);
-            int sc0, m0, sc1, m1;
-            scale_min_k4(2 * jj, hd[r], sc0, m0);
-            scale_min_k4(2 * jj + 1, hd[r], sc1, m1);
-            int isum = sc0 * dlo + sc1 * dhi;
-            int imin = m0 * bslo + m1 * bshi;
-            isum += __shfl_xor(isum, 1);
-            isum += __shfl_xor(isum, 2);
-            isum += __shfl_xor(isum, 4);
-            imin += __shfl_xor(imin, 1);
-            imin += __shfl_xor(imin, 2);
-            imin += __shfl_xor(imin, 4);
-            if (ok && pc == 0) {
-                const float d = h2f(hd[r].x & 0xFFFF) * da;
-                const float dmin = h2f(hd[r].x >> 16) * da;
-                float v = d * (float)isum;
-                v = v - dmin * (float)imin;
-                acc[r] += v;
-            }
-        }
-    }
-#pragma unroll
-    for (int r = 0; r < NR; ++r) out[r] = wave_sum(acc[r]);
-}
-
-template <int NR>
-__device__ void dot_q6k(const QMat &W, const int (&rows)[NR], const ActL &a, float (&out)[NR]) {
-    const int lane = threadIdx.x & 63;
-    const int nsb = W.k >> 8;
-    const int pc = lane & 7, n = pc >> 2, qq = pc & 3, gl = qq >> 1, l0 = 16 * (qq & 1);
-    float acc[NR];
-#pragma unroll
-    for (int r = 0; r < NR; ++r) acc[r] = 0.0f;
-    for (int sb0 = 0; sb0 < nsb; sb0 += 8) {
-        const int sb = sb0 + (lane >> 3);
+        const float d = h2f(f.b.x & 0xFFFF) * da;
+        const float dmin = h2f(f.b.x >> 16) * da;
+        float v = d * (float)isum;
+        v = v - dmin * (float)imin;
+        return v;
+    } else if (W.type == 14) {
+        const int nsb = W.k >> 8, sb = pass * 8 + (lane >> 3), pc = lane & 7;
+        const int n = pc >> 2, qq = pc & 3, gl = qq >> 1, l0 = 16 * (qq & 1);
         const bool ok = sb < nsb;
-        uint4 ql[NR], qh[NR];
-        int s0[NR], s1[NR];
-        uint32_t db[NR];
-#pragma unroll
-        for (int r = 0; r < NR; ++r) {
-            if (ok && rows[r] >= 0) {
-                const size_t row = (size_t)rows[r];
-                ql[r] = ld16(W.p0 + row * (W.k / 2) + sb * 128 + pc * 16);
-                qh[r] = ld16(W.p1 + row * (W.k / 4) + sb * 64 + 32 * n + l0);
-                const int8_t *sc = (const int8_t *)W.p2 + row * (W.k / 16) + sb * 16 + 8 * n + 2 * gl + (l0 >> 4);
-                s0[r] = sc[0];
-                s1[r] = sc[4];
-                db[r] = ((const uint16_t *)W.p3)[row * nsb + sb];
-            } else {
-                ql[r] = make_uint4(0, 0, 0, 0);
-                qh[r] = make_uint4(0, 0, 0, 0);
-                s0[r] = s1[r] = 0;
-                db[r] = 0;
-            }
-        }
         const int sbc = ok ? sb : 0;
         const int e_lo = sbc * 256 + 128 * n + 32 * gl + l0;
         const int4 alo = *reinterpret_cast<const int4 *>(a.qs + e_lo);
         const int4 ahi = *reinterpret_cast<const int4 *>(a.qs + e_lo + 64);
-        const int bslo = a.bs[e_lo >> 4], bshi = a.bs[(e_lo + 64) >> 4];
-        const float da = a.d[sbc];
         const int shl = 2 * gl, shh = 2 * gl + 4;
-#pragma unroll
-        for (int r = 0; r < NR; ++r) {
-            auto lo = [&](uint32_t l, uint32_t h) { return (int)((l & M4) | (((h >> shl) & M2) << 4)); };
-            auto hi = [&](uint32_t l, uint32_t h) { return (int)(((l >> 4) & M4) | (((h >> shh) & M2) << 4)); };
-            int dlo = 0, dhi = 0;
-            dlo = sdot4(lo(ql[r].x, qh[r].x), alo.x, dlo);
-            dlo = sdot4(lo(ql[r].y, qh[r].y), alo.y, dlo);
-            dlo = sdot4(lo(ql[r].z, qh[r].z), alo.z, dlo);
-            dlo = sdot4(lo(ql[r].w, qh[r].w), alo.w, dlo);
-            dhi = sdot4(hi(ql[r].x, qh[r].x), ahi.x, dhi);
-            dhi = sdot4(hi(ql[r].y, qh[r].y), ahi.y, dhi);
-            dhi = sdot4(hi(ql[r].z, qh[r].z), ahi.z, dhi);
-            dhi = sdot4(hi(ql[r].w, qh[r].w), ahi.w, dhi);
-            int isum = s0[r] * (dlo - 32 * bslo) + s1[r] * (dhi - 32 * bshi);
-            isum += __shfl_xor(isum, 1);
-            isum += __shfl_xor(isum, 2);
-            isum += __shfl_xor(isum, 4);
-            if (ok && pc == 0) {
-                const float d = h2f(db[r]) * da;
-                acc[r] += d * (float)isum;
-            }
-        }
+        auto lo = [&](uint32_t l, uint32_t h) { return (int)((l & M4) | (((h >> shl) & M2) << 4)); };
+        auto hi = [&](uint32_t l, uint32_t h) { return (int)(((l >> 4) & M4) | (((h >> shh) & M2) << 4)); };
+        int dlo = 0, dhi = 0;
+        dlo = sdot4(lo(f.a.x, f.b.x), alo.x, dlo);
+        dlo = sdot4(lo(f.a.y, f.b.y), alo.y, dlo);
+        dlo = sdot4(lo(f.a.z, f.b.z), alo.z, dlo);
+        dlo = sdot4(lo(f.a.w, f.b.w), alo.w, dlo);
+        dhi = sdot4(hi(f.a.x, f.b.x), ahi.x, dhi);
+        dhi = sdot4(hi(f.a.y, f.b.y), ahi.y, dhi);
+        dhi = sdot4(hi(f.a.z, f.b.z), ahi.z, dhi);
+        dhi = sdot4(hi(f.a.w, f.b.w), ahi.w, dhi);
+        int isum = f.c * (dlo - 32 * a.bs[e_lo >> 4]) + f.d * (dhi - 32 * a.bs[(e_lo + 64) >> 4]);
+        isum += __shfl_xor(isum, 1);
+        isum += __shfl_xor(isum, 2);
+        isum += __shfl_xor(isum, 4);
+        if (!(ok && pc == 0)) return 0.0f;
+        const float d = h2f(f.e) * a.d[sbc];
+        return d * (float)isum;
+    } else {
+        const int nb = W.k >> 5, b = pass * 64 + lane;
+        if (b >= nb) return 0.0f;
+        const int4 a0 = *reinterpret_cast<const int4 *>(a.qs + 32 * b);
+        const int4 a1 = *reinterpret_cast<const int4 *>(a.qs + 32 * b + 16);
+        int s = 0;
+        s = sdot4((int)f.a.x, a0.x, s);
+        s = sdot4((int)f.a.y, a0.y, s);
+        s = sdot4((int)f.a.z, a0.z, s);
+        s = sdot4((int)f.a.w, a0.w, s);
+        s = sdot4((int)f.b.x, a1.x, s);
+        s = sdot4((int)f.b.y, a1.y, s);
+        s = sdot4((int)f.b.z, a1.z, s);
+        s = sdot4((int)f.b.w, a1.w, s);
+        return (float)s * (h2f(f.e) * a.d[b]);
     }
-#pragma unroll
-    for (int r = 0; r < NR; ++r) out[r] = wave_sum(acc[r]);
 }
 
-template <int NR>
-__device__ void dot_q80(const QMat &W, const int (&rows)[NR], const ActL &a, float (&out)[NR]) {
-    const int lane = threadIdx.x & 63;
-    const int nb = W.k >> 5;
+// NR rows of W, all passes. PRE = passes whose loads were issued before the prologue
+// (pre[r][p], p < PRE); remaining passes are loaded one pass ahead.
+template <int NR, int PMAX>
+__device__ inline void preload(const QMat &W, const int (&rows)[NR], Frag (&pre)[NR][PMAX]) {
+    const int np = npass_of(W);
+#pragma unroll
+    for (int p = 0; p < PMAX; ++p)
+#pragma unroll
+        for (int r = 0; r < NR; ++r)
+            if (p < np) pre[r][p] = load_frag(W, rows[r], p);
+}
+
+template <int NR, int PMAX>
+__device__ inline void finish_rows(const QMat &W, const int (&rows)[NR], const Frag (&pre)[NR][PMAX],
+                                   const ActL &a, float (&out)[NR]) {
+    const int np = npass_of(W);
     float acc[NR];
 #pragma unroll
     for (int r = 0; r < NR; ++r) acc[r] = 0.0f;
-    for (int b0 = 0; b0 < nb; b0 += 64) {
-        const int b = b0 + lane;
-        const bool ok = b < nb;
-        uint4 q0[NR], q1[NR];
-        uint32_t db[NR];
 #pragma unroll
-        for (int r = 0; r < NR; ++r) {
-            if (ok && rows[r] >= 0) {
-                const uint8_t *p = W.p0 + (size_t)rows[r] * W.k + 32 * b;
-                q0[r] = ld16(p);
-                q1[r] = ld16(p + 16);
-                db[r] = ((const uint16_t *)W.p1)[(size_t)rows[r] * nb + b];
-            } else {
-                q0[r] = q1[r] = make_uint4(0, 0, 0, 0);
-                db[r] = 0;
-            }
-        }
-        const int bc = ok ? b : 0;
-        const int4 a0 = *reinterpret_cast<const int4 *>(a.qs + 32 * bc);
-        const int4 a1 = *reinterpret_cast<const int4 *>(a.qs + 32 * bc + 16);
-        const float da = a.d[bc];
+    for (int p = 0; p < PMAX; ++p)
 #pragma unroll
-        for (int r = 0; r < NR; ++r) {
-            int s = 0;
-            s = sdot4((int)q0[r].x, a0.x, s);
-            s = sdot4((int)q0[r].y, a0.y, s);
-            s = sdot4((int)q0[r].z, a0.z, s);
-            s = sdot4((int)q0[r].w, a0.w, s);
-            s = sdot4((int)q1[r].x, a1.x, s);
-            s = sdot4((int)q1[r].y, a1.y, s);
-            s = sdot4((int)q1[r].z, a1.z, s);
-            s = sdot4((int)q1[r].w, a1.w, s);
-            if (ok) acc[r] += (float)s * (h2f(db[r]) * da);
+        for (int r = 0; r < NR; ++r)
+            if (p < np) acc[r] += compute_frag(W, pre[r][p], p, a);
+    if (np > PMAX) {
+        Frag cur[NR], nxt[NR];
+#pragma unroll
+        for (int r = 0; r < NR; ++r) cur[r] = load_frag(W, rows[r], PMAX);
+        for (int p = PMAX; p < np; ++p) {
+#pragma unroll
+            for (int r = 0; r < NR; ++r)
+                if (p + 1 < np) nxt[r] = load_frag(W, rows[r], p + 1);
+#pragma unroll
+            for (int r = 0; r < NR; ++r) acc[r] += compute_frag(W, cur[r], p, a);
+#pragma unroll
+            for (int r = 0; r < NR; ++r) cur[r] = nxt[r];
         }
     }
 #pragma unroll
     for (int r = 0; r < NR; ++r) out[r] = wave_sum(acc[r]);
 }
 
-template <int NR>
-__device__ inline void rows_dot(const QMat &W, const int (&rows)[NR], const ActL &a, float (&out)[NR]) {
-    if (W.type == 12)
-        dot_q4k<NR>(W, rows, a, out);
-    else if (W.type == 14)
-        dot_q6k<NR>(W, rows, a, out);
-    else
-        dot_q80<NR>(W, rows, a, out);
+// Registers for the prologue input vector: x loaded as float4 before the weight loads.
+template <int XV>
+struct XRegs {
+    float4 v[XV];
+};
+
+template <int XV>
+__device__ inline void load_x(const float *x, int K, XRegs<XV> &xr) {
+#pragma unroll
+    for (int i = 0; i < XV; ++i) {
+        const int e = (threadIdx.x + i * NT) * 4;
+        xr.v[i] = e < K ? *reinterpret_cast<const float4 *>(x + e) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+}
+
+// RMSNorm (ggml_rms_norm * weight) of the register copy into s.xs, then quantize.
+template <int XV>
+__device__ void rmsnorm_quant(const XRegs<XV> &xr, const float *w, int K, float eps, bool kquant, const Smem &s) {
+    double acc = 0.0;
+#pragma unroll
+    for (int i = 0; i < XV; ++i) {
+        const int e = (threadIdx.x + i * NT) * 4;
+        if (e < K) {
+            const float4 v = xr.v[i];
+            acc += (double)(v.x * v.x);
+            acc += (double)(v.y * v.y);
+            acc += (double)(v.z * v.z);
+            acc += (double)(v.w * v.w);
+        }
+    }
+    const double tot = block_sum(acc, s.red);
+    const float mean = (float)(tot / K);
+    const float scale = 1.0f / sqrtf(mean + eps);
+#pragma unroll
+    for (int i = 0; i < XV; ++i) {
+        const int e = (threadIdx.x + i * NT) * 4;
+        if (e < K) {
+            const float4 v = xr.v[i];
+            const float4 ww = *reinterpret_cast<const float4 *>(w + e);
+            float t;
+            t = v.x * scale, s.xs[e + 0] = t * ww.x;
+            t = v.y * scale, s.xs[e + 1] = t * ww.y;
+            t = v.z * scale, s.xs[e + 2] = t * ww.z;
+            t = v.w * scale, s.xs[e + 3] = t * ww.w;
+        }
+    }
+    __syncthreads();
+    quantize(s.xs, K, kquant, s.a);
+}
+
+template <int XV>
+__device__ inline void plain_quant(const XRegs<XV> &xr, int K, bool kquant, const Smem &s) {
+#pragma unroll
+    for (int i = 0; i < XV; ++i) {
+        const int e = (threadIdx.x + i * NT) * 4;
+        if (e < K) *reinterpret_cast<float4 *>(s.xs + e) = xr.v[i];
+    }
+    __syncthreads();
+    quantize(s.xs, K, kquant, s.a);
+}
+
+// Quantized activation blob in global memory (same carve layout) -> LDS.
+__device__ inline void act_from_global(const float *blob, int K, const Smem &s) {
+    const Smem gs = carve((char *)blob, K);
+    for (int i = threadIdx.x; i < K / 4; i += NT) ((int *)s.a.qs)[i] = ((const int *)gs.a.qs)[i];
+    for (int i = threadIdx.x; i < K / 32; i += NT) s.a.d[i] = gs.a.d[i];
+    for (int i = threadIdx.x; i < K / 16; i += NT) s.a.bs[i] = gs.a.bs[i];
+    __syncthreads();
 }
 
 // ------------------------------------------------------------------ kernels
-constexpr int QKV_ROWS = 16;   // rows per workgroup (4 waves x 2 x NR=2)
+constexpr int QKV_ROWS = 16;   // rows per workgroup (4 waves x NR=4)
 constexpr int RES_ROWS = 8;    // O / down: 4 waves x NR=2
 constexpr int FFN_PAIRS = 8;   // gate/up pairs per workgroup: 4 waves x NR=2
-constexpr int LM_ROWS = 64;    // lm_head: 4 waves x 4 x NR=4
+constexpr int LM_ROWS = 64;    // lm_head: 4 waves x 4 groups x NR=4
 
+template <int P, int XV>
 __global__ __launch_bounds__(NT) void k_attn_in(LlmDims d, const float *norm_w, QMat wq, QMat wk, QMat wv,
                                                 LlmBuffers b) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int K = d.n_embd;
     const Smem s = carve(smem, K);
-    rmsnorm_to(b.x, norm_w, K, d.eps, s);
-    quantize(s.xs, K, wq.type != 8, s.a);
+    XRegs<XV> xr;
+    load_x(b.x, K, xr);
     int row0 = blockIdx.x * QKV_ROWS;
     const int seg = row0 >= wq.rows + wk.rows ? 2 : (row0 >= wq.rows ? 1 : 0);
     const QMat W = seg == 2 ? wv : (seg == 1 ? wk : wq);
@@ -403,19 +464,18 @@ __global__ __launch_bounds__(NT) void k_attn_in(LlmDims d, const float *norm_w, 
     row0 -= off;
     float *out = b.qkv + off;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    int rows[4];
 #pragma unroll
-    for (int g = 0; g < 2; ++g) {
-        int rows[2];
-        const int r0 = row0 + wave * 4 + g * 2;
-        rows[0] = r0 < W.rows ? r0 : -1;
-        rows[1] = r0 + 1 < W.rows ? r0 + 1 : -1;
-        float o[2];
-        rows_dot<2>(W, rows, s.a, o);
-        if (lane == 0) {
-            if (rows[0] >= 0) out[rows[0]] = o[0];
-            if (rows[1] >= 0) out[rows[1]] = o[1];
-        }
-    }
+    for (int r = 0; r < 4; ++r) rows[r] = row0 + wave * 4 + r < W.rows ? row0 + wave * 4 + r : -1;
+    Frag pre[4][P];
+    preload<4, P>(W, rows, pre);
+    rmsnorm_quant(xr, norm_w, K, d.eps, wq.type != 8, s);
+    float o[4];
+    finish_rows<4, P>(W, rows, pre, s.a, o);
+    if (lane == 0)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            if (rows[r] >= 0) out[rows[r]] = o[r];
 }
 
 // Attention for one (kv head, split of d.split positions). HD = head dim.
@@ -595,36 +655,61 @@ void launch_attention(int G, dim3 grid, size_t lds, hipStream_t s, const LlmDims
     }
 }
 
+// Split combine of the attention partials + re-quantization of the attention output
+// (one workgroup per 256 outputs = one Q8_K block / eight Q8_0 blocks) -> global blob.
+__global__ __launch_bounds__(NT) void k_attn_combine(LlmDims d, int kquant, LlmBuffers b) {
+    __shared__ float xs[NT];
+    __shared__ __attribute__((aligned(16))) int8_t qs[NT];
+    __shared__ float dd[8];
+    __shared__ int16_t bs[16];
+    const int K = d.n_head * d.hd;
+    const int pos = b.st->pos;
+    const int nsp = pos / d.split + 1;
+    const int rec = d.hd + 2;
+    const int e = blockIdx.x * NT + threadIdx.x;
+    const int ec = e < K ? e : K - 1;
+    const int h = ec / d.hd, dd_ = ec - h * d.hd;
+    const float *base = b.part + (size_t)h * d.max_splits * rec;
+    float M = -INFINITY;
+    for (int sp = 0; sp < nsp; ++sp) M = fmaxf(M, base[(size_t)sp * rec + d.hd]);
+    float L = 0.0f, O = 0.0f;
+    for (int sp = 0; sp < nsp; ++sp) {
+        const float *r = base + (size_t)sp * rec;
+        const float w = expf(r[d.hd] - M);
+        L += w * r[d.hd + 1];
+        O += w * r[dd_];
+    }
+    if (e >= K) O = 0.0f, L = 1.0f;
+    xs[threadIdx.x] = O / L;
+    __syncthreads();
+    ActL a{qs, dd, bs};
+    quantize(xs, NT, kquant != 0, a);
+    const Smem gs = carve((char *)b.act2, K);
+    if (threadIdx.x < NT / 4 && blockIdx.x * NT + 4 * threadIdx.x < K)
+        ((int *)gs.a.qs)[blockIdx.x * (NT / 4) + threadIdx.x] = ((const int *)qs)[threadIdx.x];
+    if (kquant) {
+        if (threadIdx.x == 0) gs.a.d[blockIdx.x] = dd[0];
+        if (threadIdx.x < 16) gs.a.bs[blockIdx.x * 16 + threadIdx.x] = bs[threadIdx.x];
+    } else if (threadIdx.x < 8 && blockIdx.x * NT + 32 * threadIdx.x < K) {
+        gs.a.d[blockIdx.x * 8 + threadIdx.x] = dd[threadIdx.x];
+    }
+}
+
+template <int P, int XV>
 __global__ __launch_bounds__(NT) void k_attn_out(LlmDims d, QMat wo, LlmBuffers b) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int K = d.n_head * d.hd;
     const Smem s = carve(smem, K);
-    const int pos = b.st->pos;
-    const int nsp = pos / d.split + 1;
-    const int rec = d.hd + 2;
-    for (int e = threadIdx.x; e < K; e += NT) {
-        const int h = e / d.hd, dd = e - h * d.hd;
-        const float *base = b.part + (size_t)h * d.max_splits * rec;
-        float M = -INFINITY;
-        for (int sp = 0; sp < nsp; ++sp) M = fmaxf(M, base[(size_t)sp * rec + d.hd]);
-        float L = 0.0f, O = 0.0f;
-        for (int sp = 0; sp < nsp; ++sp) {
-            const float *r = base + (size_t)sp * rec;
-            const float w = expf(r[d.hd] - M);
-            L += w * r[d.hd + 1];
-            O += w * r[dd];
-        }
-        s.xs[e] = O / L;
-    }
-    __syncthreads();
-    quantize(s.xs, K, wo.type != 8, s.a);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     int rows[2];
     const int r0 = blockIdx.x * RES_ROWS + wave * 2;
     rows[0] = r0 < wo.rows ? r0 : -1;
     rows[1] = r0 + 1 < wo.rows ? r0 + 1 : -1;
+    Frag pre[2][P];
+    preload<2, P>(wo, rows, pre);
+    act_from_global(b.act2, K, s);
     float o[2];
-    rows_dot<2>(wo, rows, s.a, o);
+    finish_rows<2, P>(wo, rows, pre, s.a, o);
     if (lane == 0) {
         if (rows[0] >= 0) b.x[rows[0]] = o[0] + b.x[rows[0]];
         if (rows[1] >= 0) b.x[rows[1]] = o[1] + b.x[rows[1]];
@@ -633,40 +718,48 @@ __global__ __launch_bounds__(NT) void k_attn_out(LlmDims d, QMat wo, LlmBuffers 
 
 __device__ inline float silu_f(float x) { return x / (1.0f + expf(-x)); }
 
+template <int P, int XV>
 __global__ __launch_bounds__(NT) void k_ffn_in(LlmDims d, const float *norm_w, QMat gate, QMat up, LlmBuffers b) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int K = d.n_embd;
     const Smem s = carve(smem, K);
-    rmsnorm_to(b.x, norm_w, K, d.eps, s);
-    quantize(s.xs, K, gate.type != 8, s.a);
+    XRegs<XV> xr;
+    load_x(b.x, K, xr);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     int rows[2];
     const int r0 = blockIdx.x * FFN_PAIRS + wave * 2;
     rows[0] = r0 < gate.rows ? r0 : -1;
     rows[1] = r0 + 1 < gate.rows ? r0 + 1 : -1;
+    Frag pg[2][P], pu[2][P];
+    preload<2, P>(gate, rows, pg);
+    preload<2, P>(up, rows, pu);
+    rmsnorm_quant(xr, norm_w, K, d.eps, gate.type != 8, s);
     float g[2], u[2];
-    rows_dot<2>(gate, rows, s.a, g);
-    rows_dot<2>(up, rows, s.a, u);
+    finish_rows<2, P>(gate, rows, pg, s.a, g);
+    finish_rows<2, P>(up, rows, pu, s.a, u);
     if (lane == 0) {
         if (rows[0] >= 0) b.h[rows[0]] = silu_f(g[0]) * u[0];
         if (rows[1] >= 0) b.h[rows[1]] = silu_f(g[1]) * u[1];
     }
 }
 
+template <int P, int XV>
 __global__ __launch_bounds__(NT) void k_ffn_down(LlmDims d, QMat down, LlmBuffers b) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int K = d.n_ff;
     const Smem s = carve(smem, K);
-    for (int i = threadIdx.x; i < K; i += NT) s.xs[i] = b.h[i];
-    __syncthreads();
-    quantize(s.xs, K, down.type != 8, s.a);
+    XRegs<XV> xr;
+    load_x(b.h, K, xr);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     int rows[2];
     const int r0 = blockIdx.x * RES_ROWS + wave * 2;
     rows[0] = r0 < down.rows ? r0 : -1;
     rows[1] = r0 + 1 < down.rows ? r0 + 1 : -1;
+    Frag pre[2][P];
+    preload<2, P>(down, rows, pre);
+    plain_quant(xr, K, down.type != 8, s);
     float o[2];
-    rows_dot<2>(down, rows, s.a, o);
+    finish_rows<2, P>(down, rows, pre, s.a, o);
     if (lane == 0) {
         if (rows[0] >= 0) b.x[rows[0]] = o[0] + b.x[rows[0]];
         if (rows[1] >= 0) b.x[rows[1]] = o[1] + b.x[rows[1]];
@@ -674,12 +767,14 @@ __global__ __launch_bounds__(NT) void k_ffn_down(LlmDims d, QMat down, LlmBuffer
 }
 
 // final RMSNorm + re-quantization once per step -> global (read by every lm_head block)
+template <int P, int XV>
 __global__ __launch_bounds__(NT) void k_final_norm(LlmDims d, const float *norm_w, int kquant, LlmBuffers b) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int K = d.n_embd;
     const Smem s = carve(smem, K);
-    rmsnorm_to(b.x, norm_w, K, d.eps, s);
-    quantize(s.xs, K, kquant != 0, s.a);
+    XRegs<XV> xr;
+    load_x(b.x, K, xr);
+    rmsnorm_quant(xr, norm_w, K, d.eps, kquant != 0, s);
     const Smem gs = carve((char *)b.act, K);
     for (int i = threadIdx.x; i < K / 4; i += NT) ((int *)gs.a.qs)[i] = ((const int *)s.a.qs)[i];
     for (int i = threadIdx.x; i < K / 32; i += NT) gs.a.d[i] = s.a.d[i];
@@ -700,38 +795,49 @@ __device__ inline float gumbel(uint64_t seed, int step, int idx) {
     return -logf(-logf(u));
 }
 
+template <int P>
 __global__ __launch_bounds__(NT) void k_lm_head(LlmDims d, QMat lm, SampleCfg sc, LlmBuffers b) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __shared__ float bs_[NWAVE];
     __shared__ int bi_[NWAVE];
     const int K = d.n_embd;
     const Smem s = carve(smem, K);
-    const Smem gs = carve((char *)b.act, K);
-    for (int i = threadIdx.x; i < K / 4; i += NT) ((int *)s.a.qs)[i] = ((const int *)gs.a.qs)[i];
-    for (int i = threadIdx.x; i < K / 32; i += NT) s.a.d[i] = gs.a.d[i];
-    for (int i = threadIdx.x; i < K / 16; i += NT) s.a.bs[i] = gs.a.bs[i];
-    __syncthreads();
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    constexpr int NG = LM_ROWS / (NWAVE * 4);
+    const int rbase = blockIdx.x * LM_ROWS + wave * (LM_ROWS / NWAVE);
+    int rows[NG][4];
+#pragma unroll
+    for (int g = 0; g < NG; ++g)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) rows[g][r] = rbase + g * 4 + r < lm.rows ? rbase + g * 4 + r : -1;
+    // lm_head rows are one pass at K <= 2048: load two groups ahead of the prologue
+    Frag f0[4][P], f1[4][P];
+    preload<4, P>(lm, rows[0], f0);
+    preload<4, P>(lm, rows[1], f1);
+    act_from_global(b.act, K, s);
     const int step = b.st->step;
     const uint64_t seed = ((uint64_t)sc.seed_hi << 32) | sc.seed_lo;
     float best = -INFINITY;
     int bi = INT_MAX;
 #pragma unroll
-    for (int g = 0; g < LM_ROWS / (NWAVE * 4); ++g) {
-        int rows[4];
-        const int r0 = blockIdx.x * LM_ROWS + wave * (LM_ROWS / NWAVE) + g * 4;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) rows[r] = r0 + r < lm.rows ? r0 + r : -1;
+    for (int g = 0; g < NG; ++g) {
         float o[4];
-        rows_dot<4>(lm, rows, s.a, o);
+        if (g % 2 == 0) {
+            finish_rows<4, P>(lm, rows[g], f0, s.a, o);
+            if (g + 2 < NG) preload<4, P>(lm, rows[g + 2], f0);
+        } else {
+            finish_rows<4, P>(lm, rows[g], f1, s.a, o);
+            if (g + 2 < NG) preload<4, P>(lm, rows[g + 2], f1);
+        }
         if (lane == 0) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                if (rows[r] < 0) continue;
-                b.logits[rows[r]] = o[r];
-                if (rows[r] >= sc.lo && rows[r] < sc.hi) {
-                    const float v = sc.temp > 0.0f ? o[r] / sc.temp + gumbel(seed, step, rows[r]) : o[r];
-                    if (v > best || (v == best && rows[r] < bi)) best = v, bi = rows[r];
+                const int row = rows[g][r];
+                if (row < 0) continue;
+                b.logits[row] = o[r];
+                if (row >= sc.lo && row < sc.hi) {
+                    const float v = sc.temp > 0.0f ? o[r] / sc.temp + gumbel(seed, step, row) : o[r];
+                    if (v > best || (v == best && row < bi)) best = v, bi = row;
                 }
             }
         }
@@ -824,8 +930,25 @@ void launch_embed_token(const LlmDims &d, const QMat &tok_embd, const LlmBuffers
     hipLaunchKernelGGL(k_embed, dim3(1), dim3(NT), 0, s, d, tok_embd, b);
 }
 
-// Launch one kernel of the step: which = 0 attn_in, 1 attention, 2 attn_out, 3 ffn_in,
-// 4 ffn_down (layer il), 5 final_norm, 6 lm_head, 7 sample.
+inline int pick_p(int K) { return (K + 2047) / 2048 <= 1 ? 1 : 3; }
+inline int pick_xv(int K) {
+    const int v = (K + 1023) / 1024;
+    return v <= 1 ? 1 : (v <= 2 ? 2 : (v <= 6 ? 6 : 12));
+}
+
+// Calls F.template operator()<P, XV>() with P = passes preloaded, XV = float4 x-registers.
+template <class F>
+void dispatch_px(int K, F &&f) {
+    const int p = pick_p(K), xv = pick_xv(K);
+#define PX(PP, XX) \
+    if (p == PP && xv == XX) return f.template operator()<PP, XX>();
+    PX(1, 1) PX(1, 2) PX(1, 6) PX(1, 12) PX(3, 1) PX(3, 2) PX(3, 6) PX(3, 12)
+#undef PX
+}
+
+// Launch one kernel of the step: which = 0 attn_in, 1 attention, 2 attn_out (with its
+// combine kernel in front), 3 ffn_in, 4 ffn_down (layer il), 5 final_norm, 6 lm_head,
+// 7 sample.
 void launch_step_kernel(int which, const LlmDims &d, const LayerW *layers, int il, _Float16 *kcache,
                         _Float16 *vcache, const float *out_norm, const QMat &lm, const QMat &tok_embd,
                         const LlmBuffers &b, const SampleCfg &sc, hipStream_t s) {
@@ -838,8 +961,10 @@ void launch_step_kernel(int which, const LlmDims &d, const LayerW *layers, int i
         case 0: {
             const LayerW &L = layers[il];
             const int qkv_rows = L.wq.rows + L.wk.rows + L.wv.rows;
-            hipLaunchKernelGGL(k_attn_in, dim3((qkv_rows + QKV_ROWS - 1) / QKV_ROWS), dim3(NT), smem_bytes(d.n_embd),
-                               s, d, L.attn_norm, L.wq, L.wk, L.wv, b);
+            dispatch_px(d.n_embd, [&]<int P, int XV>() {
+                hipLaunchKernelGGL((k_attn_in<P, XV>), dim3((qkv_rows + QKV_ROWS - 1) / QKV_ROWS), dim3(NT),
+                                   smem_bytes(d.n_embd), s, d, L.attn_norm, L.wq, L.wk, L.wv, b);
+            });
             break;
         }
         case 1: {
@@ -854,27 +979,42 @@ void launch_step_kernel(int which, const LlmDims &d, const LayerW *layers, int i
         }
         case 2: {
             const LayerW &L = layers[il];
-            hipLaunchKernelGGL(k_attn_out, dim3((L.wo.rows + RES_ROWS - 1) / RES_ROWS), dim3(NT),
-                               smem_bytes(d.n_head * d.hd), s, d, L.wo, b);
+            const int K = d.n_head * d.hd;
+            hipLaunchKernelGGL(k_attn_combine, dim3((K + NT - 1) / NT), dim3(NT), 0, s, d, L.wo.type != 8 ? 1 : 0, b);
+            dispatch_px(K, [&]<int P, int XV>() {
+                hipLaunchKernelGGL((k_attn_out<P, XV>), dim3((L.wo.rows + RES_ROWS - 1) / RES_ROWS), dim3(NT),
+                                   smem_bytes(K), s, d, L.wo, b);
+            });
             break;
         }
         case 3: {
             const LayerW &L = layers[il];
-            hipLaunchKernelGGL(k_ffn_in, dim3((L.gate.rows + FFN_PAIRS - 1) / FFN_PAIRS), dim3(NT),
-                               smem_bytes(d.n_embd), s, d, L.ffn_norm, L.gate, L.up, b);
+            dispatch_px(d.n_embd, [&]<int P, int XV>() {
+                hipLaunchKernelGGL((k_ffn_in<P, XV>), dim3((L.gate.rows + FFN_PAIRS - 1) / FFN_PAIRS), dim3(NT),
+                                   smem_bytes(d.n_embd), s, d, L.ffn_norm, L.gate, L.up, b);
+            });
             break;
         }
         case 4: {
             const LayerW &L = layers[il];
-            hipLaunchKernelGGL(k_ffn_down, dim3((L.down.rows + RES_ROWS - 1) / RES_ROWS), dim3(NT),
-                               smem_bytes(d.n_ff), s, d, L.down, b);
+            dispatch_px(d.n_ff, [&]<int P, int XV>() {
+                hipLaunchKernelGGL((k_ffn_down<P, XV>), dim3((L.down.rows + RES_ROWS - 1) / RES_ROWS), dim3(NT),
+                                   smem_bytes(d.n_ff), s, d, L.down, b);
+            });
             break;
         }
         case 5:
-            hipLaunchKernelGGL(k_final_norm, dim3(1), dim3(NT), smem_bytes(d.n_embd), s, d, out_norm,
-                               lm.type != 8 ? 1 : 0, b);
+            dispatch_px(d.n_embd, [&]<int P, int XV>() {
+                hipLaunchKernelGGL((k_final_norm<P, XV>), dim3(1), dim3(NT), smem_bytes(d.n_embd), s, d, out_norm,
+                                   lm.type != 8 ? 1 : 0, b);
+            });
             break;
-        case 6: hipLaunchKernelGGL(k_lm_head, dim3(nblk), dim3(NT), smem_bytes(d.n_embd), s, d, lm, sc, b); break;
+        case 6:
+            if (pick_p(d.n_embd) == 1)
+                hipLaunchKernelGGL(k_lm_head<1>, dim3(nblk), dim3(NT), smem_bytes(d.n_embd), s, d, lm, sc, b);
+            else
+                hipLaunchKernelGGL(k_lm_head<3>, dim3(nblk), dim3(NT), smem_bytes(d.n_embd), s, d, lm, sc, b);
+            break;
         case 7: hipLaunchKernelGGL(k_sample, dim3(1), dim3(NT), 0, s, d, sc, tok_embd, nblk, b); break;
         default: break;
     }
@@ -893,20 +1033,23 @@ void launch_decode_step(const LlmDims &d, const LayerW *layers, int n_layer, _Fl
 // ------------------------------------------------------------------ parity entry point
 namespace mio {
 namespace {
+template <int P, int XV>
 __global__ __launch_bounds__(NT) void k_debug_matvec(QMat W, const float *x, float *y) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int K = W.k;
     const Smem s = carve(smem, K);
-    for (int i = threadIdx.x; i < K; i += NT) s.xs[i] = x[i];
-    __syncthreads();
-    quantize(s.xs, K, W.type != 8, s.a);
+    XRegs<XV> xr;
+    load_x(x, K, xr);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     int rows[2];
     const int r0 = blockIdx.x * RES_ROWS + wave * 2;
     rows[0] = r0 < W.rows ? r0 : -1;
     rows[1] = r0 + 1 < W.rows ? r0 + 1 : -1;
+    Frag pre[2][P];
+    preload<2, P>(W, rows, pre);
+    plain_quant(xr, K, W.type != 8, s);
     float o[2];
-    rows_dot<2>(W, rows, s.a, o);
+    finish_rows<2, P>(W, rows, pre, s.a, o);
     if (lane == 0) {
         if (rows[0] >= 0) y[rows[0]] = o[0];
         if (rows[1] >= 0) y[rows[1]] = o[1];
@@ -915,6 +1058,9 @@ __global__ __launch_bounds__(NT) void k_debug_matvec(QMat W, const float *x, flo
 }  // namespace
 
 void launch_debug_matvec(const QMat &W, const float *x, float *y, hipStream_t s) {
-    hipLaunchKernelGGL(k_debug_matvec, dim3((W.rows + RES_ROWS - 1) / RES_ROWS), dim3(NT), smem_bytes(W.k), s, W, x, y);
+    dispatch_px(W.k, [&]<int P, int XV>() {
+        hipLaunchKernelGGL((k_debug_matvec<P, XV>), dim3((W.rows + RES_ROWS - 1) / RES_ROWS), dim3(NT), smem_bytes(W.k),
+                           s, W, x, y);
+    });
 }
 }  // namespace mio

@@ -7,6 +7,7 @@
 #include "llm.h"
 
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -169,8 +170,16 @@ int llm_begin(mio_hip_llm *m, const int32_t *prompt, int n_prompt, int max_new, 
 int llm_run(mio_hip_llm *m, int n_steps) {
     int rc = mio::bind(m->d);
     if (rc) return rc;
-    for (int i = 0; i < n_steps && m->steps_issued < m->steps_total; ++i, ++m->steps_issued)
-        MIO_HIP_CHECK(hipGraphLaunch(m->graph, m->d->stream));
+    // MIO_NO_GRAPH=1: eager launches (rocprofv3 kernel tracing of graph replays crashes on
+    // ROCm 7.2 here; kernels and arguments are identical either way)
+    static const bool eager = getenv("MIO_NO_GRAPH") && getenv("MIO_NO_GRAPH")[0] == '1';
+    for (int i = 0; i < n_steps && m->steps_issued < m->steps_total; ++i, ++m->steps_issued) {
+        if (eager)
+            mio::launch_decode_step(m->dims, m->layers.data(), m->n_layer, m->kc, m->vc, m->out_norm, m->lm, m->tok,
+                                    m->buf, m->cfg, m->d->stream);
+        else
+            MIO_HIP_CHECK(hipGraphLaunch(m->graph, m->d->stream));
+    }
     return MIO_OK;
 }
 
@@ -291,6 +300,7 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
     m->buf.h = dalloc<float>(m, D.n_ff);
     m->buf.logits = dalloc<float>(m, D.n_vocab);
     m->buf.act = dalloc<float>(m, D.n_embd * 2 + 1024);
+    m->buf.act2 = dalloc<float>(m, D.n_head * D.hd * 2 + 1024);
     m->buf.smp = dalloc<float>(m, 2 * mio::lm_head_blocks(D) + 16);
     m->buf.st = dalloc<mio::StepState>(m, 1);
     m->max_steps = n_ctx;
