@@ -130,6 +130,10 @@ int mio_hip_llm_generate(mio_hip_llm *m, const int32_t *prompt, int n_prompt, in
  * the runner's stream between HIP events (state/buffers of the last generate/eval).
  * *avg_ms = mean duration; *bytes = algorithmic HBM bytes per launch. */
 int mio_hip_llm_time_kernel(mio_hip_llm *m, int which, int iters, float *avg_ms, uint64_t *bytes);
+/* Diagnostic: one launch of kernel `which` with in-kernel checkpoint tracing; out[0..15]
+ * = s_memtime (shader clock) at checkpoints of workgroup 0 / thread 0 (0 = not reached),
+ * out[16] / out[31] = s_memrealtime (100 MHz) at the first / last checkpoint. */
+int mio_hip_llm_trace_kernel(mio_hip_llm *m, int which, uint64_t *out);
 /* Stage times (ms, HIP events) of the last mio_hip_codec_decode_pcm: [0] codec, [1] iSTFT. */
 int mio_hip_codec_last_timings(const mio_hip_codec *c, float *ms2);
 

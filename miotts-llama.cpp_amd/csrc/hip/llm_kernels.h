@@ -7,6 +7,9 @@
 
 namespace mio {
 
+// attention positions per chunk (k_attention workgroup), = LlmDims::split
+constexpr int kAttChunk = 128;
+
 // One quantized matrix in the split layout (csrc/host/quant.h), rows x k.
 struct QMat {
     int type;  // ggml type id: 8 Q8_0, 12 Q4_K, 14 Q6_K
@@ -43,21 +46,21 @@ struct LlmDims {
     int n_embd, n_head, n_kv, hd, n_ff, n_vocab, n_ctx;
     float eps, scale;
     int neox, qk_norm;
-    int split;        // attention positions per split
+    int split;        // attention positions per chunk (ATT_CHUNK = 64)
     int max_splits;
+    int n_wg;         // streaming-matvec workgroups (one per CU)
 };
 
 struct LlmBuffers {
     float *x;          // [n_embd] residual stream
     float *qkv;        // [(H + 2 Hkv) hd]
-    float *part;       // [H][max_splits][hd + 2] attention partials
     float *h;          // [n_ff] ffn activation
     float *logits;     // [n_vocab]
-    float *act;        // quantized final-norm activation (global)
-    float *act2;       // quantized attention output (global, written by k_attn_combine)
+    float *part;       // [H][max_splits][hd + 4] attention chunk partials {O, m, l}
     float *smp;        // sampler partials [2 * n_lm_blocks]
     const float2 *rope;  // [n_ctx][hd/2] (cos, sin)
     StepState *st;
+    unsigned long long *trace;  // optional: per-kernel checkpoint timestamps (workgroup 0, thread 0)
 };
 
 // Launch one decode step (all layers + head + sampler) on stream s.
@@ -70,7 +73,11 @@ void launch_step_kernel(int which, const LlmDims &d, const LayerW *layers, int i
 // Embedding of `token` (row of token_embd) -> b.x, and state reset to (pos, token).
 void launch_embed_token(const LlmDims &d, const QMat &tok_embd, const LlmBuffers &b, hipStream_t s);
 int lm_head_blocks(const LlmDims &d);
+// workgroups of a streaming matvec over `rows` rows; passes of 2048 weights for K
+int matvec_grid(const LlmDims &d, int rows);
+int pick_np(int K);
+size_t matvec_lds(int K);
 // y = W x with x re-quantized to the vec_dot_type (parity test of the matvec kernels).
-void launch_debug_matvec(const QMat &W, const float *x, float *y, hipStream_t s);
+void launch_debug_matvec(const QMat &W, const float *x, float *y, int n_wg, hipStream_t s);
 
 }  // namespace mio

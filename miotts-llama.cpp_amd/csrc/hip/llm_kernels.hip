@@ -1,17 +1,26 @@
 // Single-token LLM decode step for gfx950 (replaces llama_decode for one token,
 // test-to-speech.cpp:178-185 / :589-596, and the sampler chain :127-130, :165-166).
 //
-// Per layer, five launches, every one of them streaming its weights exactly once:
+// Per layer, four weight-streaming launches plus attention:
 //   k_attn_in   RMSNorm(x) -> act re-quantized in LDS (Q8_K / Q8_0, ggml vec_dot_type)
-//               -> fused q|k|v dequant-matvec
-//   k_attention per (kv head, 64-position split): q/k RMSNorm (qwen3) + RoPE, F16 KV-cache
-//               append by the split that owns `pos`, online-softmax partials
-//   k_attn_out  split combine -> re-quantize -> O matvec -> x += .
+//               -> q|k|v dequant-matvec
+//   k_attention per (128-position chunk, kv head): q/k RMSNorm (qwen3) + RoPE, F16 KV-cache
+//               append by the chunk that owns `pos`, online-softmax partial records
+//   k_attn_out  chunk merge + re-quantization in the prologue -> O matvec -> x += .
 //   k_ffn_in    RMSNorm(x) -> re-quantize -> gate & up matvec -> silu(g)*u
 //   k_ffn_down  re-quantize h -> down matvec -> x += .
-// then k_final_norm, k_lm_head (logits + per-block Gumbel-max), k_sample (token,
+// then k_lm_head (final RMSNorm + logits + per-workgroup Gumbel-max) and k_sample (token,
 // next embedding, position++). All state is device-resident (StepState), so one hipGraph
 // of a step replays every token with no host round trip.
+//
+// Matvec engine ("streaming rows"): one 512-thread workgroup per CU, each wave streams a
+// contiguous run of rows. A row is NP "passes" of 2048 weights; one pass of one row is a
+// unit = one 16-B-per-lane load (+ block headers). Units are loaded U at a time into
+// registers, one group ahead of the group being reduced, and the first group is issued
+// before the activation prologue so HBM latency overlaps the RMSNorm/quantization, which
+// runs once per CU. The other global loads a workgroup needs up front (x, norm weights,
+// residual values) are issued before the first weight load, so in-order vmcnt waits
+// never stall on the prefetched group.
 //
 // Matvec arithmetic = ggml's integer block dots: per superblock the integer sums
 // (v_dot4c_i32_i8 on the raw 4/6/8-bit codes x int8 activations) are bit-exact with
@@ -22,14 +31,30 @@
 
 #include <cfloat>
 #include <climits>
+#include <type_traits>
 
 #pragma clang fp contract(off)
 
 namespace mio {
 namespace {
 
-constexpr int NT = 256;
+// Checkpoint timestamps (s_memtime) of workgroup 0 / thread 0, only when b.trace is set
+// (mio_hip_llm_trace_kernel); a uniform branch otherwise.
+#define MIO_TRACE(bufs, k)                                                                    \
+    do {                                                                                      \
+        if ((bufs).trace && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {        \
+            asm volatile("" ::: "memory");                                                    \
+            (bufs).trace[k] = __builtin_readcyclecounter();                                   \
+            if ((k) == 0 || (k) == 15) (bufs).trace[16 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+        }                                                                                     \
+    } while (0)
+
+constexpr int NT = 256;        // threads of the attention / sampler kernels
 constexpr int NWAVE = NT / 64;
+constexpr int MT = 512;        // threads of a streaming matvec workgroup
+constexpr int MW = MT / 64;
+constexpr int ATT_CHUNK = kAttChunk;
+__host__ __device__ constexpr int part_rec(int hd) { return hd + 4; }  // partial record {O[hd], m, l, pad}
 
 __device__ __forceinline__ float h2f(uint32_t bits16) {
     const uint16_t b = (uint16_t)bits16;
@@ -38,6 +63,76 @@ __device__ __forceinline__ float h2f(uint32_t bits16) {
 __device__ __forceinline__ float f16r(float f) { return (float)(_Float16)f; }
 __device__ __forceinline__ int sdot4(int a, int b, int c) { return __builtin_amdgcn_sdot4(a, b, c, false); }
 __device__ __forceinline__ uint4 ld16(const uint8_t *p) { return *reinterpret_cast<const uint4 *>(p); }
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// ------------------------------------------------------------------ cross-lane (DPP)
+// Cross-lane sums by DPP (gfx9 row_shr / row_bcast), never through LDS.
+template <int CTRL, int RM = 0xF>
+__device__ __forceinline__ int dpp_i(int v) {
+    return __builtin_amdgcn_update_dpp(0, v, CTRL, RM, 0xF, false);
+}
+template <int CTRL, int RM = 0xF>
+__device__ __forceinline__ float dpp_f(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, RM, 0xF, false));
+}
+constexpr int ROW_SHR1 = 0x111, ROW_SHR2 = 0x112, ROW_SHR4 = 0x114, ROW_SHR8 = 0x118;
+constexpr int ROW_BCAST15 = 0x142, ROW_BCAST31 = 0x143;
+
+// wave-wide reductions to lane 63 (row_shr prefix within rows, then row_bcast), returned
+// wave-uniform. `id` is the identity of the operation (what out-of-row lanes contribute).
+__device__ __forceinline__ float wave_max_f(float v, float id) {
+    v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(id), __float_as_int(v), ROW_SHR1, 0xF, 0xF, false)));
+    v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(id), __float_as_int(v), ROW_SHR2, 0xF, 0xF, false)));
+    v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(id), __float_as_int(v), ROW_SHR4, 0xF, 0xF, false)));
+    v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(id), __float_as_int(v), ROW_SHR8, 0xF, 0xF, false)));
+    v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(id), __float_as_int(v), ROW_BCAST15, 0xA, 0xF, false)));
+    v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(id), __float_as_int(v), ROW_BCAST31, 0xC, 0xF, false)));
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+__device__ __forceinline__ int wave_min_i(int v) {
+    const int id = INT_MAX;
+    v = min(v, __builtin_amdgcn_update_dpp(id, v, ROW_SHR1, 0xF, 0xF, false));
+    v = min(v, __builtin_amdgcn_update_dpp(id, v, ROW_SHR2, 0xF, 0xF, false));
+    v = min(v, __builtin_amdgcn_update_dpp(id, v, ROW_SHR4, 0xF, 0xF, false));
+    v = min(v, __builtin_amdgcn_update_dpp(id, v, ROW_SHR8, 0xF, 0xF, false));
+    v = min(v, __builtin_amdgcn_update_dpp(id, v, ROW_BCAST15, 0xA, 0xF, false));
+    v = min(v, __builtin_amdgcn_update_dpp(id, v, ROW_BCAST31, 0xC, 0xF, false));
+    return __builtin_amdgcn_readlane(v, 63);
+}
+template <int CTRL, int RM = 0xF>
+__device__ __forceinline__ double dpp_d(double v) {
+    const int2 p = __builtin_bit_cast(int2, v);
+    int2 r;
+    r.x = __builtin_amdgcn_update_dpp(0, p.x, CTRL, RM, 0xF, false);
+    r.y = __builtin_amdgcn_update_dpp(0, p.y, CTRL, RM, 0xF, false);
+    return __builtin_bit_cast(double, r);
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+    v += dpp_d<ROW_SHR1>(v);
+    v += dpp_d<ROW_SHR2>(v);
+    v += dpp_d<ROW_SHR4>(v);
+    v += dpp_d<ROW_SHR8>(v);
+    v += dpp_d<ROW_BCAST15, 0xA>(v);
+    v += dpp_d<ROW_BCAST31, 0xC>(v);
+    const int2 p = __builtin_bit_cast(int2, v);
+    int2 r;
+    r.x = __builtin_amdgcn_readlane(p.x, 63);
+    r.y = __builtin_amdgcn_readlane(p.y, 63);
+    return __builtin_bit_cast(double, r);
+}
+// all-reduce (max) within aligned 8-lane groups; every lane gets the result
+__device__ __forceinline__ float group8_max(float v) {
+    v = fmaxf(v, dpp_f<0xB1>(v));   // quad_perm [1,0,3,2]
+    v = fmaxf(v, dpp_f<0x4E>(v));   // quad_perm [2,3,0,1]
+    v = fmaxf(v, dpp_f<0x141>(v));  // row_half_mirror
+    return v;
+}
+// all-reduce (sum) within aligned 4-lane groups
+__device__ __forceinline__ int quad_sum_i(int v) {
+    v += dpp_i<0xB1>(v);
+    v += dpp_i<0x4E>(v);
+    return v;
+}
 
 // ------------------------------------------------------------------ activation in LDS
 struct ActL {
@@ -49,11 +144,12 @@ struct ActL {
 struct Smem {
     float *xs;   // [K] float staging
     ActL a;
-    double *red; // [NWAVE]
+    double *red; // [16]
 };
 
+// LDS layout: xs f32[K] | qs i8[K] | d f32[K/32+8] | bs i16[K/16+8] | red
 __host__ __device__ inline size_t smem_bytes(int K) {
-    return (size_t)K * 4 + (size_t)K + (size_t)(K / 32 + 8) * 4 + (size_t)(K / 16 + 8) * 2 + 64;
+    return (size_t)K * 4 + (size_t)K + (size_t)(K / 32 + 8) * 4 + (size_t)(K / 16 + 8) * 2 + 128;
 }
 
 __device__ inline Smem carve(char *base, int K) {
@@ -62,62 +158,37 @@ __device__ inline Smem carve(char *base, int K) {
     s.a.qs = (int8_t *)(base + (size_t)K * 4);
     s.a.d = (float *)(base + (size_t)K * 5);
     s.a.bs = (int16_t *)(base + (size_t)K * 5 + (size_t)(K / 32 + 8) * 4);
-    s.red = (double *)(base + smem_bytes(K) - 64);
+    s.red = (double *)(base + smem_bytes(K) - 128);
     return s;
 }
 
 __device__ double block_sum(double v, double *red) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+    v = wave_sum_d(v);
+    const int nw = blockDim.x >> 6;
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
     __syncthreads();
     double t = 0.0;
-#pragma unroll
-    for (int w = 0; w < NWAVE; ++w) t += red[w];
+    for (int w = 0; w < nw; ++w) t += red[w];
     __syncthreads();
     return t;
 }
 
-// ggml_rms_norm + mul(weight): xs = (x * 1/sqrtf(mean(x^2) + eps)) * w
-__device__ void rmsnorm_to(const float *x, const float *w, int K, float eps, const Smem &s) {
-    double acc = 0.0;
-    for (int i = threadIdx.x; i < K; i += NT) {
-        const float v = x[i];
-        s.xs[i] = v;
-        acc += (double)(v * v);
-    }
-    const double tot = block_sum(acc, s.red);
-    const float mean = (float)(tot / K);
-    const float scale = 1.0f / sqrtf(mean + eps);
-    for (int i = threadIdx.x; i < K; i += NT) {
-        const float v = s.xs[i] * scale;
-        s.xs[i] = v * w[i];
-    }
-    __syncthreads();
-}
-
-// quantize_row_q8_K_ref semantics (iscale = -127/max_signed, nearest-even, clamp 127, bsums)
+// quantize_row_q8_K_ref semantics (iscale = -127/max_signed with max_signed the first
+// element of largest |x|, nearest-even, clamp 127, bsums); reductions by DPP.
 __device__ void quant_q8k(const float *xs, int K, const ActL &a) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    for (int b = wave; b < K / 256; b += NWAVE) {
-        float v[4];
-        float am = -1.0f;
-        int ai = 0;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            v[i] = xs[b * 256 + 4 * lane + i];
-            const float t = fabsf(v[i]);
-            if (t > am) am = t, ai = 4 * lane + i;
-        }
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) {
-            const float om = __shfl_xor(am, o);
-            const int oi = __shfl_xor(ai, o);
-            if (om > am || (om == am && oi < ai)) am = om, ai = oi;
-        }
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    for (int b = wave; b < K / 256; b += nw) {
+        const float4 v4 = *reinterpret_cast<const float4 *>(xs + b * 256 + 4 * lane);
+        const float v[4] = {v4.x, v4.y, v4.z, v4.w};
+        const float am = wave_max_f(fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))), 0.0f);
         int q[4] = {0, 0, 0, 0};
         float dd = 0.0f;
         if (am > 0.0f) {
+            int first = INT_MAX;
+#pragma unroll
+            for (int i = 3; i >= 0; --i)
+                if (fabsf(v[i]) == am) first = 4 * lane + i;
+            const int ai = wave_min_i(first);
             const float mx = xs[b * 256 + ai];
             const float iscale = -127.f / mx;
 #pragma unroll
@@ -129,9 +200,7 @@ __device__ void quant_q8k(const float *xs, int K, const ActL &a) {
         }
         const int packed = (q[0] & 0xFF) | ((q[1] & 0xFF) << 8) | ((q[2] & 0xFF) << 16) | ((q[3] & 0xFF) << 24);
         *reinterpret_cast<int *>(a.qs + b * 256 + 4 * lane) = packed;
-        int sm = q[0] + q[1] + q[2] + q[3];
-        sm += __shfl_xor(sm, 1);
-        sm += __shfl_xor(sm, 2);
+        const int sm = quad_sum_i(q[0] + q[1] + q[2] + q[3]);
         if ((lane & 3) == 0) a.bs[b * 16 + (lane >> 2)] = (int16_t)sm;
         if (lane == 0) a.d[b] = dd;
     }
@@ -139,9 +208,9 @@ __device__ void quant_q8k(const float *xs, int K, const ActL &a) {
 
 // quantize_row_q8_0_ref semantics (d = amax/127 stored as f16, q = roundf(x * 1/d))
 __device__ void quant_q80(const float *xs, int K, const ActL &a) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
     const int nb = K / 32;
-    for (int b0 = wave * 8; b0 < nb; b0 += NWAVE * 8) {
+    for (int b0 = wave * 8; b0 < nb; b0 += nw * 8) {
         const int b = b0 + (lane >> 3);
         const bool ok = b < nb;
         float v[4];
@@ -151,9 +220,7 @@ __device__ void quant_q80(const float *xs, int K, const ActL &a) {
             v[i] = ok ? xs[b * 32 + 4 * (lane & 7) + i] : 0.0f;
             am = fmaxf(am, fabsf(v[i]));
         }
-        am = fmaxf(am, __shfl_xor(am, 1));
-        am = fmaxf(am, __shfl_xor(am, 2));
-        am = fmaxf(am, __shfl_xor(am, 4));
+        am = group8_max(am);
         const float dd = am / 127.0f;
         const float id = dd != 0.0f ? 1.0f / dd : 0.0f;
         int q[4];
@@ -175,226 +242,35 @@ __device__ inline void quantize(const float *xs, int K, bool kquant, const ActL 
     __syncthreads();
 }
 
-// ------------------------------------------------------------------ row dots (one wave)
-// A row's quant payload for one "pass" (8 superblocks = 2048 weights for K-quants, 64
-// blocks = 2048 weights for Q8_0) is one 16-B-per-lane load (+ headers); loads are issued
-// into Frags BEFORE the activation prologue so HBM latency overlaps the RMSNorm/quantize.
-__device__ inline int sbyte(const uint4 &h, int i) {
-    const uint32_t w = i < 4 ? h.y : (i < 8 ? h.z : h.w);
-    return (int)((w >> ((i & 3) * 8)) & 0xFF);
-}
-
-__device__ inline void scale_min_k4(int j, const uint4 &h, int &sc, int &m) {
-    if (j < 4) {
-        sc = sbyte(h, j) & 63;
-        m = sbyte(h, j + 4) & 63;
-    } else {
-        sc = (sbyte(h, j + 4) & 0xF) | ((sbyte(h, j - 4) >> 6) << 4);
-        m = (sbyte(h, j + 4) >> 4) | ((sbyte(h, j) >> 6) << 4);
-    }
-}
-
-__device__ inline float wave_sum(float v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
-    return v;
-}
-
-constexpr uint32_t M4 = 0x0F0F0F0Fu, M2 = 0x03030303u;
-
-struct Frag {
-    uint4 a, b;
-    int c, d;
-    uint32_t e;
-};
-
-__device__ inline int npass_of(const QMat &W) {
-    return W.type == 8 ? ((W.k >> 5) + 63) / 64 : ((W.k >> 8) + 7) / 8;
-}
-
-__device__ inline Frag load_frag(const QMat &W, int row, int pass) {
-    const int lane = threadIdx.x & 63;
-    Frag f;
-    f.a = f.b = make_uint4(0, 0, 0, 0);
-    f.c = f.d = 0;
-    f.e = 0;
-    if (row < 0) return f;
-    if (W.type == 12) {
-        const int nsb = W.k >> 8, sb = pass * 8 + (lane >> 3), pc = lane & 7;
-        if (sb < nsb) {
-            f.a = ld16(W.p0 + (size_t)row * (W.k / 2) + sb * 128 + pc * 16);
-            f.b = ld16(W.p1 + ((size_t)row * nsb + sb) * 16);
-        }
-    } else if (W.type == 14) {
-        const int nsb = W.k >> 8, sb = pass * 8 + (lane >> 3), pc = lane & 7;
-        if (sb < nsb) {
-            const int n = pc >> 2, qq = pc & 3, gl = qq >> 1, l0 = 16 * (qq & 1);
-            f.a = ld16(W.p0 + (size_t)row * (W.k / 2) + sb * 128 + pc * 16);
-            f.b = ld16(W.p1 + (size_t)row * (W.k / 4) + sb * 64 + 32 * n + l0);
-            const int8_t *sc = (const int8_t *)W.p2 + (size_t)row * (W.k / 16) + sb * 16 + 8 * n + 2 * gl + (l0 >> 4);
-            f.c = sc[0];
-            f.d = sc[4];
-            f.e = ((const uint16_t *)W.p3)[(size_t)row * nsb + sb];
-        }
-    } else {
-        const int nb = W.k >> 5, b = pass * 64 + lane;
-        if (b < nb) {
-            const uint8_t *p = W.p0 + (size_t)row * W.k + 32 * b;
-            f.a = ld16(p);
-            f.b = ld16(p + 16);
-            f.e = ((const uint16_t *)W.p1)[(size_t)row * nb + b];
-        }
-    }
-    return f;
-}
-
-// This lane's share of the row dot for one pass (summed over lanes by the caller).
-// Integer parts per superblock / block are exact (ggml vec_dot semantics).
-__device__ inline float compute_frag(const QMat &W, const Frag &f, int pass, const ActL &a) {
-    const int lane = threadIdx.x & 63;
-    if (W.type == 12) {
-        const int nsb = W.k >> 8, sb = pass * 8 + (lane >> 3), pc = lane & 7, jj = pc >> 1, hh = pc & 1;
-        const bool ok = sb < nsb;
-        const int sbc = ok ? sb : 0;
-        const int e_lo = sbc * 256 + 64 * jj + 16 * hh;
-        const int4 alo = *reinterpret_cast<const int4 *>(a.qs + e_lo);
-        const int4 ahi = *reinterpret_cast<const int4 *>(a.qs + e_lo + 32);
-        int dlo = 0, dhi = 0;
-        dlo = sdot4((int)(f.a.x & M4), alo.x, dlo);
-        dlo = sdot4((int)(f.a.y & M4), alo.y, dlo);
-        dlo = sdot4((int)(f.a.z & M4), alo.z, dlo);
-        dlo = sdot4((int)(f.a.w & M4), alo.w, dlo);
-        dhi = sdot4((int)((f.a.x >> 4) & M4), ahi.x, dhi);
-        dhi = sdot4((int)((f.a.y >> 4) & M4), ahi.y, dhi);
-        dhi = sdot4((int)((f.a.z >> 4) & M4), ahi.z, dhi);
-        dhi = sdot4((int)((f.a.w >> 4) & M4), ahi.w, dhi);
-        int sc0, m0, sc1, m1;
-        scale_min_k4(2 * jj, f.b, sc0, m0);
-        scale_min_k4(2 * jj + 1, f.b, sc1, m1);
-        int isum = sc0 * dlo + sc1 * dhi;
-        int imin = m0 * a.bs[e_lo >> 4] + m1 * a.bs[(e_lo + 32) >> 4];
-        isum += __shfl_xor(isum, 1);
-        isum += __shfl_xor(isum, 2);
-        isum += __shfl_xor(isum, 4);
-        imin += __shfl_xor(imin, 1);
-        imin += __shfl_xor(imin, 2);
-        imin += __shfl_xor(imin, 4);
-        if (!(ok && pc == 0)) return 0.0f;
-        const float da = a.d[sbc];
-        const float d = h2f(f.b.x & 0xFFFF) * da;
-        const float dmin = h2f(f.b.x >> 16) * da;
-        float v = d * (float)isum;
-        v = v - dmin * (float)imin;
-        return v;
-    } else if (W.type == 14) {
-        const int nsb = W.k >> 8, sb = pass * 8 + (lane >> 3), pc = lane & 7;
-        const int n = pc >> 2, qq = pc & 3, gl = qq >> 1, l0 = 16 * (qq & 1);
-        const bool ok = sb < nsb;
-        const int sbc = ok ? sb : 0;
-        const int e_lo = sbc * 256 + 128 * n + 32 * gl + l0;
-        const int4 alo = *reinterpret_cast<const int4 *>(a.qs + e_lo);
-        const int4 ahi = *reinterpret_cast<const int4 *>(a.qs + e_lo + 64);
-        const int shl = 2 * gl, shh = 2 * gl + 4;
-        auto lo = [&](uint32_t l, uint32_t h) { return (int)((l & M4) | (((h >> shl) & M2) << 4)); };
-        auto hi = [&](uint32_t l, uint32_t h) { return (int)(((l >> 4) & M4) | (((h >> shh) & M2) << 4)); };
-        int dlo = 0, dhi = 0;
-        dlo = sdot4(lo(f.a.x, f.b.x), alo.x, dlo);
-        dlo = sdot4(lo(f.a.y, f.b.y), alo.y, dlo);
-        dlo = sdot4(lo(f.a.z, f.b.z), alo.z, dlo);
-        dlo = sdot4(lo(f.a.w, f.b.w), alo.w, dlo);
-        dhi = sdot4(hi(f.a.x, f.b.x), ahi.x, dhi);
-        dhi = sdot4(hi(f.a.y, f.b.y), ahi.y, dhi);
-        dhi = sdot4(hi(f.a.z, f.b.z), ahi.z, dhi);
-        dhi = sdot4(hi(f.a.w, f.b.w), ahi.w, dhi);
-        int isum = f.c * (dlo - 32 * a.bs[e_lo >> 4]) + f.d * (dhi - 32 * a.bs[(e_lo + 64) >> 4]);
-        isum += __shfl_xor(isum, 1);
-        isum += __shfl_xor(isum, 2);
-        isum += __shfl_xor(isum, 4);
-        if (!(ok && pc == 0)) return 0.0f;
-        const float d = h2f(f.e) * a.d[sbc];
-        return d * (float)isum;
-    } else {
-        const int nb = W.k >> 5, b = pass * 64 + lane;
-        if (b >= nb) return 0.0f;
-        const int4 a0 = *reinterpret_cast<const int4 *>(a.qs + 32 * b);
-        const int4 a1 = *reinterpret_cast<const int4 *>(a.qs + 32 * b + 16);
-        int s = 0;
-        s = sdot4((int)f.a.x, a0.x, s);
-        s = sdot4((int)f.a.y, a0.y, s);
-        s = sdot4((int)f.a.z, a0.z, s);
-        s = sdot4((int)f.a.w, a0.w, s);
-        s = sdot4((int)f.b.x, a1.x, s);
-        s = sdot4((int)f.b.y, a1.y, s);
-        s = sdot4((int)f.b.z, a1.z, s);
-        s = sdot4((int)f.b.w, a1.w, s);
-        return (float)s * (h2f(f.e) * a.d[b]);
-    }
-}
-
-// NR rows of W, all passes. PRE = passes whose loads were issued before the prologue
-// (pre[r][p], p < PRE); remaining passes are loaded one pass ahead.
-template <int NR, int PMAX>
-__device__ inline void preload(const QMat &W, const int (&rows)[NR], Frag (&pre)[NR][PMAX]) {
-    const int np = npass_of(W);
-#pragma unroll
-    for (int p = 0; p < PMAX; ++p)
-#pragma unroll
-        for (int r = 0; r < NR; ++r)
-            if (p < np) pre[r][p] = load_frag(W, rows[r], p);
-}
-
-template <int NR, int PMAX>
-__device__ inline void finish_rows(const QMat &W, const int (&rows)[NR], const Frag (&pre)[NR][PMAX],
-                                   const ActL &a, float (&out)[NR]) {
-    const int np = npass_of(W);
-    float acc[NR];
-#pragma unroll
-    for (int r = 0; r < NR; ++r) acc[r] = 0.0f;
-#pragma unroll
-    for (int p = 0; p < PMAX; ++p)
-#pragma unroll
-        for (int r = 0; r < NR; ++r)
-            if (p < np) acc[r] += compute_frag(W, pre[r][p], p, a);
-    if (np > PMAX) {
-        Frag cur[NR], nxt[NR];
-#pragma unroll
-        for (int r = 0; r < NR; ++r) cur[r] = load_frag(W, rows[r], PMAX);
-        for (int p = PMAX; p < np; ++p) {
-#pragma unroll
-            for (int r = 0; r < NR; ++r)
-                if (p + 1 < np) nxt[r] = load_frag(W, rows[r], p + 1);
-#pragma unroll
-            for (int r = 0; r < NR; ++r) acc[r] += compute_frag(W, cur[r], p, a);
-#pragma unroll
-            for (int r = 0; r < NR; ++r) cur[r] = nxt[r];
-        }
-    }
-#pragma unroll
-    for (int r = 0; r < NR; ++r) out[r] = wave_sum(acc[r]);
-}
-
-// Registers for the prologue input vector: x loaded as float4 before the weight loads.
+// ------------------------------------------------------------------ prologue registers
+// x (and the norm weight) as float4 per thread, loaded before any weight load.
 template <int XV>
 struct XRegs {
     float4 v[XV];
+    float4 w[XV];
 };
 
 template <int XV>
-__device__ inline void load_x(const float *x, int K, XRegs<XV> &xr) {
+__device__ inline void load_x(const float *x, const float *w, int K, XRegs<XV> &xr) {
+    const auto rx = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(x), 0, K * 4, 0x00020000);
+    const auto rw = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(w), 0, w ? K * 4 : 0, 0x00020000);
 #pragma unroll
     for (int i = 0; i < XV; ++i) {
-        const int e = (threadIdx.x + i * NT) * 4;
-        xr.v[i] = e < K ? *reinterpret_cast<const float4 *>(x + e) : make_float4(0.f, 0.f, 0.f, 0.f);
+        const int e = (threadIdx.x + i * MT) * 4;
+        const u32x4 a = __builtin_amdgcn_raw_buffer_load_b128(rx, e * 4, 0, 0);
+        const u32x4 c = __builtin_amdgcn_raw_buffer_load_b128(rw, e * 4, 0, 0);
+        xr.v[i] = make_float4(__uint_as_float(a.x), __uint_as_float(a.y), __uint_as_float(a.z), __uint_as_float(a.w));
+        xr.w[i] = make_float4(__uint_as_float(c.x), __uint_as_float(c.y), __uint_as_float(c.z), __uint_as_float(c.w));
     }
 }
 
-// RMSNorm (ggml_rms_norm * weight) of the register copy into s.xs, then quantize.
+// ggml_rms_norm + mul(weight): xs = (x * 1/sqrtf(mean(x^2) + eps)) * w, then quantize.
 template <int XV>
-__device__ void rmsnorm_quant(const XRegs<XV> &xr, const float *w, int K, float eps, bool kquant, const Smem &s) {
+__device__ void rmsnorm_quant(const XRegs<XV> &xr, int K, float eps, bool kquant, const Smem &s) {
     double acc = 0.0;
 #pragma unroll
     for (int i = 0; i < XV; ++i) {
-        const int e = (threadIdx.x + i * NT) * 4;
+        const int e = (threadIdx.x + i * MT) * 4;
         if (e < K) {
             const float4 v = xr.v[i];
             acc += (double)(v.x * v.x);
@@ -408,10 +284,9 @@ __device__ void rmsnorm_quant(const XRegs<XV> &xr, const float *w, int K, float 
     const float scale = 1.0f / sqrtf(mean + eps);
 #pragma unroll
     for (int i = 0; i < XV; ++i) {
-        const int e = (threadIdx.x + i * NT) * 4;
+        const int e = (threadIdx.x + i * MT) * 4;
         if (e < K) {
-            const float4 v = xr.v[i];
-            const float4 ww = *reinterpret_cast<const float4 *>(w + e);
+            const float4 v = xr.v[i], ww = xr.w[i];
             float t;
             t = v.x * scale, s.xs[e + 0] = t * ww.x;
             t = v.y * scale, s.xs[e + 1] = t * ww.y;
@@ -427,358 +302,474 @@ template <int XV>
 __device__ inline void plain_quant(const XRegs<XV> &xr, int K, bool kquant, const Smem &s) {
 #pragma unroll
     for (int i = 0; i < XV; ++i) {
-        const int e = (threadIdx.x + i * NT) * 4;
+        const int e = (threadIdx.x + i * MT) * 4;
         if (e < K) *reinterpret_cast<float4 *>(s.xs + e) = xr.v[i];
     }
     __syncthreads();
     quantize(s.xs, K, kquant, s.a);
 }
 
-// Quantized activation blob in global memory (same carve layout) -> LDS.
-__device__ inline void act_from_global(const float *blob, int K, const Smem &s) {
-    const Smem gs = carve((char *)blob, K);
-    for (int i = threadIdx.x; i < K / 4; i += NT) ((int *)s.a.qs)[i] = ((const int *)gs.a.qs)[i];
-    for (int i = threadIdx.x; i < K / 32; i += NT) s.a.d[i] = gs.a.d[i];
-    for (int i = threadIdx.x; i < K / 16; i += NT) s.a.bs[i] = gs.a.bs[i];
-    __syncthreads();
+// ------------------------------------------------------------------ typed row dots
+// exact integer sum of each 8-lane group, valid in lanes 8k+7
+__device__ __forceinline__ int sum8_i(int v) {
+    v += dpp_i<ROW_SHR1>(v);
+    v += dpp_i<ROW_SHR2>(v);
+    v += dpp_i<ROW_SHR4>(v);
+    return v;
+}
+__device__ __forceinline__ float sum8_f(float v) {
+    v += dpp_f<ROW_SHR1>(v);
+    v += dpp_f<ROW_SHR2>(v);
+    v += dpp_f<ROW_SHR4>(v);
+    return v;
+}
+// sum of the values held in lanes 8k+7 (k = 0..7), returned wave-uniform
+__device__ __forceinline__ float sum_lanes7(float v) {
+    v += dpp_f<ROW_SHR8>(v);
+    v += dpp_f<ROW_BCAST15, 0xA>(v);
+    v += dpp_f<ROW_BCAST31, 0xC>(v);
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
 }
 
-// ------------------------------------------------------------------ kernels
-constexpr int QKV_ROWS = 16;   // rows per workgroup (4 waves x NR=4)
-constexpr int RES_ROWS = 8;    // O / down: 4 waves x NR=2
-constexpr int FFN_PAIRS = 8;   // gate/up pairs per workgroup: 4 waves x NR=2
-constexpr int LM_ROWS = 64;    // lm_head: 4 waves x 4 groups x NR=4
+__device__ inline float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
 
-template <int P, int XV>
-__global__ __launch_bounds__(NT) void k_attn_in(LlmDims d, const float *norm_w, QMat wq, QMat wk, QMat wv,
-                                                LlmBuffers b) {
+constexpr uint32_t M4 = 0x0F0F0F0Fu, M2 = 0x03030303u;
+
+// One unit's weight registers.
+//   Q4_K: a = 16 B of nibbles, b = superblock header {d, dmin, 4 x 24-bit scale pairs}
+//   Q6_K: a = 16 B of ql, b = 16 B of qh, c = the lane's two int8 sub-block scales, e = d
+//   Q8_0: a, b = the lane's 32 codes, e = d
+struct Frag {
+    uint4 a, b;
+    uint32_t c, e;
+};
+
+// One unit's activation registers (the lane's 32 int8 values, two bsums, the scale).
+struct ALane {
+    int4 lo, hi;
+    int b0, b1;
+    float d;
+};
+
+// Lane mapping per pass: K-quants - 8 superblocks x 8 lanes (lane>>3 = superblock,
+// lane&7 = 16-byte piece); Q8_0 - 64 blocks, one per lane (32 codes = two 16-B loads).
+// `row` is wave-uniform, so the row base address is scalar. Loads are unconditional
+// (indices past K are clamped to the row's last block and their terms zeroed in
+// dot_frag): no branches around loads, so vmcnt accounting stays exact and raw data is
+// only converted where it is consumed.
+// Raw buffer loads: descriptor from the (uniform) base and its exact byte size, the row
+// offset in an SGPR (soffset), the lane's constant byte offset in voffset - no per-load
+// address VALU; lanes past the end read 0 (range-checked).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void *p, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), 0, (int)min(bytes, 0x7FFFFFF0u), 0x00020000);
+}
+__device__ __forceinline__ uint4 bld16(const uint8_t *base, uint32_t bytes, uint32_t voff, uint32_t soff) {
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rsrc(base, bytes), voff, soff, 0);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ uint32_t bld2(const uint8_t *base, uint32_t bytes, uint32_t voff, uint32_t soff) {
+    return __builtin_amdgcn_raw_buffer_load_b16(rsrc(base, bytes), voff, soff, 0);
+}
+
+template <int T>
+__device__ __forceinline__ Frag load_frag(const QMat W, int row, int pass) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t R = (uint32_t)W.rows, r = (uint32_t)min(max(row, 0), W.rows - 1);
+    Frag f;
+    if constexpr (T == 12) {
+        const int nsb = W.k >> 8, sb = min(pass * 8 + (lane >> 3), nsb - 1), pc = lane & 7;
+        const uint32_t qb = (uint32_t)(W.k / 2), hb = (uint32_t)nsb * 16;
+        f.a = bld16(W.p0, R * qb, sb * 128 + pc * 16, r * qb);
+        f.b = bld16(W.p1, R * hb, sb * 16, r * hb);
+        f.c = f.e = 0;
+    } else if constexpr (T == 14) {
+        const int nsb = W.k >> 8, sb = min(pass * 8 + (lane >> 3), nsb - 1), pc = lane & 7;
+        const uint32_t lb = (uint32_t)(W.k / 2), hb = (uint32_t)(W.k / 4), sbb = (uint32_t)(W.k / 16),
+                       db = (uint32_t)nsb * 2;
+        f.a = bld16(W.p0, R * lb, sb * 128 + pc * 16, r * lb);
+        f.b = bld16(W.p1, R * hb, sb * 64 + 32 * (pc >> 2) + 16 * (pc & 1), r * hb);
+        f.c = bld2(W.p2, R * sbb, sb * 16 + 2 * pc, r * sbb);
+        f.e = bld2(W.p3, R * db, sb * 2, r * db);
+    } else {
+        const int nb = W.k >> 5, b = min(pass * 64 + lane, nb - 1);
+        const uint32_t qb = (uint32_t)W.k, db = (uint32_t)nb * 2;
+        f.a = bld16(W.p0, R * qb, 32 * b, r * qb);
+        f.b = bld16(W.p0, R * qb, 32 * b + 16, r * qb);
+        f.c = 0;
+        f.e = bld2(W.p1, R * db, 2 * b, r * db);
+    }
+    return f;
+}
+
+template <int T>
+__device__ __forceinline__ ALane load_alane(const ActL &a, int K, int pass) {
+    const int lane = threadIdx.x & 63;
+    ALane r;
+    if constexpr (T == 12 || T == 14) {
+        const int nsb = K >> 8, sb = pass * 8 + (lane >> 3), pc = lane & 7;
+        const int sbc = sb < nsb ? sb : 0;
+        int e, e2;
+        if constexpr (T == 12) {
+            e = sbc * 256 + 64 * (pc >> 1) + 16 * (pc & 1);
+            e2 = e + 32;
+        } else {
+            const int n = pc >> 2, qq = pc & 3;
+            e = sbc * 256 + 128 * n + 32 * (qq >> 1) + 16 * (qq & 1);
+            e2 = e + 64;
+        }
+        r.lo = *reinterpret_cast<const int4 *>(a.qs + e);
+        r.hi = *reinterpret_cast<const int4 *>(a.qs + e2);
+        r.b0 = a.bs[e >> 4];
+        r.b1 = a.bs[e2 >> 4];
+        r.d = a.d[sbc];
+    } else {
+        const int nb = K >> 5, b = pass * 64 + lane, bc = b < nb ? b : 0;
+        r.lo = *reinterpret_cast<const int4 *>(a.qs + 32 * bc);
+        r.hi = *reinterpret_cast<const int4 *>(a.qs + 32 * bc + 16);
+        r.b0 = r.b1 = 0;
+        r.d = a.d[bc];
+    }
+    return r;
+}
+
+// This lane's partial of the row dot for one pass. K-quants: the per-superblock integer
+// sums are reduced exactly over the superblock's 8 lanes (ggml vec_dot semantics) and the
+// superblock's float term is valid in lane 8k+7; Q8_0: every lane holds one block's term.
+// Lanes whose superblock / block lies past K have zero codes and zero scales -> 0.
+template <int T>
+__device__ __forceinline__ float dot_frag(const Frag &f, const ALane &al, int K, int pass) {
+    const int lane = threadIdx.x & 63;
+    if constexpr (T == 12) {
+        const int jj = (lane & 7) >> 1;
+        const uint4 h = f.b;
+        const uint32_t wlo = jj < 2 ? h.y : (jj == 2 ? h.z : h.w);
+        const uint32_t whi = jj < 2 ? h.z : h.w;
+        const uint32_t F = __builtin_amdgcn_alignbit(whi, wlo, (24 * jj) & 31);
+        const int sc0 = F & 63, m0 = (F >> 6) & 63, sc1 = (F >> 12) & 63, m1 = (F >> 18) & 63;
+        int dlo = 0, dhi = 0;
+        dlo = sdot4((int)(f.a.x & M4), al.lo.x, dlo);
+        dlo = sdot4((int)(f.a.y & M4), al.lo.y, dlo);
+        dlo = sdot4((int)(f.a.z & M4), al.lo.z, dlo);
+        dlo = sdot4((int)(f.a.w & M4), al.lo.w, dlo);
+        dhi = sdot4((int)((f.a.x >> 4) & M4), al.hi.x, dhi);
+        dhi = sdot4((int)((f.a.y >> 4) & M4), al.hi.y, dhi);
+        dhi = sdot4((int)((f.a.z >> 4) & M4), al.hi.z, dhi);
+        dhi = sdot4((int)((f.a.w >> 4) & M4), al.hi.w, dhi);
+        int isum = __mul24(sc0, dlo) + __mul24(sc1, dhi);
+        int imin = __mul24(m0, al.b0) + __mul24(m1, al.b1);
+        isum = sum8_i(isum);
+        imin = sum8_i(imin);
+        const float d = h2f(h.x & 0xFFFF) * al.d;
+        const float dmin = h2f(h.x >> 16) * al.d;
+        float v = d * (float)isum;
+        v = v - dmin * (float)imin;
+        return pass * 8 + (lane >> 3) < (K >> 8) ? v : 0.0f;
+    } else if constexpr (T == 14) {
+        // high 2 bits of the low-nibble codes sit at bit 2*gl of each qh byte, of the
+        // high-nibble codes at bit 2*gl+4 (gl = (lane&3)>>1); move them to bits 4-5
+        const int shl = 2 * ((lane & 3) >> 1);
+        auto lo = [&](uint32_t l, uint32_t h) { return (int)((l & M4) | ((h << (4 - shl)) & 0x30303030u)); };
+        auto hi = [&](uint32_t l, uint32_t h) { return (int)(((l >> 4) & M4) | ((h >> shl) & 0x30303030u)); };
+        int dlo = 0, dhi = 0;
+        dlo = sdot4(lo(f.a.x, f.b.x), al.lo.x, dlo);
+        dlo = sdot4(lo(f.a.y, f.b.y), al.lo.y, dlo);
+        dlo = sdot4(lo(f.a.z, f.b.z), al.lo.z, dlo);
+        dlo = sdot4(lo(f.a.w, f.b.w), al.lo.w, dlo);
+        dhi = sdot4(hi(f.a.x, f.b.x), al.hi.x, dhi);
+        dhi = sdot4(hi(f.a.y, f.b.y), al.hi.y, dhi);
+        dhi = sdot4(hi(f.a.z, f.b.z), al.hi.z, dhi);
+        dhi = sdot4(hi(f.a.w, f.b.w), al.hi.w, dhi);
+        const int sa = (int)(int8_t)(f.c & 0xFF), sb = (int)(int8_t)(f.c >> 8);
+        int isum = __mul24(sa, dlo - 32 * al.b0) + __mul24(sb, dhi - 32 * al.b1);
+        isum = sum8_i(isum);
+        const float d = h2f(f.e) * al.d;
+        const float v = d * (float)isum;
+        return pass * 8 + (lane >> 3) < (K >> 8) ? v : 0.0f;
+    } else {
+        int s = 0;
+        s = sdot4((int)f.a.x, al.lo.x, s);
+        s = sdot4((int)f.a.y, al.lo.y, s);
+        s = sdot4((int)f.a.z, al.lo.z, s);
+        s = sdot4((int)f.a.w, al.lo.w, s);
+        s = sdot4((int)f.b.x, al.hi.x, s);
+        s = sdot4((int)f.b.y, al.hi.y, s);
+        s = sdot4((int)f.b.z, al.hi.z, s);
+        s = sdot4((int)f.b.w, al.hi.w, s);
+        const float v = (float)s * (h2f(f.e) * al.d);
+        return pass * 64 + lane < (K >> 5) ? v : 0.0f;
+    }
+}
+
+// Row total of the per-lane partials (accumulated over the row's passes), wave-uniform.
+template <int T>
+__device__ __forceinline__ float row_total(float acc) {
+    if constexpr (T == 8) acc = sum8_f(acc);
+    return sum_lanes7(acc);
+}
+
+// ------------------------------------------------------------------ streaming rows
+// NP passes per row (1, 3 or 6); U units per register group; NP <= 3 keeps the lane's
+// activation slices in registers for the whole stream.
+template <int NP>
+struct Cfg {
+    static constexpr int U = NP == 1 ? 4 : 3;
+    static constexpr bool AREG = NP <= 3;
+};
+
+// Loads units [u0, u0 + U) (clamped into [0, n): loads are never skipped, so the
+// compiler's in-order vmcnt accounting stays exact). Unit u -> row lo + u/(NP*NM),
+// matrix (u/NP)%NM, pass u%NP. With NM == 1, rows >= split come from W1 (row - split):
+// two matrices of one type streamed as one row space (q|k).
+template <int T, int NP, int NM>
+__device__ __forceinline__ void load_group(const QMat W0, const QMat W1, int lo, int n, int u0,
+                                           Frag (&f)[Cfg<NP>::U], int split = INT_MAX) {
+#pragma unroll
+    for (int j = 0; j < Cfg<NP>::U; ++j) {
+        const int u = max(0, min(u0 + j, n - 1));
+        const int p = u % NP, m = (u / NP) % NM, i = u / (NP * NM);
+        if constexpr (NM == 1) {
+            const int r = lo + i;
+            f[j] = load_frag<T>(r >= split ? W1 : W0, r >= split ? r - split : r, p);
+        } else {
+            f[j] = load_frag<T>(m ? W1 : W0, lo + i, p);
+        }
+    }
+}
+
+// Streams rows [lo, hi) (wave-uniform) of W0 (and W1 when NM == 2: row pairs, e.g.
+// gate/up); calls epi(row, dot0, dot1) once per row with wave-uniform values. A holds the
+// first group when pre is true; groups alternate between A and B (no register copies).
+template <int T, int NP, int NM, class Epi>
+__device__ __forceinline__ void stream_rows(const QMat W0, const QMat W1, int lo, int hi, Frag (&A)[Cfg<NP>::U],
+                                            bool pre, const ActL &a, Epi &&epi, int split = INT_MAX) {
+    constexpr int U = Cfg<NP>::U;
+    const int K = W0.k;
+    const int n = (hi - lo) * NM * NP;
+    if (n <= 0) return;
+    if (!pre) load_group<T, NP, NM>(W0, W1, lo, n, 0, A, split);
+    ALane al[Cfg<NP>::AREG ? NP : 1];
+    if constexpr (Cfg<NP>::AREG) {
+#pragma unroll
+        for (int p = 0; p < NP; ++p) al[p] = load_alane<T>(a, K, p);
+    }
+    float acc = 0.0f, g = 0.0f;
+    auto consume = [&](const Frag (&F)[U], int u0) {
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            const int u = u0 + j;
+            if (u < n) {
+                int p;
+                ALane av;
+                if constexpr (NP == 1) {
+                    p = 0;
+                    av = al[0];
+                } else if constexpr (NP == U) {
+                    p = j;
+                    av = al[j];
+                } else {
+                    p = u % NP;
+                    av = load_alane<T>(a, K, p);
+                }
+                acc += dot_frag<T>(F[j], av, K, p);
+                if (p == NP - 1) {
+                    const float v = row_total<T>(acc);
+                    acc = 0.0f;
+                    const int i = u / (NP * NM);
+                    if constexpr (NM == 1) {
+                        epi(lo + i, v, 0.0f);
+                    } else {
+                        if ((u / NP) % NM == 0)
+                            g = v;
+                        else
+                            epi(lo + i, g, v);
+                    }
+                }
+            }
+        }
+    };
+    Frag B[U];
+    for (int u0 = 0;;) {
+        load_group<T, NP, NM>(W0, W1, lo, n, u0 + U, B, split);
+        consume(A, u0);
+        u0 += U;
+        if (u0 >= n) break;
+        load_group<T, NP, NM>(W0, W1, lo, n, u0 + U, A, split);
+        consume(B, u0);
+        u0 += U;
+        if (u0 >= n) break;
+    }
+}
+
+// Rows [0, R) over G workgroups: workgroup b owns [R*b/G, R*(b+1)/G), wave w a contiguous
+// eighth of that (wave-uniform, held in scalar registers). R*G < 2^31.
+__device__ inline void wave_range(int R, int &lo, int &hi, int b, int G) {
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int ra = (R * b) / G, rb = (R * (b + 1)) / G;
+    lo = ra + (rb - ra) * w / MW;
+    hi = ra + (rb - ra) * (w + 1) / MW;
+}
+__device__ inline void wave_range(int R, int &lo, int &hi) { wave_range(R, lo, hi, blockIdx.x, gridDim.x); }
+
+// ------------------------------------------------------------------ matvec kernels
+// Every kernel is instantiated per weight type T (ggml id 8 / 12 / 14): the unit loop is
+// straight-line code with no run-time type dispatch.
+// q|k rows (type TQ) on the first g_qk workgroups, v rows (type TV) on the rest; each
+// branch is WG-uniform and runs its own prologue, so neither path merges load counts.
+template <int NP, int TQ, int TV>
+__global__ __launch_bounds__(MT) void k_attn_in(LlmDims d, const float *norm_w, QMat wq, QMat wk, QMat wv,
+                                                int g_qk, LlmBuffers b) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int K = d.n_embd;
     const Smem s = carve(smem, K);
-    XRegs<XV> xr;
-    load_x(b.x, K, xr);
-    int row0 = blockIdx.x * QKV_ROWS;
-    const int seg = row0 >= wq.rows + wk.rows ? 2 : (row0 >= wq.rows ? 1 : 0);
-    const QMat W = seg == 2 ? wv : (seg == 1 ? wk : wq);
-    const int off = seg == 2 ? wq.rows + wk.rows : (seg == 1 ? wq.rows : 0);
-    row0 -= off;
-    float *out = b.qkv + off;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    int rows[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) rows[r] = row0 + wave * 4 + r < W.rows ? row0 + wave * 4 + r : -1;
-    Frag pre[4][P];
-    preload<4, P>(W, rows, pre);
-    rmsnorm_quant(xr, norm_w, K, d.eps, wq.type != 8, s);
-    float o[4];
-    finish_rows<4, P>(W, rows, pre, s.a, o);
-    if (lane == 0)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-            if (rows[r] >= 0) out[rows[r]] = o[r];
+    MIO_TRACE(b, 0);
+    XRegs<NP> xr;
+    load_x(b.x, norm_w, K, xr);
+    const int o1 = wq.rows, o2 = wq.rows + wk.rows;
+    Frag cur[Cfg<NP>::U];
+    int lo, hi;
+    if ((int)blockIdx.x < g_qk) {
+        wave_range(o2, lo, hi, blockIdx.x, g_qk);
+        load_group<TQ, NP, 1>(wq, wk, lo, (hi - lo) * NP, 0, cur, o1);
+        MIO_TRACE(b, 1);
+        rmsnorm_quant(xr, K, d.eps, TQ != 8, s);
+        MIO_TRACE(b, 2);
+        stream_rows<TQ, NP, 1>(wq, wk, lo, hi, cur, true, s.a, [&](int row, float v, float) {
+            if ((threadIdx.x & 63) == 0) b.qkv[row] = v;
+        }, o1);
+        MIO_TRACE(b, 15);
+    } else {
+        wave_range(wv.rows, lo, hi, blockIdx.x - g_qk, gridDim.x - g_qk);
+        load_group<TV, NP, 1>(wv, wv, lo, (hi - lo) * NP, 0, cur);
+        rmsnorm_quant(xr, K, d.eps, TQ != 8, s);
+        stream_rows<TV, NP, 1>(wv, wv, lo, hi, cur, true, s.a, [&](int row, float v, float) {
+            if ((threadIdx.x & 63) == 0) b.qkv[o2 + row] = v;
+        });
+    }
 }
 
-// Attention for one (kv head, split of d.split positions). HD = head dim.
-template <int HD, int G>
-__global__ __launch_bounds__(NT) void k_attention(LlmDims d, const float *q_norm, const float *k_norm,
-                                                  _Float16 *kc, _Float16 *vc, LlmBuffers b) {
-    constexpr int LP = HD / 8;          // lanes per position (8 dims each)
-    constexpr int NS = NT / LP;         // position slots per workgroup
-    constexpr int GMAX = G;
-    __shared__ float qs[GMAX][HD];
-    __shared__ float knew[HD], vnew[HD];
+// residual rows of this wave (<= 64) in one register: lane i holds x[lo + i]
+__device__ inline float load_resid(const float *x, int lo, int hi) {
+    const int lane = threadIdx.x & 63;
+    return lo + lane < hi ? x[lo + lane] : 0.0f;
+}
+__device__ inline float lane_value(float v, int i) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), i));
+}
+
+// Merge of the attention chunks' partial records (k_attention) for all heads: thread t
+// owns outputs 4(t + i*MT) .. +3; online softmax merge over chunks, 8 chunks' loads in
+// flight; normalized outputs -> s.xs, then re-quantized into s.a.
+template <int NP>
+__device__ void merge_attention(const LlmDims &d, const float *part, int nch, int K, bool kquant, const Smem &s) {
+    const int hd = d.hd, rec = part_rec(hd);
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+        const int e = (threadIdx.x + i * MT) * 4;
+        if (e < K) {
+            const int h = e / hd, dd = e - h * hd;
+            const float *base = part + (size_t)h * d.max_splits * rec;
+            float M = -INFINITY, L = 0.0f;
+            float4 O = make_float4(0.f, 0.f, 0.f, 0.f);
+            constexpr int CB = 8;  // chunks per batch of loads
+            for (int c0 = 0; c0 < nch; c0 += CB) {
+                float2 ml[CB];
+                float4 oc[CB];
+#pragma unroll
+                for (int j = 0; j < CB; ++j) {
+                    const int c = min(c0 + j, nch - 1);
+                    ml[j] = *reinterpret_cast<const float2 *>(base + (size_t)c * rec + hd);
+                    oc[j] = *reinterpret_cast<const float4 *>(base + (size_t)c * rec + dd);
+                }
+                float mb = M;
+#pragma unroll
+                for (int j = 0; j < CB; ++j) mb = fmaxf(mb, ml[j].x);
+                const float a = M == -INFINITY ? 0.0f : expf(M - mb);
+                L *= a;
+                O.x *= a, O.y *= a, O.z *= a, O.w *= a;
+#pragma unroll
+                for (int j = 0; j < CB; ++j) {
+                    const float w = c0 + j < nch ? expf(ml[j].x - mb) : 0.0f;
+                    L += w * ml[j].y;
+                    O.x += w * oc[j].x, O.y += w * oc[j].y, O.z += w * oc[j].z, O.w += w * oc[j].w;
+                }
+                M = mb;
+            }
+            *reinterpret_cast<float4 *>(s.xs + e) = make_float4(O.x / L, O.y / L, O.z / L, O.w / L);
+        }
+    }
+    __syncthreads();
+    quantize(s.xs, K, kquant, s.a);
+}
+
+template <int NP, int T>
+__global__ __launch_bounds__(MT) void k_attn_out(LlmDims d, QMat wo, LlmBuffers b) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    float *slot = (float *)smem;  // [NS][G][HD + 2]
-
-    const int kvh = blockIdx.y, sp = blockIdx.x;
-    const int pos = b.st->pos;
-    const int t0 = sp * d.split;
-    if (t0 > pos) return;
-    const int t1 = min(t0 + d.split, pos + 1);
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const float2 *rope = b.rope + (size_t)pos * (HD / 2);
-
-    // q (and, for the owner of `pos`, k/v): optional per-head RMSNorm, RoPE, f16 rounding
-    auto prep = [&](const float *src, const float *nw, float *dst, bool round_f16) {
-        // one wave, HD values
-        float v[HD / 64 > 0 ? HD / 64 : 1];
-        constexpr int PER = HD / 64;
-        double ss = 0.0;
-#pragma unroll
-        for (int i = 0; i < PER; ++i) {
-            v[i] = src[lane + 64 * i];
-            ss += (double)(v[i] * v[i]);
-        }
-        if (d.qk_norm) {
-#pragma unroll
-            for (int o = 32; o >= 1; o >>= 1) ss += __shfl_xor(ss, o);
-            const float mean = (float)(ss / HD);
-            const float scale = 1.0f / sqrtf(mean + d.eps);
-#pragma unroll
-            for (int i = 0; i < PER; ++i) {
-                const float t = v[i] * scale;
-                v[i] = t * nw[lane + 64 * i];
-            }
-        }
-#pragma unroll
-        for (int i = 0; i < PER; ++i) dst[lane + 64 * i] = v[i];
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        // rope: pair p (HD/2 pairs)
-        float o0[PER], o1[PER];
-        int i0s[PER], i1s[PER];
-#pragma unroll
-        for (int i = 0; i < PER; ++i) {
-            const int p = lane + 64 * i;
-            i0s[i] = -1;
-            if (p < HD / 2) {
-                const int i0 = d.neox ? p : 2 * p, i1 = d.neox ? p + HD / 2 : 2 * p + 1;
-                const float x0 = dst[i0], x1 = dst[i1];
-                const float2 cs = rope[p];
-                o0[i] = x0 * cs.x - x1 * cs.y;
-                o1[i] = x0 * cs.y + x1 * cs.x;
-                i0s[i] = i0, i1s[i] = i1;
-            }
-        }
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-#pragma unroll
-        for (int i = 0; i < PER; ++i)
-            if (i0s[i] >= 0) {
-                dst[i0s[i]] = round_f16 ? f16r(o0[i]) : o0[i];
-                dst[i1s[i]] = round_f16 ? f16r(o1[i]) : o1[i];
-            }
-    };
-    for (int g = wave; g < G; g += NWAVE)
-        prep(b.qkv + (size_t)(kvh * G + g) * HD, q_norm, qs[g], true);
-    const bool owner = pos >= t0 && pos < t0 + d.split;
-    if (owner && wave == NWAVE - 1) {
-        const float *kr = b.qkv + (size_t)d.n_head * HD + (size_t)kvh * HD;
-        const float *vr = b.qkv + (size_t)(d.n_head + d.n_kv) * HD + (size_t)kvh * HD;
-        prep(kr, k_norm, knew, true);
-        __builtin_amdgcn_wave_barrier();
-        _Float16 *kd = kc + ((size_t)kvh * d.n_ctx + pos) * HD;
-        _Float16 *vd = vc + ((size_t)kvh * d.n_ctx + pos) * HD;
-        for (int i = lane; i < HD; i += 64) {
-            const float vv = f16r(vr[i]);
-            vnew[i] = vv;
-            kd[i] = (_Float16)knew[i];
-            vd[i] = (_Float16)vv;
-        }
-    }
-    __syncthreads();
-
-    // main loop: LP lanes per position, 8 dims per lane, online softmax per q head
-    const int lp = lane % LP;
-    const int sl = tid / LP;
-    float qv[GMAX][8];
-#pragma unroll
-    for (int g = 0; g < G; ++g)
-#pragma unroll
-        for (int i = 0; i < 8; ++i) qv[g][i] = qs[g][lp * 8 + i];
-    float m[GMAX], l[GMAX], acc[GMAX][8];
-#pragma unroll
-    for (int g = 0; g < GMAX; ++g) {
-        m[g] = -INFINITY, l[g] = 0.0f;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) acc[g][i] = 0.0f;
-    }
-    const _Float16 *kbase = kc + (size_t)kvh * d.n_ctx * HD;
-    const _Float16 *vbase = vc + (size_t)kvh * d.n_ctx * HD;
-    for (int t = t0 + sl; t < t1; t += NS) {
-        float kf[8], vf[8];
-        if (t == pos) {
-#pragma unroll
-            for (int i = 0; i < 8; ++i) kf[i] = knew[lp * 8 + i], vf[i] = vnew[lp * 8 + i];
-        } else {
-            typedef _Float16 h8 __attribute__((ext_vector_type(8)));
-            const h8 kk = *reinterpret_cast<const h8 *>(kbase + (size_t)t * HD + lp * 8);
-            const h8 vv = *reinterpret_cast<const h8 *>(vbase + (size_t)t * HD + lp * 8);
-#pragma unroll
-            for (int i = 0; i < 8; ++i) kf[i] = (float)kk[i], vf[i] = (float)vv[i];
-        }
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-            float sdot = 0.0f;
-#pragma unroll
-            for (int i = 0; i < 8; ++i) sdot = fmaf(qv[g][i], kf[i], sdot);
-#pragma unroll
-            for (int o = 1; o < LP; o <<= 1) sdot += __shfl_xor(sdot, o);
-            const float sc = sdot * d.scale;
-            const float mn = fmaxf(m[g], sc);
-            const float c = expf(m[g] - mn);
-            const float p = expf(sc - mn);
-            l[g] = l[g] * c + p;
-#pragma unroll
-            for (int i = 0; i < 8; ++i) acc[g][i] = acc[g][i] * c + p * vf[i];
-            m[g] = mn;
-        }
-    }
-    // slot partials -> LDS
-    const int rec = HD + 2;
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-        float *sp_ = slot + ((size_t)sl * G + g) * rec;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) sp_[lp * 8 + i] = acc[g][i];
-        if (lp == 0) sp_[HD] = m[g], sp_[HD + 1] = l[g];
-    }
-    __syncthreads();
-    // combine slots: thread per (g, dim)
-    for (int e = tid; e < G * HD; e += NT) {
-        const int g = e / HD, dd = e - g * HD;
-        float M = -INFINITY;
-        for (int q = 0; q < NS; ++q) M = fmaxf(M, slot[((size_t)q * G + g) * rec + HD]);
-        float L = 0.0f, O = 0.0f;
-        for (int q = 0; q < NS; ++q) {
-            const float *r = slot + ((size_t)q * G + g) * rec;
-            const float w = r[HD] == -INFINITY ? 0.0f : expf(r[HD] - M);
-            L += w * r[HD + 1];
-            O += w * r[dd];
-        }
-        float *dst = b.part + ((size_t)(kvh * G + g) * d.max_splits + sp) * rec;
-        dst[dd] = O;
-        if (dd == 0) dst[HD] = M, dst[HD + 1] = L;
-    }
-}
-
-template <int HD>
-void launch_attention(int G, dim3 grid, size_t lds, hipStream_t s, const LlmDims &d, const float *qn,
-                      const float *kn, _Float16 *kc, _Float16 *vc, const LlmBuffers &b) {
-    switch (G) {
-        case 1: hipLaunchKernelGGL((k_attention<HD, 1>), grid, dim3(NT), lds, s, d, qn, kn, kc, vc, b); break;
-        case 2: hipLaunchKernelGGL((k_attention<HD, 2>), grid, dim3(NT), lds, s, d, qn, kn, kc, vc, b); break;
-        case 3: hipLaunchKernelGGL((k_attention<HD, 3>), grid, dim3(NT), lds, s, d, qn, kn, kc, vc, b); break;
-        case 4: hipLaunchKernelGGL((k_attention<HD, 4>), grid, dim3(NT), lds, s, d, qn, kn, kc, vc, b); break;
-        case 8: hipLaunchKernelGGL((k_attention<HD, 8>), grid, dim3(NT), lds, s, d, qn, kn, kc, vc, b); break;
-        default: break;
-    }
-}
-
-// Split combine of the attention partials + re-quantization of the attention output
-// (one workgroup per 256 outputs = one Q8_K block / eight Q8_0 blocks) -> global blob.
-__global__ __launch_bounds__(NT) void k_attn_combine(LlmDims d, int kquant, LlmBuffers b) {
-    __shared__ float xs[NT];
-    __shared__ __attribute__((aligned(16))) int8_t qs[NT];
-    __shared__ float dd[8];
-    __shared__ int16_t bs[16];
-    const int K = d.n_head * d.hd;
-    const int pos = b.st->pos;
-    const int nsp = pos / d.split + 1;
-    const int rec = d.hd + 2;
-    const int e = blockIdx.x * NT + threadIdx.x;
-    const int ec = e < K ? e : K - 1;
-    const int h = ec / d.hd, dd_ = ec - h * d.hd;
-    const float *base = b.part + (size_t)h * d.max_splits * rec;
-    float M = -INFINITY;
-    for (int sp = 0; sp < nsp; ++sp) M = fmaxf(M, base[(size_t)sp * rec + d.hd]);
-    float L = 0.0f, O = 0.0f;
-    for (int sp = 0; sp < nsp; ++sp) {
-        const float *r = base + (size_t)sp * rec;
-        const float w = expf(r[d.hd] - M);
-        L += w * r[d.hd + 1];
-        O += w * r[dd_];
-    }
-    if (e >= K) O = 0.0f, L = 1.0f;
-    xs[threadIdx.x] = O / L;
-    __syncthreads();
-    ActL a{qs, dd, bs};
-    quantize(xs, NT, kquant != 0, a);
-    const Smem gs = carve((char *)b.act2, K);
-    if (threadIdx.x < NT / 4 && blockIdx.x * NT + 4 * threadIdx.x < K)
-        ((int *)gs.a.qs)[blockIdx.x * (NT / 4) + threadIdx.x] = ((const int *)qs)[threadIdx.x];
-    if (kquant) {
-        if (threadIdx.x == 0) gs.a.d[blockIdx.x] = dd[0];
-        if (threadIdx.x < 16) gs.a.bs[blockIdx.x * 16 + threadIdx.x] = bs[threadIdx.x];
-    } else if (threadIdx.x < 8 && blockIdx.x * NT + 32 * threadIdx.x < K) {
-        gs.a.d[blockIdx.x * 8 + threadIdx.x] = dd[threadIdx.x];
-    }
-}
-
-template <int P, int XV>
-__global__ __launch_bounds__(NT) void k_attn_out(LlmDims d, QMat wo, LlmBuffers b) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int K = d.n_head * d.hd;
+    MIO_TRACE(b, 0);
+    const int K = wo.k;
     const Smem s = carve(smem, K);
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    int rows[2];
-    const int r0 = blockIdx.x * RES_ROWS + wave * 2;
-    rows[0] = r0 < wo.rows ? r0 : -1;
-    rows[1] = r0 + 1 < wo.rows ? r0 + 1 : -1;
-    Frag pre[2][P];
-    preload<2, P>(wo, rows, pre);
-    act_from_global(b.act2, K, s);
-    float o[2];
-    finish_rows<2, P>(wo, rows, pre, s.a, o);
-    if (lane == 0) {
-        if (rows[0] >= 0) b.x[rows[0]] = o[0] + b.x[rows[0]];
-        if (rows[1] >= 0) b.x[rows[1]] = o[1] + b.x[rows[1]];
-    }
+    int lo, hi;
+    wave_range(wo.rows, lo, hi);
+    const float xres = load_resid(b.x, lo, hi);
+    Frag cur[Cfg<NP>::U];
+    load_group<T, NP, 1>(wo, wo, lo, (hi - lo) * NP, 0, cur);
+    MIO_TRACE(b, 1);
+    merge_attention<NP>(d, b.part, b.st->pos / ATT_CHUNK + 1, K, T != 8, s);
+    MIO_TRACE(b, 2);
+    stream_rows<T, NP, 1>(wo, wo, lo, hi, cur, true, s.a, [&](int row, float v, float) {
+        const float r = lane_value(xres, row - lo);
+        if ((threadIdx.x & 63) == 0) b.x[row] = v + r;
+    });
+    MIO_TRACE(b, 15);
 }
 
 __device__ inline float silu_f(float x) { return x / (1.0f + expf(-x)); }
 
-template <int P, int XV>
-__global__ __launch_bounds__(NT) void k_ffn_in(LlmDims d, const float *norm_w, QMat gate, QMat up, LlmBuffers b) {
+template <int NP, int T>
+__global__ __launch_bounds__(MT) void k_ffn_in(LlmDims d, const float *norm_w, QMat gate, QMat up, LlmBuffers b) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
+    MIO_TRACE(b, 0);
     const int K = d.n_embd;
     const Smem s = carve(smem, K);
-    XRegs<XV> xr;
-    load_x(b.x, K, xr);
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    int rows[2];
-    const int r0 = blockIdx.x * FFN_PAIRS + wave * 2;
-    rows[0] = r0 < gate.rows ? r0 : -1;
-    rows[1] = r0 + 1 < gate.rows ? r0 + 1 : -1;
-    Frag pg[2][P], pu[2][P];
-    preload<2, P>(gate, rows, pg);
-    preload<2, P>(up, rows, pu);
-    rmsnorm_quant(xr, norm_w, K, d.eps, gate.type != 8, s);
-    float g[2], u[2];
-    finish_rows<2, P>(gate, rows, pg, s.a, g);
-    finish_rows<2, P>(up, rows, pu, s.a, u);
-    if (lane == 0) {
-        if (rows[0] >= 0) b.h[rows[0]] = silu_f(g[0]) * u[0];
-        if (rows[1] >= 0) b.h[rows[1]] = silu_f(g[1]) * u[1];
-    }
+    XRegs<NP> xr;
+    load_x(b.x, norm_w, K, xr);
+    int lo, hi;
+    wave_range(gate.rows, lo, hi);
+    Frag cur[Cfg<NP>::U];
+    load_group<T, NP, 2>(gate, up, lo, (hi - lo) * NP * 2, 0, cur);
+    MIO_TRACE(b, 1);
+    rmsnorm_quant(xr, K, d.eps, T != 8, s);
+    MIO_TRACE(b, 2);
+    stream_rows<T, NP, 2>(gate, up, lo, hi, cur, true, s.a, [&](int row, float g, float u) {
+        if ((threadIdx.x & 63) == 0) b.h[row] = silu_f(g) * u;
+    });
+    MIO_TRACE(b, 15);
 }
 
-template <int P, int XV>
-__global__ __launch_bounds__(NT) void k_ffn_down(LlmDims d, QMat down, LlmBuffers b) {
+template <int NP, int T>
+__global__ __launch_bounds__(MT) void k_ffn_down(LlmDims d, QMat down, LlmBuffers b) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int K = d.n_ff;
+    MIO_TRACE(b, 0);
+    const int K = down.k;
     const Smem s = carve(smem, K);
-    XRegs<XV> xr;
-    load_x(b.h, K, xr);
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    int rows[2];
-    const int r0 = blockIdx.x * RES_ROWS + wave * 2;
-    rows[0] = r0 < down.rows ? r0 : -1;
-    rows[1] = r0 + 1 < down.rows ? r0 + 1 : -1;
-    Frag pre[2][P];
-    preload<2, P>(down, rows, pre);
-    plain_quant(xr, K, down.type != 8, s);
-    float o[2];
-    finish_rows<2, P>(down, rows, pre, s.a, o);
-    if (lane == 0) {
-        if (rows[0] >= 0) b.x[rows[0]] = o[0] + b.x[rows[0]];
-        if (rows[1] >= 0) b.x[rows[1]] = o[1] + b.x[rows[1]];
-    }
-}
-
-// final RMSNorm + re-quantization once per step -> global (read by every lm_head block)
-template <int P, int XV>
-__global__ __launch_bounds__(NT) void k_final_norm(LlmDims d, const float *norm_w, int kquant, LlmBuffers b) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int K = d.n_embd;
-    const Smem s = carve(smem, K);
-    XRegs<XV> xr;
-    load_x(b.x, K, xr);
-    rmsnorm_quant(xr, norm_w, K, d.eps, kquant != 0, s);
-    const Smem gs = carve((char *)b.act, K);
-    for (int i = threadIdx.x; i < K / 4; i += NT) ((int *)gs.a.qs)[i] = ((const int *)s.a.qs)[i];
-    for (int i = threadIdx.x; i < K / 32; i += NT) gs.a.d[i] = s.a.d[i];
-    for (int i = threadIdx.x; i < K / 16; i += NT) gs.a.bs[i] = s.a.bs[i];
+    XRegs<NP> xr;
+    load_x(b.h, nullptr, K, xr);
+    int lo, hi;
+    wave_range(down.rows, lo, hi);
+    const float xres = load_resid(b.x, lo, hi);
+    Frag cur[Cfg<NP>::U];
+    load_group<T, NP, 1>(down, down, lo, (hi - lo) * NP, 0, cur);
+    MIO_TRACE(b, 1);
+    plain_quant(xr, K, T != 8, s);
+    MIO_TRACE(b, 2);
+    stream_rows<T, NP, 1>(down, down, lo, hi, cur, true, s.a, [&](int row, float v, float) {
+        const float r = lane_value(xres, row - lo);
+        if ((threadIdx.x & 63) == 0) b.x[row] = v + r;
+    });
+    MIO_TRACE(b, 15);
 }
 
 __device__ inline uint64_t mix64(uint64_t x) {
@@ -795,78 +786,316 @@ __device__ inline float gumbel(uint64_t seed, int step, int idx) {
     return -logf(-logf(u));
 }
 
-template <int P>
-__global__ __launch_bounds__(NT) void k_lm_head(LlmDims d, QMat lm, SampleCfg sc, LlmBuffers b) {
+// final RMSNorm (once per CU) + logits + per-workgroup Gumbel-max partial. A wave's rows
+// (<= 128) are parked one per lane (two registers) and the noise is drawn for 64 rows at
+// a time after the stream.
+template <int NP, int T>
+__global__ __launch_bounds__(MT) void k_lm_head(LlmDims d, const float *norm_w, QMat lm, SampleCfg sc, LlmBuffers b) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    __shared__ float bs_[NWAVE];
-    __shared__ int bi_[NWAVE];
+    __shared__ float bs_[MW];
+    __shared__ int bi_[MW];
     const int K = d.n_embd;
+    MIO_TRACE(b, 0);
     const Smem s = carve(smem, K);
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    constexpr int NG = LM_ROWS / (NWAVE * 4);
-    const int rbase = blockIdx.x * LM_ROWS + wave * (LM_ROWS / NWAVE);
-    int rows[NG][4];
-#pragma unroll
-    for (int g = 0; g < NG; ++g)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) rows[g][r] = rbase + g * 4 + r < lm.rows ? rbase + g * 4 + r : -1;
-    // lm_head rows are one pass at K <= 2048: load two groups ahead of the prologue
-    Frag f0[4][P], f1[4][P];
-    preload<4, P>(lm, rows[0], f0);
-    preload<4, P>(lm, rows[1], f1);
-    act_from_global(b.act, K, s);
+    XRegs<NP> xr;
+    load_x(b.x, norm_w, K, xr);
     const int step = b.st->step;
+    int lo, hi;
+    wave_range(lm.rows, lo, hi);
+    Frag cur[Cfg<NP>::U];
+    load_group<T, NP, 1>(lm, lm, lo, (hi - lo) * NP, 0, cur);
+    MIO_TRACE(b, 1);
+    rmsnorm_quant(xr, K, d.eps, T != 8, s);
+    MIO_TRACE(b, 2);
+    const int lane = threadIdx.x & 63;
+    float r0 = -INFINITY, r1 = -INFINITY;
+    stream_rows<T, NP, 1>(lm, lm, lo, hi, cur, true, s.a, [&](int row, float v, float) {
+        const int k = row - lo;
+        r0 = lane == k ? v : r0;
+        r1 = lane + 64 == k ? v : r1;
+    });
+    MIO_TRACE(b, 3);
     const uint64_t seed = ((uint64_t)sc.seed_hi << 32) | sc.seed_lo;
     float best = -INFINITY;
     int bi = INT_MAX;
 #pragma unroll
-    for (int g = 0; g < NG; ++g) {
-        float o[4];
-        if (g % 2 == 0) {
-            finish_rows<4, P>(lm, rows[g], f0, s.a, o);
-            if (g + 2 < NG) preload<4, P>(lm, rows[g + 2], f0);
-        } else {
-            finish_rows<4, P>(lm, rows[g], f1, s.a, o);
-            if (g + 2 < NG) preload<4, P>(lm, rows[g + 2], f1);
-        }
-        if (lane == 0) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int row = rows[g][r];
-                if (row < 0) continue;
-                b.logits[row] = o[r];
-                if (row >= sc.lo && row < sc.hi) {
-                    const float v = sc.temp > 0.0f ? o[r] / sc.temp + gumbel(seed, step, row) : o[r];
-                    if (v > best || (v == best && row < bi)) best = v, bi = row;
-                }
+    for (int h = 0; h < 2; ++h) {
+        const int row = lo + lane + 64 * h;
+        const float v = h ? r1 : r0;
+        if (row < hi) {
+            b.logits[row] = v;
+            if (row >= sc.lo && row < sc.hi) {
+                const float t = sc.temp > 0.0f ? v / sc.temp + gumbel(seed, step, row) : v;
+                if (t > best || (t == best && row < bi)) best = t, bi = row;
             }
         }
     }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        const float ov = __shfl_xor(best, o);
+        const int oi = __shfl_xor(bi, o);
+        if (ov > best || (ov == best && oi < bi)) best = ov, bi = oi;
+    }
+    const int wave = threadIdx.x >> 6;
     if (lane == 0) bs_[wave] = best, bi_[wave] = bi;
     __syncthreads();
     if (threadIdx.x == 0) {
-        for (int w = 1; w < NWAVE; ++w)
+        for (int w = 1; w < MW; ++w)
             if (bs_[w] > best || (bs_[w] == best && bi_[w] < bi)) best = bs_[w], bi = bi_[w];
         b.smp[2 * blockIdx.x] = best;
         b.smp[2 * blockIdx.x + 1] = __int_as_float(bi);
     }
+    MIO_TRACE(b, 15);
 }
 
+// ------------------------------------------------------------------ attention
+// One 256-thread workgroup per (chunk of ATT_CHUNK = 128 positions, kv head): q/k RMSNorm
+// (qwen3) + RoPE + f16 rounding, the chunk owning `pos` appends the new k/v row to the F16
+// cache, then an online softmax over the chunk for the G q heads sharing the kv head. Its
+// partial record {O[HD], m, l} per q head is merged with the other chunks' in the prologue
+// of k_attn_out (the launch-boundary reduce: no extra launch, no in-kernel hand-off).
+// all-reduce over aligned groups of LP (8 or 16) lanes, by DPP; every lane of a group gets
+// the bitwise-same sum
+template <int LP>
+__device__ __forceinline__ float group_sum(float v) {
+    v += dpp_f<0xB1>(v);   // quad_perm [1,0,3,2]
+    v += dpp_f<0x4E>(v);   // quad_perm [2,3,0,1]
+    v += dpp_f<0x141>(v);  // row_half_mirror
+    if constexpr (LP == 16) v += dpp_f<0x140>(v);  // row_mirror
+    return v;
+}
+
+template <int HD, int G>
+__global__ __launch_bounds__(NT) void k_attention(LlmDims d, const float *q_norm, const float *k_norm,
+                                                  _Float16 *kc, _Float16 *vc, LlmBuffers b) {
+    constexpr int LP = HD / 8;
+    constexpr int NS = NT / LP;
+    constexpr int IT = ATT_CHUNK / NS;
+    constexpr int REC = part_rec(HD);
+    constexpr int PER = HD / 64;
+    typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+    __shared__ float qs[G][HD];
+    __shared__ float knew[HD], vnew[HD];
+    __shared__ float wres[NWAVE][G][HD + 2];
+
+    MIO_TRACE(b, 0);
+    const int kvh = blockIdx.y, ch = blockIdx.x;
+    const int pos = b.st->pos;
+    const int t0 = ch * ATT_CHUNK;
+    if (t0 > pos) return;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int lp = lane % LP, sl = tid / LP;
+    const float2 *rope = b.rope + (size_t)pos * (HD / 2);
+    const _Float16 *kbase = kc + (size_t)kvh * d.n_ctx * HD;
+    const _Float16 *vbase = vc + (size_t)kvh * d.n_ctx * HD;
+
+    // K/V rows of this slot first (row `pos` is never consumed from the cache)
+    h8 kr[IT], vr[IT];
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+        const int t = min(t0 + sl + NS * it, pos);
+        kr[it] = *reinterpret_cast<const h8 *>(kbase + (size_t)t * HD + lp * 8);
+        vr[it] = *reinterpret_cast<const h8 *>(vbase + (size_t)t * HD + lp * 8);
+    }
+    // q heads (waves 0..G-1, strided) and, for the chunk owning `pos`, the new k/v row
+    const bool owner = pos < t0 + ATT_CHUNK;
+    for (int hh = wave; hh < G + (owner ? 1 : 0); hh += NWAVE) {
+        const bool isk = hh == G;
+        const float *src = isk ? b.qkv + (size_t)(d.n_head + kvh) * HD : b.qkv + (size_t)(kvh * G + hh) * HD;
+        const float *vsrc = b.qkv + (size_t)(d.n_head + d.n_kv + kvh) * HD;
+        const float *nw = isk ? k_norm : q_norm;
+        float v[PER], w[PER], vv[PER];
+        float2 cs[PER];
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int p = lane + 64 * i;
+            v[i] = src[p];
+            w[i] = d.qk_norm ? nw[p] : 1.0f;
+            vv[i] = isk ? vsrc[p] : 0.0f;
+            cs[i] = p < HD / 2 ? rope[p] : make_float2(0.0f, 0.0f);
+        }
+        if (d.qk_norm) {
+            double ss = 0.0;
+#pragma unroll
+            for (int i = 0; i < PER; ++i) ss += (double)(v[i] * v[i]);
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) ss += __shfl_xor(ss, o);
+            const float mean = (float)(ss / HD);
+            const float scale = 1.0f / sqrtf(mean + d.eps);
+#pragma unroll
+            for (int i = 0; i < PER; ++i) {
+                const float t = v[i] * scale;
+                v[i] = t * w[i];
+            }
+        }
+        float *dst = isk ? knew : qs[hh];
+#pragma unroll
+        for (int i = 0; i < PER; ++i) dst[lane + 64 * i] = v[i];
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        float o0[PER], o1[PER];
+        int i0s[PER], i1s[PER];
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int p = lane + 64 * i;
+            i0s[i] = -1;
+            if (p < HD / 2) {
+                const int i0 = d.neox ? p : 2 * p, i1 = d.neox ? p + HD / 2 : 2 * p + 1;
+                const float x0 = dst[i0], x1 = dst[i1];
+                o0[i] = x0 * cs[i].x - x1 * cs[i].y;
+                o1[i] = x0 * cs[i].y + x1 * cs[i].x;
+                i0s[i] = i0, i1s[i] = i1;
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+#pragma unroll
+        for (int i = 0; i < PER; ++i)
+            if (i0s[i] >= 0) {
+                dst[i0s[i]] = f16r(o0[i]);
+                dst[i1s[i]] = f16r(o1[i]);
+            }
+        if (isk) {
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            _Float16 *kd = kc + ((size_t)kvh * d.n_ctx + pos) * HD;
+            _Float16 *vd = vc + ((size_t)kvh * d.n_ctx + pos) * HD;
+#pragma unroll
+            for (int i = 0; i < PER; ++i) {
+                const int p = lane + 64 * i;
+                const float vr16 = f16r(vv[i]);
+                vnew[p] = vr16;
+                kd[p] = (_Float16)knew[p];
+                vd[p] = (_Float16)vr16;
+            }
+        }
+    }
+    __syncthreads();
+    MIO_TRACE(b, 2);
+
+    float qv[G][8];
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) qv[g][i] = qs[g][lp * 8 + i];
+    float m[G], l[G], acc[G][8];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        m[g] = -INFINITY, l[g] = 0.0f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[g][i] = 0.0f;
+    }
+    // online softmax over this slot's positions (ggml soft_max semantics up to order)
+    auto update = [&](const float (&kf)[8], const float (&vf)[8], bool valid) {
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            float sdot = 0.0f;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) sdot = fmaf(qv[g][i], kf[i], sdot);
+            sdot = group_sum<LP>(sdot);
+            const float sc = valid ? sdot * d.scale : -INFINITY;
+            const float mn = fmaxf(m[g], sc);
+            const float c = m[g] == mn ? 1.0f : expf(m[g] - mn);
+            const float p = valid ? expf(sc - mn) : 0.0f;
+            l[g] = l[g] * c + p;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) acc[g][i] = acc[g][i] * c + p * vf[i];
+            m[g] = mn;
+        }
+    };
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+        const int t = t0 + sl + NS * it;
+        float kf[8], vf[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) kf[i] = (float)kr[it][i], vf[i] = (float)vr[it][i];
+        update(kf, vf, t < pos);
+    }
+    if (owner && sl == (pos - t0) % NS) {
+        float kf[8], vf[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) kf[i] = knew[lp * 8 + i], vf[i] = vnew[lp * 8 + i];
+        update(kf, vf, true);
+    }
+    MIO_TRACE(b, 3);
+    // merge the wave's slots (lane stride LP)
+#pragma unroll
+    for (int o = LP; o < 64; o <<= 1) {
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const float m2 = __shfl_xor(m[g], o), l2 = __shfl_xor(l[g], o);
+            const float mn = fmaxf(m[g], m2);
+            const float c1 = m[g] == -INFINITY ? 0.0f : expf(m[g] - mn);
+            const float c2 = m2 == -INFINITY ? 0.0f : expf(m2 - mn);
+            l[g] = l[g] * c1 + l2 * c2;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const float a2 = __shfl_xor(acc[g][i], o);
+                acc[g][i] = acc[g][i] * c1 + a2 * c2;
+            }
+            m[g] = mn;
+        }
+    }
+    if (lane < LP) {
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) wres[wave][g][lp * 8 + i] = acc[g][i];
+            if (lp == 0) wres[wave][g][HD] = m[g], wres[wave][g][HD + 1] = l[g];
+        }
+    }
+    __syncthreads();
+    // merge the 4 waves -> this chunk's partial record per q head
+    for (int e = tid; e < G * HD; e += NT) {
+        const int g = e / HD, dd = e - g * HD;
+        float M = -INFINITY;
+#pragma unroll
+        for (int w = 0; w < NWAVE; ++w) M = fmaxf(M, wres[w][g][HD]);
+        float L = 0.0f, O = 0.0f;
+#pragma unroll
+        for (int w = 0; w < NWAVE; ++w) {
+            const float mw = wres[w][g][HD];
+            const float c = mw == -INFINITY ? 0.0f : expf(mw - M);
+            L += c * wres[w][g][HD + 1];
+            O += c * wres[w][g][dd];
+        }
+        float *dst = b.part + ((size_t)(kvh * G + g) * d.max_splits + ch) * REC;
+        dst[dd] = O;
+        if (dd == 0) dst[HD] = M, dst[HD + 1] = L;
+    }
+    MIO_TRACE(b, 15);
+}
+
+template <int HD>
+void launch_attention(int G, dim3 grid, hipStream_t s, const LlmDims &d, const float *qn, const float *kn,
+                      _Float16 *kc, _Float16 *vc, const LlmBuffers &b) {
+    switch (G) {
+        case 1: hipLaunchKernelGGL((k_attention<HD, 1>), grid, dim3(NT), 0, s, d, qn, kn, kc, vc, b); break;
+        case 2: hipLaunchKernelGGL((k_attention<HD, 2>), grid, dim3(NT), 0, s, d, qn, kn, kc, vc, b); break;
+        case 3: hipLaunchKernelGGL((k_attention<HD, 3>), grid, dim3(NT), 0, s, d, qn, kn, kc, vc, b); break;
+        case 4: hipLaunchKernelGGL((k_attention<HD, 4>), grid, dim3(NT), 0, s, d, qn, kn, kc, vc, b); break;
+        case 8: hipLaunchKernelGGL((k_attention<HD, 8>), grid, dim3(NT), 0, s, d, qn, kn, kc, vc, b); break;
+        default: break;
+    }
+}
+
+// ------------------------------------------------------------------ sampler / embedding
 __device__ float dequant_elem(const QMat &W, int row, int e) {
     if (W.type == 12) {
         const int nsb = W.k >> 8, sb = e >> 8, c = e & 255, j = c >> 6, w = c & 63, hi = w >> 5, l = w & 31;
         const uint8_t q = W.p0[(size_t)row * (W.k / 2) + sb * 128 + 32 * j + l];
-        const uint4 hd = ld16(W.p1 + ((size_t)row * nsb + sb) * 16);
-        int sc, m;
-        scale_min_k4(2 * j + hi, hd, sc, m);
-        const float d1 = h2f(hd.x & 0xFFFF) * sc, m1 = h2f(hd.x >> 16) * m;
+        const uint8_t *hd = W.p1 + ((size_t)row * nsb + sb) * 16;
+        const uint32_t F = (uint32_t)hd[4 + 3 * j] | ((uint32_t)hd[5 + 3 * j] << 8) | ((uint32_t)hd[6 + 3 * j] << 16);
+        const int sc = (F >> (12 * hi)) & 63, m = (F >> (12 * hi + 6)) & 63;
+        const float d1 = h2f(hd[0] | (hd[1] << 8)) * sc, m1 = h2f(hd[2] | (hd[3] << 8)) * m;
         return d1 * (float)(hi ? (q >> 4) : (q & 0xF)) - m1;
     } else if (W.type == 14) {
         const int nsb = W.k >> 8, sb = e >> 8, c = e & 255, n = c >> 7, w = c & 127, g = w >> 5, l = w & 31;
         const uint8_t ql = W.p0[(size_t)row * (W.k / 2) + sb * 128 + 64 * n + l + 32 * (g & 1)];
         const uint8_t qh = W.p1[(size_t)row * (W.k / 4) + sb * 64 + 32 * n + l];
         const int q = (int)((g < 2 ? (ql & 0xF) : (ql >> 4)) | (((qh >> (2 * g)) & 3) << 4)) - 32;
-        const int sc = ((const int8_t *)W.p2)[(size_t)row * (W.k / 16) + sb * 16 + (c >> 4)];
+        const int is = c >> 4, sn = is >> 3, sw = is & 7;
+        const int sc = ((const int8_t *)W.p2)[(size_t)row * (W.k / 16) + sb * 16 + 2 * (4 * sn + (sw & 3)) + (sw >> 2)];
         const float dd = h2f(((const uint16_t *)W.p3)[(size_t)row * nsb + sb]);
         return dd * (float)sc * (float)q;
     } else {
@@ -876,38 +1105,57 @@ __device__ float dequant_elem(const QMat &W, int row, int e) {
     }
 }
 
-__global__ __launch_bounds__(NT) void k_sample(LlmDims d, SampleCfg sc, QMat emb, int nblk, LlmBuffers b) {
-    __shared__ float bs_[NT];
-    __shared__ int bi_[NT];
+constexpr int ST = 1024;  // sampler / embedding threads (n_embd <= 4 * ST)
+
+__device__ inline void embed_row(const QMat &emb, int tok, int n, float *x) {
+    float v[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int e = threadIdx.x + i * ST;
+        v[i] = e < n ? dequant_elem(emb, tok, e) : 0.0f;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int e = threadIdx.x + i * ST;
+        if (e < n) x[e] = v[i];
+    }
+}
+
+__global__ __launch_bounds__(ST) void k_sample(LlmDims d, SampleCfg sc, QMat emb, int nblk, LlmBuffers b) {
+    __shared__ float bs_[ST / 64];
+    __shared__ int bi_[ST / 64];
     __shared__ int tok_s;
-    const int tid = threadIdx.x;
+    MIO_TRACE(b, 0);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int step = b.st->step;
     float best = -INFINITY;
     int bi = INT_MAX;
-    for (int i = tid; i < nblk; i += NT) {
+    for (int i = tid; i < nblk; i += ST) {
         const float v = b.smp[2 * i];
         const int ix = __float_as_int(b.smp[2 * i + 1]);
         if (v > best || (v == best && ix < bi)) best = v, bi = ix;
     }
-    bs_[tid] = best, bi_[tid] = bi;
-    __syncthreads();
-    for (int o = NT / 2; o > 0; o >>= 1) {
-        if (tid < o) {
-            const float v = bs_[tid + o];
-            const int ix = bi_[tid + o];
-            if (v > bs_[tid] || (v == bs_[tid] && ix < bi_[tid])) bs_[tid] = v, bi_[tid] = ix;
-        }
-        __syncthreads();
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        const float v = __shfl_xor(best, o);
+        const int ix = __shfl_xor(bi, o);
+        if (v > best || (v == best && ix < bi)) best = v, bi = ix;
     }
+    if (lane == 0) bs_[wave] = best, bi_[wave] = bi;
+    __syncthreads();
     if (tid == 0) {
-        int tok = bi_[0];
+        for (int w = 1; w < ST / 64; ++w)
+            if (bs_[w] > best || (bs_[w] == best && bi_[w] < bi)) best = bs_[w], bi = bi_[w];
+        int tok = bi;
         if (tok == INT_MAX) tok = sc.lo;
         if (sc.force && step < sc.n_force && sc.force[step] >= 0) tok = sc.force[step];
         tok_s = tok;
     }
     __syncthreads();
     const int tok = tok_s;
-    for (int e = tid; e < d.n_embd; e += NT) b.x[e] = dequant_elem(emb, tok, e);
+    MIO_TRACE(b, 1);
+    embed_row(emb, tok, d.n_embd, b.x);
+    MIO_TRACE(b, 15);
     if (tid == 0) {
         if (step < sc.max_steps) sc.out_tokens[step] = tok;
         if (tok == sc.eos0 || tok == sc.eos1) b.st->done = 1;
@@ -917,105 +1165,117 @@ __global__ __launch_bounds__(NT) void k_sample(LlmDims d, SampleCfg sc, QMat emb
     }
 }
 
-__global__ void k_embed(LlmDims d, QMat emb, LlmBuffers b) {
-    const int tok = b.st->token;
-    for (int e = threadIdx.x; e < d.n_embd; e += blockDim.x) b.x[e] = dequant_elem(emb, tok, e);
+__global__ __launch_bounds__(ST) void k_embed(LlmDims d, QMat emb, LlmBuffers b) {
+    embed_row(emb, b.st->token, d.n_embd, b.x);
 }
 
 }  // namespace
 
-int lm_head_blocks(const LlmDims &d) { return (d.n_vocab + LM_ROWS - 1) / LM_ROWS; }
+// ------------------------------------------------------------------ host launchers
+int pick_np(int K) { return K <= 2048 ? 1 : (K <= 6144 ? 3 : 6); }
+
+// at least MW rows per workgroup (every wave owns >= 1 row), at most one workgroup per CU
+int matvec_grid(const LlmDims &d, int rows) {
+    int g = rows / MW;
+    g = g < d.n_wg ? g : d.n_wg;
+    return g < 2 ? 2 : g;
+}
+
+int lm_head_blocks(const LlmDims &d) { return matvec_grid(d, d.n_vocab); }
+
+size_t matvec_lds(int K) { return smem_bytes(K); }
+
 
 void launch_embed_token(const LlmDims &d, const QMat &tok_embd, const LlmBuffers &b, hipStream_t s) {
-    hipLaunchKernelGGL(k_embed, dim3(1), dim3(NT), 0, s, d, tok_embd, b);
+    hipLaunchKernelGGL(k_embed, dim3(1), dim3(ST), 0, s, d, tok_embd, b);
 }
 
-inline int pick_p(int K) { return (K + 2047) / 2048 <= 1 ? 1 : 3; }
-inline int pick_xv(int K) {
-    const int v = (K + 1023) / 1024;
-    return v <= 1 ? 1 : (v <= 2 ? 2 : (v <= 6 ? 6 : 12));
-}
-
-// Calls F.template operator()<P, XV>() with P = passes preloaded, XV = float4 x-registers.
+// Calls f.template operator()<NP, T>() for the matrix's pass count and weight type.
 template <class F>
-void dispatch_px(int K, F &&f) {
-    const int p = pick_p(K), xv = pick_xv(K);
-#define PX(PP, XX) \
-    if (p == PP && xv == XX) return f.template operator()<PP, XX>();
-    PX(1, 1) PX(1, 2) PX(1, 6) PX(1, 12) PX(3, 1) PX(3, 2) PX(3, 6) PX(3, 12)
-#undef PX
+void dispatch_nt(int K, int type, F &&f) {
+    const int np = pick_np(K);
+#define NT_CASE(NPV, TV) \
+    if (np == NPV && type == TV) return f.template operator()<NPV, TV>();
+    NT_CASE(1, 8) NT_CASE(1, 12) NT_CASE(1, 14) NT_CASE(3, 8) NT_CASE(3, 12) NT_CASE(3, 14)
+    NT_CASE(6, 8) NT_CASE(6, 12) NT_CASE(6, 14)
+#undef NT_CASE
 }
 
-// Launch one kernel of the step: which = 0 attn_in, 1 attention, 2 attn_out (with its
-// combine kernel in front), 3 ffn_in, 4 ffn_down (layer il), 5 final_norm, 6 lm_head,
-// 7 sample.
+// Launch one kernel of the step: which = 0 attn_in, 1 attention (+ split merge),
+// 2 attn_out, 3 ffn_in, 4 ffn_down (layer il), 5 (unused: the final norm is fused into
+// lm_head), 6 lm_head, 7 sample.
 void launch_step_kernel(int which, const LlmDims &d, const LayerW *layers, int il, _Float16 *kcache,
                         _Float16 *vcache, const float *out_norm, const QMat &lm, const QMat &tok_embd,
                         const LlmBuffers &b, const SampleCfg &sc, hipStream_t s) {
     const size_t layer_kv = (size_t)d.n_kv * d.n_ctx * d.hd;
     const int G = d.n_head / d.n_kv;
-    const int ns = NT / (d.hd / 8);
-    const size_t att_lds = (size_t)ns * G * (d.hd + 2) * 4;
-    const int nblk = lm_head_blocks(d);
     switch (which) {
         case 0: {
             const LayerW &L = layers[il];
-            const int qkv_rows = L.wq.rows + L.wk.rows + L.wv.rows;
-            dispatch_px(d.n_embd, [&]<int P, int XV>() {
-                hipLaunchKernelGGL((k_attn_in<P, XV>), dim3((qkv_rows + QKV_ROWS - 1) / QKV_ROWS), dim3(NT),
-                                   smem_bytes(d.n_embd), s, d, L.attn_norm, L.wq, L.wk, L.wv, b);
+            const int rows = L.wq.rows + L.wk.rows + L.wv.rows, qk = L.wq.rows + L.wk.rows;
+            const int G = matvec_grid(d, rows);
+            int g_qk = (G * qk + rows / 2) / rows;
+            g_qk = g_qk < 1 ? 1 : (g_qk > G - 1 ? G - 1 : g_qk);
+            const dim3 grid(G);
+            const size_t lds = smem_bytes(d.n_embd);
+            dispatch_nt(d.n_embd, L.wq.type, [&]<int NP, int TQ>() {
+                auto go = [&]<int TV>() {
+                    hipLaunchKernelGGL((k_attn_in<NP, TQ, TV>), grid, dim3(MT), lds, s, d, L.attn_norm, L.wq, L.wk,
+                                       L.wv, g_qk, b);
+                };
+                if constexpr (TQ == 8) {
+                    go.template operator()<8>();
+                } else {
+                    if (L.wv.type == 14)
+                        go.template operator()<14>();
+                    else
+                        go.template operator()<12>();
+                }
             });
             break;
         }
         case 1: {
             const LayerW &L = layers[il];
+            const dim3 grid(d.max_splits, d.n_kv);
             if (d.hd == 128)
-                launch_attention<128>(G, dim3(d.max_splits, d.n_kv), att_lds, s, d, L.q_norm, L.k_norm,
-                                      kcache + il * layer_kv, vcache + il * layer_kv, b);
+                launch_attention<128>(G, grid, s, d, L.q_norm, L.k_norm, kcache + il * layer_kv, vcache + il * layer_kv, b);
             else
-                launch_attention<64>(G, dim3(d.max_splits, d.n_kv), att_lds, s, d, L.q_norm, L.k_norm,
-                                     kcache + il * layer_kv, vcache + il * layer_kv, b);
+                launch_attention<64>(G, grid, s, d, L.q_norm, L.k_norm, kcache + il * layer_kv, vcache + il * layer_kv, b);
             break;
         }
         case 2: {
             const LayerW &L = layers[il];
-            const int K = d.n_head * d.hd;
-            hipLaunchKernelGGL(k_attn_combine, dim3((K + NT - 1) / NT), dim3(NT), 0, s, d, L.wo.type != 8 ? 1 : 0, b);
-            dispatch_px(K, [&]<int P, int XV>() {
-                hipLaunchKernelGGL((k_attn_out<P, XV>), dim3((L.wo.rows + RES_ROWS - 1) / RES_ROWS), dim3(NT),
-                                   smem_bytes(K), s, d, L.wo, b);
+            dispatch_nt(L.wo.k, L.wo.type, [&]<int NP, int T>() {
+                hipLaunchKernelGGL((k_attn_out<NP, T>), dim3(matvec_grid(d, L.wo.rows)), dim3(MT), smem_bytes(L.wo.k),
+                                   s, d, L.wo, b);
             });
             break;
         }
         case 3: {
             const LayerW &L = layers[il];
-            dispatch_px(d.n_embd, [&]<int P, int XV>() {
-                hipLaunchKernelGGL((k_ffn_in<P, XV>), dim3((L.gate.rows + FFN_PAIRS - 1) / FFN_PAIRS), dim3(NT),
-                                   smem_bytes(d.n_embd), s, d, L.ffn_norm, L.gate, L.up, b);
+            dispatch_nt(d.n_embd, L.gate.type, [&]<int NP, int T>() {
+                hipLaunchKernelGGL((k_ffn_in<NP, T>), dim3(matvec_grid(d, L.gate.rows)), dim3(MT), smem_bytes(d.n_embd),
+                                   s, d, L.ffn_norm, L.gate, L.up, b);
             });
             break;
         }
         case 4: {
             const LayerW &L = layers[il];
-            dispatch_px(d.n_ff, [&]<int P, int XV>() {
-                hipLaunchKernelGGL((k_ffn_down<P, XV>), dim3((L.down.rows + RES_ROWS - 1) / RES_ROWS), dim3(NT),
-                                   smem_bytes(d.n_ff), s, d, L.down, b);
+            dispatch_nt(L.down.k, L.down.type, [&]<int NP, int T>() {
+                hipLaunchKernelGGL((k_ffn_down<NP, T>), dim3(matvec_grid(d, L.down.rows)), dim3(MT),
+                                   smem_bytes(L.down.k), s, d, L.down, b);
             });
             break;
         }
-        case 5:
-            dispatch_px(d.n_embd, [&]<int P, int XV>() {
-                hipLaunchKernelGGL((k_final_norm<P, XV>), dim3(1), dim3(NT), smem_bytes(d.n_embd), s, d, out_norm,
-                                   lm.type != 8 ? 1 : 0, b);
+        case 6:
+            dispatch_nt(d.n_embd, lm.type, [&]<int NP, int T>() {
+                hipLaunchKernelGGL((k_lm_head<NP, T>), dim3(lm_head_blocks(d)), dim3(MT), smem_bytes(d.n_embd), s, d,
+                                   out_norm, lm, sc, b);
             });
             break;
-        case 6:
-            if (pick_p(d.n_embd) == 1)
-                hipLaunchKernelGGL(k_lm_head<1>, dim3(nblk), dim3(NT), smem_bytes(d.n_embd), s, d, lm, sc, b);
-            else
-                hipLaunchKernelGGL(k_lm_head<3>, dim3(nblk), dim3(NT), smem_bytes(d.n_embd), s, d, lm, sc, b);
+        case 7:
+            hipLaunchKernelGGL(k_sample, dim3(1), dim3(ST), 0, s, d, sc, tok_embd, lm_head_blocks(d), b);
             break;
-        case 7: hipLaunchKernelGGL(k_sample, dim3(1), dim3(NT), 0, s, d, sc, tok_embd, nblk, b); break;
         default: break;
     }
 }
@@ -1025,42 +1285,36 @@ void launch_decode_step(const LlmDims &d, const LayerW *layers, int n_layer, _Fl
                         const LlmBuffers &b, const SampleCfg &sc, hipStream_t s) {
     for (int il = 0; il < n_layer; ++il)
         for (int k = 0; k < 5; ++k) launch_step_kernel(k, d, layers, il, kcache, vcache, out_norm, lm, tok_embd, b, sc, s);
-    for (int k = 5; k < 8; ++k) launch_step_kernel(k, d, layers, 0, kcache, vcache, out_norm, lm, tok_embd, b, sc, s);
+    launch_step_kernel(6, d, layers, 0, kcache, vcache, out_norm, lm, tok_embd, b, sc, s);
+    launch_step_kernel(7, d, layers, 0, kcache, vcache, out_norm, lm, tok_embd, b, sc, s);
 }
 
-}  // namespace mio
-
 // ------------------------------------------------------------------ parity entry point
-namespace mio {
 namespace {
-template <int P, int XV>
-__global__ __launch_bounds__(NT) void k_debug_matvec(QMat W, const float *x, float *y) {
+template <int NP, int T>
+__global__ __launch_bounds__(MT) void k_debug_matvec(QMat W, const float *x, float *y) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int K = W.k;
     const Smem s = carve(smem, K);
-    XRegs<XV> xr;
-    load_x(x, K, xr);
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    int rows[2];
-    const int r0 = blockIdx.x * RES_ROWS + wave * 2;
-    rows[0] = r0 < W.rows ? r0 : -1;
-    rows[1] = r0 + 1 < W.rows ? r0 + 1 : -1;
-    Frag pre[2][P];
-    preload<2, P>(W, rows, pre);
-    plain_quant(xr, K, W.type != 8, s);
-    float o[2];
-    finish_rows<2, P>(W, rows, pre, s.a, o);
-    if (lane == 0) {
-        if (rows[0] >= 0) y[rows[0]] = o[0];
-        if (rows[1] >= 0) y[rows[1]] = o[1];
-    }
+    XRegs<NP> xr;
+    load_x(x, nullptr, K, xr);
+    int lo, hi;
+    wave_range(W.rows, lo, hi);
+    Frag cur[Cfg<NP>::U];
+    load_group<T, NP, 1>(W, W, lo, (hi - lo) * NP, 0, cur);
+    plain_quant(xr, K, T != 8, s);
+    stream_rows<T, NP, 1>(W, W, lo, hi, cur, true, s.a, [&](int row, float v, float) {
+        if ((threadIdx.x & 63) == 0) y[row] = v;
+    });
 }
 }  // namespace
 
-void launch_debug_matvec(const QMat &W, const float *x, float *y, hipStream_t s) {
-    dispatch_px(W.k, [&]<int P, int XV>() {
-        hipLaunchKernelGGL((k_debug_matvec<P, XV>), dim3((W.rows + RES_ROWS - 1) / RES_ROWS), dim3(NT), smem_bytes(W.k),
-                           s, W, x, y);
+void launch_debug_matvec(const QMat &W, const float *x, float *y, int n_wg, hipStream_t s) {
+    LlmDims d{};
+    d.n_wg = n_wg;
+    dispatch_nt(W.k, W.type, [&]<int NP, int T>() {
+        hipLaunchKernelGGL((k_debug_matvec<NP, T>), dim3(matvec_grid(d, W.rows)), dim3(MT), smem_bytes(W.k), s, W, x,
+                           y);
     });
 }
 }  // namespace mio

@@ -236,12 +236,14 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
     D.qk_norm = arch == "qwen3" ? 1 : 0;
     D.n_ctx = n_ctx;
     D.scale = 1.0f / sqrtf((float)D.hd);
-    D.split = 64;
+    D.split = mio::kAttChunk;
     D.max_splits = (n_ctx + D.split - 1) / D.split;
+    D.n_wg = d->n_cu > 0 ? d->n_cu : 256;
+    MIO_REQUIRE(n_ctx <= 32768, MIO_ERR_UNSUPPORTED, "llm_load: n_ctx %d > 32768", n_ctx);
     const int G = D.n_kv ? D.n_head / D.n_kv : 0;
     if (D.n_embd <= 0 || m->n_layer <= 0 || D.n_head <= 0 || D.n_kv <= 0 || D.n_head % D.n_kv ||
         !(G == 1 || G == 2 || G == 3 || G == 4 || G == 8) || !(D.hd == 64 || D.hd == 128) ||
-        D.n_embd % 256 != 0 && D.n_embd % 32 != 0) {
+        (D.n_embd % 256 != 0 && D.n_embd % 32 != 0)) {
         mio::set_error("llm_load: unsupported dims (n_embd %d, heads %d/%d, head_dim %d)", D.n_embd, D.n_head,
                        D.n_kv, D.hd);
         return fail(MIO_ERR_UNSUPPORTED);
@@ -252,6 +254,8 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
         return fail(MIO_ERR_FORMAT);
     }
     D.n_vocab = (int)te->ne[1];
+    MIO_REQUIRE(D.n_vocab <= 128 * 8 * D.n_wg, MIO_ERR_UNSUPPORTED, "llm_load: vocab %d > %d", D.n_vocab,
+                128 * 8 * D.n_wg);
     if (!upload_qmat(m, te, m->tok)) return fail(MIO_ERR_FORMAT);
     const uint64_t embd_bytes = te->nbytes;
     m->weight_bytes -= embd_bytes;  // one embedding row per step, not the whole table
@@ -283,7 +287,9 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
             return fail(MIO_ERR_FORMAT);
         if (L.wq.rows != D.n_head * D.hd || L.wk.rows != D.n_kv * D.hd || L.wv.rows != D.n_kv * D.hd ||
             L.gate.rows != D.n_ff || L.down.k != D.n_ff || fam(L.wq.type) != fam(L.wk.type) ||
-            fam(L.wq.type) != fam(L.wv.type) || fam(L.gate.type) != fam(L.up.type)) {
+            fam(L.wq.type) != fam(L.wv.type) || L.wq.type != L.wk.type || L.gate.type != L.up.type ||
+            D.n_ff > 12288 ||
+            D.n_embd > 64 * 8 * D.n_wg) {
             mio::set_error("llm_load: layer %d shapes / quant families not supported", i);
             return fail(MIO_ERR_UNSUPPORTED);
         }
@@ -296,11 +302,9 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
     m->vc = dalloc<_Float16>(m, kv);
     m->buf.x = dalloc<float>(m, D.n_embd);
     m->buf.qkv = dalloc<float>(m, qkv);
-    m->buf.part = dalloc<float>(m, (size_t)D.n_head * D.max_splits * (D.hd + 2));
     m->buf.h = dalloc<float>(m, D.n_ff);
     m->buf.logits = dalloc<float>(m, D.n_vocab);
-    m->buf.act = dalloc<float>(m, D.n_embd * 2 + 1024);
-    m->buf.act2 = dalloc<float>(m, D.n_head * D.hd * 2 + 1024);
+    m->buf.part = dalloc<float>(m, (size_t)D.n_head * D.max_splits * (D.hd + 4));
     m->buf.smp = dalloc<float>(m, 2 * mio::lm_head_blocks(D) + 16);
     m->buf.st = dalloc<mio::StepState>(m, 1);
     m->max_steps = n_ctx;
@@ -317,8 +321,8 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
         }
     }
     float2 *dr = dalloc<float2>(m, rope.size());
-    if (!m->kc || !m->vc || !m->buf.x || !m->buf.qkv || !m->buf.part || !m->buf.h || !m->buf.logits ||
-        !m->buf.act || !m->buf.smp || !m->buf.st || !m->d_tokens || !m->d_force || !dr) {
+    if (!m->kc || !m->vc || !m->buf.x || !m->buf.qkv || !m->buf.h || !m->buf.logits ||
+        !m->buf.part || !m->buf.smp || !m->buf.st || !m->d_tokens || !m->d_force || !dr) {
         mio::set_error("llm_load: device allocation failed");
         return fail(MIO_ERR_OOM);
     }
@@ -420,7 +424,7 @@ extern "C" int mio_hip_debug_matvec(mio_hip_device *d, uint32_t type, const void
     hipMemcpy(dw, host.data(), L.bytes, hipMemcpyHostToDevice);
     hipMemcpy(dx, x, (size_t)k * 4, hipMemcpyHostToDevice);
     mio::QMat q{(int)type, rows, k, dw + L.off[0], dw + L.off[1], dw + L.off[2], dw + L.off[3]};
-    mio::launch_debug_matvec(q, dx, dy, d->stream);
+    mio::launch_debug_matvec(q, dx, dy, d->n_cu > 0 ? d->n_cu : 256, d->stream);
     hipError_t e = hipStreamSynchronize(d->stream);
     if (e == hipSuccess) e = hipMemcpy(y, dy, (size_t)rows * 4, hipMemcpyDeviceToHost);
     hipFree(dw), hipFree(dx), hipFree(dy);
@@ -481,5 +485,30 @@ extern "C" int mio_hip_llm_time_kernel(mio_hip_llm *m, int which, int iters, flo
     hipEventDestroy(e0), hipEventDestroy(e1);
     *avg_ms = ms / iters;
     *bytes = b;
+    return MIO_OK;
+}
+
+// Runs kernel `which` once (after a warm launch) with checkpoint tracing on; out[0..31]:
+// s_memtime at checkpoints 0..15 of workgroup 0 / thread 0, s_memrealtime (100 MHz) at
+// checkpoints 0 and 15 in out[16] / out[31]. Diagnostic only.
+extern "C" int mio_hip_llm_trace_kernel(mio_hip_llm *m, int which, uint64_t *out) {
+    MIO_REQUIRE(m && out && m->graph, MIO_ERR_INVALID, "llm_trace_kernel: run generate/eval first");
+    MIO_REQUIRE(which >= 0 && which <= 7 && which != 5, MIO_ERR_INVALID, "llm_trace_kernel: which %d", which);
+    int rc = mio::bind(m->d);
+    if (rc) return rc;
+    const int il = m->n_layer / 2;
+    hipStream_t s = m->d->stream;
+    unsigned long long *dt = nullptr;
+    MIO_HIP_CHECK(hipMalloc(&dt, 32 * sizeof(unsigned long long)));
+    MIO_HIP_CHECK(hipMemsetAsync(dt, 0, 32 * sizeof(unsigned long long), s));
+    mio::launch_step_kernel(which, m->dims, m->layers.data(), il, m->kc, m->vc, m->out_norm, m->lm, m->tok, m->buf,
+                            m->graph_cfg, s);
+    mio::LlmBuffers tb = m->buf;
+    tb.trace = dt;
+    mio::launch_step_kernel(which, m->dims, m->layers.data(), il, m->kc, m->vc, m->out_norm, m->lm, m->tok, tb,
+                            m->graph_cfg, s);
+    MIO_HIP_CHECK(hipMemcpyAsync(out, dt, 32 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+    MIO_HIP_CHECK(hipStreamSynchronize(s));
+    hipFree(dt);
     return MIO_OK;
 }

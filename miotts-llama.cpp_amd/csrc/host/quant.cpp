@@ -281,7 +281,21 @@ bool to_split(uint32_t type, const void *src, int64_t R, int64_t K, uint8_t *dst
                 std::memcpy(qs + 128 * i, b[i].qs, 128);
                 std::memcpy(hd + 16 * i, &b[i].d, 2);
                 std::memcpy(hd + 16 * i + 2, &b[i].dmin, 2);
-                std::memcpy(hd + 16 * i + 4, b[i].scales, 12);
+                // scales re-packed (same 96 bits) as 4 x 24-bit pairs {sc(2j), m(2j), sc(2j+1),
+                // m(2j+1)} at bit 24j, so a lane extracts its pair with one funnel shift
+                for (int j = 0; j < 4; ++j) {
+                    uint32_t f = 0;
+                    for (int t = 0; t < 2; ++t) {
+                        const int sj = 2 * j + t;
+                        const uint8_t *sc = b[i].scales;
+                        const uint32_t d = sj < 4 ? (sc[sj] & 63) : ((sc[sj + 4] & 0xF) | ((sc[sj - 4] >> 6) << 4));
+                        const uint32_t m = sj < 4 ? (sc[sj + 4] & 63) : ((sc[sj + 4] >> 4) | ((sc[sj] >> 6) << 4));
+                        f |= (d | (m << 6)) << (12 * t);
+                    }
+                    hd[16 * i + 4 + 3 * j + 0] = (uint8_t)f;
+                    hd[16 * i + 4 + 3 * j + 1] = (uint8_t)(f >> 8);
+                    hd[16 * i + 4 + 3 * j + 2] = (uint8_t)(f >> 16);
+                }
             }
         } else {  // Q6_K
             const BlockQ6_K *b = (const BlockQ6_K *)row;
@@ -292,7 +306,12 @@ bool to_split(uint32_t type, const void *src, int64_t R, int64_t K, uint8_t *dst
             for (int64_t i = 0; i < K / 256; ++i) {
                 std::memcpy(ql + 128 * i, b[i].ql, 128);
                 std::memcpy(qh + 64 * i, b[i].qh, 64);
-                std::memcpy(sc + 16 * i, b[i].scales, 16);
+                // scales re-ordered in lane pairs: pair p = 4n + r -> {scales[8n + r], scales[8n + r + 4]}
+                for (int p = 0; p < 8; ++p) {
+                    const int n = p >> 2, r = p & 3;
+                    sc[16 * i + 2 * p] = b[i].scales[8 * n + r];
+                    sc[16 * i + 2 * p + 1] = b[i].scales[8 * n + r + 4];
+                }
                 d[i] = b[i].d;
             }
         }

@@ -4,8 +4,8 @@
 // into the "split" layout the gfx950 matvec kernels stream:
 //
 //   Q8_0 : qs [R][K]      int8          | d  [R][K/32]  f16
-//   Q4_K : qs [R][K/2]    u8 nibbles    | hd [R][K/256] 16 B = {d, dmin, scales[12]}
-//   Q6_K : ql [R][K/2]    u8            | qh [R][K/4] u8 | sc [R][K/16] i8 | d [R][K/256] f16
+//   Q4_K : qs [R][K/2]    u8 nibbles    | hd [R][K/256] 16 B = {d, dmin, 4 x 24-bit scale pairs}
+//   Q6_K : ql [R][K/2]    u8            | qh [R][K/4] u8 | sc [R][K/16] i8 (lane-pair order) | d [R][K/256] f16
 //
 // Same bytes per weight as GGUF (algorithmic bytes unchanged); each row's quant payload
 // becomes one contiguous, 16-B aligned run, so one wave reads a row with 16 B per lane.

@@ -85,6 +85,7 @@ def _declare(L: ctypes.CDLL) -> None:
         "mio_parse_speech_tokens": (c_int, [ctypes.c_char_p, _vp, c_int, ctypes.POINTER(c_int)]),
         "mio_wav_encode": (c_int, [_vp, c_int, c_int, _vp, c_int, ctypes.POINTER(c_int)]),
         "mio_hip_llm_time_kernel": (c_int, [_vp, c_int, c_int, _f32p, ctypes.POINTER(ctypes.c_uint64)]),
+        "mio_hip_llm_trace_kernel": (c_int, [_vp, c_int, _vp]),
         "mio_hip_codec_last_timings": (c_int, [_vp, _f32p]),
         "mio_hip_debug_matvec": (c_int, [_vp, ctypes.c_uint32, _vp, c_int, c_int, _vp, _vp]),
         "mio_quantize_rows": (c_int, [ctypes.c_uint32, _vp, c_int, c_int, _vp]),
@@ -386,6 +387,12 @@ class Llm:
         b = ctypes.c_uint64(0)
         check(lib().mio_hip_llm_time_kernel(self.h, which, iters, ctypes.byref(ms), ctypes.byref(b)))
         return ms.value, b.value
+
+    def trace_kernel(self, which: int) -> np.ndarray:
+        """Checkpoint timestamps of one launch (diagnostic, mio_hip_llm_trace_kernel)."""
+        out = np.zeros(32, np.uint64)
+        check(lib().mio_hip_llm_trace_kernel(self.h, which, _ptr(out)))
+        return out
 
     def generate(self, prompt, max_tokens: int, temperature: float = 0.8, seed: int = 42,
                  allow=(-1, -1), eos=(-1, -1), check_interval: int = 20) -> np.ndarray:
