@@ -37,6 +37,16 @@ struct SampleCfg {
     int max_steps;
 };
 
+// Rows of the NEXT matvec launch that workgroup b of the current launch sweeps into
+// L2 / Infinity Cache (fire-and-forget LDS-DMA loads): mode 0 none, 1 rows of m[0] over
+// `grid` workgroups, 2 the same rows of m[0] and m[1] (gate/up), 3 q|k rows over the first
+// g_qk workgroups and v rows over the rest (attn_in). At most `cap` bytes per array.
+struct Prefetch {
+    QMat m[3];
+    int mode, grid, g_qk;
+    uint32_t cap;
+};
+
 struct LayerW {
     const float *attn_norm, *q_norm, *k_norm, *ffn_norm;
     QMat wq, wk, wv, wo, gate, up, down;
@@ -49,6 +59,8 @@ struct LlmDims {
     int split;        // attention positions per chunk (ATT_CHUNK = 64)
     int max_splits;
     int n_wg;         // streaming-matvec workgroups (one per CU)
+    int n_layer;
+    int prefetch;     // matvec launches prefetch the next launch's rows (MIO_PREFETCH=0: off)
 };
 
 struct LlmBuffers {
@@ -61,6 +73,8 @@ struct LlmBuffers {
     const float2 *rope;  // [n_ctx][hd/2] (cos, sin)
     StepState *st;
     unsigned long long *trace;  // optional: per-kernel checkpoint timestamps (workgroup 0, thread 0)
+    unsigned long long *tl;     // optional: step timeline {min start, max end} per launch (s_memrealtime)
+    int seq;                    // launch index within the step (timeline slot)
 };
 
 // Launch one decode step (all layers + head + sampler) on stream s.

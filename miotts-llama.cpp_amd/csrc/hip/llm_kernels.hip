@@ -49,11 +49,27 @@ namespace {
         }                                                                                     \
     } while (0)
 
+// Step timeline (diagnostic, mio_hip_llm_timeline): start / end of every workgroup of
+// each launch, s_memrealtime ticks (100 MHz), plain stores to slot [seq][wg] (wg < 256).
+#define MIO_TL_SLOT(bufs) ((bufs).tl + 2 * ((size_t)(bufs).seq * 256 + ((blockIdx.x + blockIdx.y * gridDim.x) & 255)))
+#define MIO_TL_BEGIN(bufs)                                                                      \
+    do {                                                                                        \
+        if ((bufs).tl && threadIdx.x == 0) MIO_TL_SLOT(bufs)[0] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#define MIO_TL_END(bufs)                                                                        \
+    do {                                                                                        \
+        if ((bufs).tl && threadIdx.x == 0) MIO_TL_SLOT(bufs)[1] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+
 constexpr int NT = 256;        // threads of the attention / sampler kernels
 constexpr int NWAVE = NT / 64;
 constexpr int MT = 512;        // threads of a streaming matvec workgroup
 constexpr int MW = MT / 64;
 constexpr int ATT_CHUNK = kAttChunk;
+constexpr int PF_SLOT = 1024;  // LDS bytes per wave that receive discarded prefetch data
+constexpr int PF_LDS = MW * PF_SLOT;
+// dynamic LDS of a matvec launch: activation staging, then the prefetch slots
+__host__ __device__ inline size_t pf_offset(size_t base) { return (base + 15) & ~(size_t)15; }
 __host__ __device__ constexpr int part_rec(int hd) { return hd + 4; }  // partial record {O[hd], m, l, pad}
 
 __device__ __forceinline__ float h2f(uint32_t bits16) {
@@ -541,16 +557,18 @@ __device__ __forceinline__ void load_group(const QMat W0, const QMat W1, int lo,
 }
 
 // Streams rows [lo, hi) (wave-uniform) of W0 (and W1 when NM == 2: row pairs, e.g.
-// gate/up); calls epi(row, dot0, dot1) once per row with wave-uniform values. A holds the
-// first group when pre is true; groups alternate between A and B (no register copies).
+// gate/up); calls epi(row, dot0, dot1) once per row with wave-uniform values. A and B hold
+// the first two groups (units [0, U) and [U, 2U)), issued by the caller before its
+// prologue; groups then alternate between A and B, one group in flight while the other is
+// reduced (no register copies).
 template <int T, int NP, int NM, class Epi>
 __device__ __forceinline__ void stream_rows(const QMat W0, const QMat W1, int lo, int hi, Frag (&A)[Cfg<NP>::U],
-                                            bool pre, const ActL &a, Epi &&epi, int split = INT_MAX) {
+                                            Frag (&B)[Cfg<NP>::U], const ActL &a, Epi &&epi, int split = INT_MAX,
+                                            unsigned long long *trace = nullptr) {
     constexpr int U = Cfg<NP>::U;
     const int K = W0.k;
     const int n = (hi - lo) * NM * NP;
     if (n <= 0) return;
-    if (!pre) load_group<T, NP, NM>(W0, W1, lo, n, 0, A, split);
     ALane al[Cfg<NP>::AREG ? NP : 1];
     if constexpr (Cfg<NP>::AREG) {
 #pragma unroll
@@ -591,17 +609,26 @@ __device__ __forceinline__ void stream_rows(const QMat W0, const QMat W1, int lo
             }
         }
     };
-    Frag B[U];
     for (int u0 = 0;;) {
-        load_group<T, NP, NM>(W0, W1, lo, n, u0 + U, B, split);
         consume(A, u0);
+        if (trace && u0 == 0 && blockIdx.x == 0 && threadIdx.x == 0) trace[3] = __builtin_readcyclecounter();
         u0 += U;
         if (u0 >= n) break;
         load_group<T, NP, NM>(W0, W1, lo, n, u0 + U, A, split);
         consume(B, u0);
         u0 += U;
         if (u0 >= n) break;
+        load_group<T, NP, NM>(W0, W1, lo, n, u0 + U, B, split);
     }
+}
+
+// The first two groups of a wave's stream (before the prologue).
+template <int T, int NP, int NM>
+__device__ __forceinline__ void load_first(const QMat W0, const QMat W1, int lo, int hi, Frag (&A)[Cfg<NP>::U],
+                                           Frag (&B)[Cfg<NP>::U], int split = INT_MAX) {
+    const int n = (hi - lo) * NM * NP;
+    load_group<T, NP, NM>(W0, W1, lo, n, 0, A, split);
+    load_group<T, NP, NM>(W0, W1, lo, n, Cfg<NP>::U, B, split);
 }
 
 // Rows [0, R) over G workgroups: workgroup b owns [R*b/G, R*(b+1)/G), wave w a contiguous
@@ -614,6 +641,57 @@ __device__ inline void wave_range(int R, int &lo, int &hi, int b, int G) {
 }
 __device__ inline void wave_range(int R, int &lo, int &hi) { wave_range(R, lo, hi, blockIdx.x, gridDim.x); }
 
+// ------------------------------------------------------------------ cross-launch prefetch
+
+__device__ inline void prefetch_range(const uint8_t *base, uint32_t total, uint32_t off, uint32_t bytes,
+                                      char *slot) {
+    const auto r = rsrc(base, total);
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    for (uint32_t c = w; c * 1024u < bytes; c += MW)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void *)slot, 16, lane * 16,
+                                                 off + c * 1024u, 0, 0);
+}
+
+// all arrays of rows [r0, r1) of W
+__device__ inline void prefetch_rows(const QMat &W, int r0, int r1, uint32_t cap, char *slot) {
+    if (r1 <= r0) return;
+    const uint32_t R = (uint32_t)W.rows, n = (uint32_t)(r1 - r0);
+    uint32_t rb[4] = {0, 0, 0, 0};
+    const uint8_t *p[4] = {W.p0, W.p1, W.p2, W.p3};
+    if (W.type == 12) {
+        rb[0] = W.k / 2, rb[1] = (W.k >> 8) * 16;
+    } else if (W.type == 14) {
+        rb[0] = W.k / 2, rb[1] = W.k / 4, rb[2] = W.k / 16, rb[3] = (W.k >> 8) * 2;
+    } else {
+        rb[0] = W.k, rb[1] = (W.k >> 5) * 2;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        if (rb[i]) prefetch_range(p[i], R * rb[i], (uint32_t)r0 * rb[i], min(n * rb[i], cap), slot);
+}
+
+__device__ inline void prefetch_next(const Prefetch &pf, char *lds_slots) {
+    if (pf.mode == 0) return;
+    char *slot = lds_slots + PF_SLOT * __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int b = blockIdx.x;
+    if (pf.mode == 3) {
+        if (b < pf.g_qk) {
+            const int o1 = pf.m[0].rows, o2 = o1 + pf.m[1].rows;
+            const int ra = (o2 * b) / pf.g_qk, rb = (o2 * (b + 1)) / pf.g_qk;
+            prefetch_rows(pf.m[0], ra, min(rb, o1), pf.cap, slot);
+            prefetch_rows(pf.m[1], max(ra, o1) - o1, rb - o1, pf.cap, slot);
+        } else if (b < pf.grid) {
+            const int gv = pf.grid - pf.g_qk, bv = b - pf.g_qk, R = pf.m[2].rows;
+            prefetch_rows(pf.m[2], (R * bv) / gv, (R * (bv + 1)) / gv, pf.cap, slot);
+        }
+        return;
+    }
+    if (b >= pf.grid) return;
+    const int R = pf.m[0].rows, ra = (R * b) / pf.grid, rb = (R * (b + 1)) / pf.grid;
+    prefetch_rows(pf.m[0], ra, rb, pf.cap, slot);
+    if (pf.mode == 2) prefetch_rows(pf.m[1], ra, rb, pf.cap, slot);
+}
+
 // ------------------------------------------------------------------ matvec kernels
 // Every kernel is instantiated per weight type T (ggml id 8 / 12 / 14): the unit loop is
 // straight-line code with no run-time type dispatch.
@@ -621,33 +699,39 @@ __device__ inline void wave_range(int R, int &lo, int &hi) { wave_range(R, lo, h
 // branch is WG-uniform and runs its own prologue, so neither path merges load counts.
 template <int NP, int TQ, int TV>
 __global__ __launch_bounds__(MT) void k_attn_in(LlmDims d, const float *norm_w, QMat wq, QMat wk, QMat wv,
-                                                int g_qk, LlmBuffers b) {
+                                                int g_qk, Prefetch pf, LlmBuffers b) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int K = d.n_embd;
     const Smem s = carve(smem, K);
+    char *pf_lds = smem + pf_offset(smem_bytes(K));
     MIO_TRACE(b, 0);
+    MIO_TL_BEGIN(b);
     XRegs<NP> xr;
     load_x(b.x, norm_w, K, xr);
     const int o1 = wq.rows, o2 = wq.rows + wk.rows;
-    Frag cur[Cfg<NP>::U];
+    Frag ga[Cfg<NP>::U], gb[Cfg<NP>::U];
     int lo, hi;
     if ((int)blockIdx.x < g_qk) {
         wave_range(o2, lo, hi, blockIdx.x, g_qk);
-        load_group<TQ, NP, 1>(wq, wk, lo, (hi - lo) * NP, 0, cur, o1);
+        load_first<TQ, NP, 1>(wq, wk, lo, hi, ga, gb, o1);
+        prefetch_next(pf, pf_lds);
         MIO_TRACE(b, 1);
         rmsnorm_quant(xr, K, d.eps, TQ != 8, s);
         MIO_TRACE(b, 2);
-        stream_rows<TQ, NP, 1>(wq, wk, lo, hi, cur, true, s.a, [&](int row, float v, float) {
+        stream_rows<TQ, NP, 1>(wq, wk, lo, hi, ga, gb, s.a, [&](int row, float v, float) {
             if ((threadIdx.x & 63) == 0) b.qkv[row] = v;
         }, o1);
-        MIO_TRACE(b, 15);
+        MIO_TL_END(b);
+    MIO_TRACE(b, 15);
     } else {
         wave_range(wv.rows, lo, hi, blockIdx.x - g_qk, gridDim.x - g_qk);
-        load_group<TV, NP, 1>(wv, wv, lo, (hi - lo) * NP, 0, cur);
+        load_first<TV, NP, 1>(wv, wv, lo, hi, ga, gb);
+        prefetch_next(pf, pf_lds);
         rmsnorm_quant(xr, K, d.eps, TQ != 8, s);
-        stream_rows<TV, NP, 1>(wv, wv, lo, hi, cur, true, s.a, [&](int row, float v, float) {
+        stream_rows<TV, NP, 1>(wv, wv, lo, hi, ga, gb, s.a, [&](int row, float v, float) {
             if ((threadIdx.x & 63) == 0) b.qkv[o2 + row] = v;
         });
+        MIO_TL_END(b);
     }
 }
 
@@ -706,53 +790,61 @@ __device__ void merge_attention(const LlmDims &d, const float *part, int nch, in
 }
 
 template <int NP, int T>
-__global__ __launch_bounds__(MT) void k_attn_out(LlmDims d, QMat wo, LlmBuffers b) {
+__global__ __launch_bounds__(MT) void k_attn_out(LlmDims d, QMat wo, Prefetch pf, LlmBuffers b) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     MIO_TRACE(b, 0);
+    MIO_TL_BEGIN(b);
     const int K = wo.k;
     const Smem s = carve(smem, K);
     int lo, hi;
     wave_range(wo.rows, lo, hi);
     const float xres = load_resid(b.x, lo, hi);
-    Frag cur[Cfg<NP>::U];
-    load_group<T, NP, 1>(wo, wo, lo, (hi - lo) * NP, 0, cur);
+    Frag ga[Cfg<NP>::U], gb[Cfg<NP>::U];
+    load_first<T, NP, 1>(wo, wo, lo, hi, ga, gb);
+    prefetch_next(pf, smem + pf_offset(smem_bytes(K)));
     MIO_TRACE(b, 1);
     merge_attention<NP>(d, b.part, b.st->pos / ATT_CHUNK + 1, K, T != 8, s);
     MIO_TRACE(b, 2);
-    stream_rows<T, NP, 1>(wo, wo, lo, hi, cur, true, s.a, [&](int row, float v, float) {
+    stream_rows<T, NP, 1>(wo, wo, lo, hi, ga, gb, s.a, [&](int row, float v, float) {
         const float r = lane_value(xres, row - lo);
         if ((threadIdx.x & 63) == 0) b.x[row] = v + r;
     });
+    MIO_TL_END(b);
     MIO_TRACE(b, 15);
 }
 
 __device__ inline float silu_f(float x) { return x / (1.0f + expf(-x)); }
 
 template <int NP, int T>
-__global__ __launch_bounds__(MT) void k_ffn_in(LlmDims d, const float *norm_w, QMat gate, QMat up, LlmBuffers b) {
+__global__ __launch_bounds__(MT) void k_ffn_in(LlmDims d, const float *norm_w, QMat gate, QMat up, Prefetch pf,
+                                               LlmBuffers b) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     MIO_TRACE(b, 0);
+    MIO_TL_BEGIN(b);
     const int K = d.n_embd;
     const Smem s = carve(smem, K);
     XRegs<NP> xr;
     load_x(b.x, norm_w, K, xr);
     int lo, hi;
     wave_range(gate.rows, lo, hi);
-    Frag cur[Cfg<NP>::U];
-    load_group<T, NP, 2>(gate, up, lo, (hi - lo) * NP * 2, 0, cur);
+    Frag ga[Cfg<NP>::U], gb[Cfg<NP>::U];
+    load_first<T, NP, 2>(gate, up, lo, hi, ga, gb);
+    prefetch_next(pf, smem + pf_offset(smem_bytes(K)));
     MIO_TRACE(b, 1);
     rmsnorm_quant(xr, K, d.eps, T != 8, s);
     MIO_TRACE(b, 2);
-    stream_rows<T, NP, 2>(gate, up, lo, hi, cur, true, s.a, [&](int row, float g, float u) {
+    stream_rows<T, NP, 2>(gate, up, lo, hi, ga, gb, s.a, [&](int row, float g, float u) {
         if ((threadIdx.x & 63) == 0) b.h[row] = silu_f(g) * u;
-    });
+    }, INT_MAX, b.trace);
+    MIO_TL_END(b);
     MIO_TRACE(b, 15);
 }
 
 template <int NP, int T>
-__global__ __launch_bounds__(MT) void k_ffn_down(LlmDims d, QMat down, LlmBuffers b) {
+__global__ __launch_bounds__(MT) void k_ffn_down(LlmDims d, QMat down, Prefetch pf, LlmBuffers b) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     MIO_TRACE(b, 0);
+    MIO_TL_BEGIN(b);
     const int K = down.k;
     const Smem s = carve(smem, K);
     XRegs<NP> xr;
@@ -760,15 +852,17 @@ __global__ __launch_bounds__(MT) void k_ffn_down(LlmDims d, QMat down, LlmBuffer
     int lo, hi;
     wave_range(down.rows, lo, hi);
     const float xres = load_resid(b.x, lo, hi);
-    Frag cur[Cfg<NP>::U];
-    load_group<T, NP, 1>(down, down, lo, (hi - lo) * NP, 0, cur);
+    Frag ga[Cfg<NP>::U], gb[Cfg<NP>::U];
+    load_first<T, NP, 1>(down, down, lo, hi, ga, gb);
+    prefetch_next(pf, smem + pf_offset(smem_bytes(K)));
     MIO_TRACE(b, 1);
     plain_quant(xr, K, T != 8, s);
     MIO_TRACE(b, 2);
-    stream_rows<T, NP, 1>(down, down, lo, hi, cur, true, s.a, [&](int row, float v, float) {
+    stream_rows<T, NP, 1>(down, down, lo, hi, ga, gb, s.a, [&](int row, float v, float) {
         const float r = lane_value(xres, row - lo);
         if ((threadIdx.x & 63) == 0) b.x[row] = v + r;
-    });
+    }, INT_MAX, b.trace);
+    MIO_TL_END(b);
     MIO_TRACE(b, 15);
 }
 
@@ -790,26 +884,29 @@ __device__ inline float gumbel(uint64_t seed, int step, int idx) {
 // (<= 128) are parked one per lane (two registers) and the noise is drawn for 64 rows at
 // a time after the stream.
 template <int NP, int T>
-__global__ __launch_bounds__(MT) void k_lm_head(LlmDims d, const float *norm_w, QMat lm, SampleCfg sc, LlmBuffers b) {
+__global__ __launch_bounds__(MT) void k_lm_head(LlmDims d, const float *norm_w, QMat lm, SampleCfg sc, Prefetch pf,
+                                                LlmBuffers b) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __shared__ float bs_[MW];
     __shared__ int bi_[MW];
     const int K = d.n_embd;
     MIO_TRACE(b, 0);
+    MIO_TL_BEGIN(b);
     const Smem s = carve(smem, K);
     XRegs<NP> xr;
     load_x(b.x, norm_w, K, xr);
     const int step = b.st->step;
     int lo, hi;
     wave_range(lm.rows, lo, hi);
-    Frag cur[Cfg<NP>::U];
-    load_group<T, NP, 1>(lm, lm, lo, (hi - lo) * NP, 0, cur);
+    Frag ga[Cfg<NP>::U], gb[Cfg<NP>::U];
+    load_first<T, NP, 1>(lm, lm, lo, hi, ga, gb);
+    prefetch_next(pf, smem + pf_offset(smem_bytes(K)));
     MIO_TRACE(b, 1);
     rmsnorm_quant(xr, K, d.eps, T != 8, s);
     MIO_TRACE(b, 2);
     const int lane = threadIdx.x & 63;
     float r0 = -INFINITY, r1 = -INFINITY;
-    stream_rows<T, NP, 1>(lm, lm, lo, hi, cur, true, s.a, [&](int row, float v, float) {
+    stream_rows<T, NP, 1>(lm, lm, lo, hi, ga, gb, s.a, [&](int row, float v, float) {
         const int k = row - lo;
         r0 = lane == k ? v : r0;
         r1 = lane + 64 == k ? v : r1;
@@ -845,6 +942,7 @@ __global__ __launch_bounds__(MT) void k_lm_head(LlmDims d, const float *norm_w, 
         b.smp[2 * blockIdx.x] = best;
         b.smp[2 * blockIdx.x + 1] = __int_as_float(bi);
     }
+    MIO_TL_END(b);
     MIO_TRACE(b, 15);
 }
 
@@ -879,6 +977,7 @@ __global__ __launch_bounds__(NT) void k_attention(LlmDims d, const float *q_norm
     __shared__ float wres[NWAVE][G][HD + 2];
 
     MIO_TRACE(b, 0);
+    MIO_TL_BEGIN(b);
     const int kvh = blockIdx.y, ch = blockIdx.x;
     const int pos = b.st->pos;
     const int t0 = ch * ATT_CHUNK;
@@ -1063,6 +1162,7 @@ __global__ __launch_bounds__(NT) void k_attention(LlmDims d, const float *q_norm
         dst[dd] = O;
         if (dd == 0) dst[HD] = M, dst[HD + 1] = L;
     }
+    MIO_TL_END(b);
     MIO_TRACE(b, 15);
 }
 
@@ -1126,6 +1226,7 @@ __global__ __launch_bounds__(ST) void k_sample(LlmDims d, SampleCfg sc, QMat emb
     __shared__ int bi_[ST / 64];
     __shared__ int tok_s;
     MIO_TRACE(b, 0);
+    MIO_TL_BEGIN(b);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int step = b.st->step;
     float best = -INFINITY;
@@ -1155,6 +1256,7 @@ __global__ __launch_bounds__(ST) void k_sample(LlmDims d, SampleCfg sc, QMat emb
     const int tok = tok_s;
     MIO_TRACE(b, 1);
     embed_row(emb, tok, d.n_embd, b.x);
+    MIO_TL_END(b);
     MIO_TRACE(b, 15);
     if (tid == 0) {
         if (step < sc.max_steps) sc.out_tokens[step] = tok;
@@ -1201,27 +1303,63 @@ void dispatch_nt(int K, int type, F &&f) {
 #undef NT_CASE
 }
 
-// Launch one kernel of the step: which = 0 attn_in, 1 attention (+ split merge),
-// 2 attn_out, 3 ffn_in, 4 ffn_down (layer il), 5 (unused: the final norm is fused into
+inline size_t mv_lds(int K) { return pf_offset(smem_bytes(K)) + PF_LDS; }
+
+// attn_in grid: q|k rows on the first g_qk workgroups, v rows on the rest
+inline void attn_in_grid(const LlmDims &d, const LayerW &L, int &G, int &g_qk) {
+    const int rows = L.wq.rows + L.wk.rows + L.wv.rows, qk = L.wq.rows + L.wk.rows;
+    G = matvec_grid(d, rows);
+    g_qk = (G * qk + rows / 2) / rows;
+    g_qk = g_qk < 1 ? 1 : (g_qk > G - 1 ? G - 1 : g_qk);
+}
+
+// what launch `which` of layer il prefetches: the next matvec launch's rows
+Prefetch prefetch_plan(int which, const LlmDims &d, const LayerW *layers, int il, const QMat &lm) {
+    Prefetch p{};
+    p.cap = 0xFFFFFFFFu;
+    auto qkv = [&](const LayerW &L) {
+        p.mode = 3;
+        p.m[0] = L.wq, p.m[1] = L.wk, p.m[2] = L.wv;
+        attn_in_grid(d, L, p.grid, p.g_qk);
+    };
+    const LayerW &L = layers[il];
+    switch (which) {
+        case 0: p.mode = 1, p.m[0] = L.wo, p.grid = matvec_grid(d, L.wo.rows); break;
+        case 2: p.mode = 2, p.m[0] = L.gate, p.m[1] = L.up, p.grid = matvec_grid(d, L.gate.rows); break;
+        case 3: p.mode = 1, p.m[0] = L.down, p.grid = matvec_grid(d, L.down.rows); break;
+        case 4:
+            if (il + 1 < d.n_layer) {
+                qkv(layers[il + 1]);
+            } else {
+                p.mode = 1, p.m[0] = lm, p.grid = lm_head_blocks(d);
+                p.cap = 64u << 10;
+            }
+            break;
+        case 6: qkv(layers[0]); break;
+        default: p.mode = 0; break;
+    }
+    return p;
+}
+
+// Launch one kernel of the step: which = 0 attn_in, 1 attention, 2 attn_out (+ chunk
+// merge), 3 ffn_in, 4 ffn_down (layer il), 5 (unused: the final norm is fused into
 // lm_head), 6 lm_head, 7 sample.
 void launch_step_kernel(int which, const LlmDims &d, const LayerW *layers, int il, _Float16 *kcache,
                         _Float16 *vcache, const float *out_norm, const QMat &lm, const QMat &tok_embd,
                         const LlmBuffers &b, const SampleCfg &sc, hipStream_t s) {
     const size_t layer_kv = (size_t)d.n_kv * d.n_ctx * d.hd;
     const int G = d.n_head / d.n_kv;
+    const Prefetch pf = d.prefetch ? prefetch_plan(which, d, layers, il, lm) : Prefetch{};
     switch (which) {
         case 0: {
             const LayerW &L = layers[il];
-            const int rows = L.wq.rows + L.wk.rows + L.wv.rows, qk = L.wq.rows + L.wk.rows;
-            const int G = matvec_grid(d, rows);
-            int g_qk = (G * qk + rows / 2) / rows;
-            g_qk = g_qk < 1 ? 1 : (g_qk > G - 1 ? G - 1 : g_qk);
-            const dim3 grid(G);
-            const size_t lds = smem_bytes(d.n_embd);
+            int GW, g_qk;
+            attn_in_grid(d, L, GW, g_qk);
+            const size_t lds = mv_lds(d.n_embd);
             dispatch_nt(d.n_embd, L.wq.type, [&]<int NP, int TQ>() {
                 auto go = [&]<int TV>() {
-                    hipLaunchKernelGGL((k_attn_in<NP, TQ, TV>), grid, dim3(MT), lds, s, d, L.attn_norm, L.wq, L.wk,
-                                       L.wv, g_qk, b);
+                    hipLaunchKernelGGL((k_attn_in<NP, TQ, TV>), dim3(GW), dim3(MT), lds, s, d, L.attn_norm, L.wq, L.wk,
+                                       L.wv, g_qk, pf, b);
                 };
                 if constexpr (TQ == 8) {
                     go.template operator()<8>();
@@ -1246,31 +1384,31 @@ void launch_step_kernel(int which, const LlmDims &d, const LayerW *layers, int i
         case 2: {
             const LayerW &L = layers[il];
             dispatch_nt(L.wo.k, L.wo.type, [&]<int NP, int T>() {
-                hipLaunchKernelGGL((k_attn_out<NP, T>), dim3(matvec_grid(d, L.wo.rows)), dim3(MT), smem_bytes(L.wo.k),
-                                   s, d, L.wo, b);
+                hipLaunchKernelGGL((k_attn_out<NP, T>), dim3(matvec_grid(d, L.wo.rows)), dim3(MT), mv_lds(L.wo.k), s, d,
+                                   L.wo, pf, b);
             });
             break;
         }
         case 3: {
             const LayerW &L = layers[il];
             dispatch_nt(d.n_embd, L.gate.type, [&]<int NP, int T>() {
-                hipLaunchKernelGGL((k_ffn_in<NP, T>), dim3(matvec_grid(d, L.gate.rows)), dim3(MT), smem_bytes(d.n_embd),
-                                   s, d, L.ffn_norm, L.gate, L.up, b);
+                hipLaunchKernelGGL((k_ffn_in<NP, T>), dim3(matvec_grid(d, L.gate.rows)), dim3(MT), mv_lds(d.n_embd), s,
+                                   d, L.ffn_norm, L.gate, L.up, pf, b);
             });
             break;
         }
         case 4: {
             const LayerW &L = layers[il];
             dispatch_nt(L.down.k, L.down.type, [&]<int NP, int T>() {
-                hipLaunchKernelGGL((k_ffn_down<NP, T>), dim3(matvec_grid(d, L.down.rows)), dim3(MT),
-                                   smem_bytes(L.down.k), s, d, L.down, b);
+                hipLaunchKernelGGL((k_ffn_down<NP, T>), dim3(matvec_grid(d, L.down.rows)), dim3(MT), mv_lds(L.down.k),
+                                   s, d, L.down, pf, b);
             });
             break;
         }
         case 6:
             dispatch_nt(d.n_embd, lm.type, [&]<int NP, int T>() {
-                hipLaunchKernelGGL((k_lm_head<NP, T>), dim3(lm_head_blocks(d)), dim3(MT), smem_bytes(d.n_embd), s, d,
-                                   out_norm, lm, sc, b);
+                hipLaunchKernelGGL((k_lm_head<NP, T>), dim3(lm_head_blocks(d)), dim3(MT), mv_lds(d.n_embd), s, d,
+                                   out_norm, lm, sc, pf, b);
             });
             break;
         case 7:
@@ -1300,10 +1438,10 @@ __global__ __launch_bounds__(MT) void k_debug_matvec(QMat W, const float *x, flo
     load_x(x, nullptr, K, xr);
     int lo, hi;
     wave_range(W.rows, lo, hi);
-    Frag cur[Cfg<NP>::U];
-    load_group<T, NP, 1>(W, W, lo, (hi - lo) * NP, 0, cur);
+    Frag ga[Cfg<NP>::U], gb[Cfg<NP>::U];
+    load_first<T, NP, 1>(W, W, lo, hi, ga, gb);
     plain_quant(xr, K, T != 8, s);
-    stream_rows<T, NP, 1>(W, W, lo, hi, cur, true, s.a, [&](int row, float v, float) {
+    stream_rows<T, NP, 1>(W, W, lo, hi, ga, gb, s.a, [&](int row, float v, float) {
         if ((threadIdx.x & 63) == 0) y[row] = v;
     });
 }
@@ -1313,7 +1451,7 @@ void launch_debug_matvec(const QMat &W, const float *x, float *y, int n_wg, hipS
     LlmDims d{};
     d.n_wg = n_wg;
     dispatch_nt(W.k, W.type, [&]<int NP, int T>() {
-        hipLaunchKernelGGL((k_debug_matvec<NP, T>), dim3(matvec_grid(d, W.rows)), dim3(MT), smem_bytes(W.k), s, W, x,
+        hipLaunchKernelGGL((k_debug_matvec<NP, T>), dim3(matvec_grid(d, W.rows)), dim3(MT), mv_lds(W.k), s, W, x,
                            y);
     });
 }

@@ -6,15 +6,18 @@
 // llama_sampler_sample / llama_decode (:164-192) and the temp+dist sampler chain (:127-130).
 #include "llm.h"
 
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <string>
 #include <vector>
 
 #include "common.h"
 #include "gguf.h"
 #include "llm_kernels.h"
+#include "prefetch.h"
 #include "quant.h"
 
 struct mio_hip_llm {
@@ -30,6 +33,15 @@ struct mio_hip_llm {
     int max_steps = 0;
     std::vector<void *> allocs;
     uint64_t weight_bytes = 0;
+    // all quantized matrices live in one arena, in the order a step streams them
+    uint8_t *arena = nullptr;
+    std::map<std::string, size_t> arena_off;
+    // weight byte range streamed by each launch: [il * 5 + which] (which 0/2/3/4), lm_head last
+    struct Range {
+        const uint8_t *p = nullptr;
+        uint64_t bytes = 0;
+    };
+    std::vector<Range> ranges;
 
     hipGraphExec_t graph = nullptr;
     mio::SampleCfg graph_cfg{};
@@ -71,7 +83,8 @@ bool upload_qmat(mio_hip_llm *m, const mio::GgufTensor *t, mio::QMat &q) {
         mio::set_error("llm: re-layout of %s failed", t->name.c_str());
         return false;
     }
-    uint8_t *dp = dalloc<uint8_t>(m, L.bytes);
+    const auto it = m->arena_off.find(t->name);
+    uint8_t *dp = (m->arena && it != m->arena_off.end()) ? m->arena + it->second : dalloc<uint8_t>(m, L.bytes);
     if (!dp || hipMemcpy(dp, host.data(), L.bytes, hipMemcpyHostToDevice) != hipSuccess) {
         mio::set_error("llm: upload of %s failed", t->name.c_str());
         return false;
@@ -100,6 +113,24 @@ float *upload_f32(mio_hip_llm *m, const mio::GgufTensor *t, int64_t n) {
 
 bool same_cfg(const mio::SampleCfg &a, const mio::SampleCfg &b) { return std::memcmp(&a, &b, sizeof(a)) == 0; }
 
+// One decode step on m->d->stream (tl: optional step timeline, diagnostic).
+int issue_step(mio_hip_llm *m, const mio::SampleCfg &cfg, unsigned long long *tl = nullptr) {
+    hipStream_t s = m->d->stream;
+    int seq = 0;
+    auto bufs = [&]() {
+        mio::LlmBuffers b = m->buf;
+        if (tl) b.tl = tl, b.seq = seq++;
+        return b;
+    };
+    for (int il = 0; il < m->n_layer; ++il)
+        for (int k = 0; k < 5; ++k)
+            mio::launch_step_kernel(k, m->dims, m->layers.data(), il, m->kc, m->vc, m->out_norm, m->lm, m->tok, bufs(),
+                                    cfg, s);
+    mio::launch_step_kernel(6, m->dims, m->layers.data(), 0, m->kc, m->vc, m->out_norm, m->lm, m->tok, bufs(), cfg, s);
+    mio::launch_step_kernel(7, m->dims, m->layers.data(), 0, m->kc, m->vc, m->out_norm, m->lm, m->tok, bufs(), cfg, s);
+    return MIO_OK;
+}
+
 int ensure_graph(mio_hip_llm *m, const mio::SampleCfg &cfg) {
     if (m->graph && same_cfg(cfg, m->graph_cfg)) return MIO_OK;
     if (m->graph) {
@@ -109,9 +140,9 @@ int ensure_graph(mio_hip_llm *m, const mio::SampleCfg &cfg) {
     hipStream_t s = m->d->stream;
     hipGraph_t g = nullptr;
     MIO_HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
-    mio::launch_decode_step(m->dims, m->layers.data(), m->n_layer, m->kc, m->vc, m->out_norm, m->lm, m->tok,
-                            m->buf, cfg, s);
+    const int rc = issue_step(m, cfg);
     MIO_HIP_CHECK(hipStreamEndCapture(s, &g));
+    if (rc) return rc;
     MIO_HIP_CHECK(hipGraphInstantiate(&m->graph, g, nullptr, nullptr, 0));
     hipGraphDestroy(g);
     m->graph_cfg = cfg;
@@ -174,10 +205,9 @@ int llm_run(mio_hip_llm *m, int n_steps) {
     // ROCm 7.2 here; kernels and arguments are identical either way)
     static const bool eager = getenv("MIO_NO_GRAPH") && getenv("MIO_NO_GRAPH")[0] == '1';
     for (int i = 0; i < n_steps && m->steps_issued < m->steps_total; ++i, ++m->steps_issued) {
-        if (eager)
-            mio::launch_decode_step(m->dims, m->layers.data(), m->n_layer, m->kc, m->vc, m->out_norm, m->lm, m->tok,
-                                    m->buf, m->cfg, m->d->stream);
-        else
+        if (eager) {
+            if ((rc = issue_step(m, m->cfg))) return rc;
+        } else
             MIO_HIP_CHECK(hipGraphLaunch(m->graph, m->d->stream));
     }
     return MIO_OK;
@@ -239,6 +269,7 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
     D.split = mio::kAttChunk;
     D.max_splits = (n_ctx + D.split - 1) / D.split;
     D.n_wg = d->n_cu > 0 ? d->n_cu : 256;
+    D.n_layer = m->n_layer;
     MIO_REQUIRE(n_ctx <= 32768, MIO_ERR_UNSUPPORTED, "llm_load: n_ctx %d > 32768", n_ctx);
     const int G = D.n_kv ? D.n_head / D.n_kv : 0;
     if (D.n_embd <= 0 || m->n_layer <= 0 || D.n_head <= 0 || D.n_kv <= 0 || D.n_head % D.n_kv ||
@@ -247,6 +278,29 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
         mio::set_error("llm_load: unsupported dims (n_embd %d, heads %d/%d, head_dim %d)", D.n_embd, D.n_head,
                        D.n_kv, D.hd);
         return fail(MIO_ERR_UNSUPPORTED);
+    }
+    {
+        // arena: layer matrices in step order, then the lm_head, then the embedding table
+        std::vector<std::string> order;
+        static const char *mats[] = {"attn_q", "attn_k", "attn_v", "attn_output", "ffn_gate", "ffn_up", "ffn_down"};
+        for (int i = 0; i < m->n_layer; ++i)
+            for (const char *n : mats) order.push_back("blk." + std::to_string(i) + "." + n + ".weight");
+        order.push_back("output.weight");
+        order.push_back("token_embd.weight");
+        size_t total = 0;
+        for (const std::string &n : order) {
+            const mio::GgufTensor *t = g.tensor(n);
+            if (!t || t->n_dims != 2) continue;
+            const mio::SplitLayout L = mio::split_layout(t->type, t->ne[1], t->ne[0]);
+            if (!L.bytes) continue;
+            m->arena_off[n] = total;
+            total += (L.bytes + 255) & ~(size_t)255;
+        }
+        m->arena = dalloc<uint8_t>(m, total);
+        if (!m->arena) {
+            mio::set_error("llm_load: weight arena of %zu bytes: allocation failed", total);
+            return fail(MIO_ERR_OOM);
+        }
     }
     const mio::GgufTensor *te = g.tensor("token_embd.weight");
     if (!te || te->ne[0] != D.n_embd) {
@@ -295,6 +349,19 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
         }
         m->layers.push_back(L);
     }
+    // per-launch weight ranges (prefetch)
+    auto span = [&](const mio::QMat &a, const mio::QMat &z) {
+        const mio::SplitLayout L = mio::split_layout(z.type, z.rows, z.k);
+        return mio_hip_llm::Range{a.p0, (uint64_t)(z.p0 + L.bytes - a.p0)};
+    };
+    for (const mio::LayerW &L : m->layers) {
+        m->ranges.push_back(span(L.wq, L.wv));
+        m->ranges.push_back({});
+        m->ranges.push_back(span(L.wo, L.wo));
+        m->ranges.push_back(span(L.gate, L.up));
+        m->ranges.push_back(span(L.down, L.down));
+    }
+    m->ranges.push_back(span(m->lm, m->lm));
     // buffers
     const int qkv = (D.n_head + 2 * D.n_kv) * D.hd;
     const size_t kv = (size_t)m->n_layer * D.n_kv * n_ctx * D.hd;
@@ -327,6 +394,9 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
         return fail(MIO_ERR_OOM);
     }
     hipMemcpy(dr, rope.data(), rope.size() * sizeof(float2), hipMemcpyHostToDevice);
+    // MIO_PREFETCH=1: matvec launches also sweep the next launch's rows into the caches
+    // (measured slower on MI355X: kept as an opt-in experiment)
+    D.prefetch = (getenv("MIO_PREFETCH") && getenv("MIO_PREFETCH")[0] == '1') ? 1 : 0;
     m->buf.rope = dr;
     *out = m;
     return MIO_OK;
@@ -503,6 +573,18 @@ extern "C" int mio_hip_llm_trace_kernel(mio_hip_llm *m, int which, uint64_t *out
     MIO_HIP_CHECK(hipMemsetAsync(dt, 0, 32 * sizeof(unsigned long long), s));
     mio::launch_step_kernel(which, m->dims, m->layers.data(), il, m->kc, m->vc, m->out_norm, m->lm, m->tok, m->buf,
                             m->graph_cfg, s);
+    // evict L2 / MALL so the traced launch streams its weights from HBM as in a real step
+    void *flush = nullptr;
+    const size_t flush_bytes = (size_t)1 << 30;
+    if (hipMalloc(&flush, flush_bytes) == hipSuccess) {
+        hipMemsetAsync(flush, 1, flush_bytes, s);
+        hipMemsetAsync(flush, 2, flush_bytes, s);
+    }
+    // MIO_TRACE_PREFETCH=1: the launch's weights are swept into the Infinity Cache first
+    if (getenv("MIO_TRACE_PREFETCH") && getenv("MIO_TRACE_PREFETCH")[0] == '1') {
+        const size_t ri = which == 6 ? m->ranges.size() - 1 : (size_t)il * 5 + which;
+        if (ri < m->ranges.size()) mio::launch_touch(m->ranges[ri].p, m->ranges[ri].bytes, m->dims.n_wg, s);
+    }
     mio::LlmBuffers tb = m->buf;
     tb.trace = dt;
     mio::launch_step_kernel(which, m->dims, m->layers.data(), il, m->kc, m->vc, m->out_norm, m->lm, m->tok, tb,
@@ -510,5 +592,40 @@ extern "C" int mio_hip_llm_trace_kernel(mio_hip_llm *m, int which, uint64_t *out
     MIO_HIP_CHECK(hipMemcpyAsync(out, dt, 32 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
     MIO_HIP_CHECK(hipStreamSynchronize(s));
     hipFree(dt);
+    if (flush) hipFree(flush);
+    return MIO_OK;
+}
+
+// Diagnostic: captures one decode step as a graph with the step timeline on, replays it
+// (advancing the decode state by 3 steps: reset/eval afterwards), and returns per launch
+// {first workgroup start, last workgroup end} in s_memrealtime ticks (100 MHz).
+extern "C" int mio_hip_llm_timeline(mio_hip_llm *m, uint64_t *out, int max_launches, int *n_launches) {
+    MIO_REQUIRE(m && out && n_launches && m->graph, MIO_ERR_INVALID, "llm_timeline: run generate/eval first");
+    int rc = mio::bind(m->d);
+    if (rc) return rc;
+    const int nl = m->n_layer * 5 + 2;
+    MIO_REQUIRE(max_launches >= nl, MIO_ERR_INVALID, "llm_timeline: need %d launch slots", nl);
+    hipStream_t s = m->d->stream;
+    const size_t nslot = (size_t)nl * 256 * 2;
+    unsigned long long *tl = nullptr;
+    MIO_HIP_CHECK(hipMalloc(&tl, sizeof(unsigned long long) * nslot));
+    hipGraph_t g = nullptr;
+    hipGraphExec_t ge = nullptr;
+    MIO_HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+    rc = issue_step(m, m->graph_cfg, tl);
+    MIO_HIP_CHECK(hipStreamEndCapture(s, &g));
+    MIO_HIP_CHECK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+    for (int rep = 0; rep < 3; ++rep) {
+        MIO_HIP_CHECK(hipMemsetAsync(tl, 0, sizeof(unsigned long long) * nslot, s));
+        MIO_HIP_CHECK(hipGraphLaunch(ge, s));
+    }
+    std::vector<unsigned long long> h(nslot);
+    MIO_HIP_CHECK(hipMemcpyAsync(h.data(), tl, sizeof(unsigned long long) * nslot, hipMemcpyDeviceToHost, s));
+    MIO_HIP_CHECK(hipStreamSynchronize(s));
+    std::memcpy(out, h.data(), sizeof(unsigned long long) * nslot);
+    hipGraphExecDestroy(ge);
+    hipGraphDestroy(g);
+    hipFree(tl);
+    *n_launches = nl;
     return MIO_OK;
 }

@@ -86,6 +86,7 @@ def _declare(L: ctypes.CDLL) -> None:
         "mio_wav_encode": (c_int, [_vp, c_int, c_int, _vp, c_int, ctypes.POINTER(c_int)]),
         "mio_hip_llm_time_kernel": (c_int, [_vp, c_int, c_int, _f32p, ctypes.POINTER(ctypes.c_uint64)]),
         "mio_hip_llm_trace_kernel": (c_int, [_vp, c_int, _vp]),
+        "mio_hip_llm_timeline": (c_int, [_vp, _vp, c_int, ctypes.POINTER(c_int)]),
         "mio_hip_codec_last_timings": (c_int, [_vp, _f32p]),
         "mio_hip_debug_matvec": (c_int, [_vp, ctypes.c_uint32, _vp, c_int, c_int, _vp, _vp]),
         "mio_quantize_rows": (c_int, [ctypes.c_uint32, _vp, c_int, c_int, _vp]),
@@ -393,6 +394,16 @@ class Llm:
         out = np.zeros(32, np.uint64)
         check(lib().mio_hip_llm_trace_kernel(self.h, which, _ptr(out)))
         return out
+
+    def timeline(self) -> np.ndarray:
+        """Per-launch, per-workgroup [start, end] (us from the step start, NaN = absent) of one
+        graph-replayed step (diagnostic, mio_hip_llm_timeline; advances the decode state)."""
+        out = np.zeros(1024 * 256 * 2, np.uint64)
+        n = ctypes.c_int(0)
+        check(lib().mio_hip_llm_timeline(self.h, _ptr(out), 1024, ctypes.byref(n)))
+        t = out[: n.value * 512].astype(np.float64).reshape(n.value, 256, 2)
+        t[t == 0] = np.nan
+        return (t - np.nanmin(t[0, :, 0])) * 0.01
 
     def generate(self, prompt, max_tokens: int, temperature: float = 0.8, seed: int = 42,
                  allow=(-1, -1), eos=(-1, -1), check_interval: int = 20) -> np.ndarray:

@@ -1,0 +1,41 @@
+"""Diagnostic: timeline of one graph-replayed decode step (1.7B preset by default): per
+kernel the duration (first workgroup start -> last workgroup end), the spread of workgroup
+start and end times, and the gaps between consecutive launches. Run on the GPU box:
+    python tools/step_timeline.py [--preset 3] [--pos 700]"""
+import argparse
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "miotts-llama.cpp_amd", "python"))
+import numpy as np  # noqa: E402
+import miotts_amd as m  # noqa: E402
+
+p = argparse.ArgumentParser()
+p.add_argument("--preset", type=int, default=3)
+p.add_argument("--pos", type=int, default=700)
+a = p.parse_args()
+path = f"/tmp/trace_llm{a.preset}.gguf"
+if not os.path.exists(path):
+    m.synth_llm(path, a.preset, 1)
+dev = m.Device(0)
+llm = m.Llm(dev, path, 2048)
+llm.generate([256, 257, 65, 258, 257], a.pos, 0.8, 1, allow=(m.SYNTH_SPEECH0, m.SYNTH_SPEECH0 + 12800),
+             check_interval=50)
+t = llm.timeline()
+nl = t.shape[0]
+names = ["attn_in", "attention", "attn_out", "ffn_in", "ffn_down"] * ((nl - 2) // 5) + ["lm_head", "sample"]
+s0 = np.nanmin(t[:, :, 0], axis=1)
+s1 = np.nanmax(t[:, :, 0], axis=1)
+e0 = np.nanmin(t[:, :, 1], axis=1)
+e1 = np.nanmax(t[:, :, 1], axis=1)
+wd = np.nanmedian(t[:, :, 1] - t[:, :, 0], axis=1)
+dur = e1 - s0
+gap = np.r_[0.0, s0[1:] - e1[:-1]]
+print(f"step wall {e1[-1] - s0[0]:.1f} us over {nl} launches; kernel time {dur.sum():.1f} us, "
+      f"gaps {gap[1:].sum():.1f} us (mean {gap[1:].mean():.2f}, min {gap[1:].min():.2f}, max {gap[1:].max():.2f})")
+print("  kernel      dur    gap-before  start-spread  end-spread  median-wg")
+for k in ["attn_in", "attention", "attn_out", "ffn_in", "ffn_down", "lm_head", "sample"]:
+    idx = [i for i, n in enumerate(names) if n == k]
+    print(f"  {k:10s} {dur[idx].mean():6.2f} {gap[idx].mean():8.2f} {(s1 - s0)[idx].mean():12.2f} "
+          f"{(e1 - e0)[idx].mean():11.2f} {wd[idx].mean():10.2f}")
