@@ -39,6 +39,7 @@ typedef struct mio_hip_device mio_hip_device;
 typedef struct mio_hip_istft mio_hip_istft;
 typedef struct mio_hip_codec mio_hip_codec;
 typedef struct mio_hip_llm mio_hip_llm;
+typedef struct mio_tokenizer mio_tokenizer;
 
 /* ---------------- device / memory ---------------- */
 const char *mio_hip_last_error(void);
@@ -155,6 +156,21 @@ int mio_quantize_rows(uint32_t type, const float *x, int rows, int k, void *out)
 int mio_normalize_tts_text(const char *text, char *out, int cap, int *out_len);
 int mio_parse_speech_tokens(const char *text, int32_t *codes, int cap, int *n);
 int mio_wav_encode(const float *samples, int n, int sample_rate, uint8_t *out, int cap, int *out_len);
+
+/* ---------------- GGUF tokenizer ----------------
+ * Replaces llama_tokenize(vocab, text, add_special, parse_special) (test-to-speech.cpp:117-125),
+ * llama_token_to_piece(..., special=true) (:173-176), llama_vocab_eos (:150) and the
+ * "<|im_end|>" lookup (:151-159) for gpt2-type (byte-level BPE) GGUF vocabularies.
+ * info[4] = {n_vocab, bos, eos, im_end (-1 if not a single token)}. */
+int mio_tokenizer_load(const char *gguf_path, mio_tokenizer **out);
+void mio_tokenizer_free(mio_tokenizer *t);
+int mio_tokenizer_info(const mio_tokenizer *t, int *info);
+int mio_tokenize(const mio_tokenizer *t, const char *text, int add_special, int parse_special, int32_t *out,
+                 int cap, int *n);
+int mio_token_piece(const mio_tokenizer *t, int32_t id, char *out, int cap, int *len);
+/* Streaming commit cadence (test-to-speech.cpp:496-571) for n_tokens speech tokens:
+ * number of codec decode calls and total decoded codes (KAT: 700 -> 18 / 7160). */
+int mio_stream_cadence(int n_tokens, int *decode_calls, int64_t *decoded_codes);
 
 /* ---------------- synthetic model files ----------------
  * No GGUF model files exist offline. These write files with the

@@ -1,0 +1,309 @@
+// GGUF byte-level BPE tokenizer (see tokenizer.h).
+#include "tokenizer.h"
+
+#include <algorithm>
+#include <climits>
+#include <set>
+
+#include "common.h"
+#include "gguf.h"
+
+namespace mio {
+namespace {
+
+// ------------------------------------------------------------------ UTF-8
+uint32_t utf8_decode(const std::string &s, size_t i, size_t *len) {
+    const uint8_t c = (uint8_t)s[i];
+    auto cont = [&](size_t k) { return i + k < s.size() ? ((uint8_t)s[i + k] & 0x3F) : 0u; };
+    if (c < 0x80) return *len = 1, c;
+    if ((c >> 5) == 6 && i + 1 < s.size()) return *len = 2, ((c & 0x1Fu) << 6) | cont(1);
+    if ((c >> 4) == 14 && i + 2 < s.size()) return *len = 3, ((c & 0x0Fu) << 12) | (cont(1) << 6) | cont(2);
+    if ((c >> 3) == 30 && i + 3 < s.size())
+        return *len = 4, ((c & 0x07u) << 18) | (cont(1) << 12) | (cont(2) << 6) | cont(3);
+    return *len = 1, c;  // invalid byte: passed through as its own "code point"
+}
+
+std::string utf8_encode(uint32_t cp) {
+    std::string o;
+    if (cp < 0x80) {
+        o += (char)cp;
+    } else if (cp < 0x800) {
+        o += (char)(0xC0 | (cp >> 6));
+        o += (char)(0x80 | (cp & 0x3F));
+    } else if (cp < 0x10000) {
+        o += (char)(0xE0 | (cp >> 12));
+        o += (char)(0x80 | ((cp >> 6) & 0x3F));
+        o += (char)(0x80 | (cp & 0x3F));
+    } else {
+        o += (char)(0xF0 | (cp >> 18));
+        o += (char)(0x80 | ((cp >> 12) & 0x3F));
+        o += (char)(0x80 | ((cp >> 6) & 0x3F));
+        o += (char)(0x80 | (cp & 0x3F));
+    }
+    return o;
+}
+
+// ------------------------------------------------------------------ Unicode classes
+struct R {
+    uint32_t a, b;
+};
+
+bool in(const R *r, size_t n, uint32_t cp) {
+    for (size_t i = 0; i < n; ++i)
+        if (cp >= r[i].a && cp <= r[i].b) return true;
+    return false;
+}
+
+bool is_space(uint32_t cp) {
+    static const R r[] = {{0x09, 0x0D}, {0x20, 0x20}, {0x85, 0x85}, {0xA0, 0xA0}, {0x1680, 0x1680},
+                          {0x2000, 0x200A}, {0x2028, 0x2029}, {0x202F, 0x202F}, {0x205F, 0x205F}, {0x3000, 0x3000}};
+    return in(r, sizeof(r) / sizeof(r[0]), cp);
+}
+
+bool is_number(uint32_t cp) {
+    static const R r[] = {{0x30, 0x39},     {0xB2, 0xB3},     {0xB9, 0xB9},     {0xBC, 0xBE},     {0x660, 0x669},
+                          {0x6F0, 0x6F9},   {0x966, 0x96F},   {0x2070, 0x2070}, {0x2074, 0x2079}, {0x2080, 0x2089},
+                          {0x2150, 0x2182}, {0x2185, 0x2189}, {0x2460, 0x249B}, {0x24EA, 0x24FF}, {0x2776, 0x2793},
+                          {0x3007, 0x3007}, {0x3021, 0x3029}, {0x3038, 0x303A}, {0x3192, 0x3195}, {0x3220, 0x3229},
+                          {0x3248, 0x324F}, {0x3251, 0x325F}, {0x3280, 0x3289}, {0x32B1, 0x32BF}, {0xFF10, 0xFF19}};
+    return in(r, sizeof(r) / sizeof(r[0]), cp);
+}
+
+bool is_letter(uint32_t cp) {
+    static const R r[] = {
+        {0x41, 0x5A},       {0x61, 0x7A},     {0xAA, 0xAA},     {0xB5, 0xB5},     {0xBA, 0xBA},     {0xC0, 0xD6},
+        {0xD8, 0xF6},       {0xF8, 0x2C1},    {0x2C6, 0x2D1},   {0x2E0, 0x2E4},   {0x2EC, 0x2EC},   {0x2EE, 0x2EE},
+        {0x370, 0x374},     {0x376, 0x377},   {0x37A, 0x37D},   {0x37F, 0x37F},   {0x386, 0x386},   {0x388, 0x3F5},
+        {0x3F7, 0x481},     {0x48A, 0x52F},   {0x531, 0x556},   {0x561, 0x587},   {0x5D0, 0x5EA},   {0x620, 0x64A},
+        {0x671, 0x6D3},     {0x904, 0x939},   {0xE01, 0xE30},   {0x10A0, 0x10FF}, {0x1100, 0x11FF}, {0x1E00, 0x1FBC},
+        {0x1FC2, 0x1FCC},   {0x1FD0, 0x1FDB}, {0x1FE0, 0x1FEC}, {0x1FF2, 0x1FFC}, {0x2071, 0x2071}, {0x207F, 0x207F},
+        {0x2090, 0x209C},   {0x2102, 0x2102}, {0x2107, 0x2107}, {0x210A, 0x2113}, {0x2115, 0x2115}, {0x2119, 0x211D},
+        {0x2124, 0x2124},   {0x2126, 0x2126}, {0x2128, 0x2128}, {0x212A, 0x212D}, {0x212F, 0x2139}, {0x2C00, 0x2CE4},
+        {0x3005, 0x3006},   {0x3031, 0x3035}, {0x303B, 0x303C}, {0x3041, 0x3096}, {0x309D, 0x309F}, {0x30A1, 0x30FA},
+        {0x30FC, 0x30FF},   {0x3105, 0x312F}, {0x3131, 0x318E}, {0x31A0, 0x31BF}, {0x31F0, 0x31FF}, {0x3400, 0x4DBF},
+        {0x4E00, 0x9FFF},   {0xA000, 0xA48C}, {0xAC00, 0xD7A3}, {0xF900, 0xFAFF}, {0xFF21, 0xFF3A}, {0xFF41, 0xFF5A},
+        {0xFF66, 0xFFBE},   {0x20000, 0x2FA1F}};
+    return in(r, sizeof(r) / sizeof(r[0]), cp);
+}
+
+bool is_nl(uint32_t cp) { return cp == '\r' || cp == '\n'; }
+uint32_t lower_ascii(uint32_t cp) { return cp >= 'A' && cp <= 'Z' ? cp + 32 : cp; }
+
+}  // namespace
+
+// ------------------------------------------------------------------ load
+bool BpeTokenizer::load(const GgufFile &g) {
+    const std::string model = g.get_str("tokenizer.ggml.model");
+    const GgufValue *tv = g.get("tokenizer.ggml.tokens");
+    if (model != "gpt2" || !tv || tv->arr_s.empty()) {
+        set_error("tokenizer: GGUF has no gpt2 (byte-level BPE) vocabulary (model '%s')", model.c_str());
+        return false;
+    }
+    tokens_ = tv->arr_s;
+    types_.assign(tokens_.size(), 1);
+    if (const GgufValue *tt = g.get("tokenizer.ggml.token_type"))
+        for (size_t i = 0; i < tt->arr_i.size() && i < types_.size(); ++i) types_[i] = (int32_t)tt->arr_i[i];
+    id_.reserve(tokens_.size() * 2);
+    for (size_t i = 0; i < tokens_.size(); ++i) id_.emplace(tokens_[i], (int32_t)i);
+    if (const GgufValue *mv = g.get("tokenizer.ggml.merges"))
+        for (size_t i = 0; i < mv->arr_s.size(); ++i) merge_rank_.emplace(mv->arr_s[i], (int)i);
+    std::set<size_t, std::greater<size_t>> lens;
+    for (size_t i = 0; i < tokens_.size(); ++i)
+        if ((types_[i] == 3 || types_[i] == 4) && !tokens_[i].empty()) {  // CONTROL, USER_DEFINED
+            special_.emplace(tokens_[i], (int32_t)i);
+            lens.insert(tokens_[i].size());
+        }
+    special_lens_.assign(lens.begin(), lens.end());
+    eos_ = (int32_t)g.get_int("tokenizer.ggml.eos_token_id", -1);
+    bos_ = (int32_t)g.get_int("tokenizer.ggml.bos_token_id", -1);
+    const GgufValue *ab = g.get("tokenizer.ggml.add_bos_token");
+    add_bos_ = ab ? ab->u != 0 : false;
+    const std::string pre = g.get_str("tokenizer.ggml.pre", "default");
+    qwen2_ = pre == "qwen2";
+    // GPT-2 bytes_to_unicode: printable bytes map to themselves, the rest to 256 + n
+    int n = 0;
+    for (int b = 0; b < 256; ++b) {
+        const bool keep = (b >= 33 && b <= 126) || (b >= 161 && b <= 172) || (b >= 174 && b <= 255);
+        const uint32_t cp = keep ? (uint32_t)b : (uint32_t)(256 + n++);
+        byte_enc_[b] = utf8_encode(cp);
+        byte_dec_[cp] = (uint8_t)b;
+    }
+    return true;
+}
+
+int32_t BpeTokenizer::special_id(const std::string &text) const {
+    const auto it = special_.find(text);
+    return it == special_.end() ? -1 : it->second;
+}
+
+// ------------------------------------------------------------------ pre-tokenizer
+// qwen2: (?i:'s|'t|'re|'ve|'m|'ll|'d)|[^\r\n\p{L}\p{N}]?\p{L}+|\p{N}| ?[^\s\p{L}\p{N}]+[\r\n]*|\s*[\r\n]+|\s+(?!\S)|\s+
+// gpt2 : 's|'t|'re|'ve|'m|'ll|'d| ?\p{L}+| ?\p{N}+| ?[^\s\p{L}\p{N}]+|\s+(?!\S)|\s+
+void BpeTokenizer::pretokenize(const std::string &text, std::vector<std::string> &pieces) const {
+    std::vector<uint32_t> cp;
+    std::vector<size_t> off;
+    for (size_t i = 0; i < text.size();) {
+        size_t l = 1;
+        cp.push_back(utf8_decode(text, i, &l));
+        off.push_back(i);
+        i += l;
+    }
+    off.push_back(text.size());
+    const size_t n = cp.size();
+    auto L = [&](size_t k) { return k < n && is_letter(cp[k]); };
+    auto N = [&](size_t k) { return k < n && is_number(cp[k]); };
+    auto S = [&](size_t k) { return k < n && is_space(cp[k]); };
+    auto other = [&](size_t k) { return k < n && !is_space(cp[k]) && !is_letter(cp[k]) && !is_number(cp[k]); };
+    size_t i = 0;
+    while (i < n) {
+        size_t m = 0;  // match length in code points
+        // contractions
+        if (cp[i] == '\'' && i + 1 < n) {
+            const uint32_t a = qwen2_ ? lower_ascii(cp[i + 1]) : cp[i + 1];
+            const uint32_t b = i + 2 < n ? (qwen2_ ? lower_ascii(cp[i + 2]) : cp[i + 2]) : 0;
+            if (a == 's' || a == 't' || a == 'm' || a == 'd')
+                m = 2;
+            else if ((a == 'r' && b == 'e') || (a == 'v' && b == 'e') || (a == 'l' && b == 'l'))
+                m = 3;
+        }
+        if (!m && qwen2_) {
+            // [^\r\n\p{L}\p{N}]?\p{L}+
+            size_t k = i;
+            if (!L(k) && k < n && !is_nl(cp[k]) && !N(k) && L(k + 1)) ++k;
+            if (L(k)) {
+                while (L(k)) ++k;
+                m = k - i;
+            }
+            // \p{N}
+            if (!m && N(i)) m = 1;
+        } else if (!m) {
+            size_t k = i + (cp[i] == ' ' ? 1 : 0);
+            if (L(k)) {
+                while (L(k)) ++k;
+                m = k - i;
+            } else if (N(k)) {
+                while (N(k)) ++k;
+                m = k - i;
+            }
+        }
+        if (!m) {
+            // ' ?[^\s\p{L}\p{N}]+' (+ '[\r\n]*' for qwen2)
+            size_t k = i + (cp[i] == ' ' ? 1 : 0);
+            if (other(k)) {
+                while (other(k)) ++k;
+                if (qwen2_)
+                    while (k < n && is_nl(cp[k])) ++k;
+                m = k - i;
+            }
+        }
+        if (!m && S(i)) {
+            size_t j = i;
+            while (S(j)) ++j;
+            if (qwen2_) {
+                // \s*[\r\n]+ : up to the last newline of the whitespace run
+                size_t last = SIZE_MAX;
+                for (size_t k = i; k < j; ++k)
+                    if (is_nl(cp[k])) last = k;
+                if (last != SIZE_MAX) m = last + 1 - i;
+            }
+            if (!m) {
+                // \s+(?!\S) then \s+
+                if (j == n || j - i == 1)
+                    m = j - i;
+                else
+                    m = j - i - 1;
+            }
+        }
+        if (!m) m = 1;
+        pieces.emplace_back(text.substr(off[i], off[i + m] - off[i]));
+        i += m;
+    }
+}
+
+// ------------------------------------------------------------------ BPE
+void BpeTokenizer::bpe(const std::string &piece, std::vector<int32_t> &out) const {
+    std::vector<std::string> sym;
+    for (unsigned char c : piece) sym.push_back(byte_enc_[c]);
+    if (sym.empty()) return;
+    while (sym.size() > 1 && !merge_rank_.empty()) {
+        int best = INT_MAX;
+        size_t at = 0;
+        for (size_t k = 0; k + 1 < sym.size(); ++k) {
+            const auto it = merge_rank_.find(sym[k] + " " + sym[k + 1]);
+            if (it != merge_rank_.end() && it->second < best) best = it->second, at = k;
+        }
+        if (best == INT_MAX) break;
+        sym[at] += sym[at + 1];
+        sym.erase(sym.begin() + at + 1);
+    }
+    for (const std::string &s : sym) {
+        const auto it = id_.find(s);
+        if (it != id_.end()) {
+            out.push_back(it->second);
+            continue;
+        }
+        // not in the vocabulary: fall back to its single-byte symbols
+        for (size_t i = 0; i < s.size();) {
+            size_t l = 1;
+            utf8_decode(s, i, &l);
+            const auto jt = id_.find(s.substr(i, l));
+            if (jt != id_.end()) out.push_back(jt->second);
+            i += l;
+        }
+    }
+}
+
+std::vector<int32_t> BpeTokenizer::tokenize(const std::string &text, bool add_special, bool parse_special) const {
+    std::vector<int32_t> out;
+    if (add_special && add_bos_ && bos_ >= 0) out.push_back(bos_);
+    std::string run;
+    auto flush = [&]() {
+        if (run.empty()) return;
+        std::vector<std::string> pieces;
+        pretokenize(run, pieces);
+        for (const std::string &p : pieces) bpe(p, out);
+        run.clear();
+    };
+    for (size_t i = 0; i < text.size();) {
+        int32_t sid = -1;
+        size_t slen = 0;
+        if (parse_special)
+            for (size_t l : special_lens_) {
+                if (l > text.size() - i) continue;
+                const auto it = special_.find(text.substr(i, l));
+                if (it != special_.end()) {
+                    sid = it->second, slen = l;
+                    break;
+                }
+            }
+        if (sid >= 0) {
+            flush();
+            out.push_back(sid);
+            i += slen;
+        } else {
+            run += text[i++];
+        }
+    }
+    flush();
+    return out;
+}
+
+std::string BpeTokenizer::piece(int32_t id) const {
+    if (id < 0 || id >= (int32_t)tokens_.size()) return "";
+    const std::string &t = tokens_[id];
+    if (types_[id] == 3 || types_[id] == 4) return t;  // special: rendered as text
+    std::string o;
+    for (size_t i = 0; i < t.size();) {
+        size_t l = 1;
+        const uint32_t c = utf8_decode(t, i, &l);
+        const auto it = byte_dec_.find(c);
+        if (it != byte_dec_.end())
+            o += (char)it->second;
+        else
+            o += t.substr(i, l);
+        i += l;
+    }
+    return o;
+}
+
+}  // namespace mio

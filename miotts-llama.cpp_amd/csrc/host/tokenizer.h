@@ -1,0 +1,57 @@
+// GGUF byte-level BPE tokenizer (tokenizer.ggml.model == "gpt2": Qwen2/Qwen3/Llama-3
+// style vocabularies, which the MioTTS LLMs use). Replaces the llama_vocab calls of
+// TestToSpeech::run_llm: llama_tokenize(text, add_special=true, parse_special=true)
+// (test-to-speech.cpp:117-125), the "<|im_end|>" lookup (:150-159), llama_vocab_eos
+// (:150) and llama_token_to_piece(..., special=true) (:173-176).
+//
+// Algorithm (the public GPT-2 / llama.cpp BPE scheme, restated):
+//   1. split the text on special tokens (token_type CONTROL / USER_DEFINED), longest match;
+//   2. pre-tokenize the remaining runs with the vocabulary's regex ("qwen2" or GPT-2
+//      default), evaluated on code points with built-in Unicode letter/number/space classes;
+//   3. map each piece's bytes through the GPT-2 byte->unicode table and apply the merges in
+//      rank order; pieces are then looked up in the vocabulary (bytes as a fallback).
+// Parity is unpinned: llama.cpp is absent here and the Unicode class tables are a compact
+// restatement (Latin, Greek, Cyrillic, CJK, kana, Hangul, fullwidth forms), see DESIGN.md.
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+namespace mio {
+
+class GgufFile;
+
+class BpeTokenizer {
+public:
+    // false + set_error when the GGUF has no usable tokenizer
+    bool load(const GgufFile &g);
+
+    std::vector<int32_t> tokenize(const std::string &text, bool add_special, bool parse_special) const;
+    // token text as llama_token_to_piece(special=true) renders it (bytes for normal tokens)
+    std::string piece(int32_t id) const;
+    int32_t eos() const { return eos_; }
+    int32_t bos() const { return bos_; }
+    // id of a single-token special text, -1 when it is not one token
+    int32_t special_id(const std::string &text) const;
+    int n_vocab() const { return (int)tokens_.size(); }
+
+private:
+    void bpe(const std::string &piece, std::vector<int32_t> &out) const;
+    void pretokenize(const std::string &text, std::vector<std::string> &pieces) const;
+
+    std::vector<std::string> tokens_;
+    std::vector<int32_t> types_;
+    std::unordered_map<std::string, int32_t> id_;
+    std::unordered_map<std::string, int> merge_rank_;  // "left right" -> rank
+    std::unordered_map<std::string, int32_t> special_;  // special text -> id
+    std::vector<size_t> special_lens_;                  // distinct lengths, descending
+    std::string byte_enc_[256];                          // byte -> UTF-8 of its unicode stand-in
+    std::unordered_map<uint32_t, uint8_t> byte_dec_;     // stand-in code point -> byte
+    int32_t eos_ = -1, bos_ = -1;
+    bool add_bos_ = false;
+    bool qwen2_ = false;
+};
+
+}  // namespace mio

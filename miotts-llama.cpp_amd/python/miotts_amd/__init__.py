@@ -86,6 +86,12 @@ def _declare(L: ctypes.CDLL) -> None:
         "mio_wav_encode": (c_int, [_vp, c_int, c_int, _vp, c_int, ctypes.POINTER(c_int)]),
         "mio_hip_llm_time_kernel": (c_int, [_vp, c_int, c_int, _f32p, ctypes.POINTER(ctypes.c_uint64)]),
         "mio_hip_llm_trace_kernel": (c_int, [_vp, c_int, _vp]),
+        "mio_tokenizer_load": (c_int, [ctypes.c_char_p, ctypes.POINTER(_vp)]),
+        "mio_stream_cadence": (c_int, [c_int, ctypes.POINTER(c_int), ctypes.POINTER(ctypes.c_int64)]),
+        "mio_tokenizer_free": (None, [_vp]),
+        "mio_tokenizer_info": (c_int, [_vp, ctypes.POINTER(c_int)]),
+        "mio_tokenize": (c_int, [_vp, ctypes.c_char_p, c_int, c_int, _vp, c_int, ctypes.POINTER(c_int)]),
+        "mio_token_piece": (c_int, [_vp, ctypes.c_int32, ctypes.c_char_p, c_int, ctypes.POINTER(c_int)]),
         "mio_hip_llm_timeline": (c_int, [_vp, _vp, c_int, ctypes.POINTER(c_int)]),
         "mio_hip_codec_last_timings": (c_int, [_vp, _f32p]),
         "mio_hip_debug_matvec": (c_int, [_vp, ctypes.c_uint32, _vp, c_int, c_int, _vp, _vp]),
@@ -435,6 +441,50 @@ def debug_matvec(dev: Device, qtype: int, w_rows: np.ndarray, k: int, x: np.ndar
     y = np.empty(w_rows.shape[0], np.float32)
     check(lib().mio_hip_debug_matvec(dev.h, qtype, _ptr(w_rows), w_rows.shape[0], k, _ptr(x), _ptr(y)))
     return y
+
+
+# ---------------------------------------------------------------- tokenizer
+class Tokenizer:
+    """GGUF byte-level BPE tokenizer (csrc/host/tokenizer.h) through the C-ABI: llama_tokenize /
+    llama_token_to_piece / llama_vocab_eos equivalents (test-to-speech.cpp:117-176)."""
+
+    def __init__(self, gguf_path: str):
+        h = _vp()
+        check(lib().mio_tokenizer_load(gguf_path.encode(), ctypes.byref(h)))
+        self.h = h
+        info = (ctypes.c_int * 4)()
+        check(lib().mio_tokenizer_info(self.h, info))
+        self.n_vocab, self.bos, self.eos, self.im_end = list(info)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().mio_tokenizer_free(self.h)
+            self.h = None
+
+    def tokenize(self, text: str, add_special: bool = True, parse_special: bool = True) -> list:
+        b = text.encode("utf-8")
+        cap = len(b) + 16
+        out = np.zeros(cap, np.int32)
+        n = ctypes.c_int(0)
+        check(lib().mio_tokenize(self.h, b, int(add_special), int(parse_special), _ptr(out), cap, ctypes.byref(n)))
+        return out[: n.value].tolist()
+
+    def piece(self, tok: int) -> bytes:
+        cap = 1024
+        buf = ctypes.create_string_buffer(cap)
+        n = ctypes.c_int(0)
+        check(lib().mio_token_piece(self.h, int(tok), buf, cap, ctypes.byref(n)))
+        return buf.raw[: n.value]
+
+    def detokenize(self, toks) -> str:
+        return b"".join(self.piece(t) for t in toks).decode("utf-8", errors="replace")
+
+
+def stream_cadence(n_tokens: int):
+    """(decode_calls, decoded_codes) of the streaming commit policy for n_tokens codes."""
+    c, k = ctypes.c_int(0), ctypes.c_int64(0)
+    check(lib().mio_stream_cadence(int(n_tokens), ctypes.byref(c), ctypes.byref(k)))
+    return c.value, k.value
 
 
 # ---------------------------------------------------------------- host text utilities

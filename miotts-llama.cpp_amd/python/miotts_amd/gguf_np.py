@@ -98,3 +98,31 @@ class GGUFReader:
 
     def tensor(self, name: str) -> Tensor:
         return self.by_name[name]
+
+
+def write_kv_gguf(path: str, kv: Dict[str, Any]) -> None:
+    """Minimal GGUF v3 writer (metadata only, no tensors) for tokenizer tests.
+    Values: str, bool, int (u32), float (f32), list[str], list[int] (i32)."""
+    def s(x: str) -> bytes:
+        b = x.encode("utf-8")
+        return struct.pack("<Q", len(b)) + b
+
+    out = bytearray(b"GGUF" + struct.pack("<IQQ", 3, 0, len(kv)))
+    for k, v in kv.items():
+        out += s(k)
+        if isinstance(v, bool):
+            out += struct.pack("<I?", 7, v)
+        elif isinstance(v, int):
+            out += struct.pack("<II", 4, v)
+        elif isinstance(v, float):
+            out += struct.pack("<If", 6, v)
+        elif isinstance(v, str):
+            out += struct.pack("<I", 8) + s(v)
+        elif isinstance(v, list) and (not v or isinstance(v[0], str)):
+            out += struct.pack("<IIQ", 9, 8, len(v)) + b"".join(s(x) for x in v)
+        elif isinstance(v, list):
+            out += struct.pack("<IIQ", 9, 5, len(v)) + b"".join(struct.pack("<i", x) for x in v)
+        else:
+            raise TypeError(k)
+    with open(path, "wb") as f:
+        f.write(bytes(out))
