@@ -4,18 +4,24 @@
 Metric (BASELINE.json): realtime factor (audio s / wall s) + stage ms llm/codec/istft on
 MioTTS-1.7B Q4_K_M (configs[2]): one "step" = one whole utterance of the reference
 pipeline (test-to-speech.cpp:94-246): chat-template prompt -> prefill -> 700 sampled
-speech tokens (temp 0.8, device sampler, speech ids only so synthetic weights yield
+speech tokens (temp 0.8, on-device sampler, speech ids only so synthetic weights yield
 exactly 700 codes: flagged harness deviation) -> MioCodec decode -> iSTFT ->
-PCM in host memory. Weights are synthetic (no checkpoints offline) with the
-published shapes; "data": "synthetic".
+PCM left in HBM (`value`; the PCIe-inclusive rate with the PCM copied to host memory is
+reported beside it as `value_pcie_inclusive`). Weights are synthetic (no checkpoints
+offline) with the published shapes; "data": "synthetic".
 
 Multi-GPU: one process per GPU (torchrun), each rank synthesizes its own utterances
 (utterances are independent: no collective on the data path, "scaling": "weak"); a gloo
 barrier brackets the timed region and the max elapsed over ranks is used.
 
-roofline: the decode-step kernel with the largest per-token time, timed live with HIP
-events on the runner's stream (mio_hip_llm_time_kernel) after the timed region;
-achieved = its algorithmic bytes per launch / mean launch time; peak = 8 TB/s HBM3E.
+roofline: the dominant decode-step kernel (largest time per token), timed inside the
+captured step graph by the step timeline (first workgroup start -> last workgroup end of
+every launch, s_memrealtime, mio_hip_llm_timeline) right after the timed region:
+achieved = its algorithmic bytes per launch (GGUF bytes of the matrices it streams + its
+activations) / mean launch duration; peak = 8 TB/s HBM3E. traffic = the same kernel's
+HBM bytes per launch from rocprofv3 PMC (FETCH_SIZE x 2 on gfx950 + WRITE_SIZE,
+profiles/pmc_traffic.json, tools/pmc_traffic.py). HIP-event timing of back-to-back
+launches of the same kernel is reported as event_avg_launch_us (cache-warm).
 cpu_baseline: the C oracle (oracle/, "port") on rank 0 at N=1 only, timed on a bounded
 sample (decode steps + codec/iSTFT of a few codes) and extrapolated to one utterance.
 """
@@ -130,12 +136,17 @@ def main():
     stage = {"llm_ms": 0.0, "codec_ms": 0.0, "istft_ms": 0.0, "codec_wall_ms": 0.0}
     audio_samples = 0
 
+    d_emb = dev.upload(np.ascontiguousarray(emb, np.float32))
+    d_pcm = dev.empty((a.tokens * codec.samples_per_token,), np.float32)
+
     def utterance(seed, record):
         nonlocal audio_samples
         t0 = time.perf_counter()
         toks = llm.generate(prompt, a.tokens, 0.8, seed, allow=allow, check_interval=20)
         t1 = time.perf_counter()
-        pcm = codec.decode_pcm(toks - m.SYNTH_SPEECH0, emb)
+        d_codes = dev.upload((toks - m.SYNTH_SPEECH0).astype(np.int32))
+        n = codec.decode_pcm_device(d_codes, len(toks), d_emb, d_pcm)
+        dev.sync()
         t2 = time.perf_counter()
         if record:
             c_ms, i_ms = codec.last_timings()
@@ -143,9 +154,9 @@ def main():
             stage["codec_wall_ms"] += (t2 - t1) * 1e3
             stage["codec_ms"] += c_ms
             stage["istft_ms"] += i_ms
-            audio_samples += len(pcm)
-        if len(toks) != a.tokens or len(pcm) != a.tokens * codec.samples_per_token:
-            raise RuntimeError(f"utterance produced {len(toks)} tokens / {len(pcm)} samples")
+            audio_samples += n
+        if len(toks) != a.tokens or n != a.tokens * codec.samples_per_token:
+            raise RuntimeError(f"utterance produced {len(toks)} tokens / {n} samples")
 
     for w in range(a.warmup):
         for u in range(a.utts_per_step):
@@ -172,22 +183,39 @@ def main():
     audio_s = total_samples / codec.sample_rate
     value = audio_s / elapsed
 
-    # roofline of the dominant decode-step kernel, timed live on the runner's stream
-    per_token = {}
+    # PCIe-inclusive: the PCM of one utterance copied to host memory (never `value`)
+    t0 = time.perf_counter()
+    for _ in range(3):
+        d_pcm.numpy()
+    d2h_s = (time.perf_counter() - t0) / 3
+    value_pcie = audio_s / (elapsed + d2h_s * a.steps * a.utts_per_step * world)
+
+    # roofline: dominant kernel inside the captured step graph (timeline), then HIP events
+    tl = llm.timeline()
+    nl = tl.shape[0]
+    names = [KERNEL_NAMES[k] for k in (0, 1, 2, 3, 4)] * ((nl - 2) // 5) + [KERNEL_NAMES[6], "k_sample"]
+    dur = np.nanmax(tl[:, :, 1], axis=1) - np.nanmin(tl[:, :, 0], axis=1)
+    step_wall_us = float(np.nanmax(tl[-1, :, 1]) - np.nanmin(tl[0, :, 0]))
+    per_kernel = {}
+    for i, nm in enumerate(names):
+        per_kernel.setdefault(nm, []).append(float(dur[i]))
+    bytes_of = {}
+    event_us = {}
     for which in (0, 1, 2, 3, 4, 6):
         ms, by = llm.time_kernel(which, 40)
-        count = 1 if which == 6 else llm.n_layer
-        per_token[which] = (ms * count, ms, by)
-    dom = max((w for w in per_token if per_token[w][2] > 0), key=lambda w: per_token[w][0])
-    _, dom_ms, dom_bytes = per_token[dom]
-    achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
+        bytes_of[KERNEL_NAMES[which]] = by
+        event_us[KERNEL_NAMES[which]] = ms * 1e3
+    dom = max((k for k in bytes_of if bytes_of[k] > 0), key=lambda k: sum(per_kernel[k]))
+    dom_us = float(np.mean(per_kernel[dom]))
+    dom_bytes = bytes_of[dom]
+    achieved = dom_bytes / (dom_us * 1e-6) / 1e9
     traffic = None
     tfile = os.path.join(REPO, "profiles", "pmc_traffic.json")
     if os.path.exists(tfile):
         try:
             tj = json.load(open(tfile))
             if tj.get("preset") == a.preset:
-                traffic = tj.get("per_launch_bytes", {}).get(KERNEL_NAMES[dom])
+                traffic = tj.get("per_launch_bytes", {}).get(dom)
         except Exception:
             traffic = None
 
@@ -211,12 +239,15 @@ def main():
                    "seq_len": a.tokens, "parallelism": f"utterance-sharded x{world} (no collective)"},
         "stage_ms": {k: round(v / steps_total, 3) for k, v in stage.items()},
         "llm_ms_per_token": round(stage["llm_ms"] / steps_total / a.tokens, 4),
-        "roofline": {"bound": "hbm", "kernel": KERNEL_NAMES[dom], "achieved": round(achieved, 1),
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "bytes_per_launch": dom_bytes,
-                     "avg_launch_us": round(dom_ms * 1e3, 3),
+                     "avg_launch_us": round(dom_us, 3),
+                     "event_avg_launch_us": round(event_us[dom], 3),
                      "step_weight_bytes": llm.weight_bytes(),
-                     "per_token_ms": {KERNEL_NAMES[w]: round(v[0], 4) for w, v in per_token.items()}},
+                     "step_graph_wall_us": round(step_wall_us, 1),
+                     "per_token_us": {k: round(sum(v), 1) for k, v in per_kernel.items()}},
+        "value_pcie_inclusive": round(value_pcie, 3),
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
