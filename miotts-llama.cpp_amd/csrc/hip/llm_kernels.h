@@ -72,6 +72,7 @@ struct LlmBuffers {
     float *smp;        // sampler partials [2 * n_lm_blocks]
     const float2 *rope;  // [n_ctx][hd/2] (cos, sin)
     StepState *st;
+    const SampleCfg *cfg;       // sampling configuration (device-resident: graphs never re-capture)
     unsigned long long *trace;  // optional: per-kernel checkpoint timestamps (workgroup 0, thread 0)
     unsigned long long *tl;     // optional: step timeline {min start, max end} per launch (s_memrealtime)
     int seq;                    // launch index within the step (timeline slot)
@@ -80,10 +81,10 @@ struct LlmBuffers {
 // Launch one decode step (all layers + head + sampler) on stream s.
 void launch_decode_step(const LlmDims &d, const LayerW *layers, int n_layer, _Float16 *kcache,
                         _Float16 *vcache, const float *out_norm, const QMat &lm, const QMat &tok_embd,
-                        const LlmBuffers &b, const SampleCfg &sc, hipStream_t s);
+                        const LlmBuffers &b, hipStream_t s);
 void launch_step_kernel(int which, const LlmDims &d, const LayerW *layers, int il, _Float16 *kcache,
                         _Float16 *vcache, const float *out_norm, const QMat &lm, const QMat &tok_embd,
-                        const LlmBuffers &b, const SampleCfg &sc, hipStream_t s);
+                        const LlmBuffers &b, hipStream_t s);
 // Embedding of `token` (row of token_embd) -> b.x, and state reset to (pos, token).
 void launch_embed_token(const LlmDims &d, const QMat &tok_embd, const LlmBuffers &b, hipStream_t s);
 int lm_head_blocks(const LlmDims &d);

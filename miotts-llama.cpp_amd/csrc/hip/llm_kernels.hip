@@ -884,8 +884,8 @@ __device__ inline float gumbel(uint64_t seed, int step, int idx) {
 // (<= 128) are parked one per lane (two registers) and the noise is drawn for 64 rows at
 // a time after the stream.
 template <int NP, int T>
-__global__ __launch_bounds__(MT) void k_lm_head(LlmDims d, const float *norm_w, QMat lm, SampleCfg sc, Prefetch pf,
-                                                LlmBuffers b) {
+__global__ __launch_bounds__(MT) void k_lm_head(LlmDims d, const float *norm_w, QMat lm, Prefetch pf, LlmBuffers b) {
+    const SampleCfg sc = *b.cfg;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __shared__ float bs_[MW];
     __shared__ int bi_[MW];
@@ -1221,7 +1221,8 @@ __device__ inline void embed_row(const QMat &emb, int tok, int n, float *x) {
     }
 }
 
-__global__ __launch_bounds__(ST) void k_sample(LlmDims d, SampleCfg sc, QMat emb, int nblk, LlmBuffers b) {
+__global__ __launch_bounds__(ST) void k_sample(LlmDims d, QMat emb, int nblk, LlmBuffers b) {
+    const SampleCfg sc = *b.cfg;
     __shared__ float bs_[ST / 64];
     __shared__ int bi_[ST / 64];
     __shared__ int tok_s;
@@ -1346,7 +1347,7 @@ Prefetch prefetch_plan(int which, const LlmDims &d, const LayerW *layers, int il
 // lm_head), 6 lm_head, 7 sample.
 void launch_step_kernel(int which, const LlmDims &d, const LayerW *layers, int il, _Float16 *kcache,
                         _Float16 *vcache, const float *out_norm, const QMat &lm, const QMat &tok_embd,
-                        const LlmBuffers &b, const SampleCfg &sc, hipStream_t s) {
+                        const LlmBuffers &b, hipStream_t s) {
     const size_t layer_kv = (size_t)d.n_kv * d.n_ctx * d.hd;
     const int G = d.n_head / d.n_kv;
     const Prefetch pf = d.prefetch ? prefetch_plan(which, d, layers, il, lm) : Prefetch{};
@@ -1408,11 +1409,11 @@ void launch_step_kernel(int which, const LlmDims &d, const LayerW *layers, int i
         case 6:
             dispatch_nt(d.n_embd, lm.type, [&]<int NP, int T>() {
                 hipLaunchKernelGGL((k_lm_head<NP, T>), dim3(lm_head_blocks(d)), dim3(MT), mv_lds(d.n_embd), s, d,
-                                   out_norm, lm, sc, pf, b);
+                                   out_norm, lm, pf, b);
             });
             break;
         case 7:
-            hipLaunchKernelGGL(k_sample, dim3(1), dim3(ST), 0, s, d, sc, tok_embd, lm_head_blocks(d), b);
+            hipLaunchKernelGGL(k_sample, dim3(1), dim3(ST), 0, s, d, tok_embd, lm_head_blocks(d), b);
             break;
         default: break;
     }
@@ -1420,11 +1421,11 @@ void launch_step_kernel(int which, const LlmDims &d, const LayerW *layers, int i
 
 void launch_decode_step(const LlmDims &d, const LayerW *layers, int n_layer, _Float16 *kcache,
                         _Float16 *vcache, const float *out_norm, const QMat &lm, const QMat &tok_embd,
-                        const LlmBuffers &b, const SampleCfg &sc, hipStream_t s) {
+                        const LlmBuffers &b, hipStream_t s) {
     for (int il = 0; il < n_layer; ++il)
-        for (int k = 0; k < 5; ++k) launch_step_kernel(k, d, layers, il, kcache, vcache, out_norm, lm, tok_embd, b, sc, s);
-    launch_step_kernel(6, d, layers, 0, kcache, vcache, out_norm, lm, tok_embd, b, sc, s);
-    launch_step_kernel(7, d, layers, 0, kcache, vcache, out_norm, lm, tok_embd, b, sc, s);
+        for (int k = 0; k < 5; ++k) launch_step_kernel(k, d, layers, il, kcache, vcache, out_norm, lm, tok_embd, b, s);
+    launch_step_kernel(6, d, layers, 0, kcache, vcache, out_norm, lm, tok_embd, b, s);
+    launch_step_kernel(7, d, layers, 0, kcache, vcache, out_norm, lm, tok_embd, b, s);
 }
 
 // ------------------------------------------------------------------ parity entry point

@@ -43,8 +43,10 @@ struct mio_hip_llm {
     };
     std::vector<Range> ranges;
 
-    hipGraphExec_t graph = nullptr;
-    mio::SampleCfg graph_cfg{};
+    // decode-step graphs, captured once (the sampling config is device-resident):
+    // one step, and kGraphSteps steps back to back (fewer graph launches per token)
+    hipGraphExec_t graph = nullptr, graph_n = nullptr;
+    mio::SampleCfg *d_cfg = nullptr;
     // generation state
     int n_prompt = 0, max_new = 0, steps_total = 0, steps_issued = 0;
     mio::SampleCfg cfg{};
@@ -52,6 +54,7 @@ struct mio_hip_llm {
     ~mio_hip_llm() {
         if (d) hipSetDevice(d->dev);
         if (graph) hipGraphExecDestroy(graph);
+        if (graph_n) hipGraphExecDestroy(graph_n);
         for (void *p : allocs) hipFree(p);
     }
 };
@@ -111,10 +114,10 @@ float *upload_f32(mio_hip_llm *m, const mio::GgufTensor *t, int64_t n) {
     return p;
 }
 
-bool same_cfg(const mio::SampleCfg &a, const mio::SampleCfg &b) { return std::memcmp(&a, &b, sizeof(a)) == 0; }
+constexpr int kGraphSteps = 8;
 
 // One decode step on m->d->stream (tl: optional step timeline, diagnostic).
-int issue_step(mio_hip_llm *m, const mio::SampleCfg &cfg, unsigned long long *tl = nullptr) {
+int issue_step(mio_hip_llm *m, unsigned long long *tl = nullptr) {
     hipStream_t s = m->d->stream;
     int seq = 0;
     auto bufs = [&]() {
@@ -125,27 +128,36 @@ int issue_step(mio_hip_llm *m, const mio::SampleCfg &cfg, unsigned long long *tl
     for (int il = 0; il < m->n_layer; ++il)
         for (int k = 0; k < 5; ++k)
             mio::launch_step_kernel(k, m->dims, m->layers.data(), il, m->kc, m->vc, m->out_norm, m->lm, m->tok, bufs(),
-                                    cfg, s);
-    mio::launch_step_kernel(6, m->dims, m->layers.data(), 0, m->kc, m->vc, m->out_norm, m->lm, m->tok, bufs(), cfg, s);
-    mio::launch_step_kernel(7, m->dims, m->layers.data(), 0, m->kc, m->vc, m->out_norm, m->lm, m->tok, bufs(), cfg, s);
+                                    s);
+    mio::launch_step_kernel(6, m->dims, m->layers.data(), 0, m->kc, m->vc, m->out_norm, m->lm, m->tok, bufs(), s);
+    mio::launch_step_kernel(7, m->dims, m->layers.data(), 0, m->kc, m->vc, m->out_norm, m->lm, m->tok, bufs(), s);
     return MIO_OK;
 }
 
-int ensure_graph(mio_hip_llm *m, const mio::SampleCfg &cfg) {
-    if (m->graph && same_cfg(cfg, m->graph_cfg)) return MIO_OK;
-    if (m->graph) {
-        hipGraphExecDestroy(m->graph);
-        m->graph = nullptr;
-    }
+int capture_steps(mio_hip_llm *m, int n, hipGraphExec_t *out) {
     hipStream_t s = m->d->stream;
     hipGraph_t g = nullptr;
     MIO_HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
-    const int rc = issue_step(m, cfg);
+    int rc = MIO_OK;
+    for (int i = 0; i < n && !rc; ++i) rc = issue_step(m);
     MIO_HIP_CHECK(hipStreamEndCapture(s, &g));
     if (rc) return rc;
-    MIO_HIP_CHECK(hipGraphInstantiate(&m->graph, g, nullptr, nullptr, 0));
+    MIO_HIP_CHECK(hipGraphInstantiate(out, g, nullptr, nullptr, 0));
     hipGraphDestroy(g);
-    m->graph_cfg = cfg;
+    return MIO_OK;
+}
+
+int ensure_graph(mio_hip_llm *m) {
+    if (m->graph && m->graph_n) return MIO_OK;
+    int rc;
+    if (!m->graph && (rc = capture_steps(m, 1, &m->graph))) return rc;
+    if (!m->graph_n && (rc = capture_steps(m, kGraphSteps, &m->graph_n))) return rc;
+    return MIO_OK;
+}
+
+int put_cfg(mio_hip_llm *m, const mio::SampleCfg &c) {
+    m->cfg = c;
+    MIO_HIP_CHECK(hipMemcpyAsync(m->d_cfg, &c, sizeof(c), hipMemcpyHostToDevice, m->d->stream));
     return MIO_OK;
 }
 
@@ -189,8 +201,7 @@ int llm_begin(mio_hip_llm *m, const int32_t *prompt, int n_prompt, int max_new, 
     c.eos0 = sp.eos0, c.eos1 = sp.eos1;
     c.force = m->d_force, c.n_force = m->max_steps;
     c.out_tokens = m->d_tokens, c.max_steps = m->max_steps;
-    if ((rc = ensure_graph(m, c))) return rc;
-    m->cfg = c;
+    if ((rc = put_cfg(m, c)) || (rc = ensure_graph(m))) return rc;
     m->n_prompt = n_prompt;
     m->max_new = max_new;
     m->steps_total = n_prompt - 1 + max_new;
@@ -204,12 +215,15 @@ int llm_run(mio_hip_llm *m, int n_steps) {
     // MIO_NO_GRAPH=1: eager launches (rocprofv3 kernel tracing of graph replays crashes on
     // ROCm 7.2 here; kernels and arguments are identical either way)
     static const bool eager = getenv("MIO_NO_GRAPH") && getenv("MIO_NO_GRAPH")[0] == '1';
-    for (int i = 0; i < n_steps && m->steps_issued < m->steps_total; ++i, ++m->steps_issued) {
-        if (eager) {
-            if ((rc = issue_step(m, m->cfg))) return rc;
-        } else
-            MIO_HIP_CHECK(hipGraphLaunch(m->graph, m->d->stream));
+    int n = std::min(n_steps, m->steps_total - m->steps_issued);
+    m->steps_issued += n > 0 ? n : 0;
+    if (eager) {
+        for (int i = 0; i < n; ++i)
+            if ((rc = issue_step(m))) return rc;
+        return MIO_OK;
     }
+    for (; n >= kGraphSteps; n -= kGraphSteps) MIO_HIP_CHECK(hipGraphLaunch(m->graph_n, m->d->stream));
+    for (; n > 0; --n) MIO_HIP_CHECK(hipGraphLaunch(m->graph, m->d->stream));
     return MIO_OK;
 }
 
@@ -374,6 +388,8 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
     m->buf.part = dalloc<float>(m, (size_t)D.n_head * D.max_splits * (D.hd + 4));
     m->buf.smp = dalloc<float>(m, 2 * mio::lm_head_blocks(D) + 16);
     m->buf.st = dalloc<mio::StepState>(m, 1);
+    m->d_cfg = dalloc<mio::SampleCfg>(m, 1);
+    m->buf.cfg = m->d_cfg;
     m->max_steps = n_ctx;
     m->d_tokens = dalloc<int>(m, m->max_steps);
     m->d_force = dalloc<int>(m, m->max_steps);
@@ -389,7 +405,7 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
     }
     float2 *dr = dalloc<float2>(m, rope.size());
     if (!m->kc || !m->vc || !m->buf.x || !m->buf.qkv || !m->buf.h || !m->buf.logits ||
-        !m->buf.part || !m->buf.smp || !m->buf.st || !m->d_tokens || !m->d_force || !dr) {
+        !m->buf.part || !m->buf.smp || !m->buf.st || !m->d_cfg || !m->d_tokens || !m->d_force || !dr) {
         mio::set_error("llm_load: device allocation failed");
         return fail(MIO_ERR_OOM);
     }
@@ -426,7 +442,7 @@ extern "C" int mio_hip_llm_eval(mio_hip_llm *m, int32_t token, int pos, float *l
     mio::SampleCfg c{};
     c.temp = 0.0f, c.lo = 0, c.hi = m->dims.n_vocab, c.eos0 = c.eos1 = -1;
     c.force = m->d_force, c.n_force = m->max_steps, c.out_tokens = m->d_tokens, c.max_steps = m->max_steps;
-    if ((rc = ensure_graph(m, c))) return rc;
+    if ((rc = put_cfg(m, c)) || (rc = ensure_graph(m))) return rc;
     const int zero = 0;
     MIO_HIP_CHECK(hipMemcpyAsync(m->d_force, &zero, 4, hipMemcpyHostToDevice, m->d->stream));
     if ((rc = set_state(m, pos, token))) return rc;
@@ -543,11 +559,11 @@ extern "C" int mio_hip_llm_time_kernel(mio_hip_llm *m, int which, int iters, flo
     hipStream_t s = m->d->stream;
     // warm
     mio::launch_step_kernel(which, D, m->layers.data(), il, m->kc, m->vc, m->out_norm, m->lm, m->tok, m->buf,
-                            m->graph_cfg, s);
+                            s);
     MIO_HIP_CHECK(hipEventRecord(e0, s));
     for (int i = 0; i < iters; ++i)
         mio::launch_step_kernel(which, D, m->layers.data(), il, m->kc, m->vc, m->out_norm, m->lm, m->tok, m->buf,
-                                m->graph_cfg, s);
+                                s);
     MIO_HIP_CHECK(hipEventRecord(e1, s));
     MIO_HIP_CHECK(hipEventSynchronize(e1));
     float ms = 0;
@@ -572,7 +588,7 @@ extern "C" int mio_hip_llm_trace_kernel(mio_hip_llm *m, int which, uint64_t *out
     MIO_HIP_CHECK(hipMalloc(&dt, 32 * sizeof(unsigned long long)));
     MIO_HIP_CHECK(hipMemsetAsync(dt, 0, 32 * sizeof(unsigned long long), s));
     mio::launch_step_kernel(which, m->dims, m->layers.data(), il, m->kc, m->vc, m->out_norm, m->lm, m->tok, m->buf,
-                            m->graph_cfg, s);
+                            s);
     // evict L2 / MALL so the traced launch streams its weights from HBM as in a real step
     void *flush = nullptr;
     const size_t flush_bytes = (size_t)1 << 30;
@@ -588,7 +604,7 @@ extern "C" int mio_hip_llm_trace_kernel(mio_hip_llm *m, int which, uint64_t *out
     mio::LlmBuffers tb = m->buf;
     tb.trace = dt;
     mio::launch_step_kernel(which, m->dims, m->layers.data(), il, m->kc, m->vc, m->out_norm, m->lm, m->tok, tb,
-                            m->graph_cfg, s);
+                            s);
     MIO_HIP_CHECK(hipMemcpyAsync(out, dt, 32 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
     MIO_HIP_CHECK(hipStreamSynchronize(s));
     hipFree(dt);
@@ -612,7 +628,7 @@ extern "C" int mio_hip_llm_timeline(mio_hip_llm *m, uint64_t *out, int max_launc
     hipGraph_t g = nullptr;
     hipGraphExec_t ge = nullptr;
     MIO_HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
-    rc = issue_step(m, m->graph_cfg, tl);
+    rc = issue_step(m, tl);
     MIO_HIP_CHECK(hipStreamEndCapture(s, &g));
     MIO_HIP_CHECK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
     for (int rep = 0; rep < 3; ++rep) {
