@@ -108,6 +108,39 @@ def cpu_baseline(llm_path, codec_path, voice_path, n_tok, n_codes, utt_tokens):
                       f"{n_codes} codes ({t_code * 1e3:.2f} ms/code), extrapolated to {utt_tokens} tokens"}
 
 
+def utterance_seed(rank: int, index: int) -> int:
+    """Distinct sampler seed per (rank, utterance index): ranks never replay each other's work."""
+    return 42 + 7919 * rank + 104729 * index
+
+
+def timed_region(warmup, steps, utts_per_step, rank, utterance, sync, barrier, dist):
+    """Weak-scaling timed region shared by every rank (no data-path collective): W untimed
+    warmup steps, then K steps bracketed by barrier + device sync on both sides. Returns
+    (max elapsed over ranks, sum of audio samples over ranks); the only collectives are
+    these two scalar reductions after the clock has stopped."""
+    for w in range(warmup):
+        for u in range(utts_per_step):
+            utterance(utterance_seed(rank, w * utts_per_step + u), False)
+    sync()
+    barrier()
+    t_start = time.perf_counter()
+    samples = 0
+    for s in range(steps):
+        for u in range(utts_per_step):
+            samples += utterance(utterance_seed(rank, 1000 + s * utts_per_step + u), True)
+    sync()
+    barrier()
+    elapsed = time.perf_counter() - t_start
+    if dist is None:
+        return elapsed, float(samples)
+    import torch
+    t = torch.tensor([elapsed], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    n = torch.tensor([samples], dtype=torch.float64)
+    dist.all_reduce(n, op=dist.ReduceOp.SUM)
+    return float(t.item()), float(n.item())
+
+
 def main():
     a = parse_args()
     rank = int(os.environ.get("RANK", 0))
@@ -134,13 +167,11 @@ def main():
     allow = (m.SYNTH_SPEECH0, m.SYNTH_SPEECH0 + 12800)
 
     stage = {"llm_ms": 0.0, "codec_ms": 0.0, "istft_ms": 0.0, "codec_wall_ms": 0.0}
-    audio_samples = 0
 
     d_emb = dev.upload(np.ascontiguousarray(emb, np.float32))
     d_pcm = dev.empty((a.tokens * codec.samples_per_token,), np.float32)
 
     def utterance(seed, record):
-        nonlocal audio_samples
         t0 = time.perf_counter()
         toks = llm.generate(prompt, a.tokens, 0.8, seed, allow=allow, check_interval=20)
         t1 = time.perf_counter()
@@ -154,32 +185,12 @@ def main():
             stage["codec_wall_ms"] += (t2 - t1) * 1e3
             stage["codec_ms"] += c_ms
             stage["istft_ms"] += i_ms
-            audio_samples += n
         if len(toks) != a.tokens or n != a.tokens * codec.samples_per_token:
             raise RuntimeError(f"utterance produced {len(toks)} tokens / {n} samples")
+        return n
 
-    for w in range(a.warmup):
-        for u in range(a.utts_per_step):
-            utterance(42 + 7919 * rank + 104729 * (w * a.utts_per_step + u), False)
-    dev.sync()
-    barrier()
-    t_start = time.perf_counter()
-    for s in range(a.steps):
-        for u in range(a.utts_per_step):
-            utterance(42 + 7919 * rank + 104729 * (1000 + s * a.utts_per_step + u), True)
-    dev.sync()
-    barrier()
-    elapsed = time.perf_counter() - t_start
-    if dist is not None:
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        n = torch.tensor([audio_samples], dtype=torch.float64)
-        dist.all_reduce(n, op=dist.ReduceOp.SUM)
-        total_samples = float(n.item())
-    else:
-        total_samples = float(audio_samples)
+    elapsed, total_samples = timed_region(a.warmup, a.steps, a.utts_per_step, rank, utterance,
+                                          dev.sync, barrier, dist)
     audio_s = total_samples / codec.sample_rate
     value = audio_s / elapsed
 
