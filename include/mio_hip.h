@@ -114,6 +114,11 @@ int mio_hip_llm_weight_bytes(const mio_hip_llm *m, uint64_t *bytes);
 /* Teacher-forced llama_decode of `token` at `pos` (KV cache of positions < pos must hold
  * earlier evals); logits[n_vocab] to host (NULL = skip). Parity entry point. */
 int mio_hip_llm_eval(mio_hip_llm *m, int32_t token, int pos, float *logits);
+/* The prefill llama_decode of test-to-speech.cpp:132-148 (logits for the last token only,
+ * :138): positions 0..n_tokens-2 go through the batched prefill (one weight pass per chunk
+ * of prompt tokens), the last token through one decode step; logits[n_vocab] to host (NULL
+ * = skip). The KV cache then holds positions < n_tokens. */
+int mio_hip_llm_prefill(mio_hip_llm *m, const int32_t *tokens, int n_tokens, float *logits);
 /* Copies the logits of the last step to host. */
 int mio_hip_llm_logits(mio_hip_llm *m, float *logits);
 /* run_llm (test-to-speech.cpp:94-199): prefill prompt[n_prompt], then up to max_tokens

@@ -1,0 +1,797 @@
+// Device-side building blocks shared by the decode-step kernels (llm_kernels.hip) and
+// the batched prompt prefill (llm_prefill.hip): DPP cross-lane reductions, ggml activation
+// quantizers (Q8_K / Q8_0), the split-layout weight fragments and their integer block dots,
+// and the streaming-rows matvec engine. Included by exactly those two translation units;
+// everything lives in an anonymous namespace.
+#pragma once
+
+#include <cfloat>
+#include <climits>
+#include <type_traits>
+
+#include "llm_kernels.h"
+
+#pragma clang fp contract(off)
+
+namespace mio {
+namespace {
+// Checkpoint timestamps (s_memtime) of workgroup 0 / thread 0, only when b.trace is set
+// (mio_hip_llm_trace_kernel); a uniform branch otherwise.
+#define MIO_TRACE(bufs, k)                                                                    \
+    do {                                                                                      \
+        if ((bufs).trace && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {        \
+            asm volatile("" ::: "memory");                                                    \
+            (bufs).trace[k] = __builtin_readcyclecounter();                                   \
+            if ((k) == 0 || (k) == 15) (bufs).trace[16 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+        }                                                                                     \
+    } while (0)
+
+// Step timeline (diagnostic, mio_hip_llm_timeline): start / end of every workgroup of
+// each launch, s_memrealtime ticks (100 MHz), plain stores to slot [seq][wg] (wg < 256).
+#define MIO_TL_SLOT(bufs) ((bufs).tl + 2 * ((size_t)(bufs).seq * 256 + ((blockIdx.x + blockIdx.y * gridDim.x) & 255)))
+#define MIO_TL_BEGIN(bufs)                                                                      \
+    do {                                                                                        \
+        if ((bufs).tl && threadIdx.x == 0) MIO_TL_SLOT(bufs)[0] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#define MIO_TL_END(bufs)                                                                        \
+    do {                                                                                        \
+        if ((bufs).tl && threadIdx.x == 0) MIO_TL_SLOT(bufs)[1] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+
+constexpr int NT = 256;        // threads of the attention / sampler kernels
+constexpr int NWAVE = NT / 64;
+constexpr int MT = 512;        // threads of a streaming matvec workgroup
+constexpr int MW = MT / 64;
+constexpr int ATT_CHUNK = kAttChunk;
+constexpr int PF_SLOT = 1024;  // LDS bytes per wave that receive discarded prefetch data
+constexpr int PF_LDS = MW * PF_SLOT;
+// dynamic LDS of a matvec launch: activation staging, then the prefetch slots
+__host__ __device__ inline size_t pf_offset(size_t base) { return (base + 15) & ~(size_t)15; }
+__host__ __device__ constexpr int part_rec(int hd) { return hd + 4; }  // partial record {O[hd], m, l, pad}
+
+__device__ __forceinline__ float h2f(uint32_t bits16) {
+    const uint16_t b = (uint16_t)bits16;
+    return (float)__builtin_bit_cast(_Float16, b);
+}
+__device__ __forceinline__ float f16r(float f) { return (float)(_Float16)f; }
+__device__ __forceinline__ int sdot4(int a, int b, int c) { return __builtin_amdgcn_sdot4(a, b, c, false); }
+__device__ __forceinline__ uint4 ld16(const uint8_t *p) { return *reinterpret_cast<const uint4 *>(p); }
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// ------------------------------------------------------------------ cross-lane (DPP)
+// Cross-lane sums by DPP (gfx9 row_shr / row_bcast), never through LDS.
+template <int CTRL, int RM = 0xF>
+__device__ __forceinline__ int dpp_i(int v) {
+    return __builtin_amdgcn_update_dpp(0, v, CTRL, RM, 0xF, false);
+}
+template <int CTRL, int RM = 0xF>
+__device__ __forceinline__ float dpp_f(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, RM, 0xF, false));
+}
+constexpr int ROW_SHR1 = 0x111, ROW_SHR2 = 0x112, ROW_SHR4 = 0x114, ROW_SHR8 = 0x118;
+constexpr int ROW_BCAST15 = 0x142, ROW_BCAST31 = 0x143;
+
+// wave-wide reductions to lane 63 (row_shr prefix within rows, then row_bcast), returned
+// wave-uniform. `id` is the identity of the operation (what out-of-row lanes contribute).
+__device__ __forceinline__ float wave_max_f(float v, float id) {
+    v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(id), __float_as_int(v), ROW_SHR1, 0xF, 0xF, false)));
+    v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(id), __float_as_int(v), ROW_SHR2, 0xF, 0xF, false)));
+    v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(id), __float_as_int(v), ROW_SHR4, 0xF, 0xF, false)));
+    v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(id), __float_as_int(v), ROW_SHR8, 0xF, 0xF, false)));
+    v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(id), __float_as_int(v), ROW_BCAST15, 0xA, 0xF, false)));
+    v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(id), __float_as_int(v), ROW_BCAST31, 0xC, 0xF, false)));
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+__device__ __forceinline__ int wave_min_i(int v) {
+    const int id = INT_MAX;
+    v = min(v, __builtin_amdgcn_update_dpp(id, v, ROW_SHR1, 0xF, 0xF, false));
+    v = min(v, __builtin_amdgcn_update_dpp(id, v, ROW_SHR2, 0xF, 0xF, false));
+    v = min(v, __builtin_amdgcn_update_dpp(id, v, ROW_SHR4, 0xF, 0xF, false));
+    v = min(v, __builtin_amdgcn_update_dpp(id, v, ROW_SHR8, 0xF, 0xF, false));
+    v = min(v, __builtin_amdgcn_update_dpp(id, v, ROW_BCAST15, 0xA, 0xF, false));
+    v = min(v, __builtin_amdgcn_update_dpp(id, v, ROW_BCAST31, 0xC, 0xF, false));
+    return __builtin_amdgcn_readlane(v, 63);
+}
+template <int CTRL, int RM = 0xF>
+__device__ __forceinline__ double dpp_d(double v) {
+    const int2 p = __builtin_bit_cast(int2, v);
+    int2 r;
+    r.x = __builtin_amdgcn_update_dpp(0, p.x, CTRL, RM, 0xF, false);
+    r.y = __builtin_amdgcn_update_dpp(0, p.y, CTRL, RM, 0xF, false);
+    return __builtin_bit_cast(double, r);
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+    v += dpp_d<ROW_SHR1>(v);
+    v += dpp_d<ROW_SHR2>(v);
+    v += dpp_d<ROW_SHR4>(v);
+    v += dpp_d<ROW_SHR8>(v);
+    v += dpp_d<ROW_BCAST15, 0xA>(v);
+    v += dpp_d<ROW_BCAST31, 0xC>(v);
+    const int2 p = __builtin_bit_cast(int2, v);
+    int2 r;
+    r.x = __builtin_amdgcn_readlane(p.x, 63);
+    r.y = __builtin_amdgcn_readlane(p.y, 63);
+    return __builtin_bit_cast(double, r);
+}
+// all-reduce (max) within aligned 8-lane groups; every lane gets the result
+__device__ __forceinline__ float group8_max(float v) {
+    v = fmaxf(v, dpp_f<0xB1>(v));   // quad_perm [1,0,3,2]
+    v = fmaxf(v, dpp_f<0x4E>(v));   // quad_perm [2,3,0,1]
+    v = fmaxf(v, dpp_f<0x141>(v));  // row_half_mirror
+    return v;
+}
+// all-reduce (sum) within aligned 4-lane groups
+__device__ __forceinline__ int quad_sum_i(int v) {
+    v += dpp_i<0xB1>(v);
+    v += dpp_i<0x4E>(v);
+    return v;
+}
+
+// ------------------------------------------------------------------ activation in LDS
+struct ActL {
+    int8_t *qs;
+    float *d;
+    int16_t *bs;
+};
+
+struct Smem {
+    float *xs;   // [K] float staging
+    ActL a;
+    double *red; // [16]
+};
+
+// LDS layout: xs f32[K] | qs i8[K] | d f32[K/32+8] | bs i16[K/16+8] | red
+__host__ __device__ inline size_t smem_bytes(int K) {
+    return (size_t)K * 4 + (size_t)K + (size_t)(K / 32 + 8) * 4 + (size_t)(K / 16 + 8) * 2 + 128;
+}
+
+__device__ inline Smem carve(char *base, int K) {
+    Smem s;
+    s.xs = (float *)base;
+    s.a.qs = (int8_t *)(base + (size_t)K * 4);
+    s.a.d = (float *)(base + (size_t)K * 5);
+    s.a.bs = (int16_t *)(base + (size_t)K * 5 + (size_t)(K / 32 + 8) * 4);
+    s.red = (double *)(base + smem_bytes(K) - 128);
+    return s;
+}
+
+__device__ double block_sum(double v, double *red) {
+    v = wave_sum_d(v);
+    const int nw = blockDim.x >> 6;
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    double t = 0.0;
+    for (int w = 0; w < nw; ++w) t += red[w];
+    __syncthreads();
+    return t;
+}
+
+// quantize_row_q8_K_ref semantics (iscale = -127/max_signed with max_signed the first
+// element of largest |x|, nearest-even, clamp 127, bsums); reductions by DPP.
+__device__ void quant_q8k(const float *xs, int K, const ActL &a) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    for (int b = wave; b < K / 256; b += nw) {
+        const float4 v4 = *reinterpret_cast<const float4 *>(xs + b * 256 + 4 * lane);
+        const float v[4] = {v4.x, v4.y, v4.z, v4.w};
+        const float am = wave_max_f(fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))), 0.0f);
+        int q[4] = {0, 0, 0, 0};
+        float dd = 0.0f;
+        if (am > 0.0f) {
+            int first = INT_MAX;
+#pragma unroll
+            for (int i = 3; i >= 0; --i)
+                if (fabsf(v[i]) == am) first = 4 * lane + i;
+            const int ai = wave_min_i(first);
+            const float mx = xs[b * 256 + ai];
+            const float iscale = -127.f / mx;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int t = (int)rintf(iscale * v[i]);
+                q[i] = t < 127 ? t : 127;
+            }
+            dd = 1.0f / iscale;
+        }
+        const int packed = (q[0] & 0xFF) | ((q[1] & 0xFF) << 8) | ((q[2] & 0xFF) << 16) | ((q[3] & 0xFF) << 24);
+        *reinterpret_cast<int *>(a.qs + b * 256 + 4 * lane) = packed;
+        const int sm = quad_sum_i(q[0] + q[1] + q[2] + q[3]);
+        if ((lane & 3) == 0) a.bs[b * 16 + (lane >> 2)] = (int16_t)sm;
+        if (lane == 0) a.d[b] = dd;
+    }
+}
+
+// quantize_row_q8_0_ref semantics (d = amax/127 stored as f16, q = roundf(x * 1/d))
+__device__ void quant_q80(const float *xs, int K, const ActL &a) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const int nb = K / 32;
+    for (int b0 = wave * 8; b0 < nb; b0 += nw * 8) {
+        const int b = b0 + (lane >> 3);
+        const bool ok = b < nb;
+        float v[4];
+        float am = 0.0f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            v[i] = ok ? xs[b * 32 + 4 * (lane & 7) + i] : 0.0f;
+            am = fmaxf(am, fabsf(v[i]));
+        }
+        am = group8_max(am);
+        const float dd = am / 127.0f;
+        const float id = dd != 0.0f ? 1.0f / dd : 0.0f;
+        int q[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) q[i] = (int)roundf(v[i] * id);
+        if (ok) {
+            *reinterpret_cast<int *>(a.qs + b * 32 + 4 * (lane & 7)) =
+                (q[0] & 0xFF) | ((q[1] & 0xFF) << 8) | ((q[2] & 0xFF) << 16) | ((q[3] & 0xFF) << 24);
+            if ((lane & 7) == 0) a.d[b] = f16r(dd);
+        }
+    }
+}
+
+__device__ inline void quantize(const float *xs, int K, bool kquant, const ActL &a) {
+    if (kquant)
+        quant_q8k(xs, K, a);
+    else
+        quant_q80(xs, K, a);
+    __syncthreads();
+}
+
+// ------------------------------------------------------------------ prologue registers
+// x (and the norm weight) as float4 per thread, loaded before any weight load.
+template <int XV>
+struct XRegs {
+    float4 v[XV];
+    float4 w[XV];
+};
+
+template <int XV>
+__device__ inline void load_x(const float *x, const float *w, int K, XRegs<XV> &xr) {
+    const auto rx = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(x), 0, K * 4, 0x00020000);
+    const auto rw = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(w), 0, w ? K * 4 : 0, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < XV; ++i) {
+        const int e = (threadIdx.x + i * MT) * 4;
+        const u32x4 a = __builtin_amdgcn_raw_buffer_load_b128(rx, e * 4, 0, 0);
+        const u32x4 c = __builtin_amdgcn_raw_buffer_load_b128(rw, e * 4, 0, 0);
+        xr.v[i] = make_float4(__uint_as_float(a.x), __uint_as_float(a.y), __uint_as_float(a.z), __uint_as_float(a.w));
+        xr.w[i] = make_float4(__uint_as_float(c.x), __uint_as_float(c.y), __uint_as_float(c.z), __uint_as_float(c.w));
+    }
+}
+
+// ggml_rms_norm + mul(weight): xs = (x * 1/sqrtf(mean(x^2) + eps)) * w, then quantize.
+template <int XV>
+__device__ void rmsnorm_quant(const XRegs<XV> &xr, int K, float eps, bool kquant, const Smem &s) {
+    double acc = 0.0;
+#pragma unroll
+    for (int i = 0; i < XV; ++i) {
+        const int e = (threadIdx.x + i * MT) * 4;
+        if (e < K) {
+            const float4 v = xr.v[i];
+            acc += (double)(v.x * v.x);
+            acc += (double)(v.y * v.y);
+            acc += (double)(v.z * v.z);
+            acc += (double)(v.w * v.w);
+        }
+    }
+    const double tot = block_sum(acc, s.red);
+    const float mean = (float)(tot / K);
+    const float scale = 1.0f / sqrtf(mean + eps);
+#pragma unroll
+    for (int i = 0; i < XV; ++i) {
+        const int e = (threadIdx.x + i * MT) * 4;
+        if (e < K) {
+            const float4 v = xr.v[i], ww = xr.w[i];
+            float t;
+            t = v.x * scale, s.xs[e + 0] = t * ww.x;
+            t = v.y * scale, s.xs[e + 1] = t * ww.y;
+            t = v.z * scale, s.xs[e + 2] = t * ww.z;
+            t = v.w * scale, s.xs[e + 3] = t * ww.w;
+        }
+    }
+    __syncthreads();
+    quantize(s.xs, K, kquant, s.a);
+}
+
+template <int XV>
+__device__ inline void plain_quant(const XRegs<XV> &xr, int K, bool kquant, const Smem &s) {
+#pragma unroll
+    for (int i = 0; i < XV; ++i) {
+        const int e = (threadIdx.x + i * MT) * 4;
+        if (e < K) *reinterpret_cast<float4 *>(s.xs + e) = xr.v[i];
+    }
+    __syncthreads();
+    quantize(s.xs, K, kquant, s.a);
+}
+
+// ------------------------------------------------------------------ typed row dots
+// exact integer sum of each 8-lane group, valid in lanes 8k+7
+__device__ __forceinline__ int sum8_i(int v) {
+    v += dpp_i<ROW_SHR1>(v);
+    v += dpp_i<ROW_SHR2>(v);
+    v += dpp_i<ROW_SHR4>(v);
+    return v;
+}
+__device__ __forceinline__ float sum8_f(float v) {
+    v += dpp_f<ROW_SHR1>(v);
+    v += dpp_f<ROW_SHR2>(v);
+    v += dpp_f<ROW_SHR4>(v);
+    return v;
+}
+// sum of the values held in lanes 8k+7 (k = 0..7), returned wave-uniform
+__device__ __forceinline__ float sum_lanes7(float v) {
+    v += dpp_f<ROW_SHR8>(v);
+    v += dpp_f<ROW_BCAST15, 0xA>(v);
+    v += dpp_f<ROW_BCAST31, 0xC>(v);
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+
+__device__ inline float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+constexpr uint32_t M4 = 0x0F0F0F0Fu, M2 = 0x03030303u;
+
+// One unit's weight registers.
+//   Q4_K: a = 16 B of nibbles, b = superblock header {d, dmin, 4 x 24-bit scale pairs}
+//   Q6_K: a = 16 B of ql, b = 16 B of qh, c = the lane's two int8 sub-block scales, e = d
+//   Q8_0: a, b = the lane's 32 codes, e = d
+struct Frag {
+    uint4 a, b;
+    uint32_t c, e;
+};
+
+// One unit's activation registers (the lane's 32 int8 values, two bsums, the scale).
+struct ALane {
+    int4 lo, hi;
+    int b0, b1;
+    float d;
+};
+
+// Lane mapping per pass: K-quants - 8 superblocks x 8 lanes (lane>>3 = superblock,
+// lane&7 = 16-byte piece); Q8_0 - 64 blocks, one per lane (32 codes = two 16-B loads).
+// `row` is wave-uniform, so the row base address is scalar. Loads are unconditional
+// (indices past K are clamped to the row's last block and their terms zeroed in
+// dot_frag): no branches around loads, so vmcnt accounting stays exact and raw data is
+// only converted where it is consumed.
+// Raw buffer loads: descriptor from the (uniform) base and its exact byte size, the row
+// offset in an SGPR (soffset), the lane's constant byte offset in voffset - no per-load
+// address VALU; lanes past the end read 0 (range-checked).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void *p, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), 0, (int)min(bytes, 0x7FFFFFF0u), 0x00020000);
+}
+__device__ __forceinline__ uint4 bld16(const uint8_t *base, uint32_t bytes, uint32_t voff, uint32_t soff) {
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rsrc(base, bytes), voff, soff, 0);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ uint32_t bld2(const uint8_t *base, uint32_t bytes, uint32_t voff, uint32_t soff) {
+    return __builtin_amdgcn_raw_buffer_load_b16(rsrc(base, bytes), voff, soff, 0);
+}
+
+template <int T>
+__device__ __forceinline__ Frag load_frag(const QMat W, int row, int pass) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t R = (uint32_t)W.rows, r = (uint32_t)min(max(row, 0), W.rows - 1);
+    Frag f;
+    if constexpr (T == 12) {
+        const int nsb = W.k >> 8, sb = min(pass * 8 + (lane >> 3), nsb - 1), pc = lane & 7;
+        const uint32_t qb = (uint32_t)(W.k / 2), hb = (uint32_t)nsb * 16;
+        f.a = bld16(W.p0, R * qb, sb * 128 + pc * 16, r * qb);
+        f.b = bld16(W.p1, R * hb, sb * 16, r * hb);
+        f.c = f.e = 0;
+    } else if constexpr (T == 14) {
+        const int nsb = W.k >> 8, sb = min(pass * 8 + (lane >> 3), nsb - 1), pc = lane & 7;
+        const uint32_t lb = (uint32_t)(W.k / 2), hb = (uint32_t)(W.k / 4), sbb = (uint32_t)(W.k / 16),
+                       db = (uint32_t)nsb * 2;
+        f.a = bld16(W.p0, R * lb, sb * 128 + pc * 16, r * lb);
+        f.b = bld16(W.p1, R * hb, sb * 64 + 32 * (pc >> 2) + 16 * (pc & 1), r * hb);
+        f.c = bld2(W.p2, R * sbb, sb * 16 + 2 * pc, r * sbb);
+        f.e = bld2(W.p3, R * db, sb * 2, r * db);
+    } else {
+        const int nb = W.k >> 5, b = min(pass * 64 + lane, nb - 1);
+        const uint32_t qb = (uint32_t)W.k, db = (uint32_t)nb * 2;
+        f.a = bld16(W.p0, R * qb, 32 * b, r * qb);
+        f.b = bld16(W.p0, R * qb, 32 * b + 16, r * qb);
+        f.c = 0;
+        f.e = bld2(W.p1, R * db, 2 * b, r * db);
+    }
+    return f;
+}
+
+template <int T>
+__device__ __forceinline__ ALane load_alane(const ActL &a, int K, int pass) {
+    const int lane = threadIdx.x & 63;
+    ALane r;
+    if constexpr (T == 12 || T == 14) {
+        const int nsb = K >> 8, sb = pass * 8 + (lane >> 3), pc = lane & 7;
+        const int sbc = sb < nsb ? sb : 0;
+        int e, e2;
+        if constexpr (T == 12) {
+            e = sbc * 256 + 64 * (pc >> 1) + 16 * (pc & 1);
+            e2 = e + 32;
+        } else {
+            const int n = pc >> 2, qq = pc & 3;
+            e = sbc * 256 + 128 * n + 32 * (qq >> 1) + 16 * (qq & 1);
+            e2 = e + 64;
+        }
+        r.lo = *reinterpret_cast<const int4 *>(a.qs + e);
+        r.hi = *reinterpret_cast<const int4 *>(a.qs + e2);
+        r.b0 = a.bs[e >> 4];
+        r.b1 = a.bs[e2 >> 4];
+        r.d = a.d[sbc];
+    } else {
+        const int nb = K >> 5, b = pass * 64 + lane, bc = b < nb ? b : 0;
+        r.lo = *reinterpret_cast<const int4 *>(a.qs + 32 * bc);
+        r.hi = *reinterpret_cast<const int4 *>(a.qs + 32 * bc + 16);
+        r.b0 = r.b1 = 0;
+        r.d = a.d[bc];
+    }
+    return r;
+}
+
+// This lane's partial of the row dot for one pass. K-quants: the per-superblock integer
+// sums are reduced exactly over the superblock's 8 lanes (ggml vec_dot semantics) and the
+// superblock's float term is valid in lane 8k+7; Q8_0: every lane holds one block's term.
+// Lanes whose superblock / block lies past K have zero codes and zero scales -> 0.
+template <int T>
+__device__ __forceinline__ float dot_frag(const Frag &f, const ALane &al, int K, int pass) {
+    const int lane = threadIdx.x & 63;
+    if constexpr (T == 12) {
+        const int jj = (lane & 7) >> 1;
+        const uint4 h = f.b;
+        const uint32_t wlo = jj < 2 ? h.y : (jj == 2 ? h.z : h.w);
+        const uint32_t whi = jj < 2 ? h.z : h.w;
+        const uint32_t F = __builtin_amdgcn_alignbit(whi, wlo, (24 * jj) & 31);
+        const int sc0 = F & 63, m0 = (F >> 6) & 63, sc1 = (F >> 12) & 63, m1 = (F >> 18) & 63;
+        int dlo = 0, dhi = 0;
+        dlo = sdot4((int)(f.a.x & M4), al.lo.x, dlo);
+        dlo = sdot4((int)(f.a.y & M4), al.lo.y, dlo);
+        dlo = sdot4((int)(f.a.z & M4), al.lo.z, dlo);
+        dlo = sdot4((int)(f.a.w & M4), al.lo.w, dlo);
+        dhi = sdot4((int)((f.a.x >> 4) & M4), al.hi.x, dhi);
+        dhi = sdot4((int)((f.a.y >> 4) & M4), al.hi.y, dhi);
+        dhi = sdot4((int)((f.a.z >> 4) & M4), al.hi.z, dhi);
+        dhi = sdot4((int)((f.a.w >> 4) & M4), al.hi.w, dhi);
+        int isum = __mul24(sc0, dlo) + __mul24(sc1, dhi);
+        int imin = __mul24(m0, al.b0) + __mul24(m1, al.b1);
+        isum = sum8_i(isum);
+        imin = sum8_i(imin);
+        const float d = h2f(h.x & 0xFFFF) * al.d;
+        const float dmin = h2f(h.x >> 16) * al.d;
+        float v = d * (float)isum;
+        v = v - dmin * (float)imin;
+        return pass * 8 + (lane >> 3) < (K >> 8) ? v : 0.0f;
+    } else if constexpr (T == 14) {
+        // high 2 bits of the low-nibble codes sit at bit 2*gl of each qh byte, of the
+        // high-nibble codes at bit 2*gl+4 (gl = (lane&3)>>1); move them to bits 4-5
+        const int shl = 2 * ((lane & 3) >> 1);
+        auto lo = [&](uint32_t l, uint32_t h) { return (int)((l & M4) | ((h << (4 - shl)) & 0x30303030u)); };
+        auto hi = [&](uint32_t l, uint32_t h) { return (int)(((l >> 4) & M4) | ((h >> shl) & 0x30303030u)); };
+        int dlo = 0, dhi = 0;
+        dlo = sdot4(lo(f.a.x, f.b.x), al.lo.x, dlo);
+        dlo = sdot4(lo(f.a.y, f.b.y), al.lo.y, dlo);
+        dlo = sdot4(lo(f.a.z, f.b.z), al.lo.z, dlo);
+        dlo = sdot4(lo(f.a.w, f.b.w), al.lo.w, dlo);
+        dhi = sdot4(hi(f.a.x, f.b.x), al.hi.x, dhi);
+        dhi = sdot4(hi(f.a.y, f.b.y), al.hi.y, dhi);
+        dhi = sdot4(hi(f.a.z, f.b.z), al.hi.z, dhi);
+        dhi = sdot4(hi(f.a.w, f.b.w), al.hi.w, dhi);
+        const int sa = (int)(int8_t)(f.c & 0xFF), sb = (int)(int8_t)(f.c >> 8);
+        int isum = __mul24(sa, dlo - 32 * al.b0) + __mul24(sb, dhi - 32 * al.b1);
+        isum = sum8_i(isum);
+        const float d = h2f(f.e) * al.d;
+        const float v = d * (float)isum;
+        return pass * 8 + (lane >> 3) < (K >> 8) ? v : 0.0f;
+    } else {
+        int s = 0;
+        s = sdot4((int)f.a.x, al.lo.x, s);
+        s = sdot4((int)f.a.y, al.lo.y, s);
+        s = sdot4((int)f.a.z, al.lo.z, s);
+        s = sdot4((int)f.a.w, al.lo.w, s);
+        s = sdot4((int)f.b.x, al.hi.x, s);
+        s = sdot4((int)f.b.y, al.hi.y, s);
+        s = sdot4((int)f.b.z, al.hi.z, s);
+        s = sdot4((int)f.b.w, al.hi.w, s);
+        const float v = (float)s * (h2f(f.e) * al.d);
+        return pass * 64 + lane < (K >> 5) ? v : 0.0f;
+    }
+}
+
+// Row total of the per-lane partials (accumulated over the row's passes), wave-uniform.
+template <int T>
+__device__ __forceinline__ float row_total(float acc) {
+    if constexpr (T == 8) acc = sum8_f(acc);
+    return sum_lanes7(acc);
+}
+
+// ------------------------------------------------------------------ streaming rows
+// NP passes per row (1, 3 or 6); U units per register group; NP <= 3 keeps the lane's
+// activation slices in registers for the whole stream.
+template <int NP>
+struct Cfg {
+    static constexpr int U = NP == 1 ? 4 : 3;
+    static constexpr bool AREG = NP <= 3;
+};
+
+// Loads units [u0, u0 + U) (clamped into [0, n): loads are never skipped, so the
+// compiler's in-order vmcnt accounting stays exact). Unit u -> row lo + u/(NP*NM),
+// matrix (u/NP)%NM, pass u%NP. With NM == 1, rows >= split come from W1 (row - split):
+// two matrices of one type streamed as one row space (q|k).
+template <int T, int NP, int NM>
+__device__ __forceinline__ void load_group(const QMat W0, const QMat W1, int lo, int n, int u0,
+                                           Frag (&f)[Cfg<NP>::U], int split = INT_MAX) {
+#pragma unroll
+    for (int j = 0; j < Cfg<NP>::U; ++j) {
+        const int u = max(0, min(u0 + j, n - 1));
+        const int p = u % NP, m = (u / NP) % NM, i = u / (NP * NM);
+        if constexpr (NM == 1) {
+            const int r = lo + i;
+            f[j] = load_frag<T>(r >= split ? W1 : W0, r >= split ? r - split : r, p);
+        } else {
+            f[j] = load_frag<T>(m ? W1 : W0, lo + i, p);
+        }
+    }
+}
+
+// Streams rows [lo, hi) (wave-uniform) of W0 (and W1 when NM == 2: row pairs, e.g.
+// gate/up); calls epi(row, dot0, dot1) once per row with wave-uniform values. A and B hold
+// the first two groups (units [0, U) and [U, 2U)), issued by the caller before its
+// prologue; groups then alternate between A and B, one group in flight while the other is
+// reduced (no register copies).
+template <int T, int NP, int NM, class Epi>
+__device__ __forceinline__ void stream_rows(const QMat W0, const QMat W1, int lo, int hi, Frag (&A)[Cfg<NP>::U],
+                                            Frag (&B)[Cfg<NP>::U], const ActL &a, Epi &&epi, int split = INT_MAX,
+                                            unsigned long long *trace = nullptr) {
+    constexpr int U = Cfg<NP>::U;
+    const int K = W0.k;
+    const int n = (hi - lo) * NM * NP;
+    if (n <= 0) return;
+    ALane al[Cfg<NP>::AREG ? NP : 1];
+    if constexpr (Cfg<NP>::AREG) {
+#pragma unroll
+        for (int p = 0; p < NP; ++p) al[p] = load_alane<T>(a, K, p);
+    }
+    float acc = 0.0f, g = 0.0f;
+    auto consume = [&](const Frag (&F)[U], int u0) {
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            const int u = u0 + j;
+            if (u < n) {
+                int p;
+                ALane av;
+                if constexpr (NP == 1) {
+                    p = 0;
+                    av = al[0];
+                } else if constexpr (NP == U) {
+                    p = j;
+                    av = al[j];
+                } else {
+                    p = u % NP;
+                    av = load_alane<T>(a, K, p);
+                }
+                acc += dot_frag<T>(F[j], av, K, p);
+                if (p == NP - 1) {
+                    const float v = row_total<T>(acc);
+                    acc = 0.0f;
+                    const int i = u / (NP * NM);
+                    if constexpr (NM == 1) {
+                        epi(lo + i, v, 0.0f);
+                    } else {
+                        if ((u / NP) % NM == 0)
+                            g = v;
+                        else
+                            epi(lo + i, g, v);
+                    }
+                }
+            }
+        }
+    };
+    for (int u0 = 0;;) {
+        consume(A, u0);
+        if (trace && u0 == 0 && blockIdx.x == 0 && threadIdx.x == 0) trace[3] = __builtin_readcyclecounter();
+        u0 += U;
+        if (u0 >= n) break;
+        load_group<T, NP, NM>(W0, W1, lo, n, u0 + U, A, split);
+        consume(B, u0);
+        u0 += U;
+        if (u0 >= n) break;
+        load_group<T, NP, NM>(W0, W1, lo, n, u0 + U, B, split);
+    }
+}
+
+// The first two groups of a wave's stream (before the prologue).
+template <int T, int NP, int NM>
+__device__ __forceinline__ void load_first(const QMat W0, const QMat W1, int lo, int hi, Frag (&A)[Cfg<NP>::U],
+                                           Frag (&B)[Cfg<NP>::U], int split = INT_MAX) {
+    const int n = (hi - lo) * NM * NP;
+    load_group<T, NP, NM>(W0, W1, lo, n, 0, A, split);
+    load_group<T, NP, NM>(W0, W1, lo, n, Cfg<NP>::U, B, split);
+}
+
+// Rows [0, R) over G workgroups: workgroup b owns [R*b/G, R*(b+1)/G), wave w a contiguous
+// eighth of that (wave-uniform, held in scalar registers). R*G < 2^31.
+__device__ inline void wave_range(int R, int &lo, int &hi, int b, int G) {
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int ra = (R * b) / G, rb = (R * (b + 1)) / G;
+    lo = ra + (rb - ra) * w / MW;
+    hi = ra + (rb - ra) * (w + 1) / MW;
+}
+__device__ inline void wave_range(int R, int &lo, int &hi) { wave_range(R, lo, hi, blockIdx.x, gridDim.x); }
+
+// ------------------------------------------------------------------ cross-launch prefetch
+
+__device__ inline void prefetch_range(const uint8_t *base, uint32_t total, uint32_t off, uint32_t bytes,
+                                      char *slot) {
+    const auto r = rsrc(base, total);
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    for (uint32_t c = w; c * 1024u < bytes; c += MW)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void *)slot, 16, lane * 16,
+                                                 off + c * 1024u, 0, 0);
+}
+
+// all arrays of rows [r0, r1) of W
+__device__ inline void prefetch_rows(const QMat &W, int r0, int r1, uint32_t cap, char *slot) {
+    if (r1 <= r0) return;
+    const uint32_t R = (uint32_t)W.rows, n = (uint32_t)(r1 - r0);
+    uint32_t rb[4] = {0, 0, 0, 0};
+    const uint8_t *p[4] = {W.p0, W.p1, W.p2, W.p3};
+    if (W.type == 12) {
+        rb[0] = W.k / 2, rb[1] = (W.k >> 8) * 16;
+    } else if (W.type == 14) {
+        rb[0] = W.k / 2, rb[1] = W.k / 4, rb[2] = W.k / 16, rb[3] = (W.k >> 8) * 2;
+    } else {
+        rb[0] = W.k, rb[1] = (W.k >> 5) * 2;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        if (rb[i]) prefetch_range(p[i], R * rb[i], (uint32_t)r0 * rb[i], min(n * rb[i], cap), slot);
+}
+
+__device__ inline void prefetch_next(const Prefetch &pf, char *lds_slots) {
+    if (pf.mode == 0) return;
+    char *slot = lds_slots + PF_SLOT * __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int b = blockIdx.x;
+    if (pf.mode == 3) {
+        if (b < pf.g_qk) {
+            const int o1 = pf.m[0].rows, o2 = o1 + pf.m[1].rows;
+            const int ra = (o2 * b) / pf.g_qk, rb = (o2 * (b + 1)) / pf.g_qk;
+            prefetch_rows(pf.m[0], ra, min(rb, o1), pf.cap, slot);
+            prefetch_rows(pf.m[1], max(ra, o1) - o1, rb - o1, pf.cap, slot);
+        } else if (b < pf.grid) {
+            const int gv = pf.grid - pf.g_qk, bv = b - pf.g_qk, R = pf.m[2].rows;
+            prefetch_rows(pf.m[2], (R * bv) / gv, (R * (bv + 1)) / gv, pf.cap, slot);
+        }
+        return;
+    }
+    if (b >= pf.grid) return;
+    const int R = pf.m[0].rows, ra = (R * b) / pf.grid, rb = (R * (b + 1)) / pf.grid;
+    prefetch_rows(pf.m[0], ra, rb, pf.cap, slot);
+    if (pf.mode == 2) prefetch_rows(pf.m[1], ra, rb, pf.cap, slot);
+}
+
+// ------------------------------------------------------------------ embedding rows
+__device__ float dequant_elem(const QMat &W, int row, int e) {
+    if (W.type == 12) {
+        const int nsb = W.k >> 8, sb = e >> 8, c = e & 255, j = c >> 6, w = c & 63, hi = w >> 5, l = w & 31;
+        const uint8_t q = W.p0[(size_t)row * (W.k / 2) + sb * 128 + 32 * j + l];
+        const uint8_t *hd = W.p1 + ((size_t)row * nsb + sb) * 16;
+        const uint32_t F = (uint32_t)hd[4 + 3 * j] | ((uint32_t)hd[5 + 3 * j] << 8) | ((uint32_t)hd[6 + 3 * j] << 16);
+        const int sc = (F >> (12 * hi)) & 63, m = (F >> (12 * hi + 6)) & 63;
+        const float d1 = h2f(hd[0] | (hd[1] << 8)) * sc, m1 = h2f(hd[2] | (hd[3] << 8)) * m;
+        return d1 * (float)(hi ? (q >> 4) : (q & 0xF)) - m1;
+    } else if (W.type == 14) {
+        const int nsb = W.k >> 8, sb = e >> 8, c = e & 255, n = c >> 7, w = c & 127, g = w >> 5, l = w & 31;
+        const uint8_t ql = W.p0[(size_t)row * (W.k / 2) + sb * 128 + 64 * n + l + 32 * (g & 1)];
+        const uint8_t qh = W.p1[(size_t)row * (W.k / 4) + sb * 64 + 32 * n + l];
+        const int q = (int)((g < 2 ? (ql & 0xF) : (ql >> 4)) | (((qh >> (2 * g)) & 3) << 4)) - 32;
+        const int is = c >> 4, sn = is >> 3, sw = is & 7;
+        const int sc = ((const int8_t *)W.p2)[(size_t)row * (W.k / 16) + sb * 16 + 2 * (4 * sn + (sw & 3)) + (sw >> 2)];
+        const float dd = h2f(((const uint16_t *)W.p3)[(size_t)row * nsb + sb]);
+        return dd * (float)sc * (float)q;
+    } else {
+        const int nb = W.k >> 5;
+        const int8_t q = ((const int8_t *)W.p0)[(size_t)row * W.k + e];
+        return (float)q * h2f(((const uint16_t *)W.p1)[(size_t)row * nb + (e >> 5)]);
+    }
+}
+
+constexpr int ST = 1024;  // sampler / embedding threads (n_embd <= 4 * ST)
+
+__device__ inline void embed_row(const QMat &emb, int tok, int n, float *x) {
+    float v[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int e = threadIdx.x + i * ST;
+        v[i] = e < n ? dequant_elem(emb, tok, e) : 0.0f;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int e = threadIdx.x + i * ST;
+        if (e < n) x[e] = v[i];
+    }
+}
+
+
+// ------------------------------------------------------------------ host-side grids
+// attn_in grid: q|k rows on the first g_qk workgroups, v rows on the rest
+inline void attn_in_grid(const LlmDims &d, const LayerW &L, int &G, int &g_qk) {
+    const int rows = L.wq.rows + L.wk.rows + L.wv.rows, qk = L.wq.rows + L.wk.rows;
+    G = matvec_grid(d, rows);
+    g_qk = (G * qk + rows / 2) / rows;
+    g_qk = g_qk < 1 ? 1 : (g_qk > G - 1 ? G - 1 : g_qk);
+}
+
+
+// ------------------------------------------------------------------ attention helpers
+// all-reduce over aligned groups of LP (8 or 16) lanes, by DPP; every lane of a group gets
+// the bitwise-same sum
+template <int LP>
+__device__ __forceinline__ float group_sum(float v) {
+    v += dpp_f<0xB1>(v);   // quad_perm [1,0,3,2]
+    v += dpp_f<0x4E>(v);   // quad_perm [2,3,0,1]
+    v += dpp_f<0x141>(v);  // row_half_mirror
+    if constexpr (LP == 16) v += dpp_f<0x140>(v);  // row_mirror
+    return v;
+}
+
+// Merge of the attention chunks' partial records (k_attention) for all heads: thread t
+// owns outputs 4(t + i*MT) .. +3; online softmax merge over chunks, 8 chunks' loads in
+// flight; normalized outputs -> s.xs, then re-quantized into s.a.
+template <int NP>
+__device__ void merge_attention(const LlmDims &d, const float *part, int nch, int K, bool kquant, const Smem &s) {
+    const int hd = d.hd, rec = part_rec(hd);
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+        const int e = (threadIdx.x + i * MT) * 4;
+        if (e < K) {
+            const int h = e / hd, dd = e - h * hd;
+            const float *base = part + (size_t)h * d.max_splits * rec;
+            float M = -INFINITY, L = 0.0f;
+            float4 O = make_float4(0.f, 0.f, 0.f, 0.f);
+            constexpr int CB = 8;  // chunks per batch of loads
+            for (int c0 = 0; c0 < nch; c0 += CB) {
+                float2 ml[CB];
+                float4 oc[CB];
+#pragma unroll
+                for (int j = 0; j < CB; ++j) {
+                    const int c = min(c0 + j, nch - 1);
+                    ml[j] = *reinterpret_cast<const float2 *>(base + (size_t)c * rec + hd);
+                    oc[j] = *reinterpret_cast<const float4 *>(base + (size_t)c * rec + dd);
+                }
+                float mb = M;
+#pragma unroll
+                for (int j = 0; j < CB; ++j) mb = fmaxf(mb, ml[j].x);
+                const float a = M == -INFINITY ? 0.0f : expf(M - mb);
+                L *= a;
+                O.x *= a, O.y *= a, O.z *= a, O.w *= a;
+#pragma unroll
+                for (int j = 0; j < CB; ++j) {
+                    const float w = c0 + j < nch ? expf(ml[j].x - mb) : 0.0f;
+                    L += w * ml[j].y;
+                    O.x += w * oc[j].x, O.y += w * oc[j].y, O.z += w * oc[j].z, O.w += w * oc[j].w;
+                }
+                M = mb;
+            }
+            *reinterpret_cast<float4 *>(s.xs + e) = make_float4(O.x / L, O.y / L, O.z / L, O.w / L);
+        }
+    }
+    __syncthreads();
+    quantize(s.xs, K, kquant, s.a);
+}
+
+__device__ inline float silu_f(float x) { return x / (1.0f + expf(-x)); }
+
+
+// Calls f.template operator()<NP, T>() for the matrix's pass count and weight type.
+template <class F>
+void dispatch_nt(int K, int type, F &&f) {
+    const int np = pick_np(K);
+#define NT_CASE(NPV, TV) \
+    if (np == NPV && type == TV) return f.template operator()<NPV, TV>();
+    NT_CASE(1, 8) NT_CASE(1, 12) NT_CASE(1, 14) NT_CASE(3, 8) NT_CASE(3, 12) NT_CASE(3, 14)
+    NT_CASE(6, 8) NT_CASE(6, 12) NT_CASE(6, 14)
+#undef NT_CASE
+}
+
+}  // namespace
+}  // namespace mio

@@ -78,6 +78,25 @@ struct LlmBuffers {
     int seq;                    // launch index within the step (timeline slot)
 };
 
+// Batched prompt prefill (csrc/hip/llm_prefill.hip): up to kPrefillB prompt tokens per chunk
+// go through every layer with ONE weight pass per launch (the prefill llama_decode of
+// test-to-speech.cpp:132-148); K/V rows are written, no logits are produced.
+constexpr int kPrefillB = 16;
+
+struct PrefillBuffers {
+    float *x;            // [kPrefillB][n_embd] residual streams
+    float *qkv;          // [kPrefillB][(H + 2 Hkv) hd]; q rows are RoPE'd in place
+    float *h;            // [kPrefillB][n_ff]
+    float *part;         // [kPrefillB][H][max_splits][hd + 4] attention chunk partials
+    const float2 *rope;  // [n_ctx][hd/2]
+    const int *tokens;   // device prompt ids (token of position p at tokens[p])
+};
+
+// Prefill of positions [p0, p0 + nt), nt <= kPrefillB: embedding, all layers, K/V rows.
+void launch_prefill_chunk(const LlmDims &d, const LayerW *layers, int n_layer, _Float16 *kcache,
+                          _Float16 *vcache, const QMat &tok_embd, const PrefillBuffers &pb, int p0, int nt,
+                          hipStream_t s);
+
 // Launch one decode step (all layers + head + sampler) on stream s.
 void launch_decode_step(const LlmDims &d, const LayerW *layers, int n_layer, _Float16 *kcache,
                         _Float16 *vcache, const float *out_norm, const QMat &lm, const QMat &tok_embd,

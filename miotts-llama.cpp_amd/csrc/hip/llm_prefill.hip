@@ -1,0 +1,582 @@
+// Batched prompt prefill for gfx950 (replaces the prefill llama_decode of
+// test-to-speech.cpp:132-148: every prompt token through every layer, K/V cache rows
+// written, logits needed only for the last token, which the decode step then produces).
+//
+// The decode step streams all weights once per token; the prompt (tens of tokens) would pay
+// that once per prompt token. Here a chunk of up to kPrefillB tokens shares ONE weight pass
+// per launch: the streaming-rows engine (llm_device.h) loads each weight fragment once and
+// dots it with every token's re-quantized activation slice, which lives in LDS. Per layer:
+//   k_pf_attn_in   RMSNorm + quantize nt tokens -> q|k|v for all of them
+//   k_pf_rope      q/k RMSNorm (qwen3) + RoPE + f16 rounding; k/v rows -> F16 KV cache
+//   k_pf_attention per (128-position chunk, kv head, token): causal online softmax over
+//                  positions <= the token's own, chunk partial records
+//   k_pf_attn_out  per-token chunk merge + quantize -> O matvec -> x += .
+//   k_pf_ffn_in    RMSNorm + quantize -> gate|up -> silu(g)*u
+//   k_pf_ffn_down  quantize -> down -> x += .
+// Arithmetic is the decode step's, token by token, in the same order (same quantizers,
+// same per-superblock integer sums, the same pass order per row, the same online-softmax
+// order): the K/V cache and the last token's logits equal a token-by-token decode bit for
+// bit (tests/test_llm_gpu.py::test_batched_prefill_matches_sequential).
+#include "llm_device.h"
+
+#pragma clang fp contract(off)
+
+namespace mio {
+namespace {
+
+constexpr int LDS_MAX = 160 * 1024;
+
+// ------------------------------------------------------------------ LDS layout
+// xs f32[K] | red 128 B | act[t] = {qs i8[K] | d f32[K/32+8] | bs i16[K/16+8]} x nt |
+// resid f32[MW][nt * rpw] (the wave's residual rows per token)
+__host__ __device__ inline size_t act_bytes(int K) {
+    return ((size_t)K + (size_t)(K / 32 + 8) * 4 + (size_t)(K / 16 + 8) * 2 + 15) & ~(size_t)15;
+}
+__host__ __device__ inline size_t act_base(int K) { return (size_t)K * 4 + 128; }
+__host__ __device__ inline size_t pf_lds_bytes(int K, int nt, int rpw) {
+    return act_base(K) + act_bytes(K) * nt + (size_t)MW * nt * rpw * 4;
+}
+
+__device__ inline Smem carve_t(char *base, int K, int t) {
+    Smem s;
+    s.xs = (float *)base;
+    s.red = (double *)(base + (size_t)K * 4);
+    char *a = base + act_base(K) + act_bytes(K) * t;
+    s.a.qs = (int8_t *)a;
+    s.a.d = (float *)(a + K);
+    s.a.bs = (int16_t *)(a + K + (size_t)(K / 32 + 8) * 4);
+    return s;
+}
+__device__ inline float *resid_lds(char *base, int K, int nt, int rpw) {
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    return (float *)(base + act_base(K) + act_bytes(K) * nt) + (size_t)w * nt * rpw;
+}
+
+// ------------------------------------------------------------------ batched streaming rows
+// A register group holds RU whole rows (all NM matrices, all NP passes): every fragment is
+// loaded once and dotted with each token's activation; row totals per token as in the
+// decode engine (acc over passes in order, then row_total).
+template <int NP, int NM>
+struct CfgB {
+    static constexpr int RU = NP * NM >= 4 ? 1 : 4 / (NP * NM);
+    static constexpr int U = RU * NP * NM;
+};
+
+template <int T, int NP, int NM>
+__device__ __forceinline__ void load_rows(const QMat W0, const QMat W1, int r, int hi, Frag (&F)[CfgB<NP, NM>::U],
+                                          int split) {
+#pragma unroll
+    for (int ri = 0; ri < CfgB<NP, NM>::RU; ++ri) {
+        const int row = min(r + ri, hi - 1);
+#pragma unroll
+        for (int m = 0; m < NM; ++m)
+#pragma unroll
+            for (int p = 0; p < NP; ++p) {
+                Frag &f = F[(ri * NM + m) * NP + p];
+                if constexpr (NM == 1)
+                    f = load_frag<T>(row >= split ? W1 : W0, row >= split ? row - split : row, p);
+                else
+                    f = load_frag<T>(m ? W1 : W0, row, p);
+            }
+    }
+}
+
+template <int T, int NP, int NM>
+__device__ __forceinline__ void load_first_b(const QMat W0, const QMat W1, int lo, int hi,
+                                             Frag (&A)[CfgB<NP, NM>::U], Frag (&B)[CfgB<NP, NM>::U],
+                                             int split = INT_MAX) {
+    if (hi <= lo) return;
+    load_rows<T, NP, NM>(W0, W1, lo, hi, A, split);
+    load_rows<T, NP, NM>(W0, W1, lo + CfgB<NP, NM>::RU, hi, B, split);
+}
+
+// epi(row, t, dot0, dot1): wave-uniform values, once per (row, token)
+template <int T, int NP, int NM, class Epi>
+__device__ __forceinline__ void stream_rows_b(const QMat W0, const QMat W1, int lo, int hi,
+                                              Frag (&A)[CfgB<NP, NM>::U], Frag (&B)[CfgB<NP, NM>::U], char *smem,
+                                              int nt, Epi &&epi, int split = INT_MAX) {
+    constexpr int RU = CfgB<NP, NM>::RU, U = CfgB<NP, NM>::U;
+    const int K = W0.k;
+    if (hi <= lo) return;
+    auto consume = [&](const Frag (&F)[U], int r) {
+        for (int t = 0; t < nt; ++t) {
+            const Smem s = carve_t(smem, K, t);
+            float acc[RU * NM];
+#pragma unroll
+            for (int i = 0; i < RU * NM; ++i) acc[i] = 0.0f;
+#pragma unroll
+            for (int p = 0; p < NP; ++p) {
+                const ALane al = load_alane<T>(s.a, K, p);
+#pragma unroll
+                for (int i = 0; i < RU * NM; ++i) acc[i] += dot_frag<T>(F[i * NP + p], al, K, p);
+            }
+#pragma unroll
+            for (int ri = 0; ri < RU; ++ri) {
+                if (r + ri < hi) {
+                    const float v0 = row_total<T>(acc[ri * NM]);
+                    const float v1 = NM == 2 ? row_total<T>(acc[ri * NM + NM - 1]) : 0.0f;
+                    epi(r + ri, t, v0, v1);
+                }
+            }
+        }
+    };
+    for (int r = lo;;) {
+        consume(A, r);
+        r += RU;
+        if (r >= hi) break;
+        load_rows<T, NP, NM>(W0, W1, r + RU, hi, A, split);
+        consume(B, r);
+        r += RU;
+        if (r >= hi) break;
+        load_rows<T, NP, NM>(W0, W1, r + RU, hi, B, split);
+    }
+}
+
+// RMSNorm + quantize of nt tokens (token 0's x was loaded before the first weight group)
+template <int NP>
+__device__ void prologue_rms(XRegs<NP> &xr, const float *x, const float *norm_w, int K, float eps, bool kq,
+                             char *smem, int nt) {
+    for (int t = 0; t < nt; ++t) {
+        if (t) load_x(x + (size_t)t * K, norm_w, K, xr);
+        rmsnorm_quant(xr, K, eps, kq, carve_t(smem, K, t));
+    }
+}
+
+// Residual rows [lo, hi) of every token (row stride E) in two registers per lane: entry
+// i = t * rpw + r at lane i % 64, register i / 64 (nt * rpw <= 128, host-checked).
+struct Resid {
+    float v0, v1;
+};
+__device__ inline Resid load_resid_b(const float *x, int E, int lo, int hi, int nt, int rpw) {
+    const int lane = threadIdx.x & 63;
+    Resid r;
+    float *o[2] = {&r.v0, &r.v1};
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const int i = lane + 64 * k, t = i / rpw, rr = i - t * rpw;
+        *o[k] = (t < nt && lo + rr < hi) ? x[(size_t)t * E + lo + rr] : 0.0f;
+    }
+    return r;
+}
+__device__ inline void store_resid_b(const Resid &r, float *lds, int nt, int rpw) {
+    const int lane = threadIdx.x & 63;
+    if (lane < nt * rpw) lds[lane] = r.v0;
+    if (lane + 64 < nt * rpw) lds[lane + 64] = r.v1;
+}
+
+// ------------------------------------------------------------------ kernels
+template <int NP, int TQ, int TV>
+__global__ __launch_bounds__(MT) void k_pf_attn_in(LlmDims d, const float *norm_w, QMat wq, QMat wk, QMat wv,
+                                                   int g_qk, PrefillBuffers pb, int nt) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int K = d.n_embd, QD = (d.n_head + 2 * d.n_kv) * d.hd;
+    const int lane = threadIdx.x & 63;
+    XRegs<NP> xr;
+    load_x(pb.x, norm_w, K, xr);
+    const int o1 = wq.rows, o2 = wq.rows + wk.rows;
+    Frag ga[CfgB<NP, 1>::U], gb[CfgB<NP, 1>::U];
+    int lo, hi;
+    if ((int)blockIdx.x < g_qk) {
+        wave_range(o2, lo, hi, blockIdx.x, g_qk);
+        load_first_b<TQ, NP, 1>(wq, wk, lo, hi, ga, gb, o1);
+        prologue_rms(xr, pb.x, norm_w, K, d.eps, TQ != 8, smem, nt);
+        stream_rows_b<TQ, NP, 1>(wq, wk, lo, hi, ga, gb, smem, nt, [&](int row, int t, float v, float) {
+            if (lane == 0) pb.qkv[(size_t)t * QD + row] = v;
+        }, o1);
+    } else {
+        wave_range(wv.rows, lo, hi, blockIdx.x - g_qk, gridDim.x - g_qk);
+        load_first_b<TV, NP, 1>(wv, wv, lo, hi, ga, gb);
+        prologue_rms(xr, pb.x, norm_w, K, d.eps, TQ != 8, smem, nt);
+        stream_rows_b<TV, NP, 1>(wv, wv, lo, hi, ga, gb, smem, nt, [&](int row, int t, float v, float) {
+            if (lane == 0) pb.qkv[(size_t)t * QD + o2 + row] = v;
+        });
+    }
+}
+
+// One wave per (head, token): q heads are normalized / rotated / f16-rounded in place, k
+// heads likewise and written with the v row to the F16 cache at the token's position.
+// Same arithmetic as k_attention's head preparation.
+template <int HD>
+__global__ __launch_bounds__(64) void k_pf_rope(LlmDims d, const float *q_norm, const float *k_norm, _Float16 *kc,
+                                                _Float16 *vc, PrefillBuffers pb, int p0) {
+    constexpr int PER = HD / 64;
+    __shared__ float row[HD];
+    const int hh = blockIdx.x, t = blockIdx.y, pos = p0 + t, lane = threadIdx.x;
+    const int QD = (d.n_head + 2 * d.n_kv) * HD;
+    const bool isk = hh >= d.n_head;
+    const int kvh = hh - d.n_head;
+    float *src = pb.qkv + (size_t)t * QD + (size_t)hh * HD;
+    const float *vsrc = pb.qkv + (size_t)t * QD + (size_t)(d.n_head + d.n_kv + (isk ? kvh : 0)) * HD;
+    const float2 *rope = pb.rope + (size_t)pos * (HD / 2);
+    const float *nw = isk ? k_norm : q_norm;
+    float v[PER], w[PER], vv[PER];
+    float2 cs[PER];
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+        const int p = lane + 64 * i;
+        v[i] = src[p];
+        w[i] = d.qk_norm ? nw[p] : 1.0f;
+        vv[i] = isk ? vsrc[p] : 0.0f;
+        cs[i] = p < HD / 2 ? rope[p] : make_float2(0.0f, 0.0f);
+    }
+    if (d.qk_norm) {
+        double ss = 0.0;
+#pragma unroll
+        for (int i = 0; i < PER; ++i) ss += (double)(v[i] * v[i]);
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) ss += __shfl_xor(ss, o);
+        const float mean = (float)(ss / HD);
+        const float scale = 1.0f / sqrtf(mean + d.eps);
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const float tt = v[i] * scale;
+            v[i] = tt * w[i];
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < PER; ++i) row[lane + 64 * i] = v[i];
+    __syncthreads();
+    float o0[PER], o1[PER];
+    int i0s[PER], i1s[PER];
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+        const int p = lane + 64 * i;
+        i0s[i] = -1;
+        if (p < HD / 2) {
+            const int i0 = d.neox ? p : 2 * p, i1 = d.neox ? p + HD / 2 : 2 * p + 1;
+            const float x0 = row[i0], x1 = row[i1];
+            o0[i] = x0 * cs[i].x - x1 * cs[i].y;
+            o1[i] = x0 * cs[i].y + x1 * cs[i].x;
+            i0s[i] = i0, i1s[i] = i1;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < PER; ++i)
+        if (i0s[i] >= 0) {
+            row[i0s[i]] = f16r(o0[i]);
+            row[i1s[i]] = f16r(o1[i]);
+        }
+    __syncthreads();
+    if (!isk) {
+#pragma unroll
+        for (int i = 0; i < PER; ++i) src[lane + 64 * i] = row[lane + 64 * i];
+    } else {
+        _Float16 *kd = kc + ((size_t)kvh * d.n_ctx + pos) * HD;
+        _Float16 *vd = vc + ((size_t)kvh * d.n_ctx + pos) * HD;
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int p = lane + 64 * i;
+            kd[p] = (_Float16)row[p];
+            vd[p] = (_Float16)f16r(vv[i]);
+        }
+    }
+}
+
+// One 256-thread workgroup per (128-position chunk, kv head, token): causal online softmax
+// over the chunk's positions <= the token's position, all rows read from the cache (this
+// chunk's own rows were written by k_pf_rope). Slot / merge order as k_attention.
+template <int HD, int G>
+__global__ __launch_bounds__(NT) void k_pf_attention(LlmDims d, const _Float16 *kc, const _Float16 *vc,
+                                                     PrefillBuffers pb, int p0) {
+    constexpr int LP = HD / 8;
+    constexpr int NS = NT / LP;
+    constexpr int IT = ATT_CHUNK / NS;
+    constexpr int REC = part_rec(HD);
+    typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+    __shared__ float qs[G][HD];
+    __shared__ float wres[NWAVE][G][HD + 2];
+    const int kvh = blockIdx.y, ch = blockIdx.x, t = blockIdx.z, pos = p0 + t;
+    const int t0 = ch * ATT_CHUNK;
+    if (t0 > pos) return;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int lp = lane % LP, sl = tid / LP;
+    const int QD = (d.n_head + 2 * d.n_kv) * HD;
+    const _Float16 *kbase = kc + (size_t)kvh * d.n_ctx * HD;
+    const _Float16 *vbase = vc + (size_t)kvh * d.n_ctx * HD;
+    h8 kr[IT], vr[IT];
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+        const int tt = min(t0 + sl + NS * it, pos);
+        kr[it] = *reinterpret_cast<const h8 *>(kbase + (size_t)tt * HD + lp * 8);
+        vr[it] = *reinterpret_cast<const h8 *>(vbase + (size_t)tt * HD + lp * 8);
+    }
+    const float *qsrc = pb.qkv + (size_t)t * QD + (size_t)kvh * G * HD;
+    for (int e = tid; e < G * HD; e += NT) qs[e / HD][e % HD] = qsrc[e];
+    __syncthreads();
+    float qv[G][8];
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) qv[g][i] = qs[g][lp * 8 + i];
+    float m[G], l[G], acc[G][8];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        m[g] = -INFINITY, l[g] = 0.0f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[g][i] = 0.0f;
+    }
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+        const bool valid = t0 + sl + NS * it <= pos;
+        float kf[8], vf[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) kf[i] = (float)kr[it][i], vf[i] = (float)vr[it][i];
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            float sdot = 0.0f;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) sdot = fmaf(qv[g][i], kf[i], sdot);
+            sdot = group_sum<LP>(sdot);
+            const float sc = valid ? sdot * d.scale : -INFINITY;
+            const float mn = fmaxf(m[g], sc);
+            const float c = m[g] == mn ? 1.0f : expf(m[g] - mn);
+            const float p = valid ? expf(sc - mn) : 0.0f;
+            l[g] = l[g] * c + p;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) acc[g][i] = acc[g][i] * c + p * vf[i];
+            m[g] = mn;
+        }
+    }
+#pragma unroll
+    for (int o = LP; o < 64; o <<= 1) {
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const float m2 = __shfl_xor(m[g], o), l2 = __shfl_xor(l[g], o);
+            const float mn = fmaxf(m[g], m2);
+            const float c1 = m[g] == -INFINITY ? 0.0f : expf(m[g] - mn);
+            const float c2 = m2 == -INFINITY ? 0.0f : expf(m2 - mn);
+            l[g] = l[g] * c1 + l2 * c2;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const float a2 = __shfl_xor(acc[g][i], o);
+                acc[g][i] = acc[g][i] * c1 + a2 * c2;
+            }
+            m[g] = mn;
+        }
+    }
+    if (lane < LP) {
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) wres[wave][g][lp * 8 + i] = acc[g][i];
+            if (lp == 0) wres[wave][g][HD] = m[g], wres[wave][g][HD + 1] = l[g];
+        }
+    }
+    __syncthreads();
+    for (int e = tid; e < G * HD; e += NT) {
+        const int g = e / HD, dd = e - g * HD;
+        float M = -INFINITY;
+#pragma unroll
+        for (int w = 0; w < NWAVE; ++w) M = fmaxf(M, wres[w][g][HD]);
+        float L = 0.0f, O = 0.0f;
+#pragma unroll
+        for (int w = 0; w < NWAVE; ++w) {
+            const float mw = wres[w][g][HD];
+            const float c = mw == -INFINITY ? 0.0f : expf(mw - M);
+            L += c * wres[w][g][HD + 1];
+            O += c * wres[w][g][dd];
+        }
+        float *dst = pb.part + (((size_t)t * d.n_head + kvh * G + g) * d.max_splits + ch) * REC;
+        dst[dd] = O;
+        if (dd == 0) dst[HD] = M, dst[HD + 1] = L;
+    }
+}
+
+template <int NP, int T>
+__global__ __launch_bounds__(MT) void k_pf_attn_out(LlmDims d, QMat wo, PrefillBuffers pb, int p0, int nt, int rpw) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int K = wo.k, E = d.n_embd;
+    int lo, hi;
+    wave_range(wo.rows, lo, hi);
+    const Resid xr = load_resid_b(pb.x, E, lo, hi, nt, rpw);
+    Frag ga[CfgB<NP, 1>::U], gb[CfgB<NP, 1>::U];
+    load_first_b<T, NP, 1>(wo, wo, lo, hi, ga, gb);
+    float *res = resid_lds(smem, K, nt, rpw);
+    store_resid_b(xr, res, nt, rpw);
+    const size_t tstride = (size_t)d.n_head * d.max_splits * part_rec(d.hd);
+    for (int t = 0; t < nt; ++t)
+        merge_attention<NP>(d, pb.part + t * tstride, (p0 + t) / ATT_CHUNK + 1, K, T != 8, carve_t(smem, K, t));
+    stream_rows_b<T, NP, 1>(wo, wo, lo, hi, ga, gb, smem, nt, [&](int row, int t, float v, float) {
+        const float r = res[t * rpw + row - lo];
+        if ((threadIdx.x & 63) == 0) pb.x[(size_t)t * E + row] = v + r;
+    });
+}
+
+template <int NP, int T>
+__global__ __launch_bounds__(MT) void k_pf_ffn_in(LlmDims d, const float *norm_w, QMat gate, QMat up,
+                                                  PrefillBuffers pb, int nt) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int K = d.n_embd;
+    XRegs<NP> xr;
+    load_x(pb.x, norm_w, K, xr);
+    int lo, hi;
+    wave_range(gate.rows, lo, hi);
+    Frag ga[CfgB<NP, 2>::U], gb[CfgB<NP, 2>::U];
+    load_first_b<T, NP, 2>(gate, up, lo, hi, ga, gb);
+    prologue_rms(xr, pb.x, norm_w, K, d.eps, T != 8, smem, nt);
+    stream_rows_b<T, NP, 2>(gate, up, lo, hi, ga, gb, smem, nt, [&](int row, int t, float g, float u) {
+        if ((threadIdx.x & 63) == 0) pb.h[(size_t)t * d.n_ff + row] = silu_f(g) * u;
+    });
+}
+
+template <int NP, int T>
+__global__ __launch_bounds__(MT) void k_pf_ffn_down(LlmDims d, QMat down, PrefillBuffers pb, int nt, int rpw) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int K = down.k, E = d.n_embd;
+    XRegs<NP> xr;
+    load_x(pb.h, nullptr, K, xr);
+    int lo, hi;
+    wave_range(down.rows, lo, hi);
+    const Resid rr = load_resid_b(pb.x, E, lo, hi, nt, rpw);
+    Frag ga[CfgB<NP, 1>::U], gb[CfgB<NP, 1>::U];
+    load_first_b<T, NP, 1>(down, down, lo, hi, ga, gb);
+    float *res = resid_lds(smem, K, nt, rpw);
+    store_resid_b(rr, res, nt, rpw);
+    for (int t = 0; t < nt; ++t) {
+        if (t) load_x(pb.h + (size_t)t * K, nullptr, K, xr);
+        plain_quant(xr, K, T != 8, carve_t(smem, K, t));
+    }
+    stream_rows_b<T, NP, 1>(down, down, lo, hi, ga, gb, smem, nt, [&](int row, int t, float v, float) {
+        const float r = res[t * rpw + row - lo];
+        if ((threadIdx.x & 63) == 0) pb.x[(size_t)t * E + row] = v + r;
+    });
+}
+
+__global__ __launch_bounds__(ST) void k_pf_embed(LlmDims d, QMat emb, PrefillBuffers pb, int p0) {
+    const int t = blockIdx.x;
+    embed_row(emb, pb.tokens[p0 + t], d.n_embd, pb.x + (size_t)t * d.n_embd);
+}
+
+template <int HD>
+void launch_pf_attention(int G, dim3 grid, hipStream_t s, const LlmDims &d, const _Float16 *kc, const _Float16 *vc,
+                         const PrefillBuffers &pb, int p0) {
+    switch (G) {
+        case 1: hipLaunchKernelGGL((k_pf_attention<HD, 1>), grid, dim3(NT), 0, s, d, kc, vc, pb, p0); break;
+        case 2: hipLaunchKernelGGL((k_pf_attention<HD, 2>), grid, dim3(NT), 0, s, d, kc, vc, pb, p0); break;
+        case 3: hipLaunchKernelGGL((k_pf_attention<HD, 3>), grid, dim3(NT), 0, s, d, kc, vc, pb, p0); break;
+        case 4: hipLaunchKernelGGL((k_pf_attention<HD, 4>), grid, dim3(NT), 0, s, d, kc, vc, pb, p0); break;
+        case 8: hipLaunchKernelGGL((k_pf_attention<HD, 8>), grid, dim3(NT), 0, s, d, kc, vc, pb, p0); break;
+        default: break;
+    }
+}
+
+// Dynamic LDS beyond the default 64 KB needs the per-kernel opt-in (once per instantiation).
+template <class Kern>
+void allow_lds(Kern k) {
+    static bool done = false;
+    if (!done) {
+        hipFuncSetAttribute(reinterpret_cast<const void *>(k), hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
+        done = true;
+    }
+}
+
+// residual rows per wave of a matvec over `rows` rows on `grid` workgroups (wave_range)
+int rows_per_wave(int rows, int grid) {
+    const int rg = (rows + grid - 1) / grid;
+    return (rg + MW - 1) / MW;
+}
+
+// Largest token count per launch that fits LDS (and the two residual registers).
+int tokens_per_launch(int K, int nt, int rpw) {
+    int n = nt;
+    while (n > 1 && (pf_lds_bytes(K, n, rpw) > (size_t)LDS_MAX || n * rpw > 128)) --n;
+    return n;
+}
+
+PrefillBuffers shifted(const LlmDims &d, const PrefillBuffers &pb, int t) {
+    PrefillBuffers q = pb;
+    q.x += (size_t)t * d.n_embd;
+    q.qkv += (size_t)t * (d.n_head + 2 * d.n_kv) * d.hd;
+    q.h += (size_t)t * d.n_ff;
+    q.part += (size_t)t * d.n_head * d.max_splits * part_rec(d.hd);
+    return q;
+}
+
+}  // namespace
+
+void launch_prefill_chunk(const LlmDims &d, const LayerW *layers, int n_layer, _Float16 *kcache,
+                          _Float16 *vcache, const QMat &tok_embd, const PrefillBuffers &pb, int p0, int nt,
+                          hipStream_t s) {
+    if (nt <= 0) return;
+    const size_t layer_kv = (size_t)d.n_kv * d.n_ctx * d.hd;
+    const int G = d.n_head / d.n_kv;
+    hipLaunchKernelGGL(k_pf_embed, dim3(nt), dim3(ST), 0, s, d, tok_embd, pb, p0);
+    // sub-launches over token ranges that fit LDS: f(t_off, n, shifted buffers)
+    auto over_tokens = [&](int K, int rpw, auto &&f) {
+        const int per = tokens_per_launch(K, nt, rpw);
+        for (int t = 0; t < nt; t += per) f(t, nt - t < per ? nt - t : per, shifted(d, pb, t));
+    };
+    for (int il = 0; il < n_layer; ++il) {
+        const LayerW &L = layers[il];
+        _Float16 *kc = kcache + il * layer_kv, *vc = vcache + il * layer_kv;
+        {
+            int GW, g_qk;
+            attn_in_grid(d, L, GW, g_qk);
+            over_tokens(d.n_embd, 0, [&](int, int n, const PrefillBuffers &q) {
+                const size_t lds = pf_lds_bytes(d.n_embd, n, 0);
+                dispatch_nt(d.n_embd, L.wq.type, [&]<int NP, int TQ>() {
+                    auto go = [&]<int TV>() {
+                        allow_lds(k_pf_attn_in<NP, TQ, TV>);
+                        hipLaunchKernelGGL((k_pf_attn_in<NP, TQ, TV>), dim3(GW), dim3(MT), lds, s, d, L.attn_norm,
+                                           L.wq, L.wk, L.wv, g_qk, q, n);
+                    };
+                    if constexpr (TQ == 8) {
+                        go.template operator()<8>();
+                    } else {
+                        if (L.wv.type == 14)
+                            go.template operator()<14>();
+                        else
+                            go.template operator()<12>();
+                    }
+                });
+            });
+        }
+        {
+            const dim3 grid(d.n_head + d.n_kv, nt);
+            if (d.hd == 128)
+                hipLaunchKernelGGL((k_pf_rope<128>), grid, dim3(64), 0, s, d, L.q_norm, L.k_norm, kc, vc, pb, p0);
+            else
+                hipLaunchKernelGGL((k_pf_rope<64>), grid, dim3(64), 0, s, d, L.q_norm, L.k_norm, kc, vc, pb, p0);
+        }
+        {
+            const dim3 grid((p0 + nt - 1) / ATT_CHUNK + 1, d.n_kv, nt);
+            if (d.hd == 128)
+                launch_pf_attention<128>(G, grid, s, d, kc, vc, pb, p0);
+            else
+                launch_pf_attention<64>(G, grid, s, d, kc, vc, pb, p0);
+        }
+        {
+            const int grid = matvec_grid(d, L.wo.rows), rpw = rows_per_wave(L.wo.rows, grid);
+            over_tokens(L.wo.k, rpw, [&](int t, int n, const PrefillBuffers &q) {
+                dispatch_nt(L.wo.k, L.wo.type, [&]<int NP, int T>() {
+                    allow_lds(k_pf_attn_out<NP, T>);
+                    hipLaunchKernelGGL((k_pf_attn_out<NP, T>), dim3(grid), dim3(MT), pf_lds_bytes(L.wo.k, n, rpw), s,
+                                       d, L.wo, q, p0 + t, n, rpw);
+                });
+            });
+        }
+        {
+            const int grid = matvec_grid(d, L.gate.rows);
+            over_tokens(d.n_embd, 0, [&](int, int n, const PrefillBuffers &q) {
+                dispatch_nt(d.n_embd, L.gate.type, [&]<int NP, int T>() {
+                    allow_lds(k_pf_ffn_in<NP, T>);
+                    hipLaunchKernelGGL((k_pf_ffn_in<NP, T>), dim3(grid), dim3(MT), pf_lds_bytes(d.n_embd, n, 0), s, d,
+                                       L.ffn_norm, L.gate, L.up, q, n);
+                });
+            });
+        }
+        {
+            const int grid = matvec_grid(d, L.down.rows), rpw = rows_per_wave(L.down.rows, grid);
+            over_tokens(L.down.k, rpw, [&](int, int n, const PrefillBuffers &q) {
+                dispatch_nt(L.down.k, L.down.type, [&]<int NP, int T>() {
+                    allow_lds(k_pf_ffn_down<NP, T>);
+                    hipLaunchKernelGGL((k_pf_ffn_down<NP, T>), dim3(grid), dim3(MT), pf_lds_bytes(L.down.k, n, rpw),
+                                       s, d, L.down, q, n, rpw);
+                });
+            });
+        }
+    }
+}
+
+}  // namespace mio

@@ -29,7 +29,8 @@ struct mio_hip_llm {
     float *out_norm = nullptr;
     _Float16 *kc = nullptr, *vc = nullptr;
     mio::LlmBuffers buf{};
-    int *d_tokens = nullptr, *d_force = nullptr;
+    int *d_tokens = nullptr, *d_force = nullptr, *d_prompt = nullptr;
+    mio::PrefillBuffers pf{};  // batched prompt prefill (kPrefillB tokens per chunk)
     int max_steps = 0;
     std::vector<void *> allocs;
     uint64_t weight_bytes = 0;
@@ -161,12 +162,35 @@ int put_cfg(mio_hip_llm *m, const mio::SampleCfg &c) {
     return MIO_OK;
 }
 
-int set_state(mio_hip_llm *m, int pos, int token) {
-    mio::StepState st{pos, 0, token, 0};
+int set_state(mio_hip_llm *m, int pos, int token, int step = 0) {
+    mio::StepState st{pos, step, token, 0};
     MIO_HIP_CHECK(hipMemcpyAsync(m->buf.st, &st, sizeof(st), hipMemcpyHostToDevice, m->d->stream));
     mio::launch_embed_token(m->dims, m->tok, m->buf, m->d->stream);
     MIO_HIP_CHECK(hipGetLastError());
     return MIO_OK;
+}
+
+// Batched prefill of prompt positions [0, n) (tokens already in m->d_prompt): chunks of
+// kPrefillB tokens, one weight pass per launch (llm_prefill.hip). MIO_SEQ_PREFILL=1 is not
+// handled here (see llm_begin).
+int prefill(mio_hip_llm *m, int n) {
+    for (int p0 = 0; p0 < n; p0 += mio::kPrefillB) {
+        const int nt = n - p0 < mio::kPrefillB ? n - p0 : mio::kPrefillB;
+        mio::launch_prefill_chunk(m->dims, m->layers.data(), m->n_layer, m->kc, m->vc, m->tok, m->pf, p0, nt,
+                                  m->d->stream);
+        MIO_HIP_CHECK(hipGetLastError());
+    }
+    return MIO_OK;
+}
+
+int upload_prompt(mio_hip_llm *m, const int32_t *prompt, int n) {
+    MIO_HIP_CHECK(hipMemcpyAsync(m->d_prompt, prompt, (size_t)n * 4, hipMemcpyHostToDevice, m->d->stream));
+    return MIO_OK;
+}
+
+bool sequential_prefill() {
+    static const bool seq = getenv("MIO_SEQ_PREFILL") && getenv("MIO_SEQ_PREFILL")[0] == '1';
+    return seq;
 }
 
 }  // namespace
@@ -205,8 +229,18 @@ int llm_begin(mio_hip_llm *m, const int32_t *prompt, int n_prompt, int max_new, 
     m->n_prompt = n_prompt;
     m->max_new = max_new;
     m->steps_total = n_prompt - 1 + max_new;
-    m->steps_issued = 0;
-    return set_state(m, 0, prompt[0]);
+    // prompt positions [0, P) are prefilled here: batched (one weight pass per chunk of
+    // kPrefillB tokens), or, with MIO_SEQ_PREFILL=1, as P forced decode steps; decoding
+    // then starts at position P with the step counter at P either way (same sampler stream)
+    const int P = n_prompt - 1;
+    if (sequential_prefill()) {
+        m->steps_issued = 0;
+        if ((rc = set_state(m, 0, prompt[0]))) return rc;
+        return llm_run(m, P);
+    }
+    if ((rc = upload_prompt(m, prompt, n_prompt)) || (rc = prefill(m, P))) return rc;
+    m->steps_issued = P;
+    return set_state(m, P, prompt[P], P);
 }
 
 int llm_run(mio_hip_llm *m, int n_steps) {
@@ -393,6 +427,12 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
     m->max_steps = n_ctx;
     m->d_tokens = dalloc<int>(m, m->max_steps);
     m->d_force = dalloc<int>(m, m->max_steps);
+    m->d_prompt = dalloc<int>(m, n_ctx);
+    m->pf.x = dalloc<float>(m, (size_t)mio::kPrefillB * D.n_embd);
+    m->pf.qkv = dalloc<float>(m, (size_t)mio::kPrefillB * qkv);
+    m->pf.h = dalloc<float>(m, (size_t)mio::kPrefillB * D.n_ff);
+    m->pf.part = dalloc<float>(m, (size_t)mio::kPrefillB * D.n_head * D.max_splits * (D.hd + 4));
+    m->pf.tokens = m->d_prompt;
     // RoPE table, ggml rope-cache recurrence (theta = p; theta *= base^(-2/hd) per pair)
     std::vector<float2> rope((size_t)n_ctx * (D.hd / 2));
     const float theta_scale = powf(base, -2.0f / D.hd);
@@ -405,7 +445,8 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
     }
     float2 *dr = dalloc<float2>(m, rope.size());
     if (!m->kc || !m->vc || !m->buf.x || !m->buf.qkv || !m->buf.h || !m->buf.logits ||
-        !m->buf.part || !m->buf.smp || !m->buf.st || !m->d_cfg || !m->d_tokens || !m->d_force || !dr) {
+        !m->buf.part || !m->buf.smp || !m->buf.st || !m->d_cfg || !m->d_tokens || !m->d_force || !dr ||
+        !m->d_prompt || !m->pf.x || !m->pf.qkv || !m->pf.h || !m->pf.part) {
         mio::set_error("llm_load: device allocation failed");
         return fail(MIO_ERR_OOM);
     }
@@ -414,6 +455,7 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
     // (measured slower on MI355X: kept as an opt-in experiment)
     D.prefetch = (getenv("MIO_PREFETCH") && getenv("MIO_PREFETCH")[0] == '1') ? 1 : 0;
     m->buf.rope = dr;
+    m->pf.rope = dr;
     *out = m;
     return MIO_OK;
 }
@@ -468,9 +510,8 @@ extern "C" int mio_hip_llm_generate(mio_hip_llm *m, const int32_t *prompt, int n
     if (check_interval <= 0) check_interval = total;
     std::vector<int32_t> toks;
     bool done = false;
-    // prefill (forced prompt tokens) + check every `check_interval` generated tokens (the
+    // (llm_begin prefilled the prompt) check every `check_interval` generated tokens (the
     // streaming cadence, test-to-speech.cpp:499,608) for an end token
-    if ((rc = mio::llm_run(m, n_prompt - 1))) return rc;
     while (!done) {
         if ((rc = mio::llm_run(m, check_interval))) return rc;
         if ((rc = mio::llm_poll(m, toks, &done))) return rc;
@@ -479,6 +520,18 @@ extern "C" int mio_hip_llm_generate(mio_hip_llm *m, const int32_t *prompt, int n
     std::memcpy(out_tokens, toks.data(), (size_t)n * 4);
     *n_out = n;
     return MIO_OK;
+}
+
+extern "C" int mio_hip_llm_prefill(mio_hip_llm *m, const int32_t *tokens, int n_tokens, float *logits) {
+    MIO_REQUIRE(m && tokens && n_tokens >= 1 && n_tokens <= m->dims.n_ctx, MIO_ERR_INVALID,
+                "llm_prefill: bad args");
+    for (int i = 0; i < n_tokens; ++i)
+        MIO_REQUIRE(tokens[i] >= 0 && tokens[i] < m->dims.n_vocab, MIO_ERR_INVALID, "llm_prefill: token %d",
+                    tokens[i]);
+    int rc = mio::bind(m->d);
+    if (rc) return rc;
+    if ((rc = upload_prompt(m, tokens, n_tokens)) || (rc = prefill(m, n_tokens - 1))) return rc;
+    return mio_hip_llm_eval(m, tokens[n_tokens - 1], n_tokens - 1, logits);
 }
 
 extern "C" int mio_hip_llm_logits(mio_hip_llm *m, float *logits) {

@@ -498,8 +498,7 @@ bool TestToSpeech::synthesize_stream_profiled(const VoiceModel &voice, const std
     sp.temperature = temp, sp.seed = 42, sp.eos0 = I.eos, sp.eos1 = I.im_end;
     I.harness(options, sp);
     const auto tl0 = clk::now();
-    if (mio::llm_begin(I.llm, prompt.data(), (int)prompt.size(), max_tokens, sp) ||
-        mio::llm_run(I.llm, (int)prompt.size() - 1)) {
+    if (mio::llm_begin(I.llm, prompt.data(), (int)prompt.size(), max_tokens, sp)) {
         fprintf(stderr, "TestToSpeech: initial decode failed: %s\n", mio::last_error());
         return false;
     }

@@ -99,6 +99,7 @@ def _declare(L: ctypes.CDLL) -> None:
         "mio_hip_llm_info": (c_int, [_vp, _i32p]),
         "mio_hip_llm_weight_bytes": (c_int, [_vp, ctypes.POINTER(ctypes.c_uint64)]),
         "mio_hip_llm_eval": (c_int, [_vp, ctypes.c_int32, c_int, _vp]),
+        "mio_hip_llm_prefill": (c_int, [_vp, _vp, c_int, _vp]),
         "mio_hip_llm_logits": (c_int, [_vp, _vp]),
         "mio_hip_llm_generate": (c_int, [_vp, _vp, c_int, c_int, ctypes.c_float, ctypes.c_uint64,
                                          ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
@@ -382,6 +383,14 @@ class Llm:
     def eval(self, token: int, pos: int) -> np.ndarray:
         out = np.empty(self.n_vocab, np.float32)
         check(lib().mio_hip_llm_eval(self.h, token, pos, _ptr(out)))
+        return out
+
+    def prefill(self, tokens) -> np.ndarray:
+        """Batched prefill of tokens[:-1] + one decode step of tokens[-1]: the last token's
+        logits (the reference's prompt llama_decode, test-to-speech.cpp:132-148)."""
+        t = np.ascontiguousarray(tokens, np.int32)
+        out = np.empty(self.n_vocab, np.float32)
+        check(lib().mio_hip_llm_prefill(self.h, _ptr(t), int(t.size), _ptr(out)))
         return out
 
     def logits(self) -> np.ndarray:

@@ -95,3 +95,45 @@ def test_logits_1p7b_q4km(device, tmp_path):
         d = lg.astype(np.float64) - lo
         assert np.sqrt(np.mean(d * d)) <= 0.1 * np.sqrt(np.mean(lo.astype(np.float64) ** 2))
         assert lg.argmax() == lo.argmax()
+
+
+# --- batched prompt prefill (csrc/hip/llm_prefill.hip; reference prefill llama_decode,
+# test-to-speech.cpp:132-148). The batched kernels run the decode step's arithmetic token by
+# token in the same order, so the last token's logits (and therefore the KV cache rows they
+# read) equal a token-by-token decode BIT FOR BIT; vs the oracle the teacher-forced bound
+# above applies.
+@pytest.mark.parametrize("preset,n", [(0, 2), (0, 17), (1, 40), (0, 150)])
+def test_batched_prefill_matches_sequential(device, llm_files, preset, n):
+    g = m.Llm(device, llm_files[preset], 256)
+    toks = np.random.default_rng(100 + n).integers(0, g.n_vocab, n)
+    batched = g.prefill(toks)
+    seq = None
+    for pos, t in enumerate(toks):
+        seq = g.eval(int(t), pos)
+    assert np.array_equal(batched, seq), float(np.abs(batched - seq).max())
+    o = pyoracle.Llm(llm_files[preset], 256)
+    for pos, t in enumerate(toks):
+        lo = o.eval(int(t), pos)
+    assert np.abs(batched - lo).max() <= 5e-2 * np.abs(lo).max()
+
+
+def test_batched_prefill_then_generate(device, llm_files):
+    """generate() prefills in batches; the sampled ids still follow the oracle's decode."""
+    g = m.Llm(device, llm_files[1], 256)
+    o = pyoracle.Llm(llm_files[1], 256)
+    prompt = list(range(256, 259)) + list(b"batched prefill of a longer prompt, 40 tokens") + [257]
+    allow = (m.SYNTH_SPEECH0, m.SYNTH_SPEECH0 + 12800)
+    tg = g.generate(prompt, 24, 0.8, 42, allow=allow)
+    to = o.generate(prompt, 24, 0.8, 42, allow=allow)
+    assert len(tg) == 24 and (tg == to).sum() >= 22
+
+
+def test_batched_prefill_1p7b_q4km(device, tmp_path):
+    """1.7B Q4_K_M, 68-token prompt (the bench prompt length: 5 chunks of 16, Q4_K + Q6_K)."""
+    path = m.synth_llm(str(tmp_path / "llm17.gguf"), 3, 1)
+    g = m.Llm(device, path, 256)
+    toks = np.random.default_rng(68).integers(0, 151936, 68)
+    batched = g.prefill(toks)
+    for pos, t in enumerate(toks):
+        seq = g.eval(int(t), pos)
+    assert np.array_equal(batched, seq), float(np.abs(batched - seq).max())
