@@ -26,17 +26,18 @@ namespace {
         }                                                                                     \
     } while (0)
 
-// Step timeline (diagnostic, mio_hip_llm_timeline): start / end of every workgroup of
-// each launch, s_memrealtime ticks (100 MHz), plain stores to slot [seq][wg] (wg < 256).
-#define MIO_TL_SLOT(bufs) ((bufs).tl + 2 * ((size_t)(bufs).seq * 256 + ((blockIdx.x + blockIdx.y * gridDim.x) & 255)))
-#define MIO_TL_BEGIN(bufs)                                                                      \
+// Step timeline (diagnostic, mio_hip_llm_timeline): per workgroup of each launch {start,
+// mark 1, mark 2, end}, s_memrealtime ticks (100 MHz), plain stores to slot [seq][wg][4]
+// (wg < 256). Marks: matvec kernels 1 = weight loads issued, 2 = activations quantized;
+// attention 1 = K/V loads issued, 2 = heads prepared; sampler 1 = token chosen.
+#define MIO_TL_SLOT(bufs) ((bufs).tl + 4 * ((size_t)(bufs).seq * 256 + ((blockIdx.x + blockIdx.y * gridDim.x) & 255)))
+#define MIO_TL_AT(bufs, k)                                                                      \
     do {                                                                                        \
-        if ((bufs).tl && threadIdx.x == 0) MIO_TL_SLOT(bufs)[0] = __builtin_amdgcn_s_memrealtime(); \
+        if ((bufs).tl && threadIdx.x == 0) MIO_TL_SLOT(bufs)[k] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
-#define MIO_TL_END(bufs)                                                                        \
-    do {                                                                                        \
-        if ((bufs).tl && threadIdx.x == 0) MIO_TL_SLOT(bufs)[1] = __builtin_amdgcn_s_memrealtime(); \
-    } while (0)
+#define MIO_TL_BEGIN(bufs) MIO_TL_AT(bufs, 0)
+#define MIO_TL_MARK(bufs, k) MIO_TL_AT(bufs, k)
+#define MIO_TL_END(bufs) MIO_TL_AT(bufs, 3)
 
 constexpr int NT = 256;        // threads of the attention / sampler kernels
 constexpr int NWAVE = NT / 64;
@@ -333,7 +334,8 @@ __device__ inline float wave_sum(float v) {
 constexpr uint32_t M4 = 0x0F0F0F0Fu, M2 = 0x03030303u;
 
 // One unit's weight registers.
-//   Q4_K: a = 16 B of nibbles, b = superblock header {d, dmin, 4 x 24-bit scale pairs}
+//   Q4_K: a = 16 B of nibbles, c = dword (lane & 3) of the superblock header {d, dmin,
+//         4 x 24-bit scale pairs}
 //   Q6_K: a = 16 B of ql, b = 16 B of qh, c = the lane's two int8 sub-block scales, e = d
 //   Q8_0: a, b = the lane's 32 codes, e = d
 struct Frag {
@@ -360,12 +362,21 @@ struct ALane {
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void *p, uint32_t bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), 0, (int)min(bytes, 0x7FFFFFF0u), 0x00020000);
 }
+// Cache policy of the weight stream (buffer-load aux bits; 2 = nt): weights are read once per
+// step by one CU, so they should not evict what the launch chain re-reads (kernel arguments,
+// activations, K/V rows) from L2 / Infinity Cache.
+#ifndef MIO_WEIGHT_AUX
+#define MIO_WEIGHT_AUX 2
+#endif
 __device__ __forceinline__ uint4 bld16(const uint8_t *base, uint32_t bytes, uint32_t voff, uint32_t soff) {
-    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rsrc(base, bytes), voff, soff, 0);
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rsrc(base, bytes), voff, soff, MIO_WEIGHT_AUX);
     return make_uint4(v.x, v.y, v.z, v.w);
 }
+__device__ __forceinline__ uint32_t bld4(const uint8_t *base, uint32_t bytes, uint32_t voff, uint32_t soff) {
+    return __builtin_amdgcn_raw_buffer_load_b32(rsrc(base, bytes), voff, soff, MIO_WEIGHT_AUX);
+}
 __device__ __forceinline__ uint32_t bld2(const uint8_t *base, uint32_t bytes, uint32_t voff, uint32_t soff) {
-    return __builtin_amdgcn_raw_buffer_load_b16(rsrc(base, bytes), voff, soff, 0);
+    return __builtin_amdgcn_raw_buffer_load_b16(rsrc(base, bytes), voff, soff, MIO_WEIGHT_AUX);
 }
 
 template <int T>
@@ -377,8 +388,11 @@ __device__ __forceinline__ Frag load_frag(const QMat W, int row, int pass) {
         const int nsb = W.k >> 8, sb = min(pass * 8 + (lane >> 3), nsb - 1), pc = lane & 7;
         const uint32_t qb = (uint32_t)(W.k / 2), hb = (uint32_t)nsb * 16;
         f.a = bld16(W.p0, R * qb, sb * 128 + pc * 16, r * qb);
-        f.b = bld16(W.p1, R * hb, sb * 16, r * hb);
-        f.c = f.e = 0;
+        // header dword (lane & 3) only: both quads of the superblock's 8 lanes hold all four,
+        // broadcast by DPP in dot_frag (a quarter of the load-return traffic of 16 B per lane)
+        f.c = bld4(W.p1, R * hb, sb * 16 + 4 * (pc & 3), r * hb);
+        f.b = make_uint4(0, 0, 0, 0);
+        f.e = 0;
     } else if constexpr (T == 14) {
         const int nsb = W.k >> 8, sb = min(pass * 8 + (lane >> 3), nsb - 1), pc = lane & 7;
         const uint32_t lb = (uint32_t)(W.k / 2), hb = (uint32_t)(W.k / 4), sbb = (uint32_t)(W.k / 16),
@@ -438,7 +452,11 @@ __device__ __forceinline__ float dot_frag(const Frag &f, const ALane &al, int K,
     const int lane = threadIdx.x & 63;
     if constexpr (T == 12) {
         const int jj = (lane & 7) >> 1;
-        const uint4 h = f.b;
+        uint4 h;  // the superblock header {d|dmin, scale/min words} from the quad's four dwords
+        h.x = (uint32_t)dpp_i<0x00>((int)f.c);
+        h.y = (uint32_t)dpp_i<0x55>((int)f.c);
+        h.z = (uint32_t)dpp_i<0xAA>((int)f.c);
+        h.w = (uint32_t)dpp_i<0xFF>((int)f.c);
         const uint32_t wlo = jj < 2 ? h.y : (jj == 2 ? h.z : h.w);
         const uint32_t whi = jj < 2 ? h.z : h.w;
         const uint32_t F = __builtin_amdgcn_alignbit(whi, wlo, (24 * jj) & 31);
@@ -506,10 +524,15 @@ __device__ __forceinline__ float row_total(float acc) {
 
 // ------------------------------------------------------------------ streaming rows
 // NP passes per row (1, 3 or 6); U units per register group; NP <= 3 keeps the lane's
-// activation slices in registers for the whole stream.
-template <int NP>
+// activation slices in registers for the whole stream. SU > 0: the wave's whole share (at
+// most SU units, host-checked) is ONE group of SU units, issued before the prologue - a
+// launch whose waves own only a row or two issues no duplicate (clamped) loads; every
+// vector memory instruction costs the CU's address path ~16 cycles however few bytes it
+// moves, and a launch's first loads are issued in one burst.
+template <int NP, int SU = 0>
 struct Cfg {
-    static constexpr int U = NP == 1 ? 4 : 3;
+    static constexpr int U = SU ? SU : (NP == 1 ? 4 : 3);
+    static constexpr int NG = SU ? 1 : 2;
     static constexpr bool AREG = NP <= 3;
 };
 
@@ -517,11 +540,11 @@ struct Cfg {
 // compiler's in-order vmcnt accounting stays exact). Unit u -> row lo + u/(NP*NM),
 // matrix (u/NP)%NM, pass u%NP. With NM == 1, rows >= split come from W1 (row - split):
 // two matrices of one type streamed as one row space (q|k).
-template <int T, int NP, int NM>
+template <int T, int NP, int NM, int SU = 0>
 __device__ __forceinline__ void load_group(const QMat W0, const QMat W1, int lo, int n, int u0,
-                                           Frag (&f)[Cfg<NP>::U], int split = INT_MAX) {
+                                           Frag (&f)[Cfg<NP, SU>::U], int split = INT_MAX) {
 #pragma unroll
-    for (int j = 0; j < Cfg<NP>::U; ++j) {
+    for (int j = 0; j < Cfg<NP, SU>::U; ++j) {
         const int u = max(0, min(u0 + j, n - 1));
         const int p = u % NP, m = (u / NP) % NM, i = u / (NP * NM);
         if constexpr (NM == 1) {
@@ -538,16 +561,16 @@ __device__ __forceinline__ void load_group(const QMat W0, const QMat W1, int lo,
 // the first two groups (units [0, U) and [U, 2U)), issued by the caller before its
 // prologue; groups then alternate between A and B, one group in flight while the other is
 // reduced (no register copies).
-template <int T, int NP, int NM, class Epi>
-__device__ __forceinline__ void stream_rows(const QMat W0, const QMat W1, int lo, int hi, Frag (&A)[Cfg<NP>::U],
-                                            Frag (&B)[Cfg<NP>::U], const ActL &a, Epi &&epi, int split = INT_MAX,
+template <int T, int NP, int NM, int SU = 0, class Epi>
+__device__ __forceinline__ void stream_rows(const QMat W0, const QMat W1, int lo, int hi, Frag (&A)[Cfg<NP, SU>::U],
+                                            Frag (&B)[Cfg<NP, SU>::U], const ActL &a, Epi &&epi, int split = INT_MAX,
                                             unsigned long long *trace = nullptr) {
-    constexpr int U = Cfg<NP>::U;
+    constexpr int U = Cfg<NP, SU>::U;
     const int K = W0.k;
     const int n = (hi - lo) * NM * NP;
     if (n <= 0) return;
-    ALane al[Cfg<NP>::AREG ? NP : 1];
-    if constexpr (Cfg<NP>::AREG) {
+    ALane al[Cfg<NP, SU>::AREG ? NP : 1];
+    if constexpr (Cfg<NP, SU>::AREG) {
 #pragma unroll
         for (int p = 0; p < NP; ++p) al[p] = load_alane<T>(a, K, p);
     }
@@ -589,23 +612,24 @@ __device__ __forceinline__ void stream_rows(const QMat W0, const QMat W1, int lo
     for (int u0 = 0;;) {
         consume(A, u0);
         if (trace && u0 == 0 && blockIdx.x == 0 && threadIdx.x == 0) trace[3] = __builtin_readcyclecounter();
+        if constexpr (Cfg<NP, SU>::NG == 1) break;
         u0 += U;
         if (u0 >= n) break;
-        load_group<T, NP, NM>(W0, W1, lo, n, u0 + U, A, split);
+        load_group<T, NP, NM, SU>(W0, W1, lo, n, u0 + U, A, split);
         consume(B, u0);
         u0 += U;
         if (u0 >= n) break;
-        load_group<T, NP, NM>(W0, W1, lo, n, u0 + U, B, split);
+        load_group<T, NP, NM, SU>(W0, W1, lo, n, u0 + U, B, split);
     }
 }
 
-// The first two groups of a wave's stream (before the prologue).
-template <int T, int NP, int NM>
-__device__ __forceinline__ void load_first(const QMat W0, const QMat W1, int lo, int hi, Frag (&A)[Cfg<NP>::U],
-                                           Frag (&B)[Cfg<NP>::U], int split = INT_MAX) {
+// The first group(s) of a wave's stream (before the prologue).
+template <int T, int NP, int NM, int SU = 0>
+__device__ __forceinline__ void load_first(const QMat W0, const QMat W1, int lo, int hi, Frag (&A)[Cfg<NP, SU>::U],
+                                           Frag (&B)[Cfg<NP, SU>::U], int split = INT_MAX) {
     const int n = (hi - lo) * NM * NP;
-    load_group<T, NP, NM>(W0, W1, lo, n, 0, A, split);
-    load_group<T, NP, NM>(W0, W1, lo, n, Cfg<NP>::U, B, split);
+    load_group<T, NP, NM, SU>(W0, W1, lo, n, 0, A, split);
+    if constexpr (Cfg<NP, SU>::NG == 2) load_group<T, NP, NM, SU>(W0, W1, lo, n, Cfg<NP, SU>::U, B, split);
 }
 
 // Rows [0, R) over G workgroups: workgroup b owns [R*b/G, R*(b+1)/G), wave w a contiguous
@@ -621,16 +645,16 @@ __device__ inline void wave_range(int R, int &lo, int &hi) { wave_range(R, lo, h
 // ------------------------------------------------------------------ cross-launch prefetch
 
 __device__ inline void prefetch_range(const uint8_t *base, uint32_t total, uint32_t off, uint32_t bytes,
-                                      char *slot) {
+                                      char *slot, int nw = MW) {
     const auto r = rsrc(base, total);
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    for (uint32_t c = w; c * 1024u < bytes; c += MW)
+    for (uint32_t c = w; c * 1024u < bytes; c += nw)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void *)slot, 16, lane * 16,
                                                  off + c * 1024u, 0, 0);
 }
 
 // all arrays of rows [r0, r1) of W
-__device__ inline void prefetch_rows(const QMat &W, int r0, int r1, uint32_t cap, char *slot) {
+__device__ inline void prefetch_rows(const QMat &W, int r0, int r1, uint32_t cap, char *slot, int nw = MW) {
     if (r1 <= r0) return;
     const uint32_t R = (uint32_t)W.rows, n = (uint32_t)(r1 - r0);
     uint32_t rb[4] = {0, 0, 0, 0};
@@ -644,7 +668,7 @@ __device__ inline void prefetch_rows(const QMat &W, int r0, int r1, uint32_t cap
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i)
-        if (rb[i]) prefetch_range(p[i], R * rb[i], (uint32_t)r0 * rb[i], min(n * rb[i], cap), slot);
+        if (rb[i]) prefetch_range(p[i], R * rb[i], (uint32_t)r0 * rb[i], min(n * rb[i], cap), slot, nw);
 }
 
 __device__ inline void prefetch_next(const Prefetch &pf, char *lds_slots) {
@@ -793,5 +817,213 @@ void dispatch_nt(int K, int type, F &&f) {
 #undef NT_CASE
 }
 
+
+// ------------------------------------------------------------------ attention chunk sweep
+// Shared by the decode step (k_attention) and the batched prefill (k_pf_attention), so the
+// two produce bit-identical partial records.
+constexpr int ATT_NT = 512;  // threads of an attention workgroup (2 waves per SIMD)
+constexpr int ATT_NW = ATT_NT / 64;
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+
+template <int HD>
+struct AttCfg {
+    static constexpr int LP = HD / 8;             // lanes per position slot (8 dims each)
+    static constexpr int NS = ATT_NT / LP;        // position slots per workgroup
+    static constexpr int IT = ATT_CHUNK / NS;     // positions per slot
+    static constexpr int REC = part_rec(HD);
+};
+
+// value of lane ^ O (O = 16 or 32 by the gfx950 permlane swaps, VALU; smaller O by bpermute)
+template <int O>
+__device__ __forceinline__ float xor_lane(float v) {
+    const int lane = threadIdx.x & 63;
+    if constexpr (O == 32) {
+        const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+        return __uint_as_float(lane < 32 ? r[1] : r[0]);
+    } else if constexpr (O == 16) {
+        const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+        return __uint_as_float(((lane >> 4) & 1) == 0 ? r[1] : r[0]);
+    } else {
+        return __shfl_xor(v, O);
+    }
+}
+
+// q/k head preparation by one wave (HD values at src): optional RMSNorm with weight nw
+// (qwen3 attn_q_norm / attn_k_norm), RoPE on (i, i + HD/2) pairs (NEOX) or (2i, 2i+1) (NORM)
+// with the ggml rope-cache cos/sin, f16 rounding (the F16 cache / ggml's f16 K operand).
+// row: wave-private LDS scratch [HD]; the prepared head is left in row.
+template <int HD>
+__device__ void prep_head(const float *src, const float *nw, const float2 *rope, const LlmDims &d, float *row) {
+    constexpr int PER = HD / 64;
+    const int lane = threadIdx.x & 63;
+    float v[PER], w[PER];
+    float2 cs[PER];
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+        const int p = lane + 64 * i;
+        v[i] = src[p];
+        w[i] = d.qk_norm ? nw[p] : 1.0f;
+        cs[i] = p < HD / 2 ? rope[p] : make_float2(0.0f, 0.0f);
+    }
+    if (d.qk_norm) {
+        double ss = 0.0;
+#pragma unroll
+        for (int i = 0; i < PER; ++i) ss += (double)(v[i] * v[i]);
+        ss = wave_sum_d(ss);
+        const float mean = (float)(ss / HD);
+        const float scale = 1.0f / sqrtf(mean + d.eps);
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const float t = v[i] * scale;
+            v[i] = t * w[i];
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < PER; ++i) row[lane + 64 * i] = v[i];
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    float o0[PER], o1[PER];
+    int i0s[PER], i1s[PER];
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+        const int p = lane + 64 * i;
+        i0s[i] = -1;
+        if (p < HD / 2) {
+            const int i0 = d.neox ? p : 2 * p, i1 = d.neox ? p + HD / 2 : 2 * p + 1;
+            const float x0 = row[i0], x1 = row[i1];
+            o0[i] = x0 * cs[i].x - x1 * cs[i].y;
+            o1[i] = x0 * cs[i].y + x1 * cs[i].x;
+            i0s[i] = i0, i1s[i] = i1;
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+#pragma unroll
+    for (int i = 0; i < PER; ++i)
+        if (i0s[i] >= 0) {
+            row[i0s[i]] = f16r(o0[i]);
+            row[i1s[i]] = f16r(o1[i]);
+        }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+}
+
+// K/V rows of this thread's slot (positions t0 + sl + NS*it, clamped to pos), issued early.
+template <int HD>
+__device__ __forceinline__ void load_kv_rows(const _Float16 *kbase, const _Float16 *vbase, int t0, int pos,
+                                             h8 (&kr)[AttCfg<HD>::IT], h8 (&vr)[AttCfg<HD>::IT]) {
+    constexpr int LP = AttCfg<HD>::LP, NS = AttCfg<HD>::NS;
+    const int lp = (threadIdx.x & 63) % LP, sl = threadIdx.x / LP;
+#pragma unroll
+    for (int it = 0; it < AttCfg<HD>::IT; ++it) {
+        const int t = min(t0 + sl + NS * it, pos);
+        kr[it] = *reinterpret_cast<const h8 *>(kbase + (size_t)t * HD + lp * 8);
+        vr[it] = *reinterpret_cast<const h8 *>(vbase + (size_t)t * HD + lp * 8);
+    }
+}
+
+// Online softmax of the G query heads qs (LDS, prepared) over the chunk's positions
+// [t0, min(t0 + ATT_CHUNK, pos + 1)) whose K/V rows are in kr/vr (ggml soft_max semantics up
+// to summation order), then the slots' merge: lanes (permlane / bpermute butterflies), waves
+// (LDS). Writes the chunk's partial record {O[HD], m, l} of head g to dst + g * g_stride.
+template <int HD, int G>
+__device__ void attend_chunk(const float (*qs)[HD], const h8 (&kr)[AttCfg<HD>::IT], const h8 (&vr)[AttCfg<HD>::IT],
+                             int t0, int pos, float scale, float (*wres)[G][HD + 2], float *dst, size_t g_stride,
+                             unsigned long long *trace = nullptr) {
+    // diagnostic checkpoints (mio_hip_llm_trace_kernel): 3 sweep done, 4 lane merge, 5 wave merge
+    auto mark = [&](int k) {
+        if (trace && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
+            asm volatile("" ::: "memory");
+            trace[k] = __builtin_readcyclecounter();
+        }
+    };
+    constexpr int LP = AttCfg<HD>::LP, NS = AttCfg<HD>::NS, IT = AttCfg<HD>::IT;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int lp = lane % LP, sl = tid / LP;
+    float qv[G][8];
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) qv[g][i] = qs[g][lp * 8 + i];
+    float m[G], l[G], acc[G][8];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        m[g] = -INFINITY, l[g] = 0.0f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[g][i] = 0.0f;
+    }
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+        const bool valid = t0 + sl + NS * it <= pos;
+        float kf[8], vf[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) kf[i] = (float)kr[it][i], vf[i] = (float)vr[it][i];
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            float sdot = 0.0f;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) sdot = fmaf(qv[g][i], kf[i], sdot);
+            sdot = group_sum<LP>(sdot);
+            const float sc = valid ? sdot * scale : -INFINITY;
+            const float mn = fmaxf(m[g], sc);
+            const float c = m[g] == mn ? 1.0f : expf(m[g] - mn);
+            const float p = valid ? expf(sc - mn) : 0.0f;
+            l[g] = l[g] * c + p;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) acc[g][i] = acc[g][i] * c + p * vf[i];
+            m[g] = mn;
+        }
+    }
+    mark(3);
+    // merge the wave's slots (lane stride LP): every lane of a butterfly pair ends bitwise equal
+    auto merge_step = [&](auto xl) {
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const float m2 = xl(m[g]), l2 = xl(l[g]);
+            const float mn = fmaxf(m[g], m2);
+            const float c1 = m[g] == -INFINITY ? 0.0f : expf(m[g] - mn);
+            const float c2 = m2 == -INFINITY ? 0.0f : expf(m2 - mn);
+            l[g] = l[g] * c1 + l2 * c2;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const float a2 = xl(acc[g][i]);
+                acc[g][i] = acc[g][i] * c1 + a2 * c2;
+            }
+            m[g] = mn;
+        }
+    };
+    if constexpr (LP <= 8) merge_step([](float v) { return xor_lane<8>(v); });
+    merge_step([](float v) { return xor_lane<16>(v); });
+    merge_step([](float v) { return xor_lane<32>(v); });
+    mark(4);
+    if (lane < LP) {
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) wres[wave][g][lp * 8 + i] = acc[g][i];
+            if (lp == 0) wres[wave][g][HD] = m[g], wres[wave][g][HD + 1] = l[g];
+        }
+    }
+    __syncthreads();
+    mark(5);
+    // merge the waves -> this chunk's partial record per q head
+    for (int e = tid; e < G * HD; e += ATT_NT) {
+        const int g = e / HD, dd = e - g * HD;
+        float M = -INFINITY;
+#pragma unroll
+        for (int w = 0; w < ATT_NW; ++w) M = fmaxf(M, wres[w][g][HD]);
+        float L = 0.0f, O = 0.0f;
+#pragma unroll
+        for (int w = 0; w < ATT_NW; ++w) {
+            const float mw = wres[w][g][HD];
+            const float c = mw == -INFINITY ? 0.0f : expf(mw - M);
+            L += c * wres[w][g][HD + 1];
+            O += c * wres[w][g][dd];
+        }
+        float *o = dst + g * g_stride;
+        o[dd] = O;
+        if (dd == 0) o[HD] = M, o[HD + 1] = L;
+    }
+}
 }  // namespace
 }  // namespace mio

@@ -29,6 +29,8 @@
 // csrc/host/quant.h).
 #include "llm_device.h"
 
+#include <algorithm>
+
 #pragma clang fp contract(off)
 
 namespace mio {
@@ -40,7 +42,7 @@ namespace {
 // straight-line code with no run-time type dispatch.
 // q|k rows (type TQ) on the first g_qk workgroups, v rows (type TV) on the rest; each
 // branch is WG-uniform and runs its own prologue, so neither path merges load counts.
-template <int NP, int TQ, int TV>
+template <int NP, int TQ, int TV, int SU>
 __global__ __launch_bounds__(MT) void k_attn_in(LlmDims d, const float *norm_w, QMat wq, QMat wk, QMat wv,
                                                 int g_qk, Prefetch pf, LlmBuffers b) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -52,26 +54,28 @@ __global__ __launch_bounds__(MT) void k_attn_in(LlmDims d, const float *norm_w, 
     XRegs<NP> xr;
     load_x(b.x, norm_w, K, xr);
     const int o1 = wq.rows, o2 = wq.rows + wk.rows;
-    Frag ga[Cfg<NP>::U], gb[Cfg<NP>::U];
+    Frag ga[Cfg<NP, SU>::U], gb[Cfg<NP, SU>::U];
     int lo, hi;
     if ((int)blockIdx.x < g_qk) {
         wave_range(o2, lo, hi, blockIdx.x, g_qk);
-        load_first<TQ, NP, 1>(wq, wk, lo, hi, ga, gb, o1);
+        load_first<TQ, NP, 1, SU>(wq, wk, lo, hi, ga, gb, o1);
         prefetch_next(pf, pf_lds);
         MIO_TRACE(b, 1);
+    MIO_TL_MARK(b, 1);
         rmsnorm_quant(xr, K, d.eps, TQ != 8, s);
         MIO_TRACE(b, 2);
-        stream_rows<TQ, NP, 1>(wq, wk, lo, hi, ga, gb, s.a, [&](int row, float v, float) {
+    MIO_TL_MARK(b, 2);
+        stream_rows<TQ, NP, 1, SU>(wq, wk, lo, hi, ga, gb, s.a, [&](int row, float v, float) {
             if ((threadIdx.x & 63) == 0) b.qkv[row] = v;
         }, o1);
         MIO_TL_END(b);
     MIO_TRACE(b, 15);
     } else {
         wave_range(wv.rows, lo, hi, blockIdx.x - g_qk, gridDim.x - g_qk);
-        load_first<TV, NP, 1>(wv, wv, lo, hi, ga, gb);
+        load_first<TV, NP, 1, SU>(wv, wv, lo, hi, ga, gb);
         prefetch_next(pf, pf_lds);
         rmsnorm_quant(xr, K, d.eps, TQ != 8, s);
-        stream_rows<TV, NP, 1>(wv, wv, lo, hi, ga, gb, s.a, [&](int row, float v, float) {
+        stream_rows<TV, NP, 1, SU>(wv, wv, lo, hi, ga, gb, s.a, [&](int row, float v, float) {
             if ((threadIdx.x & 63) == 0) b.qkv[o2 + row] = v;
         });
         MIO_TL_END(b);
@@ -87,7 +91,7 @@ __device__ inline float lane_value(float v, int i) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), i));
 }
 
-template <int NP, int T>
+template <int NP, int T, int SU>
 __global__ __launch_bounds__(MT) void k_attn_out(LlmDims d, QMat wo, Prefetch pf, LlmBuffers b) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     MIO_TRACE(b, 0);
@@ -97,13 +101,15 @@ __global__ __launch_bounds__(MT) void k_attn_out(LlmDims d, QMat wo, Prefetch pf
     int lo, hi;
     wave_range(wo.rows, lo, hi);
     const float xres = load_resid(b.x, lo, hi);
-    Frag ga[Cfg<NP>::U], gb[Cfg<NP>::U];
-    load_first<T, NP, 1>(wo, wo, lo, hi, ga, gb);
+    Frag ga[Cfg<NP, SU>::U], gb[Cfg<NP, SU>::U];
+    load_first<T, NP, 1, SU>(wo, wo, lo, hi, ga, gb);
     prefetch_next(pf, smem + pf_offset(smem_bytes(K)));
     MIO_TRACE(b, 1);
+    MIO_TL_MARK(b, 1);
     merge_attention<NP>(d, b.part, b.st->pos / ATT_CHUNK + 1, K, T != 8, s);
     MIO_TRACE(b, 2);
-    stream_rows<T, NP, 1>(wo, wo, lo, hi, ga, gb, s.a, [&](int row, float v, float) {
+    MIO_TL_MARK(b, 2);
+    stream_rows<T, NP, 1, SU>(wo, wo, lo, hi, ga, gb, s.a, [&](int row, float v, float) {
         const float r = lane_value(xres, row - lo);
         if ((threadIdx.x & 63) == 0) b.x[row] = v + r;
     });
@@ -111,7 +117,7 @@ __global__ __launch_bounds__(MT) void k_attn_out(LlmDims d, QMat wo, Prefetch pf
     MIO_TRACE(b, 15);
 }
 
-template <int NP, int T>
+template <int NP, int T, int SU>
 __global__ __launch_bounds__(MT) void k_ffn_in(LlmDims d, const float *norm_w, QMat gate, QMat up, Prefetch pf,
                                                LlmBuffers b) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -123,20 +129,22 @@ __global__ __launch_bounds__(MT) void k_ffn_in(LlmDims d, const float *norm_w, Q
     load_x(b.x, norm_w, K, xr);
     int lo, hi;
     wave_range(gate.rows, lo, hi);
-    Frag ga[Cfg<NP>::U], gb[Cfg<NP>::U];
-    load_first<T, NP, 2>(gate, up, lo, hi, ga, gb);
+    Frag ga[Cfg<NP, SU>::U], gb[Cfg<NP, SU>::U];
+    load_first<T, NP, 2, SU>(gate, up, lo, hi, ga, gb);
     prefetch_next(pf, smem + pf_offset(smem_bytes(K)));
     MIO_TRACE(b, 1);
+    MIO_TL_MARK(b, 1);
     rmsnorm_quant(xr, K, d.eps, T != 8, s);
     MIO_TRACE(b, 2);
-    stream_rows<T, NP, 2>(gate, up, lo, hi, ga, gb, s.a, [&](int row, float g, float u) {
+    MIO_TL_MARK(b, 2);
+    stream_rows<T, NP, 2, SU>(gate, up, lo, hi, ga, gb, s.a, [&](int row, float g, float u) {
         if ((threadIdx.x & 63) == 0) b.h[row] = silu_f(g) * u;
     }, INT_MAX, b.trace);
     MIO_TL_END(b);
     MIO_TRACE(b, 15);
 }
 
-template <int NP, int T>
+template <int NP, int T, int SU>
 __global__ __launch_bounds__(MT) void k_ffn_down(LlmDims d, QMat down, Prefetch pf, LlmBuffers b) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     MIO_TRACE(b, 0);
@@ -148,13 +156,15 @@ __global__ __launch_bounds__(MT) void k_ffn_down(LlmDims d, QMat down, Prefetch 
     int lo, hi;
     wave_range(down.rows, lo, hi);
     const float xres = load_resid(b.x, lo, hi);
-    Frag ga[Cfg<NP>::U], gb[Cfg<NP>::U];
-    load_first<T, NP, 1>(down, down, lo, hi, ga, gb);
+    Frag ga[Cfg<NP, SU>::U], gb[Cfg<NP, SU>::U];
+    load_first<T, NP, 1, SU>(down, down, lo, hi, ga, gb);
     prefetch_next(pf, smem + pf_offset(smem_bytes(K)));
     MIO_TRACE(b, 1);
+    MIO_TL_MARK(b, 1);
     plain_quant(xr, K, T != 8, s);
     MIO_TRACE(b, 2);
-    stream_rows<T, NP, 1>(down, down, lo, hi, ga, gb, s.a, [&](int row, float v, float) {
+    MIO_TL_MARK(b, 2);
+    stream_rows<T, NP, 1, SU>(down, down, lo, hi, ga, gb, s.a, [&](int row, float v, float) {
         const float r = lane_value(xres, row - lo);
         if ((threadIdx.x & 63) == 0) b.x[row] = v + r;
     }, INT_MAX, b.trace);
@@ -198,8 +208,10 @@ __global__ __launch_bounds__(MT) void k_lm_head(LlmDims d, const float *norm_w, 
     load_first<T, NP, 1>(lm, lm, lo, hi, ga, gb);
     prefetch_next(pf, smem + pf_offset(smem_bytes(K)));
     MIO_TRACE(b, 1);
+    MIO_TL_MARK(b, 1);
     rmsnorm_quant(xr, K, d.eps, T != 8, s);
     MIO_TRACE(b, 2);
+    MIO_TL_MARK(b, 2);
     const int lane = threadIdx.x & 63;
     float r0 = -INFINITY, r1 = -INFINITY;
     stream_rows<T, NP, 1>(lm, lm, lo, hi, ga, gb, s.a, [&](int row, float v, float) {
@@ -249,99 +261,54 @@ __global__ __launch_bounds__(MT) void k_lm_head(LlmDims d, const float *norm_w, 
 // partial record {O[HD], m, l} per q head is merged with the other chunks' in the prologue
 // of k_attn_out (the launch-boundary reduce: no extra launch, no in-kernel hand-off).
 template <int HD, int G>
-__global__ __launch_bounds__(NT) void k_attention(LlmDims d, const float *q_norm, const float *k_norm,
-                                                  _Float16 *kc, _Float16 *vc, LlmBuffers b) {
-    constexpr int LP = HD / 8;
-    constexpr int NS = NT / LP;
-    constexpr int IT = ATT_CHUNK / NS;
-    constexpr int REC = part_rec(HD);
+__global__ __launch_bounds__(ATT_NT) void k_attention(LlmDims d, const float *q_norm, const float *k_norm,
+                                                      _Float16 *kc, _Float16 *vc, Prefetch pf, LlmBuffers b) {
+    using C = AttCfg<HD>;
     constexpr int PER = HD / 64;
-    typedef _Float16 h8 __attribute__((ext_vector_type(8)));
     __shared__ float qs[G][HD];
     __shared__ float knew[HD], vnew[HD];
-    __shared__ float wres[NWAVE][G][HD + 2];
+    __shared__ float wres[ATT_NW][G][HD + 2];
 
     MIO_TRACE(b, 0);
     MIO_TL_BEGIN(b);
     const int kvh = blockIdx.y, ch = blockIdx.x;
+    if (ch >= d.max_splits) {
+        // prefetch workgroups (pf.mode 4): this launch leaves HBM idle, so they sweep slice
+        // i of the next launches' matrices (m[0..2]) into the caches; data is discarded
+        __shared__ __attribute__((aligned(16))) char pf_slot[ATT_NW * PF_SLOT];
+        const int P = (gridDim.x - d.max_splits) * gridDim.y, i = (ch - d.max_splits) * gridDim.y + kvh;
+        char *slot = pf_slot + PF_SLOT * __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const int R = pf.m[k].rows;
+            if (R > 0) prefetch_rows(pf.m[k], (R * i) / P, (R * (i + 1)) / P, pf.cap, slot, ATT_NW);
+        }
+        __builtin_amdgcn_s_waitcnt(0);
+        return;
+    }
     const int pos = b.st->pos;
     const int t0 = ch * ATT_CHUNK;
     if (t0 > pos) return;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int lp = lane % LP, sl = tid / LP;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const float2 *rope = b.rope + (size_t)pos * (HD / 2);
-    const _Float16 *kbase = kc + (size_t)kvh * d.n_ctx * HD;
-    const _Float16 *vbase = vc + (size_t)kvh * d.n_ctx * HD;
-
     // K/V rows of this slot first (row `pos` is never consumed from the cache)
-    h8 kr[IT], vr[IT];
-#pragma unroll
-    for (int it = 0; it < IT; ++it) {
-        const int t = min(t0 + sl + NS * it, pos);
-        kr[it] = *reinterpret_cast<const h8 *>(kbase + (size_t)t * HD + lp * 8);
-        vr[it] = *reinterpret_cast<const h8 *>(vbase + (size_t)t * HD + lp * 8);
-    }
-    // q heads (waves 0..G-1, strided) and, for the chunk owning `pos`, the new k/v row
+    h8 kr[C::IT], vr[C::IT];
+    load_kv_rows<HD>(kc + (size_t)kvh * d.n_ctx * HD, vc + (size_t)kvh * d.n_ctx * HD, t0, pos, kr, vr);
+    MIO_TRACE(b, 1);
+    MIO_TL_MARK(b, 1);
+    // q heads (waves 0..G-1) and, for the chunk owning `pos`, the new k/v row
     const bool owner = pos < t0 + ATT_CHUNK;
-    for (int hh = wave; hh < G + (owner ? 1 : 0); hh += NWAVE) {
+    for (int hh = wave; hh < G + (owner ? 1 : 0); hh += ATT_NW) {
         const bool isk = hh == G;
-        const float *src = isk ? b.qkv + (size_t)(d.n_head + kvh) * HD : b.qkv + (size_t)(kvh * G + hh) * HD;
-        const float *vsrc = b.qkv + (size_t)(d.n_head + d.n_kv + kvh) * HD;
-        const float *nw = isk ? k_norm : q_norm;
-        float v[PER], w[PER], vv[PER];
-        float2 cs[PER];
-#pragma unroll
-        for (int i = 0; i < PER; ++i) {
-            const int p = lane + 64 * i;
-            v[i] = src[p];
-            w[i] = d.qk_norm ? nw[p] : 1.0f;
-            vv[i] = isk ? vsrc[p] : 0.0f;
-            cs[i] = p < HD / 2 ? rope[p] : make_float2(0.0f, 0.0f);
-        }
-        if (d.qk_norm) {
-            double ss = 0.0;
-#pragma unroll
-            for (int i = 0; i < PER; ++i) ss += (double)(v[i] * v[i]);
-#pragma unroll
-            for (int o = 32; o >= 1; o >>= 1) ss += __shfl_xor(ss, o);
-            const float mean = (float)(ss / HD);
-            const float scale = 1.0f / sqrtf(mean + d.eps);
-#pragma unroll
-            for (int i = 0; i < PER; ++i) {
-                const float t = v[i] * scale;
-                v[i] = t * w[i];
-            }
-        }
-        float *dst = isk ? knew : qs[hh];
-#pragma unroll
-        for (int i = 0; i < PER; ++i) dst[lane + 64 * i] = v[i];
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        float o0[PER], o1[PER];
-        int i0s[PER], i1s[PER];
-#pragma unroll
-        for (int i = 0; i < PER; ++i) {
-            const int p = lane + 64 * i;
-            i0s[i] = -1;
-            if (p < HD / 2) {
-                const int i0 = d.neox ? p : 2 * p, i1 = d.neox ? p + HD / 2 : 2 * p + 1;
-                const float x0 = dst[i0], x1 = dst[i1];
-                o0[i] = x0 * cs[i].x - x1 * cs[i].y;
-                o1[i] = x0 * cs[i].y + x1 * cs[i].x;
-                i0s[i] = i0, i1s[i] = i1;
-            }
-        }
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-#pragma unroll
-        for (int i = 0; i < PER; ++i)
-            if (i0s[i] >= 0) {
-                dst[i0s[i]] = f16r(o0[i]);
-                dst[i1s[i]] = f16r(o1[i]);
-            }
+        float vv[PER];
         if (isk) {
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            const float *vsrc = b.qkv + (size_t)(d.n_head + d.n_kv + kvh) * HD;
+#pragma unroll
+            for (int i = 0; i < PER; ++i) vv[i] = vsrc[lane + 64 * i];
+        }
+        const float *src = isk ? b.qkv + (size_t)(d.n_head + kvh) * HD : b.qkv + (size_t)(kvh * G + hh) * HD;
+        prep_head<HD>(src, isk ? k_norm : q_norm, rope, d, isk ? knew : qs[hh]);
+        if (isk) {
             _Float16 *kd = kc + ((size_t)kvh * d.n_ctx + pos) * HD;
             _Float16 *vd = vc + ((size_t)kvh * d.n_ctx + pos) * HD;
 #pragma unroll
@@ -356,110 +323,35 @@ __global__ __launch_bounds__(NT) void k_attention(LlmDims d, const float *q_norm
     }
     __syncthreads();
     MIO_TRACE(b, 2);
-
-    float qv[G][8];
+    MIO_TL_MARK(b, 2);
+    // the slot owning row `pos` takes it from LDS (exact f16 values, the cache row's bits)
+    if (owner) {
+        const int sl = threadIdx.x / C::LP, lp = lane % C::LP, r = pos - t0;
+        if (sl == r % C::NS) {
+            h8 kn, vn;
 #pragma unroll
-    for (int g = 0; g < G; ++g)
+            for (int i = 0; i < 8; ++i) kn[i] = (_Float16)knew[lp * 8 + i], vn[i] = (_Float16)vnew[lp * 8 + i];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) qv[g][i] = qs[g][lp * 8 + i];
-    float m[G], l[G], acc[G][8];
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-        m[g] = -INFINITY, l[g] = 0.0f;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) acc[g][i] = 0.0f;
-    }
-    // online softmax over this slot's positions (ggml soft_max semantics up to order)
-    auto update = [&](const float (&kf)[8], const float (&vf)[8], bool valid) {
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-            float sdot = 0.0f;
-#pragma unroll
-            for (int i = 0; i < 8; ++i) sdot = fmaf(qv[g][i], kf[i], sdot);
-            sdot = group_sum<LP>(sdot);
-            const float sc = valid ? sdot * d.scale : -INFINITY;
-            const float mn = fmaxf(m[g], sc);
-            const float c = m[g] == mn ? 1.0f : expf(m[g] - mn);
-            const float p = valid ? expf(sc - mn) : 0.0f;
-            l[g] = l[g] * c + p;
-#pragma unroll
-            for (int i = 0; i < 8; ++i) acc[g][i] = acc[g][i] * c + p * vf[i];
-            m[g] = mn;
-        }
-    };
-#pragma unroll
-    for (int it = 0; it < IT; ++it) {
-        const int t = t0 + sl + NS * it;
-        float kf[8], vf[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) kf[i] = (float)kr[it][i], vf[i] = (float)vr[it][i];
-        update(kf, vf, t < pos);
-    }
-    if (owner && sl == (pos - t0) % NS) {
-        float kf[8], vf[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) kf[i] = knew[lp * 8 + i], vf[i] = vnew[lp * 8 + i];
-        update(kf, vf, true);
-    }
-    MIO_TRACE(b, 3);
-    // merge the wave's slots (lane stride LP)
-#pragma unroll
-    for (int o = LP; o < 64; o <<= 1) {
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-            const float m2 = __shfl_xor(m[g], o), l2 = __shfl_xor(l[g], o);
-            const float mn = fmaxf(m[g], m2);
-            const float c1 = m[g] == -INFINITY ? 0.0f : expf(m[g] - mn);
-            const float c2 = m2 == -INFINITY ? 0.0f : expf(m2 - mn);
-            l[g] = l[g] * c1 + l2 * c2;
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                const float a2 = __shfl_xor(acc[g][i], o);
-                acc[g][i] = acc[g][i] * c1 + a2 * c2;
-            }
-            m[g] = mn;
+            for (int it = 0; it < C::IT; ++it)
+                if (it == r / C::NS) kr[it] = kn, vr[it] = vn;
         }
     }
-    if (lane < LP) {
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-#pragma unroll
-            for (int i = 0; i < 8; ++i) wres[wave][g][lp * 8 + i] = acc[g][i];
-            if (lp == 0) wres[wave][g][HD] = m[g], wres[wave][g][HD + 1] = l[g];
-        }
-    }
-    __syncthreads();
-    // merge the 4 waves -> this chunk's partial record per q head
-    for (int e = tid; e < G * HD; e += NT) {
-        const int g = e / HD, dd = e - g * HD;
-        float M = -INFINITY;
-#pragma unroll
-        for (int w = 0; w < NWAVE; ++w) M = fmaxf(M, wres[w][g][HD]);
-        float L = 0.0f, O = 0.0f;
-#pragma unroll
-        for (int w = 0; w < NWAVE; ++w) {
-            const float mw = wres[w][g][HD];
-            const float c = mw == -INFINITY ? 0.0f : expf(mw - M);
-            L += c * wres[w][g][HD + 1];
-            O += c * wres[w][g][dd];
-        }
-        float *dst = b.part + ((size_t)(kvh * G + g) * d.max_splits + ch) * REC;
-        dst[dd] = O;
-        if (dd == 0) dst[HD] = M, dst[HD + 1] = L;
-    }
+    attend_chunk<HD, G>(qs, kr, vr, t0, pos, d.scale, wres,
+                        b.part + ((size_t)(kvh * G) * d.max_splits + ch) * C::REC, (size_t)d.max_splits * C::REC,
+                        b.trace);
     MIO_TL_END(b);
     MIO_TRACE(b, 15);
 }
 
 template <int HD>
 void launch_attention(int G, dim3 grid, hipStream_t s, const LlmDims &d, const float *qn, const float *kn,
-                      _Float16 *kc, _Float16 *vc, const LlmBuffers &b) {
+                      _Float16 *kc, _Float16 *vc, const Prefetch &pf, const LlmBuffers &b) {
     switch (G) {
-        case 1: hipLaunchKernelGGL((k_attention<HD, 1>), grid, dim3(NT), 0, s, d, qn, kn, kc, vc, b); break;
-        case 2: hipLaunchKernelGGL((k_attention<HD, 2>), grid, dim3(NT), 0, s, d, qn, kn, kc, vc, b); break;
-        case 3: hipLaunchKernelGGL((k_attention<HD, 3>), grid, dim3(NT), 0, s, d, qn, kn, kc, vc, b); break;
-        case 4: hipLaunchKernelGGL((k_attention<HD, 4>), grid, dim3(NT), 0, s, d, qn, kn, kc, vc, b); break;
-        case 8: hipLaunchKernelGGL((k_attention<HD, 8>), grid, dim3(NT), 0, s, d, qn, kn, kc, vc, b); break;
+        case 1: hipLaunchKernelGGL((k_attention<HD, 1>), grid, dim3(ATT_NT), 0, s, d, qn, kn, kc, vc, pf, b); break;
+        case 2: hipLaunchKernelGGL((k_attention<HD, 2>), grid, dim3(ATT_NT), 0, s, d, qn, kn, kc, vc, pf, b); break;
+        case 3: hipLaunchKernelGGL((k_attention<HD, 3>), grid, dim3(ATT_NT), 0, s, d, qn, kn, kc, vc, pf, b); break;
+        case 4: hipLaunchKernelGGL((k_attention<HD, 4>), grid, dim3(ATT_NT), 0, s, d, qn, kn, kc, vc, pf, b); break;
+        case 8: hipLaunchKernelGGL((k_attention<HD, 8>), grid, dim3(ATT_NT), 0, s, d, qn, kn, kc, vc, pf, b); break;
         default: break;
     }
 }
@@ -500,6 +392,7 @@ __global__ __launch_bounds__(ST) void k_sample(LlmDims d, QMat emb, int nblk, Ll
     __syncthreads();
     const int tok = tok_s;
     MIO_TRACE(b, 1);
+    MIO_TL_MARK(b, 1);
     embed_row(emb, tok, d.n_embd, b.x);
     MIO_TL_END(b);
     MIO_TRACE(b, 15);
@@ -567,6 +460,34 @@ Prefetch prefetch_plan(int which, const LlmDims &d, const LayerW *layers, int il
     return p;
 }
 
+// Units (row passes) of the busiest wave of a matvec over `rows` rows on `grid` workgroups
+// (wave_range), and the single-group size that covers them (0 = streaming groups).
+int max_wave_units(int rows, int grid, int np, int nm) {
+    const int rg = (rows + grid - 1) / grid, rw = (rg + MW - 1) / MW;
+    return rw * np * nm;
+}
+int pick_su(int units, int np) {
+    if (np == 1 && units <= 4) return units;
+    if (np == 1 && units <= 6) return 6;
+    if (np == 3 && units <= 3) return 3;
+    return 0;
+}
+// Calls f.template operator()<SU>() for the instantiated single-group sizes of NP.
+template <int NP, class F>
+void dispatch_su(int su, F &&f) {
+    if constexpr (NP == 1) {
+        if (su == 1) return f.template operator()<1>();
+        if (su == 2) return f.template operator()<2>();
+        if (su == 3) return f.template operator()<3>();
+        if (su == 4) return f.template operator()<4>();
+        if (su == 6) return f.template operator()<6>();
+    }
+    if constexpr (NP == 3) {
+        if (su == 3) return f.template operator()<3>();
+    }
+    f.template operator()<0>();
+}
+
 // Launch one kernel of the step: which = 0 attn_in, 1 attention, 2 attn_out (+ chunk
 // merge), 3 ffn_in, 4 ffn_down (layer il), 5 (unused: the final norm is fused into
 // lm_head), 6 lm_head, 7 sample.
@@ -582,10 +503,15 @@ void launch_step_kernel(int which, const LlmDims &d, const LayerW *layers, int i
             int GW, g_qk;
             attn_in_grid(d, L, GW, g_qk);
             const size_t lds = mv_lds(d.n_embd);
+            const int np = pick_np(d.n_embd);
+            const int un = std::max(max_wave_units(L.wq.rows + L.wk.rows, g_qk, np, 1),
+                                    max_wave_units(L.wv.rows, GW - g_qk, np, 1));
             dispatch_nt(d.n_embd, L.wq.type, [&]<int NP, int TQ>() {
                 auto go = [&]<int TV>() {
-                    hipLaunchKernelGGL((k_attn_in<NP, TQ, TV>), dim3(GW), dim3(MT), lds, s, d, L.attn_norm, L.wq, L.wk,
-                                       L.wv, g_qk, pf, b);
+                    dispatch_su<NP>(pick_su(un, NP), [&]<int SU>() {
+                        hipLaunchKernelGGL((k_attn_in<NP, TQ, TV, SU>), dim3(GW), dim3(MT), lds, s, d, L.attn_norm,
+                                           L.wq, L.wk, L.wv, g_qk, pf, b);
+                    });
                 };
                 if constexpr (TQ == 8) {
                     go.template operator()<8>();
@@ -600,34 +526,51 @@ void launch_step_kernel(int which, const LlmDims &d, const LayerW *layers, int i
         }
         case 1: {
             const LayerW &L = layers[il];
-            const dim3 grid(d.max_splits, d.n_kv);
+            // attention prefetch (d.att_prefetch): kAttPrefetchCols extra grid columns of
+            // workgroups sweep Wo, gate and up of this layer into the caches
+            Prefetch ap{};
+            if (d.att_prefetch) {
+                ap.mode = 4, ap.cap = 0xFFFFFFFFu;
+                ap.m[0] = L.wo, ap.m[1] = L.gate, ap.m[2] = L.up;
+            }
+            const dim3 grid(d.max_splits + (d.att_prefetch ? d.att_prefetch : 0), d.n_kv);
             if (d.hd == 128)
-                launch_attention<128>(G, grid, s, d, L.q_norm, L.k_norm, kcache + il * layer_kv, vcache + il * layer_kv, b);
+                launch_attention<128>(G, grid, s, d, L.q_norm, L.k_norm, kcache + il * layer_kv, vcache + il * layer_kv,
+                                      ap, b);
             else
-                launch_attention<64>(G, grid, s, d, L.q_norm, L.k_norm, kcache + il * layer_kv, vcache + il * layer_kv, b);
+                launch_attention<64>(G, grid, s, d, L.q_norm, L.k_norm, kcache + il * layer_kv, vcache + il * layer_kv,
+                                     ap, b);
             break;
         }
         case 2: {
             const LayerW &L = layers[il];
+            const int grid = matvec_grid(d, L.wo.rows);
             dispatch_nt(L.wo.k, L.wo.type, [&]<int NP, int T>() {
-                hipLaunchKernelGGL((k_attn_out<NP, T>), dim3(matvec_grid(d, L.wo.rows)), dim3(MT), mv_lds(L.wo.k), s, d,
-                                   L.wo, pf, b);
+                dispatch_su<NP>(pick_su(max_wave_units(L.wo.rows, grid, NP, 1), NP), [&]<int SU>() {
+                    hipLaunchKernelGGL((k_attn_out<NP, T, SU>), dim3(grid), dim3(MT), mv_lds(L.wo.k), s, d, L.wo, pf, b);
+                });
             });
             break;
         }
         case 3: {
             const LayerW &L = layers[il];
+            const int grid = matvec_grid(d, L.gate.rows);
             dispatch_nt(d.n_embd, L.gate.type, [&]<int NP, int T>() {
-                hipLaunchKernelGGL((k_ffn_in<NP, T>), dim3(matvec_grid(d, L.gate.rows)), dim3(MT), mv_lds(d.n_embd), s,
-                                   d, L.ffn_norm, L.gate, L.up, pf, b);
+                dispatch_su<NP>(pick_su(max_wave_units(L.gate.rows, grid, NP, 2), NP), [&]<int SU>() {
+                    hipLaunchKernelGGL((k_ffn_in<NP, T, SU>), dim3(grid), dim3(MT), mv_lds(d.n_embd), s, d, L.ffn_norm,
+                                       L.gate, L.up, pf, b);
+                });
             });
             break;
         }
         case 4: {
             const LayerW &L = layers[il];
+            const int grid = matvec_grid(d, L.down.rows);
             dispatch_nt(L.down.k, L.down.type, [&]<int NP, int T>() {
-                hipLaunchKernelGGL((k_ffn_down<NP, T>), dim3(matvec_grid(d, L.down.rows)), dim3(MT), mv_lds(L.down.k),
-                                   s, d, L.down, pf, b);
+                dispatch_su<NP>(pick_su(max_wave_units(L.down.rows, grid, NP, 1), NP), [&]<int SU>() {
+                    hipLaunchKernelGGL((k_ffn_down<NP, T, SU>), dim3(grid), dim3(MT), mv_lds(L.down.k), s, d, L.down,
+                                       pf, b);
+                });
             });
             break;
         }

@@ -194,8 +194,8 @@ __global__ __launch_bounds__(MT) void k_pf_attn_in(LlmDims d, const float *norm_
 }
 
 // One wave per (head, token): q heads are normalized / rotated / f16-rounded in place, k
-// heads likewise and written with the v row to the F16 cache at the token's position.
-// Same arithmetic as k_attention's head preparation.
+// heads likewise and written with the v row to the F16 cache at the token's position
+// (prep_head: the decode step's head preparation).
 template <int HD>
 __global__ __launch_bounds__(64) void k_pf_rope(LlmDims d, const float *q_norm, const float *k_norm, _Float16 *kc,
                                                 _Float16 *vc, PrefillBuffers pb, int p0) {
@@ -206,58 +206,13 @@ __global__ __launch_bounds__(64) void k_pf_rope(LlmDims d, const float *q_norm, 
     const bool isk = hh >= d.n_head;
     const int kvh = hh - d.n_head;
     float *src = pb.qkv + (size_t)t * QD + (size_t)hh * HD;
-    const float *vsrc = pb.qkv + (size_t)t * QD + (size_t)(d.n_head + d.n_kv + (isk ? kvh : 0)) * HD;
-    const float2 *rope = pb.rope + (size_t)pos * (HD / 2);
-    const float *nw = isk ? k_norm : q_norm;
-    float v[PER], w[PER], vv[PER];
-    float2 cs[PER];
+    float vv[PER];
+    if (isk) {
+        const float *vsrc = pb.qkv + (size_t)t * QD + (size_t)(d.n_head + d.n_kv + kvh) * HD;
 #pragma unroll
-    for (int i = 0; i < PER; ++i) {
-        const int p = lane + 64 * i;
-        v[i] = src[p];
-        w[i] = d.qk_norm ? nw[p] : 1.0f;
-        vv[i] = isk ? vsrc[p] : 0.0f;
-        cs[i] = p < HD / 2 ? rope[p] : make_float2(0.0f, 0.0f);
+        for (int i = 0; i < PER; ++i) vv[i] = vsrc[lane + 64 * i];
     }
-    if (d.qk_norm) {
-        double ss = 0.0;
-#pragma unroll
-        for (int i = 0; i < PER; ++i) ss += (double)(v[i] * v[i]);
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) ss += __shfl_xor(ss, o);
-        const float mean = (float)(ss / HD);
-        const float scale = 1.0f / sqrtf(mean + d.eps);
-#pragma unroll
-        for (int i = 0; i < PER; ++i) {
-            const float tt = v[i] * scale;
-            v[i] = tt * w[i];
-        }
-    }
-#pragma unroll
-    for (int i = 0; i < PER; ++i) row[lane + 64 * i] = v[i];
-    __syncthreads();
-    float o0[PER], o1[PER];
-    int i0s[PER], i1s[PER];
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-        const int p = lane + 64 * i;
-        i0s[i] = -1;
-        if (p < HD / 2) {
-            const int i0 = d.neox ? p : 2 * p, i1 = d.neox ? p + HD / 2 : 2 * p + 1;
-            const float x0 = row[i0], x1 = row[i1];
-            o0[i] = x0 * cs[i].x - x1 * cs[i].y;
-            o1[i] = x0 * cs[i].y + x1 * cs[i].x;
-            i0s[i] = i0, i1s[i] = i1;
-        }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < PER; ++i)
-        if (i0s[i] >= 0) {
-            row[i0s[i]] = f16r(o0[i]);
-            row[i1s[i]] = f16r(o1[i]);
-        }
-    __syncthreads();
+    prep_head<HD>(src, isk ? k_norm : q_norm, pb.rope + (size_t)pos * (HD / 2), d, row);
     if (!isk) {
 #pragma unroll
         for (int i = 0; i < PER; ++i) src[lane + 64 * i] = row[lane + 64 * i];
@@ -273,114 +228,27 @@ __global__ __launch_bounds__(64) void k_pf_rope(LlmDims d, const float *q_norm, 
     }
 }
 
-// One 256-thread workgroup per (128-position chunk, kv head, token): causal online softmax
-// over the chunk's positions <= the token's position, all rows read from the cache (this
-// chunk's own rows were written by k_pf_rope). Slot / merge order as k_attention.
+// One workgroup per (128-position chunk, kv head, token): causal online softmax over the
+// chunk's positions <= the token's position, all rows read from the cache (this chunk's own
+// rows were written by k_pf_rope); attend_chunk is the decode step's sweep.
 template <int HD, int G>
-__global__ __launch_bounds__(NT) void k_pf_attention(LlmDims d, const _Float16 *kc, const _Float16 *vc,
-                                                     PrefillBuffers pb, int p0) {
-    constexpr int LP = HD / 8;
-    constexpr int NS = NT / LP;
-    constexpr int IT = ATT_CHUNK / NS;
-    constexpr int REC = part_rec(HD);
-    typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+__global__ __launch_bounds__(ATT_NT) void k_pf_attention(LlmDims d, const _Float16 *kc, const _Float16 *vc,
+                                                         PrefillBuffers pb, int p0) {
+    using C = AttCfg<HD>;
     __shared__ float qs[G][HD];
-    __shared__ float wres[NWAVE][G][HD + 2];
+    __shared__ float wres[ATT_NW][G][HD + 2];
     const int kvh = blockIdx.y, ch = blockIdx.x, t = blockIdx.z, pos = p0 + t;
     const int t0 = ch * ATT_CHUNK;
     if (t0 > pos) return;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int lp = lane % LP, sl = tid / LP;
+    h8 kr[C::IT], vr[C::IT];
+    load_kv_rows<HD>(kc + (size_t)kvh * d.n_ctx * HD, vc + (size_t)kvh * d.n_ctx * HD, t0, pos, kr, vr);
     const int QD = (d.n_head + 2 * d.n_kv) * HD;
-    const _Float16 *kbase = kc + (size_t)kvh * d.n_ctx * HD;
-    const _Float16 *vbase = vc + (size_t)kvh * d.n_ctx * HD;
-    h8 kr[IT], vr[IT];
-#pragma unroll
-    for (int it = 0; it < IT; ++it) {
-        const int tt = min(t0 + sl + NS * it, pos);
-        kr[it] = *reinterpret_cast<const h8 *>(kbase + (size_t)tt * HD + lp * 8);
-        vr[it] = *reinterpret_cast<const h8 *>(vbase + (size_t)tt * HD + lp * 8);
-    }
     const float *qsrc = pb.qkv + (size_t)t * QD + (size_t)kvh * G * HD;
-    for (int e = tid; e < G * HD; e += NT) qs[e / HD][e % HD] = qsrc[e];
+    for (int e = threadIdx.x; e < G * HD; e += ATT_NT) qs[e / HD][e % HD] = qsrc[e];
     __syncthreads();
-    float qv[G][8];
-#pragma unroll
-    for (int g = 0; g < G; ++g)
-#pragma unroll
-        for (int i = 0; i < 8; ++i) qv[g][i] = qs[g][lp * 8 + i];
-    float m[G], l[G], acc[G][8];
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-        m[g] = -INFINITY, l[g] = 0.0f;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) acc[g][i] = 0.0f;
-    }
-#pragma unroll
-    for (int it = 0; it < IT; ++it) {
-        const bool valid = t0 + sl + NS * it <= pos;
-        float kf[8], vf[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) kf[i] = (float)kr[it][i], vf[i] = (float)vr[it][i];
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-            float sdot = 0.0f;
-#pragma unroll
-            for (int i = 0; i < 8; ++i) sdot = fmaf(qv[g][i], kf[i], sdot);
-            sdot = group_sum<LP>(sdot);
-            const float sc = valid ? sdot * d.scale : -INFINITY;
-            const float mn = fmaxf(m[g], sc);
-            const float c = m[g] == mn ? 1.0f : expf(m[g] - mn);
-            const float p = valid ? expf(sc - mn) : 0.0f;
-            l[g] = l[g] * c + p;
-#pragma unroll
-            for (int i = 0; i < 8; ++i) acc[g][i] = acc[g][i] * c + p * vf[i];
-            m[g] = mn;
-        }
-    }
-#pragma unroll
-    for (int o = LP; o < 64; o <<= 1) {
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-            const float m2 = __shfl_xor(m[g], o), l2 = __shfl_xor(l[g], o);
-            const float mn = fmaxf(m[g], m2);
-            const float c1 = m[g] == -INFINITY ? 0.0f : expf(m[g] - mn);
-            const float c2 = m2 == -INFINITY ? 0.0f : expf(m2 - mn);
-            l[g] = l[g] * c1 + l2 * c2;
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                const float a2 = __shfl_xor(acc[g][i], o);
-                acc[g][i] = acc[g][i] * c1 + a2 * c2;
-            }
-            m[g] = mn;
-        }
-    }
-    if (lane < LP) {
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-#pragma unroll
-            for (int i = 0; i < 8; ++i) wres[wave][g][lp * 8 + i] = acc[g][i];
-            if (lp == 0) wres[wave][g][HD] = m[g], wres[wave][g][HD + 1] = l[g];
-        }
-    }
-    __syncthreads();
-    for (int e = tid; e < G * HD; e += NT) {
-        const int g = e / HD, dd = e - g * HD;
-        float M = -INFINITY;
-#pragma unroll
-        for (int w = 0; w < NWAVE; ++w) M = fmaxf(M, wres[w][g][HD]);
-        float L = 0.0f, O = 0.0f;
-#pragma unroll
-        for (int w = 0; w < NWAVE; ++w) {
-            const float mw = wres[w][g][HD];
-            const float c = mw == -INFINITY ? 0.0f : expf(mw - M);
-            L += c * wres[w][g][HD + 1];
-            O += c * wres[w][g][dd];
-        }
-        float *dst = pb.part + (((size_t)t * d.n_head + kvh * G + g) * d.max_splits + ch) * REC;
-        dst[dd] = O;
-        if (dd == 0) dst[HD] = M, dst[HD + 1] = L;
-    }
+    attend_chunk<HD, G>(qs, kr, vr, t0, pos, d.scale, wres,
+                        pb.part + (((size_t)t * d.n_head + kvh * G) * d.max_splits + ch) * C::REC,
+                        (size_t)d.max_splits * C::REC);
 }
 
 template <int NP, int T>
@@ -452,11 +320,11 @@ template <int HD>
 void launch_pf_attention(int G, dim3 grid, hipStream_t s, const LlmDims &d, const _Float16 *kc, const _Float16 *vc,
                          const PrefillBuffers &pb, int p0) {
     switch (G) {
-        case 1: hipLaunchKernelGGL((k_pf_attention<HD, 1>), grid, dim3(NT), 0, s, d, kc, vc, pb, p0); break;
-        case 2: hipLaunchKernelGGL((k_pf_attention<HD, 2>), grid, dim3(NT), 0, s, d, kc, vc, pb, p0); break;
-        case 3: hipLaunchKernelGGL((k_pf_attention<HD, 3>), grid, dim3(NT), 0, s, d, kc, vc, pb, p0); break;
-        case 4: hipLaunchKernelGGL((k_pf_attention<HD, 4>), grid, dim3(NT), 0, s, d, kc, vc, pb, p0); break;
-        case 8: hipLaunchKernelGGL((k_pf_attention<HD, 8>), grid, dim3(NT), 0, s, d, kc, vc, pb, p0); break;
+        case 1: hipLaunchKernelGGL((k_pf_attention<HD, 1>), grid, dim3(ATT_NT), 0, s, d, kc, vc, pb, p0); break;
+        case 2: hipLaunchKernelGGL((k_pf_attention<HD, 2>), grid, dim3(ATT_NT), 0, s, d, kc, vc, pb, p0); break;
+        case 3: hipLaunchKernelGGL((k_pf_attention<HD, 3>), grid, dim3(ATT_NT), 0, s, d, kc, vc, pb, p0); break;
+        case 4: hipLaunchKernelGGL((k_pf_attention<HD, 4>), grid, dim3(ATT_NT), 0, s, d, kc, vc, pb, p0); break;
+        case 8: hipLaunchKernelGGL((k_pf_attention<HD, 8>), grid, dim3(ATT_NT), 0, s, d, kc, vc, pb, p0); break;
         default: break;
     }
 }

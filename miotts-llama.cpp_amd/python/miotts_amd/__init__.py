@@ -14,7 +14,8 @@ import numpy as np
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 REPO_ROOT = os.path.dirname(PKG_ROOT)
-BUILD_DIR = os.path.join(PKG_ROOT, "build")
+# MIO_BUILD_DIR: an alternative in-tree build (A/B experiments of compile-time variants)
+BUILD_DIR = os.environ.get("MIO_BUILD_DIR") or os.path.join(PKG_ROOT, "build")
 LIB_PATH = os.path.join(BUILD_DIR, "libmiotts.so")
 INCLUDE_DIR = os.path.join(REPO_ROOT, "include")
 
@@ -411,12 +412,13 @@ class Llm:
         return out
 
     def timeline(self) -> np.ndarray:
-        """Per-launch, per-workgroup [start, end] (us from the step start, NaN = absent) of one
-        graph-replayed step (diagnostic, mio_hip_llm_timeline; advances the decode state)."""
-        out = np.zeros(1024 * 256 * 2, np.uint64)
+        """Per-launch, per-workgroup [start, mark 1, mark 2, end] (us from the step start, NaN =
+        absent) of one graph-replayed step (diagnostic, mio_hip_llm_timeline; advances the
+        decode state). Marks: see MIO_TL_MARK in csrc/hip/llm_device.h."""
+        out = np.zeros(1024 * 256 * 4, np.uint64)
         n = ctypes.c_int(0)
         check(lib().mio_hip_llm_timeline(self.h, _ptr(out), 1024, ctypes.byref(n)))
-        t = out[: n.value * 512].astype(np.float64).reshape(n.value, 256, 2)
+        t = out[: n.value * 1024].astype(np.float64).reshape(n.value, 256, 4)
         t[t == 0] = np.nan
         return (t - np.nanmin(t[0, :, 0])) * 0.01
 

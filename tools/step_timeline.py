@@ -27,15 +27,21 @@ nl = t.shape[0]
 names = ["attn_in", "attention", "attn_out", "ffn_in", "ffn_down"] * ((nl - 2) // 5) + ["lm_head", "sample"]
 s0 = np.nanmin(t[:, :, 0], axis=1)
 s1 = np.nanmax(t[:, :, 0], axis=1)
-e0 = np.nanmin(t[:, :, 1], axis=1)
-e1 = np.nanmax(t[:, :, 1], axis=1)
-wd = np.nanmedian(t[:, :, 1] - t[:, :, 0], axis=1)
+e0 = np.nanmin(t[:, :, 3], axis=1)
+e1 = np.nanmax(t[:, :, 3], axis=1)
+wd = np.nanmedian(t[:, :, 3] - t[:, :, 0], axis=1)
+# per-workgroup phases (median over workgroups): start -> mark 1 -> mark 2 -> end
+ph1 = np.nanmedian(t[:, :, 1] - t[:, :, 0], axis=1)
+ph2 = np.nanmedian(t[:, :, 2] - t[:, :, 1], axis=1)
+ph3 = np.nanmedian(t[:, :, 3] - t[:, :, 2], axis=1)
+m2 = np.nanmax(t[:, :, 2], axis=1) - s0
 dur = e1 - s0
 gap = np.r_[0.0, s0[1:] - e1[:-1]]
 print(f"step wall {e1[-1] - s0[0]:.1f} us over {nl} launches; kernel time {dur.sum():.1f} us, "
       f"gaps {gap[1:].sum():.1f} us (mean {gap[1:].mean():.2f}, min {gap[1:].min():.2f}, max {gap[1:].max():.2f})")
-print("  kernel      dur    gap-before  start-spread  end-spread  median-wg")
+print("  kernel      dur    gap-before  start-spread  end-spread  median-wg   wg:->m1  m1->m2  m2->end  last-m2")
 for k in ["attn_in", "attention", "attn_out", "ffn_in", "ffn_down", "lm_head", "sample"]:
     idx = [i for i, n in enumerate(names) if n == k]
     print(f"  {k:10s} {dur[idx].mean():6.2f} {gap[idx].mean():8.2f} {(s1 - s0)[idx].mean():12.2f} "
-          f"{(e1 - e0)[idx].mean():11.2f} {wd[idx].mean():10.2f}")
+          f"{(e1 - e0)[idx].mean():11.2f} {wd[idx].mean():10.2f} {np.nanmean(ph1[idx]):9.2f} "
+          f"{np.nanmean(ph2[idx]):7.2f} {np.nanmean(ph3[idx]):8.2f} {np.nanmean(m2[idx]):8.2f}")
