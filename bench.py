@@ -205,8 +205,8 @@ def main():
     tl = llm.timeline()
     nl = tl.shape[0]
     names = [KERNEL_NAMES[k] for k in (0, 1, 2, 3, 4)] * ((nl - 2) // 5) + [KERNEL_NAMES[6], "k_sample"]
-    dur = np.nanmax(tl[:, :, 3], axis=1) - np.nanmin(tl[:, :, 0], axis=1)
-    step_wall_us = float(np.nanmax(tl[-1, :, 3]) - np.nanmin(tl[0, :, 0]))
+    dur = np.nanmax(tl[:, :, 7], axis=1) - np.nanmin(tl[:, :, 0], axis=1)
+    step_wall_us = float(np.nanmax(tl[-1, :, 7]) - np.nanmin(tl[0, :, 0]))
     per_kernel = {}
     for i, nm in enumerate(names):
         per_kernel.setdefault(nm, []).append(float(dur[i]))

@@ -141,10 +141,11 @@ int mio_hip_llm_time_kernel(mio_hip_llm *m, int which, int iters, float *avg_ms,
  * out[16] / out[31] = s_memrealtime (100 MHz) at the first / last checkpoint. */
 int mio_hip_llm_trace_kernel(mio_hip_llm *m, int which, uint64_t *out);
 /* Diagnostic: one decode step replayed as a graph with the step timeline on; out has
- * max_launches * 256 * 4 slots: out[(i * 256 + w) * 4 + {0,1,2,3}] = start / mark 1 /
- * mark 2 / end (s_memrealtime, 100 MHz; 0 = not recorded) of workgroup w of launch i (5
- * launches per layer, then lm_head, sample). Marks: matvec launches 1 = weight loads issued,
- * 2 = activations quantized; attention 1 = K/V loads issued, 2 = heads prepared.
+ * max_launches * 256 * 8 slots: out[(i * 256 + w) * 8 + k] = start (k 0) / marks (1-6) /
+ * end (7) (s_memrealtime, 100 MHz; 0 = not recorded) of workgroup w of launch i (5 launches
+ * per layer, then lm_head, sample). Marks: matvec launches 1 = weight loads issued,
+ * 2 = activations quantized; attention 1 = K/V loads issued, 2 = heads prepared; 3-6 =
+ * prologue steps in -DMIO_TL_DIAG builds.
  * Advances the decode state. */
 int mio_hip_llm_timeline(mio_hip_llm *m, uint64_t *out, int max_launches, int *n_launches);
 /* Stage times (ms, HIP events) of the last mio_hip_codec_decode_pcm: [0] codec, [1] iSTFT. */

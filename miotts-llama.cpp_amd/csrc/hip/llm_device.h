@@ -27,27 +27,40 @@ namespace {
     } while (0)
 
 // Step timeline (diagnostic, mio_hip_llm_timeline): per workgroup of each launch {start,
-// mark 1, mark 2, end}, s_memrealtime ticks (100 MHz), plain stores to slot [seq][wg][4]
-// (wg < 256). Marks: matvec kernels 1 = weight loads issued, 2 = activations quantized;
+// mark 1, mark 2, diagnostic marks 3-6, end}, s_memrealtime ticks (100 MHz), plain stores to
+// slot [seq][wg][8] (wg < 256). Marks: matvec kernels 1 = weight loads issued, 2 = activations quantized;
 // attention 1 = K/V loads issued, 2 = heads prepared; sampler 1 = token chosen.
-#define MIO_TL_SLOT(bufs) ((bufs).tl + 4 * ((size_t)(bufs).seq * 256 + ((blockIdx.x + blockIdx.y * gridDim.x) & 255)))
+#define MIO_TL_SLOT(bufs) ((bufs).tl + 8 * ((size_t)(bufs).seq * 256 + ((blockIdx.x + blockIdx.y * gridDim.x) & 255)))
 #define MIO_TL_AT(bufs, k)                                                                      \
     do {                                                                                        \
         if ((bufs).tl && threadIdx.x == 0) MIO_TL_SLOT(bufs)[k] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
 #define MIO_TL_BEGIN(bufs) MIO_TL_AT(bufs, 0)
 #define MIO_TL_MARK(bufs, k) MIO_TL_AT(bufs, k)
-#define MIO_TL_END(bufs) MIO_TL_AT(bufs, 3)
+#define MIO_TL_END(bufs) MIO_TL_AT(bufs, 7)
+// -DMIO_TL_DIAG: the prologue helpers also stamp marks 3-5 (activation consumed, reduced,
+// staged; diagnostic builds only)
+#ifdef MIO_TL_DIAG
+#define MIO_TL_DIAGSLOT(bufs) ((bufs).tl ? MIO_TL_SLOT(bufs) : nullptr)
+#else
+#define MIO_TL_DIAGSLOT(bufs) nullptr
+#endif
+#define MIO_TL_MARK1(bufs) MIO_TL_MARK(bufs, 1)
+// stamp after value v is available (the empty asm consumes it; the timer read cannot move
+// above a volatile asm)
+#define MIO_DIAG_STAMP(diag, k, v)                                                   \
+    do {                                                                             \
+        if ((diag) && threadIdx.x == 0) {                                            \
+            asm volatile("" ::"v"(v));                                               \
+            (diag)[k] = __builtin_amdgcn_s_memrealtime();                            \
+        }                                                                            \
+    } while (0)
 
 constexpr int NT = 256;        // threads of the attention / sampler kernels
 constexpr int NWAVE = NT / 64;
 constexpr int MT = 512;        // threads of a streaming matvec workgroup
 constexpr int MW = MT / 64;
 constexpr int ATT_CHUNK = kAttChunk;
-constexpr int PF_SLOT = 1024;  // LDS bytes per wave that receive discarded prefetch data
-constexpr int PF_LDS = MW * PF_SLOT;
-// dynamic LDS of a matvec launch: activation staging, then the prefetch slots
-__host__ __device__ inline size_t pf_offset(size_t base) { return (base + 15) & ~(size_t)15; }
 __host__ __device__ constexpr int part_rec(int hd) { return hd + 4; }  // partial record {O[hd], m, l, pad}
 
 __device__ __forceinline__ float h2f(uint32_t bits16) {
@@ -58,6 +71,12 @@ __device__ __forceinline__ float f16r(float f) { return (float)(_Float16)f; }
 __device__ __forceinline__ int sdot4(int a, int b, int c) { return __builtin_amdgcn_sdot4(a, b, c, false); }
 __device__ __forceinline__ uint4 ld16(const uint8_t *p) { return *reinterpret_cast<const uint4 *>(p); }
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS (and scalar) operations,
+// not for its vector memory operations. __syncthreads() carries a workgroup release fence,
+// which compiles to s_waitcnt vmcnt(0): in a prologue that waits for the whole weight group
+// in flight (and, in attention, for the K/V row stores) before the barrier.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // ------------------------------------------------------------------ cross-lane (DPP)
 // Cross-lane sums by DPP (gfx9 row_shr / row_bcast), never through LDS.
@@ -160,10 +179,10 @@ __device__ double block_sum(double v, double *red) {
     v = wave_sum_d(v);
     const int nw = blockDim.x >> 6;
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
-    __syncthreads();
+    lds_barrier();
     double t = 0.0;
     for (int w = 0; w < nw; ++w) t += red[w];
-    __syncthreads();
+    lds_barrier();
     return t;
 }
 
@@ -233,7 +252,24 @@ __device__ inline void quantize(const float *xs, int K, bool kquant, const ActL 
         quant_q8k(xs, K, a);
     else
         quant_q80(xs, K, a);
-    __syncthreads();
+    lds_barrier();
+}
+
+// MIO_X_FIRST=1: a matvec launch waits for its activation loads before issuing any weight
+// load (the activation is the critical path; queued behind the chip's first weight burst it
+// arrives late). Memory clobber: no load moves across it.
+#ifndef MIO_X_FIRST
+#define MIO_X_FIRST 0
+#endif
+// MIO_X_FIRST=2: every wave issues its activation loads before any wave issues weights (a
+// bare s_barrier, no waitcnt): the CU's memory queue then holds all activation requests
+// ahead of the weight burst, so no wave's activation waits behind other waves' weights.
+__device__ __forceinline__ void x_gate() {
+#if MIO_X_FIRST == 1
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#elif MIO_X_FIRST == 2
+    asm volatile("s_barrier" ::: "memory");
+#endif
 }
 
 // ------------------------------------------------------------------ prologue registers
@@ -260,7 +296,8 @@ __device__ inline void load_x(const float *x, const float *w, int K, XRegs<XV> &
 
 // ggml_rms_norm + mul(weight): xs = (x * 1/sqrtf(mean(x^2) + eps)) * w, then quantize.
 template <int XV>
-__device__ void rmsnorm_quant(const XRegs<XV> &xr, int K, float eps, bool kquant, const Smem &s) {
+__device__ void rmsnorm_quant(const XRegs<XV> &xr, int K, float eps, bool kquant, const Smem &s,
+                              unsigned long long *diag = nullptr) {
     double acc = 0.0;
 #pragma unroll
     for (int i = 0; i < XV; ++i) {
@@ -273,7 +310,9 @@ __device__ void rmsnorm_quant(const XRegs<XV> &xr, int K, float eps, bool kquant
             acc += (double)(v.w * v.w);
         }
     }
+    MIO_DIAG_STAMP(diag, 3, acc);  // activation consumed (arrived)
     const double tot = block_sum(acc, s.red);
+    MIO_DIAG_STAMP(diag, 4, tot);  // reduced over the workgroup
     const float mean = (float)(tot / K);
     const float scale = 1.0f / sqrtf(mean + eps);
 #pragma unroll
@@ -288,18 +327,22 @@ __device__ void rmsnorm_quant(const XRegs<XV> &xr, int K, float eps, bool kquant
             t = v.w * scale, s.xs[e + 3] = t * ww.w;
         }
     }
-    __syncthreads();
+    lds_barrier();
+    MIO_DIAG_STAMP(diag, 5, scale);  // normalized activation staged in LDS
     quantize(s.xs, K, kquant, s.a);
+    MIO_DIAG_STAMP(diag, 6, scale);  // quantized
 }
 
 template <int XV>
-__device__ inline void plain_quant(const XRegs<XV> &xr, int K, bool kquant, const Smem &s) {
+__device__ inline void plain_quant(const XRegs<XV> &xr, int K, bool kquant, const Smem &s,
+                                   unsigned long long *diag = nullptr) {
 #pragma unroll
     for (int i = 0; i < XV; ++i) {
         const int e = (threadIdx.x + i * MT) * 4;
         if (e < K) *reinterpret_cast<float4 *>(s.xs + e) = xr.v[i];
     }
-    __syncthreads();
+    lds_barrier();
+    MIO_DIAG_STAMP(diag, 5, 0);  // activation arrived and staged in LDS
     quantize(s.xs, K, kquant, s.a);
 }
 
@@ -382,7 +425,10 @@ __device__ __forceinline__ uint32_t bld2(const uint8_t *base, uint32_t bytes, ui
 template <int T>
 __device__ __forceinline__ Frag load_frag(const QMat W, int row, int pass) {
     const int lane = threadIdx.x & 63;
-    const uint32_t R = (uint32_t)W.rows, r = (uint32_t)min(max(row, 0), W.rows - 1);
+    // the row is wave-uniform; readfirstlane lets the compiler keep it (and the soffset) in
+    // SGPRs - without it every load became a waterfall loop over a VGPR soffset
+    const uint32_t R = (uint32_t)W.rows,
+                   r = (uint32_t)__builtin_amdgcn_readfirstlane(min(max(row, 0), W.rows - 1));
     Frag f;
     if constexpr (T == 12) {
         const int nsb = W.k >> 8, sb = min(pass * 8 + (lane >> 3), nsb - 1), pc = lane & 7;
@@ -545,10 +591,12 @@ __device__ __forceinline__ void load_group(const QMat W0, const QMat W1, int lo,
                                            Frag (&f)[Cfg<NP, SU>::U], int split = INT_MAX) {
 #pragma unroll
     for (int j = 0; j < Cfg<NP, SU>::U; ++j) {
-        const int u = max(0, min(u0 + j, n - 1));
+        // wave-uniform (readfirstlane: the compiler cannot prove it through wave_range's
+        // VALU divisions, and a VGPR unit index turns matrix selection into waterfall loops)
+        const int u = __builtin_amdgcn_readfirstlane(max(0, min(u0 + j, n - 1)));
         const int p = u % NP, m = (u / NP) % NM, i = u / (NP * NM);
         if constexpr (NM == 1) {
-            const int r = lo + i;
+            const int r = __builtin_amdgcn_readfirstlane(lo + i);
             f[j] = load_frag<T>(r >= split ? W1 : W0, r >= split ? r - split : r, p);
         } else {
             f[j] = load_frag<T>(m ? W1 : W0, lo + i, p);
@@ -642,56 +690,6 @@ __device__ inline void wave_range(int R, int &lo, int &hi, int b, int G) {
 }
 __device__ inline void wave_range(int R, int &lo, int &hi) { wave_range(R, lo, hi, blockIdx.x, gridDim.x); }
 
-// ------------------------------------------------------------------ cross-launch prefetch
-
-__device__ inline void prefetch_range(const uint8_t *base, uint32_t total, uint32_t off, uint32_t bytes,
-                                      char *slot, int nw = MW) {
-    const auto r = rsrc(base, total);
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    for (uint32_t c = w; c * 1024u < bytes; c += nw)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void *)slot, 16, lane * 16,
-                                                 off + c * 1024u, 0, 0);
-}
-
-// all arrays of rows [r0, r1) of W
-__device__ inline void prefetch_rows(const QMat &W, int r0, int r1, uint32_t cap, char *slot, int nw = MW) {
-    if (r1 <= r0) return;
-    const uint32_t R = (uint32_t)W.rows, n = (uint32_t)(r1 - r0);
-    uint32_t rb[4] = {0, 0, 0, 0};
-    const uint8_t *p[4] = {W.p0, W.p1, W.p2, W.p3};
-    if (W.type == 12) {
-        rb[0] = W.k / 2, rb[1] = (W.k >> 8) * 16;
-    } else if (W.type == 14) {
-        rb[0] = W.k / 2, rb[1] = W.k / 4, rb[2] = W.k / 16, rb[3] = (W.k >> 8) * 2;
-    } else {
-        rb[0] = W.k, rb[1] = (W.k >> 5) * 2;
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-        if (rb[i]) prefetch_range(p[i], R * rb[i], (uint32_t)r0 * rb[i], min(n * rb[i], cap), slot, nw);
-}
-
-__device__ inline void prefetch_next(const Prefetch &pf, char *lds_slots) {
-    if (pf.mode == 0) return;
-    char *slot = lds_slots + PF_SLOT * __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int b = blockIdx.x;
-    if (pf.mode == 3) {
-        if (b < pf.g_qk) {
-            const int o1 = pf.m[0].rows, o2 = o1 + pf.m[1].rows;
-            const int ra = (o2 * b) / pf.g_qk, rb = (o2 * (b + 1)) / pf.g_qk;
-            prefetch_rows(pf.m[0], ra, min(rb, o1), pf.cap, slot);
-            prefetch_rows(pf.m[1], max(ra, o1) - o1, rb - o1, pf.cap, slot);
-        } else if (b < pf.grid) {
-            const int gv = pf.grid - pf.g_qk, bv = b - pf.g_qk, R = pf.m[2].rows;
-            prefetch_rows(pf.m[2], (R * bv) / gv, (R * (bv + 1)) / gv, pf.cap, slot);
-        }
-        return;
-    }
-    if (b >= pf.grid) return;
-    const int R = pf.m[0].rows, ra = (R * b) / pf.grid, rb = (R * (b + 1)) / pf.grid;
-    prefetch_rows(pf.m[0], ra, rb, pf.cap, slot);
-    if (pf.mode == 2) prefetch_rows(pf.m[1], ra, rb, pf.cap, slot);
-}
 
 // ------------------------------------------------------------------ embedding rows
 __device__ float dequant_elem(const QMat &W, int row, int e) {
@@ -762,7 +760,8 @@ __device__ __forceinline__ float group_sum(float v) {
 // owns outputs 4(t + i*MT) .. +3; online softmax merge over chunks, 8 chunks' loads in
 // flight; normalized outputs -> s.xs, then re-quantized into s.a.
 template <int NP>
-__device__ void merge_attention(const LlmDims &d, const float *part, int nch, int K, bool kquant, const Smem &s) {
+__device__ void merge_attention(const LlmDims &d, const float *part, int nch, int K, bool kquant, const Smem &s,
+                                unsigned long long *diag = nullptr) {
     const int hd = d.hd, rec = part_rec(hd);
 #pragma unroll
     for (int i = 0; i < NP; ++i) {
@@ -799,7 +798,8 @@ __device__ void merge_attention(const LlmDims &d, const float *part, int nch, in
             *reinterpret_cast<float4 *>(s.xs + e) = make_float4(O.x / L, O.y / L, O.z / L, O.w / L);
         }
     }
-    __syncthreads();
+    lds_barrier();
+    MIO_DIAG_STAMP(diag, 5, 0);  // chunks merged, staged in LDS
     quantize(s.xs, K, kquant, s.a);
 }
 
@@ -929,7 +929,7 @@ __device__ __forceinline__ void load_kv_rows(const _Float16 *kbase, const _Float
 template <int HD, int G>
 __device__ void attend_chunk(const float (*qs)[HD], const h8 (&kr)[AttCfg<HD>::IT], const h8 (&vr)[AttCfg<HD>::IT],
                              int t0, int pos, float scale, float (*wres)[G][HD + 2], float *dst, size_t g_stride,
-                             unsigned long long *trace = nullptr) {
+                             unsigned long long *trace = nullptr, unsigned long long *diag = nullptr) {
     // diagnostic checkpoints (mio_hip_llm_trace_kernel): 3 sweep done, 4 lane merge, 5 wave merge
     auto mark = [&](int k) {
         if (trace && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
@@ -975,6 +975,7 @@ __device__ void attend_chunk(const float (*qs)[HD], const h8 (&kr)[AttCfg<HD>::I
         }
     }
     mark(3);
+    MIO_DIAG_STAMP(diag, 3, acc[0][0]);  // sweep done
     // merge the wave's slots (lane stride LP): every lane of a butterfly pair ends bitwise equal
     auto merge_step = [&](auto xl) {
 #pragma unroll
@@ -996,6 +997,7 @@ __device__ void attend_chunk(const float (*qs)[HD], const h8 (&kr)[AttCfg<HD>::I
     merge_step([](float v) { return xor_lane<16>(v); });
     merge_step([](float v) { return xor_lane<32>(v); });
     mark(4);
+    MIO_DIAG_STAMP(diag, 4, acc[0][0]);  // lane merges done
     if (lane < LP) {
 #pragma unroll
         for (int g = 0; g < G; ++g) {
@@ -1004,8 +1006,9 @@ __device__ void attend_chunk(const float (*qs)[HD], const h8 (&kr)[AttCfg<HD>::I
             if (lp == 0) wres[wave][g][HD] = m[g], wres[wave][g][HD + 1] = l[g];
         }
     }
-    __syncthreads();
+    lds_barrier();
     mark(5);
+    MIO_DIAG_STAMP(diag, 5, 0);  // wave results in LDS
     // merge the waves -> this chunk's partial record per q head
     for (int e = tid; e < G * HD; e += ATT_NT) {
         const int g = e / HD, dd = e - g * HD;

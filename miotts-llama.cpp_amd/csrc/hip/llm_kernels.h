@@ -37,17 +37,6 @@ struct SampleCfg {
     int max_steps;
 };
 
-// Rows of the NEXT matvec launch that workgroup b of the current launch sweeps into
-// L2 / Infinity Cache (fire-and-forget LDS-DMA loads): mode 0 none, 1 rows of m[0] over
-// `grid` workgroups, 2 the same rows of m[0] and m[1] (gate/up), 3 q|k rows over the first
-// g_qk workgroups and v rows over the rest (attn_in), 4 all rows of m[0..2] over the
-// attention launch's extra prefetch workgroups. At most `cap` bytes per array.
-struct Prefetch {
-    QMat m[3];
-    int mode, grid, g_qk;
-    uint32_t cap;
-};
-
 struct LayerW {
     const float *attn_norm, *q_norm, *k_norm, *ffn_norm;
     QMat wq, wk, wv, wo, gate, up, down;
@@ -61,8 +50,6 @@ struct LlmDims {
     int max_splits;
     int n_wg;         // streaming-matvec workgroups (one per CU)
     int n_layer;
-    int prefetch;     // matvec launches prefetch the next launch's rows (MIO_PREFETCH=0: off)
-    int att_prefetch; // extra attention grid columns that prefetch Wo/gate/up (0: off)
 };
 
 struct LlmBuffers {

@@ -44,25 +44,24 @@ namespace {
 // branch is WG-uniform and runs its own prologue, so neither path merges load counts.
 template <int NP, int TQ, int TV, int SU>
 __global__ __launch_bounds__(MT) void k_attn_in(LlmDims d, const float *norm_w, QMat wq, QMat wk, QMat wv,
-                                                int g_qk, Prefetch pf, LlmBuffers b) {
+                                                int g_qk, LlmBuffers b) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int K = d.n_embd;
     const Smem s = carve(smem, K);
-    char *pf_lds = smem + pf_offset(smem_bytes(K));
     MIO_TRACE(b, 0);
     MIO_TL_BEGIN(b);
     XRegs<NP> xr;
     load_x(b.x, norm_w, K, xr);
+    x_gate();
     const int o1 = wq.rows, o2 = wq.rows + wk.rows;
     Frag ga[Cfg<NP, SU>::U], gb[Cfg<NP, SU>::U];
     int lo, hi;
     if ((int)blockIdx.x < g_qk) {
         wave_range(o2, lo, hi, blockIdx.x, g_qk);
         load_first<TQ, NP, 1, SU>(wq, wk, lo, hi, ga, gb, o1);
-        prefetch_next(pf, pf_lds);
         MIO_TRACE(b, 1);
-    MIO_TL_MARK(b, 1);
-        rmsnorm_quant(xr, K, d.eps, TQ != 8, s);
+    MIO_TL_MARK1(b);
+        rmsnorm_quant(xr, K, d.eps, TQ != 8, s, MIO_TL_DIAGSLOT(b));
         MIO_TRACE(b, 2);
     MIO_TL_MARK(b, 2);
         stream_rows<TQ, NP, 1, SU>(wq, wk, lo, hi, ga, gb, s.a, [&](int row, float v, float) {
@@ -73,8 +72,7 @@ __global__ __launch_bounds__(MT) void k_attn_in(LlmDims d, const float *norm_w, 
     } else {
         wave_range(wv.rows, lo, hi, blockIdx.x - g_qk, gridDim.x - g_qk);
         load_first<TV, NP, 1, SU>(wv, wv, lo, hi, ga, gb);
-        prefetch_next(pf, pf_lds);
-        rmsnorm_quant(xr, K, d.eps, TQ != 8, s);
+        rmsnorm_quant(xr, K, d.eps, TQ != 8, s, MIO_TL_DIAGSLOT(b));
         stream_rows<TV, NP, 1, SU>(wv, wv, lo, hi, ga, gb, s.a, [&](int row, float v, float) {
             if ((threadIdx.x & 63) == 0) b.qkv[o2 + row] = v;
         });
@@ -92,7 +90,7 @@ __device__ inline float lane_value(float v, int i) {
 }
 
 template <int NP, int T, int SU>
-__global__ __launch_bounds__(MT) void k_attn_out(LlmDims d, QMat wo, Prefetch pf, LlmBuffers b) {
+__global__ __launch_bounds__(MT) void k_attn_out(LlmDims d, QMat wo, LlmBuffers b) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     MIO_TRACE(b, 0);
     MIO_TL_BEGIN(b);
@@ -103,10 +101,9 @@ __global__ __launch_bounds__(MT) void k_attn_out(LlmDims d, QMat wo, Prefetch pf
     const float xres = load_resid(b.x, lo, hi);
     Frag ga[Cfg<NP, SU>::U], gb[Cfg<NP, SU>::U];
     load_first<T, NP, 1, SU>(wo, wo, lo, hi, ga, gb);
-    prefetch_next(pf, smem + pf_offset(smem_bytes(K)));
     MIO_TRACE(b, 1);
-    MIO_TL_MARK(b, 1);
-    merge_attention<NP>(d, b.part, b.st->pos / ATT_CHUNK + 1, K, T != 8, s);
+    MIO_TL_MARK1(b);
+    merge_attention<NP>(d, b.part, b.st->pos / ATT_CHUNK + 1, K, T != 8, s, MIO_TL_DIAGSLOT(b));
     MIO_TRACE(b, 2);
     MIO_TL_MARK(b, 2);
     stream_rows<T, NP, 1, SU>(wo, wo, lo, hi, ga, gb, s.a, [&](int row, float v, float) {
@@ -118,7 +115,7 @@ __global__ __launch_bounds__(MT) void k_attn_out(LlmDims d, QMat wo, Prefetch pf
 }
 
 template <int NP, int T, int SU>
-__global__ __launch_bounds__(MT) void k_ffn_in(LlmDims d, const float *norm_w, QMat gate, QMat up, Prefetch pf,
+__global__ __launch_bounds__(MT) void k_ffn_in(LlmDims d, const float *norm_w, QMat gate, QMat up,
                                                LlmBuffers b) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     MIO_TRACE(b, 0);
@@ -127,14 +124,14 @@ __global__ __launch_bounds__(MT) void k_ffn_in(LlmDims d, const float *norm_w, Q
     const Smem s = carve(smem, K);
     XRegs<NP> xr;
     load_x(b.x, norm_w, K, xr);
+    x_gate();
     int lo, hi;
     wave_range(gate.rows, lo, hi);
     Frag ga[Cfg<NP, SU>::U], gb[Cfg<NP, SU>::U];
     load_first<T, NP, 2, SU>(gate, up, lo, hi, ga, gb);
-    prefetch_next(pf, smem + pf_offset(smem_bytes(K)));
     MIO_TRACE(b, 1);
-    MIO_TL_MARK(b, 1);
-    rmsnorm_quant(xr, K, d.eps, T != 8, s);
+    MIO_TL_MARK1(b);
+    rmsnorm_quant(xr, K, d.eps, T != 8, s, MIO_TL_DIAGSLOT(b));
     MIO_TRACE(b, 2);
     MIO_TL_MARK(b, 2);
     stream_rows<T, NP, 2, SU>(gate, up, lo, hi, ga, gb, s.a, [&](int row, float g, float u) {
@@ -145,7 +142,7 @@ __global__ __launch_bounds__(MT) void k_ffn_in(LlmDims d, const float *norm_w, Q
 }
 
 template <int NP, int T, int SU>
-__global__ __launch_bounds__(MT) void k_ffn_down(LlmDims d, QMat down, Prefetch pf, LlmBuffers b) {
+__global__ __launch_bounds__(MT) void k_ffn_down(LlmDims d, QMat down, LlmBuffers b) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     MIO_TRACE(b, 0);
     MIO_TL_BEGIN(b);
@@ -156,12 +153,12 @@ __global__ __launch_bounds__(MT) void k_ffn_down(LlmDims d, QMat down, Prefetch 
     int lo, hi;
     wave_range(down.rows, lo, hi);
     const float xres = load_resid(b.x, lo, hi);
+    x_gate();
     Frag ga[Cfg<NP, SU>::U], gb[Cfg<NP, SU>::U];
     load_first<T, NP, 1, SU>(down, down, lo, hi, ga, gb);
-    prefetch_next(pf, smem + pf_offset(smem_bytes(K)));
     MIO_TRACE(b, 1);
-    MIO_TL_MARK(b, 1);
-    plain_quant(xr, K, T != 8, s);
+    MIO_TL_MARK1(b);
+    plain_quant(xr, K, T != 8, s, MIO_TL_DIAGSLOT(b));
     MIO_TRACE(b, 2);
     MIO_TL_MARK(b, 2);
     stream_rows<T, NP, 1, SU>(down, down, lo, hi, ga, gb, s.a, [&](int row, float v, float) {
@@ -190,7 +187,7 @@ __device__ inline float gumbel(uint64_t seed, int step, int idx) {
 // (<= 128) are parked one per lane (two registers) and the noise is drawn for 64 rows at
 // a time after the stream.
 template <int NP, int T>
-__global__ __launch_bounds__(MT) void k_lm_head(LlmDims d, const float *norm_w, QMat lm, Prefetch pf, LlmBuffers b) {
+__global__ __launch_bounds__(MT) void k_lm_head(LlmDims d, const float *norm_w, QMat lm, LlmBuffers b) {
     const SampleCfg sc = *b.cfg;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __shared__ float bs_[MW];
@@ -201,15 +198,15 @@ __global__ __launch_bounds__(MT) void k_lm_head(LlmDims d, const float *norm_w, 
     const Smem s = carve(smem, K);
     XRegs<NP> xr;
     load_x(b.x, norm_w, K, xr);
+    x_gate();
     const int step = b.st->step;
     int lo, hi;
     wave_range(lm.rows, lo, hi);
     Frag ga[Cfg<NP>::U], gb[Cfg<NP>::U];
     load_first<T, NP, 1>(lm, lm, lo, hi, ga, gb);
-    prefetch_next(pf, smem + pf_offset(smem_bytes(K)));
     MIO_TRACE(b, 1);
-    MIO_TL_MARK(b, 1);
-    rmsnorm_quant(xr, K, d.eps, T != 8, s);
+    MIO_TL_MARK1(b);
+    rmsnorm_quant(xr, K, d.eps, T != 8, s, MIO_TL_DIAGSLOT(b));
     MIO_TRACE(b, 2);
     MIO_TL_MARK(b, 2);
     const int lane = threadIdx.x & 63;
@@ -243,7 +240,7 @@ __global__ __launch_bounds__(MT) void k_lm_head(LlmDims d, const float *norm_w, 
     }
     const int wave = threadIdx.x >> 6;
     if (lane == 0) bs_[wave] = best, bi_[wave] = bi;
-    __syncthreads();
+    lds_barrier();
     if (threadIdx.x == 0) {
         for (int w = 1; w < MW; ++w)
             if (bs_[w] > best || (bs_[w] == best && bi_[w] < bi)) best = bs_[w], bi = bi_[w];
@@ -262,7 +259,7 @@ __global__ __launch_bounds__(MT) void k_lm_head(LlmDims d, const float *norm_w, 
 // of k_attn_out (the launch-boundary reduce: no extra launch, no in-kernel hand-off).
 template <int HD, int G>
 __global__ __launch_bounds__(ATT_NT) void k_attention(LlmDims d, const float *q_norm, const float *k_norm,
-                                                      _Float16 *kc, _Float16 *vc, Prefetch pf, LlmBuffers b) {
+                                                      _Float16 *kc, _Float16 *vc, LlmBuffers b) {
     using C = AttCfg<HD>;
     constexpr int PER = HD / 64;
     __shared__ float qs[G][HD];
@@ -272,20 +269,6 @@ __global__ __launch_bounds__(ATT_NT) void k_attention(LlmDims d, const float *q_
     MIO_TRACE(b, 0);
     MIO_TL_BEGIN(b);
     const int kvh = blockIdx.y, ch = blockIdx.x;
-    if (ch >= d.max_splits) {
-        // prefetch workgroups (pf.mode 4): this launch leaves HBM idle, so they sweep slice
-        // i of the next launches' matrices (m[0..2]) into the caches; data is discarded
-        __shared__ __attribute__((aligned(16))) char pf_slot[ATT_NW * PF_SLOT];
-        const int P = (gridDim.x - d.max_splits) * gridDim.y, i = (ch - d.max_splits) * gridDim.y + kvh;
-        char *slot = pf_slot + PF_SLOT * __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            const int R = pf.m[k].rows;
-            if (R > 0) prefetch_rows(pf.m[k], (R * i) / P, (R * (i + 1)) / P, pf.cap, slot, ATT_NW);
-        }
-        __builtin_amdgcn_s_waitcnt(0);
-        return;
-    }
     const int pos = b.st->pos;
     const int t0 = ch * ATT_CHUNK;
     if (t0 > pos) return;
@@ -295,7 +278,7 @@ __global__ __launch_bounds__(ATT_NT) void k_attention(LlmDims d, const float *q_
     h8 kr[C::IT], vr[C::IT];
     load_kv_rows<HD>(kc + (size_t)kvh * d.n_ctx * HD, vc + (size_t)kvh * d.n_ctx * HD, t0, pos, kr, vr);
     MIO_TRACE(b, 1);
-    MIO_TL_MARK(b, 1);
+    MIO_TL_MARK1(b);
     // q heads (waves 0..G-1) and, for the chunk owning `pos`, the new k/v row
     const bool owner = pos < t0 + ATT_CHUNK;
     for (int hh = wave; hh < G + (owner ? 1 : 0); hh += ATT_NW) {
@@ -321,7 +304,7 @@ __global__ __launch_bounds__(ATT_NT) void k_attention(LlmDims d, const float *q_
             }
         }
     }
-    __syncthreads();
+    lds_barrier();
     MIO_TRACE(b, 2);
     MIO_TL_MARK(b, 2);
     // the slot owning row `pos` takes it from LDS (exact f16 values, the cache row's bits)
@@ -338,20 +321,20 @@ __global__ __launch_bounds__(ATT_NT) void k_attention(LlmDims d, const float *q_
     }
     attend_chunk<HD, G>(qs, kr, vr, t0, pos, d.scale, wres,
                         b.part + ((size_t)(kvh * G) * d.max_splits + ch) * C::REC, (size_t)d.max_splits * C::REC,
-                        b.trace);
+                        b.trace, MIO_TL_DIAGSLOT(b));
     MIO_TL_END(b);
     MIO_TRACE(b, 15);
 }
 
 template <int HD>
 void launch_attention(int G, dim3 grid, hipStream_t s, const LlmDims &d, const float *qn, const float *kn,
-                      _Float16 *kc, _Float16 *vc, const Prefetch &pf, const LlmBuffers &b) {
+                      _Float16 *kc, _Float16 *vc, const LlmBuffers &b) {
     switch (G) {
-        case 1: hipLaunchKernelGGL((k_attention<HD, 1>), grid, dim3(ATT_NT), 0, s, d, qn, kn, kc, vc, pf, b); break;
-        case 2: hipLaunchKernelGGL((k_attention<HD, 2>), grid, dim3(ATT_NT), 0, s, d, qn, kn, kc, vc, pf, b); break;
-        case 3: hipLaunchKernelGGL((k_attention<HD, 3>), grid, dim3(ATT_NT), 0, s, d, qn, kn, kc, vc, pf, b); break;
-        case 4: hipLaunchKernelGGL((k_attention<HD, 4>), grid, dim3(ATT_NT), 0, s, d, qn, kn, kc, vc, pf, b); break;
-        case 8: hipLaunchKernelGGL((k_attention<HD, 8>), grid, dim3(ATT_NT), 0, s, d, qn, kn, kc, vc, pf, b); break;
+        case 1: hipLaunchKernelGGL((k_attention<HD, 1>), grid, dim3(ATT_NT), 0, s, d, qn, kn, kc, vc, b); break;
+        case 2: hipLaunchKernelGGL((k_attention<HD, 2>), grid, dim3(ATT_NT), 0, s, d, qn, kn, kc, vc, b); break;
+        case 3: hipLaunchKernelGGL((k_attention<HD, 3>), grid, dim3(ATT_NT), 0, s, d, qn, kn, kc, vc, b); break;
+        case 4: hipLaunchKernelGGL((k_attention<HD, 4>), grid, dim3(ATT_NT), 0, s, d, qn, kn, kc, vc, b); break;
+        case 8: hipLaunchKernelGGL((k_attention<HD, 8>), grid, dim3(ATT_NT), 0, s, d, qn, kn, kc, vc, b); break;
         default: break;
     }
 }
@@ -380,7 +363,7 @@ __global__ __launch_bounds__(ST) void k_sample(LlmDims d, QMat emb, int nblk, Ll
         if (v > best || (v == best && ix < bi)) best = v, bi = ix;
     }
     if (lane == 0) bs_[wave] = best, bi_[wave] = bi;
-    __syncthreads();
+    lds_barrier();
     if (tid == 0) {
         for (int w = 1; w < ST / 64; ++w)
             if (bs_[w] > best || (bs_[w] == best && bi_[w] < bi)) best = bs_[w], bi = bi_[w];
@@ -389,10 +372,10 @@ __global__ __launch_bounds__(ST) void k_sample(LlmDims d, QMat emb, int nblk, Ll
         if (sc.force && step < sc.n_force && sc.force[step] >= 0) tok = sc.force[step];
         tok_s = tok;
     }
-    __syncthreads();
+    lds_barrier();
     const int tok = tok_s;
     MIO_TRACE(b, 1);
-    MIO_TL_MARK(b, 1);
+    MIO_TL_MARK1(b);
     embed_row(emb, tok, d.n_embd, b.x);
     MIO_TL_END(b);
     MIO_TRACE(b, 15);
@@ -430,35 +413,7 @@ void launch_embed_token(const LlmDims &d, const QMat &tok_embd, const LlmBuffers
     hipLaunchKernelGGL(k_embed, dim3(1), dim3(ST), 0, s, d, tok_embd, b);
 }
 
-inline size_t mv_lds(int K) { return pf_offset(smem_bytes(K)) + PF_LDS; }
-
-// what launch `which` of layer il prefetches: the next matvec launch's rows
-Prefetch prefetch_plan(int which, const LlmDims &d, const LayerW *layers, int il, const QMat &lm) {
-    Prefetch p{};
-    p.cap = 0xFFFFFFFFu;
-    auto qkv = [&](const LayerW &L) {
-        p.mode = 3;
-        p.m[0] = L.wq, p.m[1] = L.wk, p.m[2] = L.wv;
-        attn_in_grid(d, L, p.grid, p.g_qk);
-    };
-    const LayerW &L = layers[il];
-    switch (which) {
-        case 0: p.mode = 1, p.m[0] = L.wo, p.grid = matvec_grid(d, L.wo.rows); break;
-        case 2: p.mode = 2, p.m[0] = L.gate, p.m[1] = L.up, p.grid = matvec_grid(d, L.gate.rows); break;
-        case 3: p.mode = 1, p.m[0] = L.down, p.grid = matvec_grid(d, L.down.rows); break;
-        case 4:
-            if (il + 1 < d.n_layer) {
-                qkv(layers[il + 1]);
-            } else {
-                p.mode = 1, p.m[0] = lm, p.grid = lm_head_blocks(d);
-                p.cap = 64u << 10;
-            }
-            break;
-        case 6: qkv(layers[0]); break;
-        default: p.mode = 0; break;
-    }
-    return p;
-}
+inline size_t mv_lds(int K) { return smem_bytes(K); }
 
 // Units (row passes) of the busiest wave of a matvec over `rows` rows on `grid` workgroups
 // (wave_range), and the single-group size that covers them (0 = streaming groups).
@@ -496,7 +451,6 @@ void launch_step_kernel(int which, const LlmDims &d, const LayerW *layers, int i
                         const LlmBuffers &b, hipStream_t s) {
     const size_t layer_kv = (size_t)d.n_kv * d.n_ctx * d.hd;
     const int G = d.n_head / d.n_kv;
-    const Prefetch pf = d.prefetch ? prefetch_plan(which, d, layers, il, lm) : Prefetch{};
     switch (which) {
         case 0: {
             const LayerW &L = layers[il];
@@ -510,7 +464,7 @@ void launch_step_kernel(int which, const LlmDims &d, const LayerW *layers, int i
                 auto go = [&]<int TV>() {
                     dispatch_su<NP>(pick_su(un, NP), [&]<int SU>() {
                         hipLaunchKernelGGL((k_attn_in<NP, TQ, TV, SU>), dim3(GW), dim3(MT), lds, s, d, L.attn_norm,
-                                           L.wq, L.wk, L.wv, g_qk, pf, b);
+                                           L.wq, L.wk, L.wv, g_qk, b);
                     });
                 };
                 if constexpr (TQ == 8) {
@@ -526,20 +480,11 @@ void launch_step_kernel(int which, const LlmDims &d, const LayerW *layers, int i
         }
         case 1: {
             const LayerW &L = layers[il];
-            // attention prefetch (d.att_prefetch): kAttPrefetchCols extra grid columns of
-            // workgroups sweep Wo, gate and up of this layer into the caches
-            Prefetch ap{};
-            if (d.att_prefetch) {
-                ap.mode = 4, ap.cap = 0xFFFFFFFFu;
-                ap.m[0] = L.wo, ap.m[1] = L.gate, ap.m[2] = L.up;
-            }
-            const dim3 grid(d.max_splits + (d.att_prefetch ? d.att_prefetch : 0), d.n_kv);
+            const dim3 grid(d.max_splits, d.n_kv);
             if (d.hd == 128)
-                launch_attention<128>(G, grid, s, d, L.q_norm, L.k_norm, kcache + il * layer_kv, vcache + il * layer_kv,
-                                      ap, b);
+                launch_attention<128>(G, grid, s, d, L.q_norm, L.k_norm, kcache + il * layer_kv, vcache + il * layer_kv, b);
             else
-                launch_attention<64>(G, grid, s, d, L.q_norm, L.k_norm, kcache + il * layer_kv, vcache + il * layer_kv,
-                                     ap, b);
+                launch_attention<64>(G, grid, s, d, L.q_norm, L.k_norm, kcache + il * layer_kv, vcache + il * layer_kv, b);
             break;
         }
         case 2: {
@@ -547,7 +492,7 @@ void launch_step_kernel(int which, const LlmDims &d, const LayerW *layers, int i
             const int grid = matvec_grid(d, L.wo.rows);
             dispatch_nt(L.wo.k, L.wo.type, [&]<int NP, int T>() {
                 dispatch_su<NP>(pick_su(max_wave_units(L.wo.rows, grid, NP, 1), NP), [&]<int SU>() {
-                    hipLaunchKernelGGL((k_attn_out<NP, T, SU>), dim3(grid), dim3(MT), mv_lds(L.wo.k), s, d, L.wo, pf, b);
+                    hipLaunchKernelGGL((k_attn_out<NP, T, SU>), dim3(grid), dim3(MT), mv_lds(L.wo.k), s, d, L.wo, b);
                 });
             });
             break;
@@ -558,7 +503,7 @@ void launch_step_kernel(int which, const LlmDims &d, const LayerW *layers, int i
             dispatch_nt(d.n_embd, L.gate.type, [&]<int NP, int T>() {
                 dispatch_su<NP>(pick_su(max_wave_units(L.gate.rows, grid, NP, 2), NP), [&]<int SU>() {
                     hipLaunchKernelGGL((k_ffn_in<NP, T, SU>), dim3(grid), dim3(MT), mv_lds(d.n_embd), s, d, L.ffn_norm,
-                                       L.gate, L.up, pf, b);
+                                       L.gate, L.up, b);
                 });
             });
             break;
@@ -569,7 +514,7 @@ void launch_step_kernel(int which, const LlmDims &d, const LayerW *layers, int i
             dispatch_nt(L.down.k, L.down.type, [&]<int NP, int T>() {
                 dispatch_su<NP>(pick_su(max_wave_units(L.down.rows, grid, NP, 1), NP), [&]<int SU>() {
                     hipLaunchKernelGGL((k_ffn_down<NP, T, SU>), dim3(grid), dim3(MT), mv_lds(L.down.k), s, d, L.down,
-                                       pf, b);
+                                       b);
                 });
             });
             break;
@@ -577,7 +522,7 @@ void launch_step_kernel(int which, const LlmDims &d, const LayerW *layers, int i
         case 6:
             dispatch_nt(d.n_embd, lm.type, [&]<int NP, int T>() {
                 hipLaunchKernelGGL((k_lm_head<NP, T>), dim3(lm_head_blocks(d)), dim3(MT), mv_lds(d.n_embd), s, d,
-                                   out_norm, lm, pf, b);
+                                   out_norm, lm, b);
             });
             break;
         case 7:

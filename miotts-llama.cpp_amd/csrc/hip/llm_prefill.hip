@@ -67,7 +67,7 @@ __device__ __forceinline__ void load_rows(const QMat W0, const QMat W1, int r, i
                                           int split) {
 #pragma unroll
     for (int ri = 0; ri < CfgB<NP, NM>::RU; ++ri) {
-        const int row = min(r + ri, hi - 1);
+        const int row = __builtin_amdgcn_readfirstlane(min(r + ri, hi - 1));  // wave-uniform
 #pragma unroll
         for (int m = 0; m < NM; ++m)
 #pragma unroll
@@ -245,7 +245,7 @@ __global__ __launch_bounds__(ATT_NT) void k_pf_attention(LlmDims d, const _Float
     const int QD = (d.n_head + 2 * d.n_kv) * HD;
     const float *qsrc = pb.qkv + (size_t)t * QD + (size_t)kvh * G * HD;
     for (int e = threadIdx.x; e < G * HD; e += ATT_NT) qs[e / HD][e % HD] = qsrc[e];
-    __syncthreads();
+    lds_barrier();
     attend_chunk<HD, G>(qs, kr, vr, t0, pos, d.scale, wres,
                         pb.part + (((size_t)t * d.n_head + kvh * G) * d.max_splits + ch) * C::REC,
                         (size_t)d.max_splits * C::REC);

@@ -397,7 +397,7 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
         }
         m->layers.push_back(L);
     }
-    // per-launch weight ranges (prefetch)
+    // per-launch weight ranges (trace_kernel cache-warm diagnostic)
     auto span = [&](const mio::QMat &a, const mio::QMat &z) {
         const mio::SplitLayout L = mio::split_layout(z.type, z.rows, z.k);
         return mio_hip_llm::Range{a.p0, (uint64_t)(z.p0 + L.bytes - a.p0)};
@@ -451,13 +451,6 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
         return fail(MIO_ERR_OOM);
     }
     hipMemcpy(dr, rope.data(), rope.size() * sizeof(float2), hipMemcpyHostToDevice);
-    // MIO_PREFETCH=1: matvec launches also sweep the next launch's rows into the caches
-    // (measured slower on MI355X: kept as an opt-in experiment)
-    D.prefetch = (getenv("MIO_PREFETCH") && getenv("MIO_PREFETCH")[0] == '1') ? 1 : 0;
-    // MIO_ATT_PREFETCH=N: N extra attention grid columns (x n_kv workgroups) sweep the layer's
-    // Wo / gate / up into the caches while the attention launch leaves HBM idle
-    D.att_prefetch = getenv("MIO_ATT_PREFETCH") ? atoi(getenv("MIO_ATT_PREFETCH")) : 0;
-    if (D.att_prefetch < 0 || D.att_prefetch > 64) D.att_prefetch = 0;
     m->buf.rope = dr;
     m->pf.rope = dr;
     *out = m;
@@ -671,7 +664,7 @@ extern "C" int mio_hip_llm_trace_kernel(mio_hip_llm *m, int which, uint64_t *out
 
 // Diagnostic: captures one decode step as a graph with the step timeline on, replays it
 // (advancing the decode state by 3 steps: reset/eval afterwards), and returns per launch
-// and workgroup {start, mark 1, mark 2, end} in s_memrealtime ticks (100 MHz).
+// and workgroup {start, marks 1-6, end} in s_memrealtime ticks (100 MHz).
 extern "C" int mio_hip_llm_timeline(mio_hip_llm *m, uint64_t *out, int max_launches, int *n_launches) {
     MIO_REQUIRE(m && out && n_launches && m->graph, MIO_ERR_INVALID, "llm_timeline: run generate/eval first");
     int rc = mio::bind(m->d);
@@ -679,7 +672,7 @@ extern "C" int mio_hip_llm_timeline(mio_hip_llm *m, uint64_t *out, int max_launc
     const int nl = m->n_layer * 5 + 2;
     MIO_REQUIRE(max_launches >= nl, MIO_ERR_INVALID, "llm_timeline: need %d launch slots", nl);
     hipStream_t s = m->d->stream;
-    const size_t nslot = (size_t)nl * 256 * 4;
+    const size_t nslot = (size_t)nl * 256 * 8;
     unsigned long long *tl = nullptr;
     MIO_HIP_CHECK(hipMalloc(&tl, sizeof(unsigned long long) * nslot));
     hipGraph_t g = nullptr;

@@ -412,13 +412,13 @@ class Llm:
         return out
 
     def timeline(self) -> np.ndarray:
-        """Per-launch, per-workgroup [start, mark 1, mark 2, end] (us from the step start, NaN =
+        """Per-launch, per-workgroup [start, marks 1-6, end] (us from the step start, NaN =
         absent) of one graph-replayed step (diagnostic, mio_hip_llm_timeline; advances the
         decode state). Marks: see MIO_TL_MARK in csrc/hip/llm_device.h."""
-        out = np.zeros(1024 * 256 * 4, np.uint64)
+        out = np.zeros(1024 * 256 * 8, np.uint64)
         n = ctypes.c_int(0)
         check(lib().mio_hip_llm_timeline(self.h, _ptr(out), 1024, ctypes.byref(n)))
-        t = out[: n.value * 1024].astype(np.float64).reshape(n.value, 256, 4)
+        t = out[: n.value * 2048].astype(np.float64).reshape(n.value, 256, 8)
         t[t == 0] = np.nan
         return (t - np.nanmin(t[0, :, 0])) * 0.01
 

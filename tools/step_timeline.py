@@ -27,13 +27,13 @@ nl = t.shape[0]
 names = ["attn_in", "attention", "attn_out", "ffn_in", "ffn_down"] * ((nl - 2) // 5) + ["lm_head", "sample"]
 s0 = np.nanmin(t[:, :, 0], axis=1)
 s1 = np.nanmax(t[:, :, 0], axis=1)
-e0 = np.nanmin(t[:, :, 3], axis=1)
-e1 = np.nanmax(t[:, :, 3], axis=1)
-wd = np.nanmedian(t[:, :, 3] - t[:, :, 0], axis=1)
+e0 = np.nanmin(t[:, :, 7], axis=1)
+e1 = np.nanmax(t[:, :, 7], axis=1)
+wd = np.nanmedian(t[:, :, 7] - t[:, :, 0], axis=1)
 # per-workgroup phases (median over workgroups): start -> mark 1 -> mark 2 -> end
 ph1 = np.nanmedian(t[:, :, 1] - t[:, :, 0], axis=1)
 ph2 = np.nanmedian(t[:, :, 2] - t[:, :, 1], axis=1)
-ph3 = np.nanmedian(t[:, :, 3] - t[:, :, 2], axis=1)
+ph3 = np.nanmedian(t[:, :, 7] - t[:, :, 2], axis=1)
 m2 = np.nanmax(t[:, :, 2], axis=1) - s0
 dur = e1 - s0
 gap = np.r_[0.0, s0[1:] - e1[:-1]]
@@ -45,3 +45,12 @@ for k in ["attn_in", "attention", "attn_out", "ffn_in", "ffn_down", "lm_head", "
     print(f"  {k:10s} {dur[idx].mean():6.2f} {gap[idx].mean():8.2f} {(s1 - s0)[idx].mean():12.2f} "
           f"{(e1 - e0)[idx].mean():11.2f} {wd[idx].mean():10.2f} {np.nanmean(ph1[idx]):9.2f} "
           f"{np.nanmean(ph2[idx]):7.2f} {np.nanmean(ph3[idx]):8.2f} {np.nanmean(m2[idx]):8.2f}")
+# every recorded mark (1-6) and the end, as median offsets from the workgroup's own start
+print("  kernel      " + " ".join(f"{'m' + str(k):>6s}" for k in range(1, 7)) + "    end   (us after workgroup start)")
+for k in ["attn_in", "attention", "attn_out", "ffn_in", "ffn_down", "lm_head", "sample"]:
+    idx = [i for i, n in enumerate(names) if n == k]
+    cols = []
+    for j in list(range(1, 7)) + [7]:
+        v = t[idx, :, j] - t[idx, :, 0]
+        cols.append(f"{np.nanmedian(v):6.2f}" if np.isfinite(v).any() else "     -")
+    print(f"  {k:10s}  " + " ".join(cols))
