@@ -35,19 +35,41 @@ namespace {
     do {                                                                                        \
         if ((bufs).tl && threadIdx.x == 0) MIO_TL_SLOT(bufs)[k] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
+#ifdef MIO_TL_DIAG
+// diagnostic builds: mark 6 = the LAST wave's first instruction (wave launch skew)
+#define MIO_TL_BEGIN(bufs)                                                                     \
+    do {                                                                                       \
+        MIO_TL_AT(bufs, 0);                                                                    \
+        if ((bufs).tl && threadIdx.x == blockDim.x - 64) MIO_TL_SLOT(bufs)[6] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#else
 #define MIO_TL_BEGIN(bufs) MIO_TL_AT(bufs, 0)
+#endif
+#ifdef MIO_TL_WAVES
+#define MIO_TL_MARK(bufs, k)
+#define MIO_TL_END(bufs)
+#else
 #define MIO_TL_MARK(bufs, k) MIO_TL_AT(bufs, k)
 #define MIO_TL_END(bufs) MIO_TL_AT(bufs, 7)
+#endif
 // -DMIO_TL_DIAG: the prologue helpers also stamp marks 3-5 (activation consumed, reduced,
 // staged; diagnostic builds only)
+// and mark 1 becomes wave MIO_DIAG_WAVE's "activation consumed" (wave skew)
+#ifndef MIO_DIAG_WAVE
+#define MIO_DIAG_WAVE 7
+#endif
 #ifdef MIO_TL_DIAG
 #define MIO_TL_DIAGSLOT(bufs) ((bufs).tl ? MIO_TL_SLOT(bufs) : nullptr)
+#define MIO_TL_MARK1(bufs)
 #else
 #define MIO_TL_DIAGSLOT(bufs) nullptr
-#endif
 #define MIO_TL_MARK1(bufs) MIO_TL_MARK(bufs, 1)
+#endif
 // stamp after value v is available (the empty asm consumes it; the timer read cannot move
 // above a volatile asm)
+#ifdef MIO_TL_WAVES
+#define MIO_DIAG_STAMP(diag, k, v)
+#else
 #define MIO_DIAG_STAMP(diag, k, v)                                                   \
     do {                                                                             \
         if ((diag) && threadIdx.x == 0) {                                            \
@@ -55,6 +77,7 @@ namespace {
             (diag)[k] = __builtin_amdgcn_s_memrealtime();                            \
         }                                                                            \
     } while (0)
+#endif
 
 constexpr int NT = 256;        // threads of the attention / sampler kernels
 constexpr int NWAVE = NT / 64;
@@ -310,7 +333,24 @@ __device__ void rmsnorm_quant(const XRegs<XV> &xr, int K, float eps, bool kquant
             acc += (double)(v.w * v.w);
         }
     }
+#ifdef MIO_TL_WAVES
+    // wave-arrival diagnostic: slot w = wave w's activation consumed (w = 1..7; slot 7
+    // replaces the end mark)
+    if (diag && (threadIdx.x & 63) == 0 && threadIdx.x > 0) {
+        asm volatile("" ::"v"(acc));
+        diag[threadIdx.x >> 6] = __builtin_amdgcn_s_memrealtime();
+    }
+    if (diag && threadIdx.x == 0) {
+        asm volatile("" ::"v"(acc));
+        diag[0] = __builtin_amdgcn_s_memrealtime() - 0;  // wave 0 stays the start reference
+    }
+#else
     MIO_DIAG_STAMP(diag, 3, acc);  // activation consumed (arrived)
+    if (diag && threadIdx.x == MIO_DIAG_WAVE * 64) {  // ... by wave MIO_DIAG_WAVE (default: the last)
+        asm volatile("" ::"v"(acc));
+        diag[1] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
     const double tot = block_sum(acc, s.red);
     MIO_DIAG_STAMP(diag, 4, tot);  // reduced over the workgroup
     const float mean = (float)(tot / K);
@@ -330,7 +370,6 @@ __device__ void rmsnorm_quant(const XRegs<XV> &xr, int K, float eps, bool kquant
     lds_barrier();
     MIO_DIAG_STAMP(diag, 5, scale);  // normalized activation staged in LDS
     quantize(s.xs, K, kquant, s.a);
-    MIO_DIAG_STAMP(diag, 6, scale);  // quantized
 }
 
 template <int XV>
@@ -922,110 +961,131 @@ __device__ __forceinline__ void load_kv_rows(const _Float16 *kbase, const _Float
     }
 }
 
-// Online softmax of the G query heads qs (LDS, prepared) over the chunk's positions
-// [t0, min(t0 + ATT_CHUNK, pos + 1)) whose K/V rows are in kr/vr (ggml soft_max semantics up
-// to summation order), then the slots' merge: lanes (permlane / bpermute butterflies), waves
-// (LDS). Writes the chunk's partial record {O[HD], m, l} of head g to dst + g * g_stride.
+// Softmax attention of the G query heads qs (LDS, prepared) over the chunk's positions
+// [t0, min(t0 + ATT_CHUNK, pos + 1)) whose K/V rows are in kr/vr, in two passes like ggml's
+// soft_max (scores, chunk max, exp, sums; summation order aside): every slot's scores are
+// independent dot products, the max is exchanged once (lanes by butterflies, waves by LDS),
+// and the slots' sums then merge by plain adds (no online rescaling). Writes the chunk's
+// partial record {O[HD] = sum_t p_t v_t, m = chunk max, l = sum_t p_t} of head g to
+// dst + g * g_stride (p_t = exp(s_t - m)).
 template <int HD, int G>
 __device__ void attend_chunk(const float (*qs)[HD], const h8 (&kr)[AttCfg<HD>::IT], const h8 (&vr)[AttCfg<HD>::IT],
                              int t0, int pos, float scale, float (*wres)[G][HD + 2], float *dst, size_t g_stride,
                              unsigned long long *trace = nullptr, unsigned long long *diag = nullptr) {
-    // diagnostic checkpoints (mio_hip_llm_trace_kernel): 3 sweep done, 4 lane merge, 5 wave merge
-    auto mark = [&](int k) {
+    constexpr int LP = AttCfg<HD>::LP, NS = AttCfg<HD>::NS, IT = AttCfg<HD>::IT;
+    __shared__ float wmax[ATT_NW][G];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int lp = lane % LP, sl = tid / LP;
+    auto mark = [&](int k) {  // checkpoints of mio_hip_llm_trace_kernel (diagnostic)
         if (trace && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
             asm volatile("" ::: "memory");
             trace[k] = __builtin_readcyclecounter();
         }
     };
-    constexpr int LP = AttCfg<HD>::LP, NS = AttCfg<HD>::NS, IT = AttCfg<HD>::IT;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int lp = lane % LP, sl = tid / LP;
     float qv[G][8];
 #pragma unroll
     for (int g = 0; g < G; ++g)
 #pragma unroll
         for (int i = 0; i < 8; ++i) qv[g][i] = qs[g][lp * 8 + i];
-    float m[G], l[G], acc[G][8];
+    // pass 1: scores (valid positions <= pos) and this thread's running max per head
+    float sc[IT][G], mx[G];
 #pragma unroll
-    for (int g = 0; g < G; ++g) {
-        m[g] = -INFINITY, l[g] = 0.0f;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) acc[g][i] = 0.0f;
-    }
+    for (int g = 0; g < G; ++g) mx[g] = -INFINITY;
 #pragma unroll
     for (int it = 0; it < IT; ++it) {
         const bool valid = t0 + sl + NS * it <= pos;
-        float kf[8], vf[8];
+        float kf[8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) kf[i] = (float)kr[it][i], vf[i] = (float)vr[it][i];
+        for (int i = 0; i < 8; ++i) kf[i] = (float)kr[it][i];
 #pragma unroll
         for (int g = 0; g < G; ++g) {
             float sdot = 0.0f;
 #pragma unroll
             for (int i = 0; i < 8; ++i) sdot = fmaf(qv[g][i], kf[i], sdot);
             sdot = group_sum<LP>(sdot);
-            const float sc = valid ? sdot * scale : -INFINITY;
-            const float mn = fmaxf(m[g], sc);
-            const float c = m[g] == mn ? 1.0f : expf(m[g] - mn);
-            const float p = valid ? expf(sc - mn) : 0.0f;
-            l[g] = l[g] * c + p;
-#pragma unroll
-            for (int i = 0; i < 8; ++i) acc[g][i] = acc[g][i] * c + p * vf[i];
-            m[g] = mn;
+            sc[it][g] = valid ? sdot * scale : -INFINITY;
+            mx[g] = fmaxf(mx[g], sc[it][g]);
         }
     }
+    // chunk max: slots of the wave (butterflies), then the waves (LDS)
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        if constexpr (LP <= 8) mx[g] = fmaxf(mx[g], xor_lane<8>(mx[g]));
+        mx[g] = fmaxf(mx[g], xor_lane<16>(mx[g]));
+        mx[g] = fmaxf(mx[g], xor_lane<32>(mx[g]));
+    }
+    if (lane == 0)
+#pragma unroll
+        for (int g = 0; g < G; ++g) wmax[wave][g] = mx[g];
+    lds_barrier();
+    float M[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        M[g] = wmax[0][g];
+#pragma unroll
+        for (int w = 1; w < ATT_NW; ++w) M[g] = fmaxf(M[g], wmax[w][g]);
+    }
     mark(3);
-    MIO_DIAG_STAMP(diag, 3, acc[0][0]);  // sweep done
-    // merge the wave's slots (lane stride LP): every lane of a butterfly pair ends bitwise equal
-    auto merge_step = [&](auto xl) {
+    MIO_DIAG_STAMP(diag, 3, M[0]);  // scores and chunk max done
+    // pass 2: p = exp(s - M), sums of p and of p * v (the chunk holds position t0 <= pos,
+    // so M is finite)
+    float l[G], acc[G][8];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        l[g] = 0.0f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[g][i] = 0.0f;
+    }
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+        float vf[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) vf[i] = (float)vr[it][i];
 #pragma unroll
         for (int g = 0; g < G; ++g) {
-            const float m2 = xl(m[g]), l2 = xl(l[g]);
-            const float mn = fmaxf(m[g], m2);
-            const float c1 = m[g] == -INFINITY ? 0.0f : expf(m[g] - mn);
-            const float c2 = m2 == -INFINITY ? 0.0f : expf(m2 - mn);
-            l[g] = l[g] * c1 + l2 * c2;
+            const float p = sc[it][g] == -INFINITY ? 0.0f : expf(sc[it][g] - M[g]);
+            l[g] += p;
 #pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                const float a2 = xl(acc[g][i]);
-                acc[g][i] = acc[g][i] * c1 + a2 * c2;
-            }
-            m[g] = mn;
+            for (int i = 0; i < 8; ++i) acc[g][i] = fmaf(p, vf[i], acc[g][i]);
+        }
+    }
+    // slots of the wave: plain sums (every lane of a butterfly pair ends bitwise equal)
+    auto sum_step = [&](auto xl) {
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            l[g] += xl(l[g]);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) acc[g][i] += xl(acc[g][i]);
         }
     };
-    if constexpr (LP <= 8) merge_step([](float v) { return xor_lane<8>(v); });
-    merge_step([](float v) { return xor_lane<16>(v); });
-    merge_step([](float v) { return xor_lane<32>(v); });
+    if constexpr (LP <= 8) sum_step([](float v) { return xor_lane<8>(v); });
+    sum_step([](float v) { return xor_lane<16>(v); });
+    sum_step([](float v) { return xor_lane<32>(v); });
     mark(4);
-    MIO_DIAG_STAMP(diag, 4, acc[0][0]);  // lane merges done
+    MIO_DIAG_STAMP(diag, 4, acc[0][0]);  // wave sums done
     if (lane < LP) {
 #pragma unroll
         for (int g = 0; g < G; ++g) {
 #pragma unroll
             for (int i = 0; i < 8; ++i) wres[wave][g][lp * 8 + i] = acc[g][i];
-            if (lp == 0) wres[wave][g][HD] = m[g], wres[wave][g][HD + 1] = l[g];
+            if (lp == 0) wres[wave][g][HD] = l[g];
         }
     }
     lds_barrier();
     mark(5);
     MIO_DIAG_STAMP(diag, 5, 0);  // wave results in LDS
-    // merge the waves -> this chunk's partial record per q head
+    // the waves -> this chunk's partial record per q head
     for (int e = tid; e < G * HD; e += ATT_NT) {
         const int g = e / HD, dd = e - g * HD;
-        float M = -INFINITY;
-#pragma unroll
-        for (int w = 0; w < ATT_NW; ++w) M = fmaxf(M, wres[w][g][HD]);
-        float L = 0.0f, O = 0.0f;
+        float O = 0.0f, L = 0.0f;
 #pragma unroll
         for (int w = 0; w < ATT_NW; ++w) {
-            const float mw = wres[w][g][HD];
-            const float c = mw == -INFINITY ? 0.0f : expf(mw - M);
-            L += c * wres[w][g][HD + 1];
-            O += c * wres[w][g][dd];
+            O += wres[w][g][dd];
+            L += wres[w][g][HD];
         }
         float *o = dst + g * g_stride;
         o[dd] = O;
-        if (dd == 0) o[HD] = M, o[HD + 1] = L;
+        if (dd == 0) o[HD] = M[g], o[HD + 1] = L;
     }
 }
 }  // namespace

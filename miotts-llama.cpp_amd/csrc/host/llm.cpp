@@ -109,7 +109,8 @@ float *upload_f32(mio_hip_llm *m, const mio::GgufTensor *t, int64_t n) {
         mio::set_error("llm: norm tensor %s missing or not f32[%lld]", t ? t->name.c_str() : "?", (long long)n);
         return nullptr;
     }
-    float *p = dalloc<float>(m, n);
+    const auto it = m->arena_off.find(t->name);
+    float *p = (m->arena && it != m->arena_off.end()) ? (float *)(m->arena + it->second) : dalloc<float>(m, n);
     if (p) hipMemcpy(p, t->data, n * 4, hipMemcpyHostToDevice);
     m->weight_bytes += n * 4;
     return p;
@@ -335,14 +336,25 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
             for (const char *n : mats) order.push_back("blk." + std::to_string(i) + "." + n + ".weight");
         order.push_back("output.weight");
         order.push_back("token_embd.weight");
+        // then every f32 norm vector (kept out of many small allocations: one large mapping
+        // serves all of them)
+        static const char *norms[] = {"attn_norm", "ffn_norm", "attn_q_norm", "attn_k_norm"};
+        for (int i = 0; i < m->n_layer; ++i)
+            for (const char *n : norms) order.push_back("blk." + std::to_string(i) + "." + n + ".weight");
+        order.push_back("output_norm.weight");
         size_t total = 0;
         for (const std::string &n : order) {
             const mio::GgufTensor *t = g.tensor(n);
-            if (!t || t->n_dims != 2) continue;
-            const mio::SplitLayout L = mio::split_layout(t->type, t->ne[1], t->ne[0]);
-            if (!L.bytes) continue;
+            if (!t) continue;
+            size_t bytes = 0;
+            if (t->n_dims == 2) {
+                bytes = mio::split_layout(t->type, t->ne[1], t->ne[0]).bytes;
+            } else if (t->type == mio::GGML_F32) {
+                bytes = (size_t)t->nelements() * 4;
+            }
+            if (!bytes) continue;
             m->arena_off[n] = total;
-            total += (L.bytes + 255) & ~(size_t)255;
+            total += (bytes + 255) & ~(size_t)255;
         }
         m->arena = dalloc<uint8_t>(m, total);
         if (!m->arena) {
@@ -415,23 +427,42 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
     const size_t kv = (size_t)m->n_layer * D.n_kv * n_ctx * D.hd;
     m->kc = dalloc<_Float16>(m, kv);
     m->vc = dalloc<_Float16>(m, kv);
-    m->buf.x = dalloc<float>(m, D.n_embd);
-    m->buf.qkv = dalloc<float>(m, qkv);
-    m->buf.h = dalloc<float>(m, D.n_ff);
-    m->buf.logits = dalloc<float>(m, D.n_vocab);
-    m->buf.part = dalloc<float>(m, (size_t)D.n_head * D.max_splits * (D.hd + 4));
-    m->buf.smp = dalloc<float>(m, 2 * mio::lm_head_blocks(D) + 16);
-    m->buf.st = dalloc<mio::StepState>(m, 1);
-    m->d_cfg = dalloc<mio::SampleCfg>(m, 1);
-    m->buf.cfg = m->d_cfg;
+    // every per-step buffer (activations, partials, state, token rings, RoPE table, prefill
+    // staging) is carved from ONE allocation: one large mapping instead of many small ones
+    // (the activation vectors are read by every CU at the start of every launch)
+    std::vector<std::pair<void **, size_t>> carve;
+    auto want = [&](auto *&ptr, size_t count) {
+        carve.push_back({reinterpret_cast<void **>(&ptr), count * sizeof(*ptr)});
+    };
+    float2 *dr = nullptr;
+    want(m->buf.x, D.n_embd);
+    want(m->buf.qkv, qkv);
+    want(m->buf.h, D.n_ff);
+    want(m->buf.logits, D.n_vocab);
+    want(m->buf.part, (size_t)D.n_head * D.max_splits * (D.hd + 4));
+    want(m->buf.smp, 2 * mio::lm_head_blocks(D) + 16);
+    want(m->buf.st, 1);
+    want(m->d_cfg, 1);
     m->max_steps = n_ctx;
-    m->d_tokens = dalloc<int>(m, m->max_steps);
-    m->d_force = dalloc<int>(m, m->max_steps);
-    m->d_prompt = dalloc<int>(m, n_ctx);
-    m->pf.x = dalloc<float>(m, (size_t)mio::kPrefillB * D.n_embd);
-    m->pf.qkv = dalloc<float>(m, (size_t)mio::kPrefillB * qkv);
-    m->pf.h = dalloc<float>(m, (size_t)mio::kPrefillB * D.n_ff);
-    m->pf.part = dalloc<float>(m, (size_t)mio::kPrefillB * D.n_head * D.max_splits * (D.hd + 4));
+    want(m->d_tokens, m->max_steps);
+    want(m->d_force, m->max_steps);
+    want(m->d_prompt, n_ctx);
+    want(m->pf.x, (size_t)mio::kPrefillB * D.n_embd);
+    want(m->pf.qkv, (size_t)mio::kPrefillB * qkv);
+    want(m->pf.h, (size_t)mio::kPrefillB * D.n_ff);
+    want(m->pf.part, (size_t)mio::kPrefillB * D.n_head * D.max_splits * (D.hd + 4));
+    want(dr, (size_t)n_ctx * (D.hd / 2));
+    size_t io_bytes = 0;
+    for (auto &c : carve) io_bytes += (c.second + 255) & ~(size_t)255;
+    uint8_t *io = dalloc<uint8_t>(m, (io_bytes + (2u << 20) - 1) & ~(size_t)((2u << 20) - 1));
+    if (io) {
+        size_t off = 0;
+        for (auto &c : carve) {
+            *c.first = io + off;
+            off += (c.second + 255) & ~(size_t)255;
+        }
+    }
+    m->buf.cfg = m->d_cfg;
     m->pf.tokens = m->d_prompt;
     // RoPE table, ggml rope-cache recurrence (theta = p; theta *= base^(-2/hd) per pair)
     std::vector<float2> rope((size_t)n_ctx * (D.hd / 2));
@@ -443,7 +474,6 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
             theta *= theta_scale;
         }
     }
-    float2 *dr = dalloc<float2>(m, rope.size());
     if (!m->kc || !m->vc || !m->buf.x || !m->buf.qkv || !m->buf.h || !m->buf.logits ||
         !m->buf.part || !m->buf.smp || !m->buf.st || !m->d_cfg || !m->d_tokens || !m->d_force || !dr ||
         !m->d_prompt || !m->pf.x || !m->pf.qkv || !m->pf.h || !m->pf.part) {
