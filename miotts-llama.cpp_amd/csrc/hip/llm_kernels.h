@@ -86,10 +86,8 @@ void launch_prefill_chunk(const LlmDims &d, const LayerW *layers, int n_layer, _
                           _Float16 *vcache, const QMat &tok_embd, const PrefillBuffers &pb, int p0, int nt,
                           hipStream_t s);
 
-// Launch one decode step (all layers + head + sampler) on stream s.
-void launch_decode_step(const LlmDims &d, const LayerW *layers, int n_layer, _Float16 *kcache,
-                        _Float16 *vcache, const float *out_norm, const QMat &lm, const QMat &tok_embd,
-                        const LlmBuffers &b, hipStream_t s);
+// Launch one kernel of a decode step (which: 0 attn_in, 1 attention, 2 attn_out, 3 ffn_in,
+// 4 ffn_down of layer il; 6 lm_head, 7 sampler) on stream s.
 void launch_step_kernel(int which, const LlmDims &d, const LayerW *layers, int il, _Float16 *kcache,
                         _Float16 *vcache, const float *out_norm, const QMat &lm, const QMat &tok_embd,
                         const LlmBuffers &b, hipStream_t s);

@@ -532,14 +532,6 @@ void launch_step_kernel(int which, const LlmDims &d, const LayerW *layers, int i
     }
 }
 
-void launch_decode_step(const LlmDims &d, const LayerW *layers, int n_layer, _Float16 *kcache,
-                        _Float16 *vcache, const float *out_norm, const QMat &lm, const QMat &tok_embd,
-                        const LlmBuffers &b, hipStream_t s) {
-    for (int il = 0; il < n_layer; ++il)
-        for (int k = 0; k < 5; ++k) launch_step_kernel(k, d, layers, il, kcache, vcache, out_norm, lm, tok_embd, b, s);
-    launch_step_kernel(6, d, layers, 0, kcache, vcache, out_norm, lm, tok_embd, b, s);
-    launch_step_kernel(7, d, layers, 0, kcache, vcache, out_norm, lm, tok_embd, b, s);
-}
 
 // ------------------------------------------------------------------ parity entry point
 namespace {
