@@ -131,6 +131,14 @@ int mio_hip_llm_generate(mio_hip_llm *m, const int32_t *prompt, int n_prompt, in
                          int32_t eos0, int32_t eos1, int32_t check_interval,
                          int32_t *out_tokens, int *n_out);
 
+/* Decode engine of mio_hip_llm_generate / llm_run: mode 1 = the persistent launch (one
+ * kernel runs whole decode steps, csrc/hip/llm_persist.hip), 0 = one hipGraph of per-phase
+ * kernels per step (the default unless MIO_PERSIST=1; faster on MI355X);
+ * -1 = leave the mode unchanged (query). Both compute the same values bit for bit. *active (may be
+ * null) = 1 when the persistent launch has run for this model, 0 if its shape has no
+ * persistent instantiation (the graph path is used), -1 not yet tried. */
+int mio_hip_llm_set_decode_mode(mio_hip_llm *m, int mode, int *active);
+
 /* Live timing of one decode-step kernel (which: 0 attn_in, 1 attention, 2 attn_out,
  * 3 ffn_in, 4 ffn_down of layer n_layer/2; 6 lm_head): `iters` back-to-back launches on
  * the runner's stream between HIP events (state/buffers of the last generate/eval).
@@ -148,6 +156,11 @@ int mio_hip_llm_trace_kernel(mio_hip_llm *m, int which, uint64_t *out);
  * prologue steps in -DMIO_TL_DIAG builds.
  * Advances the decode state. */
 int mio_hip_llm_timeline(mio_hip_llm *m, uint64_t *out, int max_launches, int *n_launches);
+/* Diagnostic: one persistent decode step with its phase timeline (advances the decode
+ * state): out[(phase * n_wg + wg) * 8 + k] = s_memrealtime (100 MHz) at k = 0 body start,
+ * 1 prologue done, 2 body done, 3 arrived, 4 poll done, 5 inputs staged, 6 prefetch issued
+ * (0 = not recorded); 5 phases per layer, then lm_head and the sampler. */
+int mio_hip_llm_persist_timeline(mio_hip_llm *m, uint64_t *out, int max_phases, int *n_phases, int *n_wg);
 /* Stage times (ms, HIP events) of the last mio_hip_codec_decode_pcm: [0] codec, [1] iSTFT. */
 int mio_hip_codec_last_timings(const mio_hip_codec *c, float *ms2);
 

@@ -13,13 +13,20 @@
 
 #pragma clang fp contract(off)
 
+// Thread index used by every helper below. The persistent step (llm_persist.hip) defines it
+// as an opaque per-use value so the compiler cannot hoist each phase's lane-dependent
+// address arithmetic out of the step loop (hoisted, it stays live for the whole launch).
+#ifndef MIO_TIDX
+#define MIO_TIDX threadIdx.x
+#endif
+
 namespace mio {
 namespace {
 // Checkpoint timestamps (s_memtime) of workgroup 0 / thread 0, only when b.trace is set
 // (mio_hip_llm_trace_kernel); a uniform branch otherwise.
 #define MIO_TRACE(bufs, k)                                                                    \
     do {                                                                                      \
-        if ((bufs).trace && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {        \
+        if ((bufs).trace && blockIdx.x == 0 && blockIdx.y == 0 && MIO_TIDX == 0) {        \
             asm volatile("" ::: "memory");                                                    \
             (bufs).trace[k] = __builtin_readcyclecounter();                                   \
             if ((k) == 0 || (k) == 15) (bufs).trace[16 + (k)] = __builtin_amdgcn_s_memrealtime(); \
@@ -33,14 +40,14 @@ namespace {
 #define MIO_TL_SLOT(bufs) ((bufs).tl + 8 * ((size_t)(bufs).seq * 256 + ((blockIdx.x + blockIdx.y * gridDim.x) & 255)))
 #define MIO_TL_AT(bufs, k)                                                                      \
     do {                                                                                        \
-        if ((bufs).tl && threadIdx.x == 0) MIO_TL_SLOT(bufs)[k] = __builtin_amdgcn_s_memrealtime(); \
+        if ((bufs).tl && MIO_TIDX == 0) MIO_TL_SLOT(bufs)[k] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
 #ifdef MIO_TL_DIAG
 // diagnostic builds: mark 6 = the LAST wave's first instruction (wave launch skew)
 #define MIO_TL_BEGIN(bufs)                                                                     \
     do {                                                                                       \
         MIO_TL_AT(bufs, 0);                                                                    \
-        if ((bufs).tl && threadIdx.x == blockDim.x - 64) MIO_TL_SLOT(bufs)[6] = __builtin_amdgcn_s_memrealtime(); \
+        if ((bufs).tl && MIO_TIDX == blockDim.x - 64) MIO_TL_SLOT(bufs)[6] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
 #else
 #define MIO_TL_BEGIN(bufs) MIO_TL_AT(bufs, 0)
@@ -72,7 +79,7 @@ namespace {
 #else
 #define MIO_DIAG_STAMP(diag, k, v)                                                   \
     do {                                                                             \
-        if ((diag) && threadIdx.x == 0) {                                            \
+        if ((diag) && MIO_TIDX == 0) {                                            \
             asm volatile("" ::"v"(v));                                               \
             (diag)[k] = __builtin_amdgcn_s_memrealtime();                            \
         }                                                                            \
@@ -200,8 +207,8 @@ __device__ inline Smem carve(char *base, int K) {
 
 __device__ double block_sum(double v, double *red) {
     v = wave_sum_d(v);
-    const int nw = blockDim.x >> 6;
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    const int nw = MW;  // callers run 512-thread matvec workgroups (8 waves)
+    if ((MIO_TIDX & 63) == 0) red[MIO_TIDX >> 6] = v;
     lds_barrier();
     double t = 0.0;
     for (int w = 0; w < nw; ++w) t += red[w];
@@ -212,7 +219,7 @@ __device__ double block_sum(double v, double *red) {
 // quantize_row_q8_K_ref semantics (iscale = -127/max_signed with max_signed the first
 // element of largest |x|, nearest-even, clamp 127, bsums); reductions by DPP.
 __device__ void quant_q8k(const float *xs, int K, const ActL &a) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const int lane = MIO_TIDX & 63, wave = MIO_TIDX >> 6, nw = MW;
     for (int b = wave; b < K / 256; b += nw) {
         const float4 v4 = *reinterpret_cast<const float4 *>(xs + b * 256 + 4 * lane);
         const float v[4] = {v4.x, v4.y, v4.z, v4.w};
@@ -244,7 +251,7 @@ __device__ void quant_q8k(const float *xs, int K, const ActL &a) {
 
 // quantize_row_q8_0_ref semantics (d = amax/127 stored as f16, q = roundf(x * 1/d))
 __device__ void quant_q80(const float *xs, int K, const ActL &a) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const int lane = MIO_TIDX & 63, wave = MIO_TIDX >> 6, nw = MW;
     const int nb = K / 32;
     for (int b0 = wave * 8; b0 < nb; b0 += nw * 8) {
         const int b = b0 + (lane >> 3);
@@ -309,7 +316,7 @@ __device__ inline void load_x(const float *x, const float *w, int K, XRegs<XV> &
     const auto rw = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(w), 0, w ? K * 4 : 0, 0x00020000);
 #pragma unroll
     for (int i = 0; i < XV; ++i) {
-        const int e = (threadIdx.x + i * MT) * 4;
+        const int e = (MIO_TIDX + i * MT) * 4;
         const u32x4 a = __builtin_amdgcn_raw_buffer_load_b128(rx, e * 4, 0, 0);
         const u32x4 c = __builtin_amdgcn_raw_buffer_load_b128(rw, e * 4, 0, 0);
         xr.v[i] = make_float4(__uint_as_float(a.x), __uint_as_float(a.y), __uint_as_float(a.z), __uint_as_float(a.w));
@@ -324,7 +331,7 @@ __device__ void rmsnorm_quant(const XRegs<XV> &xr, int K, float eps, bool kquant
     double acc = 0.0;
 #pragma unroll
     for (int i = 0; i < XV; ++i) {
-        const int e = (threadIdx.x + i * MT) * 4;
+        const int e = (MIO_TIDX + i * MT) * 4;
         if (e < K) {
             const float4 v = xr.v[i];
             acc += (double)(v.x * v.x);
@@ -336,17 +343,17 @@ __device__ void rmsnorm_quant(const XRegs<XV> &xr, int K, float eps, bool kquant
 #ifdef MIO_TL_WAVES
     // wave-arrival diagnostic: slot w = wave w's activation consumed (w = 1..7; slot 7
     // replaces the end mark)
-    if (diag && (threadIdx.x & 63) == 0 && threadIdx.x > 0) {
+    if (diag && (MIO_TIDX & 63) == 0 && MIO_TIDX > 0) {
         asm volatile("" ::"v"(acc));
-        diag[threadIdx.x >> 6] = __builtin_amdgcn_s_memrealtime();
+        diag[MIO_TIDX >> 6] = __builtin_amdgcn_s_memrealtime();
     }
-    if (diag && threadIdx.x == 0) {
+    if (diag && MIO_TIDX == 0) {
         asm volatile("" ::"v"(acc));
         diag[0] = __builtin_amdgcn_s_memrealtime() - 0;  // wave 0 stays the start reference
     }
 #else
     MIO_DIAG_STAMP(diag, 3, acc);  // activation consumed (arrived)
-    if (diag && threadIdx.x == MIO_DIAG_WAVE * 64) {  // ... by wave MIO_DIAG_WAVE (default: the last)
+    if (diag && MIO_TIDX == MIO_DIAG_WAVE * 64) {  // ... by wave MIO_DIAG_WAVE (default: the last)
         asm volatile("" ::"v"(acc));
         diag[1] = __builtin_amdgcn_s_memrealtime();
     }
@@ -357,7 +364,7 @@ __device__ void rmsnorm_quant(const XRegs<XV> &xr, int K, float eps, bool kquant
     const float scale = 1.0f / sqrtf(mean + eps);
 #pragma unroll
     for (int i = 0; i < XV; ++i) {
-        const int e = (threadIdx.x + i * MT) * 4;
+        const int e = (MIO_TIDX + i * MT) * 4;
         if (e < K) {
             const float4 v = xr.v[i], ww = xr.w[i];
             float t;
@@ -377,7 +384,7 @@ __device__ inline void plain_quant(const XRegs<XV> &xr, int K, bool kquant, cons
                                    unsigned long long *diag = nullptr) {
 #pragma unroll
     for (int i = 0; i < XV; ++i) {
-        const int e = (threadIdx.x + i * MT) * 4;
+        const int e = (MIO_TIDX + i * MT) * 4;
         if (e < K) *reinterpret_cast<float4 *>(s.xs + e) = xr.v[i];
     }
     lds_barrier();
@@ -463,7 +470,7 @@ __device__ __forceinline__ uint32_t bld2(const uint8_t *base, uint32_t bytes, ui
 
 template <int T>
 __device__ __forceinline__ Frag load_frag(const QMat W, int row, int pass) {
-    const int lane = threadIdx.x & 63;
+    const int lane = MIO_TIDX & 63;
     // the row is wave-uniform; readfirstlane lets the compiler keep it (and the soffset) in
     // SGPRs - without it every load became a waterfall loop over a VGPR soffset
     const uint32_t R = (uint32_t)W.rows,
@@ -499,7 +506,7 @@ __device__ __forceinline__ Frag load_frag(const QMat W, int row, int pass) {
 
 template <int T>
 __device__ __forceinline__ ALane load_alane(const ActL &a, int K, int pass) {
-    const int lane = threadIdx.x & 63;
+    const int lane = MIO_TIDX & 63;
     ALane r;
     if constexpr (T == 12 || T == 14) {
         const int nsb = K >> 8, sb = pass * 8 + (lane >> 3), pc = lane & 7;
@@ -534,7 +541,7 @@ __device__ __forceinline__ ALane load_alane(const ActL &a, int K, int pass) {
 // Lanes whose superblock / block lies past K have zero codes and zero scales -> 0.
 template <int T>
 __device__ __forceinline__ float dot_frag(const Frag &f, const ALane &al, int K, int pass) {
-    const int lane = threadIdx.x & 63;
+    const int lane = MIO_TIDX & 63;
     if constexpr (T == 12) {
         const int jj = (lane & 7) >> 1;
         uint4 h;  // the superblock header {d|dmin, scale/min words} from the quad's four dwords
@@ -698,7 +705,7 @@ __device__ __forceinline__ void stream_rows(const QMat W0, const QMat W1, int lo
     };
     for (int u0 = 0;;) {
         consume(A, u0);
-        if (trace && u0 == 0 && blockIdx.x == 0 && threadIdx.x == 0) trace[3] = __builtin_readcyclecounter();
+        if (trace && u0 == 0 && blockIdx.x == 0 && MIO_TIDX == 0) trace[3] = __builtin_readcyclecounter();
         if constexpr (Cfg<NP, SU>::NG == 1) break;
         u0 += U;
         if (u0 >= n) break;
@@ -722,10 +729,21 @@ __device__ __forceinline__ void load_first(const QMat W0, const QMat W1, int lo,
 // Rows [0, R) over G workgroups: workgroup b owns [R*b/G, R*(b+1)/G), wave w a contiguous
 // eighth of that (wave-uniform, held in scalar registers). R*G < 2^31.
 __device__ inline void wave_range(int R, int &lo, int &hi, int b, int G) {
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int w = __builtin_amdgcn_readfirstlane(MIO_TIDX >> 6);
     const int ra = (R * b) / G, rb = (R * (b + 1)) / G;
     lo = ra + (rb - ra) * w / MW;
     hi = ra + (rb - ra) * (w + 1) / MW;
+}
+// the same over NW row waves: wave w (w0 <= w < w0 + NW) owns its share; other waves none
+__device__ inline void wave_range_n(int R, int &lo, int &hi, int b, int G, int w0, int NW) {
+    const int w = __builtin_amdgcn_readfirstlane(MIO_TIDX >> 6) - w0;
+    const int ra = (R * b) / G, rb = (R * (b + 1)) / G;
+    if (w < 0 || w >= NW) {
+        lo = hi = ra;
+        return;
+    }
+    lo = ra + (rb - ra) * w / NW;
+    hi = ra + (rb - ra) * (w + 1) / NW;
 }
 __device__ inline void wave_range(int R, int &lo, int &hi) { wave_range(R, lo, hi, blockIdx.x, gridDim.x); }
 
@@ -762,12 +780,12 @@ __device__ inline void embed_row(const QMat &emb, int tok, int n, float *x) {
     float v[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        const int e = threadIdx.x + i * ST;
+        const int e = MIO_TIDX + i * ST;
         v[i] = e < n ? dequant_elem(emb, tok, e) : 0.0f;
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        const int e = threadIdx.x + i * ST;
+        const int e = MIO_TIDX + i * ST;
         if (e < n) x[e] = v[i];
     }
 }
@@ -804,7 +822,7 @@ __device__ void merge_attention(const LlmDims &d, const float *part, int nch, in
     const int hd = d.hd, rec = part_rec(hd);
 #pragma unroll
     for (int i = 0; i < NP; ++i) {
-        const int e = (threadIdx.x + i * MT) * 4;
+        const int e = (MIO_TIDX + i * MT) * 4;
         if (e < K) {
             const int h = e / hd, dd = e - h * hd;
             const float *base = part + (size_t)h * d.max_splits * rec;
@@ -844,6 +862,21 @@ __device__ void merge_attention(const LlmDims &d, const float *part, int nch, in
 
 __device__ inline float silu_f(float x) { return x / (1.0f + expf(-x)); }
 
+__device__ inline uint64_t mix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+// same counter-based Gumbel noise as oracle/llm_ref.c mo_gumbel
+__device__ inline float gumbel(uint64_t seed, int step, int idx) {
+    const uint64_t h = mix64(seed ^ mix64(((uint64_t)(uint32_t)step << 32) | (uint32_t)idx));
+    const float u = ((float)(h >> 40) + 0.5f) * (1.0f / 16777216.0f);
+    return -logf(-logf(u));
+}
+
+
 
 // Calls f.template operator()<NP, T>() for the matrix's pass count and weight type.
 template <class F>
@@ -875,7 +908,7 @@ struct AttCfg {
 // value of lane ^ O (O = 16 or 32 by the gfx950 permlane swaps, VALU; smaller O by bpermute)
 template <int O>
 __device__ __forceinline__ float xor_lane(float v) {
-    const int lane = threadIdx.x & 63;
+    const int lane = MIO_TIDX & 63;
     if constexpr (O == 32) {
         const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
         return __uint_as_float(lane < 32 ? r[1] : r[0]);
@@ -894,7 +927,7 @@ __device__ __forceinline__ float xor_lane(float v) {
 template <int HD>
 __device__ void prep_head(const float *src, const float *nw, const float2 *rope, const LlmDims &d, float *row) {
     constexpr int PER = HD / 64;
-    const int lane = threadIdx.x & 63;
+    const int lane = MIO_TIDX & 63;
     float v[PER], w[PER];
     float2 cs[PER];
 #pragma unroll
@@ -948,16 +981,24 @@ __device__ void prep_head(const float *src, const float *nw, const float2 *rope,
 }
 
 // K/V rows of this thread's slot (positions t0 + sl + NS*it, clamped to pos), issued early.
-template <int HD>
+// SC1: device-coherent loads (the persistent step, whose own workgroup appended some of the
+// rows earlier in the same launch: never served from a CU-L1 line cached before the append)
+template <int HD, bool SC1 = false>
 __device__ __forceinline__ void load_kv_rows(const _Float16 *kbase, const _Float16 *vbase, int t0, int pos,
                                              h8 (&kr)[AttCfg<HD>::IT], h8 (&vr)[AttCfg<HD>::IT]) {
     constexpr int LP = AttCfg<HD>::LP, NS = AttCfg<HD>::NS;
-    const int lp = (threadIdx.x & 63) % LP, sl = threadIdx.x / LP;
+    const int lp = (MIO_TIDX & 63) % LP, sl = MIO_TIDX / LP;
 #pragma unroll
     for (int it = 0; it < AttCfg<HD>::IT; ++it) {
         const int t = min(t0 + sl + NS * it, pos);
-        kr[it] = *reinterpret_cast<const h8 *>(kbase + (size_t)t * HD + lp * 8);
-        vr[it] = *reinterpret_cast<const h8 *>(vbase + (size_t)t * HD + lp * 8);
+        if constexpr (SC1) {
+            const uint32_t off = (uint32_t)(((size_t)t * HD + lp * 8) * 2), bytes = (uint32_t)((size_t)(pos + 1) * HD * 2);
+            kr[it] = __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(rsrc(kbase, bytes), off, 0, 16));
+            vr[it] = __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(rsrc(vbase, bytes), off, 0, 16));
+        } else {
+            kr[it] = *reinterpret_cast<const h8 *>(kbase + (size_t)t * HD + lp * 8);
+            vr[it] = *reinterpret_cast<const h8 *>(vbase + (size_t)t * HD + lp * 8);
+        }
     }
 }
 
@@ -968,16 +1009,16 @@ __device__ __forceinline__ void load_kv_rows(const _Float16 *kbase, const _Float
 // and the slots' sums then merge by plain adds (no online rescaling). Writes the chunk's
 // partial record {O[HD] = sum_t p_t v_t, m = chunk max, l = sum_t p_t} of head g to
 // dst + g * g_stride (p_t = exp(s_t - m)).
-template <int HD, int G>
+template <int HD, int G, bool SC1 = false>
 __device__ void attend_chunk(const float (*qs)[HD], const h8 (&kr)[AttCfg<HD>::IT], const h8 (&vr)[AttCfg<HD>::IT],
                              int t0, int pos, float scale, float (*wres)[G][HD + 2], float *dst, size_t g_stride,
                              unsigned long long *trace = nullptr, unsigned long long *diag = nullptr) {
     constexpr int LP = AttCfg<HD>::LP, NS = AttCfg<HD>::NS, IT = AttCfg<HD>::IT;
     __shared__ float wmax[ATT_NW][G];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = MIO_TIDX, lane = tid & 63, wave = tid >> 6;
     const int lp = lane % LP, sl = tid / LP;
     auto mark = [&](int k) {  // checkpoints of mio_hip_llm_trace_kernel (diagnostic)
-        if (trace && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
+        if (trace && blockIdx.x == 0 && blockIdx.y == 0 && MIO_TIDX == 0) {
             asm volatile("" ::: "memory");
             trace[k] = __builtin_readcyclecounter();
         }
@@ -1084,8 +1125,16 @@ __device__ void attend_chunk(const float (*qs)[HD], const h8 (&kr)[AttCfg<HD>::I
             L += wres[w][g][HD];
         }
         float *o = dst + g * g_stride;
-        o[dd] = O;
-        if (dd == 0) o[HD] = M[g], o[HD + 1] = L;
+        if constexpr (SC1) {  // handed to other workgroups inside a persistent launch
+            __hip_atomic_store(o + dd, O, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (dd == 0) {
+                __hip_atomic_store(o + HD, M[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(o + HD + 1, L, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        } else {
+            o[dd] = O;
+            if (dd == 0) o[HD] = M[g], o[HD + 1] = L;
+        }
     }
 }
 }  // namespace

@@ -86,6 +86,23 @@ void launch_prefill_chunk(const LlmDims &d, const LayerW *layers, int n_layer, _
                           _Float16 *vcache, const QMat &tok_embd, const PrefillBuffers &pb, int p0, int nt,
                           hipStream_t s);
 
+// Persistent decode (csrc/hip/llm_persist.hip): one launch runs n_steps whole decode steps
+// (every phase of every layer, lm_head, sampler, next embedding) on G workgroups, one per CU.
+struct PersistArgs {
+    LlmDims d;
+    const LayerW *layers;  // device copy [n_layer]
+    QMat lm, tok;
+    const float *out_norm;
+    _Float16 *kc, *vc;
+    LlmBuffers b;
+    unsigned *ctl;  // hand-off words: [8 shards x 32] arrival counters, [256] error; zeroed per launch
+    int n_steps;
+    unsigned long long *tl;  // optional diagnostic phase timeline [phase][G][8]
+};
+size_t persist_ctl_bytes();
+// 0 = launched; 1 = no instantiation for this shape / grid (use the graph path); 2 = HIP error
+int launch_persist(const PersistArgs &a, int G, hipStream_t s);
+
 // Launch one kernel of a decode step (which: 0 attn_in, 1 attention, 2 attn_out, 3 ffn_in,
 // 4 ffn_down of layer il; 6 lm_head, 7 sampler) on stream s.
 void launch_step_kernel(int which, const LlmDims &d, const LayerW *layers, int il, _Float16 *kcache,

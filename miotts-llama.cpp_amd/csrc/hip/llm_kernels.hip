@@ -169,20 +169,6 @@ __global__ __launch_bounds__(MT) void k_ffn_down(LlmDims d, QMat down, LlmBuffer
     MIO_TRACE(b, 15);
 }
 
-__device__ inline uint64_t mix64(uint64_t x) {
-    x += 0x9E3779B97F4A7C15ull;
-    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
-    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
-    return x ^ (x >> 31);
-}
-
-// same counter-based Gumbel noise as oracle/llm_ref.c mo_gumbel
-__device__ inline float gumbel(uint64_t seed, int step, int idx) {
-    const uint64_t h = mix64(seed ^ mix64(((uint64_t)(uint32_t)step << 32) | (uint32_t)idx));
-    const float u = ((float)(h >> 40) + 0.5f) * (1.0f / 16777216.0f);
-    return -logf(-logf(u));
-}
-
 // final RMSNorm (once per CU) + logits + per-workgroup Gumbel-max partial. A wave's rows
 // (<= 128) are parked one per lane (two registers) and the noise is drawn for 64 rows at
 // a time after the stream.

@@ -48,6 +48,11 @@ struct mio_hip_llm {
     // one step, and kGraphSteps steps back to back (fewer graph launches per token)
     hipGraphExec_t graph = nullptr, graph_n = nullptr;
     mio::SampleCfg *d_cfg = nullptr;
+    // persistent decode (llm_persist.hip): layer table on the device, hand-off words
+    mio::LayerW *d_layers = nullptr;
+    unsigned *d_ctl = nullptr;
+    int persist = -1;  // -1 untried, 0 unavailable for this shape (graph path), 1 in use
+    int persist_on = -1;  // mio_hip_llm_set_decode_mode (-1: MIO_PERSIST default)
     // generation state
     int n_prompt = 0, max_new = 0, steps_total = 0, steps_issued = 0;
     mio::SampleCfg cfg{};
@@ -244,6 +249,36 @@ int llm_begin(mio_hip_llm *m, const int32_t *prompt, int n_prompt, int max_new, 
     return set_state(m, P, prompt[P], P);
 }
 
+// MIO_PERSIST=1: decode with the persistent launch by default (mio_hip_llm_set_decode_mode
+// selects per model). Off by default: measured slower than the graph path on MI355X
+// (profiles/r01_persist_timeline.txt: in-launch hand-offs queue behind the prefetched weight
+// stream, ~9 us per phase against ~6 us per launch + boundary).
+bool persist_enabled() {
+    static const bool on = getenv("MIO_PERSIST") && getenv("MIO_PERSIST")[0] == '1';
+    return on;
+}
+
+// n decode steps as ONE persistent launch (llm_persist.hip); 1 = shape not instantiated
+int run_persistent(mio_hip_llm *m, int n, unsigned long long *tl = nullptr) {
+    mio::PersistArgs a{};
+    a.tl = tl;
+    a.d = m->dims;
+    a.layers = m->d_layers;
+    a.lm = m->lm, a.tok = m->tok;
+    a.out_norm = m->out_norm;
+    a.kc = m->kc, a.vc = m->vc;
+    a.b = m->buf;
+    a.ctl = m->d_ctl;
+    a.n_steps = n;
+    const int r = mio::launch_persist(a, m->dims.n_wg, m->d->stream);
+    if (r == 2) {
+        mio::set_error("llm: persistent decode launch failed: %s", hipGetErrorString(hipGetLastError()));
+        return MIO_ERR_HIP;
+    }
+    if (r == 0) MIO_HIP_CHECK(hipGetLastError());
+    return r;
+}
+
 int llm_run(mio_hip_llm *m, int n_steps) {
     int rc = mio::bind(m->d);
     if (rc) return rc;
@@ -257,6 +292,16 @@ int llm_run(mio_hip_llm *m, int n_steps) {
             if ((rc = issue_step(m))) return rc;
         return MIO_OK;
     }
+    const bool want = m->persist_on < 0 ? persist_enabled() : m->persist_on == 1;
+    if (n > 0 && m->persist != 0 && want) {
+        rc = run_persistent(m, n);
+        if (rc == 0) {
+            m->persist = 1;
+            return MIO_OK;
+        }
+        if (rc != 1) return rc;
+        m->persist = 0;  // no instantiation for this shape: graph path from now on
+    }
     for (; n >= kGraphSteps; n -= kGraphSteps) MIO_HIP_CHECK(hipGraphLaunch(m->graph_n, m->d->stream));
     for (; n > 0; --n) MIO_HIP_CHECK(hipGraphLaunch(m->graph, m->d->stream));
     return MIO_OK;
@@ -266,8 +311,15 @@ int llm_poll(mio_hip_llm *m, std::vector<int32_t> &out, bool *done) {
     int rc = mio::bind(m->d);
     if (rc) return rc;
     StepState st{};
+    unsigned herr = 0;
     MIO_HIP_CHECK(hipMemcpyAsync(&st, m->buf.st, sizeof(st), hipMemcpyDeviceToHost, m->d->stream));
+    if (m->persist == 1)
+        MIO_HIP_CHECK(hipMemcpyAsync(&herr, m->d_ctl + 256, 4, hipMemcpyDeviceToHost, m->d->stream));
     MIO_HIP_CHECK(hipStreamSynchronize(m->d->stream));
+    if (herr) {
+        mio::set_error("llm: persistent decode hand-off timed out (workgroups not co-resident?)");
+        return MIO_ERR_HIP;
+    }
     const int first = m->n_prompt - 1;
     const int n = st.step > first ? st.step - first : 0;
     out.resize(n);
@@ -440,7 +492,7 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
     want(m->buf.h, D.n_ff);
     want(m->buf.logits, D.n_vocab);
     want(m->buf.part, (size_t)D.n_head * D.max_splits * (D.hd + 4));
-    want(m->buf.smp, 2 * mio::lm_head_blocks(D) + 16);
+    want(m->buf.smp, 2 * std::max(mio::lm_head_blocks(D), D.n_wg) + 16);
     want(m->buf.st, 1);
     want(m->d_cfg, 1);
     m->max_steps = n_ctx;
@@ -482,6 +534,13 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
     }
     hipMemcpy(dr, rope.data(), rope.size() * sizeof(float2), hipMemcpyHostToDevice);
     m->buf.rope = dr;
+    m->d_layers = dalloc<mio::LayerW>(m, m->layers.size());
+    m->d_ctl = (unsigned *)dalloc<uint8_t>(m, mio::persist_ctl_bytes());
+    if (!m->d_layers || !m->d_ctl) {
+        mio::set_error("llm_load: device allocation failed");
+        return fail(MIO_ERR_OOM);
+    }
+    hipMemcpy(m->d_layers, m->layers.data(), m->layers.size() * sizeof(mio::LayerW), hipMemcpyHostToDevice);
     m->pf.rope = dr;
     *out = m;
     return MIO_OK;
@@ -494,6 +553,13 @@ extern "C" int mio_hip_llm_info(const mio_hip_llm *m, int *info) {
     mio::LlmInfo i = mio::llm_info(m);
     info[0] = i.n_vocab, info[1] = i.n_embd, info[2] = i.n_layer, info[3] = i.n_head;
     info[4] = i.n_kv, info[5] = i.head_dim, info[6] = i.n_ff, info[7] = i.n_ctx;
+    return MIO_OK;
+}
+
+extern "C" int mio_hip_llm_set_decode_mode(mio_hip_llm *m, int mode, int *active) {
+    MIO_REQUIRE(m && mode >= -1 && mode <= 1, MIO_ERR_INVALID, "llm_set_decode_mode: bad args");
+    if (mode >= 0) m->persist_on = mode;
+    if (active) *active = m->persist;
     return MIO_OK;
 }
 
@@ -689,6 +755,31 @@ extern "C" int mio_hip_llm_trace_kernel(mio_hip_llm *m, int which, uint64_t *out
     MIO_HIP_CHECK(hipStreamSynchronize(s));
     hipFree(dt);
     if (flush) hipFree(flush);
+    return MIO_OK;
+}
+
+// Diagnostic: ONE persistent decode step with the phase timeline on (advances the decode
+// state by one step): out[(phase * G + wg) * 8 + k], s_memrealtime ticks (100 MHz), k = 0 body
+// start, 1 prologue done, 2 body done, 3 arrived, 4 poll done, 5 staged, 6 prefetch issued.
+extern "C" int mio_hip_llm_persist_timeline(mio_hip_llm *m, uint64_t *out, int max_phases, int *n_phases, int *n_wg) {
+    MIO_REQUIRE(m && out && n_phases && n_wg, MIO_ERR_INVALID, "llm_persist_timeline: null");
+    int rc = mio::bind(m->d);
+    if (rc) return rc;
+    const int np = m->n_layer * 5 + 2, G = m->dims.n_wg;
+    MIO_REQUIRE(max_phases >= np, MIO_ERR_INVALID, "llm_persist_timeline: need %d phase slots", np);
+    const size_t nslot = (size_t)np * G * 8;
+    unsigned long long *tl = nullptr;
+    MIO_HIP_CHECK(hipMalloc(&tl, sizeof(unsigned long long) * nslot));
+    MIO_HIP_CHECK(hipMemsetAsync(tl, 0, sizeof(unsigned long long) * nslot, m->d->stream));
+    rc = mio::run_persistent(m, 1, tl);
+    if (rc == 0) {
+        MIO_HIP_CHECK(hipMemcpyAsync(out, tl, sizeof(unsigned long long) * nslot, hipMemcpyDeviceToHost, m->d->stream));
+        MIO_HIP_CHECK(hipStreamSynchronize(m->d->stream));
+    }
+    hipFree(tl);
+    MIO_REQUIRE(rc == 0, MIO_ERR_UNSUPPORTED, "llm_persist_timeline: no persistent instantiation");
+    *n_phases = np;
+    *n_wg = G;
     return MIO_OK;
 }
 
