@@ -205,38 +205,57 @@ __device__ inline Smem carve(char *base, int K) {
     return s;
 }
 
+// Workgroup sum (8 waves). No trailing barrier: every caller writes `red` again only
+// after a later workgroup barrier (rmsnorm_quant's staging barrier).
 __device__ double block_sum(double v, double *red) {
     v = wave_sum_d(v);
-    const int nw = MW;  // callers run 512-thread matvec workgroups (8 waves)
     if ((MIO_TIDX & 63) == 0) red[MIO_TIDX >> 6] = v;
     lds_barrier();
     double t = 0.0;
-    for (int w = 0; w < nw; ++w) t += red[w];
-    lds_barrier();
+#pragma unroll
+    for (int w = 0; w < MW; ++w) t += red[w];
     return t;
 }
 
 // quantize_row_q8_K_ref semantics (iscale = -127/max_signed with max_signed the first
-// element of largest |x|, nearest-even, clamp 127, bsums); reductions by DPP.
+// element of largest |x|, nearest-even, clamp 127, bsums). One superblock per wave and
+// pass (4 values per lane), NI passes (K <= NI * 2048) unrolled so their reduction chains
+// interleave. Largest |x| by DPP; its first position by a ballot of the lanes holding it
+// (the lowest such lane, the lowest of its 4 values) - the signed value comes straight from
+// that lane's register.
+template <int NI>
 __device__ void quant_q8k(const float *xs, int K, const ActL &a) {
-    const int lane = MIO_TIDX & 63, wave = MIO_TIDX >> 6, nw = MW;
-    for (int b = wave; b < K / 256; b += nw) {
-        const float4 v4 = *reinterpret_cast<const float4 *>(xs + b * 256 + 4 * lane);
-        const float v[4] = {v4.x, v4.y, v4.z, v4.w};
-        const float am = wave_max_f(fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))), 0.0f);
+    const int lane = MIO_TIDX & 63, wave = MIO_TIDX >> 6;
+    const int nsb = K >> 8;
+    float v[NI][4], am[NI];
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+        const int b = wave + MW * j;
+        float4 v4 = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (b < nsb) v4 = *reinterpret_cast<const float4 *>(xs + b * 256 + 4 * lane);
+        v[j][0] = v4.x, v[j][1] = v4.y, v[j][2] = v4.z, v[j][3] = v4.w;
+    }
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+        am[j] = wave_max_f(fmaxf(fmaxf(fabsf(v[j][0]), fabsf(v[j][1])), fmaxf(fabsf(v[j][2]), fabsf(v[j][3]))), 0.0f);
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+        const int b = wave + MW * j;
+        if (b >= nsb) break;
         int q[4] = {0, 0, 0, 0};
         float dd = 0.0f;
-        if (am > 0.0f) {
-            int first = INT_MAX;
+        if (am[j] > 0.0f) {
+            float sel = 0.0f;
+            bool has = false;
 #pragma unroll
             for (int i = 3; i >= 0; --i)
-                if (fabsf(v[i]) == am) first = 4 * lane + i;
-            const int ai = wave_min_i(first);
-            const float mx = xs[b * 256 + ai];
+                if (fabsf(v[j][i]) == am[j]) sel = v[j][i], has = true;
+            const int src = __builtin_ctzll(__ballot(has));
+            const float mx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sel), src));
             const float iscale = -127.f / mx;
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                const int t = (int)rintf(iscale * v[i]);
+                const int t = (int)rintf(iscale * v[j][i]);
                 q[i] = t < 127 ? t : 127;
             }
             dd = 1.0f / iscale;
@@ -249,12 +268,15 @@ __device__ void quant_q8k(const float *xs, int K, const ActL &a) {
     }
 }
 
-// quantize_row_q8_0_ref semantics (d = amax/127 stored as f16, q = roundf(x * 1/d))
+// quantize_row_q8_0_ref semantics (d = amax/127 stored as f16, q = roundf(x * 1/d)); 8
+// blocks per wave and pass, NI passes unrolled
+template <int NI>
 __device__ void quant_q80(const float *xs, int K, const ActL &a) {
-    const int lane = MIO_TIDX & 63, wave = MIO_TIDX >> 6, nw = MW;
+    const int lane = MIO_TIDX & 63, wave = MIO_TIDX >> 6;
     const int nb = K / 32;
-    for (int b0 = wave * 8; b0 < nb; b0 += nw * 8) {
-        const int b = b0 + (lane >> 3);
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+        const int b = wave * 8 + MW * 8 * j + (lane >> 3);
         const bool ok = b < nb;
         float v[4];
         float am = 0.0f;
@@ -277,11 +299,13 @@ __device__ void quant_q80(const float *xs, int K, const ActL &a) {
     }
 }
 
+// K <= NI * 2048
+template <int NI>
 __device__ inline void quantize(const float *xs, int K, bool kquant, const ActL &a) {
     if (kquant)
-        quant_q8k(xs, K, a);
+        quant_q8k<NI>(xs, K, a);
     else
-        quant_q80(xs, K, a);
+        quant_q80<NI>(xs, K, a);
     lds_barrier();
 }
 
@@ -360,7 +384,8 @@ __device__ void rmsnorm_quant(const XRegs<XV> &xr, int K, float eps, bool kquant
 #endif
     const double tot = block_sum(acc, s.red);
     MIO_DIAG_STAMP(diag, 4, tot);  // reduced over the workgroup
-    const float mean = (float)(tot / K);
+    // ggml: mean = sum / ne00 in double; a power-of-two K divides exactly by a multiply
+    const float mean = (float)((K & (K - 1)) == 0 ? tot * (1.0 / K) : tot / K);
     const float scale = 1.0f / sqrtf(mean + eps);
 #pragma unroll
     for (int i = 0; i < XV; ++i) {
@@ -376,7 +401,7 @@ __device__ void rmsnorm_quant(const XRegs<XV> &xr, int K, float eps, bool kquant
     }
     lds_barrier();
     MIO_DIAG_STAMP(diag, 5, scale);  // normalized activation staged in LDS
-    quantize(s.xs, K, kquant, s.a);
+    quantize<XV>(s.xs, K, kquant, s.a);
 }
 
 template <int XV>
@@ -389,7 +414,7 @@ __device__ inline void plain_quant(const XRegs<XV> &xr, int K, bool kquant, cons
     }
     lds_barrier();
     MIO_DIAG_STAMP(diag, 5, 0);  // activation arrived and staged in LDS
-    quantize(s.xs, K, kquant, s.a);
+    quantize<XV>(s.xs, K, kquant, s.a);
 }
 
 // ------------------------------------------------------------------ typed row dots
@@ -857,7 +882,7 @@ __device__ void merge_attention(const LlmDims &d, const float *part, int nch, in
     }
     lds_barrier();
     MIO_DIAG_STAMP(diag, 5, 0);  // chunks merged, staged in LDS
-    quantize(s.xs, K, kquant, s.a);
+    quantize<NP>(s.xs, K, kquant, s.a);
 }
 
 __device__ inline float silu_f(float x) { return x / (1.0f + expf(-x)); }

@@ -135,7 +135,7 @@ __device__ void merge_attention_sc1(const LlmDims &d, const float *part, int nch
         }
     }
     lds_barrier();
-    quantize(s.xs, K, kquant, s.a);
+    quantize<NP>(s.xs, K, kquant, s.a);
 }
 
 // Ends the live range of a register group without code: the next phase's groups are loaded
