@@ -53,6 +53,8 @@ def parse_args():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-tokens", type=int, default=12)
     p.add_argument("--cpu-codes", type=int, default=40)
+    p.add_argument("--batch", type=int, default=8,
+                   help="also time B utterances decoded together per GPU (N=1 only; 0 = skip)")
     return p.parse_args()
 
 
@@ -106,6 +108,34 @@ def cpu_baseline(llm_path, codec_path, voice_path, n_tok, n_codes, utt_tokens):
             "kind": "port",
             "sample": f"oracle decode of {n_tok} tokens ({t_tok * 1e3:.1f} ms/token) + codec+iSTFT of "
                       f"{n_codes} codes ({t_code * 1e3:.2f} ms/code), extrapolated to {utt_tokens} tokens"}
+
+
+def batched_line(a, llm, codec, dev, prompt, allow, d_emb, d_pcm):
+    """B utterances per GPU decoded together (mio_hip_llm_generate_batch: one weight pass per
+    step for all B), then each through MioCodec + iSTFT into HBM. Reported beside `value`
+    (which stays the single-utterance workload BASELINE's metric is quoted on)."""
+    import numpy as np
+    import miotts_amd as m
+    B = a.batch
+    seeds = [utterance_seed(0, 5000 + b) for b in range(B)]
+    llm.generate_batch([prompt] * B, a.tokens, 0.8, seeds, allow=allow)  # warm (graph capture)
+    dev.sync()
+    t0 = time.perf_counter()
+    outs = llm.generate_batch([prompt] * B, a.tokens, 0.8, seeds, allow=allow, check_interval=64)
+    t1 = time.perf_counter()
+    samples = 0
+    for toks in outs:
+        d_codes = dev.upload((toks - m.SYNTH_SPEECH0).astype(np.int32))
+        samples += codec.decode_pcm_device(d_codes, len(toks), d_emb, d_pcm)
+    dev.sync()
+    t2 = time.perf_counter()
+    if any(len(t) != a.tokens for t in outs):
+        raise RuntimeError("batched utterance ended early")
+    wall = t2 - t0
+    return {"utterances": B, "value": round(samples / codec.sample_rate / wall, 3),
+            "unit": "x realtime (audio s / wall s), aggregate of the B utterances on one GPU",
+            "llm_ms": round((t1 - t0) * 1e3, 3), "llm_ms_per_step": round((t1 - t0) * 1e3 / a.tokens, 4),
+            "codec_istft_ms": round((t2 - t1) * 1e3, 3), "wall_ms": round(wall * 1e3, 3)}
 
 
 def utterance_seed(rank: int, index: int) -> int:
@@ -261,6 +291,8 @@ def main():
         "value_pcie_inclusive": round(value_pcie, 3),
         "cpu_baseline": None,
     }
+    if world == 1 and a.batch > 0:
+        out["batched"] = batched_line(a, llm, codec, dev, prompt, allow, d_emb, d_pcm)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(llm_path, codec_path, voice_path, a.cpu_tokens, a.cpu_codes, a.tokens)
     if rank == 0:

@@ -130,6 +130,17 @@ int mio_hip_llm_generate(mio_hip_llm *m, const int32_t *prompt, int n_prompt, in
                          float temperature, uint64_t seed, int32_t allow_lo, int32_t allow_hi,
                          int32_t eos0, int32_t eos1, int32_t check_interval,
                          int32_t *out_tokens, int *n_out);
+/* B independent run_llm calls (test-to-speech.cpp:94-199, one per utterance in the
+ * reference) decoded together on this device: every step streams the weights once for all
+ * B streams (1 <= B <= 16). prompts = the B prompts concatenated, prompt_lens[B]; stream b
+ * uses seeds[b] and returns its tokens in out_tokens[b * max_tokens ...], n_out[b] of them
+ * (stopping before an end token as mio_hip_llm_generate does). Each stream's tokens equal
+ * mio_hip_llm_generate of its prompt with its seed. Uses its own KV caches (B x the model's),
+ * allocated on first use. */
+int mio_hip_llm_generate_batch(mio_hip_llm *m, const int32_t *prompts, const int32_t *prompt_lens, int B,
+                               int max_tokens, float temperature, const uint64_t *seeds, int32_t allow_lo,
+                               int32_t allow_hi, int32_t eos0, int32_t eos1, int32_t check_interval,
+                               int32_t *out_tokens, int32_t *n_out);
 
 /* Decode engine of mio_hip_llm_generate / llm_run: mode 1 = the persistent launch (one
  * kernel runs whole decode steps, csrc/hip/llm_persist.hip), 0 = one hipGraph of per-phase

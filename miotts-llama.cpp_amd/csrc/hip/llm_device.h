@@ -857,11 +857,19 @@ __device__ void merge_attention(const LlmDims &d, const float *part, int nch, in
             for (int c0 = 0; c0 < nch; c0 += CB) {
                 float2 ml[CB];
                 float4 oc[CB];
+                // only the batch's real chunks are loaded (every vector load instruction costs
+                // the CU's address path the same, used or not); a missing chunk is
+                // {m = -inf, l = 0, O = 0}, which leaves the max and the sums unchanged
 #pragma unroll
                 for (int j = 0; j < CB; ++j) {
-                    const int c = min(c0 + j, nch - 1);
-                    ml[j] = *reinterpret_cast<const float2 *>(base + (size_t)c * rec + hd);
-                    oc[j] = *reinterpret_cast<const float4 *>(base + (size_t)c * rec + dd);
+                    const int c = c0 + j;
+                    if (c < nch) {
+                        ml[j] = *reinterpret_cast<const float2 *>(base + (size_t)c * rec + hd);
+                        oc[j] = *reinterpret_cast<const float4 *>(base + (size_t)c * rec + dd);
+                    } else {
+                        ml[j] = make_float2(-INFINITY, 0.0f);
+                        oc[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+                    }
                 }
                 float mb = M;
 #pragma unroll

@@ -72,19 +72,47 @@ struct LlmBuffers {
 // test-to-speech.cpp:132-148); K/V rows are written, no logits are produced.
 constexpr int kPrefillB = 16;
 
+// The same multi-token engine runs the batched decode step of B independent utterances
+// (one token of each per step, weights streamed once for all of them).
 struct PrefillBuffers {
     float *x;            // [kPrefillB][n_embd] residual streams
     float *qkv;          // [kPrefillB][(H + 2 Hkv) hd]; q rows are RoPE'd in place
     float *h;            // [kPrefillB][n_ff]
     float *part;         // [kPrefillB][H][max_splits][hd + 4] attention chunk partials
     const float2 *rope;  // [n_ctx][hd/2]
-    const int *tokens;   // device prompt ids (token of position p at tokens[p])
+    const int *tokens;   // device token ids (embedded token t of a chunk at tokens[p0 + t])
+    const int *pos;      // position of token t: pos[t * pos_stride] (device-resident)
+    const int *seq;      // sequence (KV cache) of token t: seq[t * seq_stride]
+    int pos_stride, seq_stride;
+    size_t seq_kv;       // K (and V) cache elements per sequence: [seq][layer][kv head][n_ctx][hd]
 };
 
-// Prefill of positions [p0, p0 + nt), nt <= kPrefillB: embedding, all layers, K/V rows.
+// One chunk of nt <= kPrefillB tokens (ids at tokens[p0 + t], positions/sequences from
+// pb.pos / pb.seq) through every layer: embedding, K/V rows, residual streams in pb.x.
+// n_chunks = attention chunks to sweep (>= max position / kAttChunk + 1).
 void launch_prefill_chunk(const LlmDims &d, const LayerW *layers, int n_layer, _Float16 *kcache,
                           _Float16 *vcache, const QMat &tok_embd, const PrefillBuffers &pb, int p0, int nt,
-                          hipStream_t s);
+                          int n_chunks, hipStream_t s);
+
+// Batched decode of B <= kPrefillB utterances (mio_hip_llm_generate_batch): per sequence b,
+// state st[b], sampling cfg[b] (cfg[b].out_tokens = its token ring), logits [B][n_vocab],
+// sampler partials smp [B][lm blocks][2]; the residual streams are pb.x[b].
+struct BatchBuffers {
+    StepState *st;
+    const SampleCfg *cfg;
+    float *logits;
+    float *smp;
+};
+// One decode step of all B sequences: every layer with one weight pass per launch, the
+// lm_head for all B, then per-sequence sampling + next embedding + state advance.
+void launch_batch_step(const LlmDims &d, const LayerW *layers, int n_layer, _Float16 *kcache, _Float16 *vcache,
+                       const float *out_norm, const QMat &lm, const QMat &tok_embd, const PrefillBuffers &pb,
+                       const BatchBuffers &bb, int B, hipStream_t s);
+// B streams fit one batched step (B <= kPrefillB and the lm_head's LDS)
+bool batch_supported(const LlmDims &d, int B);
+// Embedding of st[b].token into pb.x[b] for every sequence (decode start).
+void launch_batch_embed(const LlmDims &d, const QMat &tok_embd, const PrefillBuffers &pb, const BatchBuffers &bb,
+                        int B, hipStream_t s);
 
 // Persistent decode (csrc/hip/llm_persist.hip): one launch runs n_steps whole decode steps
 // (every phase of every layer, lm_head, sampler, next embedding) on G workgroups, one per CU.

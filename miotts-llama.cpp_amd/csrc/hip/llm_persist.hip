@@ -109,13 +109,18 @@ __device__ void merge_attention_sc1(const LlmDims &d, const float *part, int nch
                 float4 oc[CB];
 #pragma unroll
                 for (int j = 0; j < CB; ++j) {
-                    const int c = min(c0 + j, nch - 1);
-                    const uint32_t r = base + (uint32_t)(c * rec) * 4;
-                    const auto m2 = __builtin_amdgcn_raw_buffer_load_b64(rp, r + hd * 4, 0, AUX_SC1);
-                    ml[j] = make_float2(__uint_as_float(m2[0]), __uint_as_float(m2[1]));
-                    const u32x4 o4 = __builtin_amdgcn_raw_buffer_load_b128(rp, r + dd * 4, 0, AUX_SC1);
-                    oc[j] = make_float4(__uint_as_float(o4.x), __uint_as_float(o4.y), __uint_as_float(o4.z),
-                                        __uint_as_float(o4.w));
+                    const int c = c0 + j;
+                    if (c < nch) {
+                        const uint32_t r = base + (uint32_t)(c * rec) * 4;
+                        const auto m2 = __builtin_amdgcn_raw_buffer_load_b64(rp, r + hd * 4, 0, AUX_SC1);
+                        ml[j] = make_float2(__uint_as_float(m2[0]), __uint_as_float(m2[1]));
+                        const u32x4 o4 = __builtin_amdgcn_raw_buffer_load_b128(rp, r + dd * 4, 0, AUX_SC1);
+                        oc[j] = make_float4(__uint_as_float(o4.x), __uint_as_float(o4.y), __uint_as_float(o4.z),
+                                            __uint_as_float(o4.w));
+                    } else {
+                        ml[j] = make_float2(-INFINITY, 0.0f);
+                        oc[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+                    }
                 }
                 float mb = M;
 #pragma unroll

@@ -19,6 +19,8 @@
 // bit (tests/test_llm_gpu.py::test_batched_prefill_matches_sequential).
 #include "llm_device.h"
 
+#include <vector>
+
 #pragma clang fp contract(off)
 
 namespace mio {
@@ -198,10 +200,12 @@ __global__ __launch_bounds__(MT) void k_pf_attn_in(LlmDims d, const float *norm_
 // (prep_head: the decode step's head preparation).
 template <int HD>
 __global__ __launch_bounds__(64) void k_pf_rope(LlmDims d, const float *q_norm, const float *k_norm, _Float16 *kc,
-                                                _Float16 *vc, PrefillBuffers pb, int p0) {
+                                                _Float16 *vc, PrefillBuffers pb) {
     constexpr int PER = HD / 64;
     __shared__ float row[HD];
-    const int hh = blockIdx.x, t = blockIdx.y, pos = p0 + t, lane = threadIdx.x;
+    const int hh = blockIdx.x, t = blockIdx.y, lane = threadIdx.x;
+    const int pos = pb.pos[t * pb.pos_stride];
+    const size_t kvo = (size_t)pb.seq[t * pb.seq_stride] * pb.seq_kv;
     const int QD = (d.n_head + 2 * d.n_kv) * HD;
     const bool isk = hh >= d.n_head;
     const int kvh = hh - d.n_head;
@@ -217,8 +221,8 @@ __global__ __launch_bounds__(64) void k_pf_rope(LlmDims d, const float *q_norm, 
 #pragma unroll
         for (int i = 0; i < PER; ++i) src[lane + 64 * i] = row[lane + 64 * i];
     } else {
-        _Float16 *kd = kc + ((size_t)kvh * d.n_ctx + pos) * HD;
-        _Float16 *vd = vc + ((size_t)kvh * d.n_ctx + pos) * HD;
+        _Float16 *kd = kc + kvo + ((size_t)kvh * d.n_ctx + pos) * HD;
+        _Float16 *vd = vc + kvo + ((size_t)kvh * d.n_ctx + pos) * HD;
 #pragma unroll
         for (int i = 0; i < PER; ++i) {
             const int p = lane + 64 * i;
@@ -229,19 +233,22 @@ __global__ __launch_bounds__(64) void k_pf_rope(LlmDims d, const float *q_norm, 
 }
 
 // One workgroup per (128-position chunk, kv head, token): causal online softmax over the
-// chunk's positions <= the token's position, all rows read from the cache (this chunk's own
-// rows were written by k_pf_rope); attend_chunk is the decode step's sweep.
+// chunk's positions <= the token's position in the token's own sequence, all rows read from
+// the cache (this launch's own rows were written by k_pf_rope); attend_chunk is the decode
+// step's sweep. Chunks past the token's position exit at once.
 template <int HD, int G>
 __global__ __launch_bounds__(ATT_NT) void k_pf_attention(LlmDims d, const _Float16 *kc, const _Float16 *vc,
-                                                         PrefillBuffers pb, int p0) {
+                                                         PrefillBuffers pb) {
     using C = AttCfg<HD>;
     __shared__ float qs[G][HD];
     __shared__ float wres[ATT_NW][G][HD + 2];
-    const int kvh = blockIdx.y, ch = blockIdx.x, t = blockIdx.z, pos = p0 + t;
+    const int kvh = blockIdx.y, ch = blockIdx.x, t = blockIdx.z;
+    const int pos = pb.pos[t * pb.pos_stride];
     const int t0 = ch * ATT_CHUNK;
     if (t0 > pos) return;
+    const size_t kvo = (size_t)pb.seq[t * pb.seq_stride] * pb.seq_kv + (size_t)kvh * d.n_ctx * HD;
     h8 kr[C::IT], vr[C::IT];
-    load_kv_rows<HD>(kc + (size_t)kvh * d.n_ctx * HD, vc + (size_t)kvh * d.n_ctx * HD, t0, pos, kr, vr);
+    load_kv_rows<HD>(kc + kvo, vc + kvo, t0, pos, kr, vr);
     const int QD = (d.n_head + 2 * d.n_kv) * HD;
     const float *qsrc = pb.qkv + (size_t)t * QD + (size_t)kvh * G * HD;
     for (int e = threadIdx.x; e < G * HD; e += ATT_NT) qs[e / HD][e % HD] = qsrc[e];
@@ -252,7 +259,7 @@ __global__ __launch_bounds__(ATT_NT) void k_pf_attention(LlmDims d, const _Float
 }
 
 template <int NP, int T>
-__global__ __launch_bounds__(MT) void k_pf_attn_out(LlmDims d, QMat wo, PrefillBuffers pb, int p0, int nt, int rpw) {
+__global__ __launch_bounds__(MT) void k_pf_attn_out(LlmDims d, QMat wo, PrefillBuffers pb, int nt, int rpw) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int K = wo.k, E = d.n_embd;
     int lo, hi;
@@ -264,7 +271,8 @@ __global__ __launch_bounds__(MT) void k_pf_attn_out(LlmDims d, QMat wo, PrefillB
     store_resid_b(xr, res, nt, rpw);
     const size_t tstride = (size_t)d.n_head * d.max_splits * part_rec(d.hd);
     for (int t = 0; t < nt; ++t)
-        merge_attention<NP>(d, pb.part + t * tstride, (p0 + t) / ATT_CHUNK + 1, K, T != 8, carve_t(smem, K, t));
+        merge_attention<NP>(d, pb.part + t * tstride, pb.pos[t * pb.pos_stride] / ATT_CHUNK + 1, K, T != 8,
+                            carve_t(smem, K, t));
     stream_rows_b<T, NP, 1>(wo, wo, lo, hi, ga, gb, smem, nt, [&](int row, int t, float v, float) {
         const float r = res[t * rpw + row - lo];
         if ((threadIdx.x & 63) == 0) pb.x[(size_t)t * E + row] = v + r;
@@ -316,27 +324,149 @@ __global__ __launch_bounds__(ST) void k_pf_embed(LlmDims d, QMat emb, PrefillBuf
     embed_row(emb, pb.tokens[p0 + t], d.n_embd, pb.x + (size_t)t * d.n_embd);
 }
 
+// ------------------------------------------------------------------ batched decode (B utterances)
+// lm_head of the B residual streams with ONE pass over the output matrix (final RMSNorm +
+// quantization per stream in the prologue, as k_lm_head does for one): logits[b][row] and,
+// per stream, this workgroup's Gumbel-max partial over its rows (the decode sampler's noise
+// gumbel(seed_b, step_b, row), so every stream draws exactly what a single-stream decode with
+// its seed draws). A wave's row values park in LDS (<= 128 rows per wave, host-checked).
+template <int NP, int T>
+__global__ __launch_bounds__(MT) void k_bt_lm_head(LlmDims d, const float *norm_w, QMat lm, PrefillBuffers pb,
+                                                   BatchBuffers bb, int nt) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    __shared__ float bs_[MW];
+    __shared__ int bi_[MW];
+    const int K = d.n_embd;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    XRegs<NP> xr;
+    load_x(pb.x, norm_w, K, xr);
+    int lo, hi;
+    wave_range(lm.rows, lo, hi);
+    Frag ga[CfgB<NP, 1>::U], gb[CfgB<NP, 1>::U];
+    load_first_b<T, NP, 1>(lm, lm, lo, hi, ga, gb);
+    prologue_rms(xr, pb.x, norm_w, K, d.eps, T != 8, smem, nt);
+    float *vals = reinterpret_cast<float *>(smem + pf_lds_bytes(K, nt, 0)) + (size_t)wave * nt * 128;
+    stream_rows_b<T, NP, 1>(lm, lm, lo, hi, ga, gb, smem, nt, [&](int row, int t, float v, float) {
+        if (lane == 0) vals[t * 128 + row - lo] = v;
+    });
+    lds_barrier();
+    for (int t = 0; t < nt; ++t) {
+        const SampleCfg sc = bb.cfg[t];
+        const int step = bb.st[t].step;
+        const uint64_t seed = ((uint64_t)sc.seed_hi << 32) | sc.seed_lo;
+        float best = -INFINITY;
+        int bi = INT_MAX;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int row = lo + lane + 64 * h;
+            if (row < hi) {
+                const float v = vals[t * 128 + row - lo];
+                bb.logits[(size_t)t * lm.rows + row] = v;
+                if (row >= sc.lo && row < sc.hi) {
+                    const float g = sc.temp > 0.0f ? v / sc.temp + gumbel(seed, step, row) : v;
+                    if (g > best || (g == best && row < bi)) best = g, bi = row;
+                }
+            }
+        }
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            const float ov = __shfl_xor(best, o);
+            const int oi = __shfl_xor(bi, o);
+            if (ov > best || (ov == best && oi < bi)) best = ov, bi = oi;
+        }
+        if (lane == 0) bs_[wave] = best, bi_[wave] = bi;
+        lds_barrier();
+        if (threadIdx.x == 0) {
+            for (int w = 1; w < MW; ++w)
+                if (bs_[w] > best || (bs_[w] == best && bi_[w] < bi)) best = bs_[w], bi = bi_[w];
+            float *o = bb.smp + ((size_t)t * gridDim.x + blockIdx.x) * 2;
+            o[0] = best;
+            o[1] = __int_as_float(bi);
+        }
+        lds_barrier();
+    }
+}
+
+// One workgroup per stream b: the lm_head partials -> the sampled token (k_sample's
+// selection rule), the token ring, end-token flag, the next embedding into pb.x[b], and the
+// state advance. A stream whose step budget (cfg.max_steps) is spent is frozen: nothing is
+// recorded and its position no longer advances.
+__global__ __launch_bounds__(ST) void k_bt_sample(LlmDims d, QMat emb, int nblk, PrefillBuffers pb,
+                                                  BatchBuffers bb) {
+    __shared__ float bs_[ST / 64];
+    __shared__ int bi_[ST / 64];
+    __shared__ int tok_s;
+    const int t = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const SampleCfg sc = bb.cfg[t];
+    StepState *st = bb.st + t;
+    const int step = st->step;
+    const float *smp = bb.smp + (size_t)t * nblk * 2;
+    float best = -INFINITY;
+    int bi = INT_MAX;
+    for (int i = tid; i < nblk; i += ST) {
+        const float v = smp[2 * i];
+        const int ix = __float_as_int(smp[2 * i + 1]);
+        if (v > best || (v == best && ix < bi)) best = v, bi = ix;
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        const float v = __shfl_xor(best, o);
+        const int ix = __shfl_xor(bi, o);
+        if (v > best || (v == best && ix < bi)) best = v, bi = ix;
+    }
+    if (lane == 0) bs_[wave] = best, bi_[wave] = bi;
+    lds_barrier();
+    if (tid == 0) {
+        for (int w = 1; w < ST / 64; ++w)
+            if (bs_[w] > best || (bs_[w] == best && bi_[w] < bi)) best = bs_[w], bi = bi_[w];
+        int tok = bi;
+        if (tok == INT_MAX) tok = sc.lo;
+        if (sc.force && step < sc.n_force && sc.force[step] >= 0) tok = sc.force[step];
+        tok_s = tok;
+    }
+    lds_barrier();
+    const int tok = tok_s;
+    const bool live = step < sc.max_steps;
+    if (live) embed_row(emb, tok, d.n_embd, pb.x + (size_t)t * d.n_embd);
+    if (tid == 0 && live) {
+        sc.out_tokens[step] = tok;
+        if (tok == sc.eos0 || tok == sc.eos1) st->done = 1;
+        st->token = tok;
+        st->pos = st->pos + 1;
+        st->step = step + 1;
+    }
+}
+
+__global__ __launch_bounds__(ST) void k_bt_embed(LlmDims d, QMat emb, PrefillBuffers pb, BatchBuffers bb) {
+    const int t = blockIdx.x;
+    embed_row(emb, bb.st[t].token, d.n_embd, pb.x + (size_t)t * d.n_embd);
+}
+
 template <int HD>
 void launch_pf_attention(int G, dim3 grid, hipStream_t s, const LlmDims &d, const _Float16 *kc, const _Float16 *vc,
-                         const PrefillBuffers &pb, int p0) {
+                         const PrefillBuffers &pb) {
     switch (G) {
-        case 1: hipLaunchKernelGGL((k_pf_attention<HD, 1>), grid, dim3(ATT_NT), 0, s, d, kc, vc, pb, p0); break;
-        case 2: hipLaunchKernelGGL((k_pf_attention<HD, 2>), grid, dim3(ATT_NT), 0, s, d, kc, vc, pb, p0); break;
-        case 3: hipLaunchKernelGGL((k_pf_attention<HD, 3>), grid, dim3(ATT_NT), 0, s, d, kc, vc, pb, p0); break;
-        case 4: hipLaunchKernelGGL((k_pf_attention<HD, 4>), grid, dim3(ATT_NT), 0, s, d, kc, vc, pb, p0); break;
-        case 8: hipLaunchKernelGGL((k_pf_attention<HD, 8>), grid, dim3(ATT_NT), 0, s, d, kc, vc, pb, p0); break;
+        case 1: hipLaunchKernelGGL((k_pf_attention<HD, 1>), grid, dim3(ATT_NT), 0, s, d, kc, vc, pb); break;
+        case 2: hipLaunchKernelGGL((k_pf_attention<HD, 2>), grid, dim3(ATT_NT), 0, s, d, kc, vc, pb); break;
+        case 3: hipLaunchKernelGGL((k_pf_attention<HD, 3>), grid, dim3(ATT_NT), 0, s, d, kc, vc, pb); break;
+        case 4: hipLaunchKernelGGL((k_pf_attention<HD, 4>), grid, dim3(ATT_NT), 0, s, d, kc, vc, pb); break;
+        case 8: hipLaunchKernelGGL((k_pf_attention<HD, 8>), grid, dim3(ATT_NT), 0, s, d, kc, vc, pb); break;
         default: break;
     }
 }
 
-// Dynamic LDS beyond the default 64 KB needs the per-kernel opt-in (once per instantiation).
+// Dynamic LDS beyond the default 64 KB needs the per-kernel opt-in (once per kernel; the
+// limit leaves room for the kernel's static LDS). Keyed by the kernel's address: kernels of
+// one signature share a function type.
+constexpr int LDS_DYN_MAX = LDS_MAX - 1024;
 template <class Kern>
 void allow_lds(Kern k) {
-    static bool done = false;
-    if (!done) {
-        hipFuncSetAttribute(reinterpret_cast<const void *>(k), hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
-        done = true;
-    }
+    static std::vector<const void *> done;
+    const void *p = reinterpret_cast<const void *>(k);
+    for (const void *q : done)
+        if (q == p) return;
+    hipFuncSetAttribute(p, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_DYN_MAX);
+    done.push_back(p);
 }
 
 // residual rows per wave of a matvec over `rows` rows on `grid` workgroups (wave_range)
@@ -348,7 +478,7 @@ int rows_per_wave(int rows, int grid) {
 // Largest token count per launch that fits LDS (and the two residual registers).
 int tokens_per_launch(int K, int nt, int rpw) {
     int n = nt;
-    while (n > 1 && (pf_lds_bytes(K, n, rpw) > (size_t)LDS_MAX || n * rpw > 128)) --n;
+    while (n > 1 && (pf_lds_bytes(K, n, rpw) > (size_t)LDS_DYN_MAX || n * rpw > 128)) --n;
     return n;
 }
 
@@ -358,18 +488,17 @@ PrefillBuffers shifted(const LlmDims &d, const PrefillBuffers &pb, int t) {
     q.qkv += (size_t)t * (d.n_head + 2 * d.n_kv) * d.hd;
     q.h += (size_t)t * d.n_ff;
     q.part += (size_t)t * d.n_head * d.max_splits * part_rec(d.hd);
+    q.pos += (size_t)t * pb.pos_stride;
+    q.seq += (size_t)t * pb.seq_stride;
     return q;
 }
 
-}  // namespace
-
-void launch_prefill_chunk(const LlmDims &d, const LayerW *layers, int n_layer, _Float16 *kcache,
-                          _Float16 *vcache, const QMat &tok_embd, const PrefillBuffers &pb, int p0, int nt,
-                          hipStream_t s) {
-    if (nt <= 0) return;
+// Every layer for nt tokens of pb (residual streams pb.x in, out): one weight pass per
+// matvec launch (sub-launches only where a token range does not fit LDS).
+void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16 *kcache, _Float16 *vcache,
+                   const PrefillBuffers &pb, int nt, int n_chunks, hipStream_t s) {
     const size_t layer_kv = (size_t)d.n_kv * d.n_ctx * d.hd;
     const int G = d.n_head / d.n_kv;
-    hipLaunchKernelGGL(k_pf_embed, dim3(nt), dim3(ST), 0, s, d, tok_embd, pb, p0);
     // sub-launches over token ranges that fit LDS: f(t_off, n, shifted buffers)
     auto over_tokens = [&](int K, int rpw, auto &&f) {
         const int per = tokens_per_launch(K, nt, rpw);
@@ -403,24 +532,24 @@ void launch_prefill_chunk(const LlmDims &d, const LayerW *layers, int n_layer, _
         {
             const dim3 grid(d.n_head + d.n_kv, nt);
             if (d.hd == 128)
-                hipLaunchKernelGGL((k_pf_rope<128>), grid, dim3(64), 0, s, d, L.q_norm, L.k_norm, kc, vc, pb, p0);
+                hipLaunchKernelGGL((k_pf_rope<128>), grid, dim3(64), 0, s, d, L.q_norm, L.k_norm, kc, vc, pb);
             else
-                hipLaunchKernelGGL((k_pf_rope<64>), grid, dim3(64), 0, s, d, L.q_norm, L.k_norm, kc, vc, pb, p0);
+                hipLaunchKernelGGL((k_pf_rope<64>), grid, dim3(64), 0, s, d, L.q_norm, L.k_norm, kc, vc, pb);
         }
         {
-            const dim3 grid((p0 + nt - 1) / ATT_CHUNK + 1, d.n_kv, nt);
+            const dim3 grid(n_chunks, d.n_kv, nt);
             if (d.hd == 128)
-                launch_pf_attention<128>(G, grid, s, d, kc, vc, pb, p0);
+                launch_pf_attention<128>(G, grid, s, d, kc, vc, pb);
             else
-                launch_pf_attention<64>(G, grid, s, d, kc, vc, pb, p0);
+                launch_pf_attention<64>(G, grid, s, d, kc, vc, pb);
         }
         {
             const int grid = matvec_grid(d, L.wo.rows), rpw = rows_per_wave(L.wo.rows, grid);
-            over_tokens(L.wo.k, rpw, [&](int t, int n, const PrefillBuffers &q) {
+            over_tokens(L.wo.k, rpw, [&](int, int n, const PrefillBuffers &q) {
                 dispatch_nt(L.wo.k, L.wo.type, [&]<int NP, int T>() {
                     allow_lds(k_pf_attn_out<NP, T>);
                     hipLaunchKernelGGL((k_pf_attn_out<NP, T>), dim3(grid), dim3(MT), pf_lds_bytes(L.wo.k, n, rpw), s,
-                                       d, L.wo, q, p0 + t, n, rpw);
+                                       d, L.wo, q, n, rpw);
                 });
             });
         }
@@ -445,6 +574,40 @@ void launch_prefill_chunk(const LlmDims &d, const LayerW *layers, int n_layer, _
             });
         }
     }
+}
+
+}  // namespace
+
+void launch_prefill_chunk(const LlmDims &d, const LayerW *layers, int n_layer, _Float16 *kcache,
+                          _Float16 *vcache, const QMat &tok_embd, const PrefillBuffers &pb, int p0, int nt,
+                          int n_chunks, hipStream_t s) {
+    if (nt <= 0) return;
+    hipLaunchKernelGGL(k_pf_embed, dim3(nt), dim3(ST), 0, s, d, tok_embd, pb, p0);
+    launch_layers(d, layers, n_layer, kcache, vcache, pb, nt, n_chunks, s);
+}
+
+size_t batch_lm_head_lds(const LlmDims &d, int B) { return pf_lds_bytes(d.n_embd, B, 0) + (size_t)MW * B * 128 * 4; }
+
+bool batch_supported(const LlmDims &d, int B) {
+    return B >= 1 && B <= kPrefillB && batch_lm_head_lds(d, B) <= (size_t)LDS_DYN_MAX;
+}
+
+void launch_batch_step(const LlmDims &d, const LayerW *layers, int n_layer, _Float16 *kcache, _Float16 *vcache,
+                       const float *out_norm, const QMat &lm, const QMat &tok_embd, const PrefillBuffers &pb,
+                       const BatchBuffers &bb, int B, hipStream_t s) {
+    launch_layers(d, layers, n_layer, kcache, vcache, pb, B, d.max_splits, s);
+    const int nblk = lm_head_blocks(d);
+    dispatch_nt(d.n_embd, lm.type, [&]<int NP, int T>() {
+        allow_lds(k_bt_lm_head<NP, T>);
+        hipLaunchKernelGGL((k_bt_lm_head<NP, T>), dim3(nblk), dim3(MT), batch_lm_head_lds(d, B), s, d, out_norm, lm,
+                           pb, bb, B);
+    });
+    hipLaunchKernelGGL(k_bt_sample, dim3(B), dim3(ST), 0, s, d, tok_embd, nblk, pb, bb);
+}
+
+void launch_batch_embed(const LlmDims &d, const QMat &tok_embd, const PrefillBuffers &pb, const BatchBuffers &bb,
+                        int B, hipStream_t s) {
+    hipLaunchKernelGGL(k_bt_embed, dim3(B), dim3(ST), 0, s, d, tok_embd, pb, bb);
 }
 
 }  // namespace mio

@@ -31,6 +31,19 @@ struct mio_hip_llm {
     mio::LlmBuffers buf{};
     int *d_tokens = nullptr, *d_force = nullptr, *d_prompt = nullptr;
     mio::PrefillBuffers pf{};  // batched prompt prefill (kPrefillB tokens per chunk)
+    int *d_iota = nullptr;     // 0, 1, ..., n_ctx - 1 (prefill positions; batch stream ids)
+    // batched decode of B utterances (mio_hip_llm_generate_batch), allocated on first use
+    struct Batch {
+        int B = 0;
+        _Float16 *kc = nullptr, *vc = nullptr;  // [B][layer][kv head][n_ctx][hd]
+        mio::StepState *st = nullptr;
+        mio::SampleCfg *cfg = nullptr;
+        float *logits = nullptr, *smp = nullptr;
+        int *tokens = nullptr;                  // [B][n_ctx] token rings
+        int *ppos = nullptr, *pseq = nullptr, *ptok = nullptr;  // flattened prompt prefill lists
+        hipGraphExec_t graph = nullptr, graph_n = nullptr;
+        std::vector<void *> allocs;
+    } bt;
     int max_steps = 0;
     std::vector<void *> allocs;
     uint64_t weight_bytes = 0;
@@ -61,6 +74,9 @@ struct mio_hip_llm {
         if (d) hipSetDevice(d->dev);
         if (graph) hipGraphExecDestroy(graph);
         if (graph_n) hipGraphExecDestroy(graph_n);
+        if (bt.graph) hipGraphExecDestroy(bt.graph);
+        if (bt.graph_n) hipGraphExecDestroy(bt.graph_n);
+        for (void *p : bt.allocs) hipFree(p);
         for (void *p : allocs) hipFree(p);
     }
 };
@@ -182,8 +198,12 @@ int set_state(mio_hip_llm *m, int pos, int token, int step = 0) {
 int prefill(mio_hip_llm *m, int n) {
     for (int p0 = 0; p0 < n; p0 += mio::kPrefillB) {
         const int nt = n - p0 < mio::kPrefillB ? n - p0 : mio::kPrefillB;
-        mio::launch_prefill_chunk(m->dims, m->layers.data(), m->n_layer, m->kc, m->vc, m->tok, m->pf, p0, nt,
-                                  m->d->stream);
+        mio::PrefillBuffers pb = m->pf;
+        pb.pos = m->d_iota + p0, pb.pos_stride = 1;  // positions p0 .. p0 + nt - 1
+        pb.seq = m->d_iota, pb.seq_stride = 0;       // one sequence: the model's own cache
+        pb.seq_kv = 0;
+        mio::launch_prefill_chunk(m->dims, m->layers.data(), m->n_layer, m->kc, m->vc, m->tok, pb, p0, nt,
+                                  (p0 + nt - 1) / mio::kAttChunk + 1, m->d->stream);
         MIO_HIP_CHECK(hipGetLastError());
     }
     return MIO_OK;
@@ -504,6 +524,7 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
     want(m->pf.h, (size_t)mio::kPrefillB * D.n_ff);
     want(m->pf.part, (size_t)mio::kPrefillB * D.n_head * D.max_splits * (D.hd + 4));
     want(dr, (size_t)n_ctx * (D.hd / 2));
+    want(m->d_iota, (size_t)n_ctx + mio::kPrefillB);
     size_t io_bytes = 0;
     for (auto &c : carve) io_bytes += (c.second + 255) & ~(size_t)255;
     uint8_t *io = dalloc<uint8_t>(m, (io_bytes + (2u << 20) - 1) & ~(size_t)((2u << 20) - 1));
@@ -528,11 +549,16 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
     }
     if (!m->kc || !m->vc || !m->buf.x || !m->buf.qkv || !m->buf.h || !m->buf.logits ||
         !m->buf.part || !m->buf.smp || !m->buf.st || !m->d_cfg || !m->d_tokens || !m->d_force || !dr ||
-        !m->d_prompt || !m->pf.x || !m->pf.qkv || !m->pf.h || !m->pf.part) {
+        !m->d_prompt || !m->pf.x || !m->pf.qkv || !m->pf.h || !m->pf.part || !m->d_iota) {
         mio::set_error("llm_load: device allocation failed");
         return fail(MIO_ERR_OOM);
     }
     hipMemcpy(dr, rope.data(), rope.size() * sizeof(float2), hipMemcpyHostToDevice);
+    {
+        std::vector<int> iota((size_t)n_ctx + mio::kPrefillB);
+        for (size_t i = 0; i < iota.size(); ++i) iota[i] = (int)i;
+        hipMemcpy(m->d_iota, iota.data(), iota.size() * 4, hipMemcpyHostToDevice);
+    }
     m->buf.rope = dr;
     m->d_layers = dalloc<mio::LayerW>(m, m->layers.size());
     m->d_ctl = (unsigned *)dalloc<uint8_t>(m, mio::persist_ctl_bytes());
@@ -542,6 +568,11 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
     }
     hipMemcpy(m->d_layers, m->layers.data(), m->layers.size() * sizeof(mio::LayerW), hipMemcpyHostToDevice);
     m->pf.rope = dr;
+    // every memset / copy above ran on the null stream; the runner's stream is non-blocking
+    if (hipDeviceSynchronize() != hipSuccess) {
+        mio::set_error("llm_load: device synchronize failed");
+        return fail(MIO_ERR_HIP);
+    }
     *out = m;
     return MIO_OK;
 }
@@ -612,6 +643,204 @@ extern "C" int mio_hip_llm_generate(mio_hip_llm *m, const int32_t *prompt, int n
     const int n = (int)toks.size() < max_tokens ? (int)toks.size() : max_tokens;
     std::memcpy(out_tokens, toks.data(), (size_t)n * 4);
     *n_out = n;
+    return MIO_OK;
+}
+
+namespace {
+
+// Batch state for B streams (re-allocated when B changes; graphs re-captured).
+int batch_ensure(mio_hip_llm *m, int B) {
+    auto &bt = m->bt;
+    if (bt.B == B) return MIO_OK;
+    if (bt.graph) hipGraphExecDestroy(bt.graph), bt.graph = nullptr;
+    if (bt.graph_n) hipGraphExecDestroy(bt.graph_n), bt.graph_n = nullptr;
+    for (void *p : bt.allocs) hipFree(p);
+    bt.allocs.clear();
+    bt.B = 0;
+    const mio::LlmDims &D = m->dims;
+    const size_t seq_kv = (size_t)m->n_layer * D.n_kv * D.n_ctx * D.hd;
+    auto al = [&](size_t bytes) -> void * {
+        void *p = nullptr;
+        if (hipMalloc(&p, bytes + 256) != hipSuccess) return nullptr;
+        bt.allocs.push_back(p);
+        // stream-ordered: the runner's stream is non-blocking, so a null-stream memset could
+        // still be clearing the caches while the prefill below writes them
+        hipMemsetAsync(p, 0, bytes + 256, m->d->stream);
+        return p;
+    };
+    bt.kc = (_Float16 *)al((size_t)B * seq_kv * 2);
+    bt.vc = (_Float16 *)al((size_t)B * seq_kv * 2);
+    bt.st = (mio::StepState *)al((size_t)B * sizeof(mio::StepState));
+    bt.cfg = (mio::SampleCfg *)al((size_t)B * sizeof(mio::SampleCfg));
+    bt.logits = (float *)al((size_t)B * D.n_vocab * 4);
+    bt.smp = (float *)al((size_t)B * mio::lm_head_blocks(D) * 2 * 4);
+    bt.tokens = (int *)al((size_t)B * D.n_ctx * 4);
+    bt.ppos = (int *)al((size_t)B * D.n_ctx * 4);
+    bt.pseq = (int *)al((size_t)B * D.n_ctx * 4);
+    bt.ptok = (int *)al((size_t)B * D.n_ctx * 4);
+    if (!bt.kc || !bt.vc || !bt.st || !bt.cfg || !bt.logits || !bt.smp || !bt.tokens || !bt.ppos || !bt.pseq ||
+        !bt.ptok) {
+        for (void *p : bt.allocs) hipFree(p);
+        bt.allocs.clear();
+        mio::set_error("llm_generate_batch: device allocation for %d streams failed", B);
+        return MIO_ERR_OOM;
+    }
+    bt.B = B;
+    MIO_HIP_CHECK(hipStreamSynchronize(m->d->stream));
+    return MIO_OK;
+}
+
+// the decode step's view of the batch: stream b's position is st[b].pos, its cache is b
+mio::PrefillBuffers batch_pb(mio_hip_llm *m) {
+    mio::PrefillBuffers pb = m->pf;
+    pb.pos = &m->bt.st[0].pos, pb.pos_stride = (int)(sizeof(mio::StepState) / sizeof(int));
+    pb.seq = m->d_iota, pb.seq_stride = 1;
+    pb.seq_kv = (size_t)m->n_layer * m->dims.n_kv * m->dims.n_ctx * m->dims.hd;
+    return pb;
+}
+
+mio::BatchBuffers batch_bb(mio_hip_llm *m) { return mio::BatchBuffers{m->bt.st, m->bt.cfg, m->bt.logits, m->bt.smp}; }
+
+void issue_batch_step(mio_hip_llm *m) {
+    mio::launch_batch_step(m->dims, m->layers.data(), m->n_layer, m->bt.kc, m->bt.vc, m->out_norm, m->lm, m->tok,
+                           batch_pb(m), batch_bb(m), m->bt.B, m->d->stream);
+}
+
+int capture_batch(mio_hip_llm *m, int n, hipGraphExec_t *out) {
+    hipStream_t s = m->d->stream;
+    hipGraph_t g = nullptr;
+    MIO_HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+    for (int i = 0; i < n; ++i) issue_batch_step(m);
+    MIO_HIP_CHECK(hipStreamEndCapture(s, &g));
+    MIO_HIP_CHECK(hipGraphInstantiate(out, g, nullptr, nullptr, 0));
+    hipGraphDestroy(g);
+    return MIO_OK;
+}
+
+// n batched steps: the first ever step for this B runs eagerly (its launches set the
+// kernels' LDS attributes outside any capture), then 1- and kGraphSteps-step graphs replay.
+int run_batch(mio_hip_llm *m, int n) {
+    static const bool eager = getenv("MIO_NO_GRAPH") && getenv("MIO_NO_GRAPH")[0] == '1';
+    auto &bt = m->bt;
+    if (n > 0 && (eager || !bt.graph)) {
+        issue_batch_step(m);
+        MIO_HIP_CHECK(hipGetLastError());
+        --n;
+        if (eager) {
+            for (; n > 0; --n) issue_batch_step(m);
+            MIO_HIP_CHECK(hipGetLastError());
+            return MIO_OK;
+        }
+        int rc;
+        if ((rc = capture_batch(m, 1, &bt.graph)) || (rc = capture_batch(m, kGraphSteps, &bt.graph_n))) return rc;
+    }
+    for (; n >= kGraphSteps; n -= kGraphSteps) MIO_HIP_CHECK(hipGraphLaunch(bt.graph_n, m->d->stream));
+    for (; n > 0; --n) MIO_HIP_CHECK(hipGraphLaunch(bt.graph, m->d->stream));
+    return MIO_OK;
+}
+
+}  // namespace
+
+// B independent utterances decoded together (the reference runs them one after another, one
+// llama_context each: test-to-speech.cpp:94-199 per call). Prompts are concatenated;
+// stream b's sampled tokens go to out_tokens[b * max_tokens ...], n_out[b] of them (up to,
+// not including, an end token). Each stream's tokens equal a single-stream generate with
+// its seed (same kernels' arithmetic per token, same sampler noise).
+extern "C" int mio_hip_llm_generate_batch(mio_hip_llm *m, const int32_t *prompts, const int32_t *prompt_lens, int B,
+                                          int max_tokens, float temperature, const uint64_t *seeds,
+                                          int32_t allow_lo, int32_t allow_hi, int32_t eos0, int32_t eos1,
+                                          int32_t check_interval, int32_t *out_tokens, int32_t *n_out) {
+    MIO_REQUIRE(m && prompts && prompt_lens && seeds && out_tokens && n_out && max_tokens >= 1, MIO_ERR_INVALID,
+                "llm_generate_batch: bad args");
+    MIO_REQUIRE(mio::batch_supported(m->dims, B), MIO_ERR_UNSUPPORTED,
+                "llm_generate_batch: %d streams not supported (1..%d, lm_head LDS)", B, mio::kPrefillB);
+    const mio::LlmDims &D = m->dims;
+    std::vector<int> off(B + 1, 0);
+    for (int b = 0; b < B; ++b) {
+        MIO_REQUIRE(prompt_lens[b] >= 1 && prompt_lens[b] + max_tokens <= D.n_ctx, MIO_ERR_INVALID,
+                    "llm_generate_batch: stream %d: %d prompt + %d new tokens exceed n_ctx %d", b, prompt_lens[b],
+                    max_tokens, D.n_ctx);
+        off[b + 1] = off[b] + prompt_lens[b];
+    }
+    for (int i = 0; i < off[B]; ++i)
+        MIO_REQUIRE(prompts[i] >= 0 && prompts[i] < D.n_vocab, MIO_ERR_INVALID,
+                    "llm_generate_batch: token %d out of vocab", prompts[i]);
+    int rc = mio::bind(m->d);
+    if (rc || (rc = batch_ensure(m, B))) return rc;
+    auto &bt = m->bt;
+    hipStream_t s = m->d->stream;
+    // prompt positions [0, P_b) of every stream: one flattened list, kPrefillB tokens per
+    // chunk whatever stream they belong to (one weight pass per chunk)
+    std::vector<int> ftok, fpos, fseq;
+    for (int b = 0; b < B; ++b)
+        for (int p = 0; p + 1 < prompt_lens[b]; ++p) {
+            ftok.push_back(prompts[off[b] + p]);
+            fpos.push_back(p);
+            fseq.push_back(b);
+        }
+    const int nf = (int)ftok.size();
+    if (nf) {
+        MIO_HIP_CHECK(hipMemcpyAsync(bt.ptok, ftok.data(), (size_t)nf * 4, hipMemcpyHostToDevice, s));
+        MIO_HIP_CHECK(hipMemcpyAsync(bt.ppos, fpos.data(), (size_t)nf * 4, hipMemcpyHostToDevice, s));
+        MIO_HIP_CHECK(hipMemcpyAsync(bt.pseq, fseq.data(), (size_t)nf * 4, hipMemcpyHostToDevice, s));
+    }
+    for (int c0 = 0; c0 < nf; c0 += mio::kPrefillB) {
+        const int nt = nf - c0 < mio::kPrefillB ? nf - c0 : mio::kPrefillB;
+        int pmax = 0;
+        for (int t = 0; t < nt; ++t) pmax = std::max(pmax, fpos[c0 + t]);
+        mio::PrefillBuffers pb = m->pf;
+        pb.tokens = bt.ptok;
+        pb.pos = bt.ppos + c0, pb.pos_stride = 1;
+        pb.seq = bt.pseq + c0, pb.seq_stride = 1;
+        pb.seq_kv = (size_t)m->n_layer * D.n_kv * D.n_ctx * D.hd;
+        mio::launch_prefill_chunk(D, m->layers.data(), m->n_layer, bt.kc, bt.vc, m->tok, pb, c0, nt,
+                                  pmax / mio::kAttChunk + 1, s);
+        MIO_HIP_CHECK(hipGetLastError());
+    }
+    // per-stream state: decoding starts at position P_b = len_b - 1 with the step counter at
+    // P_b (the single-stream generate's sampler stream)
+    std::vector<mio::StepState> st(B);
+    std::vector<mio::SampleCfg> cf(B);
+    for (int b = 0; b < B; ++b) {
+        const int P = prompt_lens[b] - 1;
+        st[b] = mio::StepState{P, P, prompts[off[b] + P], 0};
+        mio::SampleCfg &c = cf[b];
+        c.temp = temperature;
+        c.seed_lo = (uint32_t)seeds[b], c.seed_hi = (uint32_t)(seeds[b] >> 32);
+        c.lo = allow_lo < 0 ? 0 : allow_lo;
+        c.hi = (allow_hi < 0 || allow_hi > D.n_vocab) ? D.n_vocab : allow_hi;
+        c.eos0 = eos0, c.eos1 = eos1;
+        c.force = nullptr, c.n_force = 0;
+        c.out_tokens = bt.tokens + (size_t)b * D.n_ctx;
+        c.max_steps = P + max_tokens;
+    }
+    MIO_HIP_CHECK(hipMemcpyAsync(bt.st, st.data(), B * sizeof(mio::StepState), hipMemcpyHostToDevice, s));
+    MIO_HIP_CHECK(hipMemcpyAsync(bt.cfg, cf.data(), B * sizeof(mio::SampleCfg), hipMemcpyHostToDevice, s));
+    mio::launch_batch_embed(D, m->tok, batch_pb(m), batch_bb(m), B, s);
+    MIO_HIP_CHECK(hipGetLastError());
+    if (check_interval <= 0) check_interval = max_tokens;
+    std::vector<mio::StepState> hs(B);
+    for (int done = 0; done < max_tokens;) {
+        const int n = std::min(check_interval, max_tokens - done);
+        if ((rc = run_batch(m, n))) return rc;
+        done += n;
+        MIO_HIP_CHECK(hipMemcpyAsync(hs.data(), bt.st, B * sizeof(mio::StepState), hipMemcpyDeviceToHost, s));
+        MIO_HIP_CHECK(hipStreamSynchronize(s));
+        bool all = true;
+        for (int b = 0; b < B; ++b) all = all && hs[b].done;
+        if (all) break;
+    }
+    std::vector<int32_t> ring(max_tokens);
+    for (int b = 0; b < B; ++b) {
+        const int P = prompt_lens[b] - 1;
+        const int n = std::max(0, std::min(hs[b].step - P, max_tokens));
+        if (n) MIO_HIP_CHECK(hipMemcpy(ring.data(), bt.tokens + (size_t)b * D.n_ctx + P, (size_t)n * 4,
+                                       hipMemcpyDeviceToHost));
+        int k = 0;
+        while (k < n && ring[k] != eos0 && ring[k] != eos1) ++k;
+        std::memcpy(out_tokens + (size_t)b * max_tokens, ring.data(), (size_t)k * 4);
+        n_out[b] = k;
+    }
     return MIO_OK;
 }
 

@@ -108,6 +108,9 @@ def _declare(L: ctypes.CDLL) -> None:
                                          ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                          ctypes.c_int32, ctypes.c_int32, _vp,
                                          ctypes.POINTER(c_int)]),
+        "mio_hip_llm_generate_batch": (c_int, [_vp, _vp, _vp, c_int, c_int, ctypes.c_float, _vp,
+                                               ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                               ctypes.c_int32, ctypes.c_int32, _vp, _vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -458,6 +461,22 @@ class Llm:
                                          temperature, seed, allow[0], allow[1], eos[0], eos[1],
                                          check_interval, _ptr(out), ctypes.byref(n)))
         return out[: n.value]
+
+    def generate_batch(self, prompts, max_tokens: int, temperature: float = 0.8, seeds=None,
+                       allow=(-1, -1), eos=(-1, -1), check_interval: int = 32):
+        """B utterances decoded together (mio_hip_llm_generate_batch): one weight pass per
+        step for all of them; stream b's tokens equal generate(prompts[b], seed=seeds[b])."""
+        B = len(prompts)
+        seeds = [42 + b for b in range(B)] if seeds is None else list(seeds)
+        lens = np.array([len(p) for p in prompts], np.int32)
+        flat = np.ascontiguousarray(np.concatenate([np.asarray(p, np.int32) for p in prompts]), np.int32)
+        sd = np.array(seeds, np.uint64)
+        out = np.empty((B, max_tokens), np.int32)
+        n = np.zeros(B, np.int32)
+        check(lib().mio_hip_llm_generate_batch(self.h, _ptr(flat), _ptr(lens), B, max_tokens, temperature,
+                                               _ptr(sd), allow[0], allow[1], eos[0], eos[1],
+                                               check_interval, _ptr(out), _ptr(n)))
+        return [out[b, : n[b]].copy() for b in range(B)]
 
 
 GGML_BLOCK = {8: (32, 34), 12: (256, 144), 14: (256, 210)}

@@ -1,0 +1,92 @@
+"""GPU parity: batched decode of B utterances (mio_hip_llm_generate_batch, csrc/hip/llm_prefill.hip
+k_bt_* + the multi-token layer engine) vs single-utterance decode (mio_hip_llm_generate).
+
+The reference decodes utterances one after another, one llama_context each
+(test-to-speech.cpp:94-199 per call). Batching B of them into one weight pass per step must not
+change any of them: every stream's per-token arithmetic is the single-stream decode's (same
+quantizers, same per-superblock integer sums in the same order, same attention sweep, same
+counter-based Gumbel noise gumbel(seed_b, step, id)), so stream b's tokens equal
+generate(prompt_b, seed_b) EXACTLY. Single-stream generate is itself checked against the C
+oracle in test_llm_gpu.py (>= 95% of ids, measured 100%); the first test re-checks one stream
+against the oracle directly.
+"""
+import numpy as np
+import pytest
+
+import miotts_amd as m
+import pyoracle
+
+pytestmark = pytest.mark.gpu
+
+ALLOW = (m.SYNTH_SPEECH0, m.SYNTH_SPEECH0 + 12800)
+
+
+@pytest.fixture(scope="module")
+def llm_files(tmp_path_factory):
+    d = tmp_path_factory.mktemp("llm_batch")
+    return {p: m.synth_llm(str(d / f"llm{p}.gguf"), p, 1) for p in (0, 1)}
+
+
+def _prompts(B, seed):
+    rng = np.random.default_rng(seed)
+    # ragged lengths, including a 1-token prompt (nothing to prefill for that stream)
+    lens = [1 if b == 1 else int(rng.integers(3, 40)) for b in range(B)]
+    return [list(rng.integers(0, 256, n)) for n in lens]
+
+
+@pytest.mark.parametrize("preset,B", [(0, 3), (1, 4), (0, 16)])
+def test_batch_equals_single_streams(device, llm_files, preset, B):
+    g = m.Llm(device, llm_files[preset], 256)
+    prompts = _prompts(B, 10 * preset + B)
+    seeds = [1000 + 17 * b for b in range(B)]
+    got = g.generate_batch(prompts, 24, 0.8, seeds, allow=ALLOW)
+    for b in range(B):
+        ref = g.generate(prompts[b], 24, 0.8, seeds[b], allow=ALLOW)
+        assert np.array_equal(got[b], ref), (b, got[b], ref)
+    if B == 3:
+        o = pyoracle.Llm(llm_files[preset], 256)
+        to = o.generate(prompts[0], 24, 0.8, seeds[0], allow=ALLOW)
+        assert (got[0] == to).sum() >= 22
+
+
+def test_batch_greedy_and_identical_streams(device, llm_files):
+    """temperature 0 = greedy; two streams with the same prompt and seed stay identical."""
+    g = m.Llm(device, llm_files[1], 256)
+    p = [256, 257, 84, 101, 115, 116, 258, 257]
+    got = g.generate_batch([p, p, p[:5]], 16, 0.0, [5, 5, 9], allow=ALLOW)
+    assert np.array_equal(got[0], got[1])
+    assert np.array_equal(got[0], g.generate(p, 16, 0.0, 123, allow=ALLOW))
+    assert np.array_equal(got[2], g.generate(p[:5], 16, 0.0, 9, allow=ALLOW))
+
+
+def test_batch_stops_at_eos(device, llm_files):
+    """End tokens end each stream where its single-stream decode ends (the token itself is not
+    returned, test-to-speech.cpp:168-170); the batch returns when every stream has ended."""
+    g = m.Llm(device, llm_files[0], 256)
+    prompts = [[256, 257, 65, 258, 257], [256, 257, 66, 67, 258, 257], [256, 257, 68, 258, 257]]
+    allow = (m.SYNTH_EOT, m.SYNTH_SPEECH0 + 3)
+    eos = (m.SYNTH_EOT, m.SYNTH_IM_END)
+    got = g.generate_batch(prompts, 200, 2.0, [7, 8, 9], allow=allow, eos=eos, check_interval=20)
+    for b, p in enumerate(prompts):
+        ref = g.generate(p, 200, 2.0, 7 + b, allow=allow, eos=eos, check_interval=20)
+        assert np.array_equal(got[b], ref)
+        assert len(got[b]) < 200 and (got[b] != m.SYNTH_EOT).all()
+
+
+def test_batch_rejects_bad_shapes(device, llm_files):
+    g = m.Llm(device, llm_files[0], 64)
+    with pytest.raises(m.HipError):
+        g.generate_batch([[256, 257]] * 17, 4, 0.8)
+    with pytest.raises(m.HipError):
+        g.generate_batch([[256] * 40], 30, 0.8)  # 40 + 30 > n_ctx 64
+
+
+def test_batch_1p7b_q4km(device, tmp_path):
+    """The bench model (1.7B Q4_K_M: Q4_K + Q6_K matrices, 28 layers, GQA 16/8, 164736 vocab),
+    4 streams x 16 tokens, each equal to its single-stream decode."""
+    path = m.synth_llm(str(tmp_path / "llm17.gguf"), 3, 1)
+    g = m.Llm(device, path, 512)
+    prompts = _prompts(4, 17)
+    got = g.generate_batch(prompts, 16, 0.8, [42, 43, 44, 45], allow=ALLOW)
+    for b in range(4):
+        assert np.array_equal(got[b], g.generate(prompts[b], 16, 0.8, 42 + b, allow=ALLOW)), b
