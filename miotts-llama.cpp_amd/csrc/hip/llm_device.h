@@ -217,12 +217,43 @@ __device__ double block_sum(double v, double *red) {
     return t;
 }
 
-// quantize_row_q8_K_ref semantics (iscale = -127/max_signed with max_signed the first
-// element of largest |x|, nearest-even, clamp 127, bsums). One superblock per wave and
-// pass (4 values per lane), NI passes (K <= NI * 2048) unrolled so their reduction chains
-// interleave. Largest |x| by DPP; its first position by a ballot of the lanes holding it
-// (the lowest such lane, the lowest of its 4 values) - the signed value comes straight from
-// that lane's register.
+// quantize_row_q8_K_ref semantics for superblock b held as 4 values per lane (lane l:
+// elements 4l .. 4l+3), am = the superblock's largest |x| (wave-uniform): iscale =
+// -127/max_signed with max_signed the first element of largest |x|, nearest-even, clamp
+// 127, bsums. Its first position comes from a ballot of the lanes holding it (the lowest
+// such lane, the lowest of its 4 values); the signed value straight from that lane.
+__device__ __forceinline__ void q8k_store(const float (&v)[4], float am, int b, const ActL &a) {
+    const int lane = MIO_TIDX & 63;
+    int q[4] = {0, 0, 0, 0};
+    float dd = 0.0f;
+    if (am > 0.0f) {
+        float sel = 0.0f;
+        bool has = false;
+#pragma unroll
+        for (int i = 3; i >= 0; --i)
+            if (fabsf(v[i]) == am) sel = v[i], has = true;
+        const int src = __builtin_ctzll(__ballot(has));
+        const float mx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sel), src));
+        const float iscale = -127.f / mx;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int t = (int)rintf(iscale * v[i]);
+            q[i] = t < 127 ? t : 127;
+        }
+        dd = 1.0f / iscale;
+    }
+    const int packed = (q[0] & 0xFF) | ((q[1] & 0xFF) << 8) | ((q[2] & 0xFF) << 16) | ((q[3] & 0xFF) << 24);
+    *reinterpret_cast<int *>(a.qs + b * 256 + 4 * lane) = packed;
+    const int sm = quad_sum_i(q[0] + q[1] + q[2] + q[3]);
+    if ((lane & 3) == 0) a.bs[b * 16 + (lane >> 2)] = (int16_t)sm;
+    if (lane == 0) a.d[b] = dd;
+}
+__device__ __forceinline__ float abs_max4(const float (&v)[4]) {
+    return wave_max_f(fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))), 0.0f);
+}
+
+// One superblock per wave and pass (4 values per lane), NI passes (K <= NI * 2048) unrolled
+// so their reduction chains interleave.
 template <int NI>
 __device__ void quant_q8k(const float *xs, int K, const ActL &a) {
     const int lane = MIO_TIDX & 63, wave = MIO_TIDX >> 6;
@@ -236,40 +267,36 @@ __device__ void quant_q8k(const float *xs, int K, const ActL &a) {
         v[j][0] = v4.x, v[j][1] = v4.y, v[j][2] = v4.z, v[j][3] = v4.w;
     }
 #pragma unroll
-    for (int j = 0; j < NI; ++j)
-        am[j] = wave_max_f(fmaxf(fmaxf(fabsf(v[j][0]), fabsf(v[j][1])), fmaxf(fabsf(v[j][2]), fabsf(v[j][3]))), 0.0f);
+    for (int j = 0; j < NI; ++j) am[j] = abs_max4(v[j]);
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
         const int b = wave + MW * j;
         if (b >= nsb) break;
-        int q[4] = {0, 0, 0, 0};
-        float dd = 0.0f;
-        if (am[j] > 0.0f) {
-            float sel = 0.0f;
-            bool has = false;
-#pragma unroll
-            for (int i = 3; i >= 0; --i)
-                if (fabsf(v[j][i]) == am[j]) sel = v[j][i], has = true;
-            const int src = __builtin_ctzll(__ballot(has));
-            const float mx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sel), src));
-            const float iscale = -127.f / mx;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int t = (int)rintf(iscale * v[j][i]);
-                q[i] = t < 127 ? t : 127;
-            }
-            dd = 1.0f / iscale;
-        }
-        const int packed = (q[0] & 0xFF) | ((q[1] & 0xFF) << 8) | ((q[2] & 0xFF) << 16) | ((q[3] & 0xFF) << 24);
-        *reinterpret_cast<int *>(a.qs + b * 256 + 4 * lane) = packed;
-        const int sm = quad_sum_i(q[0] + q[1] + q[2] + q[3]);
-        if ((lane & 3) == 0) a.bs[b * 16 + (lane >> 2)] = (int16_t)sm;
-        if (lane == 0) a.d[b] = dd;
+        q8k_store(v[j], am[j], b, a);
     }
 }
 
-// quantize_row_q8_0_ref semantics (d = amax/127 stored as f16, q = roundf(x * 1/d)); 8
-// blocks per wave and pass, NI passes unrolled
+// quantize_row_q8_0_ref semantics (d = amax/127 stored as f16, q = roundf(x * 1/d)) of
+// block b held by the 8-lane group of this lane (4 values per lane, lane & 7 = position)
+__device__ __forceinline__ void q80_store(const float (&v)[4], int b, bool ok, const ActL &a) {
+    const int lane = MIO_TIDX & 63;
+    float am = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) am = fmaxf(am, fabsf(v[i]));
+    am = group8_max(am);
+    const float dd = am / 127.0f;
+    const float id = dd != 0.0f ? 1.0f / dd : 0.0f;
+    int q[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) q[i] = (int)roundf(v[i] * id);
+    if (ok) {
+        *reinterpret_cast<int *>(a.qs + b * 32 + 4 * (lane & 7)) =
+            (q[0] & 0xFF) | ((q[1] & 0xFF) << 8) | ((q[2] & 0xFF) << 16) | ((q[3] & 0xFF) << 24);
+        if ((lane & 7) == 0) a.d[b] = f16r(dd);
+    }
+}
+
+// 8 blocks per wave and pass, NI passes unrolled
 template <int NI>
 __device__ void quant_q80(const float *xs, int K, const ActL &a) {
     const int lane = MIO_TIDX & 63, wave = MIO_TIDX >> 6;
@@ -279,23 +306,9 @@ __device__ void quant_q80(const float *xs, int K, const ActL &a) {
         const int b = wave * 8 + MW * 8 * j + (lane >> 3);
         const bool ok = b < nb;
         float v[4];
-        float am = 0.0f;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            v[i] = ok ? xs[b * 32 + 4 * (lane & 7) + i] : 0.0f;
-            am = fmaxf(am, fabsf(v[i]));
-        }
-        am = group8_max(am);
-        const float dd = am / 127.0f;
-        const float id = dd != 0.0f ? 1.0f / dd : 0.0f;
-        int q[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) q[i] = (int)roundf(v[i] * id);
-        if (ok) {
-            *reinterpret_cast<int *>(a.qs + b * 32 + 4 * (lane & 7)) =
-                (q[0] & 0xFF) | ((q[1] & 0xFF) << 8) | ((q[2] & 0xFF) << 16) | ((q[3] & 0xFF) << 24);
-            if ((lane & 7) == 0) a.d[b] = f16r(dd);
-        }
+        for (int i = 0; i < 4; ++i) v[i] = ok ? xs[b * 32 + 4 * (lane & 7) + i] : 0.0f;
+        q80_store(v, b, ok, a);
     }
 }
 
@@ -838,9 +851,49 @@ __device__ __forceinline__ float group_sum(float v) {
     return v;
 }
 
+// Online-softmax merge of nch chunk partial records {O[hd], m, l} for the 4 outputs
+// dd .. dd+3 of one head (base = that head's record array): 8 chunks' loads in flight per
+// batch; a missing chunk of a batch is {m = -inf, l = 0, O = 0}, which leaves the max and
+// the sums unchanged (only real chunks are loaded: every vector load instruction costs the
+// CU's address path the same, used or not).
+__device__ __forceinline__ float4 merge_out4(const float *base, int nch, int rec, int hd, int dd) {
+    float M = -INFINITY, L = 0.0f;
+    float4 O = make_float4(0.f, 0.f, 0.f, 0.f);
+    constexpr int CB = 8;  // chunks per batch of loads
+    for (int c0 = 0; c0 < nch; c0 += CB) {
+        float2 ml[CB];
+        float4 oc[CB];
+#pragma unroll
+        for (int j = 0; j < CB; ++j) {
+            const int c = c0 + j;
+            if (c < nch) {
+                ml[j] = *reinterpret_cast<const float2 *>(base + (size_t)c * rec + hd);
+                oc[j] = *reinterpret_cast<const float4 *>(base + (size_t)c * rec + dd);
+            } else {
+                ml[j] = make_float2(-INFINITY, 0.0f);
+                oc[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+        }
+        float mb = M;
+#pragma unroll
+        for (int j = 0; j < CB; ++j) mb = fmaxf(mb, ml[j].x);
+        const float a = M == -INFINITY ? 0.0f : expf(M - mb);
+        L *= a;
+        O.x *= a, O.y *= a, O.z *= a, O.w *= a;
+#pragma unroll
+        for (int j = 0; j < CB; ++j) {
+            const float w = c0 + j < nch ? expf(ml[j].x - mb) : 0.0f;
+            L += w * ml[j].y;
+            O.x += w * oc[j].x, O.y += w * oc[j].y, O.z += w * oc[j].z, O.w += w * oc[j].w;
+        }
+        M = mb;
+    }
+    return make_float4(O.x / L, O.y / L, O.z / L, O.w / L);
+}
+
 // Merge of the attention chunks' partial records (k_attention) for all heads: thread t
-// owns outputs 4(t + i*MT) .. +3; online softmax merge over chunks, 8 chunks' loads in
-// flight; normalized outputs -> s.xs, then re-quantized into s.a.
+// owns outputs 4(t + i*MT) .. +3 (merge_out4); normalized outputs -> s.xs, then
+// re-quantized into s.a.
 template <int NP>
 __device__ void merge_attention(const LlmDims &d, const float *part, int nch, int K, bool kquant, const Smem &s,
                                 unsigned long long *diag = nullptr) {
@@ -850,42 +903,7 @@ __device__ void merge_attention(const LlmDims &d, const float *part, int nch, in
         const int e = (MIO_TIDX + i * MT) * 4;
         if (e < K) {
             const int h = e / hd, dd = e - h * hd;
-            const float *base = part + (size_t)h * d.max_splits * rec;
-            float M = -INFINITY, L = 0.0f;
-            float4 O = make_float4(0.f, 0.f, 0.f, 0.f);
-            constexpr int CB = 8;  // chunks per batch of loads
-            for (int c0 = 0; c0 < nch; c0 += CB) {
-                float2 ml[CB];
-                float4 oc[CB];
-                // only the batch's real chunks are loaded (every vector load instruction costs
-                // the CU's address path the same, used or not); a missing chunk is
-                // {m = -inf, l = 0, O = 0}, which leaves the max and the sums unchanged
-#pragma unroll
-                for (int j = 0; j < CB; ++j) {
-                    const int c = c0 + j;
-                    if (c < nch) {
-                        ml[j] = *reinterpret_cast<const float2 *>(base + (size_t)c * rec + hd);
-                        oc[j] = *reinterpret_cast<const float4 *>(base + (size_t)c * rec + dd);
-                    } else {
-                        ml[j] = make_float2(-INFINITY, 0.0f);
-                        oc[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-                    }
-                }
-                float mb = M;
-#pragma unroll
-                for (int j = 0; j < CB; ++j) mb = fmaxf(mb, ml[j].x);
-                const float a = M == -INFINITY ? 0.0f : expf(M - mb);
-                L *= a;
-                O.x *= a, O.y *= a, O.z *= a, O.w *= a;
-#pragma unroll
-                for (int j = 0; j < CB; ++j) {
-                    const float w = c0 + j < nch ? expf(ml[j].x - mb) : 0.0f;
-                    L += w * ml[j].y;
-                    O.x += w * oc[j].x, O.y += w * oc[j].y, O.z += w * oc[j].z, O.w += w * oc[j].w;
-                }
-                M = mb;
-            }
-            *reinterpret_cast<float4 *>(s.xs + e) = make_float4(O.x / L, O.y / L, O.z / L, O.w / L);
+            *reinterpret_cast<float4 *>(s.xs + e) = merge_out4(part + (size_t)h * d.max_splits * rec, nch, rec, hd, dd);
         }
     }
     lds_barrier();

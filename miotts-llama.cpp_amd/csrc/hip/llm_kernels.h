@@ -85,7 +85,10 @@ struct PrefillBuffers {
     const int *seq;      // sequence (KV cache) of token t: seq[t * seq_stride]
     int pos_stride, seq_stride;
     size_t seq_kv;       // K (and V) cache elements per sequence: [seq][layer][kv head][n_ctx][hd]
+    char *act;           // [kPrefillB] quantized activation records of the next matvec
 };
+// bytes of the act records (pb.act) for K up to k_max
+size_t prefill_act_bytes(int k_max);
 
 // One chunk of nt <= kPrefillB tokens (ids at tokens[p0 + t], positions/sequences from
 // pb.pos / pb.seq) through every layer: embedding, K/V rows, residual streams in pb.x.

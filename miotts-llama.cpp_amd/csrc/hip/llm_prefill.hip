@@ -29,20 +29,21 @@ namespace {
 constexpr int LDS_MAX = 160 * 1024;
 
 // ------------------------------------------------------------------ LDS layout
-// xs f32[K] | red 128 B | act[t] = {qs i8[K] | d f32[K/32+8] | bs i16[K/16+8]} x nt |
-// resid f32[MW][nt * rpw] (the wave's residual rows per token)
+// act[t] = {qs i8[K] | d f32[K/32+8] | bs i16[K/16+8]} x nt | resid f32[MW][nt * rpw] (the
+// wave's residual rows per token). The prologues quantize straight from registers (one wave
+// per token), so no f32 staging row is needed.
 __host__ __device__ inline size_t act_bytes(int K) {
     return ((size_t)K + (size_t)(K / 32 + 8) * 4 + (size_t)(K / 16 + 8) * 2 + 15) & ~(size_t)15;
 }
-__host__ __device__ inline size_t act_base(int K) { return (size_t)K * 4 + 128; }
+__host__ __device__ inline size_t act_base(int) { return 0; }
 __host__ __device__ inline size_t pf_lds_bytes(int K, int nt, int rpw) {
     return act_base(K) + act_bytes(K) * nt + (size_t)MW * nt * rpw * 4;
 }
 
 __device__ inline Smem carve_t(char *base, int K, int t) {
     Smem s;
-    s.xs = (float *)base;
-    s.red = (double *)(base + (size_t)K * 4);
+    s.xs = nullptr;
+    s.red = nullptr;
     char *a = base + act_base(K) + act_bytes(K) * t;
     s.a.qs = (int8_t *)a;
     s.a.d = (float *)(a + K);
@@ -134,14 +135,54 @@ __device__ __forceinline__ void stream_rows_b(const QMat W0, const QMat W1, int 
     }
 }
 
-// RMSNorm + quantize of nt tokens (token 0's x was loaded before the first weight group)
-template <int NP>
-__device__ void prologue_rms(XRegs<NP> &xr, const float *x, const float *norm_w, int K, float eps, bool kq,
-                             char *smem, int nt) {
-    for (int t = 0; t < nt; ++t) {
-        if (t) load_x(x + (size_t)t * K, norm_w, K, xr);
-        rmsnorm_quant(xr, K, eps, kq, carve_t(smem, K, t));
+// ------------------------------------------------------------------ multi-token prologues
+// Every matvec workgroup needs every token's quantized activation. It is produced ONCE per
+// launch by k_bt_quant (one workgroup per token, running the single-token decode prologue
+// itself: rmsnorm_quant / plain_quant / merge_attention, so the values are the decode's bit
+// for bit) into pb.act, and each matvec workgroup copies the records into LDS with all its
+// loads in flight (one memory latency for all tokens).
+__device__ void prologue_copy(const char *act, int K, char *smem, int nt) {
+    constexpr int UN = 8;
+    const int n16 = (int)(act_bytes(K) * nt / 16);
+    const uint4 *src = reinterpret_cast<const uint4 *>(act);
+    uint4 *dst = reinterpret_cast<uint4 *>(smem + act_base(K));
+    for (int i0 = threadIdx.x; i0 < n16; i0 += UN * MT) {
+        uint4 v[UN];
+#pragma unroll
+        for (int u = 0; u < UN; ++u) v[u] = src[min(i0 + u * MT, n16 - 1)];  // clamped: all in flight
+#pragma unroll
+        for (int u = 0; u < UN; ++u) {
+            const int i = i0 + u * MT;
+            if (i < n16) dst[i] = v[u];
+        }
     }
+    lds_barrier();
+}
+
+// One workgroup per token t: MODE 0 RMSNorm(src[t]) * norm_w, 1 src[t] as is, 2 the
+// attention chunk merge of token t; quantized (Q8_K / Q8_0) into the token's act record.
+template <int NP, int MODE>
+__global__ __launch_bounds__(MT) void k_bt_quant(LlmDims d, const float *src, int K, const float *norm_w, int kq,
+                                                 PrefillBuffers pb) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int t = blockIdx.x;
+    const Smem s = carve(smem, K);
+    if constexpr (MODE == 2) {
+        const size_t tstride = (size_t)d.n_head * d.max_splits * part_rec(d.hd);
+        merge_attention<NP>(d, pb.part + t * tstride, pb.pos[t * pb.pos_stride] / ATT_CHUNK + 1, K, kq != 0, s);
+    } else {
+        XRegs<NP> xr;
+        load_x(src + (size_t)t * K, MODE == 0 ? norm_w : nullptr, K, xr);
+        if constexpr (MODE == 0)
+            rmsnorm_quant(xr, K, d.eps, kq != 0, s);
+        else
+            plain_quant(xr, K, kq != 0, s);
+    }
+    // LDS act {qs | d | bs} is contiguous from s.a.qs (carve) -> this token's global record
+    const int n16 = (int)(act_bytes(K) / 16);
+    const uint4 *l = reinterpret_cast<const uint4 *>(s.a.qs);
+    uint4 *g = reinterpret_cast<uint4 *>(pb.act + (size_t)t * act_bytes(K));
+    for (int i = threadIdx.x; i < n16; i += MT) g[i] = l[i];
 }
 
 // Residual rows [lo, hi) of every token (row stride E) in two registers per lane: entry
@@ -173,22 +214,20 @@ __global__ __launch_bounds__(MT) void k_pf_attn_in(LlmDims d, const float *norm_
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int K = d.n_embd, QD = (d.n_head + 2 * d.n_kv) * d.hd;
     const int lane = threadIdx.x & 63;
-    XRegs<NP> xr;
-    load_x(pb.x, norm_w, K, xr);
     const int o1 = wq.rows, o2 = wq.rows + wk.rows;
     Frag ga[CfgB<NP, 1>::U], gb[CfgB<NP, 1>::U];
     int lo, hi;
     if ((int)blockIdx.x < g_qk) {
         wave_range(o2, lo, hi, blockIdx.x, g_qk);
         load_first_b<TQ, NP, 1>(wq, wk, lo, hi, ga, gb, o1);
-        prologue_rms(xr, pb.x, norm_w, K, d.eps, TQ != 8, smem, nt);
+        prologue_copy(pb.act, K, smem, nt);
         stream_rows_b<TQ, NP, 1>(wq, wk, lo, hi, ga, gb, smem, nt, [&](int row, int t, float v, float) {
             if (lane == 0) pb.qkv[(size_t)t * QD + row] = v;
         }, o1);
     } else {
         wave_range(wv.rows, lo, hi, blockIdx.x - g_qk, gridDim.x - g_qk);
         load_first_b<TV, NP, 1>(wv, wv, lo, hi, ga, gb);
-        prologue_rms(xr, pb.x, norm_w, K, d.eps, TQ != 8, smem, nt);
+        prologue_copy(pb.act, K, smem, nt);
         stream_rows_b<TV, NP, 1>(wv, wv, lo, hi, ga, gb, smem, nt, [&](int row, int t, float v, float) {
             if (lane == 0) pb.qkv[(size_t)t * QD + o2 + row] = v;
         });
@@ -269,10 +308,7 @@ __global__ __launch_bounds__(MT) void k_pf_attn_out(LlmDims d, QMat wo, PrefillB
     load_first_b<T, NP, 1>(wo, wo, lo, hi, ga, gb);
     float *res = resid_lds(smem, K, nt, rpw);
     store_resid_b(xr, res, nt, rpw);
-    const size_t tstride = (size_t)d.n_head * d.max_splits * part_rec(d.hd);
-    for (int t = 0; t < nt; ++t)
-        merge_attention<NP>(d, pb.part + t * tstride, pb.pos[t * pb.pos_stride] / ATT_CHUNK + 1, K, T != 8,
-                            carve_t(smem, K, t));
+    prologue_copy(pb.act, K, smem, nt);
     stream_rows_b<T, NP, 1>(wo, wo, lo, hi, ga, gb, smem, nt, [&](int row, int t, float v, float) {
         const float r = res[t * rpw + row - lo];
         if ((threadIdx.x & 63) == 0) pb.x[(size_t)t * E + row] = v + r;
@@ -284,13 +320,11 @@ __global__ __launch_bounds__(MT) void k_pf_ffn_in(LlmDims d, const float *norm_w
                                                   PrefillBuffers pb, int nt) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int K = d.n_embd;
-    XRegs<NP> xr;
-    load_x(pb.x, norm_w, K, xr);
     int lo, hi;
     wave_range(gate.rows, lo, hi);
     Frag ga[CfgB<NP, 2>::U], gb[CfgB<NP, 2>::U];
     load_first_b<T, NP, 2>(gate, up, lo, hi, ga, gb);
-    prologue_rms(xr, pb.x, norm_w, K, d.eps, T != 8, smem, nt);
+    prologue_copy(pb.act, K, smem, nt);
     stream_rows_b<T, NP, 2>(gate, up, lo, hi, ga, gb, smem, nt, [&](int row, int t, float g, float u) {
         if ((threadIdx.x & 63) == 0) pb.h[(size_t)t * d.n_ff + row] = silu_f(g) * u;
     });
@@ -300,8 +334,6 @@ template <int NP, int T>
 __global__ __launch_bounds__(MT) void k_pf_ffn_down(LlmDims d, QMat down, PrefillBuffers pb, int nt, int rpw) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int K = down.k, E = d.n_embd;
-    XRegs<NP> xr;
-    load_x(pb.h, nullptr, K, xr);
     int lo, hi;
     wave_range(down.rows, lo, hi);
     const Resid rr = load_resid_b(pb.x, E, lo, hi, nt, rpw);
@@ -309,10 +341,7 @@ __global__ __launch_bounds__(MT) void k_pf_ffn_down(LlmDims d, QMat down, Prefil
     load_first_b<T, NP, 1>(down, down, lo, hi, ga, gb);
     float *res = resid_lds(smem, K, nt, rpw);
     store_resid_b(rr, res, nt, rpw);
-    for (int t = 0; t < nt; ++t) {
-        if (t) load_x(pb.h + (size_t)t * K, nullptr, K, xr);
-        plain_quant(xr, K, T != 8, carve_t(smem, K, t));
-    }
+    prologue_copy(pb.act, K, smem, nt);
     stream_rows_b<T, NP, 1>(down, down, lo, hi, ga, gb, smem, nt, [&](int row, int t, float v, float) {
         const float r = res[t * rpw + row - lo];
         if ((threadIdx.x & 63) == 0) pb.x[(size_t)t * E + row] = v + r;
@@ -338,13 +367,11 @@ __global__ __launch_bounds__(MT) void k_bt_lm_head(LlmDims d, const float *norm_
     __shared__ int bi_[MW];
     const int K = d.n_embd;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    XRegs<NP> xr;
-    load_x(pb.x, norm_w, K, xr);
     int lo, hi;
     wave_range(lm.rows, lo, hi);
     Frag ga[CfgB<NP, 1>::U], gb[CfgB<NP, 1>::U];
     load_first_b<T, NP, 1>(lm, lm, lo, hi, ga, gb);
-    prologue_rms(xr, pb.x, norm_w, K, d.eps, T != 8, smem, nt);
+    prologue_copy(pb.act, K, smem, nt);
     float *vals = reinterpret_cast<float *>(smem + pf_lds_bytes(K, nt, 0)) + (size_t)wave * nt * 128;
     stream_rows_b<T, NP, 1>(lm, lm, lo, hi, ga, gb, smem, nt, [&](int row, int t, float v, float) {
         if (lane == 0) vals[t * 128 + row - lo] = v;
@@ -482,8 +509,9 @@ int tokens_per_launch(int K, int nt, int rpw) {
     return n;
 }
 
-PrefillBuffers shifted(const LlmDims &d, const PrefillBuffers &pb, int t) {
+PrefillBuffers shifted(const LlmDims &d, const PrefillBuffers &pb, int t, int K) {
     PrefillBuffers q = pb;
+    q.act += (size_t)t * act_bytes(K);
     q.x += (size_t)t * d.n_embd;
     q.qkv += (size_t)t * (d.n_head + 2 * d.n_kv) * d.hd;
     q.h += (size_t)t * d.n_ff;
@@ -493,8 +521,30 @@ PrefillBuffers shifted(const LlmDims &d, const PrefillBuffers &pb, int t) {
     return q;
 }
 
+// act records of nt tokens (k_bt_quant): mode 0 RMSNorm(src) * w, 1 src, 2 attention merge
+void launch_quant(const LlmDims &d, int mode, const float *src, int K, const float *w, bool kq,
+                  const PrefillBuffers &pb, int nt, hipStream_t s) {
+    const int np = pick_np(K);
+    auto go = [&]<int NP>() {
+        const size_t lds = smem_bytes(K);
+        if (mode == 0)
+            hipLaunchKernelGGL((k_bt_quant<NP, 0>), dim3(nt), dim3(MT), lds, s, d, src, K, w, (int)kq, pb);
+        else if (mode == 1)
+            hipLaunchKernelGGL((k_bt_quant<NP, 1>), dim3(nt), dim3(MT), lds, s, d, src, K, w, (int)kq, pb);
+        else
+            hipLaunchKernelGGL((k_bt_quant<NP, 2>), dim3(nt), dim3(MT), lds, s, d, src, K, w, (int)kq, pb);
+    };
+    if (np == 1)
+        go.template operator()<1>();
+    else if (np == 3)
+        go.template operator()<3>();
+    else
+        go.template operator()<6>();
+}
+
 // Every layer for nt tokens of pb (residual streams pb.x in, out): one weight pass per
-// matvec launch (sub-launches only where a token range does not fit LDS).
+// matvec launch (sub-launches only where a token range does not fit LDS), each preceded by
+// the launch that quantizes its activations once (k_bt_quant).
 void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16 *kcache, _Float16 *vcache,
                    const PrefillBuffers &pb, int nt, int n_chunks, hipStream_t s) {
     const size_t layer_kv = (size_t)d.n_kv * d.n_ctx * d.hd;
@@ -502,11 +552,12 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
     // sub-launches over token ranges that fit LDS: f(t_off, n, shifted buffers)
     auto over_tokens = [&](int K, int rpw, auto &&f) {
         const int per = tokens_per_launch(K, nt, rpw);
-        for (int t = 0; t < nt; t += per) f(t, nt - t < per ? nt - t : per, shifted(d, pb, t));
+        for (int t = 0; t < nt; t += per) f(t, nt - t < per ? nt - t : per, shifted(d, pb, t, K));
     };
     for (int il = 0; il < n_layer; ++il) {
         const LayerW &L = layers[il];
         _Float16 *kc = kcache + il * layer_kv, *vc = vcache + il * layer_kv;
+        launch_quant(d, 0, pb.x, d.n_embd, L.attn_norm, L.wq.type != 8, pb, nt, s);
         {
             int GW, g_qk;
             attn_in_grid(d, L, GW, g_qk);
@@ -543,6 +594,7 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
             else
                 launch_pf_attention<64>(G, grid, s, d, kc, vc, pb);
         }
+        launch_quant(d, 2, nullptr, L.wo.k, nullptr, L.wo.type != 8, pb, nt, s);
         {
             const int grid = matvec_grid(d, L.wo.rows), rpw = rows_per_wave(L.wo.rows, grid);
             over_tokens(L.wo.k, rpw, [&](int, int n, const PrefillBuffers &q) {
@@ -553,6 +605,7 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
                 });
             });
         }
+        launch_quant(d, 0, pb.x, d.n_embd, L.ffn_norm, L.gate.type != 8, pb, nt, s);
         {
             const int grid = matvec_grid(d, L.gate.rows);
             over_tokens(d.n_embd, 0, [&](int, int n, const PrefillBuffers &q) {
@@ -563,6 +616,7 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
                 });
             });
         }
+        launch_quant(d, 1, pb.h, L.down.k, nullptr, L.down.type != 8, pb, nt, s);
         {
             const int grid = matvec_grid(d, L.down.rows), rpw = rows_per_wave(L.down.rows, grid);
             over_tokens(L.down.k, rpw, [&](int, int n, const PrefillBuffers &q) {
@@ -586,6 +640,8 @@ void launch_prefill_chunk(const LlmDims &d, const LayerW *layers, int n_layer, _
     launch_layers(d, layers, n_layer, kcache, vcache, pb, nt, n_chunks, s);
 }
 
+size_t prefill_act_bytes(int k_max) { return act_bytes(k_max) * kPrefillB; }
+
 size_t batch_lm_head_lds(const LlmDims &d, int B) { return pf_lds_bytes(d.n_embd, B, 0) + (size_t)MW * B * 128 * 4; }
 
 bool batch_supported(const LlmDims &d, int B) {
@@ -596,6 +652,7 @@ void launch_batch_step(const LlmDims &d, const LayerW *layers, int n_layer, _Flo
                        const float *out_norm, const QMat &lm, const QMat &tok_embd, const PrefillBuffers &pb,
                        const BatchBuffers &bb, int B, hipStream_t s) {
     launch_layers(d, layers, n_layer, kcache, vcache, pb, B, d.max_splits, s);
+    launch_quant(d, 0, pb.x, d.n_embd, out_norm, lm.type != 8, pb, B, s);
     const int nblk = lm_head_blocks(d);
     dispatch_nt(d.n_embd, lm.type, [&]<int NP, int T>() {
         allow_lds(k_bt_lm_head<NP, T>);

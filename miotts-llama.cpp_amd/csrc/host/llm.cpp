@@ -523,6 +523,7 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
     want(m->pf.qkv, (size_t)mio::kPrefillB * qkv);
     want(m->pf.h, (size_t)mio::kPrefillB * D.n_ff);
     want(m->pf.part, (size_t)mio::kPrefillB * D.n_head * D.max_splits * (D.hd + 4));
+    want(m->pf.act, mio::prefill_act_bytes(std::max(std::max(D.n_embd, D.n_ff), D.n_head * D.hd)));
     want(dr, (size_t)n_ctx * (D.hd / 2));
     want(m->d_iota, (size_t)n_ctx + mio::kPrefillB);
     size_t io_bytes = 0;
@@ -549,7 +550,7 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
     }
     if (!m->kc || !m->vc || !m->buf.x || !m->buf.qkv || !m->buf.h || !m->buf.logits ||
         !m->buf.part || !m->buf.smp || !m->buf.st || !m->d_cfg || !m->d_tokens || !m->d_force || !dr ||
-        !m->d_prompt || !m->pf.x || !m->pf.qkv || !m->pf.h || !m->pf.part || !m->d_iota) {
+        !m->d_prompt || !m->pf.x || !m->pf.qkv || !m->pf.h || !m->pf.part || !m->pf.act || !m->d_iota) {
         mio::set_error("llm_load: device allocation failed");
         return fail(MIO_ERR_OOM);
     }
