@@ -101,24 +101,45 @@ __device__ __forceinline__ void stream_rows_b(const QMat W0, const QMat W1, int 
     constexpr int RU = CfgB<NP, NM>::RU, U = CfgB<NP, NM>::U;
     const int K = W0.k;
     if (hi <= lo) return;
+    // TT tokens per iteration: their activation loads are in flight together and their dot
+    // / reduction chains interleave (the weight decode is shared); rows of the group past hi
+    // (a wave owning fewer rows than RU) are not dotted
+    constexpr int TT = NP == 1 ? 4 : (NP == 3 ? 2 : 1);
     auto consume = [&](const Frag (&F)[U], int r) {
-        for (int t = 0; t < nt; ++t) {
-            const Smem s = carve_t(smem, K, t);
-            float acc[RU * NM];
+        const int nr = min(RU, hi - r);
+        for (int t0 = 0; t0 < nt; t0 += TT) {
+            float acc[TT][RU * NM];
 #pragma unroll
-            for (int i = 0; i < RU * NM; ++i) acc[i] = 0.0f;
+            for (int j = 0; j < TT; ++j)
+#pragma unroll
+                for (int i = 0; i < RU * NM; ++i) acc[j][i] = 0.0f;
 #pragma unroll
             for (int p = 0; p < NP; ++p) {
-                const ALane al = load_alane<T>(s.a, K, p);
+                ALane al[TT];
 #pragma unroll
-                for (int i = 0; i < RU * NM; ++i) acc[i] += dot_frag<T>(F[i * NP + p], al, K, p);
+                for (int j = 0; j < TT; ++j) al[j] = load_alane<T>(carve_t(smem, K, min(t0 + j, nt - 1)).a, K, p);
+#pragma unroll
+                for (int ri = 0; ri < RU; ++ri) {
+                    if (ri < nr) {
+#pragma unroll
+                        for (int m = 0; m < NM; ++m)
+#pragma unroll
+                            for (int j = 0; j < TT; ++j)
+                                acc[j][ri * NM + m] += dot_frag<T>(F[(ri * NM + m) * NP + p], al[j], K, p);
+                    }
+                }
             }
 #pragma unroll
-            for (int ri = 0; ri < RU; ++ri) {
-                if (r + ri < hi) {
-                    const float v0 = row_total<T>(acc[ri * NM]);
-                    const float v1 = NM == 2 ? row_total<T>(acc[ri * NM + NM - 1]) : 0.0f;
-                    epi(r + ri, t, v0, v1);
+            for (int j = 0; j < TT; ++j) {
+                if (t0 + j < nt) {
+#pragma unroll
+                    for (int ri = 0; ri < RU; ++ri) {
+                        if (ri < nr) {
+                            const float v0 = row_total<T>(acc[j][ri * NM]);
+                            const float v1 = NM == 2 ? row_total<T>(acc[j][ri * NM + NM - 1]) : 0.0f;
+                            epi(r + ri, t0 + j, v0, v1);
+                        }
+                    }
                 }
             }
         }
@@ -274,14 +295,16 @@ __global__ __launch_bounds__(64) void k_pf_rope(LlmDims d, const float *q_norm, 
 // One workgroup per (128-position chunk, kv head, token): causal online softmax over the
 // chunk's positions <= the token's position in the token's own sequence, all rows read from
 // the cache (this launch's own rows were written by k_pf_rope); attend_chunk is the decode
-// step's sweep. Chunks past the token's position exit at once.
+// step's sweep. Chunks past the token's position exit at once. Grid (n_kv * nt, chunks):
+// consecutive workgroup ids are different (kv head, token) pairs of one chunk, so the
+// workgroups with work (the low chunks) spread over all XCDs instead of one.
 template <int HD, int G>
 __global__ __launch_bounds__(ATT_NT) void k_pf_attention(LlmDims d, const _Float16 *kc, const _Float16 *vc,
                                                          PrefillBuffers pb) {
     using C = AttCfg<HD>;
     __shared__ float qs[G][HD];
     __shared__ float wres[ATT_NW][G][HD + 2];
-    const int kvh = blockIdx.y, ch = blockIdx.x, t = blockIdx.z;
+    const int kvh = blockIdx.x % d.n_kv, t = blockIdx.x / d.n_kv, ch = blockIdx.y;
     const int pos = pb.pos[t * pb.pos_stride];
     const int t0 = ch * ATT_CHUNK;
     if (t0 > pos) return;
@@ -588,7 +611,7 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
                 hipLaunchKernelGGL((k_pf_rope<64>), grid, dim3(64), 0, s, d, L.q_norm, L.k_norm, kc, vc, pb);
         }
         {
-            const dim3 grid(n_chunks, d.n_kv, nt);
+            const dim3 grid(d.n_kv * nt, n_chunks);
             if (d.hd == 128)
                 launch_pf_attention<128>(G, grid, s, d, kc, vc, pb);
             else
