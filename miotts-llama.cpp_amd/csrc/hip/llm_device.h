@@ -22,11 +22,17 @@
 
 namespace mio {
 namespace {
+// Diagnostics (checkpoint trace, step timeline) compile into a kernel only where kDiag is
+// true: the decode kernels are instantiated twice (template flag DG, a local kDiag shadowing
+// this default) and the step graph uses the DG = false ones, whose kernel-argument loads
+// then issue together at entry (a diagnostic branch on a pointer argument serialized them
+// into several scalar-load round trips before the first weight load).
+constexpr bool kDiag = true;
 // Checkpoint timestamps (s_memtime) of workgroup 0 / thread 0, only when b.trace is set
 // (mio_hip_llm_trace_kernel); a uniform branch otherwise.
 #define MIO_TRACE(bufs, k)                                                                    \
     do {                                                                                      \
-        if ((bufs).trace && blockIdx.x == 0 && blockIdx.y == 0 && MIO_TIDX == 0) {        \
+        if (kDiag && (bufs).trace && blockIdx.x == 0 && blockIdx.y == 0 && MIO_TIDX == 0) { \
             asm volatile("" ::: "memory");                                                    \
             (bufs).trace[k] = __builtin_readcyclecounter();                                   \
             if ((k) == 0 || (k) == 15) (bufs).trace[16 + (k)] = __builtin_amdgcn_s_memrealtime(); \
@@ -40,14 +46,14 @@ namespace {
 #define MIO_TL_SLOT(bufs) ((bufs).tl + 8 * ((size_t)(bufs).seq * 256 + ((blockIdx.x + blockIdx.y * gridDim.x) & 255)))
 #define MIO_TL_AT(bufs, k)                                                                      \
     do {                                                                                        \
-        if ((bufs).tl && MIO_TIDX == 0) MIO_TL_SLOT(bufs)[k] = __builtin_amdgcn_s_memrealtime(); \
+        if (kDiag && (bufs).tl && MIO_TIDX == 0) MIO_TL_SLOT(bufs)[k] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
 #ifdef MIO_TL_DIAG
 // diagnostic builds: mark 6 = the LAST wave's first instruction (wave launch skew)
 #define MIO_TL_BEGIN(bufs)                                                                     \
     do {                                                                                       \
         MIO_TL_AT(bufs, 0);                                                                    \
-        if ((bufs).tl && MIO_TIDX == blockDim.x - 64) MIO_TL_SLOT(bufs)[6] = __builtin_amdgcn_s_memrealtime(); \
+        if (kDiag && (bufs).tl && MIO_TIDX == blockDim.x - 64) MIO_TL_SLOT(bufs)[6] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
 #else
 #define MIO_TL_BEGIN(bufs) MIO_TL_AT(bufs, 0)
@@ -66,7 +72,7 @@ namespace {
 #define MIO_DIAG_WAVE 7
 #endif
 #ifdef MIO_TL_DIAG
-#define MIO_TL_DIAGSLOT(bufs) ((bufs).tl ? MIO_TL_SLOT(bufs) : nullptr)
+#define MIO_TL_DIAGSLOT(bufs) ((kDiag && (bufs).tl) ? MIO_TL_SLOT(bufs) : nullptr)
 #define MIO_TL_MARK1(bufs)
 #else
 #define MIO_TL_DIAGSLOT(bufs) nullptr
@@ -783,7 +789,9 @@ __device__ inline void wave_range_n(int R, int &lo, int &hi, int b, int G, int w
     lo = ra + (rb - ra) * w / NW;
     hi = ra + (rb - ra) * (w + 1) / NW;
 }
-__device__ inline void wave_range(int R, int &lo, int &hi) { wave_range(R, lo, hi, blockIdx.x, gridDim.x); }
+__device__ inline void wave_range(const LlmDims &d, int R, int &lo, int &hi) {
+    wave_range(R, lo, hi, blockIdx.x, matvec_grid_n(d.n_wg, R));
+}
 
 
 // ------------------------------------------------------------------ embedding rows

@@ -142,7 +142,15 @@ void launch_step_kernel(int which, const LlmDims &d, const LayerW *layers, int i
 // Embedding of `token` (row of token_embd) -> b.x, and state reset to (pos, token).
 void launch_embed_token(const LlmDims &d, const QMat &tok_embd, const LlmBuffers &b, hipStream_t s);
 int lm_head_blocks(const LlmDims &d);
-// workgroups of a streaming matvec over `rows` rows; passes of 2048 weights for K
+// workgroups of a streaming matvec over `rows` rows (at least 8 rows per workgroup, at most
+// one workgroup per CU); passes of 2048 weights for K. Kernels recompute it from their
+// arguments instead of reading gridDim (an implicit kernel argument, one more scalar-load
+// round trip before the first weight load).
+__host__ __device__ inline int matvec_grid_n(int n_wg, int rows) {
+    int g = rows / 8;
+    g = g < n_wg ? g : n_wg;
+    return g < 2 ? 2 : g;
+}
 int matvec_grid(const LlmDims &d, int rows);
 int pick_np(int K);
 size_t matvec_lds(int K);

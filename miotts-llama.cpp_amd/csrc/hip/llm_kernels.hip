@@ -42,9 +42,10 @@ namespace {
 // straight-line code with no run-time type dispatch.
 // q|k rows (type TQ) on the first g_qk workgroups, v rows (type TV) on the rest; each
 // branch is WG-uniform and runs its own prologue, so neither path merges load counts.
-template <int NP, int TQ, int TV, int SU>
+template <int NP, int TQ, int TV, int SU, bool DG>
 __global__ __launch_bounds__(MT) void k_attn_in(LlmDims d, const float *norm_w, QMat wq, QMat wk, QMat wv,
                                                 int g_qk, LlmBuffers b) {
+    constexpr bool kDiag = DG;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int K = d.n_embd;
     const Smem s = carve(smem, K);
@@ -70,7 +71,7 @@ __global__ __launch_bounds__(MT) void k_attn_in(LlmDims d, const float *norm_w, 
         MIO_TL_END(b);
     MIO_TRACE(b, 15);
     } else {
-        wave_range(wv.rows, lo, hi, blockIdx.x - g_qk, gridDim.x - g_qk);
+        wave_range(wv.rows, lo, hi, blockIdx.x - g_qk, matvec_grid_n(d.n_wg, o2 + wv.rows) - g_qk);
         load_first<TV, NP, 1, SU>(wv, wv, lo, hi, ga, gb);
         rmsnorm_quant(xr, K, d.eps, TQ != 8, s, MIO_TL_DIAGSLOT(b));
         stream_rows<TV, NP, 1, SU>(wv, wv, lo, hi, ga, gb, s.a, [&](int row, float v, float) {
@@ -89,15 +90,16 @@ __device__ inline float lane_value(float v, int i) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), i));
 }
 
-template <int NP, int T, int SU>
+template <int NP, int T, int SU, bool DG>
 __global__ __launch_bounds__(MT) void k_attn_out(LlmDims d, QMat wo, LlmBuffers b) {
+    constexpr bool kDiag = DG;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     MIO_TRACE(b, 0);
     MIO_TL_BEGIN(b);
     const int K = wo.k;
     const Smem s = carve(smem, K);
     int lo, hi;
-    wave_range(wo.rows, lo, hi);
+    wave_range(d, wo.rows, lo, hi);
     const float xres = load_resid(b.x, lo, hi);
     Frag ga[Cfg<NP, SU>::U], gb[Cfg<NP, SU>::U];
     load_first<T, NP, 1, SU>(wo, wo, lo, hi, ga, gb);
@@ -114,9 +116,10 @@ __global__ __launch_bounds__(MT) void k_attn_out(LlmDims d, QMat wo, LlmBuffers 
     MIO_TRACE(b, 15);
 }
 
-template <int NP, int T, int SU>
+template <int NP, int T, int SU, bool DG>
 __global__ __launch_bounds__(MT) void k_ffn_in(LlmDims d, const float *norm_w, QMat gate, QMat up,
                                                LlmBuffers b) {
+    constexpr bool kDiag = DG;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     MIO_TRACE(b, 0);
     MIO_TL_BEGIN(b);
@@ -126,7 +129,7 @@ __global__ __launch_bounds__(MT) void k_ffn_in(LlmDims d, const float *norm_w, Q
     load_x(b.x, norm_w, K, xr);
     x_gate();
     int lo, hi;
-    wave_range(gate.rows, lo, hi);
+    wave_range(d, gate.rows, lo, hi);
     Frag ga[Cfg<NP, SU>::U], gb[Cfg<NP, SU>::U];
     load_first<T, NP, 2, SU>(gate, up, lo, hi, ga, gb);
     MIO_TRACE(b, 1);
@@ -136,13 +139,14 @@ __global__ __launch_bounds__(MT) void k_ffn_in(LlmDims d, const float *norm_w, Q
     MIO_TL_MARK(b, 2);
     stream_rows<T, NP, 2, SU>(gate, up, lo, hi, ga, gb, s.a, [&](int row, float g, float u) {
         if ((threadIdx.x & 63) == 0) b.h[row] = silu_f(g) * u;
-    }, INT_MAX, b.trace);
+    }, INT_MAX, DG ? b.trace : nullptr);
     MIO_TL_END(b);
     MIO_TRACE(b, 15);
 }
 
-template <int NP, int T, int SU>
+template <int NP, int T, int SU, bool DG>
 __global__ __launch_bounds__(MT) void k_ffn_down(LlmDims d, QMat down, LlmBuffers b) {
+    constexpr bool kDiag = DG;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     MIO_TRACE(b, 0);
     MIO_TL_BEGIN(b);
@@ -151,7 +155,7 @@ __global__ __launch_bounds__(MT) void k_ffn_down(LlmDims d, QMat down, LlmBuffer
     XRegs<NP> xr;
     load_x(b.h, nullptr, K, xr);
     int lo, hi;
-    wave_range(down.rows, lo, hi);
+    wave_range(d, down.rows, lo, hi);
     const float xres = load_resid(b.x, lo, hi);
     x_gate();
     Frag ga[Cfg<NP, SU>::U], gb[Cfg<NP, SU>::U];
@@ -164,7 +168,7 @@ __global__ __launch_bounds__(MT) void k_ffn_down(LlmDims d, QMat down, LlmBuffer
     stream_rows<T, NP, 1, SU>(down, down, lo, hi, ga, gb, s.a, [&](int row, float v, float) {
         const float r = lane_value(xres, row - lo);
         if ((threadIdx.x & 63) == 0) b.x[row] = v + r;
-    }, INT_MAX, b.trace);
+    }, INT_MAX, DG ? b.trace : nullptr);
     MIO_TL_END(b);
     MIO_TRACE(b, 15);
 }
@@ -172,8 +176,9 @@ __global__ __launch_bounds__(MT) void k_ffn_down(LlmDims d, QMat down, LlmBuffer
 // final RMSNorm (once per CU) + logits + per-workgroup Gumbel-max partial. A wave's rows
 // (<= 128) are parked one per lane (two registers) and the noise is drawn for 64 rows at
 // a time after the stream.
-template <int NP, int T>
+template <int NP, int T, bool DG>
 __global__ __launch_bounds__(MT) void k_lm_head(LlmDims d, const float *norm_w, QMat lm, LlmBuffers b) {
+    constexpr bool kDiag = DG;
     const SampleCfg sc = *b.cfg;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __shared__ float bs_[MW];
@@ -187,7 +192,7 @@ __global__ __launch_bounds__(MT) void k_lm_head(LlmDims d, const float *norm_w, 
     x_gate();
     const int step = b.st->step;
     int lo, hi;
-    wave_range(lm.rows, lo, hi);
+    wave_range(d, lm.rows, lo, hi);
     Frag ga[Cfg<NP>::U], gb[Cfg<NP>::U];
     load_first<T, NP, 1>(lm, lm, lo, hi, ga, gb);
     MIO_TRACE(b, 1);
@@ -243,9 +248,10 @@ __global__ __launch_bounds__(MT) void k_lm_head(LlmDims d, const float *norm_w, 
 // cache, then an online softmax over the chunk for the G q heads sharing the kv head. Its
 // partial record {O[HD], m, l} per q head is merged with the other chunks' in the prologue
 // of k_attn_out (the launch-boundary reduce: no extra launch, no in-kernel hand-off).
-template <int HD, int G>
+template <int HD, int G, bool DG>
 __global__ __launch_bounds__(ATT_NT) void k_attention(LlmDims d, const float *q_norm, const float *k_norm,
                                                       _Float16 *kc, _Float16 *vc, LlmBuffers b) {
+    constexpr bool kDiag = DG;
     using C = AttCfg<HD>;
     constexpr int PER = HD / 64;
     __shared__ float qs[G][HD];
@@ -307,26 +313,28 @@ __global__ __launch_bounds__(ATT_NT) void k_attention(LlmDims d, const float *q_
     }
     attend_chunk<HD, G>(qs, kr, vr, t0, pos, d.scale, wres,
                         b.part + ((size_t)(kvh * G) * d.max_splits + ch) * C::REC, (size_t)d.max_splits * C::REC,
-                        b.trace, MIO_TL_DIAGSLOT(b));
+                        DG ? b.trace : nullptr, MIO_TL_DIAGSLOT(b));
     MIO_TL_END(b);
     MIO_TRACE(b, 15);
 }
 
-template <int HD>
+template <int HD, bool DG>
 void launch_attention(int G, dim3 grid, hipStream_t s, const LlmDims &d, const float *qn, const float *kn,
                       _Float16 *kc, _Float16 *vc, const LlmBuffers &b) {
     switch (G) {
-        case 1: hipLaunchKernelGGL((k_attention<HD, 1>), grid, dim3(ATT_NT), 0, s, d, qn, kn, kc, vc, b); break;
-        case 2: hipLaunchKernelGGL((k_attention<HD, 2>), grid, dim3(ATT_NT), 0, s, d, qn, kn, kc, vc, b); break;
-        case 3: hipLaunchKernelGGL((k_attention<HD, 3>), grid, dim3(ATT_NT), 0, s, d, qn, kn, kc, vc, b); break;
-        case 4: hipLaunchKernelGGL((k_attention<HD, 4>), grid, dim3(ATT_NT), 0, s, d, qn, kn, kc, vc, b); break;
-        case 8: hipLaunchKernelGGL((k_attention<HD, 8>), grid, dim3(ATT_NT), 0, s, d, qn, kn, kc, vc, b); break;
+        case 1: hipLaunchKernelGGL((k_attention<HD, 1, DG>), grid, dim3(ATT_NT), 0, s, d, qn, kn, kc, vc, b); break;
+        case 2: hipLaunchKernelGGL((k_attention<HD, 2, DG>), grid, dim3(ATT_NT), 0, s, d, qn, kn, kc, vc, b); break;
+        case 3: hipLaunchKernelGGL((k_attention<HD, 3, DG>), grid, dim3(ATT_NT), 0, s, d, qn, kn, kc, vc, b); break;
+        case 4: hipLaunchKernelGGL((k_attention<HD, 4, DG>), grid, dim3(ATT_NT), 0, s, d, qn, kn, kc, vc, b); break;
+        case 8: hipLaunchKernelGGL((k_attention<HD, 8, DG>), grid, dim3(ATT_NT), 0, s, d, qn, kn, kc, vc, b); break;
         default: break;
     }
 }
 
 // ------------------------------------------------------------------ sampler / embedding
+template <bool DG>
 __global__ __launch_bounds__(ST) void k_sample(LlmDims d, QMat emb, int nblk, LlmBuffers b) {
+    constexpr bool kDiag = DG;
     const SampleCfg sc = *b.cfg;
     __shared__ float bs_[ST / 64];
     __shared__ int bi_[ST / 64];
@@ -384,11 +392,8 @@ __global__ __launch_bounds__(ST) void k_embed(LlmDims d, QMat emb, LlmBuffers b)
 int pick_np(int K) { return K <= 2048 ? 1 : (K <= 6144 ? 3 : 6); }
 
 // at least MW rows per workgroup (every wave owns >= 1 row), at most one workgroup per CU
-int matvec_grid(const LlmDims &d, int rows) {
-    int g = rows / MW;
-    g = g < d.n_wg ? g : d.n_wg;
-    return g < 2 ? 2 : g;
-}
+static_assert(MW == 8, "matvec_grid_n assumes 8 waves per workgroup");
+int matvec_grid(const LlmDims &d, int rows) { return matvec_grid_n(d.n_wg, rows); }
 
 int lm_head_blocks(const LlmDims &d) { return matvec_grid(d, d.n_vocab); }
 
@@ -437,6 +442,8 @@ void launch_step_kernel(int which, const LlmDims &d, const LayerW *layers, int i
                         const LlmBuffers &b, hipStream_t s) {
     const size_t layer_kv = (size_t)d.n_kv * d.n_ctx * d.hd;
     const int G = d.n_head / d.n_kv;
+    // diagnostic instantiations only when a trace / timeline buffer is attached
+    auto go_dg = [&]<bool DG>() {
     switch (which) {
         case 0: {
             const LayerW &L = layers[il];
@@ -449,7 +456,7 @@ void launch_step_kernel(int which, const LlmDims &d, const LayerW *layers, int i
             dispatch_nt(d.n_embd, L.wq.type, [&]<int NP, int TQ>() {
                 auto go = [&]<int TV>() {
                     dispatch_su<NP>(pick_su(un, NP), [&]<int SU>() {
-                        hipLaunchKernelGGL((k_attn_in<NP, TQ, TV, SU>), dim3(GW), dim3(MT), lds, s, d, L.attn_norm,
+                        hipLaunchKernelGGL((k_attn_in<NP, TQ, TV, SU, DG>), dim3(GW), dim3(MT), lds, s, d, L.attn_norm,
                                            L.wq, L.wk, L.wv, g_qk, b);
                     });
                 };
@@ -468,9 +475,9 @@ void launch_step_kernel(int which, const LlmDims &d, const LayerW *layers, int i
             const LayerW &L = layers[il];
             const dim3 grid(d.max_splits, d.n_kv);
             if (d.hd == 128)
-                launch_attention<128>(G, grid, s, d, L.q_norm, L.k_norm, kcache + il * layer_kv, vcache + il * layer_kv, b);
+                launch_attention<128, DG>(G, grid, s, d, L.q_norm, L.k_norm, kcache + il * layer_kv, vcache + il * layer_kv, b);
             else
-                launch_attention<64>(G, grid, s, d, L.q_norm, L.k_norm, kcache + il * layer_kv, vcache + il * layer_kv, b);
+                launch_attention<64, DG>(G, grid, s, d, L.q_norm, L.k_norm, kcache + il * layer_kv, vcache + il * layer_kv, b);
             break;
         }
         case 2: {
@@ -478,7 +485,7 @@ void launch_step_kernel(int which, const LlmDims &d, const LayerW *layers, int i
             const int grid = matvec_grid(d, L.wo.rows);
             dispatch_nt(L.wo.k, L.wo.type, [&]<int NP, int T>() {
                 dispatch_su<NP>(pick_su(max_wave_units(L.wo.rows, grid, NP, 1), NP), [&]<int SU>() {
-                    hipLaunchKernelGGL((k_attn_out<NP, T, SU>), dim3(grid), dim3(MT), mv_lds(L.wo.k), s, d, L.wo, b);
+                    hipLaunchKernelGGL((k_attn_out<NP, T, SU, DG>), dim3(grid), dim3(MT), mv_lds(L.wo.k), s, d, L.wo, b);
                 });
             });
             break;
@@ -488,7 +495,7 @@ void launch_step_kernel(int which, const LlmDims &d, const LayerW *layers, int i
             const int grid = matvec_grid(d, L.gate.rows);
             dispatch_nt(d.n_embd, L.gate.type, [&]<int NP, int T>() {
                 dispatch_su<NP>(pick_su(max_wave_units(L.gate.rows, grid, NP, 2), NP), [&]<int SU>() {
-                    hipLaunchKernelGGL((k_ffn_in<NP, T, SU>), dim3(grid), dim3(MT), mv_lds(d.n_embd), s, d, L.ffn_norm,
+                    hipLaunchKernelGGL((k_ffn_in<NP, T, SU, DG>), dim3(grid), dim3(MT), mv_lds(d.n_embd), s, d, L.ffn_norm,
                                        L.gate, L.up, b);
                 });
             });
@@ -499,7 +506,7 @@ void launch_step_kernel(int which, const LlmDims &d, const LayerW *layers, int i
             const int grid = matvec_grid(d, L.down.rows);
             dispatch_nt(L.down.k, L.down.type, [&]<int NP, int T>() {
                 dispatch_su<NP>(pick_su(max_wave_units(L.down.rows, grid, NP, 1), NP), [&]<int SU>() {
-                    hipLaunchKernelGGL((k_ffn_down<NP, T, SU>), dim3(grid), dim3(MT), mv_lds(L.down.k), s, d, L.down,
+                    hipLaunchKernelGGL((k_ffn_down<NP, T, SU, DG>), dim3(grid), dim3(MT), mv_lds(L.down.k), s, d, L.down,
                                        b);
                 });
             });
@@ -507,15 +514,20 @@ void launch_step_kernel(int which, const LlmDims &d, const LayerW *layers, int i
         }
         case 6:
             dispatch_nt(d.n_embd, lm.type, [&]<int NP, int T>() {
-                hipLaunchKernelGGL((k_lm_head<NP, T>), dim3(lm_head_blocks(d)), dim3(MT), mv_lds(d.n_embd), s, d,
+                hipLaunchKernelGGL((k_lm_head<NP, T, DG>), dim3(lm_head_blocks(d)), dim3(MT), mv_lds(d.n_embd), s, d,
                                    out_norm, lm, b);
             });
             break;
         case 7:
-            hipLaunchKernelGGL(k_sample, dim3(1), dim3(ST), 0, s, d, tok_embd, lm_head_blocks(d), b);
+            hipLaunchKernelGGL(k_sample<DG>, dim3(1), dim3(ST), 0, s, d, tok_embd, lm_head_blocks(d), b);
             break;
         default: break;
     }
+    };
+    if (b.tl || b.trace)
+        go_dg.template operator()<true>();
+    else
+        go_dg.template operator()<false>();
 }
 
 
@@ -529,7 +541,7 @@ __global__ __launch_bounds__(MT) void k_debug_matvec(QMat W, const float *x, flo
     XRegs<NP> xr;
     load_x(x, nullptr, K, xr);
     int lo, hi;
-    wave_range(W.rows, lo, hi);
+    wave_range(W.rows, lo, hi, blockIdx.x, gridDim.x);
     Frag ga[Cfg<NP>::U], gb[Cfg<NP>::U];
     load_first<T, NP, 1>(W, W, lo, hi, ga, gb);
     plain_quant(xr, K, T != 8, s);

@@ -325,7 +325,7 @@ __global__ __launch_bounds__(MT) void k_pf_attn_out(LlmDims d, QMat wo, PrefillB
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int K = wo.k, E = d.n_embd;
     int lo, hi;
-    wave_range(wo.rows, lo, hi);
+    wave_range(d, wo.rows, lo, hi);
     const Resid xr = load_resid_b(pb.x, E, lo, hi, nt, rpw);
     Frag ga[CfgB<NP, 1>::U], gb[CfgB<NP, 1>::U];
     load_first_b<T, NP, 1>(wo, wo, lo, hi, ga, gb);
@@ -344,7 +344,7 @@ __global__ __launch_bounds__(MT) void k_pf_ffn_in(LlmDims d, const float *norm_w
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int K = d.n_embd;
     int lo, hi;
-    wave_range(gate.rows, lo, hi);
+    wave_range(d, gate.rows, lo, hi);
     Frag ga[CfgB<NP, 2>::U], gb[CfgB<NP, 2>::U];
     load_first_b<T, NP, 2>(gate, up, lo, hi, ga, gb);
     prologue_copy(pb.act, K, smem, nt);
@@ -358,7 +358,7 @@ __global__ __launch_bounds__(MT) void k_pf_ffn_down(LlmDims d, QMat down, Prefil
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int K = down.k, E = d.n_embd;
     int lo, hi;
-    wave_range(down.rows, lo, hi);
+    wave_range(d, down.rows, lo, hi);
     const Resid rr = load_resid_b(pb.x, E, lo, hi, nt, rpw);
     Frag ga[CfgB<NP, 1>::U], gb[CfgB<NP, 1>::U];
     load_first_b<T, NP, 1>(down, down, lo, hi, ga, gb);
@@ -391,7 +391,7 @@ __global__ __launch_bounds__(MT) void k_bt_lm_head(LlmDims d, const float *norm_
     const int K = d.n_embd;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     int lo, hi;
-    wave_range(lm.rows, lo, hi);
+    wave_range(d, lm.rows, lo, hi);
     Frag ga[CfgB<NP, 1>::U], gb[CfgB<NP, 1>::U];
     load_first_b<T, NP, 1>(lm, lm, lo, hi, ga, gb);
     prologue_copy(pb.act, K, smem, nt);
