@@ -353,6 +353,18 @@ struct XRegs {
     float4 w[XV];
 };
 
+// Placed after a launch's first weight loads: nothing computed from x (or the norm weight)
+// may be hoisted above them, so the wait for x is never issued before the weight stream is
+// (measured 0.813 -> 0.801 ms/token together with the attention kernel's argument
+// ordering; forcing every kernel argument into the first scalar round trip was slower).
+template <int XV>
+__device__ __forceinline__ void x_after_weights(XRegs<XV> &xr) {
+#pragma unroll
+    for (int i = 0; i < XV; ++i)
+        asm volatile("" : "+v"(xr.v[i].x), "+v"(xr.v[i].y), "+v"(xr.v[i].z), "+v"(xr.v[i].w), "+v"(xr.w[i].x),
+                     "+v"(xr.w[i].y), "+v"(xr.w[i].z), "+v"(xr.w[i].w));
+}
+
 template <int XV>
 __device__ inline void load_x(const float *x, const float *w, int K, XRegs<XV> &xr) {
     const auto rx = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(x), 0, K * 4, 0x00020000);

@@ -60,6 +60,7 @@ __global__ __launch_bounds__(MT) void k_attn_in(LlmDims d, const float *norm_w, 
     if ((int)blockIdx.x < g_qk) {
         wave_range(o2, lo, hi, blockIdx.x, g_qk);
         load_first<TQ, NP, 1, SU>(wq, wk, lo, hi, ga, gb, o1);
+        x_after_weights(xr);
         MIO_TRACE(b, 1);
     MIO_TL_MARK1(b);
         rmsnorm_quant(xr, K, d.eps, TQ != 8, s, MIO_TL_DIAGSLOT(b));
@@ -73,6 +74,7 @@ __global__ __launch_bounds__(MT) void k_attn_in(LlmDims d, const float *norm_w, 
     } else {
         wave_range(wv.rows, lo, hi, blockIdx.x - g_qk, matvec_grid_n(d.n_wg, o2 + wv.rows) - g_qk);
         load_first<TV, NP, 1, SU>(wv, wv, lo, hi, ga, gb);
+        x_after_weights(xr);
         rmsnorm_quant(xr, K, d.eps, TQ != 8, s, MIO_TL_DIAGSLOT(b));
         stream_rows<TV, NP, 1, SU>(wv, wv, lo, hi, ga, gb, s.a, [&](int row, float v, float) {
             if ((threadIdx.x & 63) == 0) b.qkv[o2 + row] = v;
@@ -132,6 +134,7 @@ __global__ __launch_bounds__(MT) void k_ffn_in(LlmDims d, const float *norm_w, Q
     wave_range(d, gate.rows, lo, hi);
     Frag ga[Cfg<NP, SU>::U], gb[Cfg<NP, SU>::U];
     load_first<T, NP, 2, SU>(gate, up, lo, hi, ga, gb);
+    x_after_weights(xr);
     MIO_TRACE(b, 1);
     MIO_TL_MARK1(b);
     rmsnorm_quant(xr, K, d.eps, T != 8, s, MIO_TL_DIAGSLOT(b));
@@ -160,6 +163,7 @@ __global__ __launch_bounds__(MT) void k_ffn_down(LlmDims d, QMat down, LlmBuffer
     x_gate();
     Frag ga[Cfg<NP, SU>::U], gb[Cfg<NP, SU>::U];
     load_first<T, NP, 1, SU>(down, down, lo, hi, ga, gb);
+    x_after_weights(xr);
     MIO_TRACE(b, 1);
     MIO_TL_MARK1(b);
     plain_quant(xr, K, T != 8, s, MIO_TL_DIAGSLOT(b));
@@ -195,6 +199,7 @@ __global__ __launch_bounds__(MT) void k_lm_head(LlmDims d, const float *norm_w, 
     wave_range(d, lm.rows, lo, hi);
     Frag ga[Cfg<NP>::U], gb[Cfg<NP>::U];
     load_first<T, NP, 1>(lm, lm, lo, hi, ga, gb);
+    x_after_weights(xr);
     MIO_TRACE(b, 1);
     MIO_TL_MARK1(b);
     rmsnorm_quant(xr, K, d.eps, T != 8, s, MIO_TL_DIAGSLOT(b));
@@ -261,6 +266,11 @@ __global__ __launch_bounds__(ATT_NT) void k_attention(LlmDims d, const float *q_
     MIO_TRACE(b, 0);
     MIO_TL_BEGIN(b);
     const int kvh = blockIdx.y, ch = blockIdx.x;
+    // every kernel argument the workgroup uses is loaded in the round trip that fetches
+    // b.st (without this the compiler sinks them below the pos-dependent exit: a third
+    // scalar-load round trip before the first K/V load)
+    asm volatile("" ::"s"(kc), "s"(vc), "s"(d.n_ctx), "s"(b.qkv), "s"(b.rope), "s"(q_norm), "s"(k_norm),
+                 "s"(b.part), "s"(d.max_splits));
     const int pos = b.st->pos;
     const int t0 = ch * ATT_CHUNK;
     if (t0 > pos) return;
