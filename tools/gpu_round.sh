@@ -14,4 +14,5 @@ timeout -k 10 400 python -u bench.py > $out/bench.json 2> $out/bench.err
 # (same kernels, same arguments; MIO_NO_GRAPH=1, csrc/host/llm.cpp llm_run)
 MIO_NO_GRAPH=1 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $out/prof -o run -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline > $out/bench_prof.json 2> $out/prof.err
 find $out/prof -name '*kernel_stats.csv' -exec cp {} $out/kernel_stats.csv \;
+rm -rf $out/prof  # the full trace exceeds gpurun's 64 MiB copy-back
 echo done
