@@ -262,7 +262,9 @@ def main():
 
     steps_total = a.steps * a.utts_per_step
     out = {
-        "metric": "realtime factor (audio s / wall s) + stage ms llm/codec/istft, 1.7B Q4_K_M",
+        # BASELINE.json's metric (quoted on preset 3); other presets name their own model
+        "metric": "realtime factor (audio s / wall s) + stage ms llm/codec/istft, "
+                  + PRESETS[a.preset].replace("MioTTS-", ""),
         "value": round(value, 3),
         "unit": "x realtime (audio s / wall s)",
         "n_gpus": world,
@@ -272,7 +274,8 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "int8-dot (q4_K/q6_K x q8_K) + f32/f16 codec",
+        "dtype": ("int8-dot (q8_0 x q8_0)" if "Q8_0" in PRESETS[a.preset] else "int8-dot (q4_K/q6_K x q8_K)")
+                 + " + f32/f16 codec",
         "data": "synthetic",
         "config": {"workload": f"{PRESETS[a.preset]} single utterance, {a.tokens} speech tokens -> "
                                f"MioCodec -> iSTFT ({a.tokens * 1764 / 44100:.1f} s audio) per GPU",
