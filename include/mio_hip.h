@@ -61,6 +61,16 @@ int mio_hip_memset(mio_hip_device *d, void *dst, int value, size_t bytes);
 int mio_hip_timer_mark(mio_hip_device *d, void *stream, int slot);
 int mio_hip_timer_elapsed(mio_hip_device *d, int slot_a, int slot_b, float *ms);
 
+/* PCM epilogue on the device: the optional peak normalisation of test-to-speech.cpp:232-243
+ * (gain 0.95 / max|s| when max|s| > 1e-8; skipped when normalize == 0) and the sample
+ * conversion of wav_write (wav-writer.cpp:24-44: int16(clamp(s * 32767)), truncated) of n
+ * samples. samples (16-byte aligned) and pcm16 are device pointers; the 44-byte RIFF header
+ * stays with the host writer. peak (host, may be NULL) receives max|s| of the normalising pass
+ * (0 when normalize == 0) and synchronizes the stream. Bit-exact with the host path. One call
+ * at a time per device. */
+int mio_hip_pcm_finish(mio_hip_device *d, const float *samples, int64_t n, int normalize,
+                       int16_t *pcm16, float *peak, void *stream);
+
 /* ---------------- iSTFT ----------------
  * Replaces istft_cache(n_fft, win_length) (istft.h:6-30, istft.cpp:7-32) and
  * istft(spec, n_frames, hop, cache) (istft.h:38-42, istft.cpp:68-108).

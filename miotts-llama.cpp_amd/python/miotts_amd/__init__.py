@@ -63,6 +63,7 @@ def _declare(L: ctypes.CDLL) -> None:
         "mio_hip_memset": (c_int, [_vp, _vp, c_int, c_size]),
         "mio_hip_timer_mark": (c_int, [_vp, _vp, c_int]),
         "mio_hip_timer_elapsed": (c_int, [_vp, c_int, c_int, _f32p]),
+        "mio_hip_pcm_finish": (c_int, [_vp, _vp, ctypes.c_int64, c_int, _vp, _f32p, _vp]),
         "mio_hip_istft_create": (c_int, [_vp, c_int, c_int, ctypes.POINTER(_vp)]),
         "mio_hip_istft_destroy": (None, [_vp]),
         "mio_hip_istft_out_len": (c_int, [_vp, c_int, c_int, ctypes.POINTER(c_int)]),
@@ -216,6 +217,19 @@ class DeviceArray:
             self.free()
         except Exception:
             pass
+
+
+def pcm_finish(dev: "Device", samples: "DeviceArray", n: int, normalize: bool,
+               out: Optional["DeviceArray"] = None):
+    """Device PCM epilogue (mio_hip_pcm_finish): optional peak normalisation
+    (test-to-speech.cpp:232-243) + int16(clamp(s * 32767)) of wav_write (wav-writer.cpp:24-44).
+    Returns (int16 samples on the host, peak max|s| or 0.0 when not normalizing)."""
+    if out is None:
+        out = dev.empty((max(n, 1),), np.int16)
+    peak = ctypes.c_float(0)
+    check(lib().mio_hip_pcm_finish(dev.h, samples.ptr if n else None, n, 1 if normalize else 0,
+                                   out.ptr if n else None, ctypes.byref(peak), None))
+    return out.numpy()[:n], peak.value
 
 
 class Istft:
