@@ -231,6 +231,20 @@ def main():
     d2h_s = (time.perf_counter() - t0) / 3
     value_pcie = audio_s / (elapsed + d2h_s * a.steps * a.utts_per_step * world)
 
+    # WAV epilogue on the device (mio_hip_pcm_finish: peak normalise + PCM16) of the last
+    # utterance, HIP events on the device stream; reported beside the stage times
+    n_pcm = a.tokens * codec.samples_per_token
+    d_pcm16 = dev.empty((n_pcm,), np.int16)
+    lib = m.lib()
+    pf_ms = []
+    for _ in range(4):
+        dev.mark(14)
+        m.check(lib.mio_hip_pcm_finish(dev.h, d_pcm.ptr, n_pcm, 1, d_pcm16.ptr, None, None))
+        dev.mark(15)
+        dev.sync()
+        pf_ms.append(dev.elapsed_ms(14, 15))
+    pcm_finish_ms = round(min(pf_ms[1:]), 4)
+
     # roofline: dominant kernel inside the captured step graph (timeline), then HIP events
     tl = llm.timeline()
     nl = tl.shape[0]
@@ -281,7 +295,8 @@ def main():
                                f"MioCodec -> iSTFT ({a.tokens * 1764 / 44100:.1f} s audio) per GPU",
                    "model": PRESETS[a.preset], "global_batch": world * a.utts_per_step,
                    "seq_len": a.tokens, "parallelism": f"utterance-sharded x{world} (no collective)"},
-        "stage_ms": {k: round(v / steps_total, 3) for k, v in stage.items()},
+        "stage_ms": {**{k: round(v / steps_total, 3) for k, v in stage.items()},
+                     "pcm_finish_ms": pcm_finish_ms},
         "llm_ms_per_token": round(stage["llm_ms"] / steps_total / a.tokens, 4),
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
