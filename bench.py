@@ -10,24 +10,34 @@ PCM left in HBM (`value`; the PCIe-inclusive rate with the PCM copied to host me
 reported beside it as `value_pcie_inclusive`). Weights are synthetic (no checkpoints
 offline) with the published shapes; "data": "synthetic".
 
-Multi-GPU: one process per GPU (torchrun), each rank synthesizes its own utterances
-(utterances are independent: no collective on the data path, "scaling": "weak"); a gloo
-barrier brackets the timed region and the max elapsed over ranks is used.
+Multi-GPU (`--gpus N`): one process per GPU. Under torchrun (WORLD_SIZE set) this process
+is one rank; otherwise, for N > 1, it starts N fresh child processes of itself (RANK /
+LOCAL_RANK / WORLD_SIZE / MASTER_* set) BEFORE anything touches the GPU and exits with
+their status. Each rank synthesizes its own utterances (independent: no collective on the
+data path, "scaling": "weak"); a gloo barrier brackets the timed region and the max
+elapsed over ranks is used. `--utts-per-gpu B` makes every step B utterances decoded
+together by the batched engine on each rank (BASELINE configs[3], C4: `--preset 4
+--utts-per-gpu 8 --gpus 8` = 64 utterances of the 2.6B Q8_0 model over 8 GPUs).
 
-roofline: the dominant decode-step kernel (largest time per token), timed inside the
-captured step graph by the step timeline (first workgroup start -> last workgroup end of
-every launch, s_memrealtime, mio_hip_llm_timeline) right after the timed region:
-achieved = its algorithmic bytes per launch (GGUF bytes of the matrices it streams + its
-activations) / mean launch duration; peak = 8 TB/s HBM3E. traffic = the same kernel's
-HBM bytes per launch from rocprofv3 PMC (FETCH_SIZE x 2 on gfx950 + WRITE_SIZE,
-profiles/pmc_traffic.json, tools/pmc_traffic.py). HIP-event timing of back-to-back
-launches of the same kernel is reported as event_avg_launch_us (cache-warm).
+roofline: the decode-step kernel with the largest in-graph time per token, timed inside
+the captured step graph by the step timeline (first workgroup start -> last workgroup end
+of every launch, s_memrealtime, mio_hip_llm_timeline) right after the timed region, at
+the position the utterance ended on: achieved = its algorithmic bytes per launch (GGUF
+bytes of the matrices it streams + activations; attention: the F16 K/V rows of positions
+<= pos + q/k/v in + partial records out, mio_hip_llm_time_kernel) / mean launch duration;
+peak = 8 TB/s HBM3E. `frac_event` = the same bytes over the HIP-event average of
+back-to-back launches of that kernel. traffic = the same kernel's HBM bytes per launch
+from rocprofv3 PMC (FETCH_SIZE x 2 on gfx950 + WRITE_SIZE, profiles/pmc_traffic.json,
+tools/pmc_traffic.py). step_* = all bytes of one decode step over the step's graph wall.
 cpu_baseline: the C oracle (oracle/, "port") on rank 0 at N=1 only, timed on a bounded
-sample (decode steps + codec/iSTFT of a few codes) and extrapolated to one utterance.
+sample (decode steps at positions spread over 0..700 + codec/iSTFT of a few codes) and
+extrapolated to one utterance, at the box's thread share and at 4 threads.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -41,21 +51,49 @@ PRESETS = {2: "MioTTS-0.1B Q8_0", 3: "MioTTS-1.7B Q4_K_M", 4: "MioTTS-2.6B Q8_0"
 PROMPT = "こんにちは、今日はいい天気ですね。"  # README.md:83, SURVEY 8(d)
 
 
-def parse_args():
+def parse_args(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--preset", type=int, default=3, choices=sorted(PRESETS))
     p.add_argument("--tokens", type=int, default=700)
-    p.add_argument("--utts-per-step", type=int, default=1)
+    p.add_argument("--utts-per-step", type=int, default=1,
+                   help="single-utterance syntheses per step, one after another")
+    p.add_argument("--utts-per-gpu", type=int, default=1,
+                   help="B > 1: each step decodes B utterances together per GPU (batched engine)")
     p.add_argument("--workdir", default=os.environ.get("MIOTTS_BENCH_DIR", "/tmp/miotts_bench"))
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-tokens", type=int, default=12)
+    p.add_argument("--cpu-tokens", type=int, default=64)
     p.add_argument("--cpu-codes", type=int, default=40)
     p.add_argument("--batch", type=int, default=8,
                    help="also time B utterances decoded together per GPU (N=1 only; 0 = skip)")
-    return p.parse_args()
+    p.add_argument("--no-roofline", action="store_true")
+    p.add_argument("--launcher-selftest", action="store_true",
+                   help="tests only: the launcher + timed region with a CPU sleep as the utterance, no GPU; "
+                        "prints a 'launcher self-test' line, never the metric")
+    return p.parse_args(argv)
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int, argv) -> int:
+    """N fresh child processes of this script, one per GPU (rank i on LOCAL_RANK i), started
+    before this process has touched the GPU; returns the worst child exit status."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    rc = 0
+    for p in procs:
+        rc = max(rc, p.wait())
+    return rc
 
 
 def prompt_tokens(text: str):
@@ -85,57 +123,79 @@ def ensure_files(workdir, preset, rank, barrier):
     return llm, codec, voice
 
 
-def cpu_baseline(llm_path, codec_path, voice_path, n_tok, n_codes, utt_tokens):
+def cpu_baseline(llm_path, codec_path, voice_path, n_tok, n_codes, utt_tokens, threads):
+    """The C oracle ("port") on `threads` OpenMP threads: n_tok decode steps at positions
+    spread evenly over [0, utt_tokens) (attention cost grows with the position; the cache
+    rows it reads hold zeros, which costs the same as real rows) + codec/iSTFT of n_codes,
+    extrapolated to one utterance of utt_tokens tokens."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import numpy as np
     import miotts_amd as m
     import pyoracle
-    o = pyoracle.Llm(llm_path, 256)
-    t0 = time.perf_counter()
-    for pos in range(n_tok):
-        o.eval(m.SYNTH_SPEECH0 + (pos * 97) % 12800, pos)
-    t_tok = (time.perf_counter() - t0) / n_tok
-    c = pyoracle.Codec(codec_path)
-    emb = m.read_voice(voice_path)
-    codes = (np.arange(n_codes) * 7919) % 12800
-    t0 = time.perf_counter()
-    c.decode_pcm(codes, emb)
-    t_code = (time.perf_counter() - t0) / n_codes
+    prev = pyoracle.set_threads(threads)
+    try:
+        o = pyoracle.Llm(llm_path, utt_tokens + 8)
+        positions = [int(p) for p in np.linspace(0, utt_tokens - 1, n_tok)]
+        o.eval(m.SYNTH_SPEECH0, 0)  # warm (page in the weights)
+        t0 = time.perf_counter()
+        for i, pos in enumerate(positions):
+            o.eval(m.SYNTH_SPEECH0 + (i * 97) % 12800, pos)
+        t_tok = (time.perf_counter() - t0) / n_tok
+        c = pyoracle.Codec(codec_path)
+        emb = m.read_voice(voice_path)
+        codes = (np.arange(n_codes) * 7919) % 12800
+        t0 = time.perf_counter()
+        c.decode_pcm(codes, emb)
+        t_code = (time.perf_counter() - t0) / n_codes
+    finally:
+        pyoracle.set_threads(prev)
     wall = utt_tokens * t_tok + utt_tokens * t_code
     audio = utt_tokens * 1764 / 44100.0
-    cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    return {"value": round(audio / wall, 4), "unit": "x realtime (audio s / wall s)", "cores": cores,
+    return {"value": round(audio / wall, 4), "unit": "x realtime (audio s / wall s)", "cores": threads,
             "kind": "port",
-            "sample": f"oracle decode of {n_tok} tokens ({t_tok * 1e3:.1f} ms/token) + codec+iSTFT of "
-                      f"{n_codes} codes ({t_code * 1e3:.2f} ms/code), extrapolated to {utt_tokens} tokens"}
+            "sample": f"oracle decode of {n_tok} tokens at positions 0..{utt_tokens - 1} "
+                      f"({t_tok * 1e3:.1f} ms/token) + codec+iSTFT of {n_codes} codes "
+                      f"({t_code * 1e3:.2f} ms/code), extrapolated to {utt_tokens} tokens"}
 
 
 def batched_line(a, llm, codec, dev, prompt, allow, d_emb, d_pcm):
     """B utterances per GPU decoded together (mio_hip_llm_generate_batch: one weight pass per
     step for all B), then each through MioCodec + iSTFT into HBM. Reported beside `value`
     (which stays the single-utterance workload BASELINE's metric is quoted on)."""
-    import numpy as np
-    import miotts_amd as m
     B = a.batch
-    seeds = [utterance_seed(0, 5000 + b) for b in range(B)]
-    llm.generate_batch([prompt] * B, a.tokens, 0.8, seeds, allow=allow)  # warm (graph capture)
+    step = make_batch_step(a.tokens, B, llm, codec, dev, prompt, allow, d_emb, d_pcm)
+    step(0, False)  # warm (graph capture)
     dev.sync()
     t0 = time.perf_counter()
-    outs = llm.generate_batch([prompt] * B, a.tokens, 0.8, seeds, allow=allow, check_interval=64)
-    t1 = time.perf_counter()
-    samples = 0
-    for toks in outs:
-        d_codes = dev.upload((toks - m.SYNTH_SPEECH0).astype(np.int32))
-        samples += codec.decode_pcm_device(d_codes, len(toks), d_emb, d_pcm)
-    dev.sync()
-    t2 = time.perf_counter()
-    if any(len(t) != a.tokens for t in outs):
-        raise RuntimeError("batched utterance ended early")
-    wall = t2 - t0
+    samples, llm_s = step(5000, True)
+    wall = time.perf_counter() - t0
     return {"utterances": B, "value": round(samples / codec.sample_rate / wall, 3),
             "unit": "x realtime (audio s / wall s), aggregate of the B utterances on one GPU",
-            "llm_ms": round((t1 - t0) * 1e3, 3), "llm_ms_per_step": round((t1 - t0) * 1e3 / a.tokens, 4),
-            "codec_istft_ms": round((t2 - t1) * 1e3, 3), "wall_ms": round(wall * 1e3, 3)}
+            "llm_ms": round(llm_s * 1e3, 3), "llm_ms_per_step": round(llm_s * 1e3 / a.tokens, 4),
+            "codec_istft_ms": round((wall - llm_s) * 1e3, 3), "wall_ms": round(wall * 1e3, 3)}
+
+
+def make_batch_step(tokens, B, llm, codec, dev, prompt, allow, d_emb, d_pcm):
+    """One step of B utterances decoded together, then each through codec + iSTFT (PCM left
+    in HBM). step(seed_base, _) -> (audio samples, llm seconds)."""
+    import numpy as np
+    import miotts_amd as m
+
+    def step(seed_base, _record):
+        seeds = [utterance_seed(0, seed_base + b) for b in range(B)]
+        t0 = time.perf_counter()
+        outs = llm.generate_batch([prompt] * B, tokens, 0.8, seeds, allow=allow, check_interval=64)
+        t1 = time.perf_counter()
+        samples = 0
+        for toks in outs:
+            if len(toks) != tokens:
+                raise RuntimeError("batched utterance ended early")
+            d_codes = dev.upload((toks - m.SYNTH_SPEECH0).astype(np.int32))
+            samples += codec.decode_pcm_device(d_codes, len(toks), d_emb, d_pcm)
+        dev.sync()
+        return samples, t1 - t0
+
+    return step
 
 
 def utterance_seed(rank: int, index: int) -> int:
@@ -163,16 +223,67 @@ def timed_region(warmup, steps, utts_per_step, rank, utterance, sync, barrier, d
     elapsed = time.perf_counter() - t_start
     if dist is None:
         return elapsed, float(samples)
+    return all_reduce(dist, elapsed, "max"), all_reduce(dist, float(samples), "sum")
+
+
+def all_reduce(dist, v: float, op: str) -> float:
+    if dist is None:
+        return v
     import torch
-    t = torch.tensor([elapsed], dtype=torch.float64)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    n = torch.tensor([samples], dtype=torch.float64)
-    dist.all_reduce(n, op=dist.ReduceOp.SUM)
-    return float(t.item()), float(n.item())
+    t = torch.tensor([v], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM)
+    return float(t.item())
+
+
+def roofline(llm, preset):
+    """Dominant decode-step kernel by in-graph time per token (step timeline) with its
+    algorithmic bytes; see the module docstring."""
+    import numpy as np
+    tl = llm.timeline()
+    nl = tl.shape[0]
+    names = [KERNEL_NAMES[k] for k in (0, 1, 2, 3, 4)] * ((nl - 2) // 5) + [KERNEL_NAMES[6], "k_sample"]
+    dur = np.nanmax(tl[:, :, 7], axis=1) - np.nanmin(tl[:, :, 0], axis=1)
+    step_wall_us = float(np.nanmax(tl[-1, :, 7]) - np.nanmin(tl[0, :, 0]))
+    per_kernel = {}
+    for i, nm in enumerate(names):
+        per_kernel.setdefault(nm, []).append(float(dur[i]))
+    bytes_of, event_us = {}, {}
+    for which in (0, 1, 2, 3, 4, 6):
+        ms, by = llm.time_kernel(which, 40)
+        bytes_of[KERNEL_NAMES[which]] = by
+        event_us[KERNEL_NAMES[which]] = ms * 1e3
+    dom = max(bytes_of, key=lambda k: sum(per_kernel[k]))
+    dom_us = float(np.mean(per_kernel[dom]))
+    achieved = bytes_of[dom] / (dom_us * 1e-6) / 1e9
+    n_layer = (nl - 2) // 5
+    step_bytes = sum(bytes_of[KERNEL_NAMES[k]] * n_layer for k in (0, 1, 2, 3, 4)) + bytes_of["k_lm_head"]
+    step_gbs = step_bytes / (step_wall_us * 1e-6) / 1e9
+    traffic = None
+    tfile = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    if os.path.exists(tfile):
+        try:
+            tj = json.load(open(tfile))
+            if tj.get("preset") == preset:
+                traffic = tj.get("per_launch_bytes", {}).get(dom)
+        except Exception:
+            traffic = None
+    return {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "bytes_per_launch": bytes_of[dom],
+            "avg_launch_us": round(dom_us, 3), "event_avg_launch_us": round(event_us[dom], 3),
+            "frac_event": round(bytes_of[dom] / (event_us[dom] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+            "step_bytes": step_bytes, "step_graph_wall_us": round(step_wall_us, 1),
+            "step_achieved_GBps": round(step_gbs, 1), "step_frac": round(step_gbs / HBM_PEAK_GBS, 4),
+            "step_weight_bytes": llm.weight_bytes(),
+            "per_token_us": {k: round(sum(v), 1) for k, v in per_kernel.items()},
+            "bytes_per_launch_all": bytes_of,
+            "note": "timeline taken at the end-of-utterance position; attention bytes at that position"}
 
 
 def main():
-    a = parse_args()
+    argv = sys.argv[1:]
+    a = parse_args(argv)
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(a.gpus, argv))
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local_rank = int(os.environ.get("LOCAL_RANK", 0))
@@ -185,11 +296,25 @@ def main():
         if dist is not None:
             dist.barrier()
 
+    if a.launcher_selftest:  # tests/test_bench_dist.py: the N-rank launcher without a GPU
+        def fake(seed, record):
+            time.sleep(0.02 * (rank + 1))
+            return 1000
+        elapsed, samples = timed_region(a.warmup, a.steps, a.utts_per_step, rank, fake, lambda: None, barrier, dist)
+        if rank == 0:
+            print(json.dumps({"metric": "launcher self-test", "n_gpus": world, "samples": samples,
+                              "elapsed": elapsed, "pid_rank0": os.getpid(),
+                              "local_rank": local_rank}), flush=True)
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+
     import numpy as np
     import miotts_amd as m
 
     llm_path, codec_path, voice_path = ensure_files(a.workdir, a.preset, rank, barrier)
-    dev = m.Device(local_rank)
+    n_dev = m.device_count()
+    dev = m.Device(local_rank % n_dev)  # ranks share a GPU only when there are fewer GPUs than ranks
     llm = m.Llm(dev, llm_path, 2048)
     codec = m.Codec(dev, codec_path)
     emb = m.read_voice(voice_path)
@@ -200,6 +325,7 @@ def main():
 
     d_emb = dev.upload(np.ascontiguousarray(emb, np.float32))
     d_pcm = dev.empty((a.tokens * codec.samples_per_token,), np.float32)
+    B = a.utts_per_gpu
 
     def utterance(seed, record):
         t0 = time.perf_counter()
@@ -219,17 +345,30 @@ def main():
             raise RuntimeError(f"utterance produced {len(toks)} tokens / {n} samples")
         return n
 
-    elapsed, total_samples = timed_region(a.warmup, a.steps, a.utts_per_step, rank, utterance,
-                                          dev.sync, barrier, dist)
+    if B > 1:
+        bstep = make_batch_step(a.tokens, B, llm, codec, dev, prompt, allow, d_emb, d_pcm)
+
+        def step_fn(seed, record):
+            samples, llm_s = bstep(seed * 131, record)
+            if record:
+                stage["llm_ms"] += llm_s * 1e3 / B
+            return samples
+        utts = 1
+    else:
+        step_fn, utts = utterance, a.utts_per_step
+
+    elapsed, total_samples = timed_region(a.warmup, a.steps, utts, rank, step_fn, dev.sync, barrier, dist)
     audio_s = total_samples / codec.sample_rate
     value = audio_s / elapsed
+    utt_per_rank = a.steps * (B if B > 1 else a.utts_per_step)
 
-    # PCIe-inclusive: the PCM of one utterance copied to host memory (never `value`)
+    # PCIe-inclusive: each rank copies its utterances' PCM to host memory (ranks in parallel:
+    # the slowest rank's copy time counts, never `value`)
     t0 = time.perf_counter()
     for _ in range(3):
         d_pcm.numpy()
-    d2h_s = (time.perf_counter() - t0) / 3
-    value_pcie = audio_s / (elapsed + d2h_s * a.steps * a.utts_per_step * world)
+    d2h_s = all_reduce(dist, (time.perf_counter() - t0) / 3, "max")
+    value_pcie = audio_s / (elapsed + d2h_s * utt_per_rank)
 
     # WAV epilogue on the device (mio_hip_pcm_finish: peak normalise + PCM16) of the last
     # utterance, HIP events on the device stream; reported beside the stage times
@@ -245,40 +384,15 @@ def main():
         pf_ms.append(dev.elapsed_ms(14, 15))
     pcm_finish_ms = round(min(pf_ms[1:]), 4)
 
-    # roofline: dominant kernel inside the captured step graph (timeline), then HIP events
-    tl = llm.timeline()
-    nl = tl.shape[0]
-    names = [KERNEL_NAMES[k] for k in (0, 1, 2, 3, 4)] * ((nl - 2) // 5) + [KERNEL_NAMES[6], "k_sample"]
-    dur = np.nanmax(tl[:, :, 7], axis=1) - np.nanmin(tl[:, :, 0], axis=1)
-    step_wall_us = float(np.nanmax(tl[-1, :, 7]) - np.nanmin(tl[0, :, 0]))
-    per_kernel = {}
-    for i, nm in enumerate(names):
-        per_kernel.setdefault(nm, []).append(float(dur[i]))
-    bytes_of = {}
-    event_us = {}
-    for which in (0, 1, 2, 3, 4, 6):
-        ms, by = llm.time_kernel(which, 40)
-        bytes_of[KERNEL_NAMES[which]] = by
-        event_us[KERNEL_NAMES[which]] = ms * 1e3
-    dom = max((k for k in bytes_of if bytes_of[k] > 0), key=lambda k: sum(per_kernel[k]))
-    dom_us = float(np.mean(per_kernel[dom]))
-    dom_bytes = bytes_of[dom]
-    achieved = dom_bytes / (dom_us * 1e-6) / 1e9
-    traffic = None
-    tfile = os.path.join(REPO, "profiles", "pmc_traffic.json")
-    if os.path.exists(tfile):
-        try:
-            tj = json.load(open(tfile))
-            if tj.get("preset") == a.preset:
-                traffic = tj.get("per_launch_bytes", {}).get(dom)
-        except Exception:
-            traffic = None
+    roof = None
+    if rank == 0 and not a.no_roofline and B == 1:
+        roof = roofline(llm, a.preset)
 
-    steps_total = a.steps * a.utts_per_step
+    steps_total = utt_per_rank
+    model = PRESETS[a.preset]
     out = {
         # BASELINE.json's metric (quoted on preset 3); other presets name their own model
-        "metric": "realtime factor (audio s / wall s) + stage ms llm/codec/istft, "
-                  + PRESETS[a.preset].replace("MioTTS-", ""),
+        "metric": "realtime factor (audio s / wall s) + stage ms llm/codec/istft, " + model.replace("MioTTS-", ""),
         "value": round(value, 3),
         "unit": "x realtime (audio s / wall s)",
         "n_gpus": world,
@@ -288,31 +402,30 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": ("int8-dot (q8_0 x q8_0)" if "Q8_0" in PRESETS[a.preset] else "int8-dot (q4_K/q6_K x q8_K)")
+        "dtype": ("int8-dot (q8_0 x q8_0)" if "Q8_0" in model else "int8-dot (q4_K/q6_K x q8_K)")
                  + " + f32/f16 codec",
         "data": "synthetic",
-        "config": {"workload": f"{PRESETS[a.preset]} single utterance, {a.tokens} speech tokens -> "
-                               f"MioCodec -> iSTFT ({a.tokens * 1764 / 44100:.1f} s audio) per GPU",
-                   "model": PRESETS[a.preset], "global_batch": world * a.utts_per_step,
-                   "seq_len": a.tokens, "parallelism": f"utterance-sharded x{world} (no collective)"},
+        "config": {"workload": (f"{model} {'single utterance' if B == 1 else f'{B} utterances decoded together'}"
+                                f", {a.tokens} speech tokens -> MioCodec -> iSTFT "
+                                f"({a.tokens * 1764 / 44100:.1f} s audio each) per GPU"),
+                   "model": model, "global_batch": world * (B if B > 1 else a.utts_per_step),
+                   "seq_len": a.tokens, "parallelism": f"utterance-sharded x{world} (no collective)",
+                   "devices_visible": n_dev},
         "stage_ms": {**{k: round(v / steps_total, 3) for k, v in stage.items()},
                      "pcm_finish_ms": pcm_finish_ms},
         "llm_ms_per_token": round(stage["llm_ms"] / steps_total / a.tokens, 4),
-        "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1),
-                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": traffic, "bytes_per_launch": dom_bytes,
-                     "avg_launch_us": round(dom_us, 3),
-                     "event_avg_launch_us": round(event_us[dom], 3),
-                     "step_weight_bytes": llm.weight_bytes(),
-                     "step_graph_wall_us": round(step_wall_us, 1),
-                     "per_token_us": {k: round(sum(v), 1) for k, v in per_kernel.items()}},
+        "roofline": roof,
         "value_pcie_inclusive": round(value_pcie, 3),
         "cpu_baseline": None,
     }
-    if world == 1 and a.batch > 0:
+    if world == 1 and a.batch > 0 and B == 1:
         out["batched"] = batched_line(a, llm, codec, dev, prompt, allow, d_emb, d_pcm)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(llm_path, codec_path, voice_path, a.cpu_tokens, a.cpu_codes, a.tokens)
+        share = int(os.environ.get("OMP_NUM_THREADS", 0) or min(16, os.cpu_count() or 1))
+        out["cpu_baseline"] = cpu_baseline(llm_path, codec_path, voice_path, a.cpu_tokens, a.cpu_codes, a.tokens,
+                                           share)
+        out["cpu_baseline_4_threads"] = cpu_baseline(llm_path, codec_path, voice_path, max(16, a.cpu_tokens // 4),
+                                                     a.cpu_codes // 2, a.tokens, 4)
     if rank == 0:
         print(json.dumps(out, ensure_ascii=False), flush=True)
     if dist is not None:

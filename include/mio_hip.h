@@ -66,10 +66,16 @@ int mio_hip_timer_elapsed(mio_hip_device *d, int slot_a, int slot_b, float *ms);
  * conversion of wav_write (wav-writer.cpp:24-44: int16(clamp(s * 32767)), truncated) of n
  * samples. samples (16-byte aligned) and pcm16 are device pointers; the 44-byte RIFF header
  * stays with the host writer. peak (host, may be NULL) receives max|s| of the normalising pass
- * (0 when normalize == 0) and synchronizes the stream. Bit-exact with the host path. One call
- * at a time per device. */
+ * (0 when normalize == 0) and synchronizes the stream. Bit-exact with the host path and the
+ * reference's x86 bytes (NaN -> 0). Scratch is per call (stream-ordered): calls on different
+ * streams may overlap. */
 int mio_hip_pcm_finish(mio_hip_device *d, const float *samples, int64_t n, int normalize,
                        int16_t *pcm16, float *peak, void *stream);
+/* The peak normalisation alone (test-to-speech.cpp:232-243 / :289-298) on device floats:
+ * out[i] = samples[i] * 0.95 / max|s| when max|s| > 1e-8, else samples[i]; out may equal
+ * samples (in place). peak as in mio_hip_pcm_finish. Bit-exact with the host loop. */
+int mio_hip_pcm_normalize(mio_hip_device *d, const float *samples, int64_t n, float *out,
+                          float *peak, void *stream);
 
 /* ---------------- iSTFT ----------------
  * Replaces istft_cache(n_fft, win_length) (istft.h:6-30, istft.cpp:7-32) and
@@ -152,18 +158,11 @@ int mio_hip_llm_generate_batch(mio_hip_llm *m, const int32_t *prompts, const int
                                int32_t allow_hi, int32_t eos0, int32_t eos1, int32_t check_interval,
                                int32_t *out_tokens, int32_t *n_out);
 
-/* Decode engine of mio_hip_llm_generate / llm_run: mode 1 = the persistent launch (one
- * kernel runs whole decode steps, csrc/hip/llm_persist.hip), 0 = one hipGraph of per-phase
- * kernels per step (the default unless MIO_PERSIST=1; faster on MI355X);
- * -1 = leave the mode unchanged (query). Both compute the same values bit for bit. *active (may be
- * null) = 1 when the persistent launch has run for this model, 0 if its shape has no
- * persistent instantiation (the graph path is used), -1 not yet tried. */
-int mio_hip_llm_set_decode_mode(mio_hip_llm *m, int mode, int *active);
-
 /* Live timing of one decode-step kernel (which: 0 attn_in, 1 attention, 2 attn_out,
  * 3 ffn_in, 4 ffn_down of layer n_layer/2; 6 lm_head): `iters` back-to-back launches on
  * the runner's stream between HIP events (state/buffers of the last generate/eval).
- * *avg_ms = mean duration; *bytes = algorithmic HBM bytes per launch. */
+ * *avg_ms = mean duration; *bytes = algorithmic HBM bytes per launch (attention: K/V rows of
+ * positions <= the decode state's pos, q|k|v, chunk partials). */
 int mio_hip_llm_time_kernel(mio_hip_llm *m, int which, int iters, float *avg_ms, uint64_t *bytes);
 /* Diagnostic: one launch of kernel `which` with in-kernel checkpoint tracing; out[0..15]
  * = s_memtime (shader clock) at checkpoints of workgroup 0 / thread 0 (0 = not reached),
@@ -177,11 +176,6 @@ int mio_hip_llm_trace_kernel(mio_hip_llm *m, int which, uint64_t *out);
  * prologue steps in -DMIO_TL_DIAG builds.
  * Advances the decode state. */
 int mio_hip_llm_timeline(mio_hip_llm *m, uint64_t *out, int max_launches, int *n_launches);
-/* Diagnostic: one persistent decode step with its phase timeline (advances the decode
- * state): out[(phase * n_wg + wg) * 8 + k] = s_memrealtime (100 MHz) at k = 0 body start,
- * 1 prologue done, 2 body done, 3 arrived, 4 poll done, 5 inputs staged, 6 prefetch issued
- * (0 = not recorded); 5 phases per layer, then lm_head and the sampler. */
-int mio_hip_llm_persist_timeline(mio_hip_llm *m, uint64_t *out, int max_phases, int *n_phases, int *n_wg);
 /* Stage times (ms, HIP events) of the last mio_hip_codec_decode_pcm: [0] codec, [1] iSTFT. */
 int mio_hip_codec_last_timings(const mio_hip_codec *c, float *ms2);
 
@@ -222,7 +216,8 @@ int mio_stream_cadence(int n_tokens, int *decode_calls, int64_t *decoded_codes);
 int mio_synth_codec_gguf(const char *path, int preset, uint64_t seed);
 int mio_synth_voice_gguf(const char *path, uint64_t seed);
 /* Synthetic LLM (llama.cpp GGUF conventions, byte-level vocab + 12,800 speech tokens):
- * preset 0 tiny Q8_0, 1 tiny Q4_K_M, 2 "0.1B" Q8_0, 3 "1.7B" Q4_K_M, 4 "2.6B" Q8_0. */
+ * preset 0 tiny Q8_0, 1 tiny Q4_K_M, 2 "0.1B" Q8_0, 3 "1.7B" Q4_K_M, 4 "2.6B" Q8_0,
+ * 5 tiny Q8_0 qwen2 with attn_{q,k,v}.bias. */
 int mio_synth_llm_gguf(const char *path, int preset, uint64_t seed);
 
 #ifdef __cplusplus

@@ -51,4 +51,15 @@ inline int bind(const mio_hip_device *d) {
 inline hipStream_t pick_stream(const mio_hip_device *d, void *stream) {
     return stream ? (hipStream_t)stream : d->stream;
 }
+
+// One WAV sample of wav_write (wav-writer.cpp:24-44):
+// static_cast<int16_t>(std::clamp(s * 32767.0f, -32768.0f, 32767.0f)), truncated toward zero.
+// std::clamp compares (v < lo) then (hi < v), so a NaN passes through; the reference's x86
+// build converts it with cvttss2si (integer indefinite 0x80000000), whose low 16 bits are 0.
+// Host writer and device epilogue share this, so both emit the reference's bytes.
+__host__ __device__ inline int16_t pcm16_sample(float s) {
+    const float t = s * 32767.0f;
+    const float c = t < -32768.0f ? -32768.0f : (32767.0f < t ? 32767.0f : t);
+    return c != c ? (int16_t)0 : (int16_t)(int)c;
+}
 }  // namespace mio

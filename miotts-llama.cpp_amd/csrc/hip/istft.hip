@@ -215,11 +215,13 @@ extern "C" int mio_hip_istft_create(mio_hip_device *d, int n_fft, int win_length
         mio_hip_istft_destroy(h);
         return MIO_ERR_HIP;
     }
-    static bool attr_set = false;
-    if (!attr_set) {
-        hipFuncSetAttribute((const void *)istft_fused_kernel,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        attr_set = true;
+    // the 160 KB LDS opt-in applies to the current device: set it for every handle (once per
+    // create, cheap), so a second device in the same process gets it too
+    if (hipFuncSetAttribute((const void *)istft_fused_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            160 * 1024) != hipSuccess) {
+        mio::set_error("istft_create: LDS attribute: %s", hipGetErrorString(hipGetLastError()));
+        mio_hip_istft_destroy(h);
+        return MIO_ERR_HIP;
     }
     *out = h;
     return MIO_OK;

@@ -13,9 +13,7 @@
 
 #pragma clang fp contract(off)
 
-// Thread index used by every helper below. The persistent step (llm_persist.hip) defines it
-// as an opaque per-use value so the compiler cannot hoist each phase's lane-dependent
-// address arithmetic out of the step loop (hoisted, it stays live for the whole launch).
+// Thread index used by every helper below.
 #ifndef MIO_TIDX
 #define MIO_TIDX threadIdx.x
 #endif
@@ -995,8 +993,11 @@ __device__ __forceinline__ float xor_lane(float v) {
 // (qwen3 attn_q_norm / attn_k_norm), RoPE on (i, i + HD/2) pairs (NEOX) or (2i, 2i+1) (NORM)
 // with the ggml rope-cache cos/sin, f16 rounding (the F16 cache / ggml's f16 K operand).
 // row: wave-private LDS scratch [HD]; the prepared head is left in row.
+// bias (may be null): the projection bias added in f32 before anything else (qwen2,
+// llama.cpp build_attn_mha's Qcur = ggml_add(Qcur, bq)).
 template <int HD>
-__device__ void prep_head(const float *src, const float *nw, const float2 *rope, const LlmDims &d, float *row) {
+__device__ void prep_head(const float *src, const float *bias, const float *nw, const float2 *rope,
+                          const LlmDims &d, float *row) {
     constexpr int PER = HD / 64;
     const int lane = MIO_TIDX & 63;
     float v[PER], w[PER];
@@ -1005,6 +1006,7 @@ __device__ void prep_head(const float *src, const float *nw, const float2 *rope,
     for (int i = 0; i < PER; ++i) {
         const int p = lane + 64 * i;
         v[i] = src[p];
+        if (bias) v[i] = v[i] + bias[p];
         w[i] = d.qk_norm ? nw[p] : 1.0f;
         cs[i] = p < HD / 2 ? rope[p] : make_float2(0.0f, 0.0f);
     }
@@ -1052,9 +1054,7 @@ __device__ void prep_head(const float *src, const float *nw, const float2 *rope,
 }
 
 // K/V rows of this thread's slot (positions t0 + sl + NS*it, clamped to pos), issued early.
-// SC1: device-coherent loads (the persistent step, whose own workgroup appended some of the
-// rows earlier in the same launch: never served from a CU-L1 line cached before the append)
-template <int HD, bool SC1 = false>
+template <int HD>
 __device__ __forceinline__ void load_kv_rows(const _Float16 *kbase, const _Float16 *vbase, int t0, int pos,
                                              h8 (&kr)[AttCfg<HD>::IT], h8 (&vr)[AttCfg<HD>::IT]) {
     constexpr int LP = AttCfg<HD>::LP, NS = AttCfg<HD>::NS;
@@ -1062,14 +1062,8 @@ __device__ __forceinline__ void load_kv_rows(const _Float16 *kbase, const _Float
 #pragma unroll
     for (int it = 0; it < AttCfg<HD>::IT; ++it) {
         const int t = min(t0 + sl + NS * it, pos);
-        if constexpr (SC1) {
-            const uint32_t off = (uint32_t)(((size_t)t * HD + lp * 8) * 2), bytes = (uint32_t)((size_t)(pos + 1) * HD * 2);
-            kr[it] = __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(rsrc(kbase, bytes), off, 0, 16));
-            vr[it] = __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(rsrc(vbase, bytes), off, 0, 16));
-        } else {
-            kr[it] = *reinterpret_cast<const h8 *>(kbase + (size_t)t * HD + lp * 8);
-            vr[it] = *reinterpret_cast<const h8 *>(vbase + (size_t)t * HD + lp * 8);
-        }
+        kr[it] = *reinterpret_cast<const h8 *>(kbase + (size_t)t * HD + lp * 8);
+        vr[it] = *reinterpret_cast<const h8 *>(vbase + (size_t)t * HD + lp * 8);
     }
 }
 
@@ -1080,7 +1074,7 @@ __device__ __forceinline__ void load_kv_rows(const _Float16 *kbase, const _Float
 // and the slots' sums then merge by plain adds (no online rescaling). Writes the chunk's
 // partial record {O[HD] = sum_t p_t v_t, m = chunk max, l = sum_t p_t} of head g to
 // dst + g * g_stride (p_t = exp(s_t - m)).
-template <int HD, int G, bool SC1 = false>
+template <int HD, int G>
 __device__ void attend_chunk(const float (*qs)[HD], const h8 (&kr)[AttCfg<HD>::IT], const h8 (&vr)[AttCfg<HD>::IT],
                              int t0, int pos, float scale, float (*wres)[G][HD + 2], float *dst, size_t g_stride,
                              unsigned long long *trace = nullptr, unsigned long long *diag = nullptr) {
@@ -1196,16 +1190,8 @@ __device__ void attend_chunk(const float (*qs)[HD], const h8 (&kr)[AttCfg<HD>::I
             L += wres[w][g][HD];
         }
         float *o = dst + g * g_stride;
-        if constexpr (SC1) {  // handed to other workgroups inside a persistent launch
-            __hip_atomic_store(o + dd, O, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (dd == 0) {
-                __hip_atomic_store(o + HD, M[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(o + HD + 1, L, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        } else {
-            o[dd] = O;
-            if (dd == 0) o[HD] = M[g], o[HD + 1] = L;
-        }
+        o[dd] = O;
+        if (dd == 0) o[HD] = M[g], o[HD + 1] = L;
     }
 }
 }  // namespace

@@ -39,6 +39,7 @@ struct SampleCfg {
 
 struct LayerW {
     const float *attn_norm, *q_norm, *k_norm, *ffn_norm;
+    const float *bqkv;  // [(H + 2 Hkv) hd] q|k|v biases (qwen2 attn_{q,k,v}.bias), or null
     QMat wq, wk, wv, wo, gate, up, down;
 };
 
@@ -46,7 +47,7 @@ struct LlmDims {
     int n_embd, n_head, n_kv, hd, n_ff, n_vocab, n_ctx;
     float eps, scale;
     int neox, qk_norm;
-    int split;        // attention positions per chunk (ATT_CHUNK = 64)
+    int split;        // attention positions per chunk (kAttChunk)
     int max_splits;
     int n_wg;         // streaming-matvec workgroups (one per CU)
     int n_layer;
@@ -116,23 +117,6 @@ bool batch_supported(const LlmDims &d, int B);
 // Embedding of st[b].token into pb.x[b] for every sequence (decode start).
 void launch_batch_embed(const LlmDims &d, const QMat &tok_embd, const PrefillBuffers &pb, const BatchBuffers &bb,
                         int B, hipStream_t s);
-
-// Persistent decode (csrc/hip/llm_persist.hip): one launch runs n_steps whole decode steps
-// (every phase of every layer, lm_head, sampler, next embedding) on G workgroups, one per CU.
-struct PersistArgs {
-    LlmDims d;
-    const LayerW *layers;  // device copy [n_layer]
-    QMat lm, tok;
-    const float *out_norm;
-    _Float16 *kc, *vc;
-    LlmBuffers b;
-    unsigned *ctl;  // hand-off words: [8 shards x 32] arrival counters, [256] error; zeroed per launch
-    int n_steps;
-    unsigned long long *tl;  // optional diagnostic phase timeline [phase][G][8]
-};
-size_t persist_ctl_bytes();
-// 0 = launched; 1 = no instantiation for this shape / grid (use the graph path); 2 = HIP error
-int launch_persist(const PersistArgs &a, int G, hipStream_t s);
 
 // Launch one kernel of a decode step (which: 0 attn_in, 1 attention, 2 attn_out, 3 ffn_in,
 // 4 ffn_down of layer il; 6 lm_head, 7 sampler) on stream s.

@@ -255,7 +255,7 @@ __global__ __launch_bounds__(MT) void k_lm_head(LlmDims d, const float *norm_w, 
 // of k_attn_out (the launch-boundary reduce: no extra launch, no in-kernel hand-off).
 template <int HD, int G, bool DG>
 __global__ __launch_bounds__(ATT_NT) void k_attention(LlmDims d, const float *q_norm, const float *k_norm,
-                                                      _Float16 *kc, _Float16 *vc, LlmBuffers b) {
+                                                      const float *bqkv, _Float16 *kc, _Float16 *vc, LlmBuffers b) {
     constexpr bool kDiag = DG;
     using C = AttCfg<HD>;
     constexpr int PER = HD / 64;
@@ -270,7 +270,7 @@ __global__ __launch_bounds__(ATT_NT) void k_attention(LlmDims d, const float *q_
     // b.st (without this the compiler sinks them below the pos-dependent exit: a third
     // scalar-load round trip before the first K/V load)
     asm volatile("" ::"s"(kc), "s"(vc), "s"(d.n_ctx), "s"(b.qkv), "s"(b.rope), "s"(q_norm), "s"(k_norm),
-                 "s"(b.part), "s"(d.max_splits));
+                 "s"(b.part), "s"(d.max_splits), "s"(bqkv));
     const int pos = b.st->pos;
     const int t0 = ch * ATT_CHUNK;
     if (t0 > pos) return;
@@ -287,12 +287,15 @@ __global__ __launch_bounds__(ATT_NT) void k_attention(LlmDims d, const float *q_
         const bool isk = hh == G;
         float vv[PER];
         if (isk) {
-            const float *vsrc = b.qkv + (size_t)(d.n_head + d.n_kv + kvh) * HD;
+            const size_t vo = (size_t)(d.n_head + d.n_kv + kvh) * HD;
 #pragma unroll
-            for (int i = 0; i < PER; ++i) vv[i] = vsrc[lane + 64 * i];
+            for (int i = 0; i < PER; ++i) {
+                vv[i] = b.qkv[vo + lane + 64 * i];
+                if (bqkv) vv[i] = vv[i] + bqkv[vo + lane + 64 * i];
+            }
         }
-        const float *src = isk ? b.qkv + (size_t)(d.n_head + kvh) * HD : b.qkv + (size_t)(kvh * G + hh) * HD;
-        prep_head<HD>(src, isk ? k_norm : q_norm, rope, d, isk ? knew : qs[hh]);
+        const size_t so = isk ? (size_t)(d.n_head + kvh) * HD : (size_t)(kvh * G + hh) * HD;
+        prep_head<HD>(b.qkv + so, bqkv ? bqkv + so : nullptr, isk ? k_norm : q_norm, rope, d, isk ? knew : qs[hh]);
         if (isk) {
             _Float16 *kd = kc + ((size_t)kvh * d.n_ctx + pos) * HD;
             _Float16 *vd = vc + ((size_t)kvh * d.n_ctx + pos) * HD;
@@ -329,14 +332,15 @@ __global__ __launch_bounds__(ATT_NT) void k_attention(LlmDims d, const float *q_
 }
 
 template <int HD, bool DG>
-void launch_attention(int G, dim3 grid, hipStream_t s, const LlmDims &d, const float *qn, const float *kn,
-                      _Float16 *kc, _Float16 *vc, const LlmBuffers &b) {
+void launch_attention(int G, dim3 grid, hipStream_t s, const LlmDims &d, const LayerW &L, _Float16 *kc,
+                      _Float16 *vc, const LlmBuffers &b) {
+    const float *qn = L.q_norm, *kn = L.k_norm, *bi = L.bqkv;
     switch (G) {
-        case 1: hipLaunchKernelGGL((k_attention<HD, 1, DG>), grid, dim3(ATT_NT), 0, s, d, qn, kn, kc, vc, b); break;
-        case 2: hipLaunchKernelGGL((k_attention<HD, 2, DG>), grid, dim3(ATT_NT), 0, s, d, qn, kn, kc, vc, b); break;
-        case 3: hipLaunchKernelGGL((k_attention<HD, 3, DG>), grid, dim3(ATT_NT), 0, s, d, qn, kn, kc, vc, b); break;
-        case 4: hipLaunchKernelGGL((k_attention<HD, 4, DG>), grid, dim3(ATT_NT), 0, s, d, qn, kn, kc, vc, b); break;
-        case 8: hipLaunchKernelGGL((k_attention<HD, 8, DG>), grid, dim3(ATT_NT), 0, s, d, qn, kn, kc, vc, b); break;
+        case 1: hipLaunchKernelGGL((k_attention<HD, 1, DG>), grid, dim3(ATT_NT), 0, s, d, qn, kn, bi, kc, vc, b); break;
+        case 2: hipLaunchKernelGGL((k_attention<HD, 2, DG>), grid, dim3(ATT_NT), 0, s, d, qn, kn, bi, kc, vc, b); break;
+        case 3: hipLaunchKernelGGL((k_attention<HD, 3, DG>), grid, dim3(ATT_NT), 0, s, d, qn, kn, bi, kc, vc, b); break;
+        case 4: hipLaunchKernelGGL((k_attention<HD, 4, DG>), grid, dim3(ATT_NT), 0, s, d, qn, kn, bi, kc, vc, b); break;
+        case 8: hipLaunchKernelGGL((k_attention<HD, 8, DG>), grid, dim3(ATT_NT), 0, s, d, qn, kn, bi, kc, vc, b); break;
         default: break;
     }
 }
@@ -485,9 +489,9 @@ void launch_step_kernel(int which, const LlmDims &d, const LayerW *layers, int i
             const LayerW &L = layers[il];
             const dim3 grid(d.max_splits, d.n_kv);
             if (d.hd == 128)
-                launch_attention<128, DG>(G, grid, s, d, L.q_norm, L.k_norm, kcache + il * layer_kv, vcache + il * layer_kv, b);
+                launch_attention<128, DG>(G, grid, s, d, L, kcache + il * layer_kv, vcache + il * layer_kv, b);
             else
-                launch_attention<64, DG>(G, grid, s, d, L.q_norm, L.k_norm, kcache + il * layer_kv, vcache + il * layer_kv, b);
+                launch_attention<64, DG>(G, grid, s, d, L, kcache + il * layer_kv, vcache + il * layer_kv, b);
             break;
         }
         case 2: {

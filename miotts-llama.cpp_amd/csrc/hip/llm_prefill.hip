@@ -19,6 +19,8 @@
 // bit (tests/test_llm_gpu.py::test_batched_prefill_matches_sequential).
 #include "llm_device.h"
 
+#include <mutex>
+#include <utility>
 #include <vector>
 
 #pragma clang fp contract(off)
@@ -259,8 +261,8 @@ __global__ __launch_bounds__(MT) void k_pf_attn_in(LlmDims d, const float *norm_
 // heads likewise and written with the v row to the F16 cache at the token's position
 // (prep_head: the decode step's head preparation).
 template <int HD>
-__global__ __launch_bounds__(64) void k_pf_rope(LlmDims d, const float *q_norm, const float *k_norm, _Float16 *kc,
-                                                _Float16 *vc, PrefillBuffers pb) {
+__global__ __launch_bounds__(64) void k_pf_rope(LlmDims d, const float *q_norm, const float *k_norm,
+                                                const float *bqkv, _Float16 *kc, _Float16 *vc, PrefillBuffers pb) {
     constexpr int PER = HD / 64;
     __shared__ float row[HD];
     const int hh = blockIdx.x, t = blockIdx.y, lane = threadIdx.x;
@@ -272,11 +274,15 @@ __global__ __launch_bounds__(64) void k_pf_rope(LlmDims d, const float *q_norm, 
     float *src = pb.qkv + (size_t)t * QD + (size_t)hh * HD;
     float vv[PER];
     if (isk) {
-        const float *vsrc = pb.qkv + (size_t)t * QD + (size_t)(d.n_head + d.n_kv + kvh) * HD;
+        const size_t vo = (size_t)(d.n_head + d.n_kv + kvh) * HD;
 #pragma unroll
-        for (int i = 0; i < PER; ++i) vv[i] = vsrc[lane + 64 * i];
+        for (int i = 0; i < PER; ++i) {
+            vv[i] = pb.qkv[(size_t)t * QD + vo + lane + 64 * i];
+            if (bqkv) vv[i] = vv[i] + bqkv[vo + lane + 64 * i];
+        }
     }
-    prep_head<HD>(src, isk ? k_norm : q_norm, pb.rope + (size_t)pos * (HD / 2), d, row);
+    prep_head<HD>(src, bqkv ? bqkv + (size_t)hh * HD : nullptr, isk ? k_norm : q_norm,
+                  pb.rope + (size_t)pos * (HD / 2), d, row);
     if (!isk) {
 #pragma unroll
         for (int i = 0; i < PER; ++i) src[lane + 64 * i] = row[lane + 64 * i];
@@ -505,18 +511,23 @@ void launch_pf_attention(int G, dim3 grid, hipStream_t s, const LlmDims &d, cons
     }
 }
 
-// Dynamic LDS beyond the default 64 KB needs the per-kernel opt-in (once per kernel; the
-// limit leaves room for the kernel's static LDS). Keyed by the kernel's address: kernels of
-// one signature share a function type.
+// Dynamic LDS beyond the default 64 KB needs the per-kernel opt-in (once per kernel and
+// device: the attribute applies to the current device; the limit leaves room for the
+// kernel's static LDS). Keyed by (device, kernel address): kernels of one signature share a
+// function type.
 constexpr int LDS_DYN_MAX = LDS_MAX - 1024;
 template <class Kern>
 void allow_lds(Kern k) {
-    static std::vector<const void *> done;
+    static std::mutex mu;
+    static std::vector<std::pair<int, const void *>> done;
     const void *p = reinterpret_cast<const void *>(k);
-    for (const void *q : done)
-        if (q == p) return;
+    int dev = 0;
+    hipGetDevice(&dev);
+    std::lock_guard<std::mutex> lk(mu);
+    for (const auto &q : done)
+        if (q.first == dev && q.second == p) return;
     hipFuncSetAttribute(p, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_DYN_MAX);
-    done.push_back(p);
+    done.push_back({dev, p});
 }
 
 // residual rows per wave of a matvec over `rows` rows on `grid` workgroups (wave_range)
@@ -606,9 +617,9 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
         {
             const dim3 grid(d.n_head + d.n_kv, nt);
             if (d.hd == 128)
-                hipLaunchKernelGGL((k_pf_rope<128>), grid, dim3(64), 0, s, d, L.q_norm, L.k_norm, kc, vc, pb);
+                hipLaunchKernelGGL((k_pf_rope<128>), grid, dim3(64), 0, s, d, L.q_norm, L.k_norm, L.bqkv, kc, vc, pb);
             else
-                hipLaunchKernelGGL((k_pf_rope<64>), grid, dim3(64), 0, s, d, L.q_norm, L.k_norm, kc, vc, pb);
+                hipLaunchKernelGGL((k_pf_rope<64>), grid, dim3(64), 0, s, d, L.q_norm, L.k_norm, L.bqkv, kc, vc, pb);
         }
         {
             const dim3 grid(d.n_kv * nt, n_chunks);

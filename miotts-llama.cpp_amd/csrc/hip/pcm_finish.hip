@@ -5,10 +5,12 @@
 // Bit-exact with the host path (csrc/host/tts.cpp peak_normalize, text.cpp wav_bytes): the
 // same float operations in the same order, no contraction.
 //
-// HBM-bound: 4 B read twice (peak pass, convert pass) + 2 B written per sample.
+// HBM-bound: 4 B read twice (peak pass, convert pass) + 2 B written per sample. Scratch (peak
+// partials) is allocated per call, stream-ordered, so concurrent calls never share it.
 #include "common.h"
 
 #include <algorithm>
+#include <type_traits>
 
 #pragma clang fp contract(off)
 
@@ -17,14 +19,11 @@ namespace {
 constexpr int PT = 256;        // threads per workgroup
 constexpr int MAX_PARTS = 1024;
 
-// per-workgroup max|s| partials of the peak pass (one call at a time per device, like every
-// handle of this ABI)
-__device__ float g_peak_part[MAX_PARTS];
-
 // NaN-ignoring max, as std::max(peak, fabs(s)) in peak_normalize (a NaN never replaces peak)
 __device__ __forceinline__ float max_keep(float peak, float a) { return peak < a ? a : peak; }
 
-__global__ __launch_bounds__(PT) void k_peak(const float *s, long long n) {
+// part[blockIdx.x] = this workgroup's max|s| (part: per-call stream-ordered scratch)
+__global__ __launch_bounds__(PT) void k_peak(const float *s, long long n, float *part) {
     __shared__ float red[PT / 64];
     float m = 0.0f;
     const long long n4 = n / 4;
@@ -44,13 +43,16 @@ __global__ __launch_bounds__(PT) void k_peak(const float *s, long long n) {
     if (threadIdx.x == 0) {
         float r = red[0];
         for (int w = 1; w < PT / 64; ++w) r = max_keep(r, red[w]);
-        g_peak_part[blockIdx.x] = r;
+        part[blockIdx.x] = r;
     }
 }
 
-// every workgroup reduces the partials itself (no third launch, no atomics), then converts
-__global__ __launch_bounds__(PT) void k_pcm16(const float *s, long long n, int n_parts, int normalize,
-                                              short *out, float *peak_out) {
+// every workgroup reduces the partials itself (no third launch, no atomics), then converts:
+// OutT short = the WAV sample (pcm16_sample), float = the normalised float sample (in place
+// allowed: each element is read once, by the thread that writes it)
+template <class OutT>
+__global__ __launch_bounds__(PT) void k_finish(const float *s, long long n, const float *part, int n_parts,
+                                               int normalize, OutT *out, float *peak_out) {
     __shared__ float red[PT / 64];
     __shared__ float gain_s;
     __shared__ int scale_s;
@@ -58,7 +60,7 @@ __global__ __launch_bounds__(PT) void k_pcm16(const float *s, long long n, int n
     bool scale = false;
     if (normalize) {
         float m = 0.0f;
-        for (int i = threadIdx.x; i < n_parts; i += PT) m = max_keep(m, g_peak_part[i]);
+        for (int i = threadIdx.x; i < n_parts; i += PT) m = max_keep(m, part[i]);
         for (int o = 32; o > 0; o >>= 1) m = max_keep(m, __shfl_xor(m, o));
         if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
         __syncthreads();
@@ -76,50 +78,62 @@ __global__ __launch_bounds__(PT) void k_pcm16(const float *s, long long n, int n
     for (long long i = blockIdx.x * (long long)PT + threadIdx.x; i < n; i += (long long)gridDim.x * PT) {
         float v = s[i];
         if (scale) v = v * gain;
-        const float t = v * 32767.0f;
-        // std::min(32767, std::max(-32768, t)) with std::max/min's comparison order
-        const float a = (-32768.0f < t) ? t : -32768.0f;
-        const float c = (a < 32767.0f) ? a : 32767.0f;
-        out[i] = (short)(int)c;
+        if constexpr (std::is_same_v<OutT, short>)
+            out[i] = mio::pcm16_sample(v);
+        else
+            out[i] = v;
     }
 }
 
 }  // namespace
 
-extern "C" int mio_hip_pcm_finish(mio_hip_device *d, const float *samples, int64_t n, int normalize,
-                                  int16_t *pcm16, float *peak, void *stream) {
+namespace {
+template <class OutT>
+int finish(mio_hip_device *d, const float *samples, int64_t n, int normalize, OutT *out, float *peak,
+           void *stream) {
     MIO_REQUIRE(d && n >= 0, MIO_ERR_INVALID, "pcm_finish: bad argument");
     if (n == 0) {
         if (peak) *peak = 0.0f;
         return MIO_OK;
     }
-    MIO_REQUIRE(samples && pcm16, MIO_ERR_INVALID, "pcm_finish: null buffer");
+    MIO_REQUIRE(samples && out, MIO_ERR_INVALID, "pcm_finish: null buffer");
     MIO_REQUIRE(((uintptr_t)samples & 15) == 0, MIO_ERR_INVALID, "pcm_finish: samples must be 16-byte aligned");
     int rc = mio::bind(d);
     if (rc) return rc;
     hipStream_t s = mio::pick_stream(d, stream);
     const long long n4 = n / 4;
     int parts = (int)std::min<long long>(MAX_PARTS, std::max<long long>(1, (n4 + PT * 4 - 1) / (PT * 4)));
-    float *d_peak = nullptr;
+    // peak partials + the peak itself in stream-ordered scratch owned by this call: calls on
+    // different streams (or handles) of one GPU never share it
+    float *scratch = nullptr;
     if (normalize) {
-        hipLaunchKernelGGL(k_peak, dim3(parts), dim3(PT), 0, s, samples, (long long)n);
+        MIO_HIP_CHECK(hipMallocAsync((void **)&scratch, sizeof(float) * (parts + 1), s));
+        hipLaunchKernelGGL(k_peak, dim3(parts), dim3(PT), 0, s, samples, (long long)n, scratch);
         MIO_HIP_CHECK(hipGetLastError());
-        if (peak) {
-            MIO_HIP_CHECK(hipMallocAsync((void **)&d_peak, sizeof(float), s));
-        }
     }
+    float *d_peak = scratch && peak ? scratch + parts : nullptr;
     const int grid = (int)std::min<long long>(4 * (long long)d->n_cu, std::max<long long>(1, (n + PT * 8 - 1) / (PT * 8)));
-    hipLaunchKernelGGL(k_pcm16, dim3(grid), dim3(PT), 0, s, samples, (long long)n, parts, normalize,
-                       reinterpret_cast<short *>(pcm16), d_peak);
+    hipLaunchKernelGGL(k_finish<OutT>, dim3(grid), dim3(PT), 0, s, samples, (long long)n, scratch, parts, normalize,
+                       out, d_peak);
     MIO_HIP_CHECK(hipGetLastError());
+    if (d_peak) MIO_HIP_CHECK(hipMemcpyAsync(peak, d_peak, sizeof(float), hipMemcpyDeviceToHost, s));
+    if (scratch) MIO_HIP_CHECK(hipFreeAsync(scratch, s));
     if (peak) {
-        if (d_peak) {
-            MIO_HIP_CHECK(hipMemcpyAsync(peak, d_peak, sizeof(float), hipMemcpyDeviceToHost, s));
-            MIO_HIP_CHECK(hipFreeAsync(d_peak, s));
+        if (d_peak)
             MIO_HIP_CHECK(hipStreamSynchronize(s));
-        } else {
+        else
             *peak = 0.0f;  // not normalizing: no peak pass was run
-        }
     }
     return MIO_OK;
+}
+}  // namespace
+
+extern "C" int mio_hip_pcm_finish(mio_hip_device *d, const float *samples, int64_t n, int normalize,
+                                  int16_t *pcm16, float *peak, void *stream) {
+    return finish<short>(d, samples, n, normalize, reinterpret_cast<short *>(pcm16), peak, stream);
+}
+
+extern "C" int mio_hip_pcm_normalize(mio_hip_device *d, const float *samples, int64_t n, float *out,
+                                     float *peak, void *stream) {
+    return finish<float>(d, samples, n, 1, out, peak, stream);
 }

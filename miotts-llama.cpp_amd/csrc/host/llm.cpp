@@ -61,11 +61,6 @@ struct mio_hip_llm {
     // one step, and kGraphSteps steps back to back (fewer graph launches per token)
     hipGraphExec_t graph = nullptr, graph_n = nullptr;
     mio::SampleCfg *d_cfg = nullptr;
-    // persistent decode (llm_persist.hip): layer table on the device, hand-off words
-    mio::LayerW *d_layers = nullptr;
-    unsigned *d_ctl = nullptr;
-    int persist = -1;  // -1 untried, 0 unavailable for this shape (graph path), 1 in use
-    int persist_on = -1;  // mio_hip_llm_set_decode_mode (-1: MIO_PERSIST default)
     // generation state
     int n_prompt = 0, max_new = 0, steps_total = 0, steps_issued = 0;
     mio::SampleCfg cfg{};
@@ -232,9 +227,11 @@ uint64_t llm_step_weight_bytes(const mio_hip_llm *m) { return m->weight_bytes; }
 
 int llm_begin(mio_hip_llm *m, const int32_t *prompt, int n_prompt, int max_new, const SamplingParams &sp) {
     MIO_REQUIRE(m && prompt && n_prompt >= 1 && max_new >= 1, MIO_ERR_INVALID, "llm_begin: bad args");
-    MIO_REQUIRE(n_prompt - 1 + max_new <= m->max_steps && n_prompt + max_new <= m->dims.n_ctx,
-                MIO_ERR_INVALID, "llm_begin: %d prompt + %d new tokens exceed n_ctx %d", n_prompt,
-                max_new, m->dims.n_ctx);
+    MIO_REQUIRE(n_prompt <= m->dims.n_ctx, MIO_ERR_INVALID, "llm_begin: %d prompt tokens exceed n_ctx %d",
+                n_prompt, m->dims.n_ctx);
+    // the reference decodes until llama_decode fails at a full context and keeps the token
+    // sampled last (test-to-speech.cpp:163-187): at most n_ctx - n_prompt + 1 new tokens
+    max_new = std::min(max_new, m->dims.n_ctx - n_prompt + 1);
     for (int i = 0; i < n_prompt; ++i)
         MIO_REQUIRE(prompt[i] >= 0 && prompt[i] < m->dims.n_vocab, MIO_ERR_INVALID,
                     "llm_begin: token %d out of vocab", prompt[i]);
@@ -269,36 +266,6 @@ int llm_begin(mio_hip_llm *m, const int32_t *prompt, int n_prompt, int max_new, 
     return set_state(m, P, prompt[P], P);
 }
 
-// MIO_PERSIST=1: decode with the persistent launch by default (mio_hip_llm_set_decode_mode
-// selects per model). Off by default: measured slower than the graph path on MI355X
-// (profiles/r01_persist_timeline.txt: in-launch hand-offs queue behind the prefetched weight
-// stream, ~9 us per phase against ~6 us per launch + boundary).
-bool persist_enabled() {
-    static const bool on = getenv("MIO_PERSIST") && getenv("MIO_PERSIST")[0] == '1';
-    return on;
-}
-
-// n decode steps as ONE persistent launch (llm_persist.hip); 1 = shape not instantiated
-int run_persistent(mio_hip_llm *m, int n, unsigned long long *tl = nullptr) {
-    mio::PersistArgs a{};
-    a.tl = tl;
-    a.d = m->dims;
-    a.layers = m->d_layers;
-    a.lm = m->lm, a.tok = m->tok;
-    a.out_norm = m->out_norm;
-    a.kc = m->kc, a.vc = m->vc;
-    a.b = m->buf;
-    a.ctl = m->d_ctl;
-    a.n_steps = n;
-    const int r = mio::launch_persist(a, m->dims.n_wg, m->d->stream);
-    if (r == 2) {
-        mio::set_error("llm: persistent decode launch failed: %s", hipGetErrorString(hipGetLastError()));
-        return MIO_ERR_HIP;
-    }
-    if (r == 0) MIO_HIP_CHECK(hipGetLastError());
-    return r;
-}
-
 int llm_run(mio_hip_llm *m, int n_steps) {
     int rc = mio::bind(m->d);
     if (rc) return rc;
@@ -312,16 +279,6 @@ int llm_run(mio_hip_llm *m, int n_steps) {
             if ((rc = issue_step(m))) return rc;
         return MIO_OK;
     }
-    const bool want = m->persist_on < 0 ? persist_enabled() : m->persist_on == 1;
-    if (n > 0 && m->persist != 0 && want) {
-        rc = run_persistent(m, n);
-        if (rc == 0) {
-            m->persist = 1;
-            return MIO_OK;
-        }
-        if (rc != 1) return rc;
-        m->persist = 0;  // no instantiation for this shape: graph path from now on
-    }
     for (; n >= kGraphSteps; n -= kGraphSteps) MIO_HIP_CHECK(hipGraphLaunch(m->graph_n, m->d->stream));
     for (; n > 0; --n) MIO_HIP_CHECK(hipGraphLaunch(m->graph, m->d->stream));
     return MIO_OK;
@@ -331,15 +288,8 @@ int llm_poll(mio_hip_llm *m, std::vector<int32_t> &out, bool *done) {
     int rc = mio::bind(m->d);
     if (rc) return rc;
     StepState st{};
-    unsigned herr = 0;
     MIO_HIP_CHECK(hipMemcpyAsync(&st, m->buf.st, sizeof(st), hipMemcpyDeviceToHost, m->d->stream));
-    if (m->persist == 1)
-        MIO_HIP_CHECK(hipMemcpyAsync(&herr, m->d_ctl + 256, 4, hipMemcpyDeviceToHost, m->d->stream));
     MIO_HIP_CHECK(hipStreamSynchronize(m->d->stream));
-    if (herr) {
-        mio::set_error("llm: persistent decode hand-off timed out (workgroups not co-resident?)");
-        return MIO_ERR_HIP;
-    }
     const int first = m->n_prompt - 1;
     const int n = st.step > first ? st.step - first : 0;
     out.resize(n);
@@ -365,9 +315,27 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
     mio::GgufFile g;
     if (!g.open(path)) return MIO_ERR_IO;
     const std::string arch = g.get_str("general.architecture");
+    // lfm2 (LiquidAI LFM2, the <|startoftext|><|im_start|> template family) interleaves
+    // gated short-conv blocks (depthwise causal conv1d with a rolling state) with attention
+    // layers; no kernel of this path implements that block, so refuse it by name
+    MIO_REQUIRE(arch != "lfm2", MIO_ERR_UNSUPPORTED,
+                "llm_load: architecture 'lfm2' needs the hybrid short-conv block (depthwise causal "
+                "conv1d with rolling state), which this path does not implement; supported: llama, "
+                "mistral, qwen2, qwen3");
     MIO_REQUIRE(arch == "llama" || arch == "qwen3" || arch == "qwen2" || arch == "mistral",
-                MIO_ERR_UNSUPPORTED, "llm_load: architecture '%s' not supported (llama, qwen2, qwen3)",
+                MIO_ERR_UNSUPPORTED, "llm_load: architecture '%s' not supported (llama, mistral, qwen2, qwen3)",
                 arch.c_str());
+    // the only bias tensors any supported block has are qwen2's attn_{q,k,v}.bias: anything
+    // else (output / ffn biases) would be silently dropped, so refuse the file instead
+    for (const mio::GgufTensor &t : g.tensors()) {
+        const std::string &n = t.name;
+        if (n.size() > 5 && n.compare(n.size() - 5, 5, ".bias") == 0 &&
+            !(n.find(".attn_q.bias") != std::string::npos || n.find(".attn_k.bias") != std::string::npos ||
+              n.find(".attn_v.bias") != std::string::npos)) {
+            mio::set_error("llm_load: bias tensor %s is not supported (only attn_{q,k,v}.bias)", n.c_str());
+            return MIO_ERR_UNSUPPORTED;
+        }
+    }
     auto *m = new mio_hip_llm();
     m->d = d;
     auto fail = [&](int code) {
@@ -471,6 +439,31 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
             !upload_qmat(m, g.tensor(p + "ffn_gate.weight"), L.gate) ||
             !upload_qmat(m, g.tensor(p + "ffn_up.weight"), L.up) || !upload_qmat(m, g.tensor(p + "ffn_down.weight"), L.down))
             return fail(MIO_ERR_FORMAT);
+        {
+            // qwen2 q/k/v projection biases, one f32 vector in qkv order (added before
+            // RoPE by the attention kernels' head preparation)
+            const mio::GgufTensor *bt[3] = {g.tensor(p + "attn_q.bias"), g.tensor(p + "attn_k.bias"),
+                                            g.tensor(p + "attn_v.bias")};
+            const int64_t bn[3] = {(int64_t)D.n_head * D.hd, (int64_t)D.n_kv * D.hd, (int64_t)D.n_kv * D.hd};
+            if (bt[0] || bt[1] || bt[2]) {
+                std::vector<float> hb;
+                for (int j = 0; j < 3; ++j) {
+                    if (!bt[j] || bt[j]->type != mio::GGML_F32 || bt[j]->nelements() != bn[j]) {
+                        mio::set_error("llm_load: layer %d: attn_q/k/v.bias must all be f32 of the projection sizes", i);
+                        return fail(MIO_ERR_FORMAT);
+                    }
+                    const float *f = (const float *)bt[j]->data;
+                    hb.insert(hb.end(), f, f + bn[j]);
+                }
+                float *db = dalloc<float>(m, hb.size());
+                if (!db || hipMemcpy(db, hb.data(), hb.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+                    mio::set_error("llm_load: bias upload failed");
+                    return fail(MIO_ERR_OOM);
+                }
+                L.bqkv = db;
+                m->weight_bytes += hb.size() * 4;
+            }
+        }
         if (L.wq.rows != D.n_head * D.hd || L.wk.rows != D.n_kv * D.hd || L.wv.rows != D.n_kv * D.hd ||
             L.gate.rows != D.n_ff || L.down.k != D.n_ff || fam(L.wq.type) != fam(L.wk.type) ||
             fam(L.wq.type) != fam(L.wv.type) || L.wq.type != L.wk.type || L.gate.type != L.up.type ||
@@ -561,13 +554,6 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
         hipMemcpy(m->d_iota, iota.data(), iota.size() * 4, hipMemcpyHostToDevice);
     }
     m->buf.rope = dr;
-    m->d_layers = dalloc<mio::LayerW>(m, m->layers.size());
-    m->d_ctl = (unsigned *)dalloc<uint8_t>(m, mio::persist_ctl_bytes());
-    if (!m->d_layers || !m->d_ctl) {
-        mio::set_error("llm_load: device allocation failed");
-        return fail(MIO_ERR_OOM);
-    }
-    hipMemcpy(m->d_layers, m->layers.data(), m->layers.size() * sizeof(mio::LayerW), hipMemcpyHostToDevice);
     m->pf.rope = dr;
     // every memset / copy above ran on the null stream; the runner's stream is non-blocking
     if (hipDeviceSynchronize() != hipSuccess) {
@@ -585,13 +571,6 @@ extern "C" int mio_hip_llm_info(const mio_hip_llm *m, int *info) {
     mio::LlmInfo i = mio::llm_info(m);
     info[0] = i.n_vocab, info[1] = i.n_embd, info[2] = i.n_layer, info[3] = i.n_head;
     info[4] = i.n_kv, info[5] = i.head_dim, info[6] = i.n_ff, info[7] = i.n_ctx;
-    return MIO_OK;
-}
-
-extern "C" int mio_hip_llm_set_decode_mode(mio_hip_llm *m, int mode, int *active) {
-    MIO_REQUIRE(m && mode >= -1 && mode <= 1, MIO_ERR_INVALID, "llm_set_decode_mode: bad args");
-    if (mode >= 0) m->persist_on = mode;
-    if (active) *active = m->persist;
     return MIO_OK;
 }
 
@@ -758,9 +737,8 @@ extern "C" int mio_hip_llm_generate_batch(mio_hip_llm *m, const int32_t *prompts
     const mio::LlmDims &D = m->dims;
     std::vector<int> off(B + 1, 0);
     for (int b = 0; b < B; ++b) {
-        MIO_REQUIRE(prompt_lens[b] >= 1 && prompt_lens[b] + max_tokens <= D.n_ctx, MIO_ERR_INVALID,
-                    "llm_generate_batch: stream %d: %d prompt + %d new tokens exceed n_ctx %d", b, prompt_lens[b],
-                    max_tokens, D.n_ctx);
+        MIO_REQUIRE(prompt_lens[b] >= 1 && prompt_lens[b] <= D.n_ctx, MIO_ERR_INVALID,
+                    "llm_generate_batch: stream %d: %d prompt tokens exceed n_ctx %d", b, prompt_lens[b], D.n_ctx);
         off[b + 1] = off[b] + prompt_lens[b];
     }
     for (int i = 0; i < off[B]; ++i)
@@ -813,7 +791,8 @@ extern "C" int mio_hip_llm_generate_batch(mio_hip_llm *m, const int32_t *prompts
         c.eos0 = eos0, c.eos1 = eos1;
         c.force = nullptr, c.n_force = 0;
         c.out_tokens = bt.tokens + (size_t)b * D.n_ctx;
-        c.max_steps = P + max_tokens;
+        // as llm_begin: a full context ends the stream after n_ctx - len + 1 tokens
+        c.max_steps = P + std::min(max_tokens, D.n_ctx - prompt_lens[b] + 1);
     }
     MIO_HIP_CHECK(hipMemcpyAsync(bt.st, st.data(), B * sizeof(mio::StepState), hipMemcpyHostToDevice, s));
     MIO_HIP_CHECK(hipMemcpyAsync(bt.cfg, cf.data(), B * sizeof(mio::SampleCfg), hipMemcpyHostToDevice, s));
@@ -907,7 +886,9 @@ extern "C" int mio_quantize_rows(uint32_t type, const float *x, int rows, int k,
 // `which` (0 attn_in, 1 attention, 2 attn_out, 3 ffn_in, 4 ffn_down, 6 lm_head) of layer
 // n_layer/2 `iters` times on the runner's stream between HIP events, with the buffers and
 // device state left by the last generate/eval. Returns the mean duration and the
-// algorithmic HBM bytes of one launch (weights of the matrices it streams + activations).
+// algorithmic HBM bytes of one launch (weights of the matrices it streams + activations;
+// attention: F16 K and V rows of positions 0..pos (the row at pos is written, the rest
+// read) + q|k|v in + partial records out, at the decode state's current pos).
 extern "C" int mio_hip_llm_time_kernel(mio_hip_llm *m, int which, int iters, float *avg_ms, uint64_t *bytes) {
     MIO_REQUIRE(m && avg_ms && bytes && iters > 0 && m->graph, MIO_ERR_INVALID,
                 "llm_time_kernel: run generate/eval first");
@@ -920,11 +901,17 @@ extern "C" int mio_hip_llm_time_kernel(mio_hip_llm *m, int which, int iters, flo
         return (uint64_t)mio::ggml_row_bytes(q.type, q.k) * (uint64_t)q.rows;
     };
     const mio::LlmDims &D = m->dims;
+    // attention reads the K/V rows of positions <= pos of the current decode state
+    mio::StepState st{};
+    MIO_HIP_CHECK(hipMemcpy(&st, m->buf.st, sizeof(st), hipMemcpyDeviceToHost));
+    const uint64_t pos = (uint64_t)std::max(0, std::min(st.pos, D.n_ctx - 1));
+    const uint64_t nch = pos / mio::kAttChunk + 1, qkv = (uint64_t)(D.n_head + 2 * D.n_kv) * D.hd;
+    const uint64_t part = 4ull * D.n_head * nch * (D.hd + 2);  // chunk partial records {O, m, l}
     uint64_t b = 0;
     switch (which) {
-        case 0: b = qbytes(L.wq) + qbytes(L.wk) + qbytes(L.wv) + 4ull * D.n_embd * 2; break;
-        case 1: b = 0; break;
-        case 2: b = qbytes(L.wo) + 4ull * D.n_embd * 2; break;
+        case 0: b = qbytes(L.wq) + qbytes(L.wk) + qbytes(L.wv) + 4ull * D.n_embd + 4ull * qkv; break;
+        case 1: b = 2ull * 2 * D.n_kv * D.hd * (pos + 1) + 4ull * qkv + 8ull * (D.hd / 2) + part; break;
+        case 2: b = qbytes(L.wo) + part + 4ull * D.n_embd * 2; break;
         case 3: b = qbytes(L.gate) + qbytes(L.up) + 4ull * (D.n_embd * 2 + D.n_ff); break;
         case 4: b = qbytes(L.down) + 4ull * (D.n_ff + 2 * D.n_embd); break;
         case 6: b = qbytes(m->lm) + 4ull * D.n_vocab; break;
@@ -985,31 +972,6 @@ extern "C" int mio_hip_llm_trace_kernel(mio_hip_llm *m, int which, uint64_t *out
     MIO_HIP_CHECK(hipStreamSynchronize(s));
     hipFree(dt);
     if (flush) hipFree(flush);
-    return MIO_OK;
-}
-
-// Diagnostic: ONE persistent decode step with the phase timeline on (advances the decode
-// state by one step): out[(phase * G + wg) * 8 + k], s_memrealtime ticks (100 MHz), k = 0 body
-// start, 1 prologue done, 2 body done, 3 arrived, 4 poll done, 5 staged, 6 prefetch issued.
-extern "C" int mio_hip_llm_persist_timeline(mio_hip_llm *m, uint64_t *out, int max_phases, int *n_phases, int *n_wg) {
-    MIO_REQUIRE(m && out && n_phases && n_wg, MIO_ERR_INVALID, "llm_persist_timeline: null");
-    int rc = mio::bind(m->d);
-    if (rc) return rc;
-    const int np = m->n_layer * 5 + 2, G = m->dims.n_wg;
-    MIO_REQUIRE(max_phases >= np, MIO_ERR_INVALID, "llm_persist_timeline: need %d phase slots", np);
-    const size_t nslot = (size_t)np * G * 8;
-    unsigned long long *tl = nullptr;
-    MIO_HIP_CHECK(hipMalloc(&tl, sizeof(unsigned long long) * nslot));
-    MIO_HIP_CHECK(hipMemsetAsync(tl, 0, sizeof(unsigned long long) * nslot, m->d->stream));
-    rc = mio::run_persistent(m, 1, tl);
-    if (rc == 0) {
-        MIO_HIP_CHECK(hipMemcpyAsync(out, tl, sizeof(unsigned long long) * nslot, hipMemcpyDeviceToHost, m->d->stream));
-        MIO_HIP_CHECK(hipStreamSynchronize(m->d->stream));
-    }
-    hipFree(tl);
-    MIO_REQUIRE(rc == 0, MIO_ERR_UNSUPPORTED, "llm_persist_timeline: no persistent instantiation");
-    *n_phases = np;
-    *n_wg = G;
     return MIO_OK;
 }
 

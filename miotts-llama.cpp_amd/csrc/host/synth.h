@@ -27,16 +27,18 @@ bool synth_write_voice(const std::string &path, uint64_t seed, int dim = 128);
 // speech tokens <|s_0|>..<|s_12799|> (test-to-speech.cpp:91; miocodec.h:16).
 struct SynthLlmCfg {
     const char *name = "tiny";
-    const char *arch = "llama";  // "llama" (rope NORM) | "qwen3" (rope NEOX + q/k RMSNorm)
+    const char *arch = "llama";  // "llama" (rope NORM) | "qwen3" (rope NEOX + q/k RMSNorm) | "qwen2"
     int n_embd = 256, n_layer = 2, n_head = 4, n_head_kv = 2, head_dim = 64, n_ff = 512;
     int n_vocab = 13312, n_ctx = 4096;
     float rope_base = 10000.f, rms_eps = 1e-6f, w_std = 0.02f;
     int qtype = 8;   // 8 = all Q8_0; 15 = Q4_K_M mix (Q4_K + Q6_K)
     bool tied = true;
+    bool qkv_bias = false;  // attn_{q,k,v}.bias tensors (qwen2)
     uint64_t seed = 1;
 };
 // preset: 0 tiny Q8_0 (llama), 1 tiny Q4_K_M (qwen3), 2 "0.1B" Q8_0, 3 "1.7B" Q4_K_M,
-//         4 "2.6B" Q8_0  (shapes sized to the published file sizes, README.md:189-196)
+//         4 "2.6B" Q8_0  (shapes sized to the published file sizes, README.md:189-196),
+//         5 tiny Q8_0 qwen2 with q/k/v projection biases
 SynthLlmCfg synth_llm_preset(int preset);
 bool synth_write_llm(const std::string &path, const SynthLlmCfg &cfg);
 // Token ids of the synthetic vocabulary.

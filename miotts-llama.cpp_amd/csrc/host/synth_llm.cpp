@@ -44,6 +44,9 @@ SynthLlmCfg synth_llm_preset(int p) {
             c.n_head = 16, c.n_head_kv = 8, c.head_dim = 128, c.n_ff = 6144,
             c.n_vocab = 151936 + 12800, c.qtype = 15, c.rope_base = 1000000.f;
             break;
+        case 5:
+            c.name = "tiny-qwen2-bias", c.arch = "qwen2", c.qkv_bias = true, c.rope_base = 1000000.f;
+            break;
         case 4:
             c.name = "MioTTS-2.6B-synthetic", c.n_embd = 2048, c.n_layer = 32, c.n_head = 32,
             c.n_head_kv = 8, c.head_dim = 64, c.n_ff = 10752, c.n_vocab = 65536 + 12800;
@@ -114,7 +117,7 @@ bool synth_write_llm(const std::string &path, const SynthLlmCfg &c) {
         std::string name;
         uint32_t type;
         int64_t k, rows;
-        bool ones;
+        int fill;  // 0 quantized N(0, w_std) rows, 1 ones, 2 f32 N(0, 0.5) (biases)
     };
     std::vector<T> ts;
     const uint32_t base = c.qtype == 15 ? GGML_Q4_K : GGML_Q8_0;
@@ -129,6 +132,11 @@ bool synth_write_llm(const std::string &path, const SynthLlmCfg &c) {
         ts.push_back({p + "attn_k.weight", base, c.n_embd, kv_dim, false});
         ts.push_back({p + "attn_v.weight", mb ? more : base, c.n_embd, kv_dim, false});
         ts.push_back({p + "attn_output.weight", base, q_dim, c.n_embd, false});
+        if (c.qkv_bias) {
+            ts.push_back({p + "attn_q.bias", GGML_F32, q_dim, 1, 2});
+            ts.push_back({p + "attn_k.bias", GGML_F32, kv_dim, 1, 2});
+            ts.push_back({p + "attn_v.bias", GGML_F32, kv_dim, 1, 2});
+        }
         if (a == "qwen3") {
             ts.push_back({p + "attn_q_norm.weight", GGML_F32, c.head_dim, 1, true});
             ts.push_back({p + "attn_k_norm.weight", GGML_F32, c.head_dim, 1, true});
@@ -148,9 +156,10 @@ bool synth_write_llm(const std::string &path, const SynthLlmCfg &c) {
     }
     return w.write(path, [&](size_t idx, uint8_t *dst, size_t nbytes) {
         const T &t = ts[idx];
-        if (t.ones) {
+        if (t.fill == 1 || t.fill == 2) {
             float *f = (float *)dst;
-            for (int64_t i = 0; i < t.k; ++i) f[i] = 1.0f;
+            const uint64_t key = synth_key(c.seed, t.name);
+            for (int64_t i = 0; i < t.k; ++i) f[i] = t.fill == 1 ? 1.0f : 0.5f * synth_normal_fast(key, (uint64_t)i);
             return;
         }
         const size_t rb = ggml_row_bytes(t.type, t.k);

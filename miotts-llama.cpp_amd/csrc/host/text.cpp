@@ -15,6 +15,7 @@
 #include "text-normalize.h"
 #include "token-parser.h"
 #include "wav-writer.h"
+#include "wav.h"
 
 namespace {
 
@@ -126,8 +127,7 @@ void put32(std::vector<uint8_t> &b, uint32_t v) {
 }  // namespace
 
 namespace mio {
-// RIFF/WAVE PCM16 mono image: 44-byte header then int16(clamp(s * 32767)) truncated.
-std::vector<uint8_t> wav_bytes(const float *s, size_t n, int sample_rate) {
+std::vector<uint8_t> wav_header(size_t n, int sample_rate) {
     std::vector<uint8_t> b;
     b.reserve(44 + 2 * n);
     const uint32_t data = (uint32_t)(n * 2);
@@ -143,11 +143,24 @@ std::vector<uint8_t> wav_bytes(const float *s, size_t n, int sample_rate) {
     put16(b, 16);
     b.insert(b.end(), {'d', 'a', 't', 'a'});
     put32(b, data);
-    for (size_t i = 0; i < n; ++i) {
-        const float v = std::min(32767.0f, std::max(-32768.0f, s[i] * 32767.0f));
-        put16(b, (uint16_t)(int16_t)v);
-    }
     return b;
+}
+
+// RIFF/WAVE PCM16 mono image: 44-byte header then int16(clamp(s * 32767)) truncated.
+std::vector<uint8_t> wav_bytes(const float *s, size_t n, int sample_rate) {
+    std::vector<uint8_t> b = wav_header(n, sample_rate);
+    for (size_t i = 0; i < n; ++i) put16(b, (uint16_t)pcm16_sample(s[i]));
+    return b;
+}
+
+bool wav_write_pcm16(const std::string &path, const int16_t *pcm, size_t n, int sample_rate) {
+    std::ofstream f(path, std::ios::binary);
+    if (!f) return false;
+    const std::vector<uint8_t> h = wav_header(n, sample_rate);
+    f.write((const char *)h.data(), (std::streamsize)h.size());
+    static_assert(__BYTE_ORDER__ == __ORDER_LITTLE_ENDIAN__, "WAV samples are little-endian");
+    f.write((const char *)pcm, (std::streamsize)(n * 2));
+    return f.good();
 }
 }  // namespace mio
 

@@ -5,7 +5,8 @@
 // test-to-speech.cpp; the work runs on the GPU through the C-ABI handles:
 //   run_llm              -> BpeTokenizer + mio::llm_begin/run/poll (one hipGraph per token,
 //                           on-device temperature + Gumbel-max sampling, no per-token sync)
-//   decode_*_to_audio    -> mio_hip_codec_decode_pcm (codec kernels + fused iSTFT)
+//   decode_*_to_audio    -> mio_hip_codec_decode_pcm (codec kernels + fused iSTFT) into HBM
+//   peak normalisation   -> mio_hip_pcm_normalize / mio_hip_pcm_finish (device, bit-exact)
 #include <algorithm>
 #include <chrono>
 #include <cmath>
@@ -28,6 +29,7 @@
 #include "token-parser.h"
 #include "tokenizer.h"
 #include "wav-writer.h"
+#include "wav.h"
 
 namespace mio {
 
@@ -226,9 +228,27 @@ struct TestToSpeech::Impl {
     int32_t eos = -1, im_end = -1;
     int sample_rate = 0, n_fft = 0, hop = 0, spt = 0;
 
+    // PCM of the last decode in HBM (f32) and its PCM16 image (synthesize_to_file)
+    void *d_pcm = nullptr, *d_pcm16 = nullptr;
+    size_t pcm_cap = 0, pcm16_cap = 0;
+
     ~Impl() {
         if (llm) mio_hip_llm_free(llm);
+        if (dev && d_pcm) mio_hip_free(dev, d_pcm);
+        if (dev && d_pcm16) mio_hip_free(dev, d_pcm16);
         miocodec_free(codec);
+    }
+
+    bool ensure(void *&p, size_t &cap, size_t bytes) {
+        if (cap >= bytes) return true;
+        if (p) mio_hip_free(dev, p);
+        p = nullptr, cap = 0;
+        if (mio_hip_malloc(dev, bytes, &p) != MIO_OK) {
+            fprintf(stderr, "TestToSpeech: device buffer of %zu bytes: %s\n", bytes, mio_hip_last_error());
+            return false;
+        }
+        cap = bytes;
+        return true;
     }
 
     // "<|startoftext|><|im_start|>user\n" + text + "<|im_end|>\n<|im_start|>assistant\n"
@@ -250,17 +270,16 @@ struct TestToSpeech::Impl {
         if (o.ignore_eos) sp.eos0 = sp.eos1 = -1;
     }
 
-    // codes -> PCM on the GPU (codec + fused iSTFT); stage seconds from GPU events
-    bool decode_codes(const VoiceModel &voice, const std::vector<int> &codes, std::vector<float> &pcm,
-                      double *codec_sec, double *istft_sec) {
-        pcm.assign((size_t)codes.size() * spt, 0.0f);
-        int len = 0;
+    // codes -> PCM in HBM (d_pcm, *len samples): codec + fused iSTFT, stage seconds from GPU
+    // events
+    bool decode_codes_dev(const VoiceModel &voice, const std::vector<int> &codes, int *len, double *codec_sec,
+                          double *istft_sec) {
+        if (!ensure(d_pcm, pcm_cap, (size_t)codes.size() * spt * sizeof(float) + 64)) return false;
         if (mio_hip_codec_decode_pcm(codec->codec, codes.data(), (int)codes.size(), voice.embedding().data(),
-                                     pcm.data(), &len, 0, nullptr) != MIO_OK) {
+                                     (float *)d_pcm, len, MIO_OUT_DEVICE, nullptr) != MIO_OK) {
             fprintf(stderr, "TestToSpeech: codec decode failed: %s\n", mio_hip_last_error());
             return false;
         }
-        pcm.resize(len);
         float ms[2] = {0.0f, 0.0f};
         if (mio_hip_codec_last_timings(codec->codec, ms) == MIO_OK) {
             if (codec_sec) *codec_sec += ms[0] * 1e-3;
@@ -268,16 +287,25 @@ struct TestToSpeech::Impl {
         }
         return true;
     }
-};
 
-static void peak_normalize(std::vector<float> &a) {
-    float peak = 0.0f;
-    for (float s : a) peak = std::max(peak, std::fabs(s));
-    if (peak > 1e-8f) {
-        const float g = 0.95f / peak;
-        for (float &s : a) s *= g;
+    // codes -> host PCM; the peak normalisation of test-to-speech.cpp:232-243 (when asked)
+    // runs on the device before the copy (mio_hip_pcm_normalize, bit-exact with the host loop)
+    bool decode_codes(const VoiceModel &voice, const std::vector<int> &codes, std::vector<float> &pcm,
+                      double *codec_sec, double *istft_sec, bool normalize = false) {
+        int len = 0;
+        if (!decode_codes_dev(voice, codes, &len, codec_sec, istft_sec)) return false;
+        if (normalize && mio_hip_pcm_normalize(dev, (const float *)d_pcm, len, (float *)d_pcm, nullptr, nullptr)) {
+            fprintf(stderr, "TestToSpeech: peak normalisation failed: %s\n", mio_hip_last_error());
+            return false;
+        }
+        pcm.resize(len);
+        if (len && mio_hip_memcpy_d2h(dev, pcm.data(), d_pcm, (size_t)len * sizeof(float)) != MIO_OK) {
+            fprintf(stderr, "TestToSpeech: PCM copy failed: %s\n", mio_hip_last_error());
+            return false;
+        }
+        return true;
     }
-}
+};
 
 TestToSpeech::TestToSpeech(const Config &config) : config_(config), impl_(std::make_unique<Impl>()) {
     Impl &I = *impl_;
@@ -365,9 +393,7 @@ bool TestToSpeech::synthesize_to_vector(const VoiceModel &voice, const std::stri
         fprintf(stderr, "TestToSpeech: no speech codes parsed from text\n");
         return false;
     }
-    if (!impl_->decode_codes(voice, codes, out_audio, nullptr, nullptr)) return false;
-    if (options.apply_peak_normalization) peak_normalize(out_audio);
-    return true;
+    return impl_->decode_codes(voice, codes, out_audio, nullptr, nullptr, options.apply_peak_normalization);
 }
 
 bool TestToSpeech::synthesize_to_vector(const VoiceModel &voice, const std::string &text,
@@ -375,10 +401,35 @@ bool TestToSpeech::synthesize_to_vector(const VoiceModel &voice, const std::stri
     return synthesize_to_vector(voice, text, out_audio, Options{});
 }
 
+// synthesize_to_vector + wav_write (test-to-speech.cpp:322-330) with the PCM kept in HBM:
+// peak normalisation and the PCM16 conversion run on the device (mio_hip_pcm_finish), only the
+// 2-byte samples cross PCIe; the file bytes equal wav_write(normalised floats).
 bool TestToSpeech::synthesize_to_file(const VoiceModel &voice, const std::string &text,
                                       const std::string &output_path, const Options &options) {
-    std::vector<float> audio;
-    return synthesize_to_vector(voice, text, audio, options) && wav_write(output_path, audio, sample_rate());
+    if (!is_ready() || !voice.is_ready()) {
+        fprintf(stderr, "TestToSpeech: %s\n", !is_ready() ? "not ready" : "voice model is not ready");
+        return false;
+    }
+    std::string token_text;
+    if (!generate_token_text(text, options, token_text)) return false;
+    const std::vector<int> codes = parse_speech_tokens(token_text);
+    if (codes.empty()) {
+        fprintf(stderr, "TestToSpeech: no speech codes parsed from text\n");
+        return false;
+    }
+    Impl &I = *impl_;
+    int len = 0;
+    if (!I.decode_codes_dev(voice, codes, &len, nullptr, nullptr) ||
+        !I.ensure(I.d_pcm16, I.pcm16_cap, (size_t)len * 2 + 64))
+        return false;
+    std::vector<int16_t> pcm16(len);
+    if (mio_hip_pcm_finish(I.dev, (const float *)I.d_pcm, len, options.apply_peak_normalization ? 1 : 0,
+                           (int16_t *)I.d_pcm16, nullptr, nullptr) != MIO_OK ||
+        (len && mio_hip_memcpy_d2h(I.dev, pcm16.data(), I.d_pcm16, (size_t)len * 2) != MIO_OK)) {
+        fprintf(stderr, "TestToSpeech: PCM epilogue failed: %s\n", mio_hip_last_error());
+        return false;
+    }
+    return mio::wav_write_pcm16(output_path, pcm16.data(), pcm16.size(), sample_rate());
 }
 
 bool TestToSpeech::synthesize_to_file(const VoiceModel &voice, const std::string &text,

@@ -64,6 +64,7 @@ def _declare(L: ctypes.CDLL) -> None:
         "mio_hip_timer_mark": (c_int, [_vp, _vp, c_int]),
         "mio_hip_timer_elapsed": (c_int, [_vp, c_int, c_int, _f32p]),
         "mio_hip_pcm_finish": (c_int, [_vp, _vp, ctypes.c_int64, c_int, _vp, _f32p, _vp]),
+        "mio_hip_pcm_normalize": (c_int, [_vp, _vp, ctypes.c_int64, _vp, _f32p, _vp]),
         "mio_hip_istft_create": (c_int, [_vp, c_int, c_int, ctypes.POINTER(_vp)]),
         "mio_hip_istft_destroy": (None, [_vp]),
         "mio_hip_istft_out_len": (c_int, [_vp, c_int, c_int, ctypes.POINTER(c_int)]),
@@ -99,8 +100,6 @@ def _declare(L: ctypes.CDLL) -> None:
         "mio_hip_debug_matvec": (c_int, [_vp, ctypes.c_uint32, _vp, c_int, c_int, _vp, _vp]),
         "mio_quantize_rows": (c_int, [ctypes.c_uint32, _vp, c_int, c_int, _vp]),
         "mio_hip_llm_info": (c_int, [_vp, _i32p]),
-        "mio_hip_llm_set_decode_mode": (c_int, [_vp, c_int, ctypes.POINTER(c_int)]),
-        "mio_hip_llm_persist_timeline": (c_int, [_vp, _vp, c_int, ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),
         "mio_hip_llm_weight_bytes": (c_int, [_vp, ctypes.POINTER(ctypes.c_uint64)]),
         "mio_hip_llm_eval": (c_int, [_vp, ctypes.c_int32, c_int, _vp]),
         "mio_hip_llm_prefill": (c_int, [_vp, _vp, c_int, _vp]),
@@ -395,20 +394,6 @@ class Llm:
         except Exception:
             pass
 
-    def set_decode_mode(self, persistent: bool) -> int:
-        """Select the decode engine (persistent launch or per-step hipGraph); returns whether
-        the persistent launch has run for this model (1), is unavailable for its shape (0) or
-        is untried (-1)."""
-        a = ctypes.c_int(-1)
-        check(lib().mio_hip_llm_set_decode_mode(self.h, 1 if persistent else 0, ctypes.byref(a)))
-        return a.value
-
-    def persistent_active(self) -> int:
-        """State of the persistent engine (see set_decode_mode), mode unchanged."""
-        a = ctypes.c_int(-1)
-        check(lib().mio_hip_llm_set_decode_mode(self.h, -1, ctypes.byref(a)))
-        return a.value
-
     def weight_bytes(self) -> int:
         b = ctypes.c_uint64(0)
         check(lib().mio_hip_llm_weight_bytes(self.h, ctypes.byref(b)))
@@ -452,17 +437,6 @@ class Llm:
         n = ctypes.c_int(0)
         check(lib().mio_hip_llm_timeline(self.h, _ptr(out), 1024, ctypes.byref(n)))
         t = out[: n.value * 2048].astype(np.float64).reshape(n.value, 256, 8)
-        t[t == 0] = np.nan
-        return (t - np.nanmin(t[0, :, 0])) * 0.01
-
-    def persist_timeline(self) -> np.ndarray:
-        """[phase, workgroup, 8] marks (us from the launch's first mark, NaN = absent) of one
-        persistent decode step (diagnostic, mio_hip_llm_persist_timeline; advances the state)."""
-        nmax = 5 * self.n_layer + 2
-        out = np.zeros(nmax * 1024 * 8, np.uint64)
-        n, g = ctypes.c_int(0), ctypes.c_int(0)
-        check(lib().mio_hip_llm_persist_timeline(self.h, _ptr(out), nmax, ctypes.byref(n), ctypes.byref(g)))
-        t = out[: n.value * g.value * 8].astype(np.float64).reshape(n.value, g.value, 8)
         t[t == 0] = np.nan
         return (t - np.nanmin(t[0, :, 0])) * 0.01
 

@@ -52,10 +52,13 @@ class GGUFReader:
         n_t, n_kv = struct.unpack_from("<QQ", b, 8)
         self.pos = 24
         self.kv: Dict[str, Any] = {}
+        self.kv_raw: List[tuple] = []  # (key, raw bytes of the typed value) in file order
         for _ in range(n_kv):
             k = self._str()
+            p0 = self.pos
             t = self._u32()
             self.kv[k] = self._val(t)
+            self.kv_raw.append((k, bytes(self.mm[p0:self.pos])))
         self.tensors: List[Tensor] = []
         for _ in range(n_t):
             name = self._str()
@@ -126,3 +129,38 @@ def write_kv_gguf(path: str, kv: Dict[str, Any]) -> None:
             raise TypeError(k)
     with open(path, "wb") as f:
         f.write(bytes(out))
+
+
+def _gguf_str(x: str) -> bytes:
+    b = x.encode("utf-8")
+    return struct.pack("<Q", len(b)) + b
+
+
+def rewrite(src: str, dst: str, arch: str = None, extra_f32: str = None, drop_suffix: str = None) -> None:
+    """Copy GGUF `src` to `dst` (loader tests): general.architecture replaced by `arch` when
+    given, an extra 1-element F32 tensor named `extra_f32` appended when given, tensors whose
+    name ends in `drop_suffix` left out when given."""
+    r = GGUFReader(src)
+    kvs = []
+    for k, raw in r.kv_raw:
+        if k == "general.architecture" and arch is not None:
+            raw = struct.pack("<I", 8) + _gguf_str(arch)
+        kvs.append(_gguf_str(k) + raw)
+    tens = [(t.name, t.ne, t.type, t.raw()) for t in r.tensors
+            if not (drop_suffix and t.name.endswith(drop_suffix))]
+    if extra_f32:
+        tens.append((extra_f32, [1], 0, np.zeros(4, np.uint8)))
+    align = int(r.kv.get("general.alignment", 32))
+    infos, off = [], 0
+    for name, ne, ty, data in tens:
+        infos.append(_gguf_str(name) + struct.pack("<I", len(ne)) + b"".join(struct.pack("<Q", n) for n in ne)
+                     + struct.pack("<IQ", ty, off))
+        off = (off + len(data) + align - 1) // align * align
+    head = b"GGUF" + struct.pack("<IQQ", 3, len(tens), len(kvs)) + b"".join(kvs) + b"".join(infos)
+    with open(dst, "wb") as f:
+        f.write(head)
+        f.write(b"\0" * ((len(head) + align - 1) // align * align - len(head)))
+        for _, _, _, data in tens:
+            b = bytes(data)
+            f.write(b)
+            f.write(b"\0" * ((len(b) + align - 1) // align * align - len(b)))

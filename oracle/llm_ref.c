@@ -3,7 +3,7 @@
  *
  * CPU restatement of one llama_decode step (test-to-speech.cpp:178-185, :589-596) for the
  * GGUF architectures the synthetic models use ("llama": RoPE NORM; "qwen3": RoPE NEOX +
- * per-head q/k RMSNorm), in llama.cpp / ggml CPU semantics [upstream; parity unpinned]:
+ * per-head q/k RMSNorm; "qwen2": RoPE NEOX + q/k/v projection biases), in llama.cpp / ggml CPU semantics [upstream; parity unpinned]:
  *   rms_norm : sum x^2 in double, scale = 1/sqrtf(mean + eps), then * weight
  *   matvec   : activation re-quantized to the weight's vec_dot_type (quant_ref.c)
  *   rope     : theta = pos * base^(-2i/hd) by repeated float multiplication (ggml rope cache)
@@ -35,11 +35,12 @@ int mo_dequantize_row(uint32_t type, const uint8_t *row, int64_t k, float *y);
 
 typedef struct {
     const mo_tensor *attn_norm, *wq, *wk, *wv, *wo, *q_norm, *k_norm, *ffn_norm, *gate, *up, *down;
+    const mo_tensor *bq, *bk, *bv; /* qwen2 projection biases (or NULL) */
 } mo_layer;
 
 struct mo_llm {
     mo_gguf *g;
-    int qwen3;
+    int qwen3, neox;
     int n_embd, n_layer, n_head, n_kv, hd, n_ff, n_vocab, n_ctx;
     float base, eps;
     mo_layer *L;
@@ -67,6 +68,7 @@ mo_llm *mo_llm_load(const char *path, int n_ctx) {
     m->g = g;
     const char *a = ak->str;
     m->qwen3 = strcmp(a, "qwen3") == 0;
+    m->neox = m->qwen3 || strcmp(a, "qwen2") == 0; /* llama.cpp LLM_ARCH_QWEN2/3: LLAMA_ROPE_TYPE_NEOX */
     char key[128];
 #define KI(s, def) (snprintf(key, sizeof key, "%s." s, a), (int)mo_gguf_int(g, key, def))
 #define KF(s, def) (snprintf(key, sizeof key, "%s." s, a), (float)mo_gguf_float(g, key, def))
@@ -101,6 +103,9 @@ mo_llm *mo_llm_load(const char *path, int n_ctx) {
         l->gate = T(g, "blk.%d.ffn_gate.weight", i);
         l->up = T(g, "blk.%d.ffn_up.weight", i);
         l->down = T(g, "blk.%d.ffn_down.weight", i);
+        l->bq = T(g, "blk.%d.attn_q.bias", i);
+        l->bk = T(g, "blk.%d.attn_k.bias", i);
+        l->bv = T(g, "blk.%d.attn_v.bias", i);
         if (!l->attn_norm || !l->wq || !l->wk || !l->wv || !l->wo || !l->ffn_norm || !l->gate ||
             !l->up || !l->down) {
             mo_gguf_close(g);
@@ -215,13 +220,17 @@ int mo_llm_eval(mo_llm *m, int token, int pos, float *logits) {
         matvec(m, l->wq, m->h, m->q);
         matvec(m, l->wk, m->h, m->k);
         matvec(m, l->wv, m->h, m->v);
+        /* qwen2: Qcur = ggml_add(ggml_mul_mat(wq, cur), bq), likewise K and V */
+        if (l->bq) for (int i = 0; i < H * hd; i++) m->q[i] += ((const float *)l->bq->data)[i];
+        if (l->bk) for (int i = 0; i < Hk * hd; i++) m->k[i] += ((const float *)l->bk->data)[i];
+        if (l->bv) for (int i = 0; i < Hk * hd; i++) m->v[i] += ((const float *)l->bv->data)[i];
         for (int h = 0; h < H; h++) {
             if (m->qwen3 && l->q_norm) rms_norm(m->q + h * hd, hd, (const float *)l->q_norm->data, m->eps, m->q + h * hd);
-            rope(m->q + h * hd, hd, pos, m->base, m->qwen3);
+            rope(m->q + h * hd, hd, pos, m->base, m->neox);
         }
         for (int h = 0; h < Hk; h++) {
             if (m->qwen3 && l->k_norm) rms_norm(m->k + h * hd, hd, (const float *)l->k_norm->data, m->eps, m->k + h * hd);
-            rope(m->k + h * hd, hd, pos, m->base, m->qwen3);
+            rope(m->k + h * hd, hd, pos, m->base, m->neox);
             uint16_t *kd = m->kc + (((size_t)il * Hk + h) * m->n_ctx + pos) * hd;
             uint16_t *vd = m->vc + (((size_t)il * Hk + h) * m->n_ctx + pos) * hd;
             for (int d = 0; d < hd; d++) {
@@ -301,4 +310,13 @@ int mo_sample(const float *logits, float temp, uint64_t seed, int step, int lo, 
         }
     }
     return arg;
+}
+
+/* OpenMP threads of every oracle loop (bench.py cpu_baseline times 16 and 4 threads);
+ * returns the previous maximum. */
+#include <omp.h>
+int mo_set_threads(int n) {
+    const int prev = omp_get_max_threads();
+    if (n > 0) omp_set_num_threads(n);
+    return prev;
 }

@@ -56,6 +56,7 @@ void mo_llm_reset(mo_llm *m);
 int mo_llm_eval(mo_llm *m, int token, int pos, float *logits /* [n_vocab] or NULL */);
 float mo_gumbel(uint64_t seed, int step, int idx);
 int mo_sample(const float *logits, float temp, uint64_t seed, int step, int lo, int hi);
+int mo_set_threads(int n);
 /* ggml block helpers (quant_ref.c) */
 float mo_fp16_to_f32(uint16_t h);
 uint16_t mo_f32_to_fp16(float f);

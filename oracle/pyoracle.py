@@ -56,6 +56,8 @@ def oracle() -> ctypes.CDLL:
         _o.mo_sample.restype = ci
         _o.mo_sample.argtypes = [vp, ctypes.c_float, ctypes.c_uint64, ci, ci, ci]
         _o.mo_dequantize_row.argtypes = [ctypes.c_uint32, vp, ctypes.c_int64, vp]
+        _o.mo_set_threads.restype = ci
+        _o.mo_set_threads.argtypes = [ci]
     return _o
 
 
@@ -191,3 +193,8 @@ class Llm:
 def sample(logits: np.ndarray, temperature: float, seed: int, step: int, lo: int, hi: int) -> int:
     logits = np.ascontiguousarray(logits, dtype=np.float32)
     return int(oracle().mo_sample(logits.ctypes.data, temperature, seed, step, lo, hi))
+
+
+def set_threads(n: int) -> int:
+    """OpenMP threads of the oracle's loops; returns the previous maximum."""
+    return int(oracle().mo_set_threads(int(n)))

@@ -29,3 +29,19 @@ def device():
     d = m.Device(0)
     yield d
     d.close()
+
+
+@pytest.fixture(scope="session")
+def synth_llm_path(tmp_path_factory):
+    """synth_llm_path(preset) -> path of the synthetic LLM GGUF of that preset (seed 1),
+    written once per test session (the 1.7B / 2.6B files take seconds to synthesize)."""
+    import miotts_amd as m
+    d = tmp_path_factory.mktemp("llm_models")
+    cache = {}
+
+    def get(preset: int) -> str:
+        if preset not in cache:
+            cache[preset] = m.synth_llm(str(d / f"llm{preset}.gguf"), preset, 1)
+        return cache[preset]
+
+    return get

@@ -126,6 +126,9 @@ def main() -> None:
         "noise": (rng.standard_normal(1000) * 0.5).astype(np.float32),
         "edges": np.array([1.0, -1.0, 0.99999, -0.99999, 1.00002, -1.00004, 0.5 / 32767,
                            -0.5 / 32767, 1.5 / 32767, -1.5 / 32767, 0.0, -0.0], np.float32),
+        # std::clamp passes NaN through; static_cast<int16_t> of it is the x86 cvttss2si
+        # integer-indefinite 0x80000000 truncated to 16 bits = 0 (the reference's bytes)
+        "nan_inf": np.array([np.nan, -np.nan, np.inf, -np.inf, 0.25, np.nan], np.float32),
     }
     with tempfile.TemporaryDirectory() as td:
         for k, v in vecs.items():

@@ -69,3 +69,22 @@ def test_timed_region_single_rank():
     elapsed, samples = bench.timed_region(2, 4, 1, 0, lambda seed, rec: n.append(rec) or 7,
                                           lambda: None, lambda: None, None)
     assert samples == 28 and n.count(False) == 2 and n.count(True) == 4 and elapsed >= 0
+
+
+def test_bench_launcher_spawns_ranks():
+    """`bench.py --gpus 2` without torchrun: the parent starts 2 fresh child ranks (RANK /
+    LOCAL_RANK / WORLD_SIZE / MASTER_* set, gloo rendezvous on 127.0.0.1) before any GPU use
+    and exits with their status; rank 0 prints one line with n_gpus = 2 and the SUM of both
+    ranks' audio over the MAX elapsed."""
+    import json
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "3",
+                        "--warmup", "1", "--launcher-selftest"], capture_output=True, text=True, timeout=180,
+                       env=env)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    r = json.loads(lines[0])
+    assert r["n_gpus"] == 2 and r["samples"] == 2 * 3 * 1000
+    assert r["elapsed"] >= 3 * 0.04  # the slower rank (rank 1) sets the time

@@ -113,3 +113,17 @@ def test_stream_compare_skip_llm(files):
     assert int(r["sample_diff"]) == 0
     # --skip-llm streams the whole decode in one pass: identical to the offline vector
     assert float(r["compare.max_abs"]) == 0.0
+
+
+def test_stream_benchmark_1p7b_700_tokens(files, synth_llm_path):
+    """BASELINE configs[4] (C5): the streaming path on the 1.7B Q4_K_M preset, 700 tokens ->
+    18 full re-decodes / 7160 codes (test-to-speech.cpp:496-571 cadence), every sample emitted."""
+    out = run(["miotts-stream-benchmark", "-m", synth_llm_path(3), "-c", files["codec"], "-v", files["voice"],
+               "-p", "こんにちは、今日はいい天気ですね。", "--max-tokens", 700, "--speech-only", "--ignore-eos"],
+              timeout=600)
+    r = kv(out)
+    assert int(r["stream_bench.llm_tokens"]) == 700
+    assert int(r["stream_bench.decode_calls"]) == 18
+    assert int(r["stream_bench.decoded_codes"]) == 7160
+    assert int(r["stream_bench.emitted_samples"]) == 700 * 1764
+    print({k: r[k] for k in r if k.startswith("stream_bench.")})

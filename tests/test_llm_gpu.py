@@ -3,12 +3,17 @@
 1. Single matvec per quant type (Q8_0 / Q4_K / Q6_K) on random data: the GPU's per-
    superblock integer sums are exact, only the float sum over superblocks is reordered:
    |y_gpu - y_ref| <= 1e-5 * sum_b |partial_b| (bounded here by 2e-5 * max|y| + 1e-6).
-2. Teacher-forced logits over 80 positions (crosses the 64-position attention split):
-   exact while no activation re-quantization code flips (measured 0.0 / 2e-7 at pos 0-1);
-   beyond that, int8 re-quantization (the reference's own semantics) turns ulp-level f32
-   differences into single-code flips, measured <= 1.3e-2 of max|logit| on the tiny models
-   and ~4e-2 RMS after the 28 layers of the 1.7B model. Bounds: tiny max rel <= 5e-2,
-   argmax agreement >= 95%; 1.7B RMS(diff) <= 0.1 * RMS(logits), top-1 equal.
+2. Teacher-forced logits: tiny models over 80 positions, the 1.7B model over 300 positions
+   and the 0.1B (G = 3, hd 64) / 2.6B (G = 4, hd 64) models over 160 positions, i.e. across
+   the 128-position attention chunks (kAttChunk, csrc/hip/llm_kernels.h) whose partial records
+   k_attn_out merges. Exact while no activation re-quantization code flips (measured 0.0 /
+   2e-7 at pos 0-1); beyond that, int8 re-quantization (the reference's own semantics, ggml
+   quantizes every matvec input to the weight's vec_dot_type) turns ulp-level f32 differences
+   into single-code flips, measured <= 1.3e-2 of max|logit| on the tiny models and ~4e-2 RMS
+   after the 28 layers of the 1.7B model. That error does not depend on the position, so one
+   bound holds at every position: tiny max rel <= 5e-2; large models RMS(diff) <= 0.1 *
+   RMS(logits) per position; argmax agreement >= 95% of positions. A wrong chunk merge or
+   mask at a chunk boundary moves every later position's logits by O(RMS(logits)).
 3. Free-running sampling (temperature 0.8, seed 42, speech ids only): sampled ids equal the
    oracle's (shared counter-based Gumbel-max sampler) for >= 95% of 40 tokens (measured 100%).
 """
@@ -84,17 +89,110 @@ def test_generate_stops_at_eos(device, llm_files):
     assert len(toks) < 200 and (toks != m.SYNTH_EOT).all()
 
 
-def test_logits_1p7b_q4km(device, tmp_path):
-    path = m.synth_llm(str(tmp_path / "llm17.gguf"), 3, 1)
-    g = m.Llm(device, path, 256)
-    assert g.n_layer == 28 and g.n_vocab == 164736
-    o = pyoracle.Llm(path, 256)
-    toks = [256, 257, 1000, 5000]
+def _teacher_forced(device, path, n_pos, seed):
+    """Per-position (rel RMS diff, argmax equal) of GPU vs oracle logits over n_pos positions."""
+    g = m.Llm(device, path, 512)
+    o = pyoracle.Llm(path, 512)
+    toks = np.random.default_rng(seed).integers(0, g.n_vocab, n_pos)
+    rel, agree = [], []
     for pos, t in enumerate(toks):
-        lg, lo = g.eval(t, pos), o.eval(t, pos)
+        lg, lo = g.eval(int(t), pos), o.eval(int(t), pos)
         d = lg.astype(np.float64) - lo
-        assert np.sqrt(np.mean(d * d)) <= 0.1 * np.sqrt(np.mean(lo.astype(np.float64) ** 2))
-        assert lg.argmax() == lo.argmax()
+        rel.append(np.sqrt(np.mean(d * d)) / np.sqrt(np.mean(lo.astype(np.float64) ** 2)))
+        agree.append(lg.argmax() == lo.argmax())
+    g.close()
+    return np.array(rel), np.array(agree)
+
+
+@pytest.mark.parametrize("preset,n_pos", [(3, 300), (2, 160), (4, 160)])
+def test_teacher_forced_large_models(device, synth_llm_path, preset, n_pos):
+    """1.7B Q4_K_M (G = 2, hd 128, qwen3 q/k norm), 0.1B Q8_0 (G = 3) and 2.6B Q8_0 (G = 4):
+    every position within the bound, through chunk boundaries 128 and 256."""
+    rel, agree = _teacher_forced(device, synth_llm_path(preset), n_pos, 300 + preset)
+    print(f"preset {preset}: rel RMS max {rel.max():.3g} at pos {int(rel.argmax())}, "
+          f"median {np.median(rel):.3g}, argmax agree {agree.sum()}/{n_pos}")
+    assert rel[:2].max() <= 1e-4, rel[:2]
+    assert rel.max() <= 0.1, (int(rel.argmax()), rel.max())
+    assert agree.sum() >= 0.95 * n_pos
+
+
+def _free_run_agreement(device, path, preset, temp, n):
+    g = m.Llm(device, path, 512)
+    o = pyoracle.Llm(path, 512)
+    prompt = [256, 257] + list(b"free run of the synthetic model") + [258, 257]
+    allow = (m.SYNTH_SPEECH0, m.SYNTH_SPEECH0 + 12800)
+    tg = g.generate(prompt, n, temp, 42 + preset, allow=allow)
+    to = o.generate(prompt, n, temp, 42 + preset, allow=allow)
+    g.close()
+    assert len(tg) == len(to) == n
+    same = tg == to
+    first = int(np.argmin(same)) if not same.all() else n
+    return tg, to, first
+
+
+@pytest.mark.parametrize("preset", [2, 4])
+def test_free_run_64_tokens_large_models(device, synth_llm_path, preset):
+    """64 sampled ids (temperature 0.8, shared counter-based Gumbel-max) equal the oracle's."""
+    tg, to, first = _free_run_agreement(device, synth_llm_path(preset), preset, 0.8, 64)
+    print(f"preset {preset}: first divergence at {first} of 64")
+    assert first >= 60, (first, tg, to)
+
+
+@pytest.mark.parametrize("preset", [0, 1, 2, 5])
+def test_greedy_token_equality(device, synth_llm_path, preset):
+    """Greedy decoding (-t 0: temperature <= 0 takes the argmax): the id
+    stream equals the oracle's. A divergence is accepted only at a near-tie of the oracle's
+    top two logits (within the 5e-2 teacher-forced bound); everything before it must match."""
+    path = synth_llm_path(preset)
+    g = m.Llm(device, path, 256)
+    o = pyoracle.Llm(path, 256)
+    prompt = [256, 257] + list(b"greedy") + [258, 257]
+    allow = (m.SYNTH_SPEECH0, m.SYNTH_SPEECH0 + 12800)
+    n = 48
+    tg = g.generate(prompt, n, 0.0, 1, allow=allow)
+    assert len(tg) == n
+    # oracle greedy loop with its logits kept, to judge a divergence
+    for i, t in enumerate(prompt):
+        lo = o.eval(int(t), i)
+    for j in range(n):
+        sub = lo[allow[0]:allow[1]]
+        want = allow[0] + int(sub.argmax())
+        if tg[j] != want:
+            top2 = np.sort(sub)[-2:]
+            gap = float(top2[1] - top2[0])
+            assert gap <= 5e-2 * float(np.abs(sub).max()), (j, tg[j], want, gap)
+            break
+        lo = o.eval(int(tg[j]), len(prompt) + j)
+    g.close()
+
+
+def test_qwen2_bias_logits_and_generate(device, synth_llm_path, tmp_path):
+    """qwen2 (RoPE NEOX + attn_{q,k,v}.bias added before RoPE, llama.cpp build_qwen2): the
+    biases reach the logits (they differ from the same file read without them by far more
+    than the bound) and GPU == oracle within the teacher-forced bound."""
+    from miotts_amd import gguf_np
+    rel, agree = _teacher_forced(device, synth_llm_path(5), 140, 5)
+    assert rel[:2].max() <= 1e-4 and rel.max() <= 5e-2 and agree.sum() >= 133
+    nob = str(tmp_path / "nobias.gguf")
+    gguf_np.rewrite(synth_llm_path(5), nob, drop_suffix=".bias")
+    g, g0 = m.Llm(device, synth_llm_path(5), 64), m.Llm(device, nob, 64)
+    a, b = g.eval(300, 0), g0.eval(300, 0)
+    assert np.sqrt(np.mean((a - b).astype(np.float64) ** 2)) >= 0.2 * np.sqrt(np.mean(b.astype(np.float64) ** 2))
+    g.close(), g0.close()
+    tg, to, first = _free_run_agreement(device, synth_llm_path(5), 5, 0.8, 40)
+    assert first >= 38
+
+
+def test_loader_rejects_lfm2_and_unknown_biases(device, tmp_path):
+    """lfm2 is refused by name (hybrid short-conv block not implemented); a bias tensor other
+    than attn_{q,k,v}.bias is refused rather than silently dropped."""
+    from miotts_amd import gguf_np
+    src = m.synth_llm(str(tmp_path / "q2.gguf"), 5, 1)
+    for arch, extra, msg in [("lfm2", None, "short-conv"), (None, "blk.0.ffn_down.bias", "bias tensor")]:
+        dst = str(tmp_path / "patched.gguf")
+        gguf_np.rewrite(src, dst, arch=arch, extra_f32=extra)
+        with pytest.raises(m.HipError, match=msg):
+            m.Llm(device, dst, 128)
 
 
 # --- batched prompt prefill (csrc/hip/llm_prefill.hip; reference prefill llama_decode,

@@ -118,3 +118,24 @@ def test_sampler_distribution_matches_softmax():
     assert np.abs(counts / n - p).max() < 0.015
     assert pyoracle.sample(logits, 0.0, 42, 0, 0, 5) == 1
     assert pyoracle.sample(logits, 0.8, 42, 3, 2, 4) in (2, 3)
+
+
+def test_qwen2_bias_oracle_and_rewrite(tmp_path):
+    """Synthetic qwen2 (preset 5) carries attn_{q,k,v}.bias; the oracle adds them before RoPE
+    (llama.cpp build_qwen2: Qcur = ggml_add(ggml_mul_mat(wq, cur), bq)), so logits move when
+    the biases are dropped (gguf_np.rewrite, the GPU loader tests' file patcher)."""
+    src = m.synth_llm(str(tmp_path / "q2.gguf"), 5, 1)
+    r = gguf_np.GGUFReader(src)
+    assert r.kv["general.architecture"] == "qwen2"
+    assert {"blk.0.attn_q.bias", "blk.0.attn_k.bias", "blk.0.attn_v.bias"} <= set(r.by_name)
+    nob = str(tmp_path / "nobias.gguf")
+    gguf_np.rewrite(src, nob, drop_suffix=".bias")
+    r2 = gguf_np.GGUFReader(nob)
+    assert not any(t.name.endswith(".bias") for t in r2.tensors)
+    assert np.array_equal(r2.tensor("blk.1.ffn_up.weight").raw(), r.tensor("blk.1.ffn_up.weight").raw())
+    a = pyoracle.Llm(src, 32).eval(300, 0)
+    b = pyoracle.Llm(nob, 32).eval(300, 0)
+    assert np.sqrt(np.mean((a - b).astype(np.float64) ** 2)) >= 0.2 * np.sqrt(np.mean(b.astype(np.float64) ** 2))
+    lf = str(tmp_path / "lfm2.gguf")
+    gguf_np.rewrite(src, lf, arch="lfm2")
+    assert gguf_np.GGUFReader(lf).kv["general.architecture"] == "lfm2"
