@@ -488,7 +488,8 @@ __global__ __launch_bounds__(ST) void k_bt_sample(LlmDims d, QMat emb, int nblk,
         sc.out_tokens[step] = tok;
         if (tok == sc.eos0 || tok == sc.eos1) st->done = 1;
         st->token = tok;
-        st->pos = st->pos + 1;
+        // a stream ending at a full context stays frozen on its last cache row
+        st->pos = min(st->pos + 1, d.n_ctx - 1);
         st->step = step + 1;
     }
 }

@@ -78,7 +78,19 @@ def test_batch_rejects_bad_shapes(device, llm_files):
     with pytest.raises(m.HipError):
         g.generate_batch([[256, 257]] * 17, 4, 0.8)
     with pytest.raises(m.HipError):
-        g.generate_batch([[256] * 40], 30, 0.8)  # 40 + 30 > n_ctx 64
+        g.generate_batch([[256] * 65], 4, 0.8)  # prompt longer than n_ctx 64
+
+
+def test_context_full_ends_generation(device, llm_files):
+    """40 prompt + 30 new > n_ctx 64: like the reference (test-to-speech.cpp:163-187, decode
+    fails at a full context and the last sampled token is kept), generation stops after
+    n_ctx - 40 + 1 = 25 tokens instead of failing; single and batched streams agree."""
+    g = m.Llm(device, llm_files[0], 64)
+    p = [256] + [65 + i % 20 for i in range(39)]
+    single = g.generate(p, 30, 0.8, 5, allow=ALLOW)
+    assert len(single) == 25
+    both = g.generate_batch([p, p[:10]], 30, 0.8, [5, 6], allow=ALLOW)
+    assert np.array_equal(both[0], single) and len(both[1]) == 30
 
 
 def test_batch_1p7b_q4km(device, tmp_path):
