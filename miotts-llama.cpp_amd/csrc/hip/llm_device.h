@@ -1067,22 +1067,6 @@ __device__ __forceinline__ void load_kv_rows(const _Float16 *kbase, const _Float
     }
 }
 
-// The whole chunk [t0, t0 + ATT_CHUNK) of this thread's slot, issued at kernel entry before
-// the decode position is known (rows past pos are masked by the caller; rows are clamped to
-// the cache, t_max = n_ctx - 1, so every load stays in bounds).
-template <int HD>
-__device__ __forceinline__ void load_kv_chunk(const _Float16 *kbase, const _Float16 *vbase, int t0, int t_max,
-                                              h8 (&kr)[AttCfg<HD>::IT], h8 (&vr)[AttCfg<HD>::IT]) {
-    constexpr int LP = AttCfg<HD>::LP, NS = AttCfg<HD>::NS;
-    const int lp = (MIO_TIDX & 63) % LP, sl = MIO_TIDX / LP;
-#pragma unroll
-    for (int it = 0; it < AttCfg<HD>::IT; ++it) {
-        const int t = min(t0 + sl + NS * it, t_max);
-        kr[it] = *reinterpret_cast<const h8 *>(kbase + (size_t)t * HD + lp * 8);
-        vr[it] = *reinterpret_cast<const h8 *>(vbase + (size_t)t * HD + lp * 8);
-    }
-}
-
 // Softmax attention of the G query heads qs (LDS, prepared) over the chunk's positions
 // [t0, min(t0 + ATT_CHUNK, pos + 1)) whose K/V rows are in kr/vr, in two passes like ggml's
 // soft_max (scores, chunk max, exp, sums; summation order aside): every slot's scores are

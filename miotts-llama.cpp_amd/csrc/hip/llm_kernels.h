@@ -61,8 +61,6 @@ struct LlmBuffers {
     float *part;       // [H][max_splits][hd + 4] attention chunk partials {O, m, l}
     float *smp;        // sampler partials [2 * n_lm_blocks]
     const float2 *rope;  // [n_ctx][hd/2] (cos, sin)
-    float2 *rope_cur;    // [hd/2] rope row of st->pos (written by the launch that sets pos), so
-                         // the attention kernel's loads never wait for pos
     StepState *st;
     const SampleCfg *cfg;       // sampling configuration (device-resident: graphs never re-capture)
     unsigned long long *trace;  // optional: per-kernel checkpoint timestamps (workgroup 0, thread 0)
@@ -121,14 +119,10 @@ void launch_batch_embed(const LlmDims &d, const QMat &tok_embd, const PrefillBuf
                         int B, hipStream_t s);
 
 // Launch one kernel of a decode step (which: 0 attn_in, 1 attention, 2 attn_out, 3 ffn_in,
-// 4 ffn_down of layer il; 6 lm_head, 7 sampler) on stream s. nch = attention chunks of the
-// step's position (pos / kAttChunk + 1): the attention grid and the chunk merge are sized by
-// it at launch (the step graphs are captured per nch), so no kernel waits for the device
-// state before issuing its K/V or partial-record loads.
+// 4 ffn_down of layer il; 6 lm_head, 7 sampler) on stream s.
 void launch_step_kernel(int which, const LlmDims &d, const LayerW *layers, int il, _Float16 *kcache,
                         _Float16 *vcache, const float *out_norm, const QMat &lm, const QMat &tok_embd,
-                        const LlmBuffers &b, int nch, hipStream_t s);
-inline int att_chunks(int pos) { return pos / kAttChunk + 1; }
+                        const LlmBuffers &b, hipStream_t s);
 // Embedding of `token` (row of token_embd) -> b.x, and state reset to (pos, token).
 void launch_embed_token(const LlmDims &d, const QMat &tok_embd, const LlmBuffers &b, hipStream_t s);
 int lm_head_blocks(const LlmDims &d);

@@ -93,7 +93,7 @@ __device__ inline float lane_value(float v, int i) {
 }
 
 template <int NP, int T, int SU, bool DG>
-__global__ __launch_bounds__(MT) void k_attn_out(LlmDims d, QMat wo, LlmBuffers b, int nch) {
+__global__ __launch_bounds__(MT) void k_attn_out(LlmDims d, QMat wo, LlmBuffers b) {
     constexpr bool kDiag = DG;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     MIO_TRACE(b, 0);
@@ -107,7 +107,7 @@ __global__ __launch_bounds__(MT) void k_attn_out(LlmDims d, QMat wo, LlmBuffers 
     load_first<T, NP, 1, SU>(wo, wo, lo, hi, ga, gb);
     MIO_TRACE(b, 1);
     MIO_TL_MARK1(b);
-    merge_attention<NP>(d, b.part, nch, K, T != 8, s, MIO_TL_DIAGSLOT(b));
+    merge_attention<NP>(d, b.part, b.st->pos / ATT_CHUNK + 1, K, T != 8, s, MIO_TL_DIAGSLOT(b));
     MIO_TRACE(b, 2);
     MIO_TL_MARK(b, 2);
     stream_rows<T, NP, 1, SU>(wo, wo, lo, hi, ga, gb, s.a, [&](int row, float v, float) {
@@ -248,12 +248,9 @@ __global__ __launch_bounds__(MT) void k_lm_head(LlmDims d, const float *norm_w, 
 }
 
 // ------------------------------------------------------------------ attention
-// One 512-thread workgroup per (chunk of ATT_CHUNK = 128 positions, kv head), grid = the
-// chunks of the step's position (host-sized): every load is issued at entry, independent of
-// the device state: the chunk's K/V rows (the last chunk's rows past pos are masked once pos
-// arrives), q|k|v, and the rope row of pos (rope_cur, written by the launch that set pos).
-// Then q/k RMSNorm (qwen3) + RoPE + f16 rounding, the chunk owning `pos` appends the new
-// k/v row to the F16 cache, and the G q heads sharing the kv head attend over the chunk. Its
+// One 256-thread workgroup per (chunk of ATT_CHUNK = 128 positions, kv head): q/k RMSNorm
+// (qwen3) + RoPE + f16 rounding, the chunk owning `pos` appends the new k/v row to the F16
+// cache, then an online softmax over the chunk for the G q heads sharing the kv head. Its
 // partial record {O[HD], m, l} per q head is merged with the other chunks' in the prologue
 // of k_attn_out (the launch-boundary reduce: no extra launch, no in-kernel hand-off).
 template <int HD, int G, bool DG>
@@ -269,25 +266,21 @@ __global__ __launch_bounds__(ATT_NT) void k_attention(LlmDims d, const float *q_
     MIO_TRACE(b, 0);
     MIO_TL_BEGIN(b);
     const int kvh = blockIdx.y, ch = blockIdx.x;
+    // every kernel argument the workgroup uses is loaded in the round trip that fetches
+    // b.st (without this the compiler sinks them below the pos-dependent exit: a third
+    // scalar-load round trip before the first K/V load)
+    asm volatile("" ::"s"(kc), "s"(vc), "s"(d.n_ctx), "s"(b.qkv), "s"(b.rope), "s"(q_norm), "s"(k_norm),
+                 "s"(b.part), "s"(d.max_splits), "s"(bqkv));
+    const int pos = b.st->pos;
     const int t0 = ch * ATT_CHUNK;
+    if (t0 > pos) return;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    // K/V rows of the whole chunk first: they need nothing but the kernel arguments
+    const float2 *rope = b.rope + (size_t)pos * (HD / 2);
+    // K/V rows of this slot first (row `pos` is never consumed from the cache)
     h8 kr[C::IT], vr[C::IT];
-    load_kv_chunk<HD>(kc + (size_t)kvh * d.n_ctx * HD, vc + (size_t)kvh * d.n_ctx * HD, t0, d.n_ctx - 1, kr, vr);
+    load_kv_rows<HD>(kc + (size_t)kvh * d.n_ctx * HD, vc + (size_t)kvh * d.n_ctx * HD, t0, pos, kr, vr);
     MIO_TRACE(b, 1);
     MIO_TL_MARK1(b);
-    const int pos = b.st->pos;
-    if (t0 > pos) {
-        // host-sized grid: only a diagnostic replay past its captured position gets here; an
-        // empty record {O = 0, m = -inf, l = 0} keeps the merge exact
-        float *o = b.part + ((size_t)(kvh * G) * d.max_splits + ch) * C::REC;
-        for (int e = threadIdx.x; e < G * (HD + 2); e += ATT_NT) {
-            const int g = e / (HD + 2), k = e - g * (HD + 2);
-            o[(size_t)g * d.max_splits * C::REC + k] = k == HD ? -INFINITY : 0.0f;
-        }
-        return;
-    }
-    const float2 *rope = b.rope_cur;
     // q heads (waves 0..G-1) and, for the chunk owning `pos`, the new k/v row
     const bool owner = pos < t0 + ATT_CHUNK;
     for (int hh = wave; hh < G + (owner ? 1 : 0); hh += ATT_NW) {
@@ -319,14 +312,9 @@ __global__ __launch_bounds__(ATT_NT) void k_attention(LlmDims d, const float *q_
     lds_barrier();
     MIO_TRACE(b, 2);
     MIO_TL_MARK(b, 2);
+    // the slot owning row `pos` takes it from LDS (exact f16 values, the cache row's bits)
     if (owner) {
-        // rows past pos: V zeroed (their p is 0; stale cache contents never reach a sum),
-        // and the slot owning row `pos` takes it from LDS (exact f16 values, the cache row's
-        // bits)
         const int sl = threadIdx.x / C::LP, lp = lane % C::LP, r = pos - t0;
-#pragma unroll
-        for (int it = 0; it < C::IT; ++it)
-            if (sl + C::NS * it > r) vr[it] = h8{};
         if (sl == r % C::NS) {
             h8 kn, vn;
 #pragma unroll
@@ -368,7 +356,7 @@ __global__ __launch_bounds__(ST) void k_sample(LlmDims d, QMat emb, int nblk, Ll
     MIO_TRACE(b, 0);
     MIO_TL_BEGIN(b);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int step = b.st->step, pos = b.st->pos;
+    const int step = b.st->step;
     float best = -INFINITY;
     int bi = INT_MAX;
     for (int i = tid; i < nblk; i += ST) {
@@ -397,25 +385,20 @@ __global__ __launch_bounds__(ST) void k_sample(LlmDims d, QMat emb, int nblk, Ll
     MIO_TRACE(b, 1);
     MIO_TL_MARK1(b);
     embed_row(emb, tok, d.n_embd, b.x);
-    // a full context ends generation (host-side step budget); the state never points past
-    // the cache, so later diagnostic launches stay in bounds
-    const int npos = min(pos + 1, d.n_ctx - 1);
-    for (int i = tid; i < d.hd / 2; i += ST) b.rope_cur[i] = b.rope[(size_t)npos * (d.hd / 2) + i];
     MIO_TL_END(b);
     MIO_TRACE(b, 15);
     if (tid == 0) {
         if (step < sc.max_steps) sc.out_tokens[step] = tok;
         if (tok == sc.eos0 || tok == sc.eos1) b.st->done = 1;
         b.st->token = tok;
-        b.st->pos = npos;
+        // a full context ends generation (host-side step budget); the state never points
+        // past the cache, so later diagnostic launches stay in bounds
+        b.st->pos = min(b.st->pos + 1, d.n_ctx - 1);
         b.st->step = step + 1;
     }
 }
 
-// decode start (state set by the host): embedding of st->token and the rope row of st->pos
 __global__ __launch_bounds__(ST) void k_embed(LlmDims d, QMat emb, LlmBuffers b) {
-    const int pos = b.st->pos;
-    for (int i = threadIdx.x; i < d.hd / 2; i += ST) b.rope_cur[i] = b.rope[(size_t)pos * (d.hd / 2) + i];
     embed_row(emb, b.st->token, d.n_embd, b.x);
 }
 
@@ -472,8 +455,7 @@ void dispatch_su(int su, F &&f) {
 // lm_head), 6 lm_head, 7 sample.
 void launch_step_kernel(int which, const LlmDims &d, const LayerW *layers, int il, _Float16 *kcache,
                         _Float16 *vcache, const float *out_norm, const QMat &lm, const QMat &tok_embd,
-                        const LlmBuffers &b, int nch, hipStream_t s) {
-    nch = std::max(1, std::min(nch, d.max_splits));
+                        const LlmBuffers &b, hipStream_t s) {
     const size_t layer_kv = (size_t)d.n_kv * d.n_ctx * d.hd;
     const int G = d.n_head / d.n_kv;
     // diagnostic instantiations only when a trace / timeline buffer is attached
@@ -507,7 +489,7 @@ void launch_step_kernel(int which, const LlmDims &d, const LayerW *layers, int i
         }
         case 1: {
             const LayerW &L = layers[il];
-            const dim3 grid(nch, d.n_kv);
+            const dim3 grid(d.max_splits, d.n_kv);
             if (d.hd == 128)
                 launch_attention<128, DG>(G, grid, s, d, L, kcache + il * layer_kv, vcache + il * layer_kv, b);
             else
@@ -519,8 +501,7 @@ void launch_step_kernel(int which, const LlmDims &d, const LayerW *layers, int i
             const int grid = matvec_grid(d, L.wo.rows);
             dispatch_nt(L.wo.k, L.wo.type, [&]<int NP, int T>() {
                 dispatch_su<NP>(pick_su(max_wave_units(L.wo.rows, grid, NP, 1), NP), [&]<int SU>() {
-                    hipLaunchKernelGGL((k_attn_out<NP, T, SU, DG>), dim3(grid), dim3(MT), mv_lds(L.wo.k), s, d, L.wo, b,
-                                       nch);
+                    hipLaunchKernelGGL((k_attn_out<NP, T, SU, DG>), dim3(grid), dim3(MT), mv_lds(L.wo.k), s, d, L.wo, b);
                 });
             });
             break;

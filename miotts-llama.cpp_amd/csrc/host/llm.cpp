@@ -57,13 +57,9 @@ struct mio_hip_llm {
     };
     std::vector<Range> ranges;
 
-    // decode-step graphs (the sampling config is device-resident), captured once per
-    // attention chunk count nch = pos / kAttChunk + 1 (the attention grid and the chunk merge
-    // are sized by it, so no kernel waits for the device position before its loads): one
-    // step, and kGraphSteps steps back to back (fewer graph launches per token). Captured on
-    // their own stream, launched on the runner's.
-    std::map<int, hipGraphExec_t> graph1, graphn;
-    hipStream_t cap = nullptr;
+    // decode-step graphs, captured once (the sampling config is device-resident):
+    // one step, and kGraphSteps steps back to back (fewer graph launches per token)
+    hipGraphExec_t graph = nullptr, graph_n = nullptr;
     mio::SampleCfg *d_cfg = nullptr;
     // generation state
     int n_prompt = 0, max_new = 0, steps_total = 0, steps_issued = 0;
@@ -71,9 +67,8 @@ struct mio_hip_llm {
 
     ~mio_hip_llm() {
         if (d) hipSetDevice(d->dev);
-        for (auto &g : graph1) hipGraphExecDestroy(g.second);
-        for (auto &g : graphn) hipGraphExecDestroy(g.second);
-        if (cap) hipStreamDestroy(cap);
+        if (graph) hipGraphExecDestroy(graph);
+        if (graph_n) hipGraphExecDestroy(graph_n);
         if (bt.graph) hipGraphExecDestroy(bt.graph);
         if (bt.graph_n) hipGraphExecDestroy(bt.graph_n);
         for (void *p : bt.allocs) hipFree(p);
@@ -139,8 +134,9 @@ float *upload_f32(mio_hip_llm *m, const mio::GgufTensor *t, int64_t n) {
 
 constexpr int kGraphSteps = 8;
 
-// One decode step at chunk count nch on stream s (tl: optional step timeline, diagnostic).
-int issue_step(mio_hip_llm *m, int nch, hipStream_t s, unsigned long long *tl = nullptr) {
+// One decode step on m->d->stream (tl: optional step timeline, diagnostic).
+int issue_step(mio_hip_llm *m, unsigned long long *tl = nullptr) {
+    hipStream_t s = m->d->stream;
     int seq = 0;
     auto bufs = [&]() {
         mio::LlmBuffers b = m->buf;
@@ -150,46 +146,30 @@ int issue_step(mio_hip_llm *m, int nch, hipStream_t s, unsigned long long *tl = 
     for (int il = 0; il < m->n_layer; ++il)
         for (int k = 0; k < 5; ++k)
             mio::launch_step_kernel(k, m->dims, m->layers.data(), il, m->kc, m->vc, m->out_norm, m->lm, m->tok, bufs(),
-                                    nch, s);
-    mio::launch_step_kernel(6, m->dims, m->layers.data(), 0, m->kc, m->vc, m->out_norm, m->lm, m->tok, bufs(), nch, s);
-    mio::launch_step_kernel(7, m->dims, m->layers.data(), 0, m->kc, m->vc, m->out_norm, m->lm, m->tok, bufs(), nch, s);
+                                    s);
+    mio::launch_step_kernel(6, m->dims, m->layers.data(), 0, m->kc, m->vc, m->out_norm, m->lm, m->tok, bufs(), s);
+    mio::launch_step_kernel(7, m->dims, m->layers.data(), 0, m->kc, m->vc, m->out_norm, m->lm, m->tok, bufs(), s);
     return MIO_OK;
 }
 
-// n steps at chunk count nch captured on the capture stream (tl: diagnostic timeline)
-int capture_steps(mio_hip_llm *m, int n, int nch, hipGraphExec_t *out, unsigned long long *tl = nullptr) {
-    if (!m->cap) MIO_HIP_CHECK(hipStreamCreateWithFlags(&m->cap, hipStreamNonBlocking));
+int capture_steps(mio_hip_llm *m, int n, hipGraphExec_t *out) {
+    hipStream_t s = m->d->stream;
     hipGraph_t g = nullptr;
-    MIO_HIP_CHECK(hipStreamBeginCapture(m->cap, hipStreamCaptureModeThreadLocal));
+    MIO_HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
     int rc = MIO_OK;
-    for (int i = 0; i < n && !rc; ++i) rc = issue_step(m, nch, m->cap, tl);
-    MIO_HIP_CHECK(hipStreamEndCapture(m->cap, &g));
+    for (int i = 0; i < n && !rc; ++i) rc = issue_step(m);
+    MIO_HIP_CHECK(hipStreamEndCapture(s, &g));
     if (rc) return rc;
     MIO_HIP_CHECK(hipGraphInstantiate(out, g, nullptr, nullptr, 0));
     hipGraphDestroy(g);
     return MIO_OK;
 }
 
-// the n-step graph of chunk count nch (captured on first use)
-int step_graph(mio_hip_llm *m, int n, int nch, hipGraphExec_t *out) {
-    auto &cache = n == 1 ? m->graph1 : m->graphn;
-    auto it = cache.find(nch);
-    if (it == cache.end()) {
-        hipGraphExec_t g = nullptr;
-        const int rc = capture_steps(m, n, nch, &g);
-        if (rc) return rc;
-        it = cache.emplace(nch, g).first;
-    }
-    *out = it->second;
-    return MIO_OK;
-}
-
-// decode position of the device state (host-side diagnostics)
-int state_pos(mio_hip_llm *m, int *pos) {
-    mio::StepState st{};
-    MIO_HIP_CHECK(hipMemcpyAsync(&st, m->buf.st, sizeof(st), hipMemcpyDeviceToHost, m->d->stream));
-    MIO_HIP_CHECK(hipStreamSynchronize(m->d->stream));
-    *pos = std::max(0, std::min(st.pos, m->dims.n_ctx - 1));
+int ensure_graph(mio_hip_llm *m) {
+    if (m->graph && m->graph_n) return MIO_OK;
+    int rc;
+    if (!m->graph && (rc = capture_steps(m, 1, &m->graph))) return rc;
+    if (!m->graph_n && (rc = capture_steps(m, kGraphSteps, &m->graph_n))) return rc;
     return MIO_OK;
 }
 
@@ -268,7 +248,7 @@ int llm_begin(mio_hip_llm *m, const int32_t *prompt, int n_prompt, int max_new, 
     c.eos0 = sp.eos0, c.eos1 = sp.eos1;
     c.force = m->d_force, c.n_force = m->max_steps;
     c.out_tokens = m->d_tokens, c.max_steps = m->max_steps;
-    if ((rc = put_cfg(m, c))) return rc;
+    if ((rc = put_cfg(m, c)) || (rc = ensure_graph(m))) return rc;
     m->n_prompt = n_prompt;
     m->max_new = max_new;
     m->steps_total = n_prompt - 1 + max_new;
@@ -293,22 +273,14 @@ int llm_run(mio_hip_llm *m, int n_steps) {
     // ROCm 7.2 here; kernels and arguments are identical either way)
     static const bool eager = getenv("MIO_NO_GRAPH") && getenv("MIO_NO_GRAPH")[0] == '1';
     int n = std::min(n_steps, m->steps_total - m->steps_issued);
-    // single stream: the step counter is the position (llm_begin sets both to P), so the
-    // host knows every step's position and picks the graph of its chunk count
-    while (n > 0) {
-        const int pos = m->steps_issued, nch = mio::att_chunks(pos);
-        const int run = (n >= kGraphSteps && mio::att_chunks(pos + kGraphSteps - 1) == nch) ? kGraphSteps : 1;
-        if (eager) {
-            if ((rc = issue_step(m, nch, m->d->stream))) return rc;
-            MIO_HIP_CHECK(hipGetLastError());
-            m->steps_issued += 1, n -= 1;
-            continue;
-        }
-        hipGraphExec_t g = nullptr;
-        if ((rc = step_graph(m, run, nch, &g))) return rc;
-        MIO_HIP_CHECK(hipGraphLaunch(g, m->d->stream));
-        m->steps_issued += run, n -= run;
+    m->steps_issued += n > 0 ? n : 0;
+    if (eager) {
+        for (int i = 0; i < n; ++i)
+            if ((rc = issue_step(m))) return rc;
+        return MIO_OK;
     }
+    for (; n >= kGraphSteps; n -= kGraphSteps) MIO_HIP_CHECK(hipGraphLaunch(m->graph_n, m->d->stream));
+    for (; n > 0; --n) MIO_HIP_CHECK(hipGraphLaunch(m->graph, m->d->stream));
     return MIO_OK;
 }
 
@@ -546,7 +518,6 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
     want(m->pf.part, (size_t)mio::kPrefillB * D.n_head * D.max_splits * (D.hd + 4));
     want(m->pf.act, mio::prefill_act_bytes(std::max(std::max(D.n_embd, D.n_ff), D.n_head * D.hd)));
     want(dr, (size_t)n_ctx * (D.hd / 2));
-    want(m->buf.rope_cur, (size_t)D.hd / 2);
     want(m->d_iota, (size_t)n_ctx + mio::kPrefillB);
     size_t io_bytes = 0;
     for (auto &c : carve) io_bytes += (c.second + 255) & ~(size_t)255;
@@ -572,7 +543,7 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
     }
     if (!m->kc || !m->vc || !m->buf.x || !m->buf.qkv || !m->buf.h || !m->buf.logits ||
         !m->buf.part || !m->buf.smp || !m->buf.st || !m->d_cfg || !m->d_tokens || !m->d_force || !dr ||
-        !m->d_prompt || !m->buf.rope_cur || !m->pf.x || !m->pf.qkv || !m->pf.h || !m->pf.part || !m->pf.act || !m->d_iota) {
+        !m->d_prompt || !m->pf.x || !m->pf.qkv || !m->pf.h || !m->pf.part || !m->pf.act || !m->d_iota) {
         mio::set_error("llm_load: device allocation failed");
         return fail(MIO_ERR_OOM);
     }
@@ -617,12 +588,11 @@ extern "C" int mio_hip_llm_eval(mio_hip_llm *m, int32_t token, int pos, float *l
     mio::SampleCfg c{};
     c.temp = 0.0f, c.lo = 0, c.hi = m->dims.n_vocab, c.eos0 = c.eos1 = -1;
     c.force = m->d_force, c.n_force = m->max_steps, c.out_tokens = m->d_tokens, c.max_steps = m->max_steps;
-    hipGraphExec_t g = nullptr;
-    if ((rc = put_cfg(m, c)) || (rc = step_graph(m, 1, mio::att_chunks(pos), &g))) return rc;
+    if ((rc = put_cfg(m, c)) || (rc = ensure_graph(m))) return rc;
     const int zero = 0;
     MIO_HIP_CHECK(hipMemcpyAsync(m->d_force, &zero, 4, hipMemcpyHostToDevice, m->d->stream));
     if ((rc = set_state(m, pos, token))) return rc;
-    MIO_HIP_CHECK(hipGraphLaunch(g, m->d->stream));
+    MIO_HIP_CHECK(hipGraphLaunch(m->graph, m->d->stream));
     if (logits)
         MIO_HIP_CHECK(hipMemcpyAsync(logits, m->buf.logits, (size_t)m->dims.n_vocab * 4, hipMemcpyDeviceToHost,
                                      m->d->stream));
@@ -920,7 +890,7 @@ extern "C" int mio_quantize_rows(uint32_t type, const float *x, int rows, int k,
 // attention: F16 K and V rows of positions 0..pos (the row at pos is written, the rest
 // read) + q|k|v in + partial records out, at the decode state's current pos).
 extern "C" int mio_hip_llm_time_kernel(mio_hip_llm *m, int which, int iters, float *avg_ms, uint64_t *bytes) {
-    MIO_REQUIRE(m && avg_ms && bytes && iters > 0 && !m->graph1.empty(), MIO_ERR_INVALID,
+    MIO_REQUIRE(m && avg_ms && bytes && iters > 0 && m->graph, MIO_ERR_INVALID,
                 "llm_time_kernel: run generate/eval first");
     MIO_REQUIRE(which >= 0 && which <= 6 && which != 5, MIO_ERR_INVALID, "llm_time_kernel: which %d", which);
     int rc = mio::bind(m->d);
@@ -932,11 +902,10 @@ extern "C" int mio_hip_llm_time_kernel(mio_hip_llm *m, int which, int iters, flo
     };
     const mio::LlmDims &D = m->dims;
     // attention reads the K/V rows of positions <= pos of the current decode state
-    int spos = 0;
-    if ((rc = state_pos(m, &spos))) return rc;
-    const int inch = mio::att_chunks(spos);
-    const uint64_t pos = (uint64_t)spos;
-    const uint64_t nch = (uint64_t)inch, qkv = (uint64_t)(D.n_head + 2 * D.n_kv) * D.hd;
+    mio::StepState st{};
+    MIO_HIP_CHECK(hipMemcpy(&st, m->buf.st, sizeof(st), hipMemcpyDeviceToHost));
+    const uint64_t pos = (uint64_t)std::max(0, std::min(st.pos, D.n_ctx - 1));
+    const uint64_t nch = pos / mio::kAttChunk + 1, qkv = (uint64_t)(D.n_head + 2 * D.n_kv) * D.hd;
     const uint64_t part = 4ull * D.n_head * nch * (D.hd + 2);  // chunk partial records {O, m, l}
     uint64_t b = 0;
     switch (which) {
@@ -953,11 +922,11 @@ extern "C" int mio_hip_llm_time_kernel(mio_hip_llm *m, int which, int iters, flo
     hipStream_t s = m->d->stream;
     // warm
     mio::launch_step_kernel(which, D, m->layers.data(), il, m->kc, m->vc, m->out_norm, m->lm, m->tok, m->buf,
-                            inch, s);
+                            s);
     MIO_HIP_CHECK(hipEventRecord(e0, s));
     for (int i = 0; i < iters; ++i)
         mio::launch_step_kernel(which, D, m->layers.data(), il, m->kc, m->vc, m->out_norm, m->lm, m->tok, m->buf,
-                                inch, s);
+                                s);
     MIO_HIP_CHECK(hipEventRecord(e1, s));
     MIO_HIP_CHECK(hipEventSynchronize(e1));
     float ms = 0;
@@ -972,20 +941,17 @@ extern "C" int mio_hip_llm_time_kernel(mio_hip_llm *m, int which, int iters, flo
 // s_memtime at checkpoints 0..15 of workgroup 0 / thread 0, s_memrealtime (100 MHz) at
 // checkpoints 0 and 15 in out[16] / out[31]. Diagnostic only.
 extern "C" int mio_hip_llm_trace_kernel(mio_hip_llm *m, int which, uint64_t *out) {
-    MIO_REQUIRE(m && out && !m->graph1.empty(), MIO_ERR_INVALID, "llm_trace_kernel: run generate/eval first");
+    MIO_REQUIRE(m && out && m->graph, MIO_ERR_INVALID, "llm_trace_kernel: run generate/eval first");
     MIO_REQUIRE(which >= 0 && which <= 7 && which != 5, MIO_ERR_INVALID, "llm_trace_kernel: which %d", which);
     int rc = mio::bind(m->d);
     if (rc) return rc;
-    int spos = 0;
-    if ((rc = state_pos(m, &spos))) return rc;
-    const int nch = mio::att_chunks(spos);
     const int il = m->n_layer / 2;
     hipStream_t s = m->d->stream;
     unsigned long long *dt = nullptr;
     MIO_HIP_CHECK(hipMalloc(&dt, 32 * sizeof(unsigned long long)));
     MIO_HIP_CHECK(hipMemsetAsync(dt, 0, 32 * sizeof(unsigned long long), s));
     mio::launch_step_kernel(which, m->dims, m->layers.data(), il, m->kc, m->vc, m->out_norm, m->lm, m->tok, m->buf,
-                            nch, s);
+                            s);
     // evict L2 / MALL so the traced launch streams its weights from HBM as in a real step
     void *flush = nullptr;
     const size_t flush_bytes = (size_t)1 << 30;
@@ -1001,7 +967,7 @@ extern "C" int mio_hip_llm_trace_kernel(mio_hip_llm *m, int which, uint64_t *out
     mio::LlmBuffers tb = m->buf;
     tb.trace = dt;
     mio::launch_step_kernel(which, m->dims, m->layers.data(), il, m->kc, m->vc, m->out_norm, m->lm, m->tok, tb,
-                            nch, s);
+                            s);
     MIO_HIP_CHECK(hipMemcpyAsync(out, dt, 32 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
     MIO_HIP_CHECK(hipStreamSynchronize(s));
     hipFree(dt);
@@ -1013,21 +979,21 @@ extern "C" int mio_hip_llm_trace_kernel(mio_hip_llm *m, int which, uint64_t *out
 // (advancing the decode state by 3 steps: reset/eval afterwards), and returns per launch
 // and workgroup {start, marks 1-6, end} in s_memrealtime ticks (100 MHz).
 extern "C" int mio_hip_llm_timeline(mio_hip_llm *m, uint64_t *out, int max_launches, int *n_launches) {
-    MIO_REQUIRE(m && out && n_launches && !m->graph1.empty(), MIO_ERR_INVALID,
-                "llm_timeline: run generate/eval first");
+    MIO_REQUIRE(m && out && n_launches && m->graph, MIO_ERR_INVALID, "llm_timeline: run generate/eval first");
     int rc = mio::bind(m->d);
     if (rc) return rc;
-    int spos = 0;
-    if ((rc = state_pos(m, &spos))) return rc;
     const int nl = m->n_layer * 5 + 2;
     MIO_REQUIRE(max_launches >= nl, MIO_ERR_INVALID, "llm_timeline: need %d launch slots", nl);
     hipStream_t s = m->d->stream;
     const size_t nslot = (size_t)nl * 256 * 8;
     unsigned long long *tl = nullptr;
     MIO_HIP_CHECK(hipMalloc(&tl, sizeof(unsigned long long) * nslot));
+    hipGraph_t g = nullptr;
     hipGraphExec_t ge = nullptr;
-    // the graph of the last replay's position (the replays advance the state by 3 steps)
-    if ((rc = capture_steps(m, 1, mio::att_chunks(std::min(spos + 2, m->dims.n_ctx - 1)), &ge, tl))) return rc;
+    MIO_HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+    rc = issue_step(m, tl);
+    MIO_HIP_CHECK(hipStreamEndCapture(s, &g));
+    MIO_HIP_CHECK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
     for (int rep = 0; rep < 3; ++rep) {
         MIO_HIP_CHECK(hipMemsetAsync(tl, 0, sizeof(unsigned long long) * nslot, s));
         MIO_HIP_CHECK(hipGraphLaunch(ge, s));
@@ -1037,6 +1003,7 @@ extern "C" int mio_hip_llm_timeline(mio_hip_llm *m, uint64_t *out, int max_launc
     MIO_HIP_CHECK(hipStreamSynchronize(s));
     std::memcpy(out, h.data(), sizeof(unsigned long long) * nslot);
     hipGraphExecDestroy(ge);
+    hipGraphDestroy(g);
     hipFree(tl);
     *n_launches = nl;
     return MIO_OK;
