@@ -1,6 +1,7 @@
-# One GPU-box pass: GPU tests, the default bench line (with the CPU baseline), then the
-# graph-mode bench under rocprofv3 kernel trace + stats. Outputs under gpurun_out/$TAG/.
-# usage: bash tools/gpu_round.sh TAG [skip-tests]
+# One GPU-box pass: GPU tests, the default bench line (with the CPU baseline), the eager
+# bench under rocprofv3 kernel trace + stats (graph replays crash rocprofiler-sdk 7.2's
+# queue intercept), and the two PMC passes at decode position ~400.
+# Outputs under gpurun_out/$TAG/.   usage: bash tools/gpu_round.sh TAG [skip-tests]
 set -e
 tag=${1:-run}
 out=gpurun_out/$tag
@@ -10,7 +11,11 @@ if [ "$2" != "skip-tests" ]; then
   timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $out/gpu_tests.log 2>&1
 fi
 timeout -k 10 400 python -u bench.py > $out/bench.json 2> $out/bench.err
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $out/prof -o run -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --batch 0 > $out/bench_prof.json 2> $out/prof.err
+MIO_NO_GRAPH=1 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $out/prof -o run -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --batch 0 > $out/bench_prof.json 2> $out/prof.err
 find $out/prof -name '*kernel_stats.csv' -exec cp {} $out/kernel_stats.csv \;
 rm -rf $out/prof  # the full trace exceeds gpurun's 64 MiB copy-back
+MIO_NO_GRAPH=1 timeout -k 10 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $out/pmc -o fetch -- python3 tools/pmc_run.py > $out/pmc_fetch.out 2>&1
+MIO_NO_GRAPH=1 timeout -k 10 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $out/pmc -o write -- python3 tools/pmc_run.py > $out/pmc_write.out 2>&1
+python3 tools/pmc_traffic.py $(find $out/pmc -name 'fetch_counter_collection.csv') $(find $out/pmc -name 'write_counter_collection.csv') 3 > $out/pmc_traffic.json
+find $out/pmc -name '*kernel_trace.csv' -delete
 echo done
