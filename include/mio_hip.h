@@ -185,6 +185,12 @@ int mio_hip_codec_last_timings(const mio_hip_codec *c, float *ms2);
 int mio_hip_debug_matvec(mio_hip_device *d, uint32_t type, const void *gguf_rows, int rows, int k,
                          const float *x, float *y);
 int mio_quantize_rows(uint32_t type, const float *x, int rows, int k, void *out);
+/* Parity helper: y[t][rows] = W x[t] for nt activation rows x[t][k] on the batched-prefill
+ * matmul (int8 MFMA, csrc/hip/llm_mmq.hip); each row equals mio_hip_debug_matvec of x[t].
+ * mode 0: y = W x; 1: y = W x + y (y in/out, the residual epilogue); 2: y = silu(W x) *
+ * (Wup x) with gguf_up the up matrix (the SwiGLU epilogue). */
+int mio_hip_debug_mmq(mio_hip_device *d, uint32_t type, const void *gguf_rows, int rows, int k,
+                      const float *x, int nt, int mode, const void *gguf_up, float *y);
 
 /* ---------------- host text / file utilities ----------------
  * normalize_tts_text (text-normalize.h:7), parse_speech_tokens (token-parser.h:8) and the

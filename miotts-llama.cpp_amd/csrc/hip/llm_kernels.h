@@ -71,10 +71,12 @@ struct LlmBuffers {
 // Batched prompt prefill (csrc/hip/llm_prefill.hip): up to kPrefillB prompt tokens per chunk
 // go through every layer with ONE weight pass per launch (the prefill llama_decode of
 // test-to-speech.cpp:132-148); K/V rows are written, no logits are produced.
-constexpr int kPrefillB = 16;
+constexpr int kPrefillB = 64;
+// The same multi-token layers run the batched decode step of up to kBatchMax utterances.
+constexpr int kBatchMax = 16;
 
-// The same multi-token engine runs the batched decode step of B independent utterances
-// (one token of each per step, weights streamed once for all of them).
+// The batched decode step of B independent utterances runs the same layers (one token of
+// each per step, weights streamed once for all of them).
 struct PrefillBuffers {
     float *x;            // [kPrefillB][n_embd] residual streams
     float *qkv;          // [kPrefillB][(H + 2 Hkv) hd]; q rows are RoPE'd in place
@@ -98,7 +100,7 @@ void launch_prefill_chunk(const LlmDims &d, const LayerW *layers, int n_layer, _
                           _Float16 *vcache, const QMat &tok_embd, const PrefillBuffers &pb, int p0, int nt,
                           int n_chunks, hipStream_t s);
 
-// Batched decode of B <= kPrefillB utterances (mio_hip_llm_generate_batch): per sequence b,
+// Batched decode of B <= kBatchMax utterances (mio_hip_llm_generate_batch): per sequence b,
 // state st[b], sampling cfg[b] (cfg[b].out_tokens = its token ring), logits [B][n_vocab],
 // sampler partials smp [B][lm blocks][2]; the residual streams are pb.x[b].
 struct BatchBuffers {
@@ -112,7 +114,7 @@ struct BatchBuffers {
 void launch_batch_step(const LlmDims &d, const LayerW *layers, int n_layer, _Float16 *kcache, _Float16 *vcache,
                        const float *out_norm, const QMat &lm, const QMat &tok_embd, const PrefillBuffers &pb,
                        const BatchBuffers &bb, int B, hipStream_t s);
-// B streams fit one batched step (B <= kPrefillB and the lm_head's LDS)
+// B streams fit one batched step (B <= kBatchMax and the lm_head's LDS)
 bool batch_supported(const LlmDims &d, int B);
 // Embedding of st[b].token into pb.x[b] for every sequence (decode start).
 void launch_batch_embed(const LlmDims &d, const QMat &tok_embd, const PrefillBuffers &pb, const BatchBuffers &bb,
@@ -140,5 +142,10 @@ int pick_np(int K);
 size_t matvec_lds(int K);
 // y = W x with x re-quantized to the vec_dot_type (parity test of the matvec kernels).
 void launch_debug_matvec(const QMat &W, const float *x, float *y, int n_wg, hipStream_t s);
+// y[t][rows] = W x[t] for nt tokens on the int8-MFMA multi-token matmul (act: scratch of
+// nt * debug_act_bytes(W.k) bytes); mode 0 store, 1 y += W x, 2 y = silu(W x) * (up x).
+size_t debug_act_bytes(int K);
+void launch_debug_mmq(const QMat &W, const QMat &up, int mode, const float *x, int nt, char *act, float *y,
+                      hipStream_t s);
 
 }  // namespace mio

@@ -1,0 +1,416 @@
+// Multi-token quantized matmul on the gfx950 int8 matrix cores (batched prompt prefill and
+// the batched decode of several utterances: the layers of llama_decode for a batch of tokens,
+// test-to-speech.cpp:132-148).
+//
+// y[t][row] = W[row] . a[t] for up to 32 tokens t per tile, W in the split quant layout
+// (csrc/host/quant.h: GGUF blocks regrouped per plane), a[t] the token's activation already
+// re-quantized to the weight's ggml vec_dot_type by k_bt_quant (Q8_K for K-quants, Q8_0 for
+// Q8_0) - the decode prologue's own arithmetic.
+//
+// One workgroup per (32-row tile, 32-token tile); its 8 waves split K by the decode engine's
+// lane slots (below). Every quantization group (Q4_K: 32-value
+// sub-block, Q6_K: 16-value sub-block, Q8_0: 32-value block) is one MFMA:
+//   v_mfma_i32_32x32x32_i8 (Q4_K, Q8_0) / v_mfma_i32_32x32x16_i8 (Q6_K),
+// A = the 32 tokens' int8 activations, B = the 32 rows' codes, C[token][row] = the group's
+// exact integer dot. The group scales are applied exactly as ggml's vec_dot does (integer
+// sums per superblock, then one float term per superblock / block), and the float terms are
+// summed in the decode engine's order (per-lane pass accumulation, then the balanced DPP
+// trees of row_total), so every (row, token) equals the single-token decode step's value BIT
+// FOR BIT (tests/test_llm_gpu.py::test_batched_prefill_matches_sequential).
+//   Q4_K: the min term sum_sb m_sb * sum(a in sb) is a second MFMA against m_sb broadcast
+//         (it accumulates over the superblock in the matrix core, no VALU)
+//   Q6_K: codes enter as q - 32 (signed 6-bit), so sum_j sc_j * (q - 32) . a needs no bsums
+// C/D layout (gfx950, dtype independent): lane l holds column (weight row) l & 31 and rows
+// (tokens) (r & 3) + 8 (r >> 2) + 4 (l >> 5), r = 0..15. A/B: lane l holds row/column
+// l & 31 and a contiguous half of K (the same half in A and B; exact-integer probe:
+// tools/micro/mfma_i8_probe.hip).
+#include "llm_device.h"
+#include "llm_mmq.h"
+
+#include <algorithm>
+#include <mutex>
+#include <utility>
+#include <vector>
+
+#pragma clang fp contract(off)
+
+namespace mio {
+namespace {
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v16i __attribute__((ext_vector_type(16)));
+typedef float v16f __attribute__((ext_vector_type(16)));
+
+constexpr int RT = 32;  // rows per tile (MFMA N)
+constexpr int TT = 32;  // tokens per tile (MFMA M)
+#ifndef MIO_MMQ_NT
+#define MIO_MMQ_NT 512
+#endif
+constexpr int MMQ_NT = MIO_MMQ_NT;  // 8 waves: one per decode lane slot (64: one wave, all slots)
+
+// token of accumulator register r of lane l
+__device__ __forceinline__ int tok_of(int lane, int r) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
+
+// Balanced pairwise sum over a stream of 2^L values pushed in order (the decode's DPP trees:
+// ((s7+s6)+(s5+s4))+((s3+s2)+(s1+s0)) for L = 3), 16 tokens per lane.
+template <int L>
+struct Tree {
+    v16f lv[L];
+    template <int I>
+    __device__ __forceinline__ void push(v16f x) {
+        // carry chain of the binary counter at index I (compile-time)
+        if constexpr (L >= 1 && (I & 1)) x = lv[0] + x;
+        if constexpr (L >= 2 && (I & 3) == 3) x = lv[1] + x;
+        if constexpr (L >= 3 && (I & 7) == 7) x = lv[2] + x;
+        if constexpr (L >= 4 && (I & 15) == 15) x = lv[3] + x;
+        if constexpr (L >= 5 && (I & 31) == 31) x = lv[4] + x;
+        if constexpr (L >= 6 && (I & 63) == 63) x = lv[5] + x;
+        constexpr int lvl = (I & 1) == 0 ? 0 : (I & 3) != 3 ? 1 : (I & 7) != 7 ? 2 : (I & 15) != 15 ? 3
+                          : (I & 31) != 31 ? 4 : (I & 63) != 63 ? 5 : 6;
+        if constexpr (lvl < L) lv[lvl] = x;
+        else result = x;
+    }
+    v16f result;
+};
+
+// 16 int8 activations of token row `t` (record base) at byte offset e.. e+15
+__device__ __forceinline__ v4i act16(const int8_t *qs, int e) { return *reinterpret_cast<const v4i *>(qs + e); }
+
+// ---------------------------------------------------------------- per-type slot products
+// The 8 waves of a workgroup split a 32x32 tile's K by the decode engine's lane slots: wave k
+// computes slot k's pass accumulation (superblocks s = p * 8 + k, p = 0, 1, ...; Q8_0: the
+// 8 slots of lane group k, already summed by their 8-leaf tree), and wave 0 then sums the 8
+// waves' results with the decode's tree (row_total). Each returns 16 values: this lane's row,
+// its 16 tokens.
+
+// Q4_K superblock s of row `row`: v = d * isum - dmin * imin per token (ggml vec_dot_q4_K_q8_K).
+__device__ __forceinline__ v16f sb_q4k(const uint8_t *qrow, const uint8_t *hrow, int s, const int8_t *aq,
+                                       const float *da_lds) {
+    const int lane = threadIdx.x & 63, h = lane >> 5;
+    const uint4 hd = *reinterpret_cast<const uint4 *>(hrow + (size_t)s * 16);
+    uint4 nb[4];
+    v4i al[4], ah[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        nb[c] = *reinterpret_cast<const uint4 *>(qrow + (size_t)s * 128 + 32 * c + 16 * h);
+        al[c] = act16(aq, s * 256 + 64 * c + 16 * h);
+        ah[c] = act16(aq, s * 256 + 64 * c + 32 + 16 * h);
+    }
+    v16i isum = {}, imin = {};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        // scale/min pair word of sub-blocks 2c, 2c+1 (24 bits at bit 24c of hd.yzw)
+        const uint32_t wlo = c < 2 ? hd.y : (c == 2 ? hd.z : hd.w);
+        const uint32_t whi = c < 2 ? hd.z : hd.w;
+        const uint32_t F = __builtin_amdgcn_alignbit(whi, wlo, (24 * c) & 31);
+        const int sc0 = F & 63, m0 = (F >> 6) & 63, sc1 = (F >> 12) & 63, m1 = (F >> 18) & 63;
+        const uint4 q = nb[c];
+        const v4i blo = {(int)(q.x & M4), (int)(q.y & M4), (int)(q.z & M4), (int)(q.w & M4)};
+        const v4i bhi = {(int)((q.x >> 4) & M4), (int)((q.y >> 4) & M4), (int)((q.z >> 4) & M4), (int)((q.w >> 4) & M4)};
+        const v16i clo = __builtin_amdgcn_mfma_i32_32x32x32_i8(al[c], blo, v16i{}, 0, 0, 0);
+        const v16i chi = __builtin_amdgcn_mfma_i32_32x32x32_i8(ah[c], bhi, v16i{}, 0, 0, 0);
+        const int mb0 = m0 * 0x01010101, mb1 = m1 * 0x01010101;
+        imin = __builtin_amdgcn_mfma_i32_32x32x32_i8(al[c], v4i{mb0, mb0, mb0, mb0}, imin, 0, 0, 0);
+        imin = __builtin_amdgcn_mfma_i32_32x32x32_i8(ah[c], v4i{mb1, mb1, mb1, mb1}, imin, 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) isum[r] += __mul24(sc0, clo[r]) + __mul24(sc1, chi[r]);
+    }
+    const float dw = h2f(hd.x & 0xFFFF), dmw = h2f(hd.x >> 16);
+    v16f v;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const float da = da_lds[s * TT + tok_of(lane, r)];
+        const float d = dw * da, dmin = dmw * da;
+        float x = d * (float)isum[r];
+        x = x - dmin * (float)imin[r];
+        v[r] = x;
+    }
+    return v;
+}
+
+// q - 32 for 4 packed 6-bit codes (signed int8): bit 5 set -> q & 31, clear -> q | 0xE0
+__device__ __forceinline__ int q6s(uint32_t q) {
+    const uint32_t t = q ^ 0x20202020u, m = t & 0x20202020u;
+    return (int)(t | (m << 1) | (m << 2));
+}
+
+// Q6_K superblock s: 16 sub-blocks of 16 values, one 32x32x16 MFMA each on (q - 32);
+// v = d * sum_j sc_j * C_j (ggml vec_dot_q6_K_q8_K).
+__device__ __forceinline__ v16f sb_q6k(const QMat &W, int row, int s, const int8_t *aq, const float *da_lds) {
+    const int lane = threadIdx.x & 63, h = lane >> 5;
+    const int nsb = W.k >> 8;
+    const uint8_t *qlrow = W.p0 + (size_t)row * (W.k / 2);
+    const uint8_t *qhrow = W.p1 + (size_t)row * (W.k / 4);
+    const int8_t *screw = (const int8_t *)W.p2 + (size_t)row * (W.k / 16);
+    const uint16_t *drow = (const uint16_t *)W.p3 + (size_t)row * nsb;
+    // split-layout scales: pair p2 = 4n + r -> {scales[8n + r], scales[8n + r + 4]}
+    const uint4 scr = *reinterpret_cast<const uint4 *>(screw + (size_t)s * 16);
+    int8_t sc[16];
+    __builtin_memcpy(sc, &scr, 16);
+    uint2 qh[2][2], ql[2][2][2];
+    long aa[16];
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            qh[n][b] = *reinterpret_cast<const uint2 *>(qhrow + (size_t)s * 64 + 32 * n + 16 * b + 8 * h);
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+                ql[n][a][b] = *reinterpret_cast<const uint2 *>(qlrow + (size_t)s * 128 + 64 * n + 32 * a + 16 * b + 8 * h);
+        }
+#pragma unroll
+    for (int j = 0; j < 16; ++j) aa[j] = *reinterpret_cast<const long *>(aq + s * 256 + 16 * j + 8 * h);
+    v16i isum = {};
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+                for (int hi = 0; hi < 2; ++hi) {
+                    // g = 2 hi + a: q1 (ql low, qh bits 0-1), q2 (ql[+32] low, bits 2-3), q3 (ql
+                    // high, bits 4-5), q4 (ql[+32] high, bits 6-7); value 128n + 32g + 16b + 8h + i
+                    const int g = 2 * hi + a;
+                    const int j = 8 * n + 2 * g + b;  // sub-block (values 16j ..)
+                    const uint2 l8 = ql[n][a][b], h8v = qh[n][b];
+                    const uint32_t lx = hi ? (l8.x >> 4) & M4 : l8.x & M4;
+                    const uint32_t ly = hi ? (l8.y >> 4) & M4 : l8.y & M4;
+                    const uint32_t hx = ((h8v.x >> (2 * g)) & M2) << 4, hy = ((h8v.y >> (2 * g)) & M2) << 4;
+                    const long bq = (long)(uint32_t)q6s(lx | hx) | ((long)(uint32_t)q6s(ly | hy) << 32);
+                    const v16i c = __builtin_amdgcn_mfma_i32_32x32x16_i8(aa[j], bq, v16i{}, 0, 0, 0);
+                    const int nn = j >> 3, rr = j & 7;
+                    const int scj = rr < 4 ? sc[2 * (4 * nn + rr)] : sc[2 * (4 * nn + rr - 4) + 1];
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) isum[r] += __mul24(scj, c[r]);
+                }
+    const float dw = h2f(drow[s]);
+    v16f v;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const float d = dw * da_lds[s * TT + tok_of(lane, r)];
+        v[r] = d * (float)isum[r];
+    }
+    return v;
+}
+
+// slot k's pass accumulation (K-quants)
+template <int T>
+__device__ v16f slot_kq(const QMat &W, int row, int k, const int8_t *aq, const float *da_lds) {
+    const int nsb = W.k >> 8, NP = (nsb + 7) / 8;
+    v16f acc = {};
+    for (int p = 0; p < NP; ++p) {
+        const int s = p * 8 + k;
+        v16f v = {};
+        if (s < nsb) {
+            if constexpr (T == 12)
+                v = sb_q4k(W.p0 + (size_t)row * (W.k / 2), W.p1 + (size_t)row * nsb * 16, s, aq, da_lds);
+            else
+                v = sb_q6k(W, row, s, aq, da_lds);
+        }
+        acc = acc + v;  // the decode lane's pass accumulation (0 + v0 + v1 ...)
+    }
+    return acc;
+}
+
+// Q8_0: lane group k = slots 8k .. 8k+7 (block b = p * 64 + slot), each slot's pass sum,
+// then sum8_f's tree over the group
+__device__ v16f slot_q80(const QMat &W, int row, int k, const int8_t *aq, const float *da_lds) {
+    const int lane = threadIdx.x & 63, h = lane >> 5;
+    const int nb = W.k >> 5, NP = (nb + 63) / 64;
+    const int8_t *qrow = (const int8_t *)W.p0 + (size_t)row * W.k;
+    const uint16_t *drow = (const uint16_t *)W.p1 + (size_t)row * nb;
+    Tree<3> inner;
+    auto slot = [&]<int i>() {
+        const int lam = 8 * k + i;
+        v16f acc = {};
+        for (int p = 0; p < NP; ++p) {
+            const int b = p * 64 + lam;
+            v16f v = {};
+            if (b < nb) {
+                const v4i w = *reinterpret_cast<const v4i *>(qrow + (size_t)b * 32 + 16 * h);
+                const v4i a = act16(aq, b * 32 + 16 * h);
+                const v16i c = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, w, v16i{}, 0, 0, 0);
+                const float dw = h2f(drow[b]);
+#pragma unroll
+                for (int r = 0; r < 16; ++r) v[r] = (float)c[r] * (dw * da_lds[b * TT + tok_of(lane, r)]);
+            }
+            acc = acc + v;
+        }
+        inner.template push<i>(acc);
+    };
+    slot.template operator()<0>();
+    slot.template operator()<1>();
+    slot.template operator()<2>();
+    slot.template operator()<3>();
+    slot.template operator()<4>();
+    slot.template operator()<5>();
+    slot.template operator()<6>();
+    slot.template operator()<7>();
+    return inner.result;
+}
+
+template <int T>
+__device__ __forceinline__ v16f slot_val(const QMat &W, int row, int k, const int8_t *aq, const float *da_lds) {
+    if constexpr (T == 8) return slot_q80(W, row, k, aq, da_lds);
+    else return slot_kq<T>(W, row, k, aq, da_lds);
+}
+
+// The activation scales of the tile's tokens into LDS as [group][token] (Q8_K: one per 256,
+// Q8_0: one per 32; the whole workgroup, then a barrier); returns this lane's token's codes.
+template <int T>
+__device__ __forceinline__ const int8_t *stage_act(const MmqArgs &a, int t0, int K, float *da_lds) {
+    const int ng = T == 8 ? K >> 5 : K >> 8;
+    const size_t ab = a.act_stride;
+    for (int e = threadIdx.x; e < ng * TT; e += MMQ_NT) {
+        const int g = e / TT, t = min(t0 + e % TT, a.nt - 1);
+        da_lds[e] = reinterpret_cast<const float *>(a.act + (size_t)t * ab + K)[g];
+    }
+    __syncthreads();
+    const int t = min(t0 + (threadIdx.x & 31), a.nt - 1);
+    return reinterpret_cast<const int8_t *>(a.act + (size_t)t * ab);
+}
+
+// sum of the 8 waves' slot values with the decode's row_total tree (valid in wave 0): each
+// wave stores its slot value(s) (NV sets: gate and up of SwiGLU share one barrier), then wave
+// 0 reads the 8 slots of every set in slot order
+__device__ __forceinline__ void slot_store(const v16f &mine, float *red) {
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    float *dst = red + ((size_t)wave * 64 + lane) * 16;
+#pragma unroll
+    for (int r = 0; r < 16; r += 4) *reinterpret_cast<float4 *>(dst + r) = make_float4(mine[r], mine[r + 1], mine[r + 2], mine[r + 3]);
+}
+__device__ __forceinline__ v16f slot_sum(const float *red) {
+    const int lane = threadIdx.x & 63;
+    Tree<3> t;
+    auto leaf = [&]<int k>() {
+        const float *src = red + ((size_t)k * 64 + lane) * 16;
+        v16f x;
+#pragma unroll
+        for (int r = 0; r < 16; r += 4) {
+            const float4 f = *reinterpret_cast<const float4 *>(src + r);
+            x[r] = f.x, x[r + 1] = f.y, x[r + 2] = f.z, x[r + 3] = f.w;
+        }
+        t.template push<k>(x);
+    };
+    leaf.template operator()<0>();
+    leaf.template operator()<1>();
+    leaf.template operator()<2>();
+    leaf.template operator()<3>();
+    leaf.template operator()<4>();
+    leaf.template operator()<5>();
+    leaf.template operator()<6>();
+    leaf.template operator()<7>();
+    return t.result;
+}
+
+// the tile's 16 row totals per lane of W (and of U when NV = 2), valid in wave 0
+template <int T, int NV>
+__device__ __forceinline__ void all_slots(const QMat &W, const QMat &U, int row, const int8_t *aq, const float *da,
+                                          float *red, v16f &y, v16f &u) {
+    // the slot index must be wave-uniform in the compiler's eyes: a VGPR-held slot makes
+    // every superblock branch divergent, and the matrix-core ops inside it then ran with
+    // a partial EXEC (wrong sums; tests/test_llm_gpu.py::test_mmq_equals_single_token_matvec)
+    const int k = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    slot_store(slot_val<T>(W, row, k, aq, da), red);
+    if constexpr (NV == 2) slot_store(slot_val<T>(U, row, k, aq, da), red + MMQ_NT * 16);
+    __syncthreads();
+    if (k == 0) {
+        y = slot_sum(red);
+        if constexpr (NV == 2) u = slot_sum(red + MMQ_NT * 16);
+    }
+}
+
+template <int T0, int T1, int T2, int MODE>
+__global__ __launch_bounds__(MMQ_NT) void k_mmq(MmqSeg s0, MmqSeg s1, MmqSeg s2, MmqArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    float *red = reinterpret_cast<float *>(lds);                          // [8 waves][64][16] (x2 SWIGLU)
+    float *da = red + (MODE == MMQ_SWIGLU ? 2 : 1) * MMQ_NT * 16;         // [groups][32 tokens]
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int t0 = blockIdx.y * TT;
+    int tile_id = blockIdx.x;
+    // segment of this tile (uniform branch): q | k | v of the attention input, or one matrix
+    auto run = [&]<int T>(const MmqSeg &sg, int ti) {
+        const int row0 = ti * RT, row = min(row0 + (lane & 31), sg.w.rows - 1);
+        const int8_t *aq = stage_act<T>(a, t0, a.K, da);
+        v16f y = {}, u = {};
+        all_slots<T, MODE == MMQ_SWIGLU ? 2 : 1>(sg.w, a.w_up, row, aq, da, red, y, u);
+        const int orow = row0 + (lane & 31);
+        if (wave != 0 || orow >= sg.w.rows) return;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int t = t0 + tok_of(lane, r);
+            if (t >= a.nt) continue;
+            float *o = a.out + (size_t)t * a.ld + sg.out_off + orow;
+            if constexpr (MODE == MMQ_STORE) *o = y[r];
+            else if constexpr (MODE == MMQ_RESID) *o = y[r] + *o;
+            else *o = silu_f(y[r]) * u[r];
+        }
+    };
+    if (tile_id < s0.tiles) return run.template operator()<T0>(s0, tile_id);
+    tile_id -= s0.tiles;
+    if constexpr (T1 >= 0) {
+        if (tile_id < s1.tiles) return run.template operator()<T1>(s1, tile_id);
+        tile_id -= s1.tiles;
+    }
+    if constexpr (T2 >= 0) {
+        if (tile_id < s2.tiles) return run.template operator()<T2>(s2, tile_id);
+    }
+}
+
+}  // namespace
+
+size_t mmq_lds(int type, int K, int mode) {
+    return (size_t)(mode == MMQ_SWIGLU ? 2 : 1) * MMQ_NT * 16 * sizeof(float) +
+           (size_t)(type == 8 ? K / 32 : K / 256) * TT * sizeof(float);
+}
+
+// dynamic LDS above 64 KB (Q8_0 activation scales of a long K) needs the per-kernel opt-in,
+// once per (device, kernel)
+static void allow_lds_mmq(const void *kern) {
+    static std::mutex mu;
+    static std::vector<std::pair<int, const void *>> done;
+    int dev = 0;
+    hipGetDevice(&dev);
+    std::lock_guard<std::mutex> lk(mu);
+    for (const auto &q : done)
+        if (q.first == dev && q.second == kern) return;
+    hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 1024);
+    done.push_back({dev, kern});
+}
+
+int mmq_tiles(int rows) { return (rows + RT - 1) / RT; }
+
+// types: {T0, T1, T2} (-1 = segment unused); mode MMQ_*.
+void launch_mmq(const MmqSeg *seg, const int *types, int nseg, int mode, const MmqArgs &a, hipStream_t s) {
+    MmqSeg sg[3] = {seg[0], nseg > 1 ? seg[1] : MmqSeg{}, nseg > 2 ? seg[2] : MmqSeg{}};
+    int tiles = 0;
+    for (int i = 0; i < nseg; ++i) tiles += sg[i].tiles;
+    const dim3 grid(tiles, (a.nt + TT - 1) / TT);
+    size_t lds = 0;
+    for (int i = 0; i < nseg; ++i) lds = std::max(lds, mmq_lds(types[i], a.K, mode));
+    auto go = [&]<int A, int B, int C>() {
+        auto launch = [&](auto kern) {
+            if (lds > 64 * 1024) allow_lds_mmq(reinterpret_cast<const void *>(kern));
+            hipLaunchKernelGGL(kern, grid, dim3(MMQ_NT), lds, s, sg[0], sg[1], sg[2], a);
+        };
+        if (mode == MMQ_STORE)
+            launch(k_mmq<A, B, C, MMQ_STORE>);
+        else if (mode == MMQ_RESID)
+            launch(k_mmq<A, B, C, MMQ_RESID>);
+        else
+            launch(k_mmq<A, B, C, MMQ_SWIGLU>);
+    };
+    auto one = [&]<int A>() {
+        if (nseg == 1) return go.template operator()<A, -1, -1>();
+        // attention input: q, k share a type; v is Q4_K / Q6_K (Q4_K_M) or Q8_0
+        if (types[2] == 14) return go.template operator()<A, A, 14>();
+        if (types[2] == 12) return go.template operator()<A, A, 12>();
+        return go.template operator()<A, A, 8>();
+    };
+    if (types[0] == 12) one.template operator()<12>();
+    else if (types[0] == 14) one.template operator()<14>();
+    else one.template operator()<8>();
+}
+
+}  // namespace mio

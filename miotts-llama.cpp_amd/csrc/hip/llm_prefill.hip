@@ -18,6 +18,7 @@
 // order): the K/V cache and the last token's logits equal a token-by-token decode bit for
 // bit (tests/test_llm_gpu.py::test_batched_prefill_matches_sequential).
 #include "llm_device.h"
+#include "llm_mmq.h"
 
 #include <mutex>
 #include <utility>
@@ -589,11 +590,20 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
         const int per = tokens_per_launch(K, nt, rpw);
         for (int t = 0; t < nt; t += per) f(t, nt - t < per ? nt - t : per, shifted(d, pb, t, K));
     };
+    // matvecs on the int8 matrix cores (llm_mmq.hip); MIO_MMQ=0 selects the dot4 streaming
+    // engine below (A/B only: both are bit-exact with the decode step)
+    static const bool mmq = !(getenv("MIO_MMQ") && getenv("MIO_MMQ")[0] == '0');
+    const int QD = (d.n_head + 2 * d.n_kv) * d.hd;
     for (int il = 0; il < n_layer; ++il) {
         const LayerW &L = layers[il];
         _Float16 *kc = kcache + il * layer_kv, *vc = vcache + il * layer_kv;
         launch_quant(d, 0, pb.x, d.n_embd, L.attn_norm, L.wq.type != 8, pb, nt, s);
-        {
+        if (mmq) {
+            const MmqSeg sg[3] = {{L.wq, mmq_tiles(L.wq.rows), 0}, {L.wk, mmq_tiles(L.wk.rows), L.wq.rows},
+                                  {L.wv, mmq_tiles(L.wv.rows), L.wq.rows + L.wk.rows}};
+            const int ty[3] = {L.wq.type, L.wk.type, L.wv.type};
+            launch_mmq(sg, ty, 3, MMQ_STORE, MmqArgs{pb.act, act_bytes(d.n_embd), d.n_embd, nt, pb.qkv, QD, {}}, s);
+        } else {
             int GW, g_qk;
             attn_in_grid(d, L, GW, g_qk);
             over_tokens(d.n_embd, 0, [&](int, int n, const PrefillBuffers &q) {
@@ -630,7 +640,11 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
                 launch_pf_attention<64>(G, grid, s, d, kc, vc, pb);
         }
         launch_quant(d, 2, nullptr, L.wo.k, nullptr, L.wo.type != 8, pb, nt, s);
-        {
+        if (mmq) {
+            const MmqSeg sg{L.wo, mmq_tiles(L.wo.rows), 0};
+            launch_mmq(&sg, &L.wo.type, 1, MMQ_RESID, MmqArgs{pb.act, act_bytes(L.wo.k), L.wo.k, nt, pb.x, d.n_embd, {}},
+                       s);
+        } else {
             const int grid = matvec_grid(d, L.wo.rows), rpw = rows_per_wave(L.wo.rows, grid);
             over_tokens(L.wo.k, rpw, [&](int, int n, const PrefillBuffers &q) {
                 dispatch_nt(L.wo.k, L.wo.type, [&]<int NP, int T>() {
@@ -641,7 +655,11 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
             });
         }
         launch_quant(d, 0, pb.x, d.n_embd, L.ffn_norm, L.gate.type != 8, pb, nt, s);
-        {
+        if (mmq) {
+            const MmqSeg sg{L.gate, mmq_tiles(L.gate.rows), 0};
+            launch_mmq(&sg, &L.gate.type, 1, MMQ_SWIGLU,
+                       MmqArgs{pb.act, act_bytes(d.n_embd), d.n_embd, nt, pb.h, d.n_ff, L.up}, s);
+        } else {
             const int grid = matvec_grid(d, L.gate.rows);
             over_tokens(d.n_embd, 0, [&](int, int n, const PrefillBuffers &q) {
                 dispatch_nt(d.n_embd, L.gate.type, [&]<int NP, int T>() {
@@ -652,7 +670,11 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
             });
         }
         launch_quant(d, 1, pb.h, L.down.k, nullptr, L.down.type != 8, pb, nt, s);
-        {
+        if (mmq) {
+            const MmqSeg sg{L.down, mmq_tiles(L.down.rows), 0};
+            launch_mmq(&sg, &L.down.type, 1, MMQ_RESID,
+                       MmqArgs{pb.act, act_bytes(L.down.k), L.down.k, nt, pb.x, d.n_embd, {}}, s);
+        } else {
             const int grid = matvec_grid(d, L.down.rows), rpw = rows_per_wave(L.down.rows, grid);
             over_tokens(L.down.k, rpw, [&](int, int n, const PrefillBuffers &q) {
                 dispatch_nt(L.down.k, L.down.type, [&]<int NP, int T>() {
@@ -677,10 +699,23 @@ void launch_prefill_chunk(const LlmDims &d, const LayerW *layers, int n_layer, _
 
 size_t prefill_act_bytes(int k_max) { return act_bytes(k_max) * kPrefillB; }
 
+// parity entry (mio_hip_debug_mmq): nt activation rows x[t][K] quantized as the decode does
+// (plain_quant), then y[t][rows] = W x[t] on the int8-MFMA matmul
+size_t debug_act_bytes(int K) { return act_bytes(K); }
+void launch_debug_mmq(const QMat &W, const QMat &up, int mode, const float *x, int nt, char *act, float *y,
+                      hipStream_t s) {
+    LlmDims d{};
+    PrefillBuffers pb{};
+    pb.act = act;
+    launch_quant(d, 1, x, W.k, nullptr, W.type != 8, pb, nt, s);
+    const MmqSeg sg{W, mmq_tiles(W.rows), 0};
+    launch_mmq(&sg, &W.type, 1, mode, MmqArgs{act, act_bytes(W.k), W.k, nt, y, W.rows, up}, s);
+}
+
 size_t batch_lm_head_lds(const LlmDims &d, int B) { return pf_lds_bytes(d.n_embd, B, 0) + (size_t)MW * B * 128 * 4; }
 
 bool batch_supported(const LlmDims &d, int B) {
-    return B >= 1 && B <= kPrefillB && batch_lm_head_lds(d, B) <= (size_t)LDS_DYN_MAX;
+    return B >= 1 && B <= kBatchMax && batch_lm_head_lds(d, B) <= (size_t)LDS_DYN_MAX;
 }
 
 void launch_batch_step(const LlmDims &d, const LayerW *layers, int n_layer, _Float16 *kcache, _Float16 *vcache,

@@ -99,6 +99,7 @@ def _declare(L: ctypes.CDLL) -> None:
         "mio_hip_codec_last_timings": (c_int, [_vp, _f32p]),
         "mio_hip_debug_matvec": (c_int, [_vp, ctypes.c_uint32, _vp, c_int, c_int, _vp, _vp]),
         "mio_quantize_rows": (c_int, [ctypes.c_uint32, _vp, c_int, c_int, _vp]),
+        "mio_hip_debug_mmq": (c_int, [_vp, ctypes.c_uint32, _vp, c_int, c_int, _vp, c_int, c_int, _vp, _vp]),
         "mio_hip_llm_info": (c_int, [_vp, _i32p]),
         "mio_hip_llm_weight_bytes": (c_int, [_vp, ctypes.POINTER(ctypes.c_uint64)]),
         "mio_hip_llm_eval": (c_int, [_vp, ctypes.c_int32, c_int, _vp]),
@@ -485,6 +486,19 @@ def debug_matvec(dev: Device, qtype: int, w_rows: np.ndarray, k: int, x: np.ndar
     x = np.ascontiguousarray(x, dtype=np.float32)
     y = np.empty(w_rows.shape[0], np.float32)
     check(lib().mio_hip_debug_matvec(dev.h, qtype, _ptr(w_rows), w_rows.shape[0], k, _ptr(x), _ptr(y)))
+    return y
+
+
+def debug_mmq(dev: Device, qtype: int, w_rows: np.ndarray, k: int, x: np.ndarray, mode: int = 0,
+              y_in: Optional[np.ndarray] = None, up_rows: Optional[np.ndarray] = None) -> np.ndarray:
+    """x: [nt][k] -> y [nt][rows] on the int8-MFMA batched matmul (mio_hip_debug_mmq); mode 1
+    adds y_in, mode 2 returns silu(W x) * (up x)."""
+    w_rows = np.ascontiguousarray(w_rows)
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    y = np.zeros((x.shape[0], w_rows.shape[0]), np.float32) if y_in is None else np.array(y_in, np.float32)
+    up = np.ascontiguousarray(up_rows) if up_rows is not None else None
+    check(lib().mio_hip_debug_mmq(dev.h, qtype, _ptr(w_rows), w_rows.shape[0], k, _ptr(x), x.shape[0], mode,
+                                  _ptr(up) if up is not None else None, _ptr(y)))
     return y
 
 
