@@ -30,18 +30,16 @@ struct GemmArgs {
     const float *aux;   // gate (EPI_GATED), exp(alpha) (snake)
     const float *aux2;  // exp(beta) (snake)
     int f, trim, cout, rows_out;  // CONVT remap; HEAD: cout = n_freq
+    int m_major;      // tile order (set by launch_gemm_f32)
 };
 
-// Conv1d k=taps, stride 1, "same" zero padding, as an implicit GEMM on f16 MFMA with
-// GroupNorm-affine + SiLU fused into the A-operand load (ggml conv_1d rounds both the
-// kernel and the im2col input to f16; miocodec.cpp:382-386).
+// Conv1d k=taps, stride 1, "same" zero padding, as an implicit GEMM on f16 MFMA over the
+// f16 activation written by launch_groupnorm_apply (ggml conv_1d rounds both the kernel and
+// the im2col input to f16; miocodec.cpp:382-386). Cin % 8 == 0.
 struct ConvArgs {
-    const float *X;        // [L][Cin] input (pre-GroupNorm)
+    const _Float16 *Xa;    // [L][Cin] silu(GroupNorm(x)) rounded to f16
     int L, Cin;
     int taps, pad;
-    const float *gn_mean_rstd;  // [G][2]
-    int G, cpg;
-    const float *gamma, *beta;  // GroupNorm affine [Cin]
     const _Float16 *B;     // [Cout][taps*Cin] f16 kernel, k-index = tap*Cin + ci
     int Cout;
     const float *bias;     // [Cout]
@@ -56,9 +54,15 @@ void launch_conv_f16(const ConvArgs &a, hipStream_t s);
 // 2: AdaLN (shift = p0, scale = p1: y*(1+scale)+shift). In-place (y == x) allowed.
 void launch_rownorm(const float *x, float *y, int M, int D, float eps, int mode, const float *p0,
                     const float *p1, hipStream_t s);
-// GroupNorm statistics over [L][C] in groups of cpg channels -> [G][2] (mean, 1/sqrt(var+eps)).
-void launch_groupnorm_stats(const float *x, int L, int C, int G, int cpg, float eps,
-                            float *mean_rstd, hipStream_t s);
+// xa = f16(silu(GroupNorm(x) * gamma + beta)) over [L][C], G groups of C/G channels
+// (C % 8 == 0, C <= 1024, G <= 64, 64 % (C/G) == 0). Five launches on stream s.
+struct GnScratch {
+    double *part;        // kGnPartDoubles: [P <= 256][G] slice sums
+    float2 *stat;        // [64] (mean, rstd)
+};
+constexpr int kGnPartDoubles = 256 * 64;
+void launch_groupnorm_apply(const float *x, int L, int C, int G, float eps, const float *gamma,
+                            const float *beta, GnScratch gs, _Float16 *xa, hipStream_t s);
 // Banded (|i-j| <= window/2) RoPE attention, head_dim 64, q|k|v packed per row (ld = 3*D).
 void launch_band_attention(const float *qkv, float *out, int S, int H, int window,
                            const float2 *rope /*[S][32] (cos,sin)*/, hipStream_t s);

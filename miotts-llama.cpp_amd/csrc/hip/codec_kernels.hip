@@ -1,23 +1,26 @@
 // MioCodec decoder kernels for gfx950 (CDNA4), f32 numerics matching the reference's
 // ggml CPU graph (miocodec.cpp:204-420, 599-737) up to summation order.
 //
-//  * gemm_f32_kernel   : C = A * B^T on v_mfma_f32_32x32x2_f32 (exact f32 fma chain),
-//                        LDS double-buffered 16-deep K tiles, 2x2 waves, fused epilogues
+//  * gemm_f32_kernel   : C = A * B^T on v_mfma_f32_32x32x2_f32 (exact f32 fma chains, one
+//                        per K-group, added once), 64 x 64 tiles, LDS double-buffered with
+//                        loads two stages ahead, fused epilogues
 //                        (bias / residual / AdaLN gate / SwiGLU / ConvT remap + Snake /
 //                        Snake / iSTFT-head polar->complex). The A operand may be a
 //                        sliding tap window over consecutive rows (implicit im2col for
 //                        ConvTranspose with kernel > stride).
-//  * conv_f16_kernel   : Conv1d as implicit GEMM on v_mfma_f32_32x32x16_f16 with the
-//                        GroupNorm affine + SiLU applied while staging A, then rounded to
-//                        f16 — exactly ggml's conv_1d (f16 kernel, f16 im2col, f32 sums).
+//  * conv_f16_kernel   : Conv1d as implicit GEMM on v_mfma_f32_32x32x16_f16 over the f16
+//                        GroupNorm+SiLU activation — exactly ggml's conv_1d (f16 kernel,
+//                        f16 im2col, f32 sums).
 //  * rownorm_kernel    : ggml_norm (+affine / AdaLN modulate), one wave per row.
-//  * groupnorm_stats   : ggml_group_norm statistics (double accumulation).
+//  * gn_partial/apply  : ggml_group_norm statistics (double accumulation) over 64 row
+//                        slices, then affine + SiLU -> f16 conv operand.
 //  * band_attention    : softmax(QK^T/8 + local mask) V restricted to the |i-j|<=w/2
 //                        band (masked entries are exp(-inf)=0 in the reference, so this
 //                        is the same function without the S x S work), RoPE applied on load.
 #include "codec_kernels.h"
 
 #include <cmath>
+#include <cstdlib>
 
 #pragma clang fp contract(off)
 
@@ -37,17 +40,37 @@ __device__ __forceinline__ float snake_f(float v, float a, float b) {
 }
 
 // ---------------------------------------------------------------- f32 GEMM
-template <int BM, int BN, int EPI>
-__global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs g) {
-    constexpr int BK = 16, LDK = BK + 1;
-    constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 32, TN = WN / 32;
-    constexpr int AV = BM * BK / 4 / 256, BV = BN * BK / 4 / 256;
-    __shared__ float As[2][BM * LDK];
-    __shared__ float Bs[2][BN * LDK];
+// 64 x 64 output tile per block, 2 x 2 waves of 32 x 32, times KG K-groups (256*KG threads).
+// A stage is BK = 32*KG deep; K-group kg owns k in [32kg, 32kg + 32) of every stage, so each
+// wave runs one exact f32 fma chain (16 v_mfma_f32_32x32x2_f32 per stage) and the KG chains
+// are added once, in K-group order, in the epilogue. KG grows as the tile count shrinks so
+// that small GEMMs still put 16 waves on every CU. Operands go global -> VGPR -> LDS (float4)
+// two stages ahead of the MFMAs; the MFMA reads ds_read_b128 = 4 consecutive k of one row,
+// so an octet of k feeds four MFMAs whose lane-half h supplies k = 8o + 4h + q in A and B.
+constexpr int GF_T = 64, GF_KD = 32;
 
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int wm = wave >> 1, wn = wave & 1;
-    const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+template <int KG, int EPI>
+__global__ __launch_bounds__(256 * KG) void gemm_f32_kernel(GemmArgs g) {
+    constexpr int BM = GF_T, BN = GF_T, BK = GF_KD * KG, LDK = BK + 4, NT = 256 * KG;
+    constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 32, TN = WN / 32;
+    constexpr int AV = BM * BK / 4 / NT, BV = BN * BK / 4 / NT;
+    static_assert(AV >= 1 && BV >= 1, "tile");
+    static_assert(2 * (BM + BN) * LDK >= (KG - 1) * BM * BN, "reduction area");
+    __shared__ __attribute__((aligned(16))) float smem[2 * (BM + BN) * LDK];
+    float *const As = smem, *const Bs = smem + 2 * BM * LDK;
+
+    // XCD-aware tile order: block b runs on XCD b % 8 (round-robin dispatch), so block b takes
+    // logical tile (b % 8) * per + b / 8 and each XCD owns one contiguous run of tiles. Tiles
+    // are numbered along M first (g.m_major == 0: each XCD gets a slab of N columns, all of A
+    // plus 1/8 of B in its L2) or along N first (m_major: a slab of rows, for tall A).
+    const int nM = (g.M + BM - 1) / BM, nN = (g.N + BN - 1) / BN, nb = nM * nN, per = (nb + 7) / 8;
+    const int t = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
+    if (t >= nb) return;
+    const int mt = g.m_major ? t / nN : t % nM, nt = g.m_major ? t % nN : t / nM;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int kg = wave >> 2, wm = (wave >> 1) & 1, wn = wave & 1;
+    const int m0 = mt * BM, n0 = nt * BN;
 
     f32x16 acc[TM][TN];
 #pragma unroll
@@ -57,11 +80,11 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs g) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
 
-    float4 ra[AV], rb[BV];
-    auto load = [&](int k0) {
+    float4 ra0[AV], rb0[BV], ra1[AV], rb1[BV];
+    auto load = [&](int k0, float4 (&ra)[AV], float4 (&rb)[BV]) {
 #pragma unroll
         for (int i = 0; i < AV; ++i) {
-            const int e = tid + i * 256, r = e >> 2, c4 = e & 3;
+            const int e = tid + i * NT, r = e / (BK / 4), c4 = e % (BK / 4);
             const int m = m0 + r, k = k0 + c4 * 4;
             float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
             if (m < g.M && k < g.K) {
@@ -73,51 +96,94 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs g) {
         }
 #pragma unroll
         for (int i = 0; i < BV; ++i) {
-            const int e = tid + i * 256, r = e >> 2, c4 = e & 3;
+            const int e = tid + i * NT, r = e / (BK / 4), c4 = e % (BK / 4);
             const int n = n0 + r, k = k0 + c4 * 4;
             float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
             if (n < g.N && k < g.K) v = *reinterpret_cast<const float4 *>(g.B + (long)n * g.K + k);
             rb[i] = v;
         }
     };
-    auto store = [&](int buf) {
+    auto store = [&](int buf, const float4 (&ra)[AV], const float4 (&rb)[BV]) {
 #pragma unroll
         for (int i = 0; i < AV; ++i) {
-            const int e = tid + i * 256, r = e >> 2, c = (e & 3) * 4;
-            float *d = &As[buf][r * LDK + c];
-            d[0] = ra[i].x, d[1] = ra[i].y, d[2] = ra[i].z, d[3] = ra[i].w;
+            const int e = tid + i * NT, r = e / (BK / 4), c4 = e % (BK / 4);
+            *reinterpret_cast<float4 *>(&As[buf * BM * LDK + r * LDK + c4 * 4]) = ra[i];
         }
 #pragma unroll
         for (int i = 0; i < BV; ++i) {
-            const int e = tid + i * 256, r = e >> 2, c = (e & 3) * 4;
-            float *d = &Bs[buf][r * LDK + c];
-            d[0] = rb[i].x, d[1] = rb[i].y, d[2] = rb[i].z, d[3] = rb[i].w;
+            const int e = tid + i * NT, r = e / (BK / 4), c4 = e % (BK / 4);
+            *reinterpret_cast<float4 *>(&Bs[buf * BN * LDK + r * LDK + c4 * 4]) = rb[i];
+        }
+    };
+    auto compute = [&](int buf) {
+        const float *Ab = As + buf * BM * LDK, *Bb = Bs + buf * BN * LDK;
+#pragma unroll
+        for (int o = 0; o < GF_KD / 8; ++o) {
+            const int kc = kg * GF_KD + o * 8 + 4 * (lane >> 5);
+            float4 a[TM], b[TN];
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+                a[i] = *reinterpret_cast<const float4 *>(&Ab[(wm * WM + i * 32 + (lane & 31)) * LDK + kc]);
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+                b[j] = *reinterpret_cast<const float4 *>(&Bb[(wn * WN + j * 32 + (lane & 31)) * LDK + kc]);
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].x, b[j].x, acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].y, b[j].y, acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].z, b[j].z, acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].w, b[j].w, acc[i][j], 0, 0, 0);
+                }
         }
     };
 
     const int nk = (g.K + BK - 1) / BK;
-    load(0);
-    store(0);
+    load(0, ra0, rb0);
+    if (nk > 1) load(BK, ra1, rb1);
+    store(0, ra0, rb0);
     __syncthreads();
-    for (int kt = 0; kt < nk; ++kt) {
-        const int buf = kt & 1;
-        if (kt + 1 < nk) load((kt + 1) * BK);
-#pragma unroll
-        for (int kk = 0; kk < BK; kk += 2) {
-            const int k = kk + (lane >> 5);
-            float a[TM], b[TN];
-#pragma unroll
-            for (int i = 0; i < TM; ++i) a[i] = As[buf][(wm * WM + i * 32 + (lane & 31)) * LDK + k];
-#pragma unroll
-            for (int j = 0; j < TN; ++j) b[j] = Bs[buf][(wn * WN + j * 32 + (lane & 31)) * LDK + k];
+    for (int kt = 0; kt < nk; kt += 2) {
+        // even stage: LDS buffer 0; registers 1 hold stage kt+1, registers 0 refill with kt+2
+        if (kt + 2 < nk) load((kt + 2) * BK, ra0, rb0);
+        compute(0);
+        if (kt + 1 < nk) store(1, ra1, rb1);
+        __syncthreads();
+        if (kt + 1 >= nk) break;
+        // odd stage: LDS buffer 1
+        if (kt + 3 < nk) load((kt + 3) * BK, ra1, rb1);
+        compute(1);
+        if (kt + 2 < nk) store(0, ra0, rb0);
+        __syncthreads();
+    }
+
+    // ---- K-groups 1.. hand their chains to K-group 0 through LDS (same lane, same slot)
+    if constexpr (KG > 1) {
+        constexpr int SLOT = TM * TN * 16 * 64;
+        const int sp = wave & 3;
+        if (kg > 0) {
+            float *red = smem + ((kg - 1) * 4 + sp) * SLOT;
 #pragma unroll
             for (int i = 0; i < TM; ++i)
 #pragma unroll
                 for (int j = 0; j < TN; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) red[((i * TN + j) * 16 + r) * 64 + lane] = acc[i][j][r];
         }
-        if (kt + 1 < nk) store(buf ^ 1);
         __syncthreads();
+        if (kg > 0) return;
+#pragma unroll
+        for (int q = 1; q < KG; ++q) {
+            const float *red = smem + ((q - 1) * 4 + sp) * SLOT;
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r)
+                        acc[i][j][r] = acc[i][j][r] + red[((i * TN + j) * 16 + r) * 64 + lane];
+        }
     }
 
     // ---- epilogue (C layout: col = lane&31, row = (r&3) + 8(r>>2) + 4(lane>>5))
@@ -181,7 +247,11 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs g) {
 }
 
 // ---------------------------------------------------------------- conv1d f16
-constexpr int CV_BM = 64, CV_BN = 64, CV_BK = 32, CV_LD = CV_BK + 8;
+// The A operand is the GroupNorm+SiLU activation already rounded to f16 by gn_apply_kernel
+// ([L][Cin], one pass instead of once per tap and per column tile), so staging is a plain
+// 16 B copy with the tap shift and zero padding. 64 x 64 tile, 128-deep K stages, 4 waves
+// of 32 x 32; k runs in ascending 16-chunks per output like ggml's f16 im2col GEMM row.
+constexpr int CV_BM = 64, CV_BN = 64, CV_BK = 128, CV_LD = CV_BK + 8;
 
 __global__ __launch_bounds__(256) void conv_f16_kernel(ConvArgs c) {
     __shared__ __attribute__((aligned(16))) _Float16 As[2][CV_BM * CV_LD];
@@ -190,67 +260,44 @@ __global__ __launch_bounds__(256) void conv_f16_kernel(ConvArgs c) {
     const int wm = wave >> 1, wn = wave & 1;
     const int m0 = blockIdx.y * CV_BM, n0 = blockIdx.x * CV_BN;
     const int K = c.taps * c.Cin;
+    constexpr int NV = CV_BM * CV_BK / 8 / 256;  // 16 B chunks per thread per operand
 
     f32x16 acc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
 
-    // A: 64 rows x 32 k = 512 float4 -> 2 per thread; B: 64 x 32 halves = 256 x 16B -> 1 per thread
-    float4 ra[2];
-    uint4 rb;
-    auto load = [&](int k0) {
+    uint4 ra0[NV], rb0[NV], ra1[NV], rb1[NV];
+    auto load = [&](int k0, uint4 (&ra)[NV], uint4 (&rb)[NV]) {
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int e = tid + i * 256, r = e >> 3, c4 = (e & 7) * 4;
-            const int m = m0 + r, k = k0 + c4;
-            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int i = 0; i < NV; ++i) {
+            const int e = tid + i * 256, r = e / (CV_BK / 8), c8 = (e % (CV_BK / 8)) * 8;
+            const int m = m0 + r, k = k0 + c8;
+            uint4 v = make_uint4(0, 0, 0, 0);
             if (m < c.L && k < K) {
                 const int tap = k / c.Cin, ci = k - tap * c.Cin;
                 const int src = m + tap - c.pad;
-                if (src >= 0 && src < c.L) {
-                    v = *reinterpret_cast<const float4 *>(c.X + (long)src * c.Cin + ci);
-                    float t[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        const int ch = ci + q, grp = ch / c.cpg;
-                        float y = t[q] - c.gn_mean_rstd[2 * grp];
-                        y = y * c.gn_mean_rstd[2 * grp + 1];
-                        y = y * c.gamma[ch];
-                        y = y + c.beta[ch];
-                        t[q] = silu_f(y);
-                    }
-                    v = make_float4(t[0], t[1], t[2], t[3]);
-                }
+                if (src >= 0 && src < c.L) v = *reinterpret_cast<const uint4 *>(c.Xa + (long)src * c.Cin + ci);
             }
             ra[i] = v;
         }
-        {
-            const int r = tid >> 2, c8 = (tid & 3) * 8;
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+            const int e = tid + i * 256, r = e / (CV_BK / 8), c8 = (e % (CV_BK / 8)) * 8;
             const int n = n0 + r, k = k0 + c8;
             uint4 v = make_uint4(0, 0, 0, 0);
             if (n < c.Cout && k < K) v = *reinterpret_cast<const uint4 *>(c.B + (long)n * K + k);
-            rb = v;
+            rb[i] = v;
         }
     };
-    auto store = [&](int buf) {
+    auto store = [&](int buf, const uint4 (&ra)[NV], const uint4 (&rb)[NV]) {
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int e = tid + i * 256, r = e >> 3, c4 = (e & 7) * 4;
-            _Float16 *d = &As[buf][r * CV_LD + c4];
-            d[0] = (_Float16)ra[i].x, d[1] = (_Float16)ra[i].y;
-            d[2] = (_Float16)ra[i].z, d[3] = (_Float16)ra[i].w;
+        for (int i = 0; i < NV; ++i) {
+            const int e = tid + i * 256, r = e / (CV_BK / 8), c8 = (e % (CV_BK / 8)) * 8;
+            *reinterpret_cast<uint4 *>(&As[buf][r * CV_LD + c8]) = ra[i];
+            *reinterpret_cast<uint4 *>(&Bs[buf][r * CV_LD + c8]) = rb[i];
         }
-        const int r = tid >> 2, c8 = (tid & 3) * 8;
-        *reinterpret_cast<uint4 *>(&Bs[buf][r * CV_LD + c8]) = rb;
     };
-
-    const int nk = (K + CV_BK - 1) / CV_BK;
-    load(0);
-    store(0);
-    __syncthreads();
-    for (int kt = 0; kt < nk; ++kt) {
-        const int buf = kt & 1;
-        if (kt + 1 < nk) load((kt + 1) * CV_BK);
+    auto compute = [&](int buf) {
 #pragma unroll
         for (int ks = 0; ks < CV_BK; ks += 16) {
             const f16x8 a = *reinterpret_cast<const f16x8 *>(
@@ -259,7 +306,22 @@ __global__ __launch_bounds__(256) void conv_f16_kernel(ConvArgs c) {
                 &Bs[buf][(wn * 32 + (lane & 31)) * CV_LD + ks + 8 * (lane >> 5)]);
             acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, acc, 0, 0, 0);
         }
-        if (kt + 1 < nk) store(buf ^ 1);
+    };
+
+    const int nk = (K + CV_BK - 1) / CV_BK;
+    load(0, ra0, rb0);
+    if (nk > 1) load(CV_BK, ra1, rb1);
+    store(0, ra0, rb0);
+    __syncthreads();
+    for (int kt = 0; kt < nk; kt += 2) {  // same two-stage register ring as gemm_f32_kernel
+        if (kt + 2 < nk) load((kt + 2) * CV_BK, ra0, rb0);
+        compute(0);
+        if (kt + 1 < nk) store(1, ra1, rb1);
+        __syncthreads();
+        if (kt + 1 >= nk) break;
+        if (kt + 3 < nk) load((kt + 3) * CV_BK, ra1, rb1);
+        compute(1);
+        if (kt + 2 < nk) store(0, ra0, rb0);
         __syncthreads();
     }
     const int col = n0 + wn * 32 + (lane & 31);
@@ -325,46 +387,110 @@ __global__ __launch_bounds__(256) void rownorm_kernel(const float *x, float *y, 
         }
 }
 
-// ---------------------------------------------------------------- group norm stats
-__global__ __launch_bounds__(256) void groupnorm_stats_kernel(const float *x, int L, int C, int cpg,
-                                                              float eps, float *out) {
-    __shared__ double red[256];
-    const int g = blockIdx.x, tid = threadIdx.x;
-    const int c0 = g * cpg;
-    int cn = C - c0 < cpg ? C - c0 : cpg;
-    const long n = (long)L * cn;
-    double s = 0.0;
-    for (long e = tid; e < n; e += 256) {
-        const long l = e / cn;
-        const int cc = (int)(e - l * cn);
-        s += (double)x[l * C + c0 + cc];
+// ---------------------------------------------------------------- group norm
+// ggml_group_norm (miocodec.cpp GroupNorm -> ggml.c group_norm_f32): mean = (float)(sum x / n)
+// in double, variance = (float)(sum (double)fl(fl(x - mean)^2) / n). Rows are cut into P <= 256
+// slices (one block each): pass 1 writes per-slice double sums of x, gn_final reduces the P
+// partials of every group (fixed order, see gn_final_kernel) into the means; pass 2 and a second gn_final do the same for the squared
+// deviations and write rstd; gn_apply writes the f16 conv operand. Kernel boundaries order
+// the passes (no grid-wide fences: on 8 XCDs a device-scope release flushes the L2).
+// Requires C % 8 == 0, C <= 1024, G <= 64 and cpg | 64 (groups never straddle 64 lanes).
+constexpr int GN_MAXJ = 16, GN_PMAX = 256;
+
+template <int PASS>
+__global__ __launch_bounds__(256) void gn_partial_kernel(const float *x, int L, int C, int G, int cpg,
+                                                         int rows, const float2 *stat, double *part) {
+    __shared__ double wsum[4][64];
+    const int p = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int r0 = p * rows, r1 = min(L, r0 + rows);
+    const int nj = (C + 63) / 64;
+    double acc[GN_MAXJ];
+    float mean[GN_MAXJ];
+#pragma unroll
+    for (int j = 0; j < GN_MAXJ; ++j) {
+        acc[j] = 0.0;
+        mean[j] = (PASS == 2 && j * 64 + lane < C) ? stat[(j * 64 + lane) / cpg].x : 0.0f;
     }
-    red[tid] = s;
+#pragma unroll 4
+    for (int r = r0 + wave; r < r1; r += 4) {
+        const float *xr = x + (long)r * C + lane;
+#pragma unroll
+        for (int j = 0; j < GN_MAXJ; ++j)
+            if (j < nj && j * 64 + lane < C) {
+                const float v = xr[j * 64];
+                if constexpr (PASS == 1) {
+                    acc[j] += (double)v;
+                } else {
+                    const float d = v - mean[j];
+                    acc[j] += (double)(d * d);
+                }
+            }
+    }
+    // a group is cpg consecutive lanes of one 64-channel chunk
+#pragma unroll
+    for (int j = 0; j < GN_MAXJ; ++j)
+        if (j < nj) {
+            double s = acc[j];
+            for (int o = 1; o < cpg; o <<= 1) s += __shfl_xor(s, o);
+            if (lane % cpg == 0 && j * 64 + lane < C) wsum[wave][(j * 64 + lane) / cpg] = s;
+        }
     __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
-        if (tid < o) red[tid] += red[tid + o];
-        __syncthreads();
+    for (int g = threadIdx.x; g < G; g += 256)
+        part[(long)p * G + g] = ((wsum[0][g] + wsum[1][g]) + wsum[2][g]) + wsum[3][g];
+}
+
+// One block: stat[g].x = mean (PASS 1) or stat[g].y = rstd (PASS 2) from the P slice sums;
+// 32 lanes per group, lane s takes slices p = s mod 32, then a 5-level xor tree.
+template <int PASS>
+__global__ __launch_bounds__(1024) void gn_final_kernel(const double *part, int P, int G, long n,
+                                                        float eps, float2 *stat) {
+    const int t = threadIdx.x, s32 = t & 31;
+    for (int g0 = 0; g0 < G; g0 += 32) {
+        const int g = g0 + (t >> 5), gg = g < G ? g : 0;
+        double sum = 0.0;
+#pragma unroll
+        for (int i = 0; i < GN_PMAX / 32; ++i) {
+            const int q = s32 + 32 * i;
+            if (q < P) sum += part[(long)q * G + gg];
+        }
+#pragma unroll
+        for (int o = 1; o < 32; o <<= 1) sum += __shfl_xor(sum, o);
+        if (s32 == 0 && g < G) {
+            if constexpr (PASS == 1) {
+                stat[g].x = (float)(sum / (double)n);
+            } else {
+                const float variance = (float)(sum / (double)n);
+                stat[g].y = 1.0f / sqrtf(variance + eps);
+            }
+        }
     }
-    const float mean = (float)(red[0] / (double)n);
+}
+
+// xa[l][c] = f16(silu((x - mean) * rstd * gamma + beta)), 8 channels per thread.
+__global__ __launch_bounds__(256) void gn_apply_kernel(const float *x, int L, int C, int G, int cpg,
+                                                       const float2 *stat, const float *gamma,
+                                                       const float *beta, _Float16 *xa) {
+    __shared__ float2 st[64];
+    if (threadIdx.x < G) st[threadIdx.x] = stat[threadIdx.x];
     __syncthreads();
-    double s2 = 0.0;
-    for (long e = tid; e < n; e += 256) {
-        const long l = e / cn;
-        const int cc = (int)(e - l * cn);
-        const float v = x[l * C + c0 + cc] - mean;
-        s2 += (double)(v * v);
+    const long e8 = (long)blockIdx.x * 256 + threadIdx.x;
+    if (e8 * 8 >= (long)L * C) return;
+    const int c0 = (int)((e8 * 8) % C);
+    const float4 u0 = *reinterpret_cast<const float4 *>(x + e8 * 8);
+    const float4 u1 = *reinterpret_cast<const float4 *>(x + e8 * 8 + 4);
+    const float t[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
+    f16x8 o;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const int ch = c0 + q;
+        const float2 ms = st[ch / cpg];
+        float y = t[q] - ms.x;
+        y = y * ms.y;
+        y = y * gamma[ch];
+        y = y + beta[ch];
+        o[q] = (_Float16)silu_f(y);
     }
-    red[tid] = s2;
-    __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
-        if (tid < o) red[tid] += red[tid + o];
-        __syncthreads();
-    }
-    if (tid == 0) {
-        const float variance = (float)(red[0] / (double)n);
-        out[2 * g] = mean;
-        out[2 * g + 1] = 1.0f / sqrtf(variance + eps);
-    }
+    *reinterpret_cast<f16x8 *>(xa + e8 * 8) = o;
 }
 
 // ---------------------------------------------------------------- banded attention
@@ -488,12 +614,13 @@ __global__ __launch_bounds__(256) void cond_gemv_kernel(const float *W, const fl
     if (lane == 0) y[r] = a + b[r];
 }
 
-template <int BM, int BN>
-void launch_gemm_tiles(const GemmArgs &a, int epi, hipStream_t s) {
-    dim3 grid((a.N + BN - 1) / BN, (a.M + BM - 1) / BM);
+template <int KG>
+void launch_gemm_kg(const GemmArgs &a, int epi, hipStream_t s) {
+    const long nb = (long)((a.M + GF_T - 1) / GF_T) * ((a.N + GF_T - 1) / GF_T);
+    dim3 grid((unsigned)(8 * ((nb + 7) / 8)));
     switch (epi) {
 #define CASE(E) \
-    case E: hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, E>), grid, dim3(256), 0, s, a); break;
+    case E: hipLaunchKernelGGL((gemm_f32_kernel<KG, E>), grid, dim3(256 * KG), 0, s, a); break;
         CASE(EPI_STORE)
         CASE(EPI_RESID)
         CASE(EPI_GATED)
@@ -508,12 +635,25 @@ void launch_gemm_tiles(const GemmArgs &a, int epi, hipStream_t s) {
 
 }  // namespace
 
-void launch_gemm_f32(const GemmArgs &a, int epi, hipStream_t s) {
-    const long big_tiles = (long)((a.M + 127) / 128) * ((a.N + 127) / 128);
-    if (big_tiles >= 240)
-        launch_gemm_tiles<128, 128>(a, epi, s);
-    else
-        launch_gemm_tiles<64, 64>(a, epi, s);
+// K-groups per block: enough blocks x waves to give every CU 16 waves (MIO_CODEC_KG forces).
+int gemm_kgroups(long tiles) {
+    static const int forced = [] {
+        const char *e = getenv("MIO_CODEC_KG");
+        return e ? atoi(e) : 0;
+    }();
+    if (forced == 1 || forced == 2 || forced == 4) return forced;
+    return tiles >= 512 ? 1 : tiles >= 256 ? 2 : 4;
+}
+
+void launch_gemm_f32(const GemmArgs &a0, int epi, hipStream_t s) {
+    GemmArgs a = a0;
+    a.m_major = (long)a.M * a.K > (long)a.N * a.K * 2 ? 1 : 0;  // slab the larger operand
+    const long tiles = (long)((a.M + GF_T - 1) / GF_T) * ((a.N + GF_T - 1) / GF_T);
+    switch (gemm_kgroups(tiles)) {
+        case 1: launch_gemm_kg<1>(a, epi, s); break;
+        case 2: launch_gemm_kg<2>(a, epi, s); break;
+        default: launch_gemm_kg<4>(a, epi, s); break;
+    }
 }
 
 void launch_conv_f16(const ConvArgs &a, hipStream_t s) {
@@ -526,9 +666,24 @@ void launch_rownorm(const float *x, float *y, int M, int D, float eps, int mode,
     hipLaunchKernelGGL(rownorm_kernel, dim3((M + 3) / 4), dim3(256), 0, s, x, y, M, D, eps, mode, p0, p1);
 }
 
-void launch_groupnorm_stats(const float *x, int L, int C, int G, int cpg, float eps, float *mr,
-                            hipStream_t s) {
-    hipLaunchKernelGGL(groupnorm_stats_kernel, dim3(G), dim3(256), 0, s, x, L, C, cpg, eps, mr);
+void launch_groupnorm_apply(const float *x, int L, int C, int G, float eps, const float *gamma,
+                            const float *beta, GnScratch gs, _Float16 *xa, hipStream_t s) {
+    const int cpg = C / G;
+    int rows = 4;
+    if ((L + rows - 1) / rows > GN_PMAX) rows = (L + GN_PMAX - 1) / GN_PMAX;
+    const int P = (L + rows - 1) / rows;
+    const long n = (long)L * cpg;
+    hipLaunchKernelGGL(gn_partial_kernel<1>, dim3(P), dim3(256), 0, s, x, L, C, G, cpg, rows,
+                       (const float2 *)gs.stat, gs.part);
+    hipLaunchKernelGGL(gn_final_kernel<1>, dim3(1), dim3(1024), 0, s, (const double *)gs.part, P, G, n, eps,
+                       gs.stat);
+    hipLaunchKernelGGL(gn_partial_kernel<2>, dim3(P), dim3(256), 0, s, x, L, C, G, cpg, rows,
+                       (const float2 *)gs.stat, gs.part);
+    hipLaunchKernelGGL(gn_final_kernel<2>, dim3(1), dim3(1024), 0, s, (const double *)gs.part, P, G, n, eps,
+                       gs.stat);
+    const long n8 = (long)L * C / 8;
+    hipLaunchKernelGGL(gn_apply_kernel, dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0, s, x, L, C, G,
+                       cpg, (const float2 *)gs.stat, gamma, beta, xa);
 }
 
 void launch_band_attention(const float *qkv, float *out, int S, int H, int window,

@@ -209,7 +209,9 @@ struct Ws {
     float *xS, *hS, *qkvS, *aS, *fS;
     std::vector<float *> u, t;
     std::vector<int> uL;
-    float *op, *spec, *pcm, *gn, *cond, *emb;
+    float *op, *spec, *pcm, *cond, *emb;
+    mio::GnScratch gns;
+    _Float16 *xa;
     int *codes;
     int Lf;
 };
@@ -252,7 +254,13 @@ int plan_ws(mio_hip_codec *c, int T, Ws &w, bool alloc) {
     F(&w.op, (size_t)L * c->dec_dim);
     F(&w.spec, (size_t)L * 2 * c->n_freq);
     F(&w.pcm, (size_t)L * c->hop + c->n_fft);
-    F(&w.gn, 2 * 64);
+    // GroupNorm slice partials (doubles) and the f16 conv operand of the widest ResNet
+    size_t xa_n = (size_t)S * c->dec_dim;
+    for (int st = 0; st < c->up_stages; ++st) xa_n = std::max(xa_n, (size_t)w.uL[st] * c->ups[st].Cout);
+    float *gnp_f = nullptr, *gns_f = nullptr, *xa_f = nullptr;
+    F(&gnp_f, (size_t)mio::kGnPartDoubles * 2);
+    F(&gns_f, 2 * 64);
+    F(&xa_f, (xa_n + 1) / 2);
     F(&w.cond, (size_t)c->cond_rows);
     F(&w.emb, (size_t)c->adaln);
     float *codes_f = nullptr;
@@ -269,6 +277,9 @@ int plan_ws(mio_hip_codec *c, int T, Ws &w, bool alloc) {
     }
     for (auto &s : slots) *s.first = (float *)(c->ws + s.second);
     w.codes = (int *)codes_f;
+    w.gns.part = (double *)gnp_f;
+    w.gns.stat = (float2 *)gns_f;
+    w.xa = (_Float16 *)xa_f;
     w.T = T;
     w.S = S;
     if (alloc && S > c->rope_cap) {
@@ -298,19 +309,17 @@ mio::GemmArgs gemm(const float *A, int K, int M, const float *B, int N, float *C
     return g;
 }
 
-void resnet(mio_hip_codec *c, const ResW &r, float *x, float *t, int L, int C, float *gn,
+void resnet(mio_hip_codec *c, const ResW &r, float *x, float *t, int L, int C, const Ws &w,
             hipStream_t s) {
-    const int cpg = (C + c->groups - 1) / c->groups;
     mio::ConvArgs a{};
-    a.L = L, a.Cin = C, a.taps = 3, a.pad = 1, a.G = c->groups, a.cpg = cpg, a.Cout = C;
-    a.gn_mean_rstd = gn;
+    a.L = L, a.Cin = C, a.taps = 3, a.pad = 1, a.Cout = C, a.Xa = w.xa;
     // t = conv1(silu(GN1(x))) + b1
-    mio::launch_groupnorm_stats(x, L, C, c->groups, cpg, c->gn_eps, gn, s);
-    a.X = x, a.gamma = r.gn1_w, a.beta = r.gn1_b, a.B = r.w1, a.bias = r.b1, a.Y = t, a.resid = nullptr;
+    mio::launch_groupnorm_apply(x, L, C, c->groups, c->gn_eps, r.gn1_w, r.gn1_b, w.gns, w.xa, s);
+    a.B = r.w1, a.bias = r.b1, a.Y = t, a.resid = nullptr;
     mio::launch_conv_f16(a, s);
     // x = conv2(silu(GN2(t))) + b2 + x
-    mio::launch_groupnorm_stats(t, L, C, c->groups, cpg, c->gn_eps, gn, s);
-    a.X = t, a.gamma = r.gn2_w, a.beta = r.gn2_b, a.B = r.w2, a.bias = r.b2, a.Y = x, a.resid = x;
+    mio::launch_groupnorm_apply(t, L, C, c->groups, c->gn_eps, r.gn2_w, r.gn2_b, w.gns, w.xa, s);
+    a.B = r.w2, a.bias = r.b2, a.Y = x, a.resid = x;
     mio::launch_conv_f16(a, s);
 }
 
@@ -356,7 +365,7 @@ int run_decode(mio_hip_codec *c, Ws &w, hipStream_t s, int stop_stage, const flo
     }
     if (done(w.xS, S, Dd)) return MIO_OK;
     // 4. wave_prior (:629-637)
-    for (auto &r : c->prior) resnet(c, r, w.xS, w.hS, S, Dd, w.gn, s);
+    for (auto &r : c->prior) resnet(c, r, w.xS, w.hS, S, Dd, w, s);
     if (done(w.xS, S, Dd)) return MIO_OK;
     // 5. AdaLN-Zero decoder (:640-660); all conditioning vectors in one GEMV
     mio::launch_cond_gemv(c->cond_w, c->cond_b, w.emb, c->cond_rows, c->adaln, w.cond, s);
@@ -385,7 +394,7 @@ int run_decode(mio_hip_codec *c, Ws &w, hipStream_t s, int stop_stage, const flo
     }
     if (done(w.xS, S, Dd)) return MIO_OK;
     // 6. wave_post (:663-672)
-    for (auto &r : c->post) resnet(c, r, w.xS, w.hS, S, Dd, w.gn, s);
+    for (auto &r : c->post) resnet(c, r, w.xS, w.hS, S, Dd, w, s);
     if (done(w.xS, S, Dd)) return MIO_OK;
     // 7. upsampler stages (:677-708): ConvT(+trim)+Snake as one tap-window GEMM, then ResNet
     const float *src = w.xS;
@@ -400,7 +409,7 @@ int run_decode(mio_hip_codec *c, Ws &w, hipStream_t s, int stop_stage, const flo
         g.C = w.u[st], g.ldc = u.Cout, g.bias = u.b, g.aux = u.alpha_e, g.aux2 = u.beta_e;
         g.f = u.f, g.trim = u.trim, g.cout = u.Cout, g.rows_out = Lout;
         mio::launch_gemm_f32(g, mio::EPI_CONVT_SNAKE, s);
-        resnet(c, u.res, w.u[st], w.t[st], Lout, u.Cout, w.gn, s);
+        resnet(c, u.res, w.u[st], w.t[st], Lout, u.Cout, w, s);
         src = w.u[st];
         Lin = Lout;
         if (done(w.u[st], Lout, u.Cout)) return MIO_OK;
@@ -634,6 +643,17 @@ extern "C" int mio_hip_codec_load(mio_hip_device *d, const char *path, mio_hip_c
         c->head_b = ld.up(ob);
     }
     if (!ld.ok) return fail(MIO_ERR_FORMAT);
+    {   // ResNet widths: f16 conv operand in 8-channel chunks, GroupNorm groups inside 64 lanes
+        auto gn_ok = [&](int C) {
+            return C % 8 == 0 && C <= 1024 && C % c->groups == 0 && 64 % (C / c->groups) == 0;
+        };
+        bool ok = gn_ok(Dd);
+        for (const UpW &u : c->ups) ok = ok && gn_ok(u.Cout);
+        if (!ok) {
+            mio::set_error("miocodec: ResNet widths must be multiples of 8 (<= 1024) with C/groups dividing 64");
+            return fail(MIO_ERR_UNSUPPORTED);
+        }
+    }
     rc = mio_hip_istft_create(d, c->n_fft, c->n_fft, &c->ist);
     if (rc) return fail(rc);
     *out = c;
