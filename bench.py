@@ -241,7 +241,8 @@ def roofline(llm, preset):
     import numpy as np
     tl = llm.timeline()
     nl = tl.shape[0]
-    names = [KERNEL_NAMES[k] for k in (0, 1, 2, 3, 4)] * ((nl - 2) // 5) + [KERNEL_NAMES[6], "k_sample"]
+    # 5 launches per layer + lm_head; the sampler runs inside layer 0's attn_in
+    names = [KERNEL_NAMES[k] for k in (0, 1, 2, 3, 4)] * ((nl - 1) // 5) + [KERNEL_NAMES[6]]
     dur = np.nanmax(tl[:, :, 7], axis=1) - np.nanmin(tl[:, :, 0], axis=1)
     step_wall_us = float(np.nanmax(tl[-1, :, 7]) - np.nanmin(tl[0, :, 0]))
     per_kernel = {}
@@ -257,7 +258,7 @@ def roofline(llm, preset):
     # achieved: HIP events around back-to-back launches of the kernel on its own stream (the
     # timeline's in-graph span runs the diagnostic instantiation: reported beside it)
     achieved = bytes_of[dom] / (event_us[dom] * 1e-6) / 1e9
-    n_layer = (nl - 2) // 5
+    n_layer = (nl - 1) // 5
     step_bytes = sum(bytes_of[KERNEL_NAMES[k]] * n_layer for k in (0, 1, 2, 3, 4)) + bytes_of["k_lm_head"]
     step_gbs = step_bytes / (step_wall_us * 1e-6) / 1e9
     traffic = None

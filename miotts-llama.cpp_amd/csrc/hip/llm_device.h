@@ -365,7 +365,7 @@ __device__ __forceinline__ void x_after_weights(XRegs<XV> &xr) {
 
 template <int XV>
 __device__ inline void load_x(const float *x, const float *w, int K, XRegs<XV> &xr) {
-    const auto rx = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(x), 0, K * 4, 0x00020000);
+    const auto rx = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(x), 0, x ? K * 4 : 0, 0x00020000);
     const auto rw = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(w), 0, w ? K * 4 : 0, 0x00020000);
 #pragma unroll
     for (int i = 0; i < XV; ++i) {
@@ -511,18 +511,25 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void *p, uint32_t b
 #ifndef MIO_WEIGHT_AUX
 #define MIO_WEIGHT_AUX 2
 #endif
+// policy of the small per-layer streams (attn_in q|k|v, attn_out o): A/B knob
+#ifndef MIO_SMALL_AUX
+#define MIO_SMALL_AUX MIO_WEIGHT_AUX
+#endif
+template <int AUX = MIO_WEIGHT_AUX>
 __device__ __forceinline__ uint4 bld16(const uint8_t *base, uint32_t bytes, uint32_t voff, uint32_t soff) {
-    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rsrc(base, bytes), voff, soff, MIO_WEIGHT_AUX);
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rsrc(base, bytes), voff, soff, AUX);
     return make_uint4(v.x, v.y, v.z, v.w);
 }
+template <int AUX = MIO_WEIGHT_AUX>
 __device__ __forceinline__ uint32_t bld4(const uint8_t *base, uint32_t bytes, uint32_t voff, uint32_t soff) {
-    return __builtin_amdgcn_raw_buffer_load_b32(rsrc(base, bytes), voff, soff, MIO_WEIGHT_AUX);
+    return __builtin_amdgcn_raw_buffer_load_b32(rsrc(base, bytes), voff, soff, AUX);
 }
+template <int AUX = MIO_WEIGHT_AUX>
 __device__ __forceinline__ uint32_t bld2(const uint8_t *base, uint32_t bytes, uint32_t voff, uint32_t soff) {
-    return __builtin_amdgcn_raw_buffer_load_b16(rsrc(base, bytes), voff, soff, MIO_WEIGHT_AUX);
+    return __builtin_amdgcn_raw_buffer_load_b16(rsrc(base, bytes), voff, soff, AUX);
 }
 
-template <int T>
+template <int T, int AUX = MIO_WEIGHT_AUX>
 __device__ __forceinline__ Frag load_frag(const QMat W, int row, int pass) {
     const int lane = MIO_TIDX & 63;
     // the row is wave-uniform; readfirstlane lets the compiler keep it (and the soffset) in
@@ -533,27 +540,27 @@ __device__ __forceinline__ Frag load_frag(const QMat W, int row, int pass) {
     if constexpr (T == 12) {
         const int nsb = W.k >> 8, sb = min(pass * 8 + (lane >> 3), nsb - 1), pc = lane & 7;
         const uint32_t qb = (uint32_t)(W.k / 2), hb = (uint32_t)nsb * 16;
-        f.a = bld16(W.p0, R * qb, sb * 128 + pc * 16, r * qb);
+        f.a = bld16<AUX>(W.p0, R * qb, sb * 128 + pc * 16, r * qb);
         // header dword (lane & 3) only: both quads of the superblock's 8 lanes hold all four,
         // broadcast by DPP in dot_frag (a quarter of the load-return traffic of 16 B per lane)
-        f.c = bld4(W.p1, R * hb, sb * 16 + 4 * (pc & 3), r * hb);
+        f.c = bld4<AUX>(W.p1, R * hb, sb * 16 + 4 * (pc & 3), r * hb);
         f.b = make_uint4(0, 0, 0, 0);
         f.e = 0;
     } else if constexpr (T == 14) {
         const int nsb = W.k >> 8, sb = min(pass * 8 + (lane >> 3), nsb - 1), pc = lane & 7;
         const uint32_t lb = (uint32_t)(W.k / 2), hb = (uint32_t)(W.k / 4), sbb = (uint32_t)(W.k / 16),
                        db = (uint32_t)nsb * 2;
-        f.a = bld16(W.p0, R * lb, sb * 128 + pc * 16, r * lb);
-        f.b = bld16(W.p1, R * hb, sb * 64 + 32 * (pc >> 2) + 16 * (pc & 1), r * hb);
-        f.c = bld2(W.p2, R * sbb, sb * 16 + 2 * pc, r * sbb);
-        f.e = bld2(W.p3, R * db, sb * 2, r * db);
+        f.a = bld16<AUX>(W.p0, R * lb, sb * 128 + pc * 16, r * lb);
+        f.b = bld16<AUX>(W.p1, R * hb, sb * 64 + 32 * (pc >> 2) + 16 * (pc & 1), r * hb);
+        f.c = bld2<AUX>(W.p2, R * sbb, sb * 16 + 2 * pc, r * sbb);
+        f.e = bld2<AUX>(W.p3, R * db, sb * 2, r * db);
     } else {
         const int nb = W.k >> 5, b = min(pass * 64 + lane, nb - 1);
         const uint32_t qb = (uint32_t)W.k, db = (uint32_t)nb * 2;
-        f.a = bld16(W.p0, R * qb, 32 * b, r * qb);
-        f.b = bld16(W.p0, R * qb, 32 * b + 16, r * qb);
+        f.a = bld16<AUX>(W.p0, R * qb, 32 * b, r * qb);
+        f.b = bld16<AUX>(W.p0, R * qb, 32 * b + 16, r * qb);
         f.c = 0;
-        f.e = bld2(W.p1, R * db, 2 * b, r * db);
+        f.e = bld2<AUX>(W.p1, R * db, 2 * b, r * db);
     }
     return f;
 }
@@ -686,7 +693,7 @@ struct Cfg {
 // compiler's in-order vmcnt accounting stays exact). Unit u -> row lo + u/(NP*NM),
 // matrix (u/NP)%NM, pass u%NP. With NM == 1, rows >= split come from W1 (row - split):
 // two matrices of one type streamed as one row space (q|k).
-template <int T, int NP, int NM, int SU = 0>
+template <int T, int NP, int NM, int SU = 0, int AUX = MIO_WEIGHT_AUX>
 __device__ __forceinline__ void load_group(const QMat W0, const QMat W1, int lo, int n, int u0,
                                            Frag (&f)[Cfg<NP, SU>::U], int split = INT_MAX) {
 #pragma unroll
@@ -697,9 +704,9 @@ __device__ __forceinline__ void load_group(const QMat W0, const QMat W1, int lo,
         const int p = u % NP, m = (u / NP) % NM, i = u / (NP * NM);
         if constexpr (NM == 1) {
             const int r = __builtin_amdgcn_readfirstlane(lo + i);
-            f[j] = load_frag<T>(r >= split ? W1 : W0, r >= split ? r - split : r, p);
+            f[j] = load_frag<T, AUX>(r >= split ? W1 : W0, r >= split ? r - split : r, p);
         } else {
-            f[j] = load_frag<T>(m ? W1 : W0, lo + i, p);
+            f[j] = load_frag<T, AUX>(m ? W1 : W0, lo + i, p);
         }
     }
 }
@@ -709,7 +716,7 @@ __device__ __forceinline__ void load_group(const QMat W0, const QMat W1, int lo,
 // the first two groups (units [0, U) and [U, 2U)), issued by the caller before its
 // prologue; groups then alternate between A and B, one group in flight while the other is
 // reduced (no register copies).
-template <int T, int NP, int NM, int SU = 0, class Epi>
+template <int T, int NP, int NM, int SU = 0, int AUX = MIO_WEIGHT_AUX, class Epi>
 __device__ __forceinline__ void stream_rows(const QMat W0, const QMat W1, int lo, int hi, Frag (&A)[Cfg<NP, SU>::U],
                                             Frag (&B)[Cfg<NP, SU>::U], const ActL &a, Epi &&epi, int split = INT_MAX,
                                             unsigned long long *trace = nullptr) {
@@ -763,21 +770,21 @@ __device__ __forceinline__ void stream_rows(const QMat W0, const QMat W1, int lo
         if constexpr (Cfg<NP, SU>::NG == 1) break;
         u0 += U;
         if (u0 >= n) break;
-        load_group<T, NP, NM, SU>(W0, W1, lo, n, u0 + U, A, split);
+        load_group<T, NP, NM, SU, AUX>(W0, W1, lo, n, u0 + U, A, split);
         consume(B, u0);
         u0 += U;
         if (u0 >= n) break;
-        load_group<T, NP, NM, SU>(W0, W1, lo, n, u0 + U, B, split);
+        load_group<T, NP, NM, SU, AUX>(W0, W1, lo, n, u0 + U, B, split);
     }
 }
 
 // The first group(s) of a wave's stream (before the prologue).
-template <int T, int NP, int NM, int SU = 0>
+template <int T, int NP, int NM, int SU = 0, int AUX = MIO_WEIGHT_AUX>
 __device__ __forceinline__ void load_first(const QMat W0, const QMat W1, int lo, int hi, Frag (&A)[Cfg<NP, SU>::U],
                                            Frag (&B)[Cfg<NP, SU>::U], int split = INT_MAX) {
     const int n = (hi - lo) * NM * NP;
-    load_group<T, NP, NM, SU>(W0, W1, lo, n, 0, A, split);
-    if constexpr (Cfg<NP, SU>::NG == 2) load_group<T, NP, NM, SU>(W0, W1, lo, n, Cfg<NP, SU>::U, B, split);
+    load_group<T, NP, NM, SU, AUX>(W0, W1, lo, n, 0, A, split);
+    if constexpr (Cfg<NP, SU>::NG == 2) load_group<T, NP, NM, SU, AUX>(W0, W1, lo, n, Cfg<NP, SU>::U, B, split);
 }
 
 // Rows [0, R) over G workgroups: workgroup b owns [R*b/G, R*(b+1)/G), wave w a contiguous
@@ -946,6 +953,60 @@ __device__ inline float gumbel(uint64_t seed, int step, int idx) {
 }
 
 
+
+// ------------------------------------------------------------------ sampler
+// Position of the token being decoded (StepState: the sampler of the previous step may still
+// be pending, then the token sits one past st->pos; a full context keeps the last slot).
+__device__ __forceinline__ int cur_pos(const StepState *st, const LlmDims &d) {
+    return min(st->pos + st->pending, d.n_ctx - 1);
+}
+
+// The pending sample's token: Gumbel-max winner (ties -> lowest id) over the lm_head
+// workgroups' partials {smp[2i] value, smp[2i+1] id bits}, sc.lo when no id was allowed, the
+// forced token of this step if any. Whole workgroup of NTH threads (multiple of 64, <= 1024);
+// every thread returns the same token (the winner is order-independent: a total order).
+template <int NTH>
+__device__ int sample_token(const float *smp, int nblk, const SampleCfg &sc, int step, float *rs, int *ri) {
+    const int tid = MIO_TIDX, lane = tid & 63, wave = tid >> 6;
+    float best = -INFINITY;
+    int bi = INT_MAX;
+    const bool forced = sc.force && step < sc.n_force;
+    const int ft = forced ? sc.force[step] : -1;
+    for (int i = tid; i < nblk; i += NTH) {
+        const float v = smp[2 * i];
+        const int ix = __float_as_int(smp[2 * i + 1]);
+        if (v > best || (v == best && ix < bi)) best = v, bi = ix;
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        const float v = __shfl_xor(best, o);
+        const int ix = __shfl_xor(bi, o);
+        if (v > best || (v == best && ix < bi)) best = v, bi = ix;
+    }
+    if (lane == 0) rs[wave] = best, ri[wave] = bi;
+    lds_barrier();
+    best = rs[0], bi = ri[0];
+    for (int w = 1; w < NTH / 64; ++w)
+        if (rs[w] > best || (rs[w] == best && ri[w] < bi)) best = rs[w], bi = ri[w];
+    int tok = bi == INT_MAX ? sc.lo : bi;
+    if (ft >= 0) tok = ft;
+    return tok;
+}
+
+// Embedding row of tok in the matvec prologue's register layout (thread t: elements
+// 4(t + i*MT) .. +3), the same dequantization as embed_row.
+template <int XV>
+__device__ inline void embed_regs(const QMat &emb, int tok, int K, XRegs<XV> &xr) {
+#pragma unroll
+    for (int i = 0; i < XV; ++i) {
+        const int e = (MIO_TIDX + i * MT) * 4;
+        float v[4] = {0.f, 0.f, 0.f, 0.f};
+        if (e < K)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[q] = dequant_elem(emb, tok, e + q);
+        xr.v[i] = make_float4(v[0], v[1], v[2], v[3]);
+    }
+}
 
 // Calls f.template operator()<NP, T>() for the matrix's pass count and weight type.
 template <class F>

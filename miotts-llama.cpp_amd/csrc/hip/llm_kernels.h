@@ -19,11 +19,16 @@ struct QMat {
 
 // Device-resident decode state (read by every kernel of a step; advanced by the sampler),
 // so one captured hipGraph replays every token without host involvement.
+// The sampler of step t runs inside step t+1's first launch (layer 0 attn_in) and the flush
+// launch after the last step: `pending` = the lm_head partials of step `step` are not sampled
+// yet, so the token being decoded sits at min(pos + pending, n_ctx - 1) (cur_pos) until
+// layer 0's ffn_in folds pending into pos / step.
 struct StepState {
-    int pos;     // position of the token being decoded
-    int step;    // step counter (sampler RNG counter, output slot)
-    int token;   // token being decoded
-    int done;    // set once an end token was sampled
+    int pos;      // position of the last sampled token (cur_pos: of the token being decoded)
+    int step;     // step counter (sampler RNG counter, output slot)
+    int token;    // token being decoded
+    int done;     // set once an end token was sampled
+    int pending;  // 1: lm_head partials of this step await the sampler
 };
 
 struct SampleCfg {

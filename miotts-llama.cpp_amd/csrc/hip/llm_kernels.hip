@@ -9,9 +9,11 @@
 //   k_attn_out  chunk merge + re-quantization in the prologue -> O matvec -> x += .
 //   k_ffn_in    RMSNorm(x) -> re-quantize -> gate & up matvec -> silu(g)*u
 //   k_ffn_down  re-quantize h -> down matvec -> x += .
-// then k_lm_head (final RMSNorm + logits + per-workgroup Gumbel-max) and k_sample (token,
-// next embedding, position++). All state is device-resident (StepState), so one hipGraph
-// of a step replays every token with no host round trip.
+// then k_lm_head (final RMSNorm + logits + per-workgroup Gumbel-max). The token is drawn from
+// those partials by the next step's layer-0 attn_in (its prologue, beside its first weight
+// loads) or, after the last step of a run, by k_sample (token, next embedding, position++).
+// All state is device-resident (StepState), so one hipGraph of a step replays every token
+// with no host round trip.
 //
 // Matvec engine ("streaming rows"): one 512-thread workgroup per CU, each wave streams a
 // contiguous run of rows. A row is NP "passes" of 2048 weights; one pass of one row is a
@@ -30,6 +32,7 @@
 #include "llm_device.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 #pragma clang fp contract(off)
 
@@ -42,41 +45,76 @@ namespace {
 // straight-line code with no run-time type dispatch.
 // q|k rows (type TQ) on the first g_qk workgroups, v rows (type TV) on the rest; each
 // branch is WG-uniform and runs its own prologue, so neither path merges load counts.
-template <int NP, int TQ, int TV, int SU, bool DG>
+// FS (layer 0 only): the previous step's sampler runs here when st->pending. Every
+// workgroup reduces the lm_head partials to the same token and dequantizes its embedding
+// row into its x registers while its first weight group is in flight; workgroup 0 also
+// stores x (attn_out's residual) and the token / token ring / EOS flag. pos and step are
+// advanced by layer 0's ffn_in (no kernel before it writes a StepState field it reads).
+template <int NP, int TQ, int TV, int SU, bool DG, bool FS>
 __global__ __launch_bounds__(MT) void k_attn_in(LlmDims d, const float *norm_w, QMat wq, QMat wk, QMat wv,
-                                                int g_qk, LlmBuffers b) {
+                                                int g_qk, LlmBuffers b, QMat emb, int nblk) {
     constexpr bool kDiag = DG;
     extern __shared__ __attribute__((aligned(16))) char smem[];
+    __shared__ float rs_[MW];
+    __shared__ int ri_[MW];
     const int K = d.n_embd;
     const Smem s = carve(smem, K);
     MIO_TRACE(b, 0);
     MIO_TL_BEGIN(b);
+    int pend = 0, step = 0;
+    if constexpr (FS) {
+        pend = b.st->pending;
+        step = b.st->step;
+    }
     XRegs<NP> xr;
-    load_x(b.x, norm_w, K, xr);
+    load_x(pend ? nullptr : b.x, norm_w, K, xr);
     x_gate();
+    auto sample_prologue = [&]() {
+        if constexpr (FS) {
+            if (pend) {
+                const SampleCfg sc = *b.cfg;
+                const int tok = sample_token<MT>(b.smp, nblk, sc, step, rs_, ri_);
+                embed_regs(emb, tok, K, xr);
+                if (blockIdx.x == 0) {
+#pragma unroll
+                    for (int i = 0; i < NP; ++i) {
+                        const int e = (MIO_TIDX + i * MT) * 4;
+                        if (e < K) *reinterpret_cast<float4 *>(b.x + e) = xr.v[i];
+                    }
+                    if (MIO_TIDX == 0) {
+                        if (step < sc.max_steps) sc.out_tokens[step] = tok;
+                        if (tok == sc.eos0 || tok == sc.eos1) b.st->done = 1;
+                        b.st->token = tok;
+                    }
+                }
+            }
+        }
+    };
     const int o1 = wq.rows, o2 = wq.rows + wk.rows;
     Frag ga[Cfg<NP, SU>::U], gb[Cfg<NP, SU>::U];
     int lo, hi;
     if ((int)blockIdx.x < g_qk) {
         wave_range(o2, lo, hi, blockIdx.x, g_qk);
-        load_first<TQ, NP, 1, SU>(wq, wk, lo, hi, ga, gb, o1);
+        load_first<TQ, NP, 1, SU, MIO_SMALL_AUX>(wq, wk, lo, hi, ga, gb, o1);
+        sample_prologue();
         x_after_weights(xr);
         MIO_TRACE(b, 1);
     MIO_TL_MARK1(b);
         rmsnorm_quant(xr, K, d.eps, TQ != 8, s, MIO_TL_DIAGSLOT(b));
         MIO_TRACE(b, 2);
     MIO_TL_MARK(b, 2);
-        stream_rows<TQ, NP, 1, SU>(wq, wk, lo, hi, ga, gb, s.a, [&](int row, float v, float) {
+        stream_rows<TQ, NP, 1, SU, MIO_SMALL_AUX>(wq, wk, lo, hi, ga, gb, s.a, [&](int row, float v, float) {
             if ((threadIdx.x & 63) == 0) b.qkv[row] = v;
         }, o1);
         MIO_TL_END(b);
     MIO_TRACE(b, 15);
     } else {
         wave_range(wv.rows, lo, hi, blockIdx.x - g_qk, matvec_grid_n(d.n_wg, o2 + wv.rows) - g_qk);
-        load_first<TV, NP, 1, SU>(wv, wv, lo, hi, ga, gb);
+        load_first<TV, NP, 1, SU, MIO_SMALL_AUX>(wv, wv, lo, hi, ga, gb);
+        sample_prologue();
         x_after_weights(xr);
         rmsnorm_quant(xr, K, d.eps, TQ != 8, s, MIO_TL_DIAGSLOT(b));
-        stream_rows<TV, NP, 1, SU>(wv, wv, lo, hi, ga, gb, s.a, [&](int row, float v, float) {
+        stream_rows<TV, NP, 1, SU, MIO_SMALL_AUX>(wv, wv, lo, hi, ga, gb, s.a, [&](int row, float v, float) {
             if ((threadIdx.x & 63) == 0) b.qkv[o2 + row] = v;
         });
         MIO_TL_END(b);
@@ -104,13 +142,13 @@ __global__ __launch_bounds__(MT) void k_attn_out(LlmDims d, QMat wo, LlmBuffers 
     wave_range(d, wo.rows, lo, hi);
     const float xres = load_resid(b.x, lo, hi);
     Frag ga[Cfg<NP, SU>::U], gb[Cfg<NP, SU>::U];
-    load_first<T, NP, 1, SU>(wo, wo, lo, hi, ga, gb);
+    load_first<T, NP, 1, SU, MIO_SMALL_AUX>(wo, wo, lo, hi, ga, gb);
     MIO_TRACE(b, 1);
     MIO_TL_MARK1(b);
-    merge_attention<NP>(d, b.part, b.st->pos / ATT_CHUNK + 1, K, T != 8, s, MIO_TL_DIAGSLOT(b));
+    merge_attention<NP>(d, b.part, cur_pos(b.st, d) / ATT_CHUNK + 1, K, T != 8, s, MIO_TL_DIAGSLOT(b));
     MIO_TRACE(b, 2);
     MIO_TL_MARK(b, 2);
-    stream_rows<T, NP, 1, SU>(wo, wo, lo, hi, ga, gb, s.a, [&](int row, float v, float) {
+    stream_rows<T, NP, 1, SU, MIO_SMALL_AUX>(wo, wo, lo, hi, ga, gb, s.a, [&](int row, float v, float) {
         const float r = lane_value(xres, row - lo);
         if ((threadIdx.x & 63) == 0) b.x[row] = v + r;
     });
@@ -118,9 +156,10 @@ __global__ __launch_bounds__(MT) void k_attn_out(LlmDims d, QMat wo, LlmBuffers 
     MIO_TRACE(b, 15);
 }
 
+// adv (layer 0): folds a sampled-in-attn_in token into pos / step (StepState.pending).
 template <int NP, int T, int SU, bool DG>
 __global__ __launch_bounds__(MT) void k_ffn_in(LlmDims d, const float *norm_w, QMat gate, QMat up,
-                                               LlmBuffers b) {
+                                               LlmBuffers b, int adv) {
     constexpr bool kDiag = DG;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     MIO_TRACE(b, 0);
@@ -143,6 +182,13 @@ __global__ __launch_bounds__(MT) void k_ffn_in(LlmDims d, const float *norm_w, Q
     stream_rows<T, NP, 2, SU>(gate, up, lo, hi, ga, gb, s.a, [&](int row, float g, float u) {
         if ((threadIdx.x & 63) == 0) b.h[row] = silu_f(g) * u;
     }, INT_MAX, DG ? b.trace : nullptr);
+    if (adv && blockIdx.x == 0 && MIO_TIDX == 0) {
+        StepState *st = b.st;
+        const int p = st->pending;
+        st->pos = min(st->pos + p, d.n_ctx - 1);
+        st->step = st->step + p;
+        st->pending = 0;
+    }
     MIO_TL_END(b);
     MIO_TRACE(b, 15);
 }
@@ -242,6 +288,7 @@ __global__ __launch_bounds__(MT) void k_lm_head(LlmDims d, const float *norm_w, 
             if (bs_[w] > best || (bs_[w] == best && bi_[w] < bi)) best = bs_[w], bi = bi_[w];
         b.smp[2 * blockIdx.x] = best;
         b.smp[2 * blockIdx.x + 1] = __int_as_float(bi);
+        if (blockIdx.x == 0) b.st->pending = 1;  // sampled by the next step's attn_in or the flush
     }
     MIO_TL_END(b);
     MIO_TRACE(b, 15);
@@ -271,7 +318,7 @@ __global__ __launch_bounds__(ATT_NT) void k_attention(LlmDims d, const float *q_
     // scalar-load round trip before the first K/V load)
     asm volatile("" ::"s"(kc), "s"(vc), "s"(d.n_ctx), "s"(b.qkv), "s"(b.rope), "s"(q_norm), "s"(k_norm),
                  "s"(b.part), "s"(d.max_splits), "s"(bqkv));
-    const int pos = b.st->pos;
+    const int pos = cur_pos(b.st, d);
     const int t0 = ch * ATT_CHUNK;
     if (t0 > pos) return;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -346,55 +393,34 @@ void launch_attention(int G, dim3 grid, hipStream_t s, const LlmDims &d, const L
 }
 
 // ------------------------------------------------------------------ sampler / embedding
+// The flush sampler (after the last step of a run; the step graph samples inside the next
+// step's layer-0 attn_in): the pending token, its embedding into b.x, the state advance.
 template <bool DG>
 __global__ __launch_bounds__(ST) void k_sample(LlmDims d, QMat emb, int nblk, LlmBuffers b) {
     constexpr bool kDiag = DG;
-    const SampleCfg sc = *b.cfg;
-    __shared__ float bs_[ST / 64];
-    __shared__ int bi_[ST / 64];
-    __shared__ int tok_s;
+    __shared__ float rs_[ST / 64];
+    __shared__ int ri_[ST / 64];
     MIO_TRACE(b, 0);
     MIO_TL_BEGIN(b);
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int step = b.st->step;
-    float best = -INFINITY;
-    int bi = INT_MAX;
-    for (int i = tid; i < nblk; i += ST) {
-        const float v = b.smp[2 * i];
-        const int ix = __float_as_int(b.smp[2 * i + 1]);
-        if (v > best || (v == best && ix < bi)) best = v, bi = ix;
-    }
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-        const float v = __shfl_xor(best, o);
-        const int ix = __shfl_xor(bi, o);
-        if (v > best || (v == best && ix < bi)) best = v, bi = ix;
-    }
-    if (lane == 0) bs_[wave] = best, bi_[wave] = bi;
-    lds_barrier();
-    if (tid == 0) {
-        for (int w = 1; w < ST / 64; ++w)
-            if (bs_[w] > best || (bs_[w] == best && bi_[w] < bi)) best = bs_[w], bi = bi_[w];
-        int tok = bi;
-        if (tok == INT_MAX) tok = sc.lo;
-        if (sc.force && step < sc.n_force && sc.force[step] >= 0) tok = sc.force[step];
-        tok_s = tok;
-    }
-    lds_barrier();
-    const int tok = tok_s;
+    StepState *st = b.st;
+    if (!st->pending) return;
+    const SampleCfg sc = *b.cfg;
+    const int step = st->step;
+    const int tok = sample_token<ST>(b.smp, nblk, sc, step, rs_, ri_);
     MIO_TRACE(b, 1);
     MIO_TL_MARK1(b);
     embed_row(emb, tok, d.n_embd, b.x);
     MIO_TL_END(b);
     MIO_TRACE(b, 15);
-    if (tid == 0) {
+    if (MIO_TIDX == 0) {
         if (step < sc.max_steps) sc.out_tokens[step] = tok;
-        if (tok == sc.eos0 || tok == sc.eos1) b.st->done = 1;
-        b.st->token = tok;
+        if (tok == sc.eos0 || tok == sc.eos1) st->done = 1;
+        st->token = tok;
         // a full context ends generation (host-side step budget); the state never points
         // past the cache, so later diagnostic launches stay in bounds
-        b.st->pos = min(b.st->pos + 1, d.n_ctx - 1);
-        b.st->step = step + 1;
+        st->pos = min(st->pos + 1, d.n_ctx - 1);
+        st->step = step + 1;
+        st->pending = 0;
     }
 }
 
@@ -411,7 +437,20 @@ int pick_np(int K) { return K <= 2048 ? 1 : (K <= 6144 ? 3 : 6); }
 static_assert(MW == 8, "matvec_grid_n assumes 8 waves per workgroup");
 int matvec_grid(const LlmDims &d, int rows) { return matvec_grid_n(d.n_wg, rows); }
 
-int lm_head_blocks(const LlmDims &d) { return matvec_grid(d, d.n_vocab); }
+// lm_head workgroups per CU (MIO_LM_WGM, 1..4): the lm_head launch sees n_wg scaled. Two
+// per CU (16 waves) stream the 255 MB output matrix in 47.5 us against 49.5 us for one
+// (same-box A/B, 1.7B Q4_K_M).
+LlmDims lm_dims(const LlmDims &d) {
+    static const int mult = [] {
+        const char *e = getenv("MIO_LM_WGM");
+        const int v = e ? atoi(e) : 2;
+        return v < 1 ? 1 : (v > 4 ? 4 : v);
+    }();
+    LlmDims l = d;
+    l.n_wg = d.n_wg * mult;
+    return l;
+}
+int lm_head_blocks(const LlmDims &d) { const LlmDims l = lm_dims(d); return matvec_grid(l, l.n_vocab); }
 
 size_t matvec_lds(int K) { return smem_bytes(K); }
 
@@ -452,7 +491,8 @@ void dispatch_su(int su, F &&f) {
 
 // Launch one kernel of the step: which = 0 attn_in, 1 attention, 2 attn_out (+ chunk
 // merge), 3 ffn_in, 4 ffn_down (layer il), 5 (unused: the final norm is fused into
-// lm_head), 6 lm_head, 7 sample.
+// lm_head), 6 lm_head, 7 flush sampler. Layer 0's attn_in samples the pending token of the
+// previous step and layer 0's ffn_in advances pos / step (StepState.pending).
 void launch_step_kernel(int which, const LlmDims &d, const LayerW *layers, int il, _Float16 *kcache,
                         _Float16 *vcache, const float *out_norm, const QMat &lm, const QMat &tok_embd,
                         const LlmBuffers &b, hipStream_t s) {
@@ -469,11 +509,16 @@ void launch_step_kernel(int which, const LlmDims &d, const LayerW *layers, int i
             const int np = pick_np(d.n_embd);
             const int un = std::max(max_wave_units(L.wq.rows + L.wk.rows, g_qk, np, 1),
                                     max_wave_units(L.wv.rows, GW - g_qk, np, 1));
+            const int nblk = lm_head_blocks(d);
             dispatch_nt(d.n_embd, L.wq.type, [&]<int NP, int TQ>() {
                 auto go = [&]<int TV>() {
                     dispatch_su<NP>(pick_su(un, NP), [&]<int SU>() {
-                        hipLaunchKernelGGL((k_attn_in<NP, TQ, TV, SU, DG>), dim3(GW), dim3(MT), lds, s, d, L.attn_norm,
-                                           L.wq, L.wk, L.wv, g_qk, b);
+                        if (il == 0)
+                            hipLaunchKernelGGL((k_attn_in<NP, TQ, TV, SU, DG, true>), dim3(GW), dim3(MT), lds, s, d,
+                                               L.attn_norm, L.wq, L.wk, L.wv, g_qk, b, tok_embd, nblk);
+                        else
+                            hipLaunchKernelGGL((k_attn_in<NP, TQ, TV, SU, DG, false>), dim3(GW), dim3(MT), lds, s, d,
+                                               L.attn_norm, L.wq, L.wk, L.wv, g_qk, b, tok_embd, nblk);
                     });
                 };
                 if constexpr (TQ == 8) {
@@ -512,7 +557,7 @@ void launch_step_kernel(int which, const LlmDims &d, const LayerW *layers, int i
             dispatch_nt(d.n_embd, L.gate.type, [&]<int NP, int T>() {
                 dispatch_su<NP>(pick_su(max_wave_units(L.gate.rows, grid, NP, 2), NP), [&]<int SU>() {
                     hipLaunchKernelGGL((k_ffn_in<NP, T, SU, DG>), dim3(grid), dim3(MT), mv_lds(d.n_embd), s, d, L.ffn_norm,
-                                       L.gate, L.up, b);
+                                       L.gate, L.up, b, il == 0 ? 1 : 0);
                 });
             });
             break;
@@ -528,12 +573,14 @@ void launch_step_kernel(int which, const LlmDims &d, const LayerW *layers, int i
             });
             break;
         }
-        case 6:
+        case 6: {
+            const LlmDims dl = lm_dims(d);
             dispatch_nt(d.n_embd, lm.type, [&]<int NP, int T>() {
-                hipLaunchKernelGGL((k_lm_head<NP, T, DG>), dim3(lm_head_blocks(d)), dim3(MT), mv_lds(d.n_embd), s, d,
+                hipLaunchKernelGGL((k_lm_head<NP, T, DG>), dim3(lm_head_blocks(d)), dim3(MT), mv_lds(d.n_embd), s, dl,
                                    out_norm, lm, b);
             });
             break;
+        }
         case 7:
             hipLaunchKernelGGL(k_sample<DG>, dim3(1), dim3(ST), 0, s, d, tok_embd, lm_head_blocks(d), b);
             break;

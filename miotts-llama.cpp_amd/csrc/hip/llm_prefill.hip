@@ -723,7 +723,7 @@ void launch_batch_step(const LlmDims &d, const LayerW *layers, int n_layer, _Flo
                        const BatchBuffers &bb, int B, hipStream_t s) {
     launch_layers(d, layers, n_layer, kcache, vcache, pb, B, d.max_splits, s);
     launch_quant(d, 0, pb.x, d.n_embd, out_norm, lm.type != 8, pb, B, s);
-    const int nblk = lm_head_blocks(d);
+    const int nblk = matvec_grid(d, d.n_vocab);  // the batched lm_head keeps one workgroup per CU
     dispatch_nt(d.n_embd, lm.type, [&]<int NP, int T>() {
         allow_lds(k_bt_lm_head<NP, T>);
         hipLaunchKernelGGL((k_bt_lm_head<NP, T>), dim3(nblk), dim3(MT), batch_lm_head_lds(d, B), s, d, out_norm, lm,

@@ -148,7 +148,15 @@ int issue_step(mio_hip_llm *m, unsigned long long *tl = nullptr) {
             mio::launch_step_kernel(k, m->dims, m->layers.data(), il, m->kc, m->vc, m->out_norm, m->lm, m->tok, bufs(),
                                     s);
     mio::launch_step_kernel(6, m->dims, m->layers.data(), 0, m->kc, m->vc, m->out_norm, m->lm, m->tok, bufs(), s);
-    mio::launch_step_kernel(7, m->dims, m->layers.data(), 0, m->kc, m->vc, m->out_norm, m->lm, m->tok, bufs(), s);
+    return MIO_OK;
+}
+
+// The sampler of the last issued step (the step graph samples each token inside the next
+// step's layer-0 attn_in): leaves the state with no pending sample.
+int flush_sample(mio_hip_llm *m) {
+    mio::launch_step_kernel(7, m->dims, m->layers.data(), 0, m->kc, m->vc, m->out_norm, m->lm, m->tok, m->buf,
+                            m->d->stream);
+    MIO_HIP_CHECK(hipGetLastError());
     return MIO_OK;
 }
 
@@ -277,11 +285,11 @@ int llm_run(mio_hip_llm *m, int n_steps) {
     if (eager) {
         for (int i = 0; i < n; ++i)
             if ((rc = issue_step(m))) return rc;
-        return MIO_OK;
+        return flush_sample(m);
     }
     for (; n >= kGraphSteps; n -= kGraphSteps) MIO_HIP_CHECK(hipGraphLaunch(m->graph_n, m->d->stream));
     for (; n > 0; --n) MIO_HIP_CHECK(hipGraphLaunch(m->graph, m->d->stream));
-    return MIO_OK;
+    return flush_sample(m);
 }
 
 int llm_poll(mio_hip_llm *m, std::vector<int32_t> &out, bool *done) {
@@ -505,7 +513,7 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
     want(m->buf.h, D.n_ff);
     want(m->buf.logits, D.n_vocab);
     want(m->buf.part, (size_t)D.n_head * D.max_splits * (D.hd + 4));
-    want(m->buf.smp, 2 * std::max(mio::lm_head_blocks(D), D.n_wg) + 16);
+    want(m->buf.smp, 2 * std::max(mio::lm_head_blocks(D), 4 * D.n_wg) + 16);
     want(m->buf.st, 1);
     want(m->d_cfg, 1);
     m->max_steps = n_ctx;
@@ -1020,7 +1028,7 @@ extern "C" int mio_hip_llm_timeline(mio_hip_llm *m, uint64_t *out, int max_launc
     MIO_REQUIRE(m && out && n_launches && m->graph, MIO_ERR_INVALID, "llm_timeline: run generate/eval first");
     int rc = mio::bind(m->d);
     if (rc) return rc;
-    const int nl = m->n_layer * 5 + 2;
+    const int nl = m->n_layer * 5 + 1;
     MIO_REQUIRE(max_launches >= nl, MIO_ERR_INVALID, "llm_timeline: need %d launch slots", nl);
     hipStream_t s = m->d->stream;
     const size_t nslot = (size_t)nl * 256 * 8;

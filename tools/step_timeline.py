@@ -24,7 +24,7 @@ llm.generate([256, 257, 65, 258, 257], a.pos, 0.8, 1, allow=(m.SYNTH_SPEECH0, m.
              check_interval=50)
 t = llm.timeline()
 nl = t.shape[0]
-names = ["attn_in", "attention", "attn_out", "ffn_in", "ffn_down"] * ((nl - 2) // 5) + ["lm_head", "sample"]
+names = ["attn_in", "attention", "attn_out", "ffn_in", "ffn_down"] * ((nl - 1) // 5) + ["lm_head"]
 s0 = np.nanmin(t[:, :, 0], axis=1)
 s1 = np.nanmax(t[:, :, 0], axis=1)
 e0 = np.nanmin(t[:, :, 7], axis=1)
@@ -40,14 +40,14 @@ gap = np.r_[0.0, s0[1:] - e1[:-1]]
 print(f"step wall {e1[-1] - s0[0]:.1f} us over {nl} launches; kernel time {dur.sum():.1f} us, "
       f"gaps {gap[1:].sum():.1f} us (mean {gap[1:].mean():.2f}, min {gap[1:].min():.2f}, max {gap[1:].max():.2f})")
 print("  kernel      dur    gap-before  start-spread  end-spread  median-wg   wg:->m1  m1->m2  m2->end  last-m2")
-for k in ["attn_in", "attention", "attn_out", "ffn_in", "ffn_down", "lm_head", "sample"]:
+for k in ["attn_in", "attention", "attn_out", "ffn_in", "ffn_down", "lm_head"]:
     idx = [i for i, n in enumerate(names) if n == k]
     print(f"  {k:10s} {dur[idx].mean():6.2f} {gap[idx].mean():8.2f} {(s1 - s0)[idx].mean():12.2f} "
           f"{(e1 - e0)[idx].mean():11.2f} {wd[idx].mean():10.2f} {np.nanmean(ph1[idx]):9.2f} "
           f"{np.nanmean(ph2[idx]):7.2f} {np.nanmean(ph3[idx]):8.2f} {np.nanmean(m2[idx]):8.2f}")
 # every recorded mark (1-6) and the end, as median offsets from the workgroup's own start
 print("  kernel      " + " ".join(f"{'m' + str(k):>6s}" for k in range(1, 7)) + "    end   (us after workgroup start)")
-for k in ["attn_in", "attention", "attn_out", "ffn_in", "ffn_down", "lm_head", "sample"]:
+for k in ["attn_in", "attention", "attn_out", "ffn_in", "ffn_down", "lm_head"]:
     idx = [i for i, n in enumerate(names) if n == k]
     cols = []
     for j in list(range(1, 7)) + [7]:

@@ -25,22 +25,21 @@ for n_new in (30, 330, 630):
     tl = llm.timeline()
     nl = tl.shape[0]
     dur = np.nanmax(tl[:, :, 7], axis=1) - np.nanmin(tl[:, :, 0], axis=1)
-    per = {nm: round(float(dur[i:nl - 2:5].sum()), 1) for i, nm in enumerate(names)}
-    per["lm_head"] = round(float(dur[nl - 2]), 1)
-    per["sample"] = round(float(dur[nl - 1]), 1)
+    per = {nm: round(float(dur[i:nl - 1:5].sum()), 1) for i, nm in enumerate(names)}
+    per["lm_head"] = round(float(dur[nl - 1]), 1)
     per["wall"] = round(float(np.nanmax(tl[-1, :, 7]) - np.nanmin(tl[0, :, 0])), 1)
     # attention phases (mean over the layers' launches): first WG start -> mean mark 1 / 2 /
     # end, and the gap from the previous launch's last end to this launch's first start
-    att = tl[1:nl - 2:5]
+    att = tl[1:nl - 1:5]
     t0 = np.nanmin(att[:, :, 0], axis=1)
     per["att_m1"] = round(float(np.nanmean(np.nanmean(att[:, :, 1], axis=1) - t0)), 2)
     per["att_m2"] = round(float(np.nanmean(np.nanmean(att[:, :, 2], axis=1) - t0)), 2)
     per["att_end_mean"] = round(float(np.nanmean(np.nanmean(att[:, :, 7], axis=1) - t0)), 2)
     per["att_end_max"] = round(float(np.nanmean(np.nanmax(att[:, :, 7], axis=1) - t0)), 2)
     per["att_wgs"] = int(np.sum(~np.isnan(att[0, :, 0])))
-    prev_end = np.nanmax(tl[0:nl - 2:5][:, :, 7], axis=1)
+    prev_end = np.nanmax(tl[0:nl - 1:5][:, :, 7], axis=1)
     per["gap_before_att"] = round(float(np.nanmean(t0 - prev_end)), 2)
-    nxt = tl[2:nl - 2:5]
+    nxt = tl[2:nl - 1:5]
     per["gap_after_att"] = round(float(np.nanmean(np.nanmin(nxt[:, :, 0], axis=1) - np.nanmax(att[:, :, 7], axis=1))), 2)
     res[len(prompt) + n_new] = per
 print(json.dumps({"build": os.environ.get("MIO_BUILD_DIR", "build"), "per_pos": res}), flush=True)

@@ -23,7 +23,7 @@ llm.generate([256, 257, 65, 258, 257], a.pos, 0.8, 1, allow=(m.SYNTH_SPEECH0, m.
              check_interval=50)
 t = llm.timeline()
 nl = t.shape[0]
-names = ["attn_in", "attention", "attn_out", "ffn_in", "ffn_down"] * ((nl - 2) // 5) + ["lm_head", "sample"]
+names = ["attn_in", "attention", "attn_out", "ffn_in", "ffn_down"] * ((nl - 1) // 5) + ["lm_head"]
 for k in ["attn_in", "ffn_in", "lm_head"]:
     idx = [i for i, n in enumerate(names) if n == k]
     rel = t[idx][:, :, 1:8] - t[idx][:, :, 0:1]
