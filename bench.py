@@ -20,8 +20,8 @@ together by the batched engine on each rank (BASELINE configs[3], C4: `--preset 
 --utts-per-gpu 8 --gpus 8` = 64 utterances of the 2.6B Q8_0 model over 8 GPUs).
 
 roofline: the decode-step kernel with the largest in-graph time per token (step timeline,
-mio_hip_llm_timeline, right after the timed region, at the position the utterance ended
-on): achieved = its algorithmic bytes per launch (GGUF bytes of the matrices it streams +
+mio_hip_llm_timeline, after the timed region at decode position ~400 = the utterance's mean
+position and the PMC run's): achieved = its algorithmic bytes per launch (GGUF bytes of the matrices it streams +
 activations; attention: the F16 K/V rows of positions <= pos + q/k/v in + partial records
 out, mio_hip_llm_time_kernel) / its mean launch duration from HIP events around 40
 back-to-back launches on the runner's stream; peak = 8 TB/s HBM3E. `frac_in_graph` = the
@@ -45,6 +45,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "miotts-llama.cpp_amd", "python"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+ROOF_POS = 400  # decode position of the roofline timeline / kernel timings (and of the PMC run)
 KERNEL_NAMES = {0: "k_attn_in", 1: "k_attention", 2: "k_attn_out", 3: "k_ffn_in", 4: "k_ffn_down",
                 6: "k_lm_head"}
 PRESETS = {2: "MioTTS-0.1B Q8_0", 3: "MioTTS-1.7B Q4_K_M", 4: "MioTTS-2.6B Q8_0"}
@@ -280,7 +281,7 @@ def roofline(llm, preset):
             "step_weight_bytes": llm.weight_bytes(),
             "per_token_us": {k: round(sum(v), 1) for k, v in per_kernel.items()},
             "bytes_per_launch_all": bytes_of,
-            "note": "timeline taken at the end-of-utterance position; attention bytes at that position"}
+            "note": "timeline, events and attention bytes at decode position ~400 (as the PMC run)"}
 
 
 def main():
@@ -390,6 +391,9 @@ def main():
 
     roof = None
     if rank == 0 and not a.no_roofline and B == 1:
+        # roofline at decode position ~400, the utterance's mean attention length and the
+        # position of the PMC passes (tools/pmc_run.py)
+        llm.generate(prompt, max(1, ROOF_POS + 2 - len(prompt)), 0.8, 7, allow=allow, check_interval=1000)
         roof = roofline(llm, a.preset)
 
     steps_total = utt_per_rank
