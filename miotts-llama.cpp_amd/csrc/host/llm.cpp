@@ -64,6 +64,9 @@ struct mio_hip_llm {
     // generation state
     int n_prompt = 0, max_new = 0, steps_total = 0, steps_issued = 0;
     mio::SampleCfg cfg{};
+    // pinned host mirror of the state and the token ring (llm_poll: async copies, one sync)
+    mio::StepState *h_st = nullptr;
+    int *h_tokens = nullptr;
 
     ~mio_hip_llm() {
         if (d) hipSetDevice(d->dev);
@@ -73,6 +76,8 @@ struct mio_hip_llm {
         if (bt.graph_n) hipGraphExecDestroy(bt.graph_n);
         for (void *p : bt.allocs) hipFree(p);
         for (void *p : allocs) hipFree(p);
+        if (h_st) hipHostFree(h_st);
+        if (h_tokens) hipHostFree(h_tokens);
     }
 };
 
@@ -295,13 +300,18 @@ int llm_run(mio_hip_llm *m, int n_steps) {
 int llm_poll(mio_hip_llm *m, std::vector<int32_t> &out, bool *done) {
     int rc = mio::bind(m->d);
     if (rc) return rc;
-    StepState st{};
-    MIO_HIP_CHECK(hipMemcpyAsync(&st, m->buf.st, sizeof(st), hipMemcpyDeviceToHost, m->d->stream));
-    MIO_HIP_CHECK(hipStreamSynchronize(m->d->stream));
+    // the steps issued so far bound the ring slots written: copy state and slots together
+    // into pinned memory and wait once
     const int first = m->n_prompt - 1;
-    const int n = st.step > first ? st.step - first : 0;
-    out.resize(n);
-    if (n) MIO_HIP_CHECK(hipMemcpy(out.data(), m->d_tokens + first, (size_t)n * 4, hipMemcpyDeviceToHost));
+    const int hi = std::min(m->steps_issued, m->max_steps);
+    MIO_HIP_CHECK(hipMemcpyAsync(m->h_st, m->buf.st, sizeof(StepState), hipMemcpyDeviceToHost, m->d->stream));
+    if (hi > first)
+        MIO_HIP_CHECK(hipMemcpyAsync(m->h_tokens + first, m->d_tokens + first, (size_t)(hi - first) * 4,
+                                     hipMemcpyDeviceToHost, m->d->stream));
+    MIO_HIP_CHECK(hipStreamSynchronize(m->d->stream));
+    const StepState st = *m->h_st;
+    const int n = std::min(st.step, hi) > first ? std::min(st.step, hi) - first : 0;
+    out.assign(m->h_tokens + first, m->h_tokens + first + n);
     bool d = false;
     for (int i = 0; i < n; ++i)
         if (out[i] == m->cfg.eos0 || out[i] == m->cfg.eos1) {
@@ -517,6 +527,11 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
     want(m->buf.st, 1);
     want(m->d_cfg, 1);
     m->max_steps = n_ctx;
+    if (hipHostMalloc((void **)&m->h_st, sizeof(mio::StepState), hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc((void **)&m->h_tokens, (size_t)m->max_steps * 4, hipHostMallocDefault) != hipSuccess) {
+        mio::set_error("llm_load: pinned host buffers failed");
+        return fail(MIO_ERR_OOM);
+    }
     want(m->d_tokens, m->max_steps);
     want(m->d_force, m->max_steps);
     want(m->d_prompt, n_ctx);

@@ -46,6 +46,11 @@ int mo_codec_decode_stage(mo_codec *c, const int *codes, int T, const float *emb
 int mo_codec_decode(mo_codec *c, const int *codes, int T, const float *emb, float *spec);
 float mo_f16_round(float f);
 
+/* ---- streaming emission (test-to-speech.cpp:367-417,496-571), stream_ref.c ---- */
+long mo_stream_emit(mo_codec *c, const float *emb, const int *codes, int n_codes, int check_interval,
+                    int holdback, int min_commit, long chunk_samples, float *out, long out_cap,
+                    long long *chunks, long chunk_cap, long *n_chunks, int *n_decodes);
+
 /* ---- LLM decode step (llama_decode, test-to-speech.cpp:178-185) and sampler ---- */
 typedef struct mo_llm mo_llm;
 mo_llm *mo_llm_load(const char *path, int n_ctx);

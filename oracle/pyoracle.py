@@ -138,6 +138,29 @@ class Codec:
         return istft(spec, self.n_fft, self.n_fft, self.hop_length)
 
 
+def stream_emit(codec: "Codec", emb, codes, check_interval: int = 20, holdback: int = 32, min_commit: int = 24,
+                chunk_samples: int = 4096):
+    """Samples TestToSpeech::synthesize_stream emits for speech-only codes (oracle/stream_ref.c):
+    (samples, chunk sizes, full decodes)."""
+    codes = np.ascontiguousarray(codes, dtype=np.int32)
+    emb = np.ascontiguousarray(emb, dtype=np.float32)
+    cap = len(codes) * codec.samples_per_token + 16
+    out = np.zeros(cap, np.float32)
+    chunks = np.zeros(cap // max(1, min(chunk_samples, 64)) + 64, np.int64)
+    n_chunks, n_dec = ctypes.c_long(0), ctypes.c_int(0)
+    f = oracle().mo_stream_emit
+    f.restype = ctypes.c_long
+    f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                  ctypes.c_int, ctypes.c_long, ctypes.c_void_p, ctypes.c_long, ctypes.c_void_p, ctypes.c_long,
+                  ctypes.c_void_p, ctypes.c_void_p]
+    n = f(codec.h, emb.ctypes.data, codes.ctypes.data, len(codes), check_interval, holdback, min_commit,
+          chunk_samples, out.ctypes.data, cap, chunks.ctypes.data, len(chunks), ctypes.byref(n_chunks),
+          ctypes.byref(n_dec))
+    if n < 0:
+        raise RuntimeError("oracle stream_emit failed")
+    return out[:n].copy(), chunks[:n_chunks.value].copy(), n_dec.value
+
+
 class Llm:
     """Oracle decode step (oracle/llm_ref.c) + shared counter-based sampler."""
 

@@ -10,6 +10,9 @@ the way main.cpp / examples/stream-*.cpp are used.
   SURVEY 8c KAT 4) and prints every stream_bench.* key.
 * miotts-stream-compare --skip-llm: stream concat has the offline length and differs only
   in the crossfaded splice regions.
+* the samples synthesize_stream emits (holdback 32, commit step 24, llround sample mapping,
+  30 ms crossfade, chunking) equal the C restatement of test-to-speech.cpp:367-417,496-571
+  (oracle/stream_ref.c) driven by the oracle codec, within 1e-4 RMS.
 """
 import os
 import re
@@ -44,6 +47,7 @@ def files(tmp_path_factory):
     d = tmp_path_factory.mktemp("cli")
     return {"llm": m.synth_llm(str(d / "llm1.gguf"), 1, 1),
             "codec": m.synth_codec(str(d / "codec.gguf"), 0, 1),
+            "codec_tiny": m.synth_codec(str(d / "codec_tiny.gguf"), 1, 1),
             "voice": m.synth_voice(str(d / "voice.emb.gguf"), 7),
             "dir": d}
 
@@ -127,3 +131,26 @@ def test_stream_benchmark_1p7b_700_tokens(files, synth_llm_path):
     assert int(r["stream_bench.decoded_codes"]) == 7160
     assert int(r["stream_bench.emitted_samples"]) == 700 * 1764
     print({k: r[k] for k in r if k.startswith("stream_bench.")})
+
+
+@pytest.mark.parametrize("n,chunk", [(100, 4096), (141, 1000)])
+def test_stream_emission_matches_restatement(files, n, chunk):
+    """Everything synthesize_stream hands its callback (LLM speech-only, tiny codec) against
+    oracle/stream_ref.c over the same codes: identical chunk sizes, samples within 1e-4 RMS."""
+    prefix = str(files["dir"] / f"stream_{n}_{chunk}")
+    out = run(["miotts-stream-benchmark", "-m", files["llm"], "-c", files["codec_tiny"], "-v", files["voice"],
+               "-p", "こんにちは、今日はいい天気ですね。", "--max-tokens", n, "--speech-only", "--ignore-eos",
+               "--chunk-samples", chunk, "--dump-stream", prefix])
+    r = kv(out)
+    got = np.fromfile(prefix + ".f32", np.float32)
+    chunks = np.fromfile(prefix + ".chunks.i64", np.int64)
+    codes = np.fromfile(prefix + ".codes.i32", np.int32)
+    assert codes.size == n and int(r["stream_bench.llm_tokens"]) == n
+    oc = pyoracle.Codec(files["codec_tiny"])
+    ref, ref_chunks, n_dec = pyoracle.stream_emit(oc, m.read_voice(files["voice"]), codes, 20, 32, 24, chunk)
+    assert int(r["stream_bench.decode_calls"]) == n_dec
+    assert chunks.tolist() == ref_chunks.tolist()
+    assert got.size == ref.size == n * oc.samples_per_token
+    d = got.astype(np.float64) - ref
+    rms = float(np.sqrt(np.mean(d * d)))
+    assert rms <= 1e-4 and float(np.abs(d).max()) <= 1e-3, (rms, float(np.abs(d).max()))

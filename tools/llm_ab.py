@@ -20,11 +20,12 @@ dev = m.Device(0)
 llm = m.Llm(dev, llm_path, 2048)
 prompt = bench.prompt_tokens(bench.PROMPT)
 allow = (m.SYNTH_SPEECH0, m.SYNTH_SPEECH0 + 12800)
-llm.generate(prompt, 700, 0.8, 1, allow=allow, check_interval=20)
+CI = int(os.environ.get("AB_CI", 20))
+llm.generate(prompt, 700, 0.8, 1, allow=allow, check_interval=CI)
 ts = []
 for k in range(K):
     t0 = time.perf_counter()
-    llm.generate(prompt, 700, 0.8, 2 + k, allow=allow, check_interval=20)
+    llm.generate(prompt, 700, 0.8, 2 + k, allow=allow, check_interval=CI)
     ts.append(time.perf_counter() - t0)
 ev = {}
 for which, nm in ((0, "attn_in"), (1, "attention"), (2, "attn_out"), (3, "ffn_in"), (4, "ffn_down"), (6, "lm_head")):

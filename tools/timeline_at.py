@@ -20,7 +20,7 @@ prompt = bench.prompt_tokens(bench.PROMPT)
 allow = (m.SYNTH_SPEECH0, m.SYNTH_SPEECH0 + 12800)
 names = ["attn_in", "attention", "attn_out", "ffn_in", "ffn_down"]
 res = {}
-for n_new in (30, 330, 630):
+for n_new in [int(x) for x in os.environ.get('TL_NEW', '30,330,630').split(',')]:
     llm.generate(prompt, n_new, 0.8, 1, allow=allow, check_interval=20)
     tl = llm.timeline()
     nl = tl.shape[0]
@@ -33,7 +33,19 @@ for n_new in (30, 330, 630):
     att = tl[1:nl - 1:5]
     t0 = np.nanmin(att[:, :, 0], axis=1)
     per["att_m1"] = round(float(np.nanmean(np.nanmean(att[:, :, 1], axis=1) - t0)), 2)
-    per["att_m2"] = round(float(np.nanmean(np.nanmean(att[:, :, 2], axis=1) - t0)), 2)
+    for k in (2, 3, 4, 5, 6):
+        per[f"att_m{k}"] = round(float(np.nanmean(np.nanmean(att[:, :, k], axis=1) - t0)), 2)
+    ao = tl[2:nl - 1:5]  # attn_out: mark 1 = first weights issued, 2 = merge + quant done
+    a0 = np.nanmin(ao[:, :, 0], axis=1)
+    for k in (1, 2):
+        per[f"ao_m{k}"] = round(float(np.nanmean(np.nanmean(ao[:, :, k], axis=1) - a0)), 2)
+    for i, nm in enumerate(names):  # every kernel: mean mark 2 (prologue done) after its first start
+        kk = tl[i:nl - 1:5]
+        k0 = np.nanmin(kk[:, :, 0], axis=1)
+        per[f"{nm}_m2"] = round(float(np.nanmean(np.nanmean(kk[:, :, 2], axis=1) - k0)), 2)
+        per[f"{nm}_end"] = round(float(np.nanmean(np.nanmean(kk[:, :, 7], axis=1) - k0)), 2)
+    per["ao_end_mean"] = round(float(np.nanmean(np.nanmean(ao[:, :, 7], axis=1) - a0)), 2)
+    per["ao_end_max"] = round(float(np.nanmean(np.nanmax(ao[:, :, 7], axis=1) - a0)), 2)
     per["att_end_mean"] = round(float(np.nanmean(np.nanmean(att[:, :, 7], axis=1) - t0)), 2)
     per["att_end_max"] = round(float(np.nanmean(np.nanmax(att[:, :, 7], axis=1) - t0)), 2)
     per["att_wgs"] = int(np.sum(~np.isnan(att[0, :, 0])))
