@@ -320,8 +320,12 @@ def main():
     llm_path, codec_path, voice_path = ensure_files(a.workdir, a.preset, rank, barrier)
     n_dev = m.device_count()
     dev = m.Device(local_rank % n_dev)  # ranks share a GPU only when there are fewer GPUs than ranks
+    t_load = time.perf_counter()
     llm = m.Llm(dev, llm_path, 2048)
+    t_llm = time.perf_counter()
     codec = m.Codec(dev, codec_path)
+    load = {"llm_ms": round(llm.load_ms(), 1), "llm_wall_ms": round((t_llm - t_load) * 1e3, 1),
+            "codec_wall_ms": round((time.perf_counter() - t_llm) * 1e3, 1), "llm_bytes": llm.weight_bytes()}
     emb = m.read_voice(voice_path)
     prompt = prompt_tokens(PROMPT)
     allow = (m.SYNTH_SPEECH0, m.SYNTH_SPEECH0 + 12800)
@@ -419,6 +423,7 @@ def main():
                    "model": model, "global_batch": world * (B if B > 1 else a.utts_per_step),
                    "seq_len": a.tokens, "parallelism": f"utterance-sharded x{world} (no collective)",
                    "devices_visible": n_dev},
+        "load_ms": load,
         "stage_ms": {**{k: round(v / steps_total, 3) for k, v in stage.items()},
                      "pcm_finish_ms": pcm_finish_ms},
         "llm_ms_per_token": round(stage["llm_ms"] / steps_total / a.tokens, 4),

@@ -34,6 +34,10 @@ extern "C" {
 /* buffer-location flags */
 #define MIO_IN_DEVICE 1u
 #define MIO_OUT_DEVICE 2u
+/* codec decode: reuse the prenet rows of the previous MIO_CODEC_INCREMENTAL decode of the
+ * same handle for the shared code prefix whose receptive field was complete (streaming
+ * re-decodes, test-to-speech.cpp:526-529; host codes only, otherwise ignored) */
+#define MIO_CODEC_INCREMENTAL 4u
 
 typedef struct mio_hip_device mio_hip_device;
 typedef struct mio_hip_istft mio_hip_istft;
@@ -176,6 +180,11 @@ int mio_hip_llm_trace_kernel(mio_hip_llm *m, int which, uint64_t *out);
  * prologue steps in -DMIO_TL_DIAG builds.
  * Advances the decode state. */
 int mio_hip_llm_timeline(mio_hip_llm *m, uint64_t *out, int max_launches, int *n_launches);
+/* Wall time (ms) of mio_hip_llm_load: GGUF mmap, re-layout into pinned staging buffers,
+ * asynchronous copies into the HBM weight arena (double-buffered). */
+int mio_hip_llm_load_ms(const mio_hip_llm *m, double *ms);
+/* Prenet rows the last mio_hip_codec_decode_pcm took from the incremental cache. */
+int mio_hip_codec_last_reused(const mio_hip_codec *c, int *rows);
 /* Stage times (ms, HIP events) of the last mio_hip_codec_decode_pcm: [0] codec, [1] iSTFT. */
 int mio_hip_codec_last_timings(const mio_hip_codec *c, float *ms2);
 

@@ -76,12 +76,20 @@ struct mio_hip_codec {
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
     float last_ms[2] = {0, 0};
     bool timed = false;
+    // streaming prenet cache (MIO_CODEC_INCREMENTAL): prenet + projection rows [0, pc_exact)
+    // of the previous incremental decode, whose ±pre_layers*(pre_win/2) receptive field lay
+    // inside that decode (so they equal the full-context rows), and that decode's codes
+    float *pc = nullptr;
+    int pc_cap = 0, pc_exact = 0;
+    std::vector<int32_t> pc_codes;
+    int pc_last_reused = 0;  // rows the last decode took from the cache (diagnostic)
 
     ~mio_hip_codec() {
         if (d) hipSetDevice(d->dev);
         for (void *p : allocs) hipFree(p);
         if (rope) hipFree(rope);
         if (ws) hipFree(ws);
+        if (pc) hipFree(pc);
         if (ist) mio_hip_istft_destroy(ist);
         for (auto e : ev)
             if (e) hipEventDestroy(e);
@@ -216,7 +224,7 @@ struct Ws {
     int Lf;
 };
 
-int plan_ws(mio_hip_codec *c, int T, Ws &w, bool alloc) {
+int plan_ws(mio_hip_codec *c, int T, Ws &w, bool alloc, size_t *bytes = nullptr) {
     const int S = 2 * T;
     size_t off = 0;
     std::vector<size_t> sizes;
@@ -265,15 +273,23 @@ int plan_ws(mio_hip_codec *c, int T, Ws &w, bool alloc) {
     F(&w.emb, (size_t)c->adaln);
     float *codes_f = nullptr;
     F(&codes_f, (size_t)T);
+    if (bytes) *bytes = off;
     if (alloc && off > c->ws_cap) {
+        // sized for at least 1024 codes: streaming re-decodes grow T every call, and each
+        // re-allocation (hipFree) would wait for whatever else runs on the device
+        size_t want = off;
+        if (T < 1024) {
+            Ws big;
+            plan_ws(c, 1024, big, false, &want);
+        }
         if (c->ws) hipFree(c->ws);
         c->ws = nullptr;
         c->ws_cap = 0;
-        if (hipMalloc(&c->ws, off) != hipSuccess) {
-            mio::set_error("miocodec: workspace of %zu bytes failed", off);
+        if (hipMalloc(&c->ws, want) != hipSuccess) {
+            mio::set_error("miocodec: workspace of %zu bytes failed", want);
             return MIO_ERR_OOM;
         }
-        c->ws_cap = off;
+        c->ws_cap = want;
     }
     for (auto &s : slots) *s.first = (float *)(c->ws + s.second);
     w.codes = (int *)codes_f;
@@ -323,10 +339,18 @@ void resnet(mio_hip_codec *c, const ResW &r, float *x, float *t, int L, int C, c
     mio::launch_conv_f16(a, s);
 }
 
+// Prenet receptive field in codes: each layer's banded attention reaches pre_win/2 each way.
+int prenet_radius(const mio_hip_codec *c) { return c->pre_layers * (c->pre_win / 2); }
+
 // Runs the decoder; if stop_stage >= 0, returns after that stage with *stage_buf/rows/cols set.
+// cached > 0: rows [0, cached) of the prenet output are taken from c->pc; the prenet then runs
+// only over codes [cached - radius, T) (RoPE at absolute positions), whose rows from `cached`
+// on have their whole receptive field inside that window.
 int run_decode(mio_hip_codec *c, Ws &w, hipStream_t s, int stop_stage, const float **stage_buf,
-               int *rows, int *cols) {
+               int *rows, int *cols, int cached = 0) {
     const int T = w.T, S = w.S, Dp = c->pre_dim, Dd = c->dec_dim;
+    const int s0 = cached > 0 ? std::max(0, cached - prenet_radius(c)) : 0, Tw = T - s0;
+    const float2 *rope_w = c->rope + (size_t)s0 * 32;  // [pos][hd/2], hd = 64
     int stage = 0;
     auto done = [&](const float *buf, int r, int cc) {
         if (stage == stop_stage) {
@@ -336,26 +360,29 @@ int run_decode(mio_hip_codec *c, Ws &w, hipStream_t s, int stop_stage, const flo
         ++stage;
         return false;
     };
-    // 1. embedding (:599-600)
-    mio::launch_embed(c->tok, w.codes, T, Dp, w.xT, s);
-    if (done(w.xT, T, Dp)) return MIO_OK;
-    // 2. prenet (:604-618)
+    // 1. embedding (:599-600) of codes [s0, T)
+    mio::launch_embed(c->tok, w.codes + s0, Tw, Dp, w.xT, s);
+    if (done(w.xT, Tw, Dp)) return MIO_OK;
+    // 2. prenet (:604-618) over the window's Tw rows
     for (int i = 0; i < c->pre_layers; ++i) {
         const PreW &p = c->pre[i];
-        mio::launch_rownorm(w.xT, w.hT, T, Dp, c->eps, 1, p.ln1_w, p.ln1_b, s);
-        mio::launch_gemm_f32(gemm(w.hT, Dp, T, p.qkv, 3 * Dp, w.qkvT, 3 * Dp), mio::EPI_STORE, s);
-        mio::launch_band_attention(w.qkvT, w.aT, T, c->pre_heads, c->pre_win, c->rope, s);
-        mio::launch_gemm_f32(gemm(w.aT, Dp, T, p.wo, Dp, w.xT, Dp), mio::EPI_RESID, s);
-        mio::launch_rownorm(w.xT, w.hT, T, Dp, c->eps, 1, p.ln2_w, p.ln2_b, s);
-        mio::launch_gemm_f32(gemm(w.hT, Dp, T, p.gu, 2 * c->pre_ff, w.fT, c->pre_ff), mio::EPI_SWIGLU, s);
-        mio::launch_gemm_f32(gemm(w.fT, c->pre_ff, T, p.wd, Dp, w.xT, Dp), mio::EPI_RESID, s);
+        mio::launch_rownorm(w.xT, w.hT, Tw, Dp, c->eps, 1, p.ln1_w, p.ln1_b, s);
+        mio::launch_gemm_f32(gemm(w.hT, Dp, Tw, p.qkv, 3 * Dp, w.qkvT, 3 * Dp), mio::EPI_STORE, s);
+        mio::launch_band_attention(w.qkvT, w.aT, Tw, c->pre_heads, c->pre_win, rope_w, s);
+        mio::launch_gemm_f32(gemm(w.aT, Dp, Tw, p.wo, Dp, w.xT, Dp), mio::EPI_RESID, s);
+        mio::launch_rownorm(w.xT, w.hT, Tw, Dp, c->eps, 1, p.ln2_w, p.ln2_b, s);
+        mio::launch_gemm_f32(gemm(w.hT, Dp, Tw, p.gu, 2 * c->pre_ff, w.fT, c->pre_ff), mio::EPI_SWIGLU, s);
+        mio::launch_gemm_f32(gemm(w.fT, c->pre_ff, Tw, p.wd, Dp, w.xT, Dp), mio::EPI_RESID, s);
     }
-    mio::launch_rownorm(w.xT, w.hT, T, Dp, c->eps, 1, c->pre_norm_w, c->pre_norm_b, s);
+    mio::launch_rownorm(w.xT, w.hT, Tw, Dp, c->eps, 1, c->pre_norm_w, c->pre_norm_b, s);
     {
-        mio::GemmArgs g = gemm(w.hT, Dp, T, c->pre_out_w, Dd, w.yT, Dd);
+        mio::GemmArgs g = gemm(w.hT, Dp, Tw, c->pre_out_w, Dd, w.yT + (size_t)s0 * Dd, Dd);
         g.bias = c->pre_out_b;
         mio::launch_gemm_f32(g, mio::EPI_STORE, s);
     }
+    // the cached rows replace the window's left edge (whose context was cut)
+    if (cached > 0)
+        MIO_HIP_CHECK(hipMemcpyAsync(w.yT, c->pc, (size_t)cached * Dd * 4, hipMemcpyDeviceToDevice, s));
     if (done(w.yT, T, Dd)) return MIO_OK;
     // 3. wave_upsample ConvT k=2 s=2 (:622-626): one GEMM, N = 2*Dd, remapped rows
     {
@@ -732,8 +759,37 @@ extern "C" int mio_hip_codec_decode_pcm(mio_hip_codec *c, const int32_t *codes, 
     int r = 0, cc = 0;
     if (!c->ev[0])
         for (auto &e : c->ev) MIO_HIP_CHECK(hipEventCreate(&e));
+    const bool incr = (flags & MIO_CODEC_INCREMENTAL) && !(flags & MIO_IN_DEVICE);
+    int cached = 0;
+    if (incr) {
+        int prefix = 0;
+        const int lim = std::min(n_codes, (int)c->pc_codes.size());
+        while (prefix < lim && c->pc_codes[prefix] == codes[prefix]) ++prefix;
+        // a cached row is valid while every code of its receptive field is unchanged
+        cached = std::min(c->pc_exact, std::max(0, prefix - prenet_radius(c)));
+        if (n_codes > c->pc_cap) {  // grow the cache before this decode reads it
+            float *np = nullptr;
+            const int cap = std::max(2 * n_codes, 1024);
+            MIO_HIP_CHECK(hipMalloc(&np, (size_t)cap * c->dec_dim * 4));
+            if (cached > 0)
+                MIO_HIP_CHECK(hipMemcpyAsync(np, c->pc, (size_t)cached * c->dec_dim * 4, hipMemcpyDeviceToDevice, s));
+            MIO_HIP_CHECK(hipStreamSynchronize(s));
+            if (c->pc) hipFree(c->pc);
+            c->pc = np;
+            c->pc_cap = cap;
+        }
+    }
+    c->pc_last_reused = cached;
     MIO_HIP_CHECK(hipEventRecord(c->ev[0], s));
-    if ((rc = run_decode(c, w, s, 1 << 20, &buf, &r, &cc))) return rc;
+    if ((rc = run_decode(c, w, s, 1 << 20, &buf, &r, &cc, cached))) return rc;
+    if (incr) {  // rows whose receptive field this decode held completely become the cache
+        const int exact = std::max(0, n_codes - prenet_radius(c));
+        if (exact > cached)
+            MIO_HIP_CHECK(hipMemcpyAsync(c->pc + (size_t)cached * c->dec_dim, w.yT + (size_t)cached * c->dec_dim,
+                                         (size_t)(exact - cached) * c->dec_dim * 4, hipMemcpyDeviceToDevice, s));
+        c->pc_exact = exact;
+        c->pc_codes.assign(codes, codes + n_codes);
+    }
     MIO_HIP_CHECK(hipEventRecord(c->ev[1], s));
     int len = 0;
     if ((rc = mio_hip_istft_out_len(c->ist, w.Lf, c->hop, &len))) return rc;
@@ -748,6 +804,12 @@ extern "C" int mio_hip_codec_decode_pcm(mio_hip_codec *c, const int32_t *codes, 
         MIO_HIP_CHECK(hipMemcpyAsync(out_pcm, w.pcm, (size_t)len * 4, hipMemcpyDeviceToHost, s));
         MIO_HIP_CHECK(hipStreamSynchronize(s));
     }
+    return MIO_OK;
+}
+
+extern "C" int mio_hip_codec_last_reused(const mio_hip_codec *c, int *rows) {
+    MIO_REQUIRE(c && rows, MIO_ERR_INVALID, "codec_last_reused: null");
+    *rows = c->pc_last_reused;
     return MIO_OK;
 }
 

@@ -7,6 +7,7 @@
 #include "llm.h"
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -19,6 +20,9 @@
 #include "llm_kernels.h"
 #include "prefetch.h"
 #include "quant.h"
+
+struct Stager;
+void stager_free(Stager *s);
 
 struct mio_hip_llm {
     mio_hip_device *d = nullptr;
@@ -64,6 +68,8 @@ struct mio_hip_llm {
     // generation state
     int n_prompt = 0, max_new = 0, steps_total = 0, steps_issued = 0;
     mio::SampleCfg cfg{};
+    double load_ms = 0.0;  // wall time of mio_hip_llm_load (GGUF mmap -> HBM arena)
+    Stager *stager = nullptr;  // weight upload staging (load only)
     // pinned host mirror of the state and the token ring (llm_poll: async copies, one sync)
     mio::StepState *h_st = nullptr;
     int *h_tokens = nullptr;
@@ -76,10 +82,64 @@ struct mio_hip_llm {
         if (bt.graph_n) hipGraphExecDestroy(bt.graph_n);
         for (void *p : bt.allocs) hipFree(p);
         for (void *p : allocs) hipFree(p);
+        stager_free(stager);
         if (h_st) hipHostFree(h_st);
         if (h_tokens) hipHostFree(h_tokens);
     }
 };
+
+namespace {
+
+}  // namespace
+
+// Host -> HBM weight upload: every matrix is re-laid out (to_split) from the mmapped GGUF
+// straight into one of two pinned staging buffers while the other buffer's DMA copy runs
+// (hipMemcpyAsync on a load stream), instead of a pageable vector + a synchronous copy.
+struct Stager {
+    hipStream_t s = nullptr;
+    void *buf[2] = {nullptr, nullptr};
+    size_t cap[2] = {0, 0};
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    bool used[2] = {false, false};
+    int cur = 0;
+
+    bool init() {
+        return hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess &&
+               hipEventCreateWithFlags(&ev[0], hipEventDisableTiming) == hipSuccess &&
+               hipEventCreateWithFlags(&ev[1], hipEventDisableTiming) == hipSuccess;
+    }
+    // a staging buffer of >= bytes whose previous copy has finished
+    uint8_t *acquire(size_t bytes) {
+        const int i = cur;
+        if (used[i] && hipEventSynchronize(ev[i]) != hipSuccess) return nullptr;
+        if (cap[i] < bytes) {
+            if (buf[i]) hipHostFree(buf[i]);
+            buf[i] = nullptr, cap[i] = 0;
+            const size_t want = std::max(bytes, (size_t)64 << 20);
+            if (hipHostMalloc(&buf[i], want, hipHostMallocDefault) != hipSuccess) return nullptr;
+            cap[i] = want;
+        }
+        return (uint8_t *)buf[i];
+    }
+    bool submit(void *dst, size_t bytes) {
+        const int i = cur;
+        cur ^= 1;
+        used[i] = true;
+        return hipMemcpyAsync(dst, buf[i], bytes, hipMemcpyHostToDevice, s) == hipSuccess &&
+               hipEventRecord(ev[i], s) == hipSuccess;
+    }
+    bool finish() { return !s || hipStreamSynchronize(s) == hipSuccess; }
+    ~Stager() {
+        finish();
+        for (int i = 0; i < 2; ++i) {
+            if (buf[i]) hipHostFree(buf[i]);
+            if (ev[i]) hipEventDestroy(ev[i]);
+        }
+        if (s) hipStreamDestroy(s);
+    }
+};
+
+void stager_free(Stager *s) { delete s; }
 
 namespace {
 
@@ -103,14 +163,18 @@ bool upload_qmat(mio_hip_llm *m, const mio::GgufTensor *t, mio::QMat &q) {
         return false;
     }
     const mio::SplitLayout L = mio::split_layout(t->type, t->ne[1], t->ne[0]);
-    std::vector<uint8_t> host(L.bytes);
-    if (!mio::to_split(t->type, t->data, t->ne[1], t->ne[0], host.data())) {
+    const auto it = m->arena_off.find(t->name);
+    uint8_t *dp = (m->arena && it != m->arena_off.end()) ? m->arena + it->second : dalloc<uint8_t>(m, L.bytes);
+    uint8_t *host = dp && m->stager ? m->stager->acquire(L.bytes) : nullptr;
+    if (!host) {
+        mio::set_error("llm: staging / device buffer for %s failed", t->name.c_str());
+        return false;
+    }
+    if (!mio::to_split(t->type, t->data, t->ne[1], t->ne[0], host)) {
         mio::set_error("llm: re-layout of %s failed", t->name.c_str());
         return false;
     }
-    const auto it = m->arena_off.find(t->name);
-    uint8_t *dp = (m->arena && it != m->arena_off.end()) ? m->arena + it->second : dalloc<uint8_t>(m, L.bytes);
-    if (!dp || hipMemcpy(dp, host.data(), L.bytes, hipMemcpyHostToDevice) != hipSuccess) {
+    if (!m->stager->submit(dp, L.bytes)) {
         mio::set_error("llm: upload of %s failed", t->name.c_str());
         return false;
     }
@@ -330,6 +394,7 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
     if (n_ctx <= 0) n_ctx = 2048;  // test-to-speech.cpp:104
     int rc = mio::bind(d);
     if (rc) return rc;
+    const auto t_load0 = std::chrono::steady_clock::now();
     mio::GgufFile g;
     if (!g.open(path)) return MIO_ERR_IO;
     const std::string arch = g.get_str("general.architecture");
@@ -356,6 +421,12 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
     }
     auto *m = new mio_hip_llm();
     m->d = d;
+    m->stager = new Stager();
+    if (!m->stager->init()) {
+        delete m;
+        mio::set_error("llm_load: staging stream failed");
+        return MIO_ERR_HIP;
+    }
     auto fail = [&](int code) {
         delete m;
         return code;
@@ -578,12 +649,22 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
     }
     m->buf.rope = dr;
     m->pf.rope = dr;
-    // every memset / copy above ran on the null stream; the runner's stream is non-blocking
-    if (hipDeviceSynchronize() != hipSuccess) {
+    // every memset / copy above ran on the null stream or the staging stream; the runner's
+    // stream is non-blocking
+    if (!m->stager->finish() || hipDeviceSynchronize() != hipSuccess) {
         mio::set_error("llm_load: device synchronize failed");
         return fail(MIO_ERR_HIP);
     }
+    delete m->stager;
+    m->stager = nullptr;
+    m->load_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_load0).count();
     *out = m;
+    return MIO_OK;
+}
+
+extern "C" int mio_hip_llm_load_ms(const mio_hip_llm *m, double *ms) {
+    MIO_REQUIRE(m && ms, MIO_ERR_INVALID, "llm_load_ms: null");
+    *ms = m->load_ms;
     return MIO_OK;
 }
 

@@ -231,8 +231,11 @@ struct TestToSpeech::Impl {
     // PCM of the last decode in HBM (f32) and its PCM16 image (synthesize_to_file)
     void *d_pcm = nullptr, *d_pcm16 = nullptr;
     size_t pcm_cap = 0, pcm16_cap = 0;
+    // streaming decodes run on their own stream, beside the LLM's next check interval
+    hipStream_t cstream = nullptr;
 
     ~Impl() {
+        if (cstream) hipStreamDestroy(cstream);
         if (llm) mio_hip_llm_free(llm);
         if (dev && d_pcm) mio_hip_free(dev, d_pcm);
         if (dev && d_pcm16) mio_hip_free(dev, d_pcm16);
@@ -241,6 +244,7 @@ struct TestToSpeech::Impl {
 
     bool ensure(void *&p, size_t &cap, size_t bytes) {
         if (cap >= bytes) return true;
+        bytes = std::max(bytes, 2 * cap);  // geometric growth: a free waits for the device
         if (p) mio_hip_free(dev, p);
         p = nullptr, cap = 0;
         if (mio_hip_malloc(dev, bytes, &p) != MIO_OK) {
@@ -272,11 +276,14 @@ struct TestToSpeech::Impl {
 
     // codes -> PCM in HBM (d_pcm, *len samples): codec + fused iSTFT, stage seconds from GPU
     // events
+    // incremental: streaming re-decodes reuse the prenet rows of the previous one
+    // (MIO_CODEC_INCREMENTAL; the output equals a full decode up to f32 summation order)
     bool decode_codes_dev(const VoiceModel &voice, const std::vector<int> &codes, int *len, double *codec_sec,
-                          double *istft_sec) {
+                          double *istft_sec, bool incremental = false, hipStream_t stream = nullptr) {
         if (!ensure(d_pcm, pcm_cap, (size_t)codes.size() * spt * sizeof(float) + 64)) return false;
+        const unsigned flags = MIO_OUT_DEVICE | (incremental ? MIO_CODEC_INCREMENTAL : 0u);
         if (mio_hip_codec_decode_pcm(codec->codec, codes.data(), (int)codes.size(), voice.embedding().data(),
-                                     (float *)d_pcm, len, MIO_OUT_DEVICE, nullptr) != MIO_OK) {
+                                     (float *)d_pcm, len, flags, stream) != MIO_OK) {
             fprintf(stderr, "TestToSpeech: codec decode failed: %s\n", mio_hip_last_error());
             return false;
         }
@@ -290,10 +297,22 @@ struct TestToSpeech::Impl {
 
     // codes -> host PCM; the peak normalisation of test-to-speech.cpp:232-243 (when asked)
     // runs on the device before the copy (mio_hip_pcm_normalize, bit-exact with the host loop)
+    // stream (optional): decode and copy on that stream (the streaming path's codec stream)
     bool decode_codes(const VoiceModel &voice, const std::vector<int> &codes, std::vector<float> &pcm,
-                      double *codec_sec, double *istft_sec, bool normalize = false) {
+                      double *codec_sec, double *istft_sec, bool normalize = false, bool incremental = false,
+                      hipStream_t stream = nullptr) {
         int len = 0;
-        if (!decode_codes_dev(voice, codes, &len, codec_sec, istft_sec)) return false;
+        if (!decode_codes_dev(voice, codes, &len, codec_sec, istft_sec, incremental, stream)) return false;
+        if (stream) {
+            pcm.resize(len);
+            if (len && (hipMemcpyAsync(pcm.data(), d_pcm, (size_t)len * sizeof(float), hipMemcpyDeviceToHost,
+                                       stream) != hipSuccess ||
+                        hipStreamSynchronize(stream) != hipSuccess)) {
+                fprintf(stderr, "TestToSpeech: PCM copy failed\n");
+                return false;
+            }
+            return true;
+        }
         if (normalize && mio_hip_pcm_normalize(dev, (const float *)d_pcm, len, (float *)d_pcm, nullptr, nullptr)) {
             fprintf(stderr, "TestToSpeech: peak normalisation failed: %s\n", mio_hip_last_error());
             return false;
@@ -534,7 +553,8 @@ bool TestToSpeech::synthesize_stream_profiled(const VoiceModel &voice, const std
         if (!policy.plan(codes.size(), final_, &target))
             return (final_ && target <= committed) ? call(nullptr, 0, true) : true;
         std::vector<float> audio;
-        if (!I.decode_codes(voice, codes, audio, &profile.codec_sec, &profile.istft_sec)) return false;
+        if (!I.decode_codes(voice, codes, audio, &profile.codec_sec, &profile.istft_sec, false, true, I.cstream))
+            return false;
         profile.decode_calls++;
         profile.decoded_codes += codes.size();
         const double per_code = (double)audio.size() / (double)codes.size();
@@ -557,9 +577,19 @@ bool TestToSpeech::synthesize_stream_profiled(const VoiceModel &voice, const std
     std::vector<int32_t> toks;
     size_t consumed = 0;
     bool done = false;
+    // the codec works on its own stream: each check's re-decode runs beside the LLM's next
+    // kCheck steps, which are enqueued before it (same tokens, same emitted samples)
+    if (!I.cstream && hipStreamCreateWithFlags(&I.cstream, hipStreamNonBlocking) != hipSuccess) {
+        fprintf(stderr, "TestToSpeech: codec stream creation failed\n");
+        return false;
+    }
+    if (mio::llm_run(I.llm, kCheck)) {
+        fprintf(stderr, "TestToSpeech: decode failed: %s\n", mio::last_error());
+        return false;
+    }
     while (!done && ok) {
         const auto ta = clk::now();
-        if (mio::llm_run(I.llm, kCheck) || mio::llm_poll(I.llm, toks, &done)) {
+        if (mio::llm_poll(I.llm, toks, &done) || (!done && mio::llm_run(I.llm, kCheck))) {
             fprintf(stderr, "TestToSpeech: decode failed: %s\n", mio::last_error());
             ok = false;
             break;

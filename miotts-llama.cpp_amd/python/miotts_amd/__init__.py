@@ -21,6 +21,7 @@ INCLUDE_DIR = os.path.join(REPO_ROOT, "include")
 
 MIO_IN_DEVICE = 1
 MIO_OUT_DEVICE = 2
+MIO_CODEC_INCREMENTAL = 4
 
 _lib: Optional[ctypes.CDLL] = None
 
@@ -97,6 +98,8 @@ def _declare(L: ctypes.CDLL) -> None:
         "mio_token_piece": (c_int, [_vp, ctypes.c_int32, ctypes.c_char_p, c_int, ctypes.POINTER(c_int)]),
         "mio_hip_llm_timeline": (c_int, [_vp, _vp, c_int, ctypes.POINTER(c_int)]),
         "mio_hip_codec_last_timings": (c_int, [_vp, _f32p]),
+        "mio_hip_codec_last_reused": (c_int, [_vp, ctypes.POINTER(c_int)]),
+        "mio_hip_llm_load_ms": (c_int, [_vp, ctypes.POINTER(ctypes.c_double)]),
         "mio_hip_debug_matvec": (c_int, [_vp, ctypes.c_uint32, _vp, c_int, c_int, _vp, _vp]),
         "mio_quantize_rows": (c_int, [ctypes.c_uint32, _vp, c_int, c_int, _vp]),
         "mio_hip_debug_mmq": (c_int, [_vp, ctypes.c_uint32, _vp, c_int, c_int, _vp, c_int, c_int, _vp, _vp]),
@@ -114,7 +117,12 @@ def _declare(L: ctypes.CDLL) -> None:
                                                ctypes.c_int32, ctypes.c_int32, _vp, _vp]),
     }
     for name, (res, args) in sig.items():
-        fn = getattr(L, name)
+        # a library built from an older tree (same-box A/B of MIO_BUILD_DIR builds) may lack
+        # newer entry points: they stay unbound and fail when called; tests/test_capi_exports.py
+        # checks that the built library exports every symbol include/mio_hip.h declares
+        fn = getattr(L, name, None)
+        if fn is None:
+            continue
         fn.restype = res
         fn.argtypes = args
 
@@ -328,14 +336,21 @@ class Codec:
                                          ctypes.byref(nf), 0, None))
         return out[: nf.value]
 
-    def decode_pcm(self, codes, emb) -> np.ndarray:
+    def decode_pcm(self, codes, emb, incremental: bool = False) -> np.ndarray:
+        """incremental: reuse the prenet rows of the previous incremental decode for the shared
+        code prefix (MIO_CODEC_INCREMENTAL; last_reused() reports how many rows)."""
         codes = np.ascontiguousarray(codes, dtype=np.int32)
         emb = np.ascontiguousarray(emb, dtype=np.float32)
         out = np.empty(len(codes) * self.frames_per_code * self.hop_length + self.n_fft, np.float32)
         n = ctypes.c_int(0)
         check(lib().mio_hip_codec_decode_pcm(self.h, _ptr(codes), len(codes), _ptr(emb), _ptr(out),
-                                             ctypes.byref(n), 0, None))
+                                             ctypes.byref(n), MIO_CODEC_INCREMENTAL if incremental else 0, None))
         return out[: n.value]
+
+    def last_reused(self) -> int:
+        r = ctypes.c_int(0)
+        check(lib().mio_hip_codec_last_reused(self.h, ctypes.byref(r)))
+        return r.value
 
     def decode_pcm_device(self, codes: DeviceArray, n_codes: int, emb: DeviceArray,
                           out: DeviceArray, stream: int = 0) -> int:
@@ -399,6 +414,12 @@ class Llm:
         b = ctypes.c_uint64(0)
         check(lib().mio_hip_llm_weight_bytes(self.h, ctypes.byref(b)))
         return b.value
+
+    def load_ms(self) -> float:
+        """Wall time of the load (GGUF mmap -> pinned staging -> HBM arena)."""
+        v = ctypes.c_double(0)
+        check(lib().mio_hip_llm_load_ms(self.h, ctypes.byref(v)))
+        return v.value
 
     def eval(self, token: int, pos: int) -> np.ndarray:
         out = np.empty(self.n_vocab, np.float32)

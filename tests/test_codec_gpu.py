@@ -110,3 +110,32 @@ def test_codec_rejects_bad_codes(device, files, emb):
     gc = m.Codec(device, files["tiny"])
     with pytest.raises(m.HipError):
         gc.decode([5, 12800], emb)
+
+
+def test_codec_incremental_streaming_decode(device, files, emb):
+    """f3 (test-to-speech.cpp:526-529 re-decodes every committed prefix): an incremental
+    decode reuses the prenet rows of the previous one whose +-192-code receptive field was
+    complete (6 layers x window/2), and recomputes the prenet only from 192 codes before
+    them. Its PCM equals the full decode up to f32 summation order (the recomputed window
+    picks its own GEMM tiling) and the oracle within the PCM bound."""
+    gc = m.Codec(device, files["full"])
+    oc = pyoracle.Codec(files["full"])
+    radius = 6 * (65 // 2)
+    codes = np.random.default_rng(77).integers(0, 12800, 420).astype(np.int32)
+    prev = 0
+    for n in (60, 100, 260, 300, 420):  # the streaming cadence's growing prefixes
+        inc = gc.decode_pcm(codes[:n], emb, incremental=True)
+        assert gc.last_reused() == max(0, prev - radius)
+        full = gc.decode_pcm(codes[:n], emb)  # a plain decode neither reads nor moves the cache
+        d = inc.astype(np.float64) - full
+        assert np.sqrt(np.mean(d * d)) <= 1e-5 * np.sqrt(np.mean(full.astype(np.float64) ** 2)), n
+        prev = n
+    _pcm_close(inc, oc.decode_pcm(codes, emb))
+    # a different code at 300: rows whose receptive field reaches it are recomputed
+    edited = codes.copy()
+    edited[300] = (edited[300] + 1) % 12800
+    inc = gc.decode_pcm(edited, emb, incremental=True)
+    assert gc.last_reused() == 300 - radius
+    full = gc.decode_pcm(edited, emb)
+    d = inc.astype(np.float64) - full
+    assert np.sqrt(np.mean(d * d)) <= 1e-5 * np.sqrt(np.mean(full.astype(np.float64) ** 2))
