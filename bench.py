@@ -338,7 +338,7 @@ def main():
 
     def utterance(seed, record):
         t0 = time.perf_counter()
-        toks = llm.generate(prompt, a.tokens, 0.8, seed, allow=allow, check_interval=20)
+        toks = llm.generate(prompt, a.tokens, 0.8, seed, allow=allow, check_interval=32)
         t1 = time.perf_counter()
         d_codes = dev.upload((toks - m.SYNTH_SPEECH0).astype(np.int32))
         n = codec.decode_pcm_device(d_codes, len(toks), d_emb, d_pcm)
