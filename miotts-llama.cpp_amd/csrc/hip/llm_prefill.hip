@@ -590,9 +590,13 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
         const int per = tokens_per_launch(K, nt, rpw);
         for (int t = 0; t < nt; t += per) f(t, nt - t < per ? nt - t : per, shifted(d, pb, t, K));
     };
-    // matvecs on the int8 matrix cores (llm_mmq.hip); MIO_MMQ=0 selects the dot4 streaming
-    // engine below (A/B only: both are bit-exact with the decode step)
-    static const bool mmq = !(getenv("MIO_MMQ") && getenv("MIO_MMQ")[0] == '0');
+    // matvecs on the int8 matrix cores (llm_mmq.hip) above 8 tokens per launch, the dot4
+    // streaming engine below up to 8 (both bit-exact with the decode step). Same-box A/B,
+    // aggregate x realtime: 8 streams 1.7B Q4_K_M dot4 139 / MMQ 133, 2.6B Q8_0 101 / 80;
+    // 16 streams 2.6B Q8_0 134 / 144; a 64-token prefill chunk 10.4 / 2.7 ms.
+    // MIO_MMQ=0 / 1 forces one engine.
+    static const int mmq_env = getenv("MIO_MMQ") ? atoi(getenv("MIO_MMQ")) : -1;
+    const bool mmq = mmq_env >= 0 ? mmq_env != 0 : nt > 8;
     const int QD = (d.n_head + 2 * d.n_kv) * d.hd;
     for (int il = 0; il < n_layer; ++il) {
         const LayerW &L = layers[il];
