@@ -511,6 +511,10 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void *p, uint32_t b
 #ifndef MIO_WEIGHT_AUX
 #define MIO_WEIGHT_AUX 2
 #endif
+// policy of the output matrix stream (lm_head): A/B knob
+#ifndef MIO_LM_AUX
+#define MIO_LM_AUX MIO_WEIGHT_AUX
+#endif
 // policy of the small per-layer streams (attn_in q|k|v, attn_out o): A/B knob
 #ifndef MIO_SMALL_AUX
 #define MIO_SMALL_AUX MIO_WEIGHT_AUX

@@ -244,7 +244,7 @@ __global__ __launch_bounds__(MT) void k_lm_head(LlmDims d, const float *norm_w, 
     int lo, hi;
     wave_range(d, lm.rows, lo, hi);
     Frag ga[Cfg<NP>::U], gb[Cfg<NP>::U];
-    load_first<T, NP, 1>(lm, lm, lo, hi, ga, gb);
+    load_first<T, NP, 1, 0, MIO_LM_AUX>(lm, lm, lo, hi, ga, gb);
     x_after_weights(xr);
     MIO_TRACE(b, 1);
     MIO_TL_MARK1(b);
@@ -253,7 +253,7 @@ __global__ __launch_bounds__(MT) void k_lm_head(LlmDims d, const float *norm_w, 
     MIO_TL_MARK(b, 2);
     const int lane = threadIdx.x & 63;
     float r0 = -INFINITY, r1 = -INFINITY;
-    stream_rows<T, NP, 1>(lm, lm, lo, hi, ga, gb, s.a, [&](int row, float v, float) {
+    stream_rows<T, NP, 1, 0, MIO_LM_AUX>(lm, lm, lo, hi, ga, gb, s.a, [&](int row, float v, float) {
         const int k = row - lo;
         r0 = lane == k ? v : r0;
         r1 = lane + 64 == k ? v : r1;
