@@ -20,11 +20,14 @@
 //   Y[64][N] = A[64][K] * B[K][N],  A = spec row with element 1 := Re(X_{N/2}),
 //   B[0][n] = 1, B[1][n] = (-1)^n, B[2j][n] = 2cos, B[2j+1][n] = -2sin
 // with K = 2*n_freq - 2 (= N for even N), on v_mfma_f32_32x32x2_f32 (exact f32
-// fma chain, so the f32 parity budget is spent only on summation order).
+// fma chain, so the f32 parity budget is spent only on summation order). K is walked
+// in IST_KC chunks through two LDS stages: chunk c+1 is loaded into registers before
+// chunk c's MFMAs issue and stored to the other stage after them, one barrier per chunk.
 #include "common.h"
 
 #include <cmath>
 #include <cstring>
+#include <utility>
 #include <vector>
 
 namespace {
@@ -32,10 +35,14 @@ namespace {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int IST_M = 64;    // frames per tile
-constexpr int IST_KC = 16;   // K chunk staged per iteration
+constexpr int IST_KC = 32;   // K chunk staged per iteration
 constexpr int IST_ALD = IST_KC + 1;  // padded A row (conflict-free column reads)
 constexpr int IST_THREADS = 256;
 constexpr int IST_MAX_NT = 16;  // n-tiles of 32 -> n_fft <= 512
+constexpr int IST_A_PER = IST_M * IST_KC / IST_THREADS;  // A floats per thread per chunk
+// B float4s per thread per chunk and (frame half, n-tile) pairs per wave for NT n-tiles
+template <int NT> constexpr int ist_b_per() { return (IST_KC * NT * 8 + IST_THREADS - 1) / IST_THREADS; }
+template <int NT> constexpr int ist_pairs() { return (2 * NT + 3) / 4; }
 
 struct IstftParams {
     const float *spec;   // [F][n_freq][2]
@@ -43,84 +50,135 @@ struct IstftParams {
     const float *basis;  // [Kp][NP]
     const float *hann;   // [win]
     int n_frames, n_fft, win, hop, n_freq, K, Kp, NP, R, S, n_out, n_pad;
+    int hann_off;        // LDS float offset of the window copy (past stages and frames)
     float inv_n;
 };
 
+// One K chunk of the tile's operands held in registers while the previous chunk feeds
+// the MFMAs (two LDS stages, one barrier per chunk).
+template <int NT> struct IstftStage {
+    float a[IST_A_PER];
+    float4 b[ist_b_per<NT>()];
+};
+
+template <int NT>
+__device__ __forceinline__ void istft_load(const IstftParams &p, int t0, int kc, int tid, IstftStage<NT> &st) {
+    const int row_stride = p.n_freq * 2;
+#pragma unroll
+    for (int i = 0; i < IST_A_PER; ++i) {
+        // k' -> spec element: k' (k' != 1), 2*(n_freq-1) for k' == 1.
+        const int e = tid + i * IST_THREADS;
+        const int f = t0 + e / IST_KC, k = kc + (e % IST_KC);
+        float v = 0.0f;
+        if (f >= 0 && f < p.n_frames && k < p.K) {
+            const int src = (k == 1) ? 2 * (p.n_freq - 1) : k;
+            v = p.spec[(size_t)f * row_stride + src];
+        }
+        st.a[i] = v;
+    }
+    const float4 *bsrc = reinterpret_cast<const float4 *>(p.basis + (size_t)kc * (NT * 32));
+    constexpr int nb4 = IST_KC * NT * 8;
+#pragma unroll
+    for (int i = 0; i < ist_b_per<NT>(); ++i) {
+        const int e = tid + i * IST_THREADS;
+        st.b[i] = e < nb4 ? bsrc[e] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    }
+}
+
+template <int NT>
+__device__ __forceinline__ void istft_store(float *stage, int tid, const IstftStage<NT> &st) {
+    float *A_lds = stage;
+    float4 *B_lds = reinterpret_cast<float4 *>(stage + IST_M * IST_ALD);
+#pragma unroll
+    for (int i = 0; i < IST_A_PER; ++i) {
+        const int e = tid + i * IST_THREADS;
+        A_lds[(e / IST_KC) * IST_ALD + (e % IST_KC)] = st.a[i];
+    }
+    constexpr int nb4 = IST_KC * NT * 8;
+#pragma unroll
+    for (int i = 0; i < ist_b_per<NT>(); ++i) {
+        const int e = tid + i * IST_THREADS;
+        if (nb4 % IST_THREADS == 0 || e < nb4) B_lds[e] = st.b[i];
+    }
+}
+
+// NT = NP / 32 n-tiles is a template parameter so the pair loop below is branch-free: the
+// LDS fragment reads of a K step are issued together ahead of its MFMAs.
+template <int NT>
 __global__ __launch_bounds__(IST_THREADS) void istft_fused_kernel(IstftParams p) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
     const int t0 = blockIdx.x * p.S - p.R;  // first frame of this tile (may be < 0)
-    const int row_stride = p.n_freq * 2;
 
-    float *A_lds = lds;                      // [64][IST_ALD]
-    float *B_lds = lds + IST_M * IST_ALD;    // [IST_KC][NP]
-    const int n_ntiles = p.NP >> 5;
+    // The tile's (32-frame half m, 32-column n-tile) pairs are dealt round-robin to the
+    // four waves: 2 * NT pairs, JP per wave (7/7/6/6 at n_fft = 392). A wave whose last
+    // slot has no pair runs it on a clamped pair and drops the result: the block time is the
+    // longest wave's either way.
+    constexpr int NP = NT * 32;
+    constexpr int JP = ist_pairs<NT>();
+    constexpr int stage_floats = IST_M * IST_ALD + IST_KC * NP;
+    int pm[JP], pn[JP];
+#pragma unroll
+    for (int j = 0; j < JP; ++j) {
+        int pr = wave + 4 * j;
+        if (pr >= 2 * NT) pr = 2 * NT - 1;
+        pm[j] = pr >= NT;
+        pn[j] = (pr - pm[j] * NT) * 32 + (lane & 31);
+    }
 
-    f32x16 acc[2][4];
+    f32x16 acc[JP];
 #pragma unroll
-    for (int m = 0; m < 2; ++m)
+    for (int j = 0; j < JP; ++j)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[m][j][r] = 0.0f;
+        for (int r = 0; r < 16; ++r) acc[j][r] = 0.0f;
 
+    // window -> LDS once (the epilogue reads it ~4x per output sample)
+    float *W = lds + p.hann_off;
+    for (int i = tid; i < p.win; i += IST_THREADS) W[i] = p.hann[i];
+
+    IstftStage<NT> st;
+    istft_load<NT>(p, t0, 0, tid, st);
+    istft_store<NT>(lds, tid, st);
+    __syncthreads();
+    int buf = 0;
     for (int kc = 0; kc < p.Kp; kc += IST_KC) {
-        // Stage A: 64 frames x 16 k'. k' -> spec element: k' (k' != 1), 2*(n_freq-1) for k' == 1.
-        for (int e = tid; e < IST_M * IST_KC; e += IST_THREADS) {
-            const int r = e / IST_KC, c = e - r * IST_KC;
-            const int f = t0 + r;
-            const int k = kc + c;
-            float v = 0.0f;
-            if (f >= 0 && f < p.n_frames && k < p.K) {
-                const int src = (k == 1) ? 2 * (p.n_freq - 1) : k;
-                v = p.spec[(size_t)f * row_stride + src];
-            }
-            A_lds[r * IST_ALD + c] = v;
-        }
-        // Stage B: 16 x NP (NP multiple of 32 -> float4 copies).
-        const float4 *bsrc = reinterpret_cast<const float4 *>(p.basis + (size_t)kc * p.NP);
-        float4 *bdst = reinterpret_cast<float4 *>(B_lds);
-        for (int e = tid; e < (IST_KC * p.NP) / 4; e += IST_THREADS) bdst[e] = bsrc[e];
-        __syncthreads();
-
+        const bool more = kc + IST_KC < p.Kp;
+        if (more) istft_load<NT>(p, t0, kc + IST_KC, tid, st);  // in flight under the MFMAs
+        const float *A_lds = lds + buf * stage_floats;
+        const float *B_lds = A_lds + IST_M * IST_ALD;
 #pragma unroll
         for (int kk = 0; kk < IST_KC; kk += 2) {
             const int k = kk + (lane >> 5);
             const float a0 = A_lds[(lane & 31) * IST_ALD + k];
             const float a1 = A_lds[(32 + (lane & 31)) * IST_ALD + k];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int nt = wave + 4 * j;
-                if (nt < n_ntiles) {
-                    const float b = B_lds[k * p.NP + nt * 32 + (lane & 31)];
-                    acc[0][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b, acc[0][j], 0, 0, 0);
-                    acc[1][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b, acc[1][j], 0, 0, 0);
-                }
+            for (int j = 0; j < JP; ++j) {
+                const float b = B_lds[k * NP + pn[j]];
+                acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(pm[j] ? a1 : a0, b, acc[j], 0, 0, 0);
             }
         }
+        if (more) istft_store<NT>(lds + (buf ^ 1) * stage_floats, tid, st);
         __syncthreads();
+        buf ^= 1;
     }
 
     // Windowed frames -> LDS (reuses the staging area): y[f][n] = (sum * inv_n) * w[n]
     // (istft.cpp:65 then :91, same two roundings).
     float *Y = lds;  // [64][win]
 #pragma unroll
-    for (int m = 0; m < 2; ++m) {
+    for (int j = 0; j < JP; ++j) {
+        if (wave + 4 * j < 2 * NT) {
+            const int m = pm[j];
+            const int n = pn[j];
+            if (n < p.win) {
+                const float w = W[n];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int nt = wave + 4 * j;
-            if (nt < n_ntiles) {
-                const int n = nt * 32 + (lane & 31);
-                if (n < p.win) {
-                    const float w = p.hann[n];
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) {
-                        const int row = m * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-                        const float v = acc[m][j][r] * p.inv_n;
-                        Y[row * p.win + n] = v * w;
-                    }
+                for (int r = 0; r < 16; ++r) {
+                    const int row = m * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                    const float v = acc[j][r] * p.inv_n;
+                    Y[row * p.win + n] = v * w;
                 }
             }
         }
@@ -141,13 +199,22 @@ __global__ __launch_bounds__(IST_THREADS) void istft_fused_kernel(IstftParams p)
         float a = 0.0f, ws = 0.0f;
         for (int t = tmin; t <= tmax; ++t) {
             const int jj = n - t * p.hop;
-            const float w = p.hann[jj];
+            const float w = W[jj];
             a += Y[(t - t0) * p.win + jj];
             ws += w * w;
         }
         if (ws > 1e-8f) a /= ws;
         p.out[n - p.n_pad] = a;
     }
+}
+
+template <int... I> const void *istft_kernel_pick(int nt, std::integer_sequence<int, I...>) {
+    static const void *const tab[] = {(const void *)istft_fused_kernel<I + 1>...};
+    return tab[nt - 1];
+}
+// n-tile count (1..IST_MAX_NT, checked by mio_hip_istft_create) -> kernel instantiation
+const void *istft_kernel_for(int nt) {
+    return istft_kernel_pick(nt, std::make_integer_sequence<int, IST_MAX_NT>());
 }
 
 }  // namespace
@@ -217,7 +284,7 @@ extern "C" int mio_hip_istft_create(mio_hip_device *d, int n_fft, int win_length
     }
     // the 160 KB LDS opt-in applies to the current device: set it for every handle (once per
     // create, cheap), so a second device in the same process gets it too
-    if (hipFuncSetAttribute((const void *)istft_fused_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+    if (hipFuncSetAttribute(istft_kernel_for(h->NP / 32), hipFuncAttributeMaxDynamicSharedMemorySize,
                             160 * 1024) != hipSuccess) {
         mio::set_error("istft_create: LDS attribute: %s", hipGetErrorString(hipGetLastError()));
         mio_hip_istft_destroy(h);
@@ -272,11 +339,13 @@ int mio_istft_launch_device(mio_hip_istft *h, const float *d_spec, int n_frames,
     MIO_REQUIRE(p.S >= 1, MIO_ERR_UNSUPPORTED, "istft: hop %d too small for win %d", hop, h->win);
     const int span = p.S * hop;
     const int grid = (n_out + span - 1) / span;
-    size_t lds_stage = (size_t)(IST_M * IST_ALD + IST_KC * p.NP) * 4;
+    size_t lds_stage = (size_t)2 * (IST_M * IST_ALD + IST_KC * p.NP) * 4;  // two stages
     size_t lds_frames = (size_t)IST_M * p.win * 4;
     size_t lds = lds_stage > lds_frames ? lds_stage : lds_frames;
-    hipLaunchKernelGGL(istft_fused_kernel, dim3(grid), dim3(IST_THREADS), lds, s, p);
-    MIO_HIP_CHECK(hipGetLastError());
+    p.hann_off = (int)(lds / 4);
+    lds += (size_t)p.win * 4;
+    void *args[] = {&p};
+    MIO_HIP_CHECK(hipLaunchKernel(istft_kernel_for(p.NP / 32), dim3(grid), dim3(IST_THREADS), args, lds, s));
     return MIO_OK;
 }
 
