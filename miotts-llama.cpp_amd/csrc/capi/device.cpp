@@ -2,7 +2,9 @@
 #include "common.h"
 
 #include <cstdarg>
+#include <cstdlib>
 #include <cstring>
+#include <string>
 
 namespace mio {
 
@@ -52,7 +54,13 @@ extern "C" int mio_hip_device_open(int dev, mio_hip_device **out) {
     d->dev = dev;
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, dev) == hipSuccess) d->n_cu = prop.multiProcessorCount;
-    if (hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) != hipSuccess) {
+    // MIO_STREAM_PRIO=high|low: priority of the device stream (LLM steps, one-shot codec)
+    int prio = 0, least = 0, greatest = 0;
+    if (const char *e = getenv("MIO_STREAM_PRIO")) {
+        hipDeviceGetStreamPriorityRange(&least, &greatest);
+        prio = std::string(e) == "high" ? greatest : std::string(e) == "low" ? least : 0;
+    }
+    if (hipStreamCreateWithPriority(&d->stream, hipStreamNonBlocking, prio) != hipSuccess) {
         delete d;
         mio::set_error("device_open: stream create failed");
         return MIO_ERR_HIP;

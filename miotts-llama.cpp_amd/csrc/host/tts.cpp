@@ -467,6 +467,16 @@ bool TestToSpeech::synthesize_stream(const VoiceModel &voice, const std::string 
     return synthesize_stream(voice, text, callback, chunk_samples, Options{});
 }
 
+static int cstream_priority() {
+    int least = 0, greatest = 0;
+    hipDeviceGetStreamPriorityRange(&least, &greatest);
+    const char *e = getenv("MIO_CSTREAM_PRIO");
+    const std::string v = e ? e : "normal";
+    if (v == "low") return least;
+    if (v == "high") return greatest;
+    return 0;
+}
+
 // Streaming (test-to-speech.cpp:435-614): the LLM runs 20 steps per check on the GPU
 // (stream_check_interval); every check re-decodes all codes so far (the reference's
 // quality-first full decode), commits all but a 32-code holdback once at least 24 new codes
@@ -579,7 +589,9 @@ bool TestToSpeech::synthesize_stream_profiled(const VoiceModel &voice, const std
     bool done = false;
     // the codec works on its own stream: each check's re-decode runs beside the LLM's next
     // kCheck steps, which are enqueued before it (same tokens, same emitted samples)
-    if (!I.cstream && hipStreamCreateWithFlags(&I.cstream, hipStreamNonBlocking) != hipSuccess) {
+    // MIO_CSTREAM_PRIO=low|normal|high: the codec stream's priority relative to the LLM's
+    // (normal) stream, for the scheduling of workgroups when both have work queued
+    if (!I.cstream && hipStreamCreateWithPriority(&I.cstream, hipStreamNonBlocking, cstream_priority()) != hipSuccess) {
         fprintf(stderr, "TestToSpeech: codec stream creation failed\n");
         return false;
     }
