@@ -81,26 +81,40 @@ __global__ __launch_bounds__(256 * KG) void gemm_f32_kernel(GemmArgs g) {
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
 
     float4 ra0[AV], rb0[BV], ra1[AV], rb1[BV];
+    // per-thread row bases, fixed over the K loop; a plain A (no tap window: every source row
+    // exists) skips the per-element source-row test and its division
+    const bool a_win = g.a_seg != g.K || g.a_row_off != 0 || g.a_rows < g.M;
+    const float *a_base[AV];
+    const float *b_base[BV];
+    bool a_ok[AV], b_ok[BV];
+#pragma unroll
+    for (int i = 0; i < AV; ++i) {
+        const int e = tid + i * NT, m = m0 + e / (BK / 4);
+        a_ok[i] = m < g.M;
+        a_base[i] = g.A + (long)(m + g.a_row_off) * g.a_seg + (e % (BK / 4)) * 4;
+    }
+#pragma unroll
+    for (int i = 0; i < BV; ++i) {
+        const int e = tid + i * NT, n = n0 + e / (BK / 4);
+        b_ok[i] = n < g.N;
+        b_base[i] = g.B + (long)n * g.K + (e % (BK / 4)) * 4;
+    }
     auto load = [&](int k0, float4 (&ra)[AV], float4 (&rb)[BV]) {
 #pragma unroll
         for (int i = 0; i < AV; ++i) {
-            const int e = tid + i * NT, r = e / (BK / 4), c4 = e % (BK / 4);
-            const int m = m0 + r, k = k0 + c4 * 4;
-            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (m < g.M && k < g.K) {
+            const int e = tid + i * NT, m = m0 + e / (BK / 4), k = k0 + (e % (BK / 4)) * 4;
+            bool ok = a_ok[i] && k < g.K;
+            if (a_win && ok) {
                 const int src = m + g.a_row_off + k / g.a_seg;
-                if (src >= 0 && src < g.a_rows)
-                    v = *reinterpret_cast<const float4 *>(g.A + (long)(m + g.a_row_off) * g.a_seg + k);
+                ok = src >= 0 && src < g.a_rows;
             }
-            ra[i] = v;
+            ra[i] = ok ? *reinterpret_cast<const float4 *>(a_base[i] + k0) : make_float4(0.f, 0.f, 0.f, 0.f);
         }
 #pragma unroll
         for (int i = 0; i < BV; ++i) {
-            const int e = tid + i * NT, r = e / (BK / 4), c4 = e % (BK / 4);
-            const int n = n0 + r, k = k0 + c4 * 4;
-            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (n < g.N && k < g.K) v = *reinterpret_cast<const float4 *>(g.B + (long)n * g.K + k);
-            rb[i] = v;
+            const int k = k0 + ((tid + i * NT) % (BK / 4)) * 4;
+            rb[i] = (b_ok[i] && k < g.K) ? *reinterpret_cast<const float4 *>(b_base[i] + k0)
+                                         : make_float4(0.f, 0.f, 0.f, 0.f);
         }
     };
     auto store = [&](int buf, const float4 (&ra)[AV], const float4 (&rb)[BV]) {
