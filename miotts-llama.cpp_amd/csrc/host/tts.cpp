@@ -562,17 +562,25 @@ bool TestToSpeech::synthesize_stream_profiled(const VoiceModel &voice, const std
         size_t target = 0;
         if (!policy.plan(codes.size(), final_, &target))
             return (final_ && target <= committed) ? call(nullptr, 0, true) : true;
-        std::vector<float> audio;
-        if (!I.decode_codes(voice, codes, audio, &profile.codec_sec, &profile.istft_sec, false, true, I.cstream))
+        int len = 0;
+        if (!I.decode_codes_dev(voice, codes, &len, &profile.codec_sec, &profile.istft_sec, true, I.cstream))
             return false;
         profile.decode_calls++;
         profile.decoded_codes += codes.size();
-        const double per_code = (double)audio.size() / (double)codes.size();
+        const double per_code = (double)len / (double)codes.size();
         const size_t b = (size_t)std::llround((double)committed * per_code);
-        const size_t e = std::min((size_t)std::llround((double)target * per_code), audio.size());
+        const size_t e = std::min((size_t)std::llround((double)target * per_code), (size_t)len);
         if (b >= e) return final_ ? call(nullptr, 0, true) : true;
+        // only the samples this check emits leave the device (emit reads audio[b, e) alone)
+        std::vector<float> audio(e - b);
+        if (hipMemcpyAsync(audio.data(), (const float *)I.d_pcm + b, (e - b) * sizeof(float), hipMemcpyDeviceToHost,
+                           I.cstream) != hipSuccess ||
+            hipStreamSynchronize(I.cstream) != hipSuccess) {
+            fprintf(stderr, "TestToSpeech: PCM copy failed\n");
+            return false;
+        }
         committed = target;
-        return emit(audio, b, e, final_);
+        return emit(audio, 0, e - b, final_);
     };
 
     mio::SamplingParams sp;
@@ -595,6 +603,13 @@ bool TestToSpeech::synthesize_stream_profiled(const VoiceModel &voice, const std
         fprintf(stderr, "TestToSpeech: codec stream creation failed\n");
         return false;
     }
+    // the PCM buffer holds the whole stream from the start: growing it between re-decodes
+    // frees the old one, and a free waits for the LLM steps queued beside the re-decode
+    // (MIO_STREAM_PRESIZE=0 restores the growth, for A/B)
+    const char *presize = getenv("MIO_STREAM_PRESIZE");
+    if ((!presize || atoi(presize) != 0) && I.spt > 0 &&
+        !I.ensure(I.d_pcm, I.pcm_cap, (size_t)max_tokens * I.spt * sizeof(float) + 64))
+        return false;
     if (mio::llm_run(I.llm, kCheck)) {
         fprintf(stderr, "TestToSpeech: decode failed: %s\n", mio::last_error());
         return false;
