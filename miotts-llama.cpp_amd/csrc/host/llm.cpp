@@ -446,7 +446,12 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
     D.scale = 1.0f / sqrtf((float)D.hd);
     D.split = mio::kAttChunk;
     D.max_splits = (n_ctx + D.split - 1) / D.split;
-    D.n_wg = d->n_cu > 0 ? d->n_cu : 256;
+    // matvec workgroups: one per CU (MIO_WGM=2..4 launches that many per CU, for A/B)
+    {
+        const char *e = getenv("MIO_WGM");
+        const int wgm = e ? std::max(1, std::min(4, atoi(e))) : 1;
+        D.n_wg = (d->n_cu > 0 ? d->n_cu : 256) * wgm;
+    }
     D.n_layer = m->n_layer;
     MIO_REQUIRE(n_ctx <= 32768, MIO_ERR_UNSUPPORTED, "llm_load: n_ctx %d > 32768", n_ctx);
     const int G = D.n_kv ? D.n_head / D.n_kv : 0;
