@@ -61,6 +61,19 @@ def test_istft_tile_edges_vs_oracle(ist, n_frames):
     _check(out, ref, 5.0 * 5)
 
 
+@pytest.mark.parametrize("n_fft,win,hop", [(16, 16, 4), (64, 48, 16), (100, 100, 25), (256, 256, 64),
+                                           (392, 300, 98), (480, 480, 96), (512, 512, 128), (101, 101, 25)])
+def test_istft_other_geometries_vs_oracle(device, n_fft, win, hop):
+    """Kernel instantiations for n-tile counts NP/32 = 1, 2, 4, 8, 13, 15 and 16, shorter
+    windows and an odd n_fft, against the oracle restatement of istft.cpp."""
+    ist = m.Istft(device, n_fft, win)
+    rng = np.random.default_rng(n_fft * 1000 + win)
+    spec = (rng.standard_normal((150, n_fft // 2 + 1, 2)) * 5).astype(np.float32)
+    out = ist(spec, hop)
+    ref = pyoracle.istft(spec, n_fft, win, hop)
+    _check(out, ref, 5.0 * 5)
+
+
 def test_istft_full_size_T700(ist):
     """BASELINE size: T=700 codes -> 12,600 frames -> 1,234,800 samples."""
     rng = np.random.default_rng(700)
