@@ -75,8 +75,10 @@ struct LlmBuffers {
 
 // Batched prompt prefill (csrc/hip/llm_prefill.hip): up to kPrefillB prompt tokens per chunk
 // go through every layer with ONE weight pass per launch (the prefill llama_decode of
-// test-to-speech.cpp:132-148); K/V rows are written, no logits are produced.
-constexpr int kPrefillB = 64;
+// test-to-speech.cpp:132-148); K/V rows are written, no logits are produced. 128 holds the
+// chat-template prompts of the benchmarks (≈70 tokens) in one chunk: a 64-token chunk left
+// their last few tokens to a second, dot4 weight pass (+1.5 ms per 68-token prompt).
+constexpr int kPrefillB = 128;
 // The same multi-token layers run the batched decode step of up to kBatchMax utterances.
 constexpr int kBatchMax = 16;
 

@@ -260,7 +260,7 @@ def test_batched_prefill_then_generate(device, llm_files):
 
 
 def test_batched_prefill_1p7b_q4km(device, tmp_path):
-    """1.7B Q4_K_M, 68-token prompt (the bench prompt length: 5 chunks of 16, Q4_K + Q6_K)."""
+    """1.7B Q4_K_M, 68-token prompt (the bench prompt length: one chunk, Q4_K + Q6_K)."""
     path = m.synth_llm(str(tmp_path / "llm17.gguf"), 3, 1)
     g = m.Llm(device, path, 256)
     toks = np.random.default_rng(68).integers(0, 151936, 68)

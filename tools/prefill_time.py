@@ -22,7 +22,7 @@ dev = m.Device(0)
 llm = m.Llm(dev, path, 2048)
 rng = np.random.default_rng(0)
 base = None
-for n in (1, 2, 9, 17, 33, 65, 129, 257):
+for n in (1, 2, 9, 17, 33, 65, 68, 129, 257):
     toks = rng.integers(0, 256, n).astype(np.int32)
     llm.prefill(toks)
     best = 1e9
