@@ -7,6 +7,7 @@
 
 #include "common.h"
 #include "gguf.h"
+#include "unicode_ranges.h"
 
 namespace mio {
 namespace {
@@ -60,31 +61,24 @@ bool is_space(uint32_t cp) {
     return in(r, sizeof(r) / sizeof(r[0]), cp);
 }
 
-bool is_number(uint32_t cp) {
-    static const R r[] = {{0x30, 0x39},     {0xB2, 0xB3},     {0xB9, 0xB9},     {0xBC, 0xBE},     {0x660, 0x669},
-                          {0x6F0, 0x6F9},   {0x966, 0x96F},   {0x2070, 0x2070}, {0x2074, 0x2079}, {0x2080, 0x2089},
-                          {0x2150, 0x2182}, {0x2185, 0x2189}, {0x2460, 0x249B}, {0x24EA, 0x24FF}, {0x2776, 0x2793},
-                          {0x3007, 0x3007}, {0x3021, 0x3029}, {0x3038, 0x303A}, {0x3192, 0x3195}, {0x3220, 0x3229},
-                          {0x3248, 0x324F}, {0x3251, 0x325F}, {0x3280, 0x3289}, {0x32B1, 0x32BF}, {0xFF10, 0xFF19}};
-    return in(r, sizeof(r) / sizeof(r[0]), cp);
+// \p{N} / \p{L}: general categories N* / L* (unicode_ranges.h, generated), binary search
+bool in_sorted(const CpRange *r, size_t n, uint32_t cp) {
+    size_t lo = 0, hi = n;
+    while (lo < hi) {
+        const size_t mid = (lo + hi) / 2;
+        if (cp < r[mid].a)
+            hi = mid;
+        else if (cp > r[mid].b)
+            lo = mid + 1;
+        else
+            return true;
+    }
+    return false;
 }
 
-bool is_letter(uint32_t cp) {
-    static const R r[] = {
-        {0x41, 0x5A},       {0x61, 0x7A},     {0xAA, 0xAA},     {0xB5, 0xB5},     {0xBA, 0xBA},     {0xC0, 0xD6},
-        {0xD8, 0xF6},       {0xF8, 0x2C1},    {0x2C6, 0x2D1},   {0x2E0, 0x2E4},   {0x2EC, 0x2EC},   {0x2EE, 0x2EE},
-        {0x370, 0x374},     {0x376, 0x377},   {0x37A, 0x37D},   {0x37F, 0x37F},   {0x386, 0x386},   {0x388, 0x3F5},
-        {0x3F7, 0x481},     {0x48A, 0x52F},   {0x531, 0x556},   {0x561, 0x587},   {0x5D0, 0x5EA},   {0x620, 0x64A},
-        {0x671, 0x6D3},     {0x904, 0x939},   {0xE01, 0xE30},   {0x10A0, 0x10FF}, {0x1100, 0x11FF}, {0x1E00, 0x1FBC},
-        {0x1FC2, 0x1FCC},   {0x1FD0, 0x1FDB}, {0x1FE0, 0x1FEC}, {0x1FF2, 0x1FFC}, {0x2071, 0x2071}, {0x207F, 0x207F},
-        {0x2090, 0x209C},   {0x2102, 0x2102}, {0x2107, 0x2107}, {0x210A, 0x2113}, {0x2115, 0x2115}, {0x2119, 0x211D},
-        {0x2124, 0x2124},   {0x2126, 0x2126}, {0x2128, 0x2128}, {0x212A, 0x212D}, {0x212F, 0x2139}, {0x2C00, 0x2CE4},
-        {0x3005, 0x3006},   {0x3031, 0x3035}, {0x303B, 0x303C}, {0x3041, 0x3096}, {0x309D, 0x309F}, {0x30A1, 0x30FA},
-        {0x30FC, 0x30FF},   {0x3105, 0x312F}, {0x3131, 0x318E}, {0x31A0, 0x31BF}, {0x31F0, 0x31FF}, {0x3400, 0x4DBF},
-        {0x4E00, 0x9FFF},   {0xA000, 0xA48C}, {0xAC00, 0xD7A3}, {0xF900, 0xFAFF}, {0xFF21, 0xFF3A}, {0xFF41, 0xFF5A},
-        {0xFF66, 0xFFBE},   {0x20000, 0x2FA1F}};
-    return in(r, sizeof(r) / sizeof(r[0]), cp);
-}
+bool is_number(uint32_t cp) { return in_sorted(kNumberRanges, kNumberRanges_n, cp); }
+
+bool is_letter(uint32_t cp) { return cp < 0x80 ? ((cp | 32) - 'a') < 26u : in_sorted(kLetterRanges, kLetterRanges_n, cp); }
 
 bool is_nl(uint32_t cp) { return cp == '\r' || cp == '\n'; }
 uint32_t lower_ascii(uint32_t cp) { return cp >= 'A' && cp <= 'Z' ? cp + 32 : cp; }
