@@ -62,7 +62,7 @@ struct mio_hip_llm {
     std::vector<Range> ranges;
 
     // decode-step graphs, captured once (the sampling config is device-resident):
-    // one step, and kGraphSteps steps back to back (fewer graph launches per token)
+    // one step, and graph_steps() steps back to back (fewer graph launches per token)
     hipGraphExec_t graph = nullptr, graph_n = nullptr;
     mio::SampleCfg *d_cfg = nullptr;
     // generation state
@@ -201,7 +201,15 @@ float *upload_f32(mio_hip_llm *m, const mio::GgufTensor *t, int64_t n) {
     return p;
 }
 
-constexpr int kGraphSteps = 8;
+// steps per replayed step graph (MIO_GRAPH_STEPS, 1..64; A/B knob, default 8)
+int graph_steps() {
+    static const int n = [] {
+        const char *e = getenv("MIO_GRAPH_STEPS");
+        const int v = e && *e ? atoi(e) : 8;
+        return v < 1 ? 1 : (v > 64 ? 64 : v);
+    }();
+    return n;
+}
 
 // One decode step on m->d->stream (tl: optional step timeline, diagnostic).
 int issue_step(mio_hip_llm *m, unsigned long long *tl = nullptr) {
@@ -246,7 +254,7 @@ int ensure_graph(mio_hip_llm *m) {
     if (m->graph && m->graph_n) return MIO_OK;
     int rc;
     if (!m->graph && (rc = capture_steps(m, 1, &m->graph))) return rc;
-    if (!m->graph_n && (rc = capture_steps(m, kGraphSteps, &m->graph_n))) return rc;
+    if (!m->graph_n && (rc = capture_steps(m, graph_steps(), &m->graph_n))) return rc;
     return MIO_OK;
 }
 
@@ -356,7 +364,7 @@ int llm_run(mio_hip_llm *m, int n_steps) {
             if ((rc = issue_step(m))) return rc;
         return flush_sample(m);
     }
-    for (; n >= kGraphSteps; n -= kGraphSteps) MIO_HIP_CHECK(hipGraphLaunch(m->graph_n, m->d->stream));
+    for (const int gs = graph_steps(); n >= gs; n -= gs) MIO_HIP_CHECK(hipGraphLaunch(m->graph_n, m->d->stream));
     for (; n > 0; --n) MIO_HIP_CHECK(hipGraphLaunch(m->graph, m->d->stream));
     return flush_sample(m);
 }
@@ -807,7 +815,7 @@ int capture_batch(mio_hip_llm *m, int n, hipGraphExec_t *out) {
 }
 
 // n batched steps: the first ever step for this B runs eagerly (its launches set the
-// kernels' LDS attributes outside any capture), then 1- and kGraphSteps-step graphs replay.
+// kernels' LDS attributes outside any capture), then 1- and graph_steps()-step graphs replay.
 int run_batch(mio_hip_llm *m, int n) {
     static const bool eager = getenv("MIO_NO_GRAPH") && getenv("MIO_NO_GRAPH")[0] == '1';
     auto &bt = m->bt;
@@ -821,9 +829,9 @@ int run_batch(mio_hip_llm *m, int n) {
             return MIO_OK;
         }
         int rc;
-        if ((rc = capture_batch(m, 1, &bt.graph)) || (rc = capture_batch(m, kGraphSteps, &bt.graph_n))) return rc;
+        if ((rc = capture_batch(m, 1, &bt.graph)) || (rc = capture_batch(m, graph_steps(), &bt.graph_n))) return rc;
     }
-    for (; n >= kGraphSteps; n -= kGraphSteps) MIO_HIP_CHECK(hipGraphLaunch(bt.graph_n, m->d->stream));
+    for (const int gs = graph_steps(); n >= gs; n -= gs) MIO_HIP_CHECK(hipGraphLaunch(bt.graph_n, m->d->stream));
     for (; n > 0; --n) MIO_HIP_CHECK(hipGraphLaunch(bt.graph, m->d->stream));
     return MIO_OK;
 }
