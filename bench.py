@@ -168,7 +168,7 @@ def batched_line(a, llm, codec, dev, prompt, allow, d_emb, d_pcm):
     step(0, False)  # warm (graph capture)
     dev.sync()
     t0 = time.perf_counter()
-    samples, llm_s = step(5000, True)
+    samples, llm_s, _, _ = step(5000, True)
     wall = time.perf_counter() - t0
     return {"utterances": B, "value": round(samples / codec.sample_rate / wall, 3),
             "unit": "x realtime (audio s / wall s), aggregate of the B utterances on one GPU",
@@ -187,14 +187,17 @@ def make_batch_step(tokens, B, llm, codec, dev, prompt, allow, d_emb, d_pcm):
         t0 = time.perf_counter()
         outs = llm.generate_batch([prompt] * B, tokens, 0.8, seeds, allow=allow, check_interval=64)
         t1 = time.perf_counter()
-        samples = 0
+        samples, codec_ms, istft_ms = 0, 0.0, 0.0
         for toks in outs:
             if len(toks) != tokens:
                 raise RuntimeError("batched utterance ended early")
             d_codes = dev.upload((toks - m.SYNTH_SPEECH0).astype(np.int32))
             samples += codec.decode_pcm_device(d_codes, len(toks), d_emb, d_pcm)
+            c_ms, i_ms = codec.last_timings()
+            codec_ms += c_ms
+            istft_ms += i_ms
         dev.sync()
-        return samples, t1 - t0
+        return samples, t1 - t0, codec_ms, istft_ms
 
     return step
 
@@ -242,15 +245,18 @@ def roofline(llm, preset):
     import numpy as np
     tl = llm.timeline()
     nl = tl.shape[0]
-    # 5 launches per layer + lm_head; the sampler runs inside layer 0's attn_in
-    names = [KERNEL_NAMES[k] for k in (0, 1, 2, 3, 4)] * ((nl - 1) // 5) + [KERNEL_NAMES[6]]
+    # launches per layer (4: the attention runs inside attn_in; 5: its own launch) + lm_head;
+    # the sampler runs inside layer 0's attn_in
+    lpl = llm.launches_per_layer()
+    kinds = (0, 2, 3, 4) if lpl == 4 else (0, 1, 2, 3, 4)
+    names = [KERNEL_NAMES[k] for k in kinds] * ((nl - 1) // lpl) + [KERNEL_NAMES[6]]
     dur = np.nanmax(tl[:, :, 7], axis=1) - np.nanmin(tl[:, :, 0], axis=1)
     step_wall_us = float(np.nanmax(tl[-1, :, 7]) - np.nanmin(tl[0, :, 0]))
     per_kernel = {}
     for i, nm in enumerate(names):
         per_kernel.setdefault(nm, []).append(float(dur[i]))
     bytes_of, event_us = {}, {}
-    for which in (0, 1, 2, 3, 4, 6):
+    for which in kinds + (6,):
         ms, by = llm.time_kernel(which, 40)
         bytes_of[KERNEL_NAMES[which]] = by
         event_us[KERNEL_NAMES[which]] = ms * 1e3
@@ -259,8 +265,8 @@ def roofline(llm, preset):
     # achieved: HIP events around back-to-back launches of the kernel on its own stream (the
     # timeline's in-graph span runs the diagnostic instantiation: reported beside it)
     achieved = bytes_of[dom] / (event_us[dom] * 1e-6) / 1e9
-    n_layer = (nl - 1) // 5
-    step_bytes = sum(bytes_of[KERNEL_NAMES[k]] * n_layer for k in (0, 1, 2, 3, 4)) + bytes_of["k_lm_head"]
+    n_layer = (nl - 1) // lpl
+    step_bytes = sum(bytes_of[KERNEL_NAMES[k]] * n_layer for k in kinds) + bytes_of["k_lm_head"]
     step_gbs = step_bytes / (step_wall_us * 1e-6) / 1e9
     traffic = None
     tfile = os.path.join(REPO, "profiles", "pmc_traffic.json")
@@ -280,8 +286,10 @@ def roofline(llm, preset):
             "step_achieved_GBps": round(step_gbs, 1), "step_frac": round(step_gbs / HBM_PEAK_GBS, 4),
             "step_weight_bytes": llm.weight_bytes(),
             "per_token_us": {k: round(sum(v), 1) for k, v in per_kernel.items()},
-            "bytes_per_launch_all": bytes_of,
-            "note": "timeline, events and attention bytes at decode position ~400 (as the PMC run)"}
+            "bytes_per_launch_all": bytes_of, "launches_per_layer": lpl,
+            "note": ("timeline, events and attention bytes at decode position ~400 (as the PMC run)"
+                     + ("; k_attn_in = the fused launch: q|k|v matvec + attention workgroups, its bytes "
+                        "include the K/V rows" if lpl == 4 else ""))}
 
 
 def main():
@@ -354,13 +362,19 @@ def main():
             raise RuntimeError(f"utterance produced {len(toks)} tokens / {n} samples")
         return n
 
+    batch_llm_s = []
     if B > 1:
         bstep = make_batch_step(a.tokens, B, llm, codec, dev, prompt, allow, d_emb, d_pcm)
 
         def step_fn(seed, record):
-            samples, llm_s = bstep(seed * 131, record)
+            samples, llm_s, c_ms, i_ms = bstep(seed * 131, record)
             if record:
-                stage["llm_ms"] += llm_s * 1e3 / B
+                # whole-step totals; divided by the utterances (steps * B) below: per utterance,
+                # the batched decode's wall is shared by its B utterances
+                stage["llm_ms"] += llm_s * 1e3
+                stage["codec_ms"] += c_ms
+                stage["istft_ms"] += i_ms
+                batch_llm_s.append(llm_s)
             return samples
         utts = 1
     else:
@@ -431,6 +445,18 @@ def main():
         "value_pcie_inclusive": round(value_pcie, 3),
         "cpu_baseline": None,
     }
+    if B > 1 and batch_llm_s:
+        # the batched decode step against its weight stream: one weight pass per step serves
+        # the B utterances (+ each one's K/V rows at the mean position)
+        step_s = sum(batch_llm_s) / len(batch_llm_s) / a.tokens
+        info = llm.n_layer, llm.n_kv, llm.head_dim
+        kv = 2 * 2 * info[0] * info[1] * info[2] * (len(prompt) + a.tokens // 2) * B
+        by = llm.weight_bytes() + kv
+        out["batched_step"] = {"utterances": B, "ms_per_step": round(step_s * 1e3, 4),
+                               "bytes_per_step": by, "achieved_GBps": round(by / step_s / 1e9, 1),
+                               "step_frac": round(by / step_s / 1e9 / HBM_PEAK_GBS, 4),
+                               "note": "decode steps incl. the prompt prefill; bytes = weights + K/V rows "
+                                       "of B streams at the mean position"}
     if world == 1 and a.batch > 0 and B == 1:
         out["batched"] = batched_line(a, llm, codec, dev, prompt, allow, d_emb, d_pcm)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:

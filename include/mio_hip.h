@@ -173,13 +173,16 @@ int mio_hip_llm_time_kernel(mio_hip_llm *m, int which, int iters, float *avg_ms,
  * out[16] / out[31] = s_memrealtime (100 MHz) at the first / last checkpoint. */
 int mio_hip_llm_trace_kernel(mio_hip_llm *m, int which, uint64_t *out);
 /* Diagnostic: one decode step replayed as a graph with the step timeline on; out has
- * max_launches * 256 * 8 slots: out[(i * 256 + w) * 8 + k] = start (k 0) / marks (1-6) /
- * end (7) (s_memrealtime, 100 MHz; 0 = not recorded) of workgroup w of launch i (5 launches
- * per layer, then lm_head, sample). Marks: matvec launches 1 = weight loads issued,
- * 2 = activations quantized; attention 1 = K/V loads issued, 2 = heads prepared; 3-6 =
- * prologue steps in -DMIO_TL_DIAG builds.
+ * max_launches * 512 * 8 slots: out[(i * 512 + w) * 8 + k] = start (k 0) / marks (1-6) /
+ * end (7) (s_memrealtime, 100 MHz; 0 = not recorded) of workgroup w (mod 512) of launch i
+ * (mio_hip_llm_step_layout launches per layer, then lm_head). Marks: matvec launches 1 =
+ * weight loads issued, 2 = activations quantized; attention 1 = K/V loads issued, 2 = heads
+ * prepared; 3-6 = prologue steps in -DMIO_TL_DIAG builds.
  * Advances the decode state. */
 int mio_hip_llm_timeline(mio_hip_llm *m, uint64_t *out, int max_launches, int *n_launches);
+/* Launches per decoder layer in the decode step: 5 (attention is a launch of its own), or 4
+ * when the attention runs inside the attn_in launch (MIO_ATT_FUSED=1 at load). */
+int mio_hip_llm_step_layout(const mio_hip_llm *m, int *launches_per_layer);
 /* Wall time (ms) of mio_hip_llm_load: GGUF mmap, re-layout into pinned staging buffers,
  * asynchronous copies into the HBM weight arena (double-buffered). */
 int mio_hip_llm_load_ms(const mio_hip_llm *m, double *ms);

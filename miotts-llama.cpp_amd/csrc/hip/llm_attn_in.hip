@@ -1,0 +1,173 @@
+// First launch of a decoder layer in the single-token decode step (llama_decode for one
+// token, test-to-speech.cpp:178-185 / :589-596): RMSNorm(x) -> q|k|v dequant-matvec, and,
+// in the same launch, the layer's attention (RoPE, F16 KV append, chunked softmax).
+//
+// Matvec workgroups [0, GW): q|k rows (type TQ) on the first g_qk workgroups, v rows (type
+// TV) on the rest; each branch is WG-uniform and runs its own prologue, so neither path
+// merges load counts. FS (layer 0 only): the previous step's sampler runs here when
+// st->pending. Every workgroup reduces the lm_head partials to the same token and
+// dequantizes its embedding row into its x registers while its first weight group is in
+// flight; workgroup 0 also stores x (attn_out's residual) and the token / token ring / EOS
+// flag. pos and step are advanced by layer 0's ffn_in (no kernel before it writes a
+// StepState field it reads).
+//
+// Attention workgroups [GW, GW + n_kv * max_splits) when b.qkv_g is set (the fused launch,
+// attention_role in llm_device.h): they issue their K/V row loads at launch start and wait
+// for their kv head's q|k|v rows, which the matvec workgroups store as data-tagged
+// write-through granules (put_granule). The separate k_attention launch and its boundary
+// disappear from the step, and the K/V load latency hides under the q|k|v weight stream.
+// Attention workgroups come after every matvec workgroup in dispatch order, so a waiting
+// consumer never holds a CU a producer still needs.
+#include "llm_device.h"
+
+#pragma clang fp contract(off)
+
+namespace mio {
+namespace {
+
+struct AttArgs {
+    const float *q_norm, *k_norm, *bqkv;
+    _Float16 *kc, *vc;  // this layer's caches
+    int il;
+};
+
+template <int NP, int TQ, int TV, int SU, bool DG, bool FS>
+__global__ __launch_bounds__(MT) void k_attn_in(LlmDims d, const float *norm_w, QMat wq, QMat wk, QMat wv,
+                                                int g_qk, LlmBuffers b, QMat emb, int nblk, AttArgs at) {
+    constexpr bool kDiag = DG;
+    const int o1 = wq.rows, o2 = wq.rows + wk.rows;
+    const int GW = matvec_grid_n(d.n_wg, o2 + wv.rows);
+#ifndef MIO_NO_ROLE
+    if ((int)blockIdx.x >= GW) {
+        MIO_TL_BEGIN(b);
+        const int a = (int)blockIdx.x - GW;
+        if (d.hd == 128)
+            attention_role<128>(d, a, at.il, at.q_norm, at.k_norm, at.bqkv, at.kc, at.vc, b);
+        else
+            attention_role<64>(d, a, at.il, at.q_norm, at.k_norm, at.bqkv, at.kc, at.vc, b);
+        MIO_TL_END(b);
+        return;
+    }
+#endif
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    __shared__ float rs_[MW];
+    __shared__ int ri_[MW];
+    const int K = d.n_embd;
+    const Smem s = carve(smem, K);
+    MIO_TRACE(b, 0);
+    MIO_TL_BEGIN(b);
+    int pend = 0, step = 0;
+    if constexpr (FS) {
+        pend = b.st->pending;
+        step = b.st->step;
+    }
+    XRegs<NP> xr;
+    load_x(pend ? nullptr : b.x, norm_w, K, xr);
+    x_gate();
+    auto sample_prologue = [&]() {
+        if constexpr (FS) {
+            if (pend) {
+                const SampleCfg sc = *b.cfg;
+                const int tok = sample_token<MT>(b.smp, nblk, sc, step, rs_, ri_);
+                embed_regs(emb, tok, K, xr);
+                if (blockIdx.x == 0) {
+#pragma unroll
+                    for (int i = 0; i < NP; ++i) {
+                        const int e = (MIO_TIDX + i * MT) * 4;
+                        if (e < K) *reinterpret_cast<float4 *>(b.x + e) = xr.v[i];
+                    }
+                    if (MIO_TIDX == 0) {
+                        if (step < sc.max_steps) sc.out_tokens[step] = tok;
+                        if (tok == sc.eos0 || tok == sc.eos1) b.st->done = 1;
+                        b.st->token = tok;
+                    }
+                }
+            }
+        }
+    };
+    // q|k|v rows: plain (k_attention of the unfused step, diagnostics) and, for the attention
+    // workgroups of this launch, as tagged write-through granules
+    uint32_t tag = 0;
+    if (b.qkv_g) tag = qkv_tag(*b.cfg, b.st, at.il);
+    auto put = [&](int row, float v) {
+        if ((threadIdx.x & 63) == 0) {
+            b.qkv[row] = v;
+            if (b.qkv_g) put_granule(b.qkv_g + row, v, tag);
+        }
+    };
+    Frag ga[Cfg<NP, SU>::U], gb[Cfg<NP, SU>::U];
+    int lo, hi;
+    if ((int)blockIdx.x < g_qk) {
+        wave_range(o2, lo, hi, blockIdx.x, g_qk);
+        load_first<TQ, NP, 1, SU, MIO_SMALL_AUX>(wq, wk, lo, hi, ga, gb, o1);
+        sample_prologue();
+        x_after_weights(xr);
+        MIO_TRACE(b, 1);
+        MIO_TL_MARK1(b);
+        rmsnorm_quant(xr, K, d.eps, TQ != 8, s, MIO_TL_DIAGSLOT(b));
+        MIO_TRACE(b, 2);
+        MIO_TL_MARK(b, 2);
+        stream_rows<TQ, NP, 1, SU, MIO_SMALL_AUX>(wq, wk, lo, hi, ga, gb, s.a, [&](int row, float v, float) {
+            put(row, v);
+        }, o1);
+        MIO_TL_END(b);
+        MIO_TRACE(b, 15);
+    } else {
+        const int bv = (int)blockIdx.x - g_qk, gv = GW - g_qk;
+        wave_range(wv.rows, lo, hi, bv, gv);
+        load_first<TV, NP, 1, SU, MIO_SMALL_AUX>(wv, wv, lo, hi, ga, gb);
+        sample_prologue();
+        x_after_weights(xr);
+        rmsnorm_quant(xr, K, d.eps, TQ != 8, s, MIO_TL_DIAGSLOT(b));
+        stream_rows<TV, NP, 1, SU, MIO_SMALL_AUX>(wv, wv, lo, hi, ga, gb, s.a, [&](int row, float v, float) {
+            put(o2 + row, v);
+        });
+        MIO_TL_END(b);
+    }
+}
+
+template <bool DG>
+void launch(const LlmDims &d, const LayerW &L, int il, const AttArgs &at, const QMat &tok_embd, const LlmBuffers &b,
+            hipStream_t s) {
+    int GW, g_qk;
+    attn_in_grid(d, L, GW, g_qk);
+    const size_t lds = matvec_lds(d.n_embd);
+    const int np = pick_np(d.n_embd);
+    const int un = std::max(max_wave_units(L.wq.rows + L.wk.rows, g_qk, np, 1),
+                            max_wave_units(L.wv.rows, GW - g_qk, np, 1));
+    const int nblk = lm_head_blocks(d);
+    const int grid = GW + (b.qkv_g ? d.n_kv * d.max_splits : 0);
+    dispatch_nt(d.n_embd, L.wq.type, [&]<int NP, int TQ>() {
+        auto go = [&]<int TV>() {
+            dispatch_su<NP>(pick_su(un, NP), [&]<int SU>() {
+                if (il == 0)
+                    hipLaunchKernelGGL((k_attn_in<NP, TQ, TV, SU, DG, true>), dim3(grid), dim3(MT), lds, s, d,
+                                       L.attn_norm, L.wq, L.wk, L.wv, g_qk, b, tok_embd, nblk, at);
+                else
+                    hipLaunchKernelGGL((k_attn_in<NP, TQ, TV, SU, DG, false>), dim3(grid), dim3(MT), lds, s, d,
+                                       L.attn_norm, L.wq, L.wk, L.wv, g_qk, b, tok_embd, nblk, at);
+            });
+        };
+        if constexpr (TQ == 8) {
+            go.template operator()<8>();
+        } else {
+            if (L.wv.type == 14)
+                go.template operator()<14>();
+            else
+                go.template operator()<12>();
+        }
+    });
+}
+
+}  // namespace
+
+void launch_attn_in(const LlmDims &d, const LayerW &L, int il, _Float16 *kc, _Float16 *vc, const QMat &tok_embd,
+                    const LlmBuffers &b, bool dg, hipStream_t s) {
+    const AttArgs at{L.q_norm, L.k_norm, L.bqkv, kc, vc, il};
+    if (dg)
+        launch<true>(d, L, il, at, tok_embd, b, s);
+    else
+        launch<false>(d, L, il, at, tok_embd, b, s);
+}
+
+}  // namespace mio

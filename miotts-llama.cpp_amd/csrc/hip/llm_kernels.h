@@ -29,6 +29,7 @@ struct StepState {
     int token;    // token being decoded
     int done;     // set once an end token was sampled
     int pending;  // 1: lm_head partials of this step await the sampler
+    int fault;    // != 0: a kernel gave up waiting for an in-launch hand-off (never expected)
 };
 
 struct SampleCfg {
@@ -40,6 +41,7 @@ struct SampleCfg {
     int n_force;
     int *out_tokens;     // [max_steps] sampled/forced next token per step
     int max_steps;
+    uint32_t epoch;      // >= 1, new for every generation / eval (q|k|v granule tags)
 };
 
 struct LayerW {
@@ -71,6 +73,8 @@ struct LlmBuffers {
     unsigned long long *trace;  // optional: per-kernel checkpoint timestamps (workgroup 0, thread 0)
     unsigned long long *tl;     // optional: step timeline {min start, max end} per launch (s_memrealtime)
     int seq;                    // launch index within the step (timeline slot)
+    uint2 *qkv_g;  // q|k|v rows as data-tagged granules {value, tag} for the attention workgroups
+                   // of the fused attn_in launch, or null: attention is a launch of its own
 };
 
 // Batched prompt prefill (csrc/hip/llm_prefill.hip): up to kPrefillB prompt tokens per chunk
@@ -147,6 +151,14 @@ __host__ __device__ inline int matvec_grid_n(int n_wg, int rows) {
 int matvec_grid(const LlmDims &d, int rows);
 int pick_np(int K);
 size_t matvec_lds(int K);
+// units (row passes) of the busiest wave of a matvec over `rows` rows on `grid` workgroups,
+// and the single-group size that covers them (0 = streaming groups)
+int max_wave_units(int rows, int grid, int np, int nm);
+int pick_su(int units, int np);
+// Layer il's first launch (llm_attn_in.hip): RMSNorm + q|k|v matvec, plus the attention
+// workgroups when b.qkv_g is set; kc / vc: this layer's caches.
+void launch_attn_in(const LlmDims &d, const LayerW &L, int il, _Float16 *kc, _Float16 *vc, const QMat &tok_embd,
+                    const LlmBuffers &b, bool dg, hipStream_t s);
 // y = W x with x re-quantized to the vec_dot_type (parity test of the matvec kernels).
 void launch_debug_matvec(const QMat &W, const float *x, float *y, int n_wg, hipStream_t s);
 // y[t][rows] = W x[t] for nt tokens on the int8-MFMA multi-token matmul (act: scratch of

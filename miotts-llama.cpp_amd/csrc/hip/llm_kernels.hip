@@ -40,86 +40,8 @@ namespace mio {
 namespace {
 
 
-// ------------------------------------------------------------------ matvec kernels
-// Every kernel is instantiated per weight type T (ggml id 8 / 12 / 14): the unit loop is
-// straight-line code with no run-time type dispatch.
-// q|k rows (type TQ) on the first g_qk workgroups, v rows (type TV) on the rest; each
-// branch is WG-uniform and runs its own prologue, so neither path merges load counts.
-// FS (layer 0 only): the previous step's sampler runs here when st->pending. Every
-// workgroup reduces the lm_head partials to the same token and dequantizes its embedding
-// row into its x registers while its first weight group is in flight; workgroup 0 also
-// stores x (attn_out's residual) and the token / token ring / EOS flag. pos and step are
-// advanced by layer 0's ffn_in (no kernel before it writes a StepState field it reads).
-template <int NP, int TQ, int TV, int SU, bool DG, bool FS>
-__global__ __launch_bounds__(MT) void k_attn_in(LlmDims d, const float *norm_w, QMat wq, QMat wk, QMat wv,
-                                                int g_qk, LlmBuffers b, QMat emb, int nblk) {
-    constexpr bool kDiag = DG;
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    __shared__ float rs_[MW];
-    __shared__ int ri_[MW];
-    const int K = d.n_embd;
-    const Smem s = carve(smem, K);
-    MIO_TRACE(b, 0);
-    MIO_TL_BEGIN(b);
-    int pend = 0, step = 0;
-    if constexpr (FS) {
-        pend = b.st->pending;
-        step = b.st->step;
-    }
-    XRegs<NP> xr;
-    load_x(pend ? nullptr : b.x, norm_w, K, xr);
-    x_gate();
-    auto sample_prologue = [&]() {
-        if constexpr (FS) {
-            if (pend) {
-                const SampleCfg sc = *b.cfg;
-                const int tok = sample_token<MT>(b.smp, nblk, sc, step, rs_, ri_);
-                embed_regs(emb, tok, K, xr);
-                if (blockIdx.x == 0) {
-#pragma unroll
-                    for (int i = 0; i < NP; ++i) {
-                        const int e = (MIO_TIDX + i * MT) * 4;
-                        if (e < K) *reinterpret_cast<float4 *>(b.x + e) = xr.v[i];
-                    }
-                    if (MIO_TIDX == 0) {
-                        if (step < sc.max_steps) sc.out_tokens[step] = tok;
-                        if (tok == sc.eos0 || tok == sc.eos1) b.st->done = 1;
-                        b.st->token = tok;
-                    }
-                }
-            }
-        }
-    };
-    const int o1 = wq.rows, o2 = wq.rows + wk.rows;
-    Frag ga[Cfg<NP, SU>::U], gb[Cfg<NP, SU>::U];
-    int lo, hi;
-    if ((int)blockIdx.x < g_qk) {
-        wave_range(o2, lo, hi, blockIdx.x, g_qk);
-        load_first<TQ, NP, 1, SU, MIO_SMALL_AUX>(wq, wk, lo, hi, ga, gb, o1);
-        sample_prologue();
-        x_after_weights(xr);
-        MIO_TRACE(b, 1);
-    MIO_TL_MARK1(b);
-        rmsnorm_quant(xr, K, d.eps, TQ != 8, s, MIO_TL_DIAGSLOT(b));
-        MIO_TRACE(b, 2);
-    MIO_TL_MARK(b, 2);
-        stream_rows<TQ, NP, 1, SU, MIO_SMALL_AUX>(wq, wk, lo, hi, ga, gb, s.a, [&](int row, float v, float) {
-            if ((threadIdx.x & 63) == 0) b.qkv[row] = v;
-        }, o1);
-        MIO_TL_END(b);
-    MIO_TRACE(b, 15);
-    } else {
-        wave_range(wv.rows, lo, hi, blockIdx.x - g_qk, matvec_grid_n(d.n_wg, o2 + wv.rows) - g_qk);
-        load_first<TV, NP, 1, SU, MIO_SMALL_AUX>(wv, wv, lo, hi, ga, gb);
-        sample_prologue();
-        x_after_weights(xr);
-        rmsnorm_quant(xr, K, d.eps, TQ != 8, s, MIO_TL_DIAGSLOT(b));
-        stream_rows<TV, NP, 1, SU, MIO_SMALL_AUX>(wv, wv, lo, hi, ga, gb, s.a, [&](int row, float v, float) {
-            if ((threadIdx.x & 63) == 0) b.qkv[o2 + row] = v;
-        });
-        MIO_TL_END(b);
-    }
-}
+// k_attn_in (RMSNorm + q|k|v matvec, with the attention workgroups of the fused launch)
+// lives in llm_attn_in.hip.
 
 // residual rows of this wave (<= 64) in one register: lane i holds x[lo + i]
 __device__ inline float load_resid(const float *x, int lo, int hi) {
@@ -473,22 +395,6 @@ int pick_su(int units, int np) {
     if (np == 3 && units <= 3) return 3;
     return 0;
 }
-// Calls f.template operator()<SU>() for the instantiated single-group sizes of NP.
-template <int NP, class F>
-void dispatch_su(int su, F &&f) {
-    if constexpr (NP == 1) {
-        if (su == 1) return f.template operator()<1>();
-        if (su == 2) return f.template operator()<2>();
-        if (su == 3) return f.template operator()<3>();
-        if (su == 4) return f.template operator()<4>();
-        if (su == 6) return f.template operator()<6>();
-    }
-    if constexpr (NP == 3) {
-        if (su == 3) return f.template operator()<3>();
-    }
-    f.template operator()<0>();
-}
-
 // Launch one kernel of the step: which = 0 attn_in, 1 attention, 2 attn_out (+ chunk
 // merge), 3 ffn_in, 4 ffn_down (layer il), 5 (unused: the final norm is fused into
 // lm_head), 6 lm_head, 7 flush sampler. Layer 0's attn_in samples the pending token of the
@@ -502,34 +408,7 @@ void launch_step_kernel(int which, const LlmDims &d, const LayerW *layers, int i
     auto go_dg = [&]<bool DG>() {
     switch (which) {
         case 0: {
-            const LayerW &L = layers[il];
-            int GW, g_qk;
-            attn_in_grid(d, L, GW, g_qk);
-            const size_t lds = mv_lds(d.n_embd);
-            const int np = pick_np(d.n_embd);
-            const int un = std::max(max_wave_units(L.wq.rows + L.wk.rows, g_qk, np, 1),
-                                    max_wave_units(L.wv.rows, GW - g_qk, np, 1));
-            const int nblk = lm_head_blocks(d);
-            dispatch_nt(d.n_embd, L.wq.type, [&]<int NP, int TQ>() {
-                auto go = [&]<int TV>() {
-                    dispatch_su<NP>(pick_su(un, NP), [&]<int SU>() {
-                        if (il == 0)
-                            hipLaunchKernelGGL((k_attn_in<NP, TQ, TV, SU, DG, true>), dim3(GW), dim3(MT), lds, s, d,
-                                               L.attn_norm, L.wq, L.wk, L.wv, g_qk, b, tok_embd, nblk);
-                        else
-                            hipLaunchKernelGGL((k_attn_in<NP, TQ, TV, SU, DG, false>), dim3(GW), dim3(MT), lds, s, d,
-                                               L.attn_norm, L.wq, L.wk, L.wv, g_qk, b, tok_embd, nblk);
-                    });
-                };
-                if constexpr (TQ == 8) {
-                    go.template operator()<8>();
-                } else {
-                    if (L.wv.type == 14)
-                        go.template operator()<14>();
-                    else
-                        go.template operator()<12>();
-                }
-            });
+            launch_attn_in(d, layers[il], il, kcache + il * layer_kv, vcache + il * layer_kv, tok_embd, b, DG, s);
             break;
         }
         case 1: {

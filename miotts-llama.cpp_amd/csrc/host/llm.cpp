@@ -65,14 +65,24 @@ struct mio_hip_llm {
     // one step, and graph_steps() steps back to back (fewer graph launches per token)
     hipGraphExec_t graph = nullptr, graph_n = nullptr;
     mio::SampleCfg *d_cfg = nullptr;
+    uint32_t epoch = 0;  // SampleCfg.epoch of the last put_cfg
     // generation state
     int n_prompt = 0, max_new = 0, steps_total = 0, steps_issued = 0;
     mio::SampleCfg cfg{};
     double load_ms = 0.0;  // wall time of mio_hip_llm_load (GGUF mmap -> HBM arena)
     Stager *stager = nullptr;  // weight upload staging (load only)
-    // pinned host mirror of the state and the token ring (llm_poll: async copies, one sync)
-    mio::StepState *h_st = nullptr;
-    int *h_tokens = nullptr;
+    // token-ring snapshots (pinned host mirrors of the state and the ring): llm_run enqueues
+    // one behind its steps, llm_poll waits for the OLDEST one, so a caller can enqueue the next
+    // interval before it waits for the previous (the GPU never idles at a poll)
+    struct Snap {
+        hipEvent_t ev = nullptr;
+        mio::StepState *st = nullptr;
+        int *tok = nullptr;
+        int hi = 0, issued = 0;
+    };
+    static constexpr int kSnaps = 2;
+    Snap snaps[kSnaps];
+    int snap_head = 0, snap_n = 0;  // oldest outstanding snapshot, number outstanding
 
     ~mio_hip_llm() {
         if (d) hipSetDevice(d->dev);
@@ -83,8 +93,11 @@ struct mio_hip_llm {
         for (void *p : bt.allocs) hipFree(p);
         for (void *p : allocs) hipFree(p);
         stager_free(stager);
-        if (h_st) hipHostFree(h_st);
-        if (h_tokens) hipHostFree(h_tokens);
+        for (Snap &sn : snaps) {
+            if (sn.ev) hipEventDestroy(sn.ev);
+            if (sn.st) hipHostFree(sn.st);
+            if (sn.tok) hipHostFree(sn.tok);
+        }
     }
 };
 
@@ -148,7 +161,10 @@ T *dalloc(mio_hip_llm *m, size_t n) {
     void *p = nullptr;
     if (hipMalloc(&p, n * sizeof(T) + 16) != hipSuccess) return nullptr;
     m->allocs.push_back(p);
-    hipMemset(p, 0, n * sizeof(T) + 16);
+    // zero-filled on the null stream and waited for here: the weight upload that follows
+    // runs on the stager's non-blocking stream, which does not order itself after it
+    if (hipMemset(p, 0, n * sizeof(T) + 16) != hipSuccess || hipStreamSynchronize(nullptr) != hipSuccess)
+        return nullptr;
     return (T *)p;
 }
 
@@ -212,6 +228,10 @@ int graph_steps() {
 }
 
 // One decode step on m->d->stream (tl: optional step timeline, diagnostic).
+// Launches per layer of the step: attn_in (+ attention when fused), [attention], attn_out,
+// ffn_in, ffn_down.
+int launches_per_layer(const mio_hip_llm *m) { return m->buf.qkv_g ? 4 : 5; }
+
 int issue_step(mio_hip_llm *m, unsigned long long *tl = nullptr) {
     hipStream_t s = m->d->stream;
     int seq = 0;
@@ -222,8 +242,9 @@ int issue_step(mio_hip_llm *m, unsigned long long *tl = nullptr) {
     };
     for (int il = 0; il < m->n_layer; ++il)
         for (int k = 0; k < 5; ++k)
-            mio::launch_step_kernel(k, m->dims, m->layers.data(), il, m->kc, m->vc, m->out_norm, m->lm, m->tok, bufs(),
-                                    s);
+            if (k != 1 || !m->buf.qkv_g)
+                mio::launch_step_kernel(k, m->dims, m->layers.data(), il, m->kc, m->vc, m->out_norm, m->lm, m->tok,
+                                        bufs(), s);
     mio::launch_step_kernel(6, m->dims, m->layers.data(), 0, m->kc, m->vc, m->out_norm, m->lm, m->tok, bufs(), s);
     return MIO_OK;
 }
@@ -258,7 +279,10 @@ int ensure_graph(mio_hip_llm *m) {
     return MIO_OK;
 }
 
-int put_cfg(mio_hip_llm *m, const mio::SampleCfg &c) {
+int put_cfg(mio_hip_llm *m, mio::SampleCfg c) {
+    // a new generation epoch (q|k|v granule tags): 11 bits, never 0
+    m->epoch = m->epoch % 2047 + 1;
+    c.epoch = m->epoch;
     m->cfg = c;
     MIO_HIP_CHECK(hipMemcpyAsync(m->d_cfg, &c, sizeof(c), hipMemcpyHostToDevice, m->d->stream));
     return MIO_OK;
@@ -303,6 +327,35 @@ bool sequential_prefill() {
 
 namespace mio {
 
+namespace {
+// Drops every outstanding snapshot (waits for its copies: the host buffers are reused).
+int snaps_drain(mio_hip_llm *m) {
+    for (; m->snap_n > 0; --m->snap_n, m->snap_head = (m->snap_head + 1) % mio_hip_llm::kSnaps)
+        MIO_HIP_CHECK(hipEventSynchronize(m->snaps[m->snap_head].ev));
+    return MIO_OK;
+}
+
+// Enqueues a snapshot of the state and of the token ring slots the issued steps write.
+int snap_push(mio_hip_llm *m) {
+    if (m->snap_n == mio_hip_llm::kSnaps) {  // reuse the oldest slot: its copies must be done
+        MIO_HIP_CHECK(hipEventSynchronize(m->snaps[m->snap_head].ev));
+        m->snap_head = (m->snap_head + 1) % mio_hip_llm::kSnaps;
+        --m->snap_n;
+    }
+    mio_hip_llm::Snap &sn = m->snaps[(m->snap_head + m->snap_n) % mio_hip_llm::kSnaps];
+    const int first = m->n_prompt - 1;
+    sn.hi = std::min(m->steps_issued, m->max_steps);
+    sn.issued = m->steps_issued;
+    MIO_HIP_CHECK(hipMemcpyAsync(sn.st, m->buf.st, sizeof(mio::StepState), hipMemcpyDeviceToHost, m->d->stream));
+    if (sn.hi > first)
+        MIO_HIP_CHECK(hipMemcpyAsync(sn.tok + first, m->d_tokens + first, (size_t)(sn.hi - first) * 4,
+                                     hipMemcpyDeviceToHost, m->d->stream));
+    MIO_HIP_CHECK(hipEventRecord(sn.ev, m->d->stream));
+    ++m->snap_n;
+    return MIO_OK;
+}
+}  // namespace
+
 LlmInfo llm_info(const mio_hip_llm *m) {
     return LlmInfo{m->dims.n_vocab, m->dims.n_embd, m->n_layer, m->dims.n_head, m->dims.n_kv,
                    m->dims.hd, m->dims.n_ff, m->dims.n_ctx};
@@ -321,7 +374,7 @@ int llm_begin(mio_hip_llm *m, const int32_t *prompt, int n_prompt, int max_new, 
         MIO_REQUIRE(prompt[i] >= 0 && prompt[i] < m->dims.n_vocab, MIO_ERR_INVALID,
                     "llm_begin: token %d out of vocab", prompt[i]);
     int rc = mio::bind(m->d);
-    if (rc) return rc;
+    if (rc || (rc = snaps_drain(m))) return rc;
     std::vector<int> force(m->max_steps, -1);
     for (int j = 0; j + 1 < n_prompt; ++j) force[j] = prompt[j + 1];
     MIO_HIP_CHECK(hipMemcpyAsync(m->d_force, force.data(), force.size() * 4, hipMemcpyHostToDevice, m->d->stream));
@@ -362,28 +415,29 @@ int llm_run(mio_hip_llm *m, int n_steps) {
     if (eager) {
         for (int i = 0; i < n; ++i)
             if ((rc = issue_step(m))) return rc;
-        return flush_sample(m);
+    } else {
+        for (const int gs = graph_steps(); n >= gs; n -= gs) MIO_HIP_CHECK(hipGraphLaunch(m->graph_n, m->d->stream));
+        for (; n > 0; --n) MIO_HIP_CHECK(hipGraphLaunch(m->graph, m->d->stream));
     }
-    for (const int gs = graph_steps(); n >= gs; n -= gs) MIO_HIP_CHECK(hipGraphLaunch(m->graph_n, m->d->stream));
-    for (; n > 0; --n) MIO_HIP_CHECK(hipGraphLaunch(m->graph, m->d->stream));
-    return flush_sample(m);
+    if ((rc = flush_sample(m))) return rc;
+    return snap_push(m);
 }
 
 int llm_poll(mio_hip_llm *m, std::vector<int32_t> &out, bool *done) {
     int rc = mio::bind(m->d);
     if (rc) return rc;
-    // the steps issued so far bound the ring slots written: copy state and slots together
-    // into pinned memory and wait once
+    if (m->snap_n == 0 && (rc = snap_push(m))) return rc;
+    // the oldest outstanding snapshot: steps enqueued after it keep the GPU busy meanwhile
+    const mio_hip_llm::Snap &sn = m->snaps[m->snap_head];
+    MIO_HIP_CHECK(hipEventSynchronize(sn.ev));
+    m->snap_head = (m->snap_head + 1) % mio_hip_llm::kSnaps;
+    --m->snap_n;
     const int first = m->n_prompt - 1;
-    const int hi = std::min(m->steps_issued, m->max_steps);
-    MIO_HIP_CHECK(hipMemcpyAsync(m->h_st, m->buf.st, sizeof(StepState), hipMemcpyDeviceToHost, m->d->stream));
-    if (hi > first)
-        MIO_HIP_CHECK(hipMemcpyAsync(m->h_tokens + first, m->d_tokens + first, (size_t)(hi - first) * 4,
-                                     hipMemcpyDeviceToHost, m->d->stream));
-    MIO_HIP_CHECK(hipStreamSynchronize(m->d->stream));
-    const StepState st = *m->h_st;
-    const int n = std::min(st.step, hi) > first ? std::min(st.step, hi) - first : 0;
-    out.assign(m->h_tokens + first, m->h_tokens + first + n);
+    const StepState st = *sn.st;
+    MIO_REQUIRE(!st.fault, MIO_ERR_HIP, "llm: a decode step timed out waiting for its q/k/v rows (fault %d)",
+                st.fault);
+    const int n = std::min(st.step, sn.hi) > first ? std::min(st.step, sn.hi) - first : 0;
+    out.assign(sn.tok + first, sn.tok + first + n);
     bool d = false;
     for (int i = 0; i < n; ++i)
         if (out[i] == m->cfg.eos0 || out[i] == m->cfg.eos1) {
@@ -391,7 +445,7 @@ int llm_poll(mio_hip_llm *m, std::vector<int32_t> &out, bool *done) {
             d = true;
             break;
         }
-    if (done) *done = d || m->steps_issued >= m->steps_total;
+    if (done) *done = d || sn.issued >= m->steps_total;
     return MIO_OK;
 }
 
@@ -610,12 +664,19 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
     want(m->buf.smp, 2 * std::max(mio::lm_head_blocks(D), 4 * D.n_wg) + 16);
     want(m->buf.st, 1);
     want(m->d_cfg, 1);
+    // MIO_ATT_FUSED=1: attention inside the attn_in launch (tagged-granule hand-off);
+    // default: a launch of its own
+    uint2 *qkv_g = nullptr;
+    const bool fused = getenv("MIO_ATT_FUSED") && getenv("MIO_ATT_FUSED")[0] == '1';
+    if (fused) want(qkv_g, (size_t)qkv);
     m->max_steps = n_ctx;
-    if (hipHostMalloc((void **)&m->h_st, sizeof(mio::StepState), hipHostMallocDefault) != hipSuccess ||
-        hipHostMalloc((void **)&m->h_tokens, (size_t)m->max_steps * 4, hipHostMallocDefault) != hipSuccess) {
-        mio::set_error("llm_load: pinned host buffers failed");
-        return fail(MIO_ERR_OOM);
-    }
+    for (mio_hip_llm::Snap &sn : m->snaps)
+        if (hipHostMalloc((void **)&sn.st, sizeof(mio::StepState), hipHostMallocDefault) != hipSuccess ||
+            hipHostMalloc((void **)&sn.tok, (size_t)m->max_steps * 4, hipHostMallocDefault) != hipSuccess ||
+            hipEventCreateWithFlags(&sn.ev, hipEventDisableTiming) != hipSuccess) {
+            mio::set_error("llm_load: pinned host buffers / events failed");
+            return fail(MIO_ERR_OOM);
+        }
     want(m->d_tokens, m->max_steps);
     want(m->d_force, m->max_steps);
     want(m->d_prompt, n_ctx);
@@ -637,6 +698,7 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
         }
     }
     m->buf.cfg = m->d_cfg;
+    m->buf.qkv_g = qkv_g;  // zeroed with the carve (dalloc): tag 0 is never a launch's
     m->pf.tokens = m->d_prompt;
     // RoPE table, ggml rope-cache recurrence (theta = p; theta *= base^(-2/hd) per pair)
     std::vector<float2> rope((size_t)n_ctx * (D.hd / 2));
@@ -672,6 +734,12 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
     m->stager = nullptr;
     m->load_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_load0).count();
     *out = m;
+    return MIO_OK;
+}
+
+extern "C" int mio_hip_llm_step_layout(const mio_hip_llm *m, int *launches_per_layer) {
+    MIO_REQUIRE(m && launches_per_layer, MIO_ERR_INVALID, "llm_step_layout: null");
+    *launches_per_layer = ::launches_per_layer(m);
     return MIO_OK;
 }
 
@@ -713,6 +781,8 @@ extern "C" int mio_hip_llm_eval(mio_hip_llm *m, int32_t token, int pos, float *l
     if (logits)
         MIO_HIP_CHECK(hipMemcpyAsync(logits, m->buf.logits, (size_t)m->dims.n_vocab * 4, hipMemcpyDeviceToHost,
                                      m->d->stream));
+    // the step left its sample pending (k_lm_head): take it, so the state is a settled one
+    if ((rc = flush_sample(m))) return rc;
     MIO_HIP_CHECK(hipStreamSynchronize(m->d->stream));
     return MIO_OK;
 }
@@ -732,9 +802,12 @@ extern "C" int mio_hip_llm_generate(mio_hip_llm *m, const int32_t *prompt, int n
     std::vector<int32_t> toks;
     bool done = false;
     // (llm_begin prefilled the prompt) check every `check_interval` generated tokens (the
-    // streaming cadence, test-to-speech.cpp:499,608) for an end token
+    // streaming cadence, test-to-speech.cpp:499,608) for an end token. The next interval is
+    // enqueued before the previous one is checked: the GPU never waits for the host; after
+    // an end token at most one interval of steps runs for nothing (its tokens are dropped).
+    if ((rc = mio::llm_run(m, check_interval))) return rc;
     while (!done) {
-        if ((rc = mio::llm_run(m, check_interval))) return rc;
+        if (m->steps_issued < m->steps_total && (rc = mio::llm_run(m, check_interval))) return rc;
         if ((rc = mio::llm_poll(m, toks, &done))) return rc;
     }
     const int n = (int)toks.size() < max_tokens ? (int)toks.size() : max_tokens;
@@ -850,7 +923,7 @@ extern "C" int mio_hip_llm_generate_batch(mio_hip_llm *m, const int32_t *prompts
     MIO_REQUIRE(m && prompts && prompt_lens && seeds && out_tokens && n_out && max_tokens >= 1, MIO_ERR_INVALID,
                 "llm_generate_batch: bad args");
     MIO_REQUIRE(mio::batch_supported(m->dims, B), MIO_ERR_UNSUPPORTED,
-                "llm_generate_batch: %d streams not supported (1..%d, lm_head LDS)", B, mio::kPrefillB);
+                "llm_generate_batch: %d streams not supported (1..%d, lm_head LDS)", B, mio::kBatchMax);
     const mio::LlmDims &D = m->dims;
     std::vector<int> off(B + 1, 0);
     for (int b = 0; b < B; ++b) {
@@ -1057,15 +1130,23 @@ extern "C" int mio_hip_llm_time_kernel(mio_hip_llm *m, int which, int iters, flo
     };
     const mio::LlmDims &D = m->dims;
     // attention reads the K/V rows of positions <= pos of the current decode state
+    // the state at entry is restored on exit (k_lm_head sets `pending`, k_ffn_in of layer 0
+    // folds it into pos): diagnostic launches leave the decode state as they found it
     mio::StepState st{};
+    MIO_HIP_CHECK(hipStreamSynchronize(m->d->stream));
     MIO_HIP_CHECK(hipMemcpy(&st, m->buf.st, sizeof(st), hipMemcpyDeviceToHost));
-    const uint64_t pos = (uint64_t)std::max(0, std::min(st.pos, D.n_ctx - 1));
+    // the position the attention kernels work at (cur_pos: pos + pending)
+    const uint64_t pos = (uint64_t)std::max(0, std::min(st.pos + st.pending, D.n_ctx - 1));
     const uint64_t nch = pos / mio::kAttChunk + 1, qkv = (uint64_t)(D.n_head + 2 * D.n_kv) * D.hd;
     const uint64_t part = 4ull * D.n_head * nch * (D.hd + 2);  // chunk partial records {O, m, l}
     uint64_t b = 0;
+    const uint64_t att_bytes = 2ull * 2 * D.n_kv * D.hd * (pos + 1) + 4ull * qkv + 8ull * (D.hd / 2) + part;
     switch (which) {
-        case 0: b = qbytes(L.wq) + qbytes(L.wk) + qbytes(L.wv) + 4ull * D.n_embd + 4ull * qkv; break;
-        case 1: b = 2ull * 2 * D.n_kv * D.hd * (pos + 1) + 4ull * qkv + 8ull * (D.hd / 2) + part; break;
+        case 0:  // the fused launch also moves the attention's bytes (its q|k|v read stays on-chip)
+            b = qbytes(L.wq) + qbytes(L.wk) + qbytes(L.wv) + 4ull * D.n_embd + 4ull * qkv +
+                (m->buf.qkv_g ? att_bytes - 4ull * qkv : 0);
+            break;
+        case 1: b = att_bytes; break;
         case 2: b = qbytes(L.wo) + part + 4ull * D.n_embd * 2; break;
         case 3: b = qbytes(L.gate) + qbytes(L.up) + 4ull * (D.n_embd * 2 + D.n_ff); break;
         case 4: b = qbytes(L.down) + 4ull * (D.n_ff + 2 * D.n_embd); break;
@@ -1087,6 +1168,7 @@ extern "C" int mio_hip_llm_time_kernel(mio_hip_llm *m, int which, int iters, flo
     float ms = 0;
     MIO_HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
     hipEventDestroy(e0), hipEventDestroy(e1);
+    MIO_HIP_CHECK(hipMemcpy(m->buf.st, &st, sizeof(st), hipMemcpyHostToDevice));
     *avg_ms = ms / iters;
     *bytes = b;
     return MIO_OK;
@@ -1102,6 +1184,9 @@ extern "C" int mio_hip_llm_trace_kernel(mio_hip_llm *m, int which, uint64_t *out
     if (rc) return rc;
     const int il = m->n_layer / 2;
     hipStream_t s = m->d->stream;
+    mio::StepState st0{};  // restored on exit, as in mio_hip_llm_time_kernel
+    MIO_HIP_CHECK(hipStreamSynchronize(s));
+    MIO_HIP_CHECK(hipMemcpy(&st0, m->buf.st, sizeof(st0), hipMemcpyDeviceToHost));
     unsigned long long *dt = nullptr;
     MIO_HIP_CHECK(hipMalloc(&dt, 32 * sizeof(unsigned long long)));
     MIO_HIP_CHECK(hipMemsetAsync(dt, 0, 32 * sizeof(unsigned long long), s));
@@ -1127,6 +1212,7 @@ extern "C" int mio_hip_llm_trace_kernel(mio_hip_llm *m, int which, uint64_t *out
     MIO_HIP_CHECK(hipStreamSynchronize(s));
     hipFree(dt);
     if (flush) hipFree(flush);
+    MIO_HIP_CHECK(hipMemcpy(m->buf.st, &st0, sizeof(st0), hipMemcpyHostToDevice));
     return MIO_OK;
 }
 
@@ -1137,10 +1223,10 @@ extern "C" int mio_hip_llm_timeline(mio_hip_llm *m, uint64_t *out, int max_launc
     MIO_REQUIRE(m && out && n_launches && m->graph, MIO_ERR_INVALID, "llm_timeline: run generate/eval first");
     int rc = mio::bind(m->d);
     if (rc) return rc;
-    const int nl = m->n_layer * 5 + 1;
+    const int nl = m->n_layer * launches_per_layer(m) + 1;
     MIO_REQUIRE(max_launches >= nl, MIO_ERR_INVALID, "llm_timeline: need %d launch slots", nl);
     hipStream_t s = m->d->stream;
-    const size_t nslot = (size_t)nl * 256 * 8;
+    const size_t nslot = (size_t)nl * 512 * 8;
     unsigned long long *tl = nullptr;
     MIO_HIP_CHECK(hipMalloc(&tl, sizeof(unsigned long long) * nslot));
     hipGraph_t g = nullptr;

@@ -80,6 +80,8 @@ bool is_number(uint32_t cp) { return in_sorted(kNumberRanges, kNumberRanges_n, c
 
 bool is_letter(uint32_t cp) { return cp < 0x80 ? ((cp | 32) - 'a') < 26u : in_sorted(kLetterRanges, kLetterRanges_n, cp); }
 
+bool is_punct(uint32_t cp) { return in_sorted(kPunctRanges, kPunctRanges_n, cp); }
+
 bool is_nl(uint32_t cp) { return cp == '\r' || cp == '\n'; }
 uint32_t lower_ascii(uint32_t cp) { return cp >= 'A' && cp <= 'Z' ? cp + 32 : cp; }
 
@@ -112,8 +114,25 @@ bool BpeTokenizer::load(const GgufFile &g) {
     bos_ = (int32_t)g.get_int("tokenizer.ggml.bos_token_id", -1);
     const GgufValue *ab = g.get("tokenizer.ggml.add_bos_token");
     add_bos_ = ab ? ab->u != 0 : false;
+    // llama.cpp's tokenizer.ggml.pre names (llama-vocab.cpp) of the families implemented here
     const std::string pre = g.get_str("tokenizer.ggml.pre", "default");
-    qwen2_ = pre == "qwen2";
+    if (pre == "gpt2" || pre == "mpt" || pre == "olmo" || pre == "jais")
+        pre_ = Pre::Gpt2;
+    else if (pre == "default")
+        pre_ = Pre::Default;
+    else if (pre == "qwen2" || pre == "deepseek-r1-qwen" || pre == "megrez")
+        pre_ = Pre::Qwen2;
+    else if (pre == "llama3" || pre == "llama-v3" || pre == "llama-bpe" || pre == "falcon3" || pre == "pixtral" ||
+             pre == "lfm2")
+        pre_ = Pre::Llama3;
+    else if (pre == "smollm" || pre == "starcoder" || pre == "refact" || pre == "command-r" || pre == "codeshell" ||
+             pre == "exaone" || pre == "minerva-7b")
+        pre_ = Pre::Smollm;
+    else {
+        set_error("tokenizer: pre-tokenizer '%s' is not implemented (gpt2, default, qwen2, llama3 / llama-bpe / "
+                  "lfm2, smollm families)", pre.c_str());
+        return false;
+    }
     // GPT-2 bytes_to_unicode: printable bytes map to themselves, the rest to 256 + n
     int n = 0;
     for (int b = 0; b < 256; ++b) {
@@ -131,8 +150,151 @@ int32_t BpeTokenizer::special_id(const std::string &text) const {
 }
 
 // ------------------------------------------------------------------ pre-tokenizer
-// qwen2: (?i:'s|'t|'re|'ve|'m|'ll|'d)|[^\r\n\p{L}\p{N}]?\p{L}+|\p{N}| ?[^\s\p{L}\p{N}]+[\r\n]*|\s*[\r\n]+|\s+(?!\S)|\s+
-// gpt2 : 's|'t|'re|'ve|'m|'ll|'d| ?\p{L}+| ?\p{N}+| ?[^\s\p{L}\p{N}]+|\s+(?!\S)|\s+
+// llama.cpp applies a pre-type's regexes in sequence; each one splits every fragment left by
+// the previous one into its matches and the unmatched runs between them (both kept), and
+// lookaheads see only the fragment. The regexes, per family:
+//   gpt2   : 's|'t|'re|'ve|'m|'ll|'d| ?\p{L}+| ?\p{N}+| ?[^\s\p{L}\p{N}]+|\s+(?!\S)|\s+
+//   default: [\p{P}\$\+<=>\^~\|]+ , then the gpt2 regex, then \p{N}+ , then [0-9][0-9][0-9]
+//   qwen2  : (?i:'s|'t|'re|'ve|'m|'ll|'d)|[^\r\n\p{L}\p{N}]?\p{L}+|\p{N}| ?[^\s\p{L}\p{N}]+[\r\n]*
+//            |\s*[\r\n]+|\s+(?!\S)|\s+
+//   llama3 : the qwen2 regex with \p{N}{1,3} (and ASCII-only case-insensitive contractions)
+//   smollm : \p{N} , then the gpt2 regex
+namespace {
+
+struct Cps {
+    const std::vector<uint32_t> &cp;
+    size_t e;  // fragment end: every class test past it is false
+    bool L(size_t k) const { return k < e && is_letter(cp[k]); }
+    bool N(size_t k) const { return k < e && is_number(cp[k]); }
+    bool S(size_t k) const { return k < e && is_space(cp[k]); }
+    bool O(size_t k) const { return k < e && !is_space(cp[k]) && !is_letter(cp[k]) && !is_number(cp[k]); }
+    uint32_t at(size_t k) const { return k < e ? cp[k] : 0; }
+};
+
+// 's|'t|'re|'ve|'m|'ll|'d, optionally ASCII case-insensitive
+size_t m_contraction(const Cps &c, size_t i, bool fold) {
+    if (c.at(i) != '\'') return 0;
+    auto f = [&](uint32_t x) { return fold ? lower_ascii(x) : x; };
+    const uint32_t a = f(c.at(i + 1)), b = f(c.at(i + 2));
+    if (a == 's' || a == 't' || a == 'm' || a == 'd') return 2;
+    if ((a == 'r' && b == 'e') || (a == 'v' && b == 'e') || (a == 'l' && b == 'l')) return 3;
+    return 0;
+}
+
+// \s+(?!\S)|\s+ at a whitespace run [i, j)
+size_t m_spaces(const Cps &c, size_t i) {
+    size_t j = i;
+    while (c.S(j)) ++j;
+    if (j == i) return 0;
+    return (j == c.e || j - i == 1) ? j - i : j - i - 1;
+}
+
+size_t m_gpt2(const Cps &c, size_t i) {
+    if (size_t m = m_contraction(c, i, false)) return m;
+    const size_t k = i + (c.at(i) == ' ' ? 1 : 0);
+    size_t j = k;
+    if (c.L(k)) {
+        while (c.L(j)) ++j;
+        return j - i;
+    }
+    if (c.N(k)) {
+        while (c.N(j)) ++j;
+        return j - i;
+    }
+    if (c.O(k)) {
+        while (c.O(j)) ++j;
+        return j - i;
+    }
+    return m_spaces(c, i);
+}
+
+// qwen2 (ndig 1) and llama3 (ndig 3)
+size_t m_qwen(const Cps &c, size_t i, int ndig) {
+    if (size_t m = m_contraction(c, i, true)) return m;
+    {  // [^\r\n\p{L}\p{N}]?\p{L}+
+        size_t k = i;
+        if (!c.L(k) && k < c.e && !is_nl(c.cp[k]) && !c.N(k) && c.L(k + 1)) ++k;
+        if (c.L(k)) {
+            while (c.L(k)) ++k;
+            return k - i;
+        }
+    }
+    if (c.N(i)) {  // \p{N}{1,ndig}
+        size_t k = i;
+        while (c.N(k) && (int)(k - i) < ndig) ++k;
+        return k - i;
+    }
+    {  // ' ?[^\s\p{L}\p{N}]+[\r\n]*'
+        size_t k = i + (c.at(i) == ' ' ? 1 : 0);
+        if (c.O(k)) {
+            while (c.O(k)) ++k;
+            while (k < c.e && is_nl(c.cp[k])) ++k;
+            return k - i;
+        }
+    }
+    if (c.S(i)) {  // \s*[\r\n]+ : up to the last newline of the whitespace run, else \s+(?!\S)|\s+
+        size_t j = i, last = SIZE_MAX;
+        while (c.S(j)) {
+            if (is_nl(c.cp[j])) last = j;
+            ++j;
+        }
+        if (last != SIZE_MAX) return last + 1 - i;
+        return m_spaces(c, i);
+    }
+    return 0;
+}
+
+// [\p{P}\$\+<=>\^~\|]+
+size_t m_punct(const Cps &c, size_t i) {
+    size_t k = i;
+    auto p = [&](size_t q) {
+        if (q >= c.e) return false;
+        const uint32_t x = c.cp[q];
+        return is_punct(x) || x == '$' || x == '+' || x == '<' || x == '=' || x == '>' || x == '^' || x == '~' ||
+               x == '|';
+    };
+    while (p(k)) ++k;
+    return k - i;
+}
+
+// \p{N}+ (run = true) or \p{N}
+size_t m_num(const Cps &c, size_t i, bool run) {
+    size_t k = i;
+    while (c.N(k) && (run || k == i)) ++k;
+    return k - i;
+}
+
+// [0-9][0-9][0-9]
+size_t m_dig3(const Cps &c, size_t i) {
+    for (size_t k = i; k < i + 3; ++k)
+        if (k >= c.e || c.cp[k] < '0' || c.cp[k] > '9') return 0;
+    return 3;
+}
+
+// One regex stage over the fragment boundaries `cut` (sorted code-point offsets, first 0,
+// last n): every fragment is split into its leftmost-first matches and the runs between.
+template <class M>
+void stage(const std::vector<uint32_t> &cp, std::vector<size_t> &cut, M &&match) {
+    std::vector<size_t> out{0};
+    for (size_t f = 0; f + 1 < cut.size(); ++f) {
+        const Cps c{cp, cut[f + 1]};
+        for (size_t i = cut[f]; i < c.e;) {
+            const size_t m = match(c, i);
+            if (m) {
+                if (out.back() != i) out.push_back(i);
+                out.push_back(i + m);
+                i += m;
+            } else {
+                ++i;
+            }
+        }
+        if (out.back() != c.e) out.push_back(c.e);
+    }
+    cut.swap(out);
+}
+
+}  // namespace
+
 void BpeTokenizer::pretokenize(const std::string &text, std::vector<std::string> &pieces) const {
     std::vector<uint32_t> cp;
     std::vector<size_t> off;
@@ -143,75 +305,24 @@ void BpeTokenizer::pretokenize(const std::string &text, std::vector<std::string>
         i += l;
     }
     off.push_back(text.size());
-    const size_t n = cp.size();
-    auto L = [&](size_t k) { return k < n && is_letter(cp[k]); };
-    auto N = [&](size_t k) { return k < n && is_number(cp[k]); };
-    auto S = [&](size_t k) { return k < n && is_space(cp[k]); };
-    auto other = [&](size_t k) { return k < n && !is_space(cp[k]) && !is_letter(cp[k]) && !is_number(cp[k]); };
-    size_t i = 0;
-    while (i < n) {
-        size_t m = 0;  // match length in code points
-        // contractions
-        if (cp[i] == '\'' && i + 1 < n) {
-            const uint32_t a = qwen2_ ? lower_ascii(cp[i + 1]) : cp[i + 1];
-            const uint32_t b = i + 2 < n ? (qwen2_ ? lower_ascii(cp[i + 2]) : cp[i + 2]) : 0;
-            if (a == 's' || a == 't' || a == 'm' || a == 'd')
-                m = 2;
-            else if ((a == 'r' && b == 'e') || (a == 'v' && b == 'e') || (a == 'l' && b == 'l'))
-                m = 3;
-        }
-        if (!m && qwen2_) {
-            // [^\r\n\p{L}\p{N}]?\p{L}+
-            size_t k = i;
-            if (!L(k) && k < n && !is_nl(cp[k]) && !N(k) && L(k + 1)) ++k;
-            if (L(k)) {
-                while (L(k)) ++k;
-                m = k - i;
-            }
-            // \p{N}
-            if (!m && N(i)) m = 1;
-        } else if (!m) {
-            size_t k = i + (cp[i] == ' ' ? 1 : 0);
-            if (L(k)) {
-                while (L(k)) ++k;
-                m = k - i;
-            } else if (N(k)) {
-                while (N(k)) ++k;
-                m = k - i;
-            }
-        }
-        if (!m) {
-            // ' ?[^\s\p{L}\p{N}]+' (+ '[\r\n]*' for qwen2)
-            size_t k = i + (cp[i] == ' ' ? 1 : 0);
-            if (other(k)) {
-                while (other(k)) ++k;
-                if (qwen2_)
-                    while (k < n && is_nl(cp[k])) ++k;
-                m = k - i;
-            }
-        }
-        if (!m && S(i)) {
-            size_t j = i;
-            while (S(j)) ++j;
-            if (qwen2_) {
-                // \s*[\r\n]+ : up to the last newline of the whitespace run
-                size_t last = SIZE_MAX;
-                for (size_t k = i; k < j; ++k)
-                    if (is_nl(cp[k])) last = k;
-                if (last != SIZE_MAX) m = last + 1 - i;
-            }
-            if (!m) {
-                // \s+(?!\S) then \s+
-                if (j == n || j - i == 1)
-                    m = j - i;
-                else
-                    m = j - i - 1;
-            }
-        }
-        if (!m) m = 1;
-        pieces.emplace_back(text.substr(off[i], off[i + m] - off[i]));
-        i += m;
+    std::vector<size_t> cut{0, cp.size()};
+    if (cp.empty()) return;
+    switch (pre_) {
+        case Pre::Gpt2: stage(cp, cut, m_gpt2); break;
+        case Pre::Default:
+            stage(cp, cut, m_punct);
+            stage(cp, cut, m_gpt2);
+            stage(cp, cut, [](const Cps &c, size_t i) { return m_num(c, i, true); });
+            stage(cp, cut, m_dig3);
+            break;
+        case Pre::Qwen2: stage(cp, cut, [](const Cps &c, size_t i) { return m_qwen(c, i, 1); }); break;
+        case Pre::Llama3: stage(cp, cut, [](const Cps &c, size_t i) { return m_qwen(c, i, 3); }); break;
+        case Pre::Smollm:
+            stage(cp, cut, [](const Cps &c, size_t i) { return m_num(c, i, false); });
+            stage(cp, cut, m_gpt2);
+            break;
     }
+    for (size_t k = 0; k + 1 < cut.size(); ++k) pieces.emplace_back(text.substr(off[cut[k]], off[cut[k + 1]] - off[cut[k]]));
 }
 
 // ------------------------------------------------------------------ BPE

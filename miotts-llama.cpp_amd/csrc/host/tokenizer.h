@@ -6,12 +6,14 @@
 //
 // Algorithm (the public GPT-2 / llama.cpp BPE scheme, restated):
 //   1. split the text on special tokens (token_type CONTROL / USER_DEFINED), longest match;
-//   2. pre-tokenize the remaining runs with the vocabulary's regex ("qwen2" or GPT-2
-//      default), evaluated on code points with built-in Unicode letter/number/space classes;
+//   2. pre-tokenize the remaining runs with the regex sequence of the vocabulary's
+//      tokenizer.ggml.pre (llama.cpp's llm_tokenizer_bpe families: gpt2, default, qwen2,
+//      llama3 / llama-bpe / lfm2, smollm; any other value is refused at load), evaluated on
+//      code points with generated Unicode letter/number/punctuation classes;
 //   3. map each piece's bytes through the GPT-2 byte->unicode table and apply the merges in
 //      rank order; pieces are then looked up in the vocabulary (bytes as a fallback).
-// Parity is unpinned: llama.cpp is absent here and the Unicode class tables are a compact
-// restatement (Latin, Greek, Cyrillic, CJK, kana, Hangul, fullwidth forms), see DESIGN.md.
+// Parity: llama.cpp is absent here; each pre-type is checked id for id against HuggingFace
+// `tokenizers` with the same regex sequence (tests/test_tokenizer_hf.py).
 #pragma once
 
 #include <cstdint>
@@ -51,7 +53,9 @@ private:
     std::unordered_map<uint32_t, uint8_t> byte_dec_;     // stand-in code point -> byte
     int32_t eos_ = -1, bos_ = -1;
     bool add_bos_ = false;
-    bool qwen2_ = false;
+    // pre-tokenizer family (llama.cpp LLAMA_VOCAB_PRE_TYPE_*): the regex sequence of step 2
+    enum class Pre { Gpt2, Default, Qwen2, Llama3, Smollm };
+    Pre pre_ = Pre::Gpt2;
 };
 
 }  // namespace mio

@@ -616,7 +616,9 @@ bool TestToSpeech::synthesize_stream_profiled(const VoiceModel &voice, const std
     }
     while (!done && ok) {
         const auto ta = clk::now();
-        if (mio::llm_poll(I.llm, toks, &done) || (!done && mio::llm_run(I.llm, kCheck))) {
+        // the next kCheck steps are enqueued before the previous ones are checked (llm_poll
+        // waits for the oldest outstanding interval): the GPU never waits for this loop
+        if (mio::llm_run(I.llm, kCheck) || mio::llm_poll(I.llm, toks, &done)) {
             fprintf(stderr, "TestToSpeech: decode failed: %s\n", mio::last_error());
             ok = false;
             break;

@@ -100,6 +100,7 @@ def _declare(L: ctypes.CDLL) -> None:
         "mio_hip_codec_last_timings": (c_int, [_vp, _f32p]),
         "mio_hip_codec_last_reused": (c_int, [_vp, ctypes.POINTER(c_int)]),
         "mio_hip_llm_load_ms": (c_int, [_vp, ctypes.POINTER(ctypes.c_double)]),
+        "mio_hip_llm_step_layout": (c_int, [_vp, ctypes.POINTER(c_int)]),
         "mio_hip_debug_matvec": (c_int, [_vp, ctypes.c_uint32, _vp, c_int, c_int, _vp, _vp]),
         "mio_quantize_rows": (c_int, [ctypes.c_uint32, _vp, c_int, c_int, _vp]),
         "mio_hip_debug_mmq": (c_int, [_vp, ctypes.c_uint32, _vp, c_int, c_int, _vp, c_int, c_int, _vp, _vp]),
@@ -455,12 +456,18 @@ class Llm:
         """Per-launch, per-workgroup [start, marks 1-6, end] (us from the step start, NaN =
         absent) of one graph-replayed step (diagnostic, mio_hip_llm_timeline; advances the
         decode state). Marks: see MIO_TL_MARK in csrc/hip/llm_device.h."""
-        out = np.zeros(1024 * 256 * 8, np.uint64)
+        out = np.zeros(1024 * 512 * 8, np.uint64)
         n = ctypes.c_int(0)
         check(lib().mio_hip_llm_timeline(self.h, _ptr(out), 1024, ctypes.byref(n)))
-        t = out[: n.value * 2048].astype(np.float64).reshape(n.value, 256, 8)
+        t = out[: n.value * 4096].astype(np.float64).reshape(n.value, 512, 8)
         t[t == 0] = np.nan
         return (t - np.nanmin(t[0, :, 0])) * 0.01
+
+    def launches_per_layer(self) -> int:
+        """Decode-step launches per layer (4: attention inside attn_in; 5: its own launch)."""
+        v = ctypes.c_int(0)
+        check(lib().mio_hip_llm_step_layout(self.h, ctypes.byref(v)))
+        return v.value
 
     def generate(self, prompt, max_tokens: int, temperature: float = 0.8, seed: int = 42,
                  allow=(-1, -1), eos=(-1, -1), check_interval: int = 20) -> np.ndarray:

@@ -5,8 +5,10 @@ llama.cpp's `llama_tokenize` (test-to-speech.cpp:117-125,173-176) is absent (the
 submodule), so there is no reference output to pin against. `tokenizers` is the
 published byte-level BPE that llama.cpp's `llm_tokenizer_bpe` is validated against (its
 test-tokenizer-0 vectors come from it), and the GGUF `tokenizer.ggml.pre` types map onto its
-pre-tokenizers: "qwen2" = Split(qwen2 regex, isolated) + ByteLevel(use_regex=False), "default"
-= ByteLevel(use_regex=True) (the GPT-2 regex). Each case trains a BPE vocabulary with
+pre-tokenizers: "qwen2" / "llama3" (= "llama-bpe", "lfm2") = Split(their regex, isolated) +
+ByteLevel(use_regex=False); "gpt2" = ByteLevel(use_regex=True) (the GPT-2 regex); "default" =
+llama.cpp's four regexes in sequence as four Splits; "smollm" = Digits(individual) +
+ByteLevel(use_regex=True). Each case trains a BPE vocabulary with
 `tokenizers` on a seeded corpus, writes it into a GGUF (tokens in id order, merges in rank
 order, specials as CONTROL), and requires identical ids on held-out seeded strings: mixed
 Japanese / ASCII / other scripts / digits / punctuation / whitespace runs / contractions /
@@ -24,6 +26,12 @@ tokenizers = pytest.importorskip("tokenizers")
 
 QWEN2 = (r"(?i:'s|'t|'re|'ve|'m|'ll|'d)|[^\r\n\p{L}\p{N}]?\p{L}+|\p{N}| ?[^\s\p{L}\p{N}]+[\r\n]*"
          r"|\s*[\r\n]+|\s+(?!\S)|\s+")
+# llama.cpp LLAMA_VOCAB_PRE_TYPE_LLAMA3 (also "llama-bpe", "lfm2")
+LLAMA3 = (r"(?:'[sS]|'[tT]|'[rR][eE]|'[vV][eE]|'[mM]|'[lL][lL]|'[dD])|[^\r\n\p{L}\p{N}]?\p{L}+|\p{N}{1,3}"
+          r"| ?[^\s\p{L}\p{N}]+[\r\n]*|\s*[\r\n]+|\s+(?!\S)|\s+")
+GPT2 = r"'s|'t|'re|'ve|'m|'ll|'d| ?\p{L}+| ?\p{N}+| ?[^\s\p{L}\p{N}]+|\s+(?!\S)|\s+"
+# llama.cpp's "default" pre-type: four regexes in sequence
+DEFAULT = [r"[\p{P}\$\+<=>\^~\|]+", GPT2, r"\p{N}+", r"[0-9][0-9][0-9]"]
 SPECIALS = ["<|im_start|>", "<|im_end|>", "<|startoftext|>", "<|endoftext|>"]
 
 # characters drawn from the classes the pre-tokenizers distinguish
@@ -63,12 +71,17 @@ def _trained(pre, vocab_size, seed):
     from tokenizers import Regex, Tokenizer, models, pre_tokenizers, trainers
 
     tok = Tokenizer(models.BPE())
-    if pre == "qwen2":
+    split = lambda rx: pre_tokenizers.Split(Regex(rx), behavior="isolated", invert=False)
+    bl = pre_tokenizers.ByteLevel(add_prefix_space=False, use_regex=False)
+    if pre in ("qwen2", "llama3", "llama-bpe", "lfm2"):
+        tok.pre_tokenizer = pre_tokenizers.Sequence([split(QWEN2 if pre == "qwen2" else LLAMA3), bl])
+    elif pre == "default":
+        tok.pre_tokenizer = pre_tokenizers.Sequence([split(rx) for rx in DEFAULT] + [bl])
+    elif pre == "smollm":
         tok.pre_tokenizer = pre_tokenizers.Sequence([
-            pre_tokenizers.Split(Regex(QWEN2), behavior="isolated", invert=False),
-            pre_tokenizers.ByteLevel(add_prefix_space=False, use_regex=False),
-        ])
-    else:
+            pre_tokenizers.Digits(individual_digits=True),
+            pre_tokenizers.ByteLevel(add_prefix_space=False, use_regex=True)])
+    else:  # gpt2
         tok.pre_tokenizer = pre_tokenizers.ByteLevel(add_prefix_space=False, use_regex=True)
     rng = random.Random(seed)
     corpus = [_text(rng, 200) for _ in range(600)] + _WORDS * 20
@@ -101,7 +114,9 @@ def _to_gguf(tok, path, pre):
     return len(merges)
 
 
-@pytest.mark.parametrize("pre,vocab_size,seed", [("qwen2", 1200, 1), ("qwen2", 3000, 2), ("default", 1200, 3)])
+@pytest.mark.parametrize("pre,vocab_size,seed", [("qwen2", 1200, 1), ("qwen2", 3000, 2), ("gpt2", 1200, 3),
+                                                  ("default", 1500, 4), ("llama3", 1500, 5), ("lfm2", 3000, 6),
+                                                  ("smollm", 1500, 7)])
 def test_tokenize_matches_hf_tokenizers(tmp_path, pre, vocab_size, seed):
     hf = _trained(pre, vocab_size, seed)
     path = str(tmp_path / f"hf_{pre}_{seed}.gguf")
@@ -110,7 +125,9 @@ def test_tokenize_matches_hf_tokenizers(tmp_path, pre, vocab_size, seed):
     t = m.Tokenizer(path)
     rng = random.Random(1000 + seed)
     cases = [_text(rng, rng.randint(1, 120)) for _ in range(400)]
-    cases += ["", " ", "\n", "  \n  x", "a  b   c", "x\r\ny", "'s's", "ABC'LL", "１２３", "。\n\n", "　あ"]
+    cases += ["", " ", "\n", "  \n  x", "a  b   c", "x\r\ny", "'s's", "ABC'LL", "１２３", "。\n\n", "　あ",
+              "1234567", "12345 678901", "a1b22c333d4444", "３．１４１５９", "v1.2.3-rc4", "$100+<=>^~|", "٠١٢٣٤",
+              "今日は2024年10月17日です。", "x ,y", "((a))", "¿Qué? ¡Sí!"]
     bad = []
     for s in cases:
         want = hf.encode(s, add_special_tokens=False).ids
@@ -120,3 +137,13 @@ def test_tokenize_matches_hf_tokenizers(tmp_path, pre, vocab_size, seed):
         # byte-exact inverse
         assert t.detokenize(got) == s
     assert not bad, f"{len(bad)}/{len(cases)} differ, first: {bad[0]!r}"
+
+
+def test_unknown_pre_tokenizer_is_refused(tmp_path):
+    """A tokenizer.ggml.pre outside the implemented families fails to load with a message
+    instead of silently tokenizing with another family's regex."""
+    hf = _trained("gpt2", 600, 11)
+    path = str(tmp_path / "unknown_pre.gguf")
+    _to_gguf(hf, path, "chatglm-bpe")
+    with pytest.raises(Exception, match="pre-tokenizer 'chatglm-bpe' is not implemented"):
+        m.Tokenizer(path)
