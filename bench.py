@@ -47,7 +47,7 @@ sys.path.insert(0, os.path.join(REPO, "miotts-llama.cpp_amd", "python"))
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 ROOF_POS = 400  # decode position of the roofline timeline / kernel timings (and of the PMC run)
 KERNEL_NAMES = {0: "k_attn_in", 1: "k_attention", 2: "k_attn_out", 3: "k_ffn_in", 4: "k_ffn_down",
-                6: "k_lm_head"}
+                6: "k_lm_head", 8: "k_conv_in", 9: "k_conv_out"}
 PRESETS = {2: "MioTTS-0.1B Q8_0", 3: "MioTTS-1.7B Q4_K_M", 4: "MioTTS-2.6B Q8_0"}
 PROMPT = "こんにちは、今日はいい天気ですね。"  # README.md:83, SURVEY 8(d)
 
@@ -245,18 +245,19 @@ def roofline(llm, preset):
     import numpy as np
     tl = llm.timeline()
     nl = tl.shape[0]
-    # launches per layer (4: the attention runs inside attn_in; 5: its own launch) + lm_head;
-    # the sampler runs inside layer 0's attn_in
-    lpl = llm.launches_per_layer()
-    kinds = (0, 2, 3, 4) if lpl == 4 else (0, 1, 2, 3, 4)
-    names = [KERNEL_NAMES[k] for k in kinds] * ((nl - 1) // lpl) + [KERNEL_NAMES[6]]
+    # the step's launches in order (layer kinds, then lm_head); the sampler runs inside layer
+    # 0's first launch
+    step = llm.step_kinds()
+    assert len(step) == nl, (len(step), nl)
+    names = [KERNEL_NAMES[k] for k in step]
+    fused = 1 not in step and 0 in step
     dur = np.nanmax(tl[:, :, 7], axis=1) - np.nanmin(tl[:, :, 0], axis=1)
     step_wall_us = float(np.nanmax(tl[-1, :, 7]) - np.nanmin(tl[0, :, 0]))
     per_kernel = {}
     for i, nm in enumerate(names):
         per_kernel.setdefault(nm, []).append(float(dur[i]))
     bytes_of, event_us = {}, {}
-    for which in kinds + (6,):
+    for which in sorted(set(step)):
         ms, by = llm.time_kernel(which, 40)
         bytes_of[KERNEL_NAMES[which]] = by
         event_us[KERNEL_NAMES[which]] = ms * 1e3
@@ -265,8 +266,7 @@ def roofline(llm, preset):
     # achieved: HIP events around back-to-back launches of the kernel on its own stream (the
     # timeline's in-graph span runs the diagnostic instantiation: reported beside it)
     achieved = bytes_of[dom] / (event_us[dom] * 1e-6) / 1e9
-    n_layer = (nl - 1) // lpl
-    step_bytes = sum(bytes_of[KERNEL_NAMES[k]] * n_layer for k in kinds) + bytes_of["k_lm_head"]
+    step_bytes = sum(bytes_of[KERNEL_NAMES[k]] for k in step)
     step_gbs = step_bytes / (step_wall_us * 1e-6) / 1e9
     traffic = None
     tfile = os.path.join(REPO, "profiles", "pmc_traffic.json")
@@ -286,10 +286,10 @@ def roofline(llm, preset):
             "step_achieved_GBps": round(step_gbs, 1), "step_frac": round(step_gbs / HBM_PEAK_GBS, 4),
             "step_weight_bytes": llm.weight_bytes(),
             "per_token_us": {k: round(sum(v), 1) for k, v in per_kernel.items()},
-            "bytes_per_launch_all": bytes_of, "launches_per_layer": lpl,
+            "bytes_per_launch_all": bytes_of, "launches_per_step": nl,
             "note": ("timeline, events and attention bytes at decode position ~400 (as the PMC run)"
                      + ("; k_attn_in = the fused launch: q|k|v matvec + attention workgroups, its bytes "
-                        "include the K/V rows" if lpl == 4 else ""))}
+                        "include the K/V rows" if fused else ""))}
 
 
 def main():

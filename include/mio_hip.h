@@ -122,7 +122,8 @@ int mio_hip_codec_decode_stage(mio_hip_codec *c, const int32_t *codes, int n_cod
 
 /* ---------------- LLM decode ----------------
  * Replaces llama_model_load_from_file + llama_init_from_model (test-to-speech.cpp:47-49,
- * :103-108): GGUF "llama" / "qwen2" / "qwen3" with Q8_0 / Q4_K / Q6_K matrices (Q4_K_M),
+ * :103-108): GGUF "llama" / "mistral" / "qwen2" / "qwen3" / "lfm2" (short-conv hybrid) with
+ * Q8_0 / Q4_K / Q6_K matrices (Q4_K_M),
  * F16 KV cache of n_ctx positions (0 -> 2048, :104). */
 int mio_hip_llm_load(mio_hip_device *d, const char *gguf_path, int n_ctx, mio_hip_llm **out);
 void mio_hip_llm_free(mio_hip_llm *m);
@@ -162,8 +163,16 @@ int mio_hip_llm_generate_batch(mio_hip_llm *m, const int32_t *prompts, const int
                                int32_t allow_hi, int32_t eos0, int32_t eos1, int32_t check_interval,
                                int32_t *out_tokens, int32_t *n_out);
 
+/* Parity helpers: one decode step of `token` at `pos` (as mio_hip_llm_eval), its residual
+ * stream before layer 0 and after every layer into x_layers[(n_layer + 1) * n_embd] (and the
+ * logits when not null); the F16 K / V cache rows [0, n_pos) of layer il as
+ * [n_kv][n_pos][head_dim] half-precision bit patterns. */
+int mio_hip_llm_eval_layers(mio_hip_llm *m, int32_t token, int pos, float *x_layers, float *logits);
+int mio_hip_llm_kv_rows(mio_hip_llm *m, int il, int n_pos, uint16_t *k, uint16_t *v);
+
 /* Live timing of one decode-step kernel (which: 0 attn_in, 1 attention, 2 attn_out,
- * 3 ffn_in, 4 ffn_down of layer n_layer/2; 6 lm_head): `iters` back-to-back launches on
+ * 3 ffn_in, 4 ffn_down, 8 conv_in, 9 conv_out of the first layer at or after n_layer/2 that
+ * has it; 6 lm_head): `iters` back-to-back launches on
  * the runner's stream between HIP events (state/buffers of the last generate/eval).
  * *avg_ms = mean duration; *bytes = algorithmic HBM bytes per launch (attention: K/V rows of
  * positions <= the decode state's pos, q|k|v, chunk partials). */
@@ -175,14 +184,20 @@ int mio_hip_llm_trace_kernel(mio_hip_llm *m, int which, uint64_t *out);
 /* Diagnostic: one decode step replayed as a graph with the step timeline on; out has
  * max_launches * 512 * 8 slots: out[(i * 512 + w) * 8 + k] = start (k 0) / marks (1-6) /
  * end (7) (s_memrealtime, 100 MHz; 0 = not recorded) of workgroup w (mod 512) of launch i
- * (mio_hip_llm_step_layout launches per layer, then lm_head). Marks: matvec launches 1 =
+ * (the order of mio_hip_llm_step_kinds). Marks: matvec launches 1 =
  * weight loads issued, 2 = activations quantized; attention 1 = K/V loads issued, 2 = heads
  * prepared; 3-6 = prologue steps in -DMIO_TL_DIAG builds.
  * Advances the decode state. */
 int mio_hip_llm_timeline(mio_hip_llm *m, uint64_t *out, int max_launches, int *n_launches);
-/* Launches per decoder layer in the decode step: 5 (attention is a launch of its own), or 4
- * when the attention runs inside the attn_in launch (MIO_ATT_FUSED=1 at load). */
-int mio_hip_llm_step_layout(const mio_hip_llm *m, int *launches_per_layer);
+/* The launches of one decode step in order, as the `which` of mio_hip_llm_time_kernel: per
+ * layer 0 attn_in, 1 attention (absent when it runs inside attn_in, MIO_ATT_FUSED=1 at load),
+ * 2 attn_out, or for an lfm2 short-conv layer 8 conv_in, 9 conv_out; then 3 ffn_in, 4
+ * ffn_down; last 6 lm_head. *n = the count; kinds may be null (count only), else it needs
+ * cap >= *n entries. */
+int mio_hip_llm_step_kinds(const mio_hip_llm *m, int *kinds, int cap, int *n);
+/* lfm2 short-conv state of layer il: [4][n_embd] floats, slot p & 3 = the B*X row of position
+ * p (parity tests). set = 0 copies it out, 1 in. Error for an attention layer. */
+int mio_hip_llm_conv_ring(mio_hip_llm *m, int il, float *ring, int set);
 /* Wall time (ms) of mio_hip_llm_load: GGUF mmap, re-layout into pinned staging buffers,
  * asynchronous copies into the HBM weight arena (double-buffered). */
 int mio_hip_llm_load_ms(const mio_hip_llm *m, double *ms);

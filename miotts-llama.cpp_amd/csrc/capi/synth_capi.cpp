@@ -3,7 +3,7 @@
 #include "synth.h"
 
 extern "C" int mio_synth_codec_gguf(const char *path, int preset, uint64_t seed) {
-    MIO_REQUIRE(path && (preset == 0 || preset == 1), MIO_ERR_INVALID, "synth_codec: bad args");
+    MIO_REQUIRE(path && preset >= 0 && preset <= 3, MIO_ERR_INVALID, "synth_codec: bad args");
     mio::SynthCodecCfg c = mio::synth_codec_preset(preset);
     c.seed = seed;
     MIO_REQUIRE(mio::synth_write_codec(path, c), MIO_ERR_IO, "synth_codec: cannot write %s", path);
@@ -17,7 +17,7 @@ extern "C" int mio_synth_voice_gguf(const char *path, uint64_t seed) {
 }
 
 extern "C" int mio_synth_llm_gguf(const char *path, int preset, uint64_t seed) {
-    MIO_REQUIRE(path && preset >= 0 && preset <= 5, MIO_ERR_INVALID, "synth_llm: bad args");
+    MIO_REQUIRE(path && preset >= 0 && preset <= 8, MIO_ERR_INVALID, "synth_llm: bad args");
     mio::SynthLlmCfg c = mio::synth_llm_preset(preset);
     c.seed = seed;
     MIO_REQUIRE(mio::synth_write_llm(path, c), MIO_ERR_IO, "synth_llm: cannot write %s", path);

@@ -31,6 +31,8 @@ struct GemmArgs {
     const float *aux2;  // exp(beta) (snake)
     int f, trim, cout, rows_out;  // CONVT remap; HEAD: cout = n_freq
     int m_major;      // tile order (set by launch_gemm_f32)
+    int a_f16;        // B came from an F16 GGUF tensor: A is rounded to f16 (ggml mul_mat /
+                      // conv_transpose_1d convert src1 to the F16 vec_dot_type), f32 sums
 };
 
 // Conv1d k=taps, stride 1, "same" zero padding, as an implicit GEMM on f16 MFMA over the
@@ -67,8 +69,8 @@ void launch_groupnorm_apply(const float *x, int L, int C, int G, float eps, cons
 void launch_band_attention(const float *qkv, float *out, int S, int H, int window,
                            const float2 *rope /*[S][32] (cos,sin)*/, hipStream_t s);
 void launch_embed(const float *table, const int *codes, int T, int D, float *x, hipStream_t s);
-// y[r] = W[r][:] . silu(e) + b[r], W [R][A]
-void launch_cond_gemv(const float *W, const float *b, const float *e, int R, int A, float *y,
+// y[r] = W[r][:] . silu(e) + b[r], W [R][A]; e_f16: W was F16, silu(e) is rounded to f16
+void launch_cond_gemv(const float *W, const float *b, const float *e, int R, int A, float *y, int e_f16,
                       hipStream_t s);
 
 }  // namespace mio

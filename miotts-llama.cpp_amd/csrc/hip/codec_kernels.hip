@@ -121,7 +121,12 @@ __global__ __launch_bounds__(256 * KG) void gemm_f32_kernel(GemmArgs g) {
 #pragma unroll
         for (int i = 0; i < AV; ++i) {
             const int e = tid + i * NT, r = e / (BK / 4), c4 = e % (BK / 4);
-            *reinterpret_cast<float4 *>(&As[buf * BM * LDK + r * LDK + c4 * 4]) = ra[i];
+            float4 v = ra[i];
+            if (g.a_f16) {  // F16 weight: ggml rounds the activation to f16 (exact f32 products)
+                v.x = (float)(_Float16)v.x, v.y = (float)(_Float16)v.y;
+                v.z = (float)(_Float16)v.z, v.w = (float)(_Float16)v.w;
+            }
+            *reinterpret_cast<float4 *>(&As[buf * BM * LDK + r * LDK + c4 * 4]) = v;
         }
 #pragma unroll
         for (int i = 0; i < BV; ++i) {
@@ -617,12 +622,16 @@ __global__ void embed_kernel(const float *table, const int *codes, int T, int D,
 }
 
 __global__ __launch_bounds__(256) void cond_gemv_kernel(const float *W, const float *b, const float *e,
-                                                        int R, int A, float *y) {
+                                                        int R, int A, float *y, int e_f16) {
     const int lane = threadIdx.x & 63;
     const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (r >= R) return;
     float a = 0.0f;
-    for (int k = lane; k < A; k += 64) a = fmaf(W[(long)r * A + k], silu_f(e[k]), a);
+    for (int k = lane; k < A; k += 64) {
+        float se = silu_f(e[k]);
+        if (e_f16) se = (float)(_Float16)se;
+        a = fmaf(W[(long)r * A + k], se, a);
+    }
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) a += __shfl_xor(a, o);
     if (lane == 0) y[r] = a + b[r];
@@ -710,9 +719,9 @@ void launch_embed(const float *table, const int *codes, int T, int D, float *x, 
     hipLaunchKernelGGL(embed_kernel, dim3(T), dim3(256), 0, s, table, codes, T, D, x);
 }
 
-void launch_cond_gemv(const float *W, const float *b, const float *e, int R, int A, float *y,
+void launch_cond_gemv(const float *W, const float *b, const float *e, int R, int A, float *y, int e_f16,
                       hipStream_t s) {
-    hipLaunchKernelGGL(cond_gemv_kernel, dim3((R + 3) / 4), dim3(256), 0, s, W, b, e, R, A, y);
+    hipLaunchKernelGGL(cond_gemv_kernel, dim3((R + 3) / 4), dim3(256), 0, s, W, b, e, R, A, y, e_f16);
 }
 
 }  // namespace mio

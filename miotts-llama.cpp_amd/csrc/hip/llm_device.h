@@ -446,6 +446,86 @@ __device__ inline void plain_quant(const XRegs<XV> &xr, int K, bool kquant, cons
     quantize<XV>(s.xs, K, kquant, s.a);
 }
 
+// ------------------------------------------------------------------ lfm2 gated short conv
+// llama.cpp build_shortconv_block + ggml_ssm_conv (d_conv = kConvL = 3) for one token:
+// bcx = in_proj(norm x) = B | C | X, bx = B * X, y = C * conv with, per channel e,
+// conv = ((0 + x[p-2] w[e][0]) + x[p-1] w[e][1]) + bx w[e][2] (ggml's f32 sum from 0 over the
+// window in order), x[q] = the bx of position q, 0 before the sequence start. A window input
+// comes from a ring row of bx values, or from the bcx row of an earlier token of the same
+// launch (B * X recomputed: the same f32 product), or is absent (zeros).
+struct ConvPrev {
+    const float *p;  // null: zeros
+    int bcx;         // 1: p is a bcx row (3 K floats), 0: a bx row (K floats)
+};
+template <int XV>
+struct ConvRegs {
+    float4 b[XV], c[XV], x[XV], p1[XV], p2[XV], w[XV][3];
+};
+__device__ __forceinline__ float4 ld4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
+__device__ __forceinline__ float4 mul4(float4 a, float4 b) {
+    return make_float4(a.x * b.x, a.y * b.y, a.z * b.z, a.w * b.w);
+}
+__device__ __forceinline__ float4 conv_prev4(const ConvPrev &pv, int K, int e) {
+    if (!pv.p) return make_float4(0.f, 0.f, 0.f, 0.f);
+    if (!pv.bcx) return ld4(pv.p + e);
+    return mul4(ld4(pv.p + e), ld4(pv.p + 2 * K + e));
+}
+template <int XV>
+__device__ inline void conv_load(const float *bcx, const ConvPrev &p1, const ConvPrev &p2, const float *conv_w, int K,
+                                 ConvRegs<XV> &r) {
+#pragma unroll
+    for (int i = 0; i < XV; ++i) {
+        const int e = (MIO_TIDX + i * MT) * 4;
+        if (e < K) {
+            r.b[i] = ld4(bcx + e), r.c[i] = ld4(bcx + K + e), r.x[i] = ld4(bcx + 2 * K + e);
+            r.p1[i] = conv_prev4(p1, K, e), r.p2[i] = conv_prev4(p2, K, e);
+#pragma unroll
+            for (int j = 0; j < 3; ++j) r.w[i][j] = ld4(conv_w + (size_t)e * kConvL + 4 * j);
+        }
+    }
+}
+// the conv output into s.xs (and, when bx_out is set, this token's bx row into it), then the
+// plain re-quantization of the out_proj activation
+template <int XV>
+__device__ inline void conv_quant(const ConvRegs<XV> &r, int K, bool kquant, const Smem &s, float *bx_out,
+                                  unsigned long long *diag = nullptr) {
+#pragma unroll
+    for (int i = 0; i < XV; ++i) {
+        const int e = (MIO_TIDX + i * MT) * 4;
+        if (e < K) {
+            const float4 bx = mul4(r.b[i], r.x[i]);
+            const float v2[4] = {r.p2[i].x, r.p2[i].y, r.p2[i].z, r.p2[i].w};
+            const float v1[4] = {r.p1[i].x, r.p1[i].y, r.p1[i].z, r.p1[i].w};
+            const float v0[4] = {bx.x, bx.y, bx.z, bx.w};
+            const float c[4] = {r.c[i].x, r.c[i].y, r.c[i].z, r.c[i].w};
+            // taps of channels e..e+3: w[e + j][t] = flat[(e + j) * 3 + t] = 12 consecutive floats
+            const float w[12] = {r.w[i][0].x, r.w[i][0].y, r.w[i][0].z, r.w[i][0].w, r.w[i][1].x, r.w[i][1].y,
+                                 r.w[i][1].z, r.w[i][1].w, r.w[i][2].x, r.w[i][2].y, r.w[i][2].z, r.w[i][2].w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                float acc = 0.0f;
+                acc = acc + v2[j] * w[j * 3 + 0];
+                acc = acc + v1[j] * w[j * 3 + 1];
+                acc = acc + v0[j] * w[j * 3 + 2];
+                s.xs[e + j] = c[j] * acc;
+            }
+            if (bx_out) *reinterpret_cast<float4 *>(bx_out + e) = bx;
+        }
+    }
+    lds_barrier();
+    MIO_DIAG_STAMP(diag, 5, 0);
+    quantize<XV>(s.xs, K, kquant, s.a);
+}
+// keeps the conv operands' use below the first weight loads (x_after_weights)
+template <int XV>
+__device__ __forceinline__ void conv_after_weights(ConvRegs<XV> &r) {
+#pragma unroll
+    for (int i = 0; i < XV; ++i) {
+        asm volatile("" : "+v"(r.b[i].x), "+v"(r.b[i].y), "+v"(r.b[i].z), "+v"(r.b[i].w));
+        asm volatile("" : "+v"(r.x[i].x), "+v"(r.x[i].y), "+v"(r.x[i].z), "+v"(r.x[i].w));
+    }
+}
+
 // ------------------------------------------------------------------ typed row dots
 // exact integer sum of each 8-lane group, valid in lanes 8k+7
 __device__ __forceinline__ int sum8_i(int v) {

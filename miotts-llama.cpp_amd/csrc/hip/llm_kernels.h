@@ -17,6 +17,21 @@ struct QMat {
     const uint8_t *p0, *p1, *p2, *p3;
 };
 
+// Rows [r0, r0 + n) of q as a matrix of its own (every split-layout stream is row-major).
+inline QMat qmat_rows(const QMat &q, int r0, int n) {
+    size_t rb[4] = {0, 0, 0, 0};
+    switch (q.type) {
+        case 8: rb[0] = (size_t)q.k, rb[1] = (size_t)q.k / 32 * 2; break;
+        case 12: rb[0] = (size_t)q.k / 2, rb[1] = (size_t)q.k / 256 * 16; break;
+        case 14: rb[0] = (size_t)q.k / 2, rb[1] = (size_t)q.k / 4, rb[2] = (size_t)q.k / 16, rb[3] = (size_t)q.k / 256 * 2; break;
+        default: break;
+    }
+    QMat v = q;
+    v.rows = n;
+    v.p0 = q.p0 + rb[0] * r0, v.p1 = q.p1 + rb[1] * r0, v.p2 = q.p2 + rb[2] * r0, v.p3 = q.p3 + rb[3] * r0;
+    return v;
+}
+
 // Device-resident decode state (read by every kernel of a step; advanced by the sampler),
 // so one captured hipGraph replays every token without host involvement.
 // The sampler of step t runs inside step t+1's first launch (layer 0 attn_in) and the flush
@@ -44,10 +59,20 @@ struct SampleCfg {
     uint32_t epoch;      // >= 1, new for every generation / eval (q|k|v granule tags)
 };
 
+// lfm2 gated short conv: kernel width (shortconv.l_cache) and the ring of bx values kept per
+// layer (slot p & 3 holds position p; positions p-2, p-1 are read while p is written)
+constexpr int kConvL = 3;
+constexpr int kConvSlots = 4;
+
 struct LayerW {
     const float *attn_norm, *q_norm, *k_norm, *ffn_norm;
     const float *bqkv;  // [(H + 2 Hkv) hd] q|k|v biases (qwen2 attn_{q,k,v}.bias), or null
     QMat wq, wk, wv, wo, gate, up, down;
+    // lfm2 short-conv layer (conv != 0; wq..wo unused): in_proj [3 n_embd][n_embd] -> B | C | X,
+    // depthwise taps conv_w [n_embd][kConvL] f32, out_proj [n_embd][n_embd]
+    int conv;
+    QMat in_proj, out_proj;
+    const float *conv_w;
 };
 
 struct LlmDims {
@@ -75,6 +100,7 @@ struct LlmBuffers {
     int seq;                    // launch index within the step (timeline slot)
     uint2 *qkv_g;  // q|k|v rows as data-tagged granules {value, tag} for the attention workgroups
                    // of the fused attn_in launch, or null: attention is a launch of its own
+    float *ring;   // lfm2: [n_layer][kConvSlots][n_embd] short-conv inputs bx by position
 };
 
 // Batched prompt prefill (csrc/hip/llm_prefill.hip): up to kPrefillB prompt tokens per chunk
@@ -90,7 +116,8 @@ constexpr int kBatchMax = 16;
 // each per step, weights streamed once for all of them).
 struct PrefillBuffers {
     float *x;            // [kPrefillB][n_embd] residual streams
-    float *qkv;          // [kPrefillB][(H + 2 Hkv) hd]; q rows are RoPE'd in place
+    float *qkv;          // [kPrefillB][(H + 2 Hkv) hd]; q rows are RoPE'd in place (lfm2 conv
+                         // layers: [kPrefillB][3 n_embd] B | C | X rows)
     float *h;            // [kPrefillB][n_ff]
     float *part;         // [kPrefillB][H][max_splits][hd + 4] attention chunk partials
     const float2 *rope;  // [n_ctx][hd/2]
@@ -99,6 +126,8 @@ struct PrefillBuffers {
     const int *seq;      // sequence (KV cache) of token t: seq[t * seq_stride]
     int pos_stride, seq_stride;
     size_t seq_kv;       // K (and V) cache elements per sequence: [seq][layer][kv head][n_ctx][hd]
+    float *ring;         // lfm2 short-conv rings [seq][n_layer][kConvSlots][n_embd], or null
+    size_t seq_ring;     // ring elements per sequence
     char *act;           // [kPrefillB] quantized activation records of the next matvec
 };
 // bytes of the act records (pb.act) for K up to k_max
@@ -132,7 +161,8 @@ void launch_batch_embed(const LlmDims &d, const QMat &tok_embd, const PrefillBuf
                         int B, hipStream_t s);
 
 // Launch one kernel of a decode step (which: 0 attn_in, 1 attention, 2 attn_out, 3 ffn_in,
-// 4 ffn_down of layer il; 6 lm_head, 7 sampler) on stream s.
+// 4 ffn_down of layer il; 6 lm_head, 7 sampler; lfm2 short-conv layers: 8 conv_in, 9
+// conv_out in place of 0..2) on stream s.
 void launch_step_kernel(int which, const LlmDims &d, const LayerW *layers, int il, _Float16 *kcache,
                         _Float16 *vcache, const float *out_norm, const QMat &lm, const QMat &tok_embd,
                         const LlmBuffers &b, hipStream_t s);

@@ -9,6 +9,8 @@
 //   k_attn_out  chunk merge + re-quantization in the prologue -> O matvec -> x += .
 //   k_ffn_in    RMSNorm(x) -> re-quantize -> gate & up matvec -> silu(g)*u
 //   k_ffn_down  re-quantize h -> down matvec -> x += .
+// An lfm2 short-conv layer replaces the first three with k_attn_in over in_proj (B | C | X)
+// and k_conv_out (gated depthwise conv over a 4-slot ring of earlier positions -> out_proj).
 // then k_lm_head (final RMSNorm + logits + per-workgroup Gumbel-max). The token is drawn from
 // those partials by the next step's layer-0 attn_in (its prologue, beside its first weight
 // loads) or, after the last step of a run, by k_sample (token, next embedding, position++).
@@ -71,6 +73,45 @@ __global__ __launch_bounds__(MT) void k_attn_out(LlmDims d, QMat wo, LlmBuffers 
     MIO_TRACE(b, 2);
     MIO_TL_MARK(b, 2);
     stream_rows<T, NP, 1, SU, MIO_SMALL_AUX>(wo, wo, lo, hi, ga, gb, s.a, [&](int row, float v, float) {
+        const float r = lane_value(xres, row - lo);
+        if ((threadIdx.x & 63) == 0) b.x[row] = v + r;
+    });
+    MIO_TL_END(b);
+    MIO_TRACE(b, 15);
+}
+
+// lfm2 short-conv layer, second launch (the first is k_attn_in over in_proj: bcx in b.qkv):
+// the gated conv of this position (conv_load / conv_quant: bx = B * X, the window over the
+// layer's ring, y = C * conv) re-quantized in the prologue -> out_proj matvec -> x += .
+// Workgroup 0 stores this position's bx into ring slot pos & 3; the window reads slots of
+// pos - 1 and pos - 2, so no workgroup reads what another writes in this launch.
+template <int NP, int T, int SU, bool DG>
+__global__ __launch_bounds__(MT) void k_conv_out(LlmDims d, QMat wo, const float *conv_w, float *ring, LlmBuffers b) {
+    constexpr bool kDiag = DG;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    MIO_TRACE(b, 0);
+    MIO_TL_BEGIN(b);
+    const int K = wo.k;
+    const Smem s = carve(smem, K);
+    const int pos = cur_pos(b.st, d);
+    const ConvPrev p1{pos >= 1 ? ring + (size_t)((pos - 1) & (kConvSlots - 1)) * K : nullptr, 0};
+    const ConvPrev p2{pos >= 2 ? ring + (size_t)((pos - 2) & (kConvSlots - 1)) * K : nullptr, 0};
+    ConvRegs<NP> cr;
+    conv_load(b.qkv, p1, p2, conv_w, K, cr);
+    int lo, hi;
+    wave_range(d, wo.rows, lo, hi);
+    const float xres = load_resid(b.x, lo, hi);
+    x_gate();
+    Frag ga[Cfg<NP, SU>::U], gb[Cfg<NP, SU>::U];
+    load_first<T, NP, 1, SU>(wo, wo, lo, hi, ga, gb);
+    conv_after_weights(cr);
+    MIO_TRACE(b, 1);
+    MIO_TL_MARK1(b);
+    conv_quant(cr, K, T != 8, s, blockIdx.x == 0 ? ring + (size_t)(pos & (kConvSlots - 1)) * K : nullptr,
+               MIO_TL_DIAGSLOT(b));
+    MIO_TRACE(b, 2);
+    MIO_TL_MARK(b, 2);
+    stream_rows<T, NP, 1, SU>(wo, wo, lo, hi, ga, gb, s.a, [&](int row, float v, float) {
         const float r = lane_value(xres, row - lo);
         if ((threadIdx.x & 63) == 0) b.x[row] = v + r;
     });
@@ -397,7 +438,8 @@ int pick_su(int units, int np) {
 }
 // Launch one kernel of the step: which = 0 attn_in, 1 attention, 2 attn_out (+ chunk
 // merge), 3 ffn_in, 4 ffn_down (layer il), 5 (unused: the final norm is fused into
-// lm_head), 6 lm_head, 7 flush sampler. Layer 0's attn_in samples the pending token of the
+// lm_head), 6 lm_head, 7 flush sampler; lfm2 short-conv layer il: 8 conv_in (RMSNorm +
+// in_proj, the attn_in kernel), 9 conv_out (gated conv + out_proj). Layer 0's attn_in samples the pending token of the
 // previous step and layer 0's ffn_in advances pos / step (StepState.pending).
 void launch_step_kernel(int which, const LlmDims &d, const LayerW *layers, int il, _Float16 *kcache,
                         _Float16 *vcache, const float *out_norm, const QMat &lm, const QMat &tok_embd,
@@ -448,6 +490,31 @@ void launch_step_kernel(int which, const LlmDims &d, const LayerW *layers, int i
                 dispatch_su<NP>(pick_su(max_wave_units(L.down.rows, grid, NP, 1), NP), [&]<int SU>() {
                     hipLaunchKernelGGL((k_ffn_down<NP, T, SU, DG>), dim3(grid), dim3(MT), mv_lds(L.down.k), s, d, L.down,
                                        b);
+                });
+            });
+            break;
+        }
+        case 8: {  // lfm2 conv_in: RMSNorm + in_proj as the attn_in launch (B | C rows, X rows)
+            const LayerW &L = layers[il];
+            const int n = d.n_embd;
+            LayerW V = L;
+            V.wq = qmat_rows(L.in_proj, 0, 2 * n);
+            V.wk = qmat_rows(L.in_proj, 2 * n, 0);
+            V.wv = qmat_rows(L.in_proj, 2 * n, n);
+            V.q_norm = V.k_norm = V.bqkv = nullptr;
+            LlmBuffers bv = b;
+            bv.qkv_g = nullptr;  // no attention workgroups
+            launch_attn_in(d, V, il, nullptr, nullptr, tok_embd, bv, DG, s);
+            break;
+        }
+        case 9: {
+            const LayerW &L = layers[il];
+            const int grid = matvec_grid(d, L.out_proj.rows);
+            float *ring = b.ring + (size_t)il * kConvSlots * d.n_embd;
+            dispatch_nt(L.out_proj.k, L.out_proj.type, [&]<int NP, int T>() {
+                dispatch_su<NP>(pick_su(max_wave_units(L.out_proj.rows, grid, NP, 1), NP), [&]<int SU>() {
+                    hipLaunchKernelGGL((k_conv_out<NP, T, SU, DG>), dim3(grid), dim3(MT), mv_lds(L.out_proj.k), s, d,
+                                       L.out_proj, L.conv_w, ring, b);
                 });
             });
             break;

@@ -13,6 +13,9 @@
 //   k_pf_attn_out  per-token chunk merge + quantize -> O matvec -> x += .
 //   k_pf_ffn_in    RMSNorm + quantize -> gate|up -> silu(g)*u
 //   k_pf_ffn_down  quantize -> down -> x += .
+// lfm2 short-conv layers: in_proj on the matrix cores, k_bt_conv (gated conv per token, the
+// window from earlier tokens of the chunk or the sequence's ring), k_bt_conv_state (ring),
+// out_proj.
 // Arithmetic is the decode step's, token by token, in the same order (same quantizers,
 // same per-superblock integer sums, the same pass order per row, the same online-softmax
 // order): the K/V cache and the last token's logits equal a token-by-token decode bit for
@@ -207,6 +210,52 @@ __global__ __launch_bounds__(MT) void k_bt_quant(LlmDims d, const float *src, in
     const uint4 *l = reinterpret_cast<const uint4 *>(s.a.qs);
     uint4 *g = reinterpret_cast<uint4 *>(pb.act + (size_t)t * act_bytes(K));
     for (int i = threadIdx.x; i < n16; i += MT) g[i] = l[i];
+}
+
+// lfm2 short-conv layer, one workgroup per token t: the gated conv of t (conv_load /
+// conv_quant, the decode step's prologue) quantized into t's act record. Window inputs of
+// positions pos - 1, pos - 2: the bcx rows of the tokens before t in this launch when they are
+// that sequence's previous positions, else the sequence's ring (written by an earlier chunk or
+// decode step), zeros before the sequence start. ring = layer il's ring of sequence 0.
+template <int NP>
+__global__ __launch_bounds__(MT) void k_bt_conv(LlmDims d, const float *conv_w, const float *ring, int kq,
+                                                PrefillBuffers pb) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int t = blockIdx.x, K = d.n_embd;
+    const size_t CW = (size_t)3 * K;
+    const Smem s = carve(smem, K);
+    const int pos = pb.pos[t * pb.pos_stride], sq = pb.seq[t * pb.seq_stride];
+    const float *rs = ring + (size_t)sq * pb.seq_ring;
+    ConvPrev pv[2];
+#pragma unroll
+    for (int k = 1; k <= 2; ++k) {
+        const int p = pos - k;
+        if (p < 0)
+            pv[k - 1] = ConvPrev{nullptr, 0};
+        else if (t >= k && pb.seq[(t - k) * pb.seq_stride] == sq && pb.pos[(t - k) * pb.pos_stride] == p)
+            pv[k - 1] = ConvPrev{pb.qkv + (t - k) * CW, 1};
+        else
+            pv[k - 1] = ConvPrev{rs + (size_t)(p & (kConvSlots - 1)) * K, 0};
+    }
+    ConvRegs<NP> cr;
+    conv_load(pb.qkv + t * CW, pv[0], pv[1], conv_w, K, cr);
+    conv_quant(cr, K, kq != 0, s, nullptr);
+    const int n16 = (int)(act_bytes(K) / 16);
+    const uint4 *l = reinterpret_cast<const uint4 *>(s.a.qs);
+    uint4 *g = reinterpret_cast<uint4 *>(pb.act + (size_t)t * act_bytes(K));
+    for (int i = threadIdx.x; i < n16; i += MT) g[i] = l[i];
+}
+
+// After k_bt_conv: the bx rows of each sequence's last two positions in this launch go to
+// its ring (a later chunk or decode step reads them). Sequences occupy consecutive tokens
+// with consecutive positions, so token t is among them unless t + 2 continues its run.
+__global__ __launch_bounds__(ST) void k_bt_conv_state(LlmDims d, float *ring, PrefillBuffers pb, int nt) {
+    const int t = blockIdx.x, K = d.n_embd;
+    const int pos = pb.pos[t * pb.pos_stride], sq = pb.seq[t * pb.seq_stride];
+    if (t + 2 < nt && pb.seq[(t + 2) * pb.seq_stride] == sq && pb.pos[(t + 2) * pb.pos_stride] == pos + 2) return;
+    const float *row = pb.qkv + (size_t)t * 3 * K;
+    float *dst = ring + (size_t)sq * pb.seq_ring + (size_t)(pos & (kConvSlots - 1)) * K;
+    for (int e = threadIdx.x; e < K; e += ST) dst[e] = row[e] * row[2 * K + e];
 }
 
 // Residual rows [lo, hi) of every token (row stride E) in two registers per lane: entry
@@ -600,63 +649,85 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
     const int QD = (d.n_head + 2 * d.n_kv) * d.hd;
     for (int il = 0; il < n_layer; ++il) {
         const LayerW &L = layers[il];
-        _Float16 *kc = kcache + il * layer_kv, *vc = vcache + il * layer_kv;
-        launch_quant(d, 0, pb.x, d.n_embd, L.attn_norm, L.wq.type != 8, pb, nt, s);
-        if (mmq) {
-            const MmqSeg sg[3] = {{L.wq, mmq_tiles(L.wq.rows), 0}, {L.wk, mmq_tiles(L.wk.rows), L.wq.rows},
-                                  {L.wv, mmq_tiles(L.wv.rows), L.wq.rows + L.wk.rows}};
-            const int ty[3] = {L.wq.type, L.wk.type, L.wv.type};
-            launch_mmq(sg, ty, 3, MMQ_STORE, MmqArgs{pb.act, act_bytes(d.n_embd), d.n_embd, nt, pb.qkv, QD, {}}, s);
-        } else {
-            int GW, g_qk;
-            attn_in_grid(d, L, GW, g_qk);
-            over_tokens(d.n_embd, 0, [&](int, int n, const PrefillBuffers &q) {
-                const size_t lds = pf_lds_bytes(d.n_embd, n, 0);
-                dispatch_nt(d.n_embd, L.wq.type, [&]<int NP, int TQ>() {
-                    auto go = [&]<int TV>() {
-                        allow_lds(k_pf_attn_in<NP, TQ, TV>);
-                        hipLaunchKernelGGL((k_pf_attn_in<NP, TQ, TV>), dim3(GW), dim3(MT), lds, s, d, L.attn_norm,
-                                           L.wq, L.wk, L.wv, g_qk, q, n);
-                    };
-                    if constexpr (TQ == 8) {
-                        go.template operator()<8>();
-                    } else {
-                        if (L.wv.type == 14)
-                            go.template operator()<14>();
-                        else
-                            go.template operator()<12>();
-                    }
-                });
-            });
-        }
-        {
-            const dim3 grid(d.n_head + d.n_kv, nt);
-            if (d.hd == 128)
-                hipLaunchKernelGGL((k_pf_rope<128>), grid, dim3(64), 0, s, d, L.q_norm, L.k_norm, L.bqkv, kc, vc, pb);
+        if (L.conv) {
+            // lfm2 short-conv layer: RMSNorm + in_proj -> B | C | X rows, the gated conv (k_bt_conv)
+            // -> out_proj -> x += ., ring update. Always on the matrix cores (bit-exact with the
+            // decode step's matvec at any token count).
+            const int n = d.n_embd;
+            float *ring = pb.ring + (size_t)il * kConvSlots * n;
+            launch_quant(d, 0, pb.x, n, L.attn_norm, L.in_proj.type != 8, pb, nt, s);
+            const MmqSeg sg{L.in_proj, mmq_tiles(L.in_proj.rows), 0};
+            launch_mmq(&sg, &L.in_proj.type, 1, MMQ_STORE, MmqArgs{pb.act, act_bytes(n), n, nt, pb.qkv, 3 * n, {}}, s);
+            const int np = pick_np(n);
+            const int kq = L.out_proj.type != 8;
+            if (np == 1)
+                hipLaunchKernelGGL((k_bt_conv<1>), dim3(nt), dim3(MT), smem_bytes(n), s, d, L.conv_w, ring, kq, pb);
+            else if (np == 3)
+                hipLaunchKernelGGL((k_bt_conv<3>), dim3(nt), dim3(MT), smem_bytes(n), s, d, L.conv_w, ring, kq, pb);
             else
-                hipLaunchKernelGGL((k_pf_rope<64>), grid, dim3(64), 0, s, d, L.q_norm, L.k_norm, L.bqkv, kc, vc, pb);
-        }
-        {
-            const dim3 grid(d.n_kv * nt, n_chunks);
-            if (d.hd == 128)
-                launch_pf_attention<128>(G, grid, s, d, kc, vc, pb);
-            else
-                launch_pf_attention<64>(G, grid, s, d, kc, vc, pb);
-        }
-        launch_quant(d, 2, nullptr, L.wo.k, nullptr, L.wo.type != 8, pb, nt, s);
-        if (mmq) {
-            const MmqSeg sg{L.wo, mmq_tiles(L.wo.rows), 0};
-            launch_mmq(&sg, &L.wo.type, 1, MMQ_RESID, MmqArgs{pb.act, act_bytes(L.wo.k), L.wo.k, nt, pb.x, d.n_embd, {}},
-                       s);
+                hipLaunchKernelGGL((k_bt_conv<6>), dim3(nt), dim3(MT), smem_bytes(n), s, d, L.conv_w, ring, kq, pb);
+            hipLaunchKernelGGL(k_bt_conv_state, dim3(nt), dim3(ST), 0, s, d, ring, pb, nt);
+            const MmqSeg so{L.out_proj, mmq_tiles(L.out_proj.rows), 0};
+            launch_mmq(&so, &L.out_proj.type, 1, MMQ_RESID, MmqArgs{pb.act, act_bytes(n), n, nt, pb.x, n, {}}, s);
         } else {
-            const int grid = matvec_grid(d, L.wo.rows), rpw = rows_per_wave(L.wo.rows, grid);
-            over_tokens(L.wo.k, rpw, [&](int, int n, const PrefillBuffers &q) {
-                dispatch_nt(L.wo.k, L.wo.type, [&]<int NP, int T>() {
-                    allow_lds(k_pf_attn_out<NP, T>);
-                    hipLaunchKernelGGL((k_pf_attn_out<NP, T>), dim3(grid), dim3(MT), pf_lds_bytes(L.wo.k, n, rpw), s,
-                                       d, L.wo, q, n, rpw);
+            _Float16 *kc = kcache + il * layer_kv, *vc = vcache + il * layer_kv;
+            launch_quant(d, 0, pb.x, d.n_embd, L.attn_norm, L.wq.type != 8, pb, nt, s);
+            if (mmq) {
+                const MmqSeg sg[3] = {{L.wq, mmq_tiles(L.wq.rows), 0}, {L.wk, mmq_tiles(L.wk.rows), L.wq.rows},
+                                      {L.wv, mmq_tiles(L.wv.rows), L.wq.rows + L.wk.rows}};
+                const int ty[3] = {L.wq.type, L.wk.type, L.wv.type};
+                launch_mmq(sg, ty, 3, MMQ_STORE, MmqArgs{pb.act, act_bytes(d.n_embd), d.n_embd, nt, pb.qkv, QD, {}}, s);
+            } else {
+                int GW, g_qk;
+                attn_in_grid(d, L, GW, g_qk);
+                over_tokens(d.n_embd, 0, [&](int, int n, const PrefillBuffers &q) {
+                    const size_t lds = pf_lds_bytes(d.n_embd, n, 0);
+                    dispatch_nt(d.n_embd, L.wq.type, [&]<int NP, int TQ>() {
+                        auto go = [&]<int TV>() {
+                            allow_lds(k_pf_attn_in<NP, TQ, TV>);
+                            hipLaunchKernelGGL((k_pf_attn_in<NP, TQ, TV>), dim3(GW), dim3(MT), lds, s, d, L.attn_norm,
+                                               L.wq, L.wk, L.wv, g_qk, q, n);
+                        };
+                        if constexpr (TQ == 8) {
+                            go.template operator()<8>();
+                        } else {
+                            if (L.wv.type == 14)
+                                go.template operator()<14>();
+                            else
+                                go.template operator()<12>();
+                        }
+                    });
                 });
-            });
+            }
+            {
+                const dim3 grid(d.n_head + d.n_kv, nt);
+                if (d.hd == 128)
+                    hipLaunchKernelGGL((k_pf_rope<128>), grid, dim3(64), 0, s, d, L.q_norm, L.k_norm, L.bqkv, kc, vc, pb);
+                else
+                    hipLaunchKernelGGL((k_pf_rope<64>), grid, dim3(64), 0, s, d, L.q_norm, L.k_norm, L.bqkv, kc, vc, pb);
+            }
+            {
+                const dim3 grid(d.n_kv * nt, n_chunks);
+                if (d.hd == 128)
+                    launch_pf_attention<128>(G, grid, s, d, kc, vc, pb);
+                else
+                    launch_pf_attention<64>(G, grid, s, d, kc, vc, pb);
+            }
+            launch_quant(d, 2, nullptr, L.wo.k, nullptr, L.wo.type != 8, pb, nt, s);
+            if (mmq) {
+                const MmqSeg sg{L.wo, mmq_tiles(L.wo.rows), 0};
+                launch_mmq(&sg, &L.wo.type, 1, MMQ_RESID, MmqArgs{pb.act, act_bytes(L.wo.k), L.wo.k, nt, pb.x, d.n_embd, {}},
+                           s);
+            } else {
+                const int grid = matvec_grid(d, L.wo.rows), rpw = rows_per_wave(L.wo.rows, grid);
+                over_tokens(L.wo.k, rpw, [&](int, int n, const PrefillBuffers &q) {
+                    dispatch_nt(L.wo.k, L.wo.type, [&]<int NP, int T>() {
+                        allow_lds(k_pf_attn_out<NP, T>);
+                        hipLaunchKernelGGL((k_pf_attn_out<NP, T>), dim3(grid), dim3(MT), pf_lds_bytes(L.wo.k, n, rpw), s,
+                                           d, L.wo, q, n, rpw);
+                    });
+                });
+            }
         }
         launch_quant(d, 0, pb.x, d.n_embd, L.ffn_norm, L.gate.type != 8, pb, nt, s);
         if (mmq) {

@@ -14,6 +14,7 @@
 //    to the fused iSTFT without leaving the GPU.
 #include <cmath>
 #include <cstring>
+#include <initializer_list>
 #include <string>
 #include <vector>
 
@@ -30,15 +31,20 @@ struct ResW {
     float *gn1_w, *gn1_b, *gn2_w, *gn2_b, *b1, *b2;
     _Float16 *w1, *w2;
 };
+// h16_*: the matrix came from an F16 GGUF tensor, so its GEMM rounds the activation to f16
+// (GemmArgs::a_f16; ggml mul_mat's F16 vec_dot_type)
 struct PreW {
     float *ln1_w, *ln1_b, *ln2_w, *ln2_b, *qkv, *wo, *gu, *wd;
+    int h16_qkv, h16_wo, h16_gu, h16_wd;
 };
 struct DecW {
     float *qkv, *wo, *gu, *wd;
+    int h16_qkv, h16_wo, h16_gu, h16_wd;
 };
 struct UpW {
     float *w, *b, *alpha_e, *beta_e;
     int f, K, taps, trim, Cin, Cout;
+    int h16;
     ResW res;
 };
 
@@ -58,6 +64,7 @@ struct mio_hip_codec {
     std::vector<PreW> pre;
     float *pre_norm_w = nullptr, *pre_norm_b = nullptr, *pre_out_w = nullptr, *pre_out_b = nullptr;
     float *ups_w = nullptr, *ups_b = nullptr;
+    int h16_pre_out = 0, h16_ups = 0, h16_cond = 0, h16_op = 0, h16_head = 0;
     std::vector<ResW> prior, post;
     std::vector<DecW> dec;
     float *cond_w = nullptr, *cond_b = nullptr;
@@ -146,6 +153,28 @@ struct Loader {
         return (T *)p;
     }
     float *vec(const std::string &name, size_t n) { return up(f32(name, n)); }
+    // 1 when every named tensor is F16, 0 when none is; a mix (one GEMM can round its
+    // activation one way only) is refused
+    int f16(std::initializer_list<std::string> names) {
+        int n16 = 0, n = 0;
+        for (const std::string &nm : names) {
+            const mio::GgufTensor *t = g.tensor(nm);
+            n += t != nullptr;
+            n16 += t && t->type == mio::GGML_F16;
+        }
+        if (n16 && n16 != n) {
+            if (ok) mio::set_error("miocodec: %s and the matrices fused with it mix F16 and F32", names.begin()->c_str());
+            ok = false;
+        }
+        return n16 ? 1 : 0;
+    }
+    // exp of a (log-scale) snake parameter; ggml_exp of an F16 tensor stays F16
+    std::vector<float> snake_exp(const std::string &name, size_t n) {
+        std::vector<float> v = f32(name, n);
+        const bool h = f16({name});
+        for (auto &x : v) x = h ? (float)(_Float16)expf(x) : expf(x);
+        return v;
+    }
 
     // conv1d kernel ggml [K][Cin][Cout] (mem [co][ci][k]) -> f16 [co][k*Cin + ci]
     _Float16 *conv_w(const std::string &name, int K, int Cin, int Cout) {
@@ -310,8 +339,9 @@ int plan_ws(mio_hip_codec *c, int T, Ws &w, bool alloc, size_t *bytes = nullptr)
     return MIO_OK;
 }
 
-mio::GemmArgs gemm(const float *A, int K, int M, const float *B, int N, float *C, int ldc) {
+mio::GemmArgs gemm(const float *A, int K, int M, const float *B, int N, float *C, int ldc, int a_f16 = 0) {
     mio::GemmArgs g{};
+    g.a_f16 = a_f16;
     g.A = A;
     g.a_seg = K;
     g.a_row_off = 0;
@@ -367,16 +397,16 @@ int run_decode(mio_hip_codec *c, Ws &w, hipStream_t s, int stop_stage, const flo
     for (int i = 0; i < c->pre_layers; ++i) {
         const PreW &p = c->pre[i];
         mio::launch_rownorm(w.xT, w.hT, Tw, Dp, c->eps, 1, p.ln1_w, p.ln1_b, s);
-        mio::launch_gemm_f32(gemm(w.hT, Dp, Tw, p.qkv, 3 * Dp, w.qkvT, 3 * Dp), mio::EPI_STORE, s);
+        mio::launch_gemm_f32(gemm(w.hT, Dp, Tw, p.qkv, 3 * Dp, w.qkvT, 3 * Dp, p.h16_qkv), mio::EPI_STORE, s);
         mio::launch_band_attention(w.qkvT, w.aT, Tw, c->pre_heads, c->pre_win, rope_w, s);
-        mio::launch_gemm_f32(gemm(w.aT, Dp, Tw, p.wo, Dp, w.xT, Dp), mio::EPI_RESID, s);
+        mio::launch_gemm_f32(gemm(w.aT, Dp, Tw, p.wo, Dp, w.xT, Dp, p.h16_wo), mio::EPI_RESID, s);
         mio::launch_rownorm(w.xT, w.hT, Tw, Dp, c->eps, 1, p.ln2_w, p.ln2_b, s);
-        mio::launch_gemm_f32(gemm(w.hT, Dp, Tw, p.gu, 2 * c->pre_ff, w.fT, c->pre_ff), mio::EPI_SWIGLU, s);
-        mio::launch_gemm_f32(gemm(w.fT, c->pre_ff, Tw, p.wd, Dp, w.xT, Dp), mio::EPI_RESID, s);
+        mio::launch_gemm_f32(gemm(w.hT, Dp, Tw, p.gu, 2 * c->pre_ff, w.fT, c->pre_ff, p.h16_gu), mio::EPI_SWIGLU, s);
+        mio::launch_gemm_f32(gemm(w.fT, c->pre_ff, Tw, p.wd, Dp, w.xT, Dp, p.h16_wd), mio::EPI_RESID, s);
     }
     mio::launch_rownorm(w.xT, w.hT, Tw, Dp, c->eps, 1, c->pre_norm_w, c->pre_norm_b, s);
     {
-        mio::GemmArgs g = gemm(w.hT, Dp, Tw, c->pre_out_w, Dd, w.yT + (size_t)s0 * Dd, Dd);
+        mio::GemmArgs g = gemm(w.hT, Dp, Tw, c->pre_out_w, Dd, w.yT + (size_t)s0 * Dd, Dd, c->h16_pre_out);
         g.bias = c->pre_out_b;
         mio::launch_gemm_f32(g, mio::EPI_STORE, s);
     }
@@ -386,7 +416,7 @@ int run_decode(mio_hip_codec *c, Ws &w, hipStream_t s, int stop_stage, const flo
     if (done(w.yT, T, Dd)) return MIO_OK;
     // 3. wave_upsample ConvT k=2 s=2 (:622-626): one GEMM, N = 2*Dd, remapped rows
     {
-        mio::GemmArgs g = gemm(w.yT, Dd, T, c->ups_w, 2 * Dd, w.xS, Dd);
+        mio::GemmArgs g = gemm(w.yT, Dd, T, c->ups_w, 2 * Dd, w.xS, Dd, c->h16_ups);
         g.bias = c->ups_b, g.f = 2, g.trim = 0, g.cout = Dd, g.rows_out = S;
         mio::launch_gemm_f32(g, mio::EPI_CONVT, s);
     }
@@ -395,22 +425,22 @@ int run_decode(mio_hip_codec *c, Ws &w, hipStream_t s, int stop_stage, const flo
     for (auto &r : c->prior) resnet(c, r, w.xS, w.hS, S, Dd, w, s);
     if (done(w.xS, S, Dd)) return MIO_OK;
     // 5. AdaLN-Zero decoder (:640-660); all conditioning vectors in one GEMV
-    mio::launch_cond_gemv(c->cond_w, c->cond_b, w.emb, c->cond_rows, c->adaln, w.cond, s);
+    mio::launch_cond_gemv(c->cond_w, c->cond_b, w.emb, c->cond_rows, c->adaln, w.cond, c->h16_cond, s);
     for (int i = 0; i < c->dec_layers; ++i) {
         const DecW &p = c->dec[i];
         const float *ca = w.cond + (size_t)i * 6 * Dd, *cf = ca + 3 * Dd;
         mio::launch_rownorm(w.xS, w.hS, S, Dd, c->eps, 2, ca, ca + Dd, s);
-        mio::launch_gemm_f32(gemm(w.hS, Dd, S, p.qkv, 3 * Dd, w.qkvS, 3 * Dd), mio::EPI_STORE, s);
+        mio::launch_gemm_f32(gemm(w.hS, Dd, S, p.qkv, 3 * Dd, w.qkvS, 3 * Dd, p.h16_qkv), mio::EPI_STORE, s);
         mio::launch_band_attention(w.qkvS, w.aS, S, c->dec_heads, c->dec_win, c->rope, s);
         {
-            mio::GemmArgs g = gemm(w.aS, Dd, S, p.wo, Dd, w.xS, Dd);
+            mio::GemmArgs g = gemm(w.aS, Dd, S, p.wo, Dd, w.xS, Dd, p.h16_wo);
             g.aux = ca + 2 * Dd;
             mio::launch_gemm_f32(g, mio::EPI_GATED, s);
         }
         mio::launch_rownorm(w.xS, w.hS, S, Dd, c->eps, 2, cf, cf + Dd, s);
-        mio::launch_gemm_f32(gemm(w.hS, Dd, S, p.gu, 2 * c->dec_ff, w.fS, c->dec_ff), mio::EPI_SWIGLU, s);
+        mio::launch_gemm_f32(gemm(w.hS, Dd, S, p.gu, 2 * c->dec_ff, w.fS, c->dec_ff, p.h16_gu), mio::EPI_SWIGLU, s);
         {
-            mio::GemmArgs g = gemm(w.fS, c->dec_ff, S, p.wd, Dd, w.xS, Dd);
+            mio::GemmArgs g = gemm(w.fS, c->dec_ff, S, p.wd, Dd, w.xS, Dd, p.h16_wd);
             g.aux = cf + 2 * Dd;
             mio::launch_gemm_f32(g, mio::EPI_GATED, s);
         }
@@ -434,7 +464,7 @@ int run_decode(mio_hip_codec *c, Ws &w, hipStream_t s, int stop_stage, const flo
         g.A = src, g.a_seg = u.Cin, g.a_row_off = -(u.taps - 1), g.a_rows = Lin;
         g.B = u.w, g.M = M, g.N = u.f * u.Cout, g.K = u.taps * u.Cin;
         g.C = w.u[st], g.ldc = u.Cout, g.bias = u.b, g.aux = u.alpha_e, g.aux2 = u.beta_e;
-        g.f = u.f, g.trim = u.trim, g.cout = u.Cout, g.rows_out = Lout;
+        g.f = u.f, g.trim = u.trim, g.cout = u.Cout, g.rows_out = Lout, g.a_f16 = u.h16;
         mio::launch_gemm_f32(g, mio::EPI_CONVT_SNAKE, s);
         resnet(c, u.res, w.u[st], w.t[st], Lout, u.Cout, w, s);
         src = w.u[st];
@@ -444,14 +474,14 @@ int run_decode(mio_hip_codec *c, Ws &w, hipStream_t s, int stop_stage, const flo
     const int L = Lin;
     // 8. out_proj + out_snake (:711-725)
     {
-        mio::GemmArgs g = gemm(src, c->c_last, L, c->op_w, Dd, w.op, Dd);
+        mio::GemmArgs g = gemm(src, c->c_last, L, c->op_w, Dd, w.op, Dd, c->h16_op);
         g.bias = c->op_b, g.aux = c->op_ae, g.aux2 = c->op_be;
         mio::launch_gemm_f32(g, mio::EPI_SNAKE, s);
     }
     if (done(w.op, L, Dd)) return MIO_OK;
     // 9. iSTFT head (:728-737) written as [frame][bin][re,im] (:801-808)
     {
-        mio::GemmArgs g = gemm(w.op, Dd, L, c->head_w, 2 * c->nfp, w.spec, 2 * c->n_freq);
+        mio::GemmArgs g = gemm(w.op, Dd, L, c->head_w, 2 * c->nfp, w.spec, 2 * c->n_freq, c->h16_head);
         g.bias = c->head_b, g.cout = c->n_freq;
         mio::launch_gemm_f32(g, mio::EPI_HEAD, s);
     }
@@ -540,12 +570,18 @@ extern "C" int mio_hip_codec_load(mio_hip_device *d, const char *path, mio_hip_c
         w.ln2_b = ld.vec(p + "ffn_norm.bias", Dp);
         w.gu = ld.gate_up(p + "ffn_gate.weight", p + "ffn_up.weight", Dp, c->pre_ff);
         w.wd = ld.vec(p + "ffn_down.weight", (size_t)c->pre_ff * Dp);
+        w.h16_qkv = ld.f16({p + "attn_q.weight", p + "attn_k.weight", p + "attn_v.weight"});
+        w.h16_wo = ld.f16({p + "attn_output.weight"});
+        w.h16_gu = ld.f16({p + "ffn_gate.weight", p + "ffn_up.weight"});
+        w.h16_wd = ld.f16({p + "ffn_down.weight"});
         c->pre.push_back(w);
     }
     c->pre_norm_w = ld.vec("wave_prenet.norm.weight", Dp);
     c->pre_norm_b = ld.vec("wave_prenet.norm.bias", Dp);
     c->pre_out_w = ld.vec("wave_prenet.output.weight", (size_t)Dp * Dd);
     c->pre_out_b = ld.vec("wave_prenet.output.bias", Dd);
+    c->h16_pre_out = ld.f16({"wave_prenet.output.weight"});
+    c->h16_ups = ld.f16({"wave_upsample.weight"});
     {   // ConvT k=2 s=2: ggml [2][Cout][Cin] (mem [ci][co][k]) -> B[(k*Cout+co)][ci]
         const mio::GgufTensor *tu = g.tensor("wave_upsample.weight");
         if (!tu || tu->ne[0] != 2 || tu->ne[1] != Dd || tu->ne[2] != Dd) {
@@ -575,6 +611,10 @@ extern "C" int mio_hip_codec_load(mio_hip_device *d, const char *path, mio_hip_c
             w.wo = ld.vec(p + "attn_output.weight", (size_t)Dd * Dd);
             w.gu = ld.gate_up(p + "ffn_gate.weight", p + "ffn_up.weight", Dd, c->dec_ff);
             w.wd = ld.vec(p + "ffn_down.weight", (size_t)c->dec_ff * Dd);
+            w.h16_qkv = ld.f16({p + "attn_q.weight", p + "attn_k.weight", p + "attn_v.weight"});
+            w.h16_wo = ld.f16({p + "attn_output.weight"});
+            w.h16_gu = ld.f16({p + "ffn_gate.weight", p + "ffn_up.weight"});
+            w.h16_wd = ld.f16({p + "ffn_down.weight"});
             c->dec.push_back(w);
         }
         std::vector<float> w = ld.f32("wave_decoder.norm_cond.weight", (size_t)c->adaln * 2 * Dd);
@@ -582,6 +622,19 @@ extern "C" int mio_hip_codec_load(mio_hip_device *d, const char *path, mio_hip_c
         cw.insert(cw.end(), w.begin(), w.end());
         cb.insert(cb.end(), bb.begin(), bb.end());
         c->cond_rows = (int)cb.size();
+        {   // every conditioning matrix shares one GEMV: one rounding rule for all of them
+            std::vector<std::string> names{"wave_decoder.norm_cond.weight"};
+            for (int i = 0; i < c->dec_layers; ++i)
+                for (const char *n : {"attn_cond", "ffn_cond"})
+                    names.push_back("wave_decoder.blk." + std::to_string(i) + "." + n + ".weight");
+            int n16 = 0;
+            for (const std::string &nm : names) n16 += ld.f16({nm});
+            if (n16 && n16 != (int)names.size()) {
+                mio::set_error("miocodec: the AdaLN conditioning matrices mix F16 and F32");
+                return fail(MIO_ERR_UNSUPPORTED);
+            }
+            c->h16_cond = n16 ? 1 : 0;
+        }
         c->cond_w = ld.up(cw);
         c->cond_b = ld.up(cb);
     }
@@ -629,13 +682,10 @@ extern "C" int mio_hip_codec_load(mio_hip_device *d, const char *path, mio_hip_c
                             w[((size_t)ci * u.Cout + co) * u.K + k];
                 }
         u.w = ld.up(o);
+        u.h16 = ld.f16({"wave_upsampler.up." + ss + ".weight"});
         u.b = ld.vec("wave_upsampler.up." + ss + ".bias", u.Cout);
-        std::vector<float> a = ld.f32("wave_upsampler.snake." + ss + ".alpha", u.Cout);
-        std::vector<float> be = ld.f32("wave_upsampler.snake." + ss + ".beta", u.Cout);
-        for (auto &x : a) x = expf(x);
-        for (auto &x : be) x = expf(x);
-        u.alpha_e = ld.up(a);
-        u.beta_e = ld.up(be);
+        u.alpha_e = ld.up(ld.snake_exp("wave_upsampler.snake." + ss + ".alpha", u.Cout));
+        u.beta_e = ld.up(ld.snake_exp("wave_upsampler.snake." + ss + ".beta", u.Cout));
         u.res = ld.resnet("wave_upsampler.resblk." + ss + ".", u.Cout);
         c->ups.push_back(u);
         cin = u.Cout;
@@ -643,14 +693,10 @@ extern "C" int mio_hip_codec_load(mio_hip_device *d, const char *path, mio_hip_c
     c->c_last = cin;
     c->op_w = ld.vec("wave_upsampler.out_proj.weight", (size_t)cin * Dd);
     c->op_b = ld.vec("wave_upsampler.out_proj.bias", Dd);
-    {
-        std::vector<float> a = ld.f32("wave_upsampler.out_snake.alpha", Dd);
-        std::vector<float> be = ld.f32("wave_upsampler.out_snake.beta", Dd);
-        for (auto &x : a) x = expf(x);
-        for (auto &x : be) x = expf(x);
-        c->op_ae = ld.up(a);
-        c->op_be = ld.up(be);
-    }
+    c->h16_op = ld.f16({"wave_upsampler.out_proj.weight"});
+    c->op_ae = ld.up(ld.snake_exp("wave_upsampler.out_snake.alpha", Dd));
+    c->op_be = ld.up(ld.snake_exp("wave_upsampler.out_snake.beta", Dd));
+    c->h16_head = ld.f16({"istft_head.out.weight"});
     {   // head rows interleaved per 16: [logmag 16p.., phase 16p..], zero-padded to nfp bins
         const int nf = c->n_freq;
         c->nfp = (nf + 15) / 16 * 16;

@@ -45,6 +45,7 @@ struct mio_hip_llm {
         float *logits = nullptr, *smp = nullptr;
         int *tokens = nullptr;                  // [B][n_ctx] token rings
         int *ppos = nullptr, *pseq = nullptr, *ptok = nullptr;  // flattened prompt prefill lists
+        float *ring = nullptr;  // lfm2: [B][n_layer][kConvSlots][n_embd] short-conv rings
         hipGraphExec_t graph = nullptr, graph_n = nullptr;
         std::vector<void *> allocs;
     } bt;
@@ -64,8 +65,12 @@ struct mio_hip_llm {
     // decode-step graphs, captured once (the sampling config is device-resident):
     // one step, and graph_steps() steps back to back (fewer graph launches per token)
     hipGraphExec_t graph = nullptr, graph_n = nullptr;
+    // prompt prefills replayed as graphs, by prompt length (the first prefill of a length runs
+    // eagerly and is captured: ~280 launches that eager issue makes host-bound)
+    std::map<int, hipGraphExec_t> prefill_graphs;
     mio::SampleCfg *d_cfg = nullptr;
     uint32_t epoch = 0;  // SampleCfg.epoch of the last put_cfg
+    float *d_layers = nullptr;  // mio_hip_llm_eval_layers' residual snapshots (parity tests)
     // generation state
     int n_prompt = 0, max_new = 0, steps_total = 0, steps_issued = 0;
     mio::SampleCfg cfg{};
@@ -88,6 +93,7 @@ struct mio_hip_llm {
         if (d) hipSetDevice(d->dev);
         if (graph) hipGraphExecDestroy(graph);
         if (graph_n) hipGraphExecDestroy(graph_n);
+        for (auto &kv : prefill_graphs) hipGraphExecDestroy(kv.second);
         if (bt.graph) hipGraphExecDestroy(bt.graph);
         if (bt.graph_n) hipGraphExecDestroy(bt.graph_n);
         for (void *p : bt.allocs) hipFree(p);
@@ -227,11 +233,32 @@ int graph_steps() {
     return n;
 }
 
-// One decode step on m->d->stream (tl: optional step timeline, diagnostic).
-// Launches per layer of the step: attn_in (+ attention when fused), [attention], attn_out,
-// ffn_in, ffn_down.
-int launches_per_layer(const mio_hip_llm *m) { return m->buf.qkv_g ? 4 : 5; }
+// Launches of layer il in step order (launch_step_kernel's `which`): attn_in (+ attention
+// when fused), [attention], attn_out, or an lfm2 short-conv layer's conv_in, conv_out; then
+// ffn_in, ffn_down. Returns the count (<= 5).
+int layer_kinds(const mio_hip_llm *m, int il, int *w) {
+    int n = 0;
+    if (m->layers[il].conv) {
+        w[n++] = 8, w[n++] = 9;
+    } else {
+        w[n++] = 0;
+        if (!m->buf.qkv_g) w[n++] = 1;
+        w[n++] = 2;
+    }
+    w[n++] = 3, w[n++] = 4;
+    return n;
+}
 
+// every launch of a step in order: the layers', then lm_head (6)
+std::vector<int> step_kinds(const mio_hip_llm *m) {
+    std::vector<int> k;
+    int w[5];
+    for (int il = 0; il < m->n_layer; ++il) k.insert(k.end(), w, w + layer_kinds(m, il, w));
+    k.push_back(6);
+    return k;
+}
+
+// One decode step on m->d->stream (tl: optional step timeline, diagnostic).
 int issue_step(mio_hip_llm *m, unsigned long long *tl = nullptr) {
     hipStream_t s = m->d->stream;
     int seq = 0;
@@ -240,11 +267,11 @@ int issue_step(mio_hip_llm *m, unsigned long long *tl = nullptr) {
         if (tl) b.tl = tl, b.seq = seq++;
         return b;
     };
+    int w[5];
     for (int il = 0; il < m->n_layer; ++il)
-        for (int k = 0; k < 5; ++k)
-            if (k != 1 || !m->buf.qkv_g)
-                mio::launch_step_kernel(k, m->dims, m->layers.data(), il, m->kc, m->vc, m->out_norm, m->lm, m->tok,
-                                        bufs(), s);
+        for (int i = 0, n = layer_kinds(m, il, w); i < n; ++i)
+            mio::launch_step_kernel(w[i], m->dims, m->layers.data(), il, m->kc, m->vc, m->out_norm, m->lm, m->tok,
+                                    bufs(), s);
     mio::launch_step_kernel(6, m->dims, m->layers.data(), 0, m->kc, m->vc, m->out_norm, m->lm, m->tok, bufs(), s);
     return MIO_OK;
 }
@@ -299,7 +326,7 @@ int set_state(mio_hip_llm *m, int pos, int token, int step = 0) {
 // Batched prefill of prompt positions [0, n) (tokens already in m->d_prompt): chunks of
 // kPrefillB tokens, one weight pass per launch (llm_prefill.hip). MIO_SEQ_PREFILL=1 is not
 // handled here (see llm_begin).
-int prefill(mio_hip_llm *m, int n) {
+int prefill_issue(mio_hip_llm *m, int n) {
     for (int p0 = 0; p0 < n; p0 += mio::kPrefillB) {
         const int nt = n - p0 < mio::kPrefillB ? n - p0 : mio::kPrefillB;
         mio::PrefillBuffers pb = m->pf;
@@ -310,6 +337,33 @@ int prefill(mio_hip_llm *m, int n) {
                                   (p0 + nt - 1) / mio::kAttChunk + 1, m->d->stream);
         MIO_HIP_CHECK(hipGetLastError());
     }
+    return MIO_OK;
+}
+
+// Batched prefill of positions [0, n): every launch reads only device buffers whose addresses
+// depend on n alone (prompt tokens in m->d_prompt), so one graph per prompt length replays it.
+// The first prefill of a length runs eagerly (its launches set the kernels' LDS attributes
+// outside any capture), then is captured for the next utterance. MIO_PREFILL_GRAPH=0: eager.
+int prefill(mio_hip_llm *m, int n) {
+    static const bool use_graph = !(getenv("MIO_PREFILL_GRAPH") && getenv("MIO_PREFILL_GRAPH")[0] == '0');
+    if (n <= 0) return MIO_OK;
+    const auto it = m->prefill_graphs.find(n);
+    if (use_graph && it != m->prefill_graphs.end()) {
+        MIO_HIP_CHECK(hipGraphLaunch(it->second, m->d->stream));
+        return MIO_OK;
+    }
+    int rc = prefill_issue(m, n);
+    if (rc || !use_graph || m->prefill_graphs.size() >= 16) return rc;
+    hipStream_t s = m->d->stream;
+    hipGraph_t g = nullptr;
+    hipGraphExec_t ge = nullptr;
+    MIO_HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+    rc = prefill_issue(m, n);
+    MIO_HIP_CHECK(hipStreamEndCapture(s, &g));
+    if (rc) return rc;
+    MIO_HIP_CHECK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+    hipGraphDestroy(g);
+    m->prefill_graphs[n] = ge;
     return MIO_OK;
 }
 
@@ -460,15 +514,11 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
     mio::GgufFile g;
     if (!g.open(path)) return MIO_ERR_IO;
     const std::string arch = g.get_str("general.architecture");
-    // lfm2 (LiquidAI LFM2, the <|startoftext|><|im_start|> template family) interleaves
-    // gated short-conv blocks (depthwise causal conv1d with a rolling state) with attention
-    // layers; no kernel of this path implements that block, so refuse it by name
-    MIO_REQUIRE(arch != "lfm2", MIO_ERR_UNSUPPORTED,
-                "llm_load: architecture 'lfm2' needs the hybrid short-conv block (depthwise causal "
-                "conv1d with rolling state), which this path does not implement; supported: llama, "
-                "mistral, qwen2, qwen3");
-    MIO_REQUIRE(arch == "llama" || arch == "qwen3" || arch == "qwen2" || arch == "mistral",
-                MIO_ERR_UNSUPPORTED, "llm_load: architecture '%s' not supported (llama, mistral, qwen2, qwen3)",
+    // lfm2 (LiquidAI LFM2, the <|startoftext|><|im_start|> template family): attention layers
+    // (NEOX RoPE, q/k RMSNorm) interleaved with gated short-conv layers (llama.cpp build_lfm2)
+    const bool lfm2 = arch == "lfm2";
+    MIO_REQUIRE(arch == "llama" || arch == "qwen3" || arch == "qwen2" || arch == "mistral" || lfm2,
+                MIO_ERR_UNSUPPORTED, "llm_load: architecture '%s' not supported (llama, mistral, qwen2, qwen3, lfm2)",
                 arch.c_str());
     // the only bias tensors any supported block has are qwen2's attn_{q,k,v}.bias: anything
     // else (output / ffn biases) would be silently dropped, so refuse the file instead
@@ -498,12 +548,23 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
     m->n_layer = (int)g.get_int(arch + ".block_count", 0);
     D.n_ff = (int)g.get_int(arch + ".feed_forward_length", 0);
     D.n_head = (int)g.get_int(arch + ".attention.head_count", 0);
-    D.n_kv = (int)g.get_int(arch + ".attention.head_count_kv", D.n_head);
+    // head_count_kv: a scalar, or per layer (lfm2: 0 marks a short-conv layer)
+    std::vector<int64_t> kv_arr;
+    if (const mio::GgufValue *hv = g.get(arch + ".attention.head_count_kv"); hv && !hv->arr_i.empty()) {
+        kv_arr = hv->arr_i;
+        D.n_kv = 0;
+        for (int64_t v : kv_arr) D.n_kv = std::max(D.n_kv, (int)v);
+    } else {
+        D.n_kv = (int)g.get_int(arch + ".attention.head_count_kv", D.n_head);
+    }
     D.hd = (int)g.get_int(arch + ".attention.key_length", D.n_head ? D.n_embd / D.n_head : 0);
     D.eps = (float)g.get_float(arch + ".attention.layer_norm_rms_epsilon", 1e-6);
     const float base = (float)g.get_float(arch + ".rope.freq_base", 10000.0);
-    D.neox = (arch == "qwen3" || arch == "qwen2") ? 1 : 0;
-    D.qk_norm = arch == "qwen3" ? 1 : 0;
+    D.neox = (arch == "qwen3" || arch == "qwen2" || lfm2) ? 1 : 0;
+    D.qk_norm = (arch == "qwen3" || lfm2) ? 1 : 0;
+    MIO_REQUIRE(!lfm2 || g.get_int(arch + ".shortconv.l_cache", mio::kConvL) == mio::kConvL, MIO_ERR_UNSUPPORTED,
+                "llm_load: lfm2 shortconv.l_cache %lld not supported (%d)",
+                (long long)g.get_int(arch + ".shortconv.l_cache", 0), mio::kConvL);
     D.n_ctx = n_ctx;
     D.scale = 1.0f / sqrtf((float)D.hd);
     D.split = mio::kAttChunk;
@@ -527,23 +588,25 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
     {
         // arena: layer matrices in step order, then the lm_head, then the embedding table
         std::vector<std::string> order;
-        static const char *mats[] = {"attn_q", "attn_k", "attn_v", "attn_output", "ffn_gate", "ffn_up", "ffn_down"};
+        static const char *mats[] = {"attn_q",   "attn_k",  "attn_v",   "shortconv.in_proj", "attn_output",
+                                     "shortconv.out_proj", "ffn_gate", "ffn_up", "ffn_down"};
         for (int i = 0; i < m->n_layer; ++i)
             for (const char *n : mats) order.push_back("blk." + std::to_string(i) + "." + n + ".weight");
         order.push_back("output.weight");
         order.push_back("token_embd.weight");
         // then every f32 norm vector (kept out of many small allocations: one large mapping
         // serves all of them)
-        static const char *norms[] = {"attn_norm", "ffn_norm", "attn_q_norm", "attn_k_norm"};
+        static const char *norms[] = {"attn_norm", "ffn_norm", "attn_q_norm", "attn_k_norm", "shortconv.conv"};
         for (int i = 0; i < m->n_layer; ++i)
             for (const char *n : norms) order.push_back("blk." + std::to_string(i) + "." + n + ".weight");
         order.push_back("output_norm.weight");
+        order.push_back("token_embd_norm.weight");
         size_t total = 0;
         for (const std::string &n : order) {
             const mio::GgufTensor *t = g.tensor(n);
             if (!t) continue;
             size_t bytes = 0;
-            if (t->n_dims == 2) {
+            if (t->n_dims == 2 && t->type != mio::GGML_F32) {
                 bytes = mio::split_layout(t->type, t->ne[1], t->ne[0]).bytes;
             } else if (t->type == mio::GGML_F32) {
                 bytes = (size_t)t->nelements() * 4;
@@ -576,7 +639,10 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
         m->lm = m->tok;  // tied embeddings: the table is streamed as the lm_head every step
         m->weight_bytes += embd_bytes;
     }
-    if (!(m->out_norm = upload_f32(m, g.tensor("output_norm.weight"), D.n_embd))) return fail(MIO_ERR_FORMAT);
+    // lfm2's final norm is token_embd_norm (llama.cpp model.tok_norm)
+    if (!(m->out_norm = upload_f32(m, g.tensor(lfm2 ? "token_embd_norm.weight" : "output_norm.weight"), D.n_embd)))
+        return fail(MIO_ERR_FORMAT);
+    bool any_conv = false;
     auto fam = [](int t) { return t == mio::GGML_Q8_0 ? 0 : 1; };
     for (int i = 0; i < m->n_layer; ++i) {
         const std::string p = "blk." + std::to_string(i) + ".";
@@ -584,6 +650,38 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
         if (!(L.attn_norm = upload_f32(m, g.tensor(p + "attn_norm.weight"), D.n_embd)) ||
             !(L.ffn_norm = upload_f32(m, g.tensor(p + "ffn_norm.weight"), D.n_embd)))
             return fail(MIO_ERR_FORMAT);
+        L.conv = g.tensor(p + "shortconv.in_proj.weight") ? 1 : 0;
+        if (lfm2 && (size_t)i < kv_arr.size() && (kv_arr[i] == 0) != (L.conv != 0)) {
+            mio::set_error("llm_load: layer %d: head_count_kv %lld disagrees with its tensors", i, (long long)kv_arr[i]);
+            return fail(MIO_ERR_FORMAT);
+        }
+        if (L.conv) {
+            // gated short conv: in_proj [3 n_embd][n_embd], taps [n_embd][3] f32, out_proj
+            MIO_REQUIRE(lfm2, MIO_ERR_UNSUPPORTED, "llm_load: layer %d: short-conv tensors in a '%s' model", i,
+                        arch.c_str());
+            const mio::GgufTensor *tc = g.tensor(p + "shortconv.conv.weight");
+            if (!tc || tc->type != mio::GGML_F32 || tc->ne[0] != mio::kConvL || tc->ne[1] != D.n_embd) {
+                mio::set_error("llm_load: layer %d: shortconv.conv.weight must be f32 [%d][%d]", i, D.n_embd,
+                               mio::kConvL);
+                return fail(MIO_ERR_FORMAT);
+            }
+            if (!(L.conv_w = upload_f32(m, tc, (int64_t)D.n_embd * mio::kConvL)) ||
+                !upload_qmat(m, g.tensor(p + "shortconv.in_proj.weight"), L.in_proj) ||
+                !upload_qmat(m, g.tensor(p + "shortconv.out_proj.weight"), L.out_proj) ||
+                !upload_qmat(m, g.tensor(p + "ffn_gate.weight"), L.gate) ||
+                !upload_qmat(m, g.tensor(p + "ffn_up.weight"), L.up) ||
+                !upload_qmat(m, g.tensor(p + "ffn_down.weight"), L.down))
+                return fail(MIO_ERR_FORMAT);
+            if (L.in_proj.rows != 3 * D.n_embd || L.in_proj.k != D.n_embd || L.out_proj.rows != D.n_embd ||
+                L.out_proj.k != D.n_embd || L.gate.rows != D.n_ff || L.down.k != D.n_ff ||
+                L.gate.type != L.up.type || D.n_ff > 12288 || D.n_embd > 64 * 8 * D.n_wg) {
+                mio::set_error("llm_load: layer %d (short conv) shapes / quant families not supported", i);
+                return fail(MIO_ERR_UNSUPPORTED);
+            }
+            any_conv = true;
+            m->layers.push_back(L);
+            continue;
+        }
         if (D.qk_norm) {
             if (!(L.q_norm = upload_f32(m, g.tensor(p + "attn_q_norm.weight"), D.hd)) ||
                 !(L.k_norm = upload_f32(m, g.tensor(p + "attn_k_norm.weight"), D.hd)))
@@ -636,15 +734,17 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
         return mio_hip_llm::Range{a.p0, (uint64_t)(z.p0 + L.bytes - a.p0)};
     };
     for (const mio::LayerW &L : m->layers) {
-        m->ranges.push_back(span(L.wq, L.wv));
+        m->ranges.push_back(L.conv ? span(L.in_proj, L.in_proj) : span(L.wq, L.wv));
         m->ranges.push_back({});
-        m->ranges.push_back(span(L.wo, L.wo));
+        m->ranges.push_back(L.conv ? span(L.out_proj, L.out_proj) : span(L.wo, L.wo));
         m->ranges.push_back(span(L.gate, L.up));
         m->ranges.push_back(span(L.down, L.down));
     }
     m->ranges.push_back(span(m->lm, m->lm));
     // buffers
     const int qkv = (D.n_head + 2 * D.n_kv) * D.hd;
+    // q|k|v rows, or an lfm2 short-conv layer's B | C | X rows
+    const int qkv_rows = std::max(qkv, any_conv ? 3 * D.n_embd : 0);
     const size_t kv = (size_t)m->n_layer * D.n_kv * n_ctx * D.hd;
     m->kc = dalloc<_Float16>(m, kv);
     m->vc = dalloc<_Float16>(m, kv);
@@ -657,7 +757,8 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
     };
     float2 *dr = nullptr;
     want(m->buf.x, D.n_embd);
-    want(m->buf.qkv, qkv);
+    want(m->buf.qkv, qkv_rows);
+    if (any_conv) want(m->buf.ring, (size_t)m->n_layer * mio::kConvSlots * D.n_embd);
     want(m->buf.h, D.n_ff);
     want(m->buf.logits, D.n_vocab);
     want(m->buf.part, (size_t)D.n_head * D.max_splits * (D.hd + 4));
@@ -681,7 +782,7 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
     want(m->d_force, m->max_steps);
     want(m->d_prompt, n_ctx);
     want(m->pf.x, (size_t)mio::kPrefillB * D.n_embd);
-    want(m->pf.qkv, (size_t)mio::kPrefillB * qkv);
+    want(m->pf.qkv, (size_t)mio::kPrefillB * qkv_rows);
     want(m->pf.h, (size_t)mio::kPrefillB * D.n_ff);
     want(m->pf.part, (size_t)mio::kPrefillB * D.n_head * D.max_splits * (D.hd + 4));
     want(m->pf.act, mio::prefill_act_bytes(std::max(std::max(D.n_embd, D.n_ff), D.n_head * D.hd)));
@@ -700,6 +801,8 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
     m->buf.cfg = m->d_cfg;
     m->buf.qkv_g = qkv_g;  // zeroed with the carve (dalloc): tag 0 is never a launch's
     m->pf.tokens = m->d_prompt;
+    m->pf.ring = m->buf.ring;  // the single-stream prefill is sequence 0 of the decode rings
+    m->pf.seq_ring = 0;
     // RoPE table, ggml rope-cache recurrence (theta = p; theta *= base^(-2/hd) per pair)
     std::vector<float2> rope((size_t)n_ctx * (D.hd / 2));
     const float theta_scale = powf(base, -2.0f / D.hd);
@@ -712,7 +815,8 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
     }
     if (!m->kc || !m->vc || !m->buf.x || !m->buf.qkv || !m->buf.h || !m->buf.logits ||
         !m->buf.part || !m->buf.smp || !m->buf.st || !m->d_cfg || !m->d_tokens || !m->d_force || !dr ||
-        !m->d_prompt || !m->pf.x || !m->pf.qkv || !m->pf.h || !m->pf.part || !m->pf.act || !m->d_iota) {
+        !m->d_prompt || !m->pf.x || !m->pf.qkv || !m->pf.h || !m->pf.part || !m->pf.act || !m->d_iota ||
+        (any_conv && !m->buf.ring)) {
         mio::set_error("llm_load: device allocation failed");
         return fail(MIO_ERR_OOM);
     }
@@ -737,9 +841,30 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
     return MIO_OK;
 }
 
-extern "C" int mio_hip_llm_step_layout(const mio_hip_llm *m, int *launches_per_layer) {
-    MIO_REQUIRE(m && launches_per_layer, MIO_ERR_INVALID, "llm_step_layout: null");
-    *launches_per_layer = ::launches_per_layer(m);
+extern "C" int mio_hip_llm_step_kinds(const mio_hip_llm *m, int *kinds, int cap, int *n) {
+    MIO_REQUIRE(m && n, MIO_ERR_INVALID, "llm_step_kinds: null");
+    const std::vector<int> k = step_kinds(m);
+    *n = (int)k.size();
+    MIO_REQUIRE(!kinds || cap >= (int)k.size(), MIO_ERR_INVALID, "llm_step_kinds: need %d slots", (int)k.size());
+    if (kinds) std::memcpy(kinds, k.data(), k.size() * sizeof(int));
+    return MIO_OK;
+}
+
+// lfm2 short-conv ring of layer il, [kConvSlots][n_embd] (bx of position p in slot p & 3;
+// parity tests). get: copied out; set: copied in.
+extern "C" int mio_hip_llm_conv_ring(mio_hip_llm *m, int il, float *ring, int set) {
+    MIO_REQUIRE(m && ring && il >= 0 && il < m->n_layer && m->layers[il].conv && m->buf.ring, MIO_ERR_INVALID,
+                "llm_conv_ring: layer %d is not a short-conv layer", il);
+    int rc = mio::bind(m->d);
+    if (rc) return rc;
+    const size_t n = (size_t)mio::kConvSlots * m->dims.n_embd;
+    float *dr = m->buf.ring + (size_t)il * n;
+    hipStream_t s = m->d->stream;
+    if (set)
+        MIO_HIP_CHECK(hipMemcpyAsync(dr, ring, n * 4, hipMemcpyHostToDevice, s));
+    else
+        MIO_HIP_CHECK(hipMemcpyAsync(ring, dr, n * 4, hipMemcpyDeviceToHost, s));
+    MIO_HIP_CHECK(hipStreamSynchronize(s));
     return MIO_OK;
 }
 
@@ -787,6 +912,65 @@ extern "C" int mio_hip_llm_eval(mio_hip_llm *m, int32_t token, int pos, float *l
     return MIO_OK;
 }
 
+// One decode step like mio_hip_llm_eval, launched kernel by kernel, with the residual stream
+// captured before layer 0 (the embedding) and after every layer: x_layers[(n_layer + 1) *
+// n_embd] (parity tests: the oracle re-runs each layer on the GPU's input).
+extern "C" int mio_hip_llm_eval_layers(mio_hip_llm *m, int32_t token, int pos, float *x_layers, float *logits) {
+    MIO_REQUIRE(m && x_layers && token >= 0 && token < m->dims.n_vocab && pos >= 0 && pos < m->dims.n_ctx,
+                MIO_ERR_INVALID, "llm_eval_layers: bad args");
+    int rc = mio::bind(m->d);
+    if (rc) return rc;
+    mio::SampleCfg c{};
+    c.temp = 0.0f, c.lo = 0, c.hi = m->dims.n_vocab, c.eos0 = c.eos1 = -1;
+    c.force = m->d_force, c.n_force = m->max_steps, c.out_tokens = m->d_tokens, c.max_steps = m->max_steps;
+    if ((rc = put_cfg(m, c)) || (rc = ensure_graph(m))) return rc;
+    const int zero = 0;
+    hipStream_t s = m->d->stream;
+    const size_t D = (size_t)m->dims.n_embd;
+    MIO_HIP_CHECK(hipMemcpyAsync(m->d_force, &zero, 4, hipMemcpyHostToDevice, s));
+    if ((rc = set_state(m, pos, token))) return rc;
+    if (!m->d_layers) {
+        void *p = nullptr;
+        MIO_HIP_CHECK(hipMalloc(&p, (m->n_layer + 1) * D * 4));
+        m->allocs.push_back(p);
+        m->d_layers = (float *)p;
+    }
+    float *dx = m->d_layers;
+    MIO_HIP_CHECK(hipMemcpyAsync(dx, m->buf.x, D * 4, hipMemcpyDeviceToDevice, s));
+    int w[5];
+    for (int il = 0; il < m->n_layer; ++il) {
+        for (int i = 0, n = layer_kinds(m, il, w); i < n; ++i)
+            mio::launch_step_kernel(w[i], m->dims, m->layers.data(), il, m->kc, m->vc, m->out_norm, m->lm, m->tok,
+                                    m->buf, s);
+        MIO_HIP_CHECK(hipMemcpyAsync(dx + (il + 1) * D, m->buf.x, D * 4, hipMemcpyDeviceToDevice, s));
+    }
+    mio::launch_step_kernel(6, m->dims, m->layers.data(), 0, m->kc, m->vc, m->out_norm, m->lm, m->tok, m->buf, s);
+    MIO_HIP_CHECK(hipGetLastError());
+    MIO_HIP_CHECK(hipMemcpyAsync(x_layers, dx, (m->n_layer + 1) * D * 4, hipMemcpyDeviceToHost, s));
+    if (logits)
+        MIO_HIP_CHECK(hipMemcpyAsync(logits, m->buf.logits, (size_t)m->dims.n_vocab * 4, hipMemcpyDeviceToHost, s));
+    if ((rc = flush_sample(m))) return rc;
+    MIO_HIP_CHECK(hipStreamSynchronize(s));
+    return MIO_OK;
+}
+
+// F16 K / V cache rows [0, n_pos) of layer il as [n_kv][n_pos][head_dim] (parity tests).
+extern "C" int mio_hip_llm_kv_rows(mio_hip_llm *m, int il, int n_pos, uint16_t *k, uint16_t *v) {
+    MIO_REQUIRE(m && k && v && il >= 0 && il < m->n_layer && n_pos >= 0 && n_pos <= m->dims.n_ctx, MIO_ERR_INVALID,
+                "llm_kv_rows: bad args");
+    int rc = mio::bind(m->d);
+    if (rc) return rc;
+    const mio::LlmDims &D = m->dims;
+    hipStream_t s = m->d->stream;
+    for (int h = 0; h < D.n_kv; ++h) {
+        const size_t src = (((size_t)il * D.n_kv + h) * D.n_ctx) * D.hd, dst = (size_t)h * n_pos * D.hd;
+        MIO_HIP_CHECK(hipMemcpyAsync(k + dst, m->kc + src, (size_t)n_pos * D.hd * 2, hipMemcpyDeviceToHost, s));
+        MIO_HIP_CHECK(hipMemcpyAsync(v + dst, m->vc + src, (size_t)n_pos * D.hd * 2, hipMemcpyDeviceToHost, s));
+    }
+    MIO_HIP_CHECK(hipStreamSynchronize(s));
+    return MIO_OK;
+}
+
 extern "C" int mio_hip_llm_generate(mio_hip_llm *m, const int32_t *prompt, int n_prompt, int max_tokens,
                                     float temperature, uint64_t seed, int32_t allow_lo, int32_t allow_hi,
                                     int32_t eos0, int32_t eos1, int32_t check_interval, int32_t *out_tokens,
@@ -818,6 +1002,8 @@ extern "C" int mio_hip_llm_generate(mio_hip_llm *m, const int32_t *prompt, int n
 
 namespace {
 
+size_t batch_seq_ring(const mio_hip_llm *m) { return (size_t)m->n_layer * mio::kConvSlots * m->dims.n_embd; }
+
 // Batch state for B streams (re-allocated when B changes; graphs re-captured).
 int batch_ensure(mio_hip_llm *m, int B) {
     auto &bt = m->bt;
@@ -848,8 +1034,9 @@ int batch_ensure(mio_hip_llm *m, int B) {
     bt.ppos = (int *)al((size_t)B * D.n_ctx * 4);
     bt.pseq = (int *)al((size_t)B * D.n_ctx * 4);
     bt.ptok = (int *)al((size_t)B * D.n_ctx * 4);
+    bt.ring = m->buf.ring ? (float *)al(B * batch_seq_ring(m) * 4) : nullptr;
     if (!bt.kc || !bt.vc || !bt.st || !bt.cfg || !bt.logits || !bt.smp || !bt.tokens || !bt.ppos || !bt.pseq ||
-        !bt.ptok) {
+        !bt.ptok || (m->buf.ring && !bt.ring)) {
         for (void *p : bt.allocs) hipFree(p);
         bt.allocs.clear();
         mio::set_error("llm_generate_batch: device allocation for %d streams failed", B);
@@ -866,6 +1053,7 @@ mio::PrefillBuffers batch_pb(mio_hip_llm *m) {
     pb.pos = &m->bt.st[0].pos, pb.pos_stride = (int)(sizeof(mio::StepState) / sizeof(int));
     pb.seq = m->d_iota, pb.seq_stride = 1;
     pb.seq_kv = (size_t)m->n_layer * m->dims.n_kv * m->dims.n_ctx * m->dims.hd;
+    pb.ring = m->bt.ring, pb.seq_ring = batch_seq_ring(m);
     return pb;
 }
 
@@ -962,6 +1150,7 @@ extern "C" int mio_hip_llm_generate_batch(mio_hip_llm *m, const int32_t *prompts
         pb.pos = bt.ppos + c0, pb.pos_stride = 1;
         pb.seq = bt.pseq + c0, pb.seq_stride = 1;
         pb.seq_kv = (size_t)m->n_layer * D.n_kv * D.n_ctx * D.hd;
+        pb.ring = bt.ring, pb.seq_ring = batch_seq_ring(m);
         mio::launch_prefill_chunk(D, m->layers.data(), m->n_layer, bt.kc, bt.vc, m->tok, pb, c0, nt,
                                   pmax / mio::kAttChunk + 1, s);
         MIO_HIP_CHECK(hipGetLastError());
@@ -1110,9 +1299,21 @@ extern "C" int mio_quantize_rows(uint32_t type, const float *x, int rows, int k,
     return MIO_OK;
 }
 
+// The layer a diagnostic launch of kernel `which` runs on: the first layer at or after
+// n_layer / 2 (wrapping) that has it (attention kernels 0..2: an attention layer; 8, 9: an
+// lfm2 short-conv layer; others: any), or -1.
+static int kernel_layer(const mio_hip_llm *m, int which) {
+    for (int i = 0; i < m->n_layer; ++i) {
+        const int il = (m->n_layer / 2 + i) % m->n_layer;
+        const bool conv = m->layers[il].conv != 0;
+        if (which <= 2 ? !conv : (which >= 8 ? conv : true)) return il;
+    }
+    return -1;
+}
+
 // Live timing of one kernel of the decode step (bench.py roofline): launches kernel
-// `which` (0 attn_in, 1 attention, 2 attn_out, 3 ffn_in, 4 ffn_down, 6 lm_head) of layer
-// n_layer/2 `iters` times on the runner's stream between HIP events, with the buffers and
+// `which` (0 attn_in, 1 attention, 2 attn_out, 3 ffn_in, 4 ffn_down, 6 lm_head, 8 conv_in,
+// 9 conv_out) of layer kernel_layer() `iters` times on the runner's stream between HIP events, with the buffers and
 // device state left by the last generate/eval. Returns the mean duration and the
 // algorithmic HBM bytes of one launch (weights of the matrices it streams + activations;
 // attention: F16 K and V rows of positions 0..pos (the row at pos is written, the rest
@@ -1120,10 +1321,12 @@ extern "C" int mio_quantize_rows(uint32_t type, const float *x, int rows, int k,
 extern "C" int mio_hip_llm_time_kernel(mio_hip_llm *m, int which, int iters, float *avg_ms, uint64_t *bytes) {
     MIO_REQUIRE(m && avg_ms && bytes && iters > 0 && m->graph, MIO_ERR_INVALID,
                 "llm_time_kernel: run generate/eval first");
-    MIO_REQUIRE(which >= 0 && which <= 6 && which != 5, MIO_ERR_INVALID, "llm_time_kernel: which %d", which);
+    MIO_REQUIRE(which >= 0 && which <= 9 && which != 5 && which != 7, MIO_ERR_INVALID, "llm_time_kernel: which %d",
+                which);
+    const int il = kernel_layer(m, which);
+    MIO_REQUIRE(il >= 0, MIO_ERR_INVALID, "llm_time_kernel: the model has no layer with kernel %d", which);
     int rc = mio::bind(m->d);
     if (rc) return rc;
-    const int il = m->n_layer / 2;
     const mio::LayerW &L = m->layers[il];
     auto qbytes = [](const mio::QMat &q) {
         return (uint64_t)mio::ggml_row_bytes(q.type, q.k) * (uint64_t)q.rows;
@@ -1151,6 +1354,9 @@ extern "C" int mio_hip_llm_time_kernel(mio_hip_llm *m, int which, int iters, flo
         case 3: b = qbytes(L.gate) + qbytes(L.up) + 4ull * (D.n_embd * 2 + D.n_ff); break;
         case 4: b = qbytes(L.down) + 4ull * (D.n_ff + 2 * D.n_embd); break;
         case 6: b = qbytes(m->lm) + 4ull * D.n_vocab; break;
+        case 8: b = qbytes(L.in_proj) + 4ull * D.n_embd * 4; break;
+        // B | C | X in, taps, the two window rows, this position's bx (one workgroup), x in / out
+        case 9: b = qbytes(L.out_proj) + 4ull * D.n_embd * (3 + mio::kConvL + 2 + 1 + 2); break;
     }
     hipEvent_t e0, e1;
     MIO_HIP_CHECK(hipEventCreate(&e0));
@@ -1179,10 +1385,11 @@ extern "C" int mio_hip_llm_time_kernel(mio_hip_llm *m, int which, int iters, flo
 // checkpoints 0 and 15 in out[16] / out[31]. Diagnostic only.
 extern "C" int mio_hip_llm_trace_kernel(mio_hip_llm *m, int which, uint64_t *out) {
     MIO_REQUIRE(m && out && m->graph, MIO_ERR_INVALID, "llm_trace_kernel: run generate/eval first");
-    MIO_REQUIRE(which >= 0 && which <= 7 && which != 5, MIO_ERR_INVALID, "llm_trace_kernel: which %d", which);
+    MIO_REQUIRE(which >= 0 && which <= 9 && which != 5, MIO_ERR_INVALID, "llm_trace_kernel: which %d", which);
+    const int il = kernel_layer(m, which);
+    MIO_REQUIRE(il >= 0, MIO_ERR_INVALID, "llm_trace_kernel: the model has no layer with kernel %d", which);
     int rc = mio::bind(m->d);
     if (rc) return rc;
-    const int il = m->n_layer / 2;
     hipStream_t s = m->d->stream;
     mio::StepState st0{};  // restored on exit, as in mio_hip_llm_time_kernel
     MIO_HIP_CHECK(hipStreamSynchronize(s));
@@ -1201,7 +1408,8 @@ extern "C" int mio_hip_llm_trace_kernel(mio_hip_llm *m, int which, uint64_t *out
     }
     // MIO_TRACE_PREFETCH=1: the launch's weights are swept into the Infinity Cache first
     if (getenv("MIO_TRACE_PREFETCH") && getenv("MIO_TRACE_PREFETCH")[0] == '1') {
-        const size_t ri = which == 6 ? m->ranges.size() - 1 : (size_t)il * 5 + which;
+        const int wr = which == 8 ? 0 : (which == 9 ? 2 : which);
+        const size_t ri = which == 6 ? m->ranges.size() - 1 : (size_t)il * 5 + wr;
         if (ri < m->ranges.size()) mio::launch_touch(m->ranges[ri].p, m->ranges[ri].bytes, m->dims.n_wg, s);
     }
     mio::LlmBuffers tb = m->buf;
@@ -1223,7 +1431,7 @@ extern "C" int mio_hip_llm_timeline(mio_hip_llm *m, uint64_t *out, int max_launc
     MIO_REQUIRE(m && out && n_launches && m->graph, MIO_ERR_INVALID, "llm_timeline: run generate/eval first");
     int rc = mio::bind(m->d);
     if (rc) return rc;
-    const int nl = m->n_layer * launches_per_layer(m) + 1;
+    const int nl = (int)step_kinds(m).size();
     MIO_REQUIRE(max_launches >= nl, MIO_ERR_INVALID, "llm_timeline: need %d launch slots", nl);
     hipStream_t s = m->d->stream;
     const size_t nslot = (size_t)nl * 512 * 8;

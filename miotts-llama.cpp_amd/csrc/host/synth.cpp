@@ -33,7 +33,8 @@ float synth_normal(uint64_t key, uint64_t i) {
 
 SynthCodecCfg synth_codec_preset(int preset) {
     SynthCodecCfg c;
-    if (preset == 1) {  // tiny: same topology, small widths (fast parity tests)
+    c.f16 = preset >= 2;
+    if (preset == 1 || preset == 2) {  // tiny: same topology, small widths (fast parity tests)
         c.prenet_layers = 2, c.prenet_dim = 128, c.prenet_heads = 2, c.prenet_ff = 256;
         c.dec_layers = 2, c.dec_dim = 128, c.dec_heads = 2, c.dec_ff = 384;
         c.up_ch[0] = 64, c.up_ch[1] = 32;
@@ -169,6 +170,9 @@ bool synth_write_codec(const std::string &path, const SynthCodecCfg &c) {
     w.kv_f32("miocodec.rope_theta", 10000.0f);
     w.kv_f32("miocodec.norm_eps", 1e-5f);
     w.kv_f32("miocodec.group_norm_eps", 1e-6f);
+    if (c.f16)
+        for (auto &s : S)
+            if (s.type == GGML_F32 && s.ne.size() >= 2) s.type = GGML_F16;
     for (auto &s : S) w.add_tensor(s.name, s.type, s.ne);
     return w.write(path, [&](size_t i, uint8_t *dst, size_t nbytes) {
         const Spec &s = S[i];
@@ -176,13 +180,17 @@ bool synth_write_codec(const std::string &path, const SynthCodecCfg &c) {
             std::memcpy(dst, s.ints.data(), nbytes);
             return;
         }
-        float *f = (float *)dst;
-        const size_t n = nbytes / 4;
+        const bool h = s.type == GGML_F16;
+        const size_t n = nbytes / (h ? 2 : 4);
         const uint64_t key = synth_key(c.seed, s.name);
 #pragma omp parallel for schedule(static) if (n > 65536)
         for (size_t j = 0; j < n; ++j) {
             const float z = synth_normal(key, j);
-            f[j] = s.init == ONES_JITTER ? 1.0f + s.std * z : s.std * z;
+            const float v = s.init == ONES_JITTER ? 1.0f + s.std * z : s.std * z;
+            if (h)
+                ((_Float16 *)dst)[j] = (_Float16)v;
+            else
+                ((float *)dst)[j] = v;
         }
     });
 }

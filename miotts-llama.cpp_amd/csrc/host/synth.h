@@ -14,10 +14,12 @@ struct SynthCodecCfg {
     int resnet_blocks = 2, resnet_groups = 32, up_stages = 2;
     int factors[2] = {3, 3}, kernels[2] = {7, 7}, up_ch[2] = {256, 128};
     int n_codes = 12800, n_fft = 392, hop = 98, sample_rate = 44100;
+    bool f16 = false;  // every tensor of >= 2 dims stored F16 (an F16 GGUF conversion)
     uint64_t seed = 1;
 };
 
-// preset 0 = MioCodec-25Hz-44.1kHz shapes, 1 = tiny test codec.
+// preset 0 = MioCodec-25Hz-44.1kHz shapes, 1 = tiny test codec, 2 / 3 = the
+// same with F16 matrices.
 SynthCodecCfg synth_codec_preset(int preset);
 bool synth_write_codec(const std::string &path, const SynthCodecCfg &cfg);
 bool synth_write_voice(const std::string &path, uint64_t seed, int dim = 128);
@@ -34,11 +36,15 @@ struct SynthLlmCfg {
     int qtype = 8;   // 8 = all Q8_0; 15 = Q4_K_M mix (Q4_K + Q6_K)
     bool tied = true;
     bool qkv_bias = false;  // attn_{q,k,v}.bias tensors (qwen2)
+    // lfm2: layer i is attention when (i % attn_mod) is in attn_at, else a gated short conv
+    int attn_mod = 4, attn_at0 = 2, attn_at1 = -1;
     uint64_t seed = 1;
 };
 // preset: 0 tiny Q8_0 (llama), 1 tiny Q4_K_M (qwen3), 2 "0.1B" Q8_0, 3 "1.7B" Q4_K_M,
 //         4 "2.6B" Q8_0  (shapes sized to the published file sizes, README.md:189-196),
-//         5 tiny Q8_0 qwen2 with q/k/v projection biases
+//         5 tiny Q8_0 qwen2 with q/k/v projection biases, 6 "2.6B" Q8_0 as lfm2 (the LFM2-2.6B
+//         width, FFN, vocab and GQA; short-conv / attention layer hybrid), 7 tiny Q8_0 lfm2,
+//         8 tiny Q4_K_M lfm2
 SynthLlmCfg synth_llm_preset(int preset);
 bool synth_write_llm(const std::string &path, const SynthLlmCfg &cfg);
 // Token ids of the synthetic vocabulary.

@@ -51,6 +51,19 @@ SynthLlmCfg synth_llm_preset(int p) {
             c.name = "MioTTS-2.6B-synthetic", c.n_embd = 2048, c.n_layer = 32, c.n_head = 32,
             c.n_head_kv = 8, c.head_dim = 64, c.n_ff = 10752, c.n_vocab = 65536 + 12800;
             break;
+        case 6:  // LFM2-2.6B shape: 30 layers, attention on 8 of them (i % 4 == 2, and 29)
+            c.name = "MioTTS-2.6B-lfm2-synthetic", c.arch = "lfm2", c.n_embd = 2048, c.n_layer = 30,
+            c.n_head = 32, c.n_head_kv = 8, c.head_dim = 64, c.n_ff = 10752, c.n_vocab = 65536 + 12800;
+            c.rope_base = 1000000.f, c.rms_eps = 1e-5f, c.attn_mod = 4, c.attn_at0 = 2, c.attn_at1 = -1;
+            break;
+        case 7:
+            c.name = "tiny-lfm2", c.arch = "lfm2", c.n_layer = 5, c.attn_mod = 3, c.attn_at0 = 1;
+            c.rope_base = 1000000.f, c.rms_eps = 1e-5f;
+            break;
+        case 8:
+            c.name = "tiny-lfm2-q4km", c.arch = "lfm2", c.n_layer = 5, c.attn_mod = 3, c.attn_at0 = 1, c.qtype = 15;
+            c.rope_base = 1000000.f, c.rms_eps = 1e-5f;
+            break;
         default: break;
     }
     return c;
@@ -79,9 +92,15 @@ static std::string byte_token(int b) {
 
 static bool use_more_bits(int i, int n) { return i < n / 8 || i >= 7 * n / 8 || (i - n / 8) % 3 == 2; }
 
+bool synth_lfm2_is_attn(const SynthLlmCfg &c, int i) {
+    const int r = i % c.attn_mod;
+    return r == c.attn_at0 || r == c.attn_at1 || (c.n_layer == 30 && i == 29);
+}
+
 bool synth_write_llm(const std::string &path, const SynthLlmCfg &c) {
     GgufWriter w;
     const std::string a = c.arch;
+    const bool lfm2 = a == "lfm2";
     w.kv_str("general.architecture", a);
     w.kv_str("general.name", c.name);
     w.kv_u32("general.file_type", c.qtype == 15 ? 15 : 7);
@@ -90,7 +109,15 @@ bool synth_write_llm(const std::string &path, const SynthLlmCfg &c) {
     w.kv_u32(a + ".block_count", c.n_layer);
     w.kv_u32(a + ".feed_forward_length", c.n_ff);
     w.kv_u32(a + ".attention.head_count", c.n_head);
-    w.kv_u32(a + ".attention.head_count_kv", c.n_head_kv);
+    if (lfm2) {
+        // llama.cpp LFM2: head_count_kv per layer, 0 marks a short-conv (recurrent) layer
+        std::vector<int32_t> kv;
+        for (int i = 0; i < c.n_layer; ++i) kv.push_back(synth_lfm2_is_attn(c, i) ? c.n_head_kv : 0);
+        w.kv_arr_i32(a + ".attention.head_count_kv", kv);
+        w.kv_u32(a + ".shortconv.l_cache", 3);
+    } else {
+        w.kv_u32(a + ".attention.head_count_kv", c.n_head_kv);
+    }
     w.kv_u32(a + ".attention.key_length", c.head_dim);
     w.kv_u32(a + ".attention.value_length", c.head_dim);
     w.kv_f32(a + ".rope.freq_base", c.rope_base);
@@ -117,7 +144,7 @@ bool synth_write_llm(const std::string &path, const SynthLlmCfg &c) {
         std::string name;
         uint32_t type;
         int64_t k, rows;
-        int fill;  // 0 quantized N(0, w_std) rows, 1 ones, 2 f32 N(0, 0.5) (biases)
+        int fill;  // 0 quantized N(0, w_std) rows, 1 ones, 2 f32 N(0, 0.5) (biases / conv taps)
     };
     std::vector<T> ts;
     const uint32_t base = c.qtype == 15 ? GGML_Q4_K : GGML_Q8_0;
@@ -128,6 +155,12 @@ bool synth_write_llm(const std::string &path, const SynthLlmCfg &c) {
         const std::string p = "blk." + std::to_string(i) + ".";
         const bool mb = use_more_bits(i, c.n_layer);
         ts.push_back({p + "attn_norm.weight", GGML_F32, c.n_embd, 1, true});
+        if (lfm2 && !synth_lfm2_is_attn(c, i)) {
+            // gated short conv: in_proj -> B | C | X, depthwise taps [n_embd][3], out_proj
+            ts.push_back({p + "shortconv.in_proj.weight", base, c.n_embd, 3 * c.n_embd, false});
+            ts.push_back({p + "shortconv.conv.weight", GGML_F32, 3, c.n_embd, 2});
+            ts.push_back({p + "shortconv.out_proj.weight", base, c.n_embd, c.n_embd, false});
+        } else {
         ts.push_back({p + "attn_q.weight", base, c.n_embd, q_dim, false});
         ts.push_back({p + "attn_k.weight", base, c.n_embd, kv_dim, false});
         ts.push_back({p + "attn_v.weight", mb ? more : base, c.n_embd, kv_dim, false});
@@ -137,16 +170,18 @@ bool synth_write_llm(const std::string &path, const SynthLlmCfg &c) {
             ts.push_back({p + "attn_k.bias", GGML_F32, kv_dim, 1, 2});
             ts.push_back({p + "attn_v.bias", GGML_F32, kv_dim, 1, 2});
         }
-        if (a == "qwen3") {
+        if (a == "qwen3" || lfm2) {
             ts.push_back({p + "attn_q_norm.weight", GGML_F32, c.head_dim, 1, true});
             ts.push_back({p + "attn_k_norm.weight", GGML_F32, c.head_dim, 1, true});
+        }
         }
         ts.push_back({p + "ffn_norm.weight", GGML_F32, c.n_embd, 1, true});
         ts.push_back({p + "ffn_gate.weight", base, c.n_embd, c.n_ff, false});
         ts.push_back({p + "ffn_up.weight", base, c.n_embd, c.n_ff, false});
         ts.push_back({p + "ffn_down.weight", mb ? more : base, c.n_ff, c.n_embd, false});
     }
-    ts.push_back({"output_norm.weight", GGML_F32, c.n_embd, 1, true});
+    // lfm2's final norm is token_embd_norm (llama.cpp model.tok_norm)
+    ts.push_back({lfm2 ? "token_embd_norm.weight" : "output_norm.weight", GGML_F32, c.n_embd, 1, true});
     if (!c.tied) ts.push_back({"output.weight", more, c.n_embd, c.n_vocab, false});
     for (auto &t : ts) {
         if (t.rows == 1)
@@ -159,7 +194,8 @@ bool synth_write_llm(const std::string &path, const SynthLlmCfg &c) {
         if (t.fill == 1 || t.fill == 2) {
             float *f = (float *)dst;
             const uint64_t key = synth_key(c.seed, t.name);
-            for (int64_t i = 0; i < t.k; ++i) f[i] = t.fill == 1 ? 1.0f : 0.5f * synth_normal_fast(key, (uint64_t)i);
+            for (int64_t i = 0; i < t.k * t.rows; ++i)
+                f[i] = t.fill == 1 ? 1.0f : 0.5f * synth_normal_fast(key, (uint64_t)i);
             return;
         }
         const size_t rb = ggml_row_bytes(t.type, t.k);

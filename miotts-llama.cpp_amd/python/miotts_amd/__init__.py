@@ -100,7 +100,10 @@ def _declare(L: ctypes.CDLL) -> None:
         "mio_hip_codec_last_timings": (c_int, [_vp, _f32p]),
         "mio_hip_codec_last_reused": (c_int, [_vp, ctypes.POINTER(c_int)]),
         "mio_hip_llm_load_ms": (c_int, [_vp, ctypes.POINTER(ctypes.c_double)]),
-        "mio_hip_llm_step_layout": (c_int, [_vp, ctypes.POINTER(c_int)]),
+        "mio_hip_llm_step_kinds": (c_int, [_vp, _vp, c_int, ctypes.POINTER(c_int)]),
+        "mio_hip_llm_conv_ring": (c_int, [_vp, c_int, _vp, c_int]),
+        "mio_hip_llm_eval_layers": (c_int, [_vp, ctypes.c_int32, c_int, _vp, _vp]),
+        "mio_hip_llm_kv_rows": (c_int, [_vp, c_int, c_int, _vp, _vp]),
         "mio_hip_debug_matvec": (c_int, [_vp, ctypes.c_uint32, _vp, c_int, c_int, _vp, _vp]),
         "mio_quantize_rows": (c_int, [ctypes.c_uint32, _vp, c_int, c_int, _vp]),
         "mio_hip_debug_mmq": (c_int, [_vp, ctypes.c_uint32, _vp, c_int, c_int, _vp, c_int, c_int, _vp, _vp]),
@@ -463,11 +466,39 @@ class Llm:
         t[t == 0] = np.nan
         return (t - np.nanmin(t[0, :, 0])) * 0.01
 
-    def launches_per_layer(self) -> int:
-        """Decode-step launches per layer (4: attention inside attn_in; 5: its own launch)."""
-        v = ctypes.c_int(0)
-        check(lib().mio_hip_llm_step_layout(self.h, ctypes.byref(v)))
-        return v.value
+    def eval_layers(self, token: int, pos: int):
+        """One decode step: (residual before layer 0 and after each layer [n_layer + 1,
+        n_embd], logits)."""
+        xs = np.empty((self.n_layer + 1, self.n_embd), np.float32)
+        lg = np.empty(self.n_vocab, np.float32)
+        check(lib().mio_hip_llm_eval_layers(self.h, token, pos, _ptr(xs), _ptr(lg)))
+        return xs, lg
+
+    def kv_rows(self, il: int, n_pos: int):
+        """F16 K, V cache rows [0, n_pos) of layer il: two [n_kv, n_pos, head_dim] arrays."""
+        k = np.empty((self.n_kv, n_pos, self.head_dim), np.float16)
+        v = np.empty_like(k)
+        check(lib().mio_hip_llm_kv_rows(self.h, il, n_pos, _ptr(k), _ptr(v)))
+        return k, v
+
+    def step_kinds(self) -> list:
+        """The decode step's launches in order, as time_kernel's `which` (0 attn_in,
+        1 attention, 2 attn_out, 3 ffn_in, 4 ffn_down, 8 conv_in, 9 conv_out; 6 lm_head)."""
+        n = ctypes.c_int(0)
+        check(lib().mio_hip_llm_step_kinds(self.h, None, 0, ctypes.byref(n)))
+        k = np.zeros(n.value, np.int32)
+        check(lib().mio_hip_llm_step_kinds(self.h, _ptr(k), n.value, ctypes.byref(n)))
+        return [int(v) for v in k]
+
+    def conv_ring(self, il: int, ring=None):
+        """lfm2 short-conv state of layer il, [4, n_embd] (slot p & 3 = B*X of position p);
+        with `ring`: sets it."""
+        if ring is None:
+            r = np.empty((4, self.n_embd), np.float32)
+            check(lib().mio_hip_llm_conv_ring(self.h, il, _ptr(r), 0))
+            return r
+        r = np.ascontiguousarray(ring, np.float32)
+        check(lib().mio_hip_llm_conv_ring(self.h, il, _ptr(r), 1))
 
     def generate(self, prompt, max_tokens: int, temperature: float = 0.8, seed: int = 42,
                  allow=(-1, -1), eos=(-1, -1), check_interval: int = 20) -> np.ndarray:

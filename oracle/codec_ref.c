@@ -14,10 +14,14 @@
  *   rope mode 0 adjacent pairs, theta_p,i = p * theta_scale^i by repeated float
  *               multiplication (ggml rope cache), theta_scale = powf(base,-2/n_dims) (:260-263)
  *   soft_max    scores*0.125 + mask(0/-inf), exp(x-max), sum in double, * (1/sum)  (:271-275)
- *   mul_mat f32 f32 dot products                                                 (:204-209)
+ *   mul_mat     f32 weight: f32 dot products; F16 weight: the input rounded to f16 first
+ *               (ggml's vec_dot_type of F16 is F16), products summed in f32          (:204-209)
  *   conv_1d     kernel AND im2col input rounded to f16, products summed in f32    (:381-386)
- *   conv_transpose_1d (f32 kernel) dst[t*s+k] += dot_ci(x[t], W_k) in ascending t  (:624, :685)
- *   snake       x + sin(exp(a)*x)^2 / exp(b)                                     (:410-420, :717-725)
+ *   conv_transpose_1d dst[t*s+k] += dot_ci(x[t], W_k) in ascending t; an F16 kernel rounds
+ *               the input to f16 like mul_mat                                   (:624, :685)
+ *   snake       x + sin(exp(a)*x)^2 / exp(b); F16 a / b: ggml_exp keeps F16, so exp is
+ *               rounded to f16                                                   (:410-420, :717-725)
+ *   other F16 tensors (norm / bias / embedding) enter as their exact f32 values
  *   head        mag = clamp(exp(.),0,100), (re,im) = mag*(cos,sin)(phase)         (:728-737)
  */
 #include <math.h>
@@ -30,6 +34,7 @@
 
 struct mo_codec {
     mo_gguf *g;
+    float **f32_of; /* per GGUF tensor: f32 copy of an F16 tensor, else NULL */
     int sr, n_fft, hop, n_freq, spt, head_out;
     int pre_layers, pre_dim, pre_heads, pre_ff, pre_win;
     int dec_layers, dec_dim, dec_heads, dec_ff, dec_win, adaln;
@@ -41,9 +46,30 @@ struct mo_codec {
 
 static const float *W(const mo_codec *c, const char *name) {
     const mo_tensor *t = mo_gguf_tensor(c->g, name);
-    if (!t || t->type != 0) return NULL;
-    return (const float *)t->data;
+    if (!t) return NULL;
+    if (t->type == 0) return (const float *)t->data;
+    if (t->type == 1) return c->f32_of[t - c->g->tensors];
+    return NULL;
 }
+
+/* a matrix operand and whether it was stored F16 (mul_mat then rounds its input to f16) */
+typedef struct {
+    const float *w;
+    int f16;
+} wref;
+
+static wref WR(const mo_codec *c, const char *name) {
+    const mo_tensor *t = mo_gguf_tensor(c->g, name);
+    wref r = {W(c, name), t && t->type == 1};
+    return r;
+}
+
+static int is_f16(const mo_codec *c, const char *name) {
+    const mo_tensor *t = mo_gguf_tensor(c->g, name);
+    return t && t->type == 1;
+}
+
+float mo_fp16_to_f32(uint16_t h);
 
 static int WN(const mo_codec *c, const char *name, int dim) {
     const mo_tensor *t = mo_gguf_tensor(c->g, name);
@@ -85,11 +111,24 @@ mo_codec *mo_codec_load(const char *path) {
     memcpy(c->factors, tf->data, sizeof(int) * c->up_stages);
     memcpy(c->kernels, tk->data, sizeof(int) * c->up_stages);
     c->n_codes = WN(c, "token_embd", 1);
+    c->f32_of = (float **)calloc(g->n_tensors, sizeof(float *));
+    for (int i = 0; i < g->n_tensors; i++) {
+        const mo_tensor *t = &g->tensors[i];
+        if (t->type != 1) continue;
+        size_t n = 1;
+        for (int d = 0; d < t->n_dims; d++) n *= (size_t)t->ne[d];
+        float *f = (float *)malloc(n * sizeof(float));
+        const uint16_t *h = (const uint16_t *)t->data;
+        for (size_t j = 0; j < n; j++) f[j] = mo_fp16_to_f32(h[j]);
+        c->f32_of[i] = f;
+    }
     return c;
 }
 
 void mo_codec_free(mo_codec *c) {
     if (!c) return;
+    for (int i = 0; i < c->g->n_tensors; i++) free(c->f32_of[i]);
+    free(c->f32_of);
     mo_gguf_close(c->g);
     free(c);
 }
@@ -115,9 +154,24 @@ static float dot_f32(const float *a, const float *b, int n) {
     return r;
 }
 
+float mo_f16_round(float f);
+
+/* x rounded to f16 (a fresh buffer) when rx, else x itself */
+static const float *round_in(const float *x, size_t n, int rx, float **tmp) {
+    *tmp = NULL;
+    if (!rx) return x;
+    float *r = (float *)malloc(n * sizeof(float));
+    for (size_t i = 0; i < n; i++) r[i] = mo_f16_round(x[i]);
+    *tmp = r;
+    return r;
+}
+
 /* y[m][n] = x[m][:] . w[n][:] (+ b[n]);  w is ggml [K, N] = row-major [N][K] */
-static void linear(const float *x, int M, int K, const float *w, const float *b, int N, float *y) {
+static void linear(const float *x_in, int M, int K, wref wr, const float *b, int N, float *y) {
     const int NB = 64;
+    float *tmp;
+    const float *x = round_in(x_in, (size_t)M * K, wr.f16, &tmp);
+    const float *w = wr.w;
 #pragma omp parallel for collapse(2) schedule(static)
     for (int n0 = 0; n0 < N; n0 += NB)
         for (int m = 0; m < M; m++) {
@@ -127,6 +181,7 @@ static void linear(const float *x, int M, int K, const float *w, const float *b,
                 y[(size_t)m * N + n] = b ? v + b[n] : v;
             }
         }
+    free(tmp);
 }
 
 /* ggml_norm (+ optional affine w,b applied as separate mul/add) */
@@ -348,8 +403,11 @@ static void conv1d(const float *x, int L, int Cin, const float *w /*[Cout][Cin][
 }
 
 /* conv_transpose_1d (f32 kernel ggml [K][Cout][Cin] = mem [Cin][Cout][K]) + bias + trim */
-static void conv_transpose1d(const float *x, int L, int Cin, const float *w, int K, int Cout,
+static void conv_transpose1d(const float *x_in, int L, int Cin, wref wr, int K, int Cout,
                              int stride, int trim, const float *bias, float *y /*[L*stride][Cout]*/) {
+    float *tmp;
+    const float *x = round_in(x_in, (size_t)L * Cin, wr.f16, &tmp);
+    const float *w = wr.w;
     const int Lraw = (L - 1) * stride + K;
     const int Lout = Lraw - 2 * trim;
     /* permute kernel to [Cout][K][Cin] as ggml does */
@@ -374,11 +432,15 @@ static void conv_transpose1d(const float *x, int L, int Cin, const float *w, int
         free(acc);
     }
     free(wp);
+    free(tmp);
 }
 
-static void snake_rows(float *x, int M, int C, const float *la, const float *lb) {
+static void snake_rows(float *x, int M, int C, const float *la, const float *lb, int fa, int fb) {
     float *a = (float *)malloc(sizeof(float) * C), *b = (float *)malloc(sizeof(float) * C);
-    for (int c = 0; c < C; c++) { a[c] = expf(la[c]); b[c] = expf(lb[c]); }
+    for (int c = 0; c < C; c++) {
+        a[c] = fa ? mo_f16_round(expf(la[c])) : expf(la[c]);
+        b[c] = fb ? mo_f16_round(expf(lb[c])) : expf(lb[c]);
+    }
 #pragma omp parallel for schedule(static)
     for (int m = 0; m < M; m++)
         for (int c = 0; c < C; c++) {
@@ -463,30 +525,31 @@ int mo_codec_decode_stage(mo_codec *c, const int *codes, int T, const float *emb
         const int H = c->pre_heads, hd = Dp / H;
         for (int i = 0; i < c->pre_layers; i++) {
 #define PW(s) (snprintf(n, sizeof n, "wave_prenet.blk.%d.%s", i, s), W(c, n))
+#define PWR(s) (snprintf(n, sizeof n, "wave_prenet.blk.%d.%s", i, s), WR(c, n))
             layer_norm(x, T, Dp, PW("attn_norm.weight"), PW("attn_norm.bias"), c->eps, h);
             float *q = a, *k = a + (size_t)T * Dp, *v = a + (size_t)2 * T * Dp;
-            linear(h, T, Dp, PW("attn_q.weight"), NULL, Dp, q);
-            linear(h, T, Dp, PW("attn_k.weight"), NULL, Dp, k);
-            linear(h, T, Dp, PW("attn_v.weight"), NULL, Dp, v);
+            linear(h, T, Dp, PWR("attn_q.weight"), NULL, Dp, q);
+            linear(h, T, Dp, PWR("attn_k.weight"), NULL, Dp, k);
+            linear(h, T, Dp, PWR("attn_v.weight"), NULL, Dp, v);
             attention(q, k, v, Dp, T, H, hd, c->pre_win, c->theta, b);
-            linear(b, T, Dp, PW("attn_output.weight"), NULL, Dp, h);
+            linear(b, T, Dp, PWR("attn_output.weight"), NULL, Dp, h);
             for (size_t j = 0; j < (size_t)T * Dp; j++) x[j] = x[j] + h[j];
             layer_norm(x, T, Dp, PW("ffn_norm.weight"), PW("ffn_norm.bias"), c->eps, h);
             float *g = a, *u = f;
-            linear(h, T, Dp, PW("ffn_gate.weight"), NULL, c->pre_ff, g);
-            linear(h, T, Dp, PW("ffn_up.weight"), NULL, c->pre_ff, u);
+            linear(h, T, Dp, PWR("ffn_gate.weight"), NULL, c->pre_ff, g);
+            linear(h, T, Dp, PWR("ffn_up.weight"), NULL, c->pre_ff, u);
             for (size_t j = 0; j < (size_t)T * c->pre_ff; j++) g[j] = silu(g[j]) * u[j];
-            linear(g, T, c->pre_ff, PW("ffn_down.weight"), NULL, Dp, h);
+            linear(g, T, c->pre_ff, PWR("ffn_down.weight"), NULL, Dp, h);
             for (size_t j = 0; j < (size_t)T * Dp; j++) x[j] = x[j] + h[j];
 #undef PW
         }
         layer_norm(x, T, Dp, W(c, "wave_prenet.norm.weight"), W(c, "wave_prenet.norm.bias"), c->eps, h);
-        linear(h, T, Dp, W(c, "wave_prenet.output.weight"), W(c, "wave_prenet.output.bias"), Dd, x);
+        linear(h, T, Dp, WR(c, "wave_prenet.output.weight"), W(c, "wave_prenet.output.bias"), Dd, x);
     }
     DONE(x, T, Dd);
 
     /* 3. wave_upsample ConvT k=2 s=2 (:622-626) */
-    conv_transpose1d(x, T, Dd, W(c, "wave_upsample.weight"), WN(c, "wave_upsample.weight", 0), Dd,
+    conv_transpose1d(x, T, Dd, WR(c, "wave_upsample.weight"), WN(c, "wave_upsample.weight", 0), Dd,
                      2, 0, W(c, "wave_upsample.bias"), h);
     memcpy(x, h, sizeof(float) * (size_t)S * Dd);
     DONE(x, S, Dd);
@@ -507,27 +570,28 @@ int mo_codec_decode_stage(mo_codec *c, const int *codes, int T, const float *emb
         float *cond = (float *)malloc(sizeof(float) * 3 * Dd);
         for (int i = 0; i < c->dec_layers; i++) {
 #define DW(s) (snprintf(n, sizeof n, "wave_decoder.blk.%d.%s", i, s), W(c, n))
-            linear(se, 1, A, DW("attn_cond.weight"), DW("attn_cond.bias"), 3 * Dd, cond);
+#define DWR(s) (snprintf(n, sizeof n, "wave_decoder.blk.%d.%s", i, s), WR(c, n))
+            linear(se, 1, A, DWR("attn_cond.weight"), DW("attn_cond.bias"), 3 * Dd, cond);
             adaln_norm(x, S, Dd, cond, cond + Dd, c->eps, h);
             float *q = a, *k = a + (size_t)S * Dd, *v = a + (size_t)2 * S * Dd;
-            linear(h, S, Dd, DW("attn_q.weight"), NULL, Dd, q);
-            linear(h, S, Dd, DW("attn_k.weight"), NULL, Dd, k);
-            linear(h, S, Dd, DW("attn_v.weight"), NULL, Dd, v);
+            linear(h, S, Dd, DWR("attn_q.weight"), NULL, Dd, q);
+            linear(h, S, Dd, DWR("attn_k.weight"), NULL, Dd, k);
+            linear(h, S, Dd, DWR("attn_v.weight"), NULL, Dd, v);
             attention(q, k, v, Dd, S, H, hd, c->dec_win, c->theta, b);
-            linear(b, S, Dd, DW("attn_output.weight"), NULL, Dd, h);
+            linear(b, S, Dd, DWR("attn_output.weight"), NULL, Dd, h);
             for (int m = 0; m < S; m++)
                 for (int d = 0; d < Dd; d++) {
                     const size_t j = (size_t)m * Dd + d;
                     const float gh = h[j] * cond[2 * Dd + d];
                     x[j] = x[j] + gh;
                 }
-            linear(se, 1, A, DW("ffn_cond.weight"), DW("ffn_cond.bias"), 3 * Dd, cond);
+            linear(se, 1, A, DWR("ffn_cond.weight"), DW("ffn_cond.bias"), 3 * Dd, cond);
             adaln_norm(x, S, Dd, cond, cond + Dd, c->eps, h);
             float *g = a, *u = f;
-            linear(h, S, Dd, DW("ffn_gate.weight"), NULL, c->dec_ff, g);
-            linear(h, S, Dd, DW("ffn_up.weight"), NULL, c->dec_ff, u);
+            linear(h, S, Dd, DWR("ffn_gate.weight"), NULL, c->dec_ff, g);
+            linear(h, S, Dd, DWR("ffn_up.weight"), NULL, c->dec_ff, u);
             for (size_t j = 0; j < (size_t)S * c->dec_ff; j++) g[j] = silu(g[j]) * u[j];
-            linear(g, S, c->dec_ff, DW("ffn_down.weight"), NULL, Dd, h);
+            linear(g, S, c->dec_ff, DWR("ffn_down.weight"), NULL, Dd, h);
             for (int m = 0; m < S; m++)
                 for (int d = 0; d < Dd; d++) {
                     const size_t j = (size_t)m * Dd + d;
@@ -537,7 +601,7 @@ int mo_codec_decode_stage(mo_codec *c, const int *codes, int T, const float *emb
 #undef DW
         }
         float *nc = (float *)malloc(sizeof(float) * 2 * Dd);
-        linear(se, 1, A, W(c, "wave_decoder.norm_cond.weight"), W(c, "wave_decoder.norm_cond.bias"), 2 * Dd, nc);
+        linear(se, 1, A, WR(c, "wave_decoder.norm_cond.weight"), W(c, "wave_decoder.norm_cond.bias"), 2 * Dd, nc);
         adaln_norm(x, S, Dd, nc, nc + Dd, c->eps, h);
         memcpy(x, h, sizeof(float) * (size_t)S * Dd);
         free(nc); free(se); free(cond);
@@ -558,7 +622,7 @@ int mo_codec_decode_stage(mo_codec *c, const int *codes, int T, const float *emb
         const int fac = c->factors[s], K = c->kernels[s], trim = (K - fac) / 2;
         snprintf(n, sizeof n, "wave_upsampler.up.%d.weight", s);
         const int Cout = WN(c, n, 1);
-        const float *wt = W(c, n);
+        const wref wt = WR(c, n);
         snprintf(n, sizeof n, "wave_upsampler.up.%d.bias", s);
         conv_transpose1d(x, L, C, wt, K, Cout, fac, trim > 0 ? trim : 0, W(c, n), h);
         L = (L - 1) * fac + K - 2 * (trim > 0 ? trim : 0);
@@ -567,7 +631,7 @@ int mo_codec_decode_stage(mo_codec *c, const int *codes, int T, const float *emb
         char na[96], nb[96];
         snprintf(na, sizeof na, "wave_upsampler.snake.%d.alpha", s);
         snprintf(nb, sizeof nb, "wave_upsampler.snake.%d.beta", s);
-        snake_rows(x, L, C, W(c, na), W(c, nb));
+        snake_rows(x, L, C, W(c, na), W(c, nb), is_f16(c, na), is_f16(c, nb));
         char p[64];
         snprintf(p, sizeof p, "wave_upsampler.resblk.%d.", s);
         resnet_block(c, p, x, L, C, a, b);
@@ -575,14 +639,15 @@ int mo_codec_decode_stage(mo_codec *c, const int *codes, int T, const float *emb
     }
 
     /* 8. out_proj + out_snake (:711-725) */
-    linear(x, L, C, W(c, "wave_upsampler.out_proj.weight"), W(c, "wave_upsampler.out_proj.bias"), Dd, h);
-    snake_rows(h, L, Dd, W(c, "wave_upsampler.out_snake.alpha"), W(c, "wave_upsampler.out_snake.beta"));
+    linear(x, L, C, WR(c, "wave_upsampler.out_proj.weight"), W(c, "wave_upsampler.out_proj.bias"), Dd, h);
+    snake_rows(h, L, Dd, W(c, "wave_upsampler.out_snake.alpha"), W(c, "wave_upsampler.out_snake.beta"),
+               is_f16(c, "wave_upsampler.out_snake.alpha"), is_f16(c, "wave_upsampler.out_snake.beta"));
     DONE(h, L, Dd);
 
     /* 9. iSTFT head (:728-737) + interleave (:801-808) */
     {
         const int nf = c->n_freq;
-        linear(h, L, Dd, W(c, "istft_head.out.weight"), W(c, "istft_head.out.bias"), c->head_out, a);
+        linear(h, L, Dd, WR(c, "istft_head.out.weight"), W(c, "istft_head.out.bias"), c->head_out, a);
         float *spec = b;
 #pragma omp parallel for schedule(static)
         for (int t = 0; t < L; t++)

@@ -173,6 +173,20 @@ int64_t mo_gguf_int(const mo_gguf *g, const char *key, int64_t def) {
     return (kv && kv->type != 6 && kv->type != 12 && kv->type != 8 && kv->type != 9) ? kv->i : def;
 }
 
+int64_t mo_gguf_arr_int(const mo_gguf *g, const char *key, int idx, int64_t def) {
+    const mo_kv *kv = mo_gguf_kv(g, key);
+    if (!kv) return def;
+    if (kv->type != 9) return mo_gguf_int(g, key, def);
+    if (idx < 0 || (uint64_t)idx >= kv->arr_n || !kv->arr_data) return def;
+    const unsigned char *p = (const unsigned char *)kv->arr_data;
+    switch (kv->arr_type) {
+        case 4: { uint32_t v; memcpy(&v, p + 4 * idx, 4); return v; }
+        case 5: { int32_t v; memcpy(&v, p + 4 * idx, 4); return v; }
+        case 10: case 11: { int64_t v; memcpy(&v, p + 8 * idx, 8); return v; }
+        default: return def;
+    }
+}
+
 double mo_gguf_float(const mo_gguf *g, const char *key, double def) {
     const mo_kv *kv = mo_gguf_kv(g, key);
     return (kv && (kv->type == 6 || kv->type == 12)) ? kv->f : def;

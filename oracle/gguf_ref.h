@@ -39,6 +39,8 @@ void mo_gguf_close(mo_gguf *g);
 const mo_kv *mo_gguf_kv(const mo_gguf *g, const char *key);
 int64_t mo_gguf_int(const mo_gguf *g, const char *key, int64_t def);
 double mo_gguf_float(const mo_gguf *g, const char *key, double def);
+/* element idx of an integer array KV (a scalar KV: its value; absent: def) */
+int64_t mo_gguf_arr_int(const mo_gguf *g, const char *key, int idx, int64_t def);
 const mo_tensor *mo_gguf_tensor(const mo_gguf *g, const char *name);
 size_t mo_type_size(uint32_t type, int64_t n);
 

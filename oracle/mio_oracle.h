@@ -59,6 +59,13 @@ void mo_llm_free(mo_llm *m);
 void mo_llm_info(const mo_llm *m, int *info);
 void mo_llm_reset(mo_llm *m);
 int mo_llm_eval(mo_llm *m, int token, int pos, float *logits /* [n_vocab] or NULL */);
+/* the pieces of one eval: embedding row; decoder layer il at pos (writes its K/V row pos);
+ * final norm + lm_head; F16 K/V rows [0, n_pos) of layer il as [n_kv][n_pos][hd] (set = 0:
+ * copy out of the cache, 1: into it) */
+int mo_llm_embed(mo_llm *m, int token, float *x);
+int mo_llm_layer(mo_llm *m, int il, int pos, const float *x_in, float *x_out);
+void mo_llm_head(mo_llm *m, const float *x, float *logits);
+int mo_llm_kv(mo_llm *m, int il, int n_pos, uint16_t *k, uint16_t *v, int set);
 float mo_gumbel(uint64_t seed, int step, int idx);
 int mo_sample(const float *logits, float temp, uint64_t seed, int step, int lo, int hi);
 int mo_set_threads(int n);

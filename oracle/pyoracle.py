@@ -51,6 +51,12 @@ def oracle() -> ctypes.CDLL:
         _o.mo_llm_info.argtypes = [vp, vp]
         _o.mo_llm_reset.argtypes = [vp]
         _o.mo_llm_eval.argtypes = [vp, ci, ci, vp]
+        _o.mo_llm_embed.argtypes = [vp, ci, vp]
+        _o.mo_llm_layer.argtypes = [vp, ci, ci, vp, vp]
+        _o.mo_llm_head.argtypes = [vp, vp, vp]
+        _o.mo_llm_kv.argtypes = [vp, ci, ci, vp, vp, ci]
+        _o.mo_llm_conv.argtypes = [vp, ci, vp, ci]
+        _o.mo_llm_is_conv.argtypes = [vp, ci]
         _o.mo_gumbel.restype = ctypes.c_float
         _o.mo_gumbel.argtypes = [ctypes.c_uint64, ci, ci]
         _o.mo_sample.restype = ci
@@ -190,6 +196,52 @@ class Llm:
         if rc:
             raise RuntimeError(f"oracle eval failed {rc}")
         return out
+
+    def embed(self, token: int) -> np.ndarray:
+        x = np.zeros(self.n_embd, np.float32)
+        if oracle().mo_llm_embed(self.h, token, x.ctypes.data):
+            raise RuntimeError("oracle embed failed")
+        return x
+
+    def layer(self, il: int, pos: int, x) -> np.ndarray:
+        """Residual after decoder layer il at pos for input x (writes the layer's K/V row)."""
+        xi = np.ascontiguousarray(x, np.float32)
+        out = np.zeros(self.n_embd, np.float32)
+        if oracle().mo_llm_layer(self.h, il, pos, xi.ctypes.data, out.ctypes.data):
+            raise RuntimeError("oracle layer failed")
+        return out
+
+    def head(self, x) -> np.ndarray:
+        xi = np.ascontiguousarray(x, np.float32)
+        out = np.zeros(self.n_vocab, np.float32)
+        oracle().mo_llm_head(self.h, xi.ctypes.data, out.ctypes.data)
+        return out
+
+    def kv(self, il: int, n_pos: int):
+        """F16 K, V rows [0, n_pos) of layer il: two [n_kv, n_pos, hd] float16 arrays."""
+        k = np.zeros((self.n_kv, n_pos, self.head_dim), np.float16)
+        v = np.zeros_like(k)
+        oracle().mo_llm_kv(self.h, il, n_pos, k.ctypes.data, v.ctypes.data, 0)
+        return k, v
+
+    def is_conv(self, il: int) -> bool:
+        """lfm2: layer il is a gated short-conv layer."""
+        return bool(oracle().mo_llm_is_conv(self.h, il))
+
+    def conv_ring(self, il: int) -> np.ndarray:
+        """lfm2 short-conv ring of layer il: [4, n_embd], bx of position p in row p & 3."""
+        r = np.zeros((4, self.n_embd), np.float32)
+        oracle().mo_llm_conv(self.h, il, r.ctypes.data, 0)
+        return r
+
+    def set_conv_ring(self, il: int, ring):
+        r = np.ascontiguousarray(ring, np.float32)
+        oracle().mo_llm_conv(self.h, il, r.ctypes.data, 1)
+
+    def set_kv(self, il: int, k, v):
+        k = np.ascontiguousarray(k, np.float16)
+        v = np.ascontiguousarray(v, np.float16)
+        oracle().mo_llm_kv(self.h, il, k.shape[1], k.ctypes.data, v.ctypes.data, 1)
 
     def generate(self, prompt, max_tokens, temperature=0.8, seed=42, allow=(-1, -1), eos=(-1, -1)):
         lo = 0 if allow[0] < 0 else allow[0]

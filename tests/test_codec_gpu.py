@@ -139,3 +139,57 @@ def test_codec_incremental_streaming_decode(device, files, emb):
     full = gc.decode_pcm(edited, emb)
     d = inc.astype(np.float64) - full
     assert np.sqrt(np.mean(d * d)) <= 1e-5 * np.sqrt(np.mean(full.astype(np.float64) ** 2))
+
+
+@pytest.mark.parametrize("preset,T", [(2, 7), (2, 33), (3, 20)])
+def test_codec_f16_weights(device, tmp_path, emb, preset, T):
+    """A codec GGUF whose matrices are F16 (synthetic presets 2 / 3: every tensor of >= 2 dims
+    F16): ggml's mul_mat and conv_transpose_1d then convert the activation to the F16
+    vec_dot_type (miocodec.cpp:205-209 linear, :624 / :685 ConvT), which the GPU GEMMs do in
+    their operand staging (GemmArgs::a_f16) and the oracle before its dot products (whose F16
+    path tests/test_np_codec.py checks against the numpy restatement). Stages before the
+    spectrogram: the F32 codec's bounds. The spectrogram head rounds its input to f16 and then
+    exponentiates, so one-ulp input flips (last-bit differences upstream crossing an f16
+    rounding boundary) grow into ~1e-3 of the output: there the GPU is checked teacher-forced
+    (numpy head with f16 rounding on the GPU's own stage input: tight; without the rounding:
+    measurably farther, so the rounding is proven present) and chained against the oracle
+    at 5e-3; PCM at 5e-3 of its rms."""
+    import np_codec
+    path = m.synth_codec(str(tmp_path / f"f16_{preset}.gguf"), preset, 1)
+    from miotts_amd import gguf_np
+    r = gguf_np.GGUFReader(path)
+    assert r.tensor("wave_prenet.blk.0.attn_q.weight").type == 1 and r.tensor("wave_upsample.weight").type == 1
+    gc = m.Codec(device, path)
+    oc = pyoracle.Codec(path)
+    codes = (np.arange(T, dtype=np.int64) * 7919 + 13) % 12800
+    cap = 18 * T * 512 + 4096
+    last = oc.n_stages - 1
+    for st in range(last):
+        _stage_close(gc.decode_stage(codes, emb, st, cap), oc.decode_stage(codes, emb, st, cap),
+                     f"f16 preset {preset} T={T} stage {st}")
+    g_in = gc.decode_stage(codes, emb, last - 1, cap).astype(np.float64)
+    g_spec = gc.decode_stage(codes, emb, last, cap).astype(np.float64)
+    nc = np_codec.Codec(path)
+    w, h16 = nc.W("istft_head.out.weight")
+    assert h16
+    bias = nc.W("istft_head.out.bias")[0]
+    nf = nc.n_freq
+
+    def head(x):
+        y = x @ w.T + bias
+        mag = np.clip(np.exp(y[:, :nf]), 0.0, 100.0)
+        return np.stack([mag * np.cos(y[:, nf:]), mag * np.sin(y[:, nf:])], axis=-1).reshape(len(y), 2 * nf)
+
+    def rel(a, b):
+        return float(np.sqrt(np.mean((a - b) ** 2)) / (np.sqrt(np.mean(b * b)) + 1e-30))
+
+    e_round = rel(g_spec, head(np_codec._h(g_in)))
+    e_plain = rel(g_spec, head(g_in))
+    print(f"f16 preset {preset} T={T}: spectrogram teacher-forced rel_rms {e_round:.3g} "
+          f"(without the f16 input rounding {e_plain:.3g})")
+    assert e_round <= 2e-5 and e_plain >= 5 * e_round, (e_round, e_plain)
+    o_spec = oc.decode_stage(codes, emb, last, cap).astype(np.float64)
+    assert g_spec.shape == o_spec.shape
+    assert rel(g_spec, o_spec) <= 5e-3, rel(g_spec, o_spec)
+    gp, op = gc.decode_pcm(codes, emb).astype(np.float64), oc.decode_pcm(codes, emb).astype(np.float64)
+    assert gp.shape == op.shape and rel(gp, op) <= 5e-3, rel(gp, op)

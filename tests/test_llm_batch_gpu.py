@@ -102,3 +102,25 @@ def test_batch_1p7b_q4km(device, tmp_path):
     got = g.generate_batch(prompts, 16, 0.8, [42, 43, 44, 45], allow=ALLOW)
     for b in range(4):
         assert np.array_equal(got[b], g.generate(prompts[b], 16, 0.8, 42 + b, allow=ALLOW)), b
+
+
+def test_batch_c4_2p6b_q8_b8(device, synth_llm_path):
+    """BASELINE config C4's per-GPU workload: the 2.6B Q8_0 model (32 layers, GQA 32/8 at head
+    dim 64, n_ff 10752, 78336 vocab), 8 utterances decoded together, 48 tokens each: every
+    stream equals its single-stream decode bit for bit, and stream 0 follows the oracle's
+    decode (shared counter-based sampler) up to its first divergence, which the large models'
+    flip noise allows no earlier than step 16 (test_llm_gpu.py, free-run test)."""
+    path = synth_llm_path(4)
+    g = m.Llm(device, path, 512)
+    prompts = _prompts(8, 44)
+    seeds = [4200 + 3 * b for b in range(8)]
+    got = g.generate_batch(prompts, 48, 0.8, seeds, allow=ALLOW)
+    for b in range(8):
+        ref = g.generate(prompts[b], 48, 0.8, seeds[b], allow=ALLOW)
+        assert np.array_equal(got[b], ref), b
+    g.close()
+    o = pyoracle.Llm(path, 128)
+    to = o.generate(prompts[0], 48, 0.8, seeds[0], allow=ALLOW)
+    same = got[0] == to
+    first = int(np.argmin(same)) if not same.all() else len(same)
+    assert first >= 16, (first, got[0], to)

@@ -216,16 +216,19 @@ def test_qwen2_bias_logits_and_generate(device, synth_llm_path, tmp_path):
     assert first >= 38
 
 
-def test_loader_rejects_lfm2_and_unknown_biases(device, tmp_path):
-    """lfm2 is refused by name (hybrid short-conv block not implemented); a bias tensor other
-    than attn_{q,k,v}.bias is refused rather than silently dropped."""
+def test_loader_rejects_unknown_biases_and_incomplete_lfm2(device, tmp_path):
+    """A bias tensor other than attn_{q,k,v}.bias is refused rather than silently dropped; an
+    lfm2 file whose attention layers lack their q norm is refused by the tensor's name."""
     from miotts_amd import gguf_np
     src = m.synth_llm(str(tmp_path / "q2.gguf"), 5, 1)
-    for arch, extra, msg in [("lfm2", None, "short-conv"), (None, "blk.0.ffn_down.bias", "bias tensor")]:
-        dst = str(tmp_path / "patched.gguf")
-        gguf_np.rewrite(src, dst, arch=arch, extra_f32=extra)
-        with pytest.raises(m.HipError, match=msg):
-            m.Llm(device, dst, 128)
+    dst = str(tmp_path / "patched.gguf")
+    gguf_np.rewrite(src, dst, extra_f32="blk.0.ffn_down.bias")
+    with pytest.raises(m.HipError, match="bias tensor"):
+        m.Llm(device, dst, 128)
+    lf = m.synth_llm(str(tmp_path / "lfm2.gguf"), 7, 1)
+    gguf_np.rewrite(lf, dst, drop_suffix="attn_q_norm.weight")
+    with pytest.raises(m.HipError, match="attn_q_norm"):
+        m.Llm(device, dst, 128)
 
 
 # --- batched prompt prefill (csrc/hip/llm_prefill.hip; reference prefill llama_decode,

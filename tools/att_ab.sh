@@ -6,7 +6,7 @@ out=gpurun_out/$tag
 mkdir -p $out
 export TMPDIR=/tmp
 if [ "$2" = "tests" ]; then
-  timeout -k 10 600 python -u -m pytest tests/test_llm_gpu.py tests/test_cli_gpu.py -x -v --timeout 300 --timeout-method thread > $out/tests.log 2>&1
+  MIO_ATT_FUSED=1 timeout -k 10 600 python -u -m pytest tests/test_llm_gpu.py tests/test_cli_gpu.py -x -v --timeout 300 --timeout-method thread > $out/tests.log 2>&1
 fi
 for r in 1 2; do
   for f in 0 1; do

@@ -24,7 +24,9 @@ llm.generate([256, 257, 65, 258, 257], a.pos, 0.8, 1, allow=(m.SYNTH_SPEECH0, m.
              check_interval=50)
 t = llm.timeline()
 nl = t.shape[0]
-names = ["attn_in", "attention", "attn_out", "ffn_in", "ffn_down"] * ((nl - 1) // 5) + ["lm_head"]
+KN = {0: "attn_in", 1: "attention", 2: "attn_out", 3: "ffn_in", 4: "ffn_down", 6: "lm_head", 8: "conv_in",
+      9: "conv_out"}
+names = [KN[k] for k in llm.step_kinds()]
 s0 = np.nanmin(t[:, :, 0], axis=1)
 s1 = np.nanmax(t[:, :, 0], axis=1)
 e0 = np.nanmin(t[:, :, 7], axis=1)
