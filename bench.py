@@ -292,6 +292,26 @@ def roofline(llm, preset):
                         "include the K/V rows" if fused else ""))}
 
 
+F32_MFMA_PEAK_TFS = 157.3  # MI355X_MICROARCH.md: f32 matrix (and vector) peak, exact f32
+
+
+def codec_roofline(flops, codec_ms, tokens):
+    """The codec's compute roofline: its algorithmic FLOPs (every GEMM, conv and
+    banded-attention product it issues, mio_hip_codec_last_flops) over its event-timed time
+    against the f32 MFMA peak; with the PMC run's MFMA-busy share when profiles hold one."""
+    tfs = flops / (codec_ms * 1e-3) / 1e12
+    r = {"bound": "mfma", "flops": round(flops), "ms": round(codec_ms, 3), "achieved": round(tfs, 2),
+         "peak": F32_MFMA_PEAK_TFS, "unit": "TFLOP/s", "frac": round(tfs / F32_MFMA_PEAK_TFS, 4),
+         "codes": tokens, "mfma_busy": None}
+    f = os.path.join(REPO, "profiles", "pmc_codec_mfma.json")
+    if os.path.exists(f):
+        try:
+            r["mfma_busy"] = json.load(open(f)).get("mfma_busy_frac")
+        except Exception:
+            pass
+    return r
+
+
 def main():
     argv = sys.argv[1:]
     a = parse_args(argv)
@@ -339,6 +359,7 @@ def main():
     allow = (m.SYNTH_SPEECH0, m.SYNTH_SPEECH0 + 12800)
 
     stage = {"llm_ms": 0.0, "codec_ms": 0.0, "istft_ms": 0.0, "codec_wall_ms": 0.0}
+    codec_flops = []
 
     d_emb = dev.upload(np.ascontiguousarray(emb, np.float32))
     d_pcm = dev.empty((a.tokens * codec.samples_per_token,), np.float32)
@@ -358,6 +379,7 @@ def main():
             stage["codec_wall_ms"] += (t2 - t1) * 1e3
             stage["codec_ms"] += c_ms
             stage["istft_ms"] += i_ms
+            codec_flops.append(codec.last_flops())
         if len(toks) != a.tokens or n != a.tokens * codec.samples_per_token:
             raise RuntimeError(f"utterance produced {len(toks)} tokens / {n} samples")
         return n
@@ -445,6 +467,9 @@ def main():
         "value_pcie_inclusive": round(value_pcie, 3),
         "cpu_baseline": None,
     }
+    if codec_flops and stage["codec_ms"] > 0:
+        out["codec_roofline"] = codec_roofline(sum(codec_flops) / len(codec_flops), stage["codec_ms"] / steps_total,
+                                               a.tokens)
     if B > 1 and batch_llm_s:
         # the batched decode step against its weight stream: one weight pass per step serves
         # the B utterances (+ each one's K/V rows at the mean position)

@@ -189,6 +189,10 @@ int mio_hip_llm_trace_kernel(mio_hip_llm *m, int which, uint64_t *out);
  * prepared; 3-6 = prologue steps in -DMIO_TL_DIAG builds.
  * Advances the decode state. */
 int mio_hip_llm_timeline(mio_hip_llm *m, uint64_t *out, int max_launches, int *n_launches);
+/* Diagnostic: a graph of `nodes` empty one-workgroup launches, captured on the device's
+ * stream and replayed `replays` times; *wall_ms = host wall time of the replays (synchronized).
+ * Separates graph-replay machinery (and profilers intercepting it) from the decode kernels. */
+int mio_hip_debug_graph_replay(mio_hip_device *d, int replays, int nodes, double *wall_ms);
 /* The launches of one decode step in order, as the `which` of mio_hip_llm_time_kernel: per
  * layer 0 attn_in, 1 attention (absent when it runs inside attn_in, MIO_ATT_FUSED=1 at load),
  * 2 attn_out, or for an lfm2 short-conv layer 8 conv_in, 9 conv_out; then 3 ffn_in, 4
@@ -203,6 +207,10 @@ int mio_hip_llm_conv_ring(mio_hip_llm *m, int il, float *ring, int set);
 int mio_hip_llm_load_ms(const mio_hip_llm *m, double *ms);
 /* Prenet rows the last mio_hip_codec_decode_pcm took from the incremental cache. */
 int mio_hip_codec_last_reused(const mio_hip_codec *c, int *rows);
+/* Algorithmic FLOPs of the last mio_hip_codec_decode_pcm (2 per multiply-add of every GEMM,
+ * conv and banded-attention dot product it issued; iSTFT excluded): the numerator of the
+ * codec's compute roofline against the 157.3 TF f32 MFMA peak. */
+int mio_hip_codec_last_flops(const mio_hip_codec *c, double *flops);
 /* Stage times (ms, HIP events) of the last mio_hip_codec_decode_pcm: [0] codec, [1] iSTFT. */
 int mio_hip_codec_last_timings(const mio_hip_codec *c, float *ms2);
 

@@ -43,6 +43,9 @@ public:
         int decode_calls = 0;
         size_t decoded_codes = 0;
         size_t emitted_samples = 0;
+        // (extension) codes whose prenet rows a re-decode took from the previous decode
+        // (MIO_CODEC_INCREMENTAL) instead of recomputing them
+        size_t prenet_rows_reused = 0;
     };
 
     struct Config {

@@ -377,6 +377,12 @@ __device__ inline void load_x(const float *x, const float *w, int K, XRegs<XV> &
     }
 }
 
+// ggml: mean = sum / ne00 in double; a power-of-two K divides exactly by a multiply
+__device__ __forceinline__ float rms_scale(double tot, int K, float eps) {
+    const float mean = (float)((K & (K - 1)) == 0 ? tot * (1.0 / K) : tot / K);
+    return 1.0f / sqrtf(mean + eps);
+}
+
 // ggml_rms_norm + mul(weight): xs = (x * 1/sqrtf(mean(x^2) + eps)) * w, then quantize.
 template <int XV>
 __device__ void rmsnorm_quant(const XRegs<XV> &xr, int K, float eps, bool kquant, const Smem &s,
@@ -413,9 +419,7 @@ __device__ void rmsnorm_quant(const XRegs<XV> &xr, int K, float eps, bool kquant
 #endif
     const double tot = block_sum(acc, s.red);
     MIO_DIAG_STAMP(diag, 4, tot);  // reduced over the workgroup
-    // ggml: mean = sum / ne00 in double; a power-of-two K divides exactly by a multiply
-    const float mean = (float)((K & (K - 1)) == 0 ? tot * (1.0 / K) : tot / K);
-    const float scale = 1.0f / sqrtf(mean + eps);
+    const float scale = rms_scale(tot, K, eps);
 #pragma unroll
     for (int i = 0; i < XV; ++i) {
         const int e = (MIO_TIDX + i * MT) * 4;

@@ -108,6 +108,9 @@ struct LlmBuffers {
 // test-to-speech.cpp:132-148); K/V rows are written, no logits are produced. 128 holds the
 // chat-template prompts of the benchmarks (≈70 tokens) in one chunk: a 64-token chunk left
 // their last few tokens to a second, dot4 weight pass (+1.5 ms per 68-token prompt).
+// Memory: the chunk's attention partials (PrefillBuffers.part) are kPrefillB x n_head x
+// ceil(n_ctx / kAttChunk) x (hd + 4) floats: 17 MB for the 1.7B model at n_ctx 2048, 277 MB at
+// the 32768 maximum (of 288 GB).
 constexpr int kPrefillB = 128;
 // The same multi-token layers run the batched decode step of up to kBatchMax utterances.
 constexpr int kBatchMax = 16;

@@ -423,6 +423,16 @@ void launch_embed_token(const LlmDims &d, const QMat &tok_embd, const LlmBuffers
 }
 
 inline size_t mv_lds(int K) { return smem_bytes(K); }
+// lm_head dynamic LDS, optionally padded (MIO_LM_LDS_KB, A/B knob) so that no more than
+// 160 KB / size of its workgroups fit on one CU: the dispatcher then has to spread them
+size_t lm_lds(int K) {
+    static const size_t kb = [] {
+        const char *e = getenv("MIO_LM_LDS_KB");
+        return e ? (size_t)atoi(e) : (size_t)0;
+    }();
+    const size_t b = smem_bytes(K);
+    return kb * 1024 > b ? std::min(kb * 1024, (size_t)64 * 1024) : b;
+}
 
 // Units (row passes) of the busiest wave of a matvec over `rows` rows on `grid` workgroups
 // (wave_range), and the single-group size that covers them (0 = streaming groups).
@@ -522,7 +532,7 @@ void launch_step_kernel(int which, const LlmDims &d, const LayerW *layers, int i
         case 6: {
             const LlmDims dl = lm_dims(d);
             dispatch_nt(d.n_embd, lm.type, [&]<int NP, int T>() {
-                hipLaunchKernelGGL((k_lm_head<NP, T, DG>), dim3(lm_head_blocks(d)), dim3(MT), mv_lds(d.n_embd), s, dl,
+                hipLaunchKernelGGL((k_lm_head<NP, T, DG>), dim3(lm_head_blocks(d)), dim3(MT), lm_lds(d.n_embd), s, dl,
                                    out_norm, lm, b);
             });
             break;

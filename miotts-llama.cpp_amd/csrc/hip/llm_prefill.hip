@@ -186,6 +186,88 @@ __device__ void prologue_copy(const char *act, int K, char *smem, int nt) {
     lds_barrier();
 }
 
+// The same records produced inside a matvec launch, ONE WAVE PER TOKEN (batched decode and
+// short prefill chunks: no k_bt_quant launch, no boundary before the matvec): wave w quantizes
+// tokens w, w + 8, ... of src (RMSNorm * norm_w first when norm_w is set) straight into the
+// token's LDS record while the workgroup's first weight rows are in flight. The arithmetic is
+// the workgroup prologue's (rmsnorm_quant / plain_quant), replayed by one wave: the sum of
+// squares accumulates per virtual thread tid = 64 vw + lane over its elements (tid + i MT) * 4
+// in order, each virtual wave reduces by the same DPP tree (wave_sum_d) and the 8 partial sums
+// add in wave order as block_sum does; each superblock / block is quantized by q8k_store /
+// q80_store as any wave of the workgroup would. Records equal k_bt_quant's bit for bit.
+// elements e..e+3 of the quantizer input: (x * scale) * w, or x
+__device__ __forceinline__ void wq_val4(const float *x, const float *norm_w, float scale, int e, float (&v)[4]) {
+    const float4 xv = ld4(x + e);
+    if (norm_w) {
+        const float4 w = ld4(norm_w + e);
+        float t;
+        t = xv.x * scale, v[0] = t * w.x;
+        t = xv.y * scale, v[1] = t * w.y;
+        t = xv.z * scale, v[2] = t * w.z;
+        t = xv.w * scale, v[3] = t * w.w;
+    } else {
+        v[0] = xv.x, v[1] = xv.y, v[2] = xv.z, v[3] = xv.w;
+    }
+}
+
+template <int XV>
+__device__ void wave_quant(const float *x, const float *norm_w, int K, float eps, bool kq, const ActL &a) {
+    const int lane = threadIdx.x & 63;
+    float scale = 1.0f;
+    if (norm_w) {
+        // branch-free loads (clamped address, zeroed past K) so all 8 x XV sit in one block
+        double tot = 0.0;
+#pragma unroll
+        for (int vw = 0; vw < MW; ++vw) {
+            double acc = 0.0;
+#pragma unroll
+            for (int i = 0; i < XV; ++i) {
+                const int e = (vw * 64 + lane + i * MT) * 4;
+                const float4 l = ld4(x + min(e, K - 4));
+                const float4 v = e < K ? l : make_float4(0.f, 0.f, 0.f, 0.f);
+                if (e < K) {
+                    acc += (double)(v.x * v.x);
+                    acc += (double)(v.y * v.y);
+                    acc += (double)(v.z * v.z);
+                    acc += (double)(v.w * v.w);
+                }
+            }
+            tot += wave_sum_d(acc);
+        }
+        scale = rms_scale(tot, K, eps);
+    }
+    if (kq) {
+        for (int b = 0; b < K / 256; ++b) {
+            float v[4];
+            wq_val4(x, norm_w, scale, b * 256 + 4 * lane, v);
+            q8k_store(v, abs_max4(v), b, a);
+        }
+    } else {
+        const int nb = K / 32;
+        for (int b0 = 0; b0 < nb; b0 += 8) {
+            const int b = b0 + (lane >> 3);
+            const bool ok = b < nb;
+            float v[4];
+            wq_val4(x, norm_w, scale, min(b, nb - 1) * 32 + 4 * (lane & 7), v);
+            q80_store(v, b, ok, a);
+        }
+    }
+}
+
+// The prologue of a matvec launch over nt tokens: quantize in-launch (fq, wave_quant) or copy
+// the records k_bt_quant wrote.
+template <int XV>
+__device__ void prologue_act(int fq, const float *src, const float *norm_w, int K, float eps, bool kq,
+                             const char *act, char *smem, int nt) {
+    if (!fq) {
+        prologue_copy(act, K, smem, nt);
+        return;
+    }
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    for (int t = w; t < nt; t += MW) wave_quant<XV>(src + (size_t)t * K, norm_w, K, eps, kq, carve_t(smem, K, t).a);
+    lds_barrier();
+}
+
 // One workgroup per token t: MODE 0 RMSNorm(src[t]) * norm_w, 1 src[t] as is, 2 the
 // attention chunk merge of token t; quantized (Q8_K / Q8_0) into the token's act record.
 template <int NP, int MODE>
@@ -283,7 +365,7 @@ __device__ inline void store_resid_b(const Resid &r, float *lds, int nt, int rpw
 // ------------------------------------------------------------------ kernels
 template <int NP, int TQ, int TV>
 __global__ __launch_bounds__(MT) void k_pf_attn_in(LlmDims d, const float *norm_w, QMat wq, QMat wk, QMat wv,
-                                                   int g_qk, PrefillBuffers pb, int nt) {
+                                                   int g_qk, PrefillBuffers pb, int nt, int fq) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int K = d.n_embd, QD = (d.n_head + 2 * d.n_kv) * d.hd;
     const int lane = threadIdx.x & 63;
@@ -293,14 +375,14 @@ __global__ __launch_bounds__(MT) void k_pf_attn_in(LlmDims d, const float *norm_
     if ((int)blockIdx.x < g_qk) {
         wave_range(o2, lo, hi, blockIdx.x, g_qk);
         load_first_b<TQ, NP, 1>(wq, wk, lo, hi, ga, gb, o1);
-        prologue_copy(pb.act, K, smem, nt);
+        prologue_act<NP>(fq, pb.x, norm_w, K, d.eps, TQ != 8, pb.act, smem, nt);
         stream_rows_b<TQ, NP, 1>(wq, wk, lo, hi, ga, gb, smem, nt, [&](int row, int t, float v, float) {
             if (lane == 0) pb.qkv[(size_t)t * QD + row] = v;
         }, o1);
     } else {
         wave_range(wv.rows, lo, hi, blockIdx.x - g_qk, gridDim.x - g_qk);
         load_first_b<TV, NP, 1>(wv, wv, lo, hi, ga, gb);
-        prologue_copy(pb.act, K, smem, nt);
+        prologue_act<NP>(fq, pb.x, norm_w, K, d.eps, TQ != 8, pb.act, smem, nt);
         stream_rows_b<TV, NP, 1>(wv, wv, lo, hi, ga, gb, smem, nt, [&](int row, int t, float v, float) {
             if (lane == 0) pb.qkv[(size_t)t * QD + o2 + row] = v;
         });
@@ -376,6 +458,75 @@ __global__ __launch_bounds__(ATT_NT) void k_pf_attention(LlmDims d, const _Float
                         (size_t)d.max_splits * C::REC);
 }
 
+// Batched decode attention (one token per sequence, so no token of the launch reads a row
+// another one writes): per (kv head, token, chunk) the decode step's k_attention — the
+// token's q heads (and, in the chunk owning its position, its k / v row) get q/k RMSNorm +
+// bias + RoPE + f16 rounding in LDS, the owner appends the row to the sequence's cache and
+// takes it from LDS, then the chunk's softmax partials. Replaces k_pf_rope + k_pf_attention
+// (one launch less per layer; the same prep_head / attend_chunk arithmetic, so the partial
+// records equal theirs bit for bit).
+template <int HD, int G>
+__global__ __launch_bounds__(ATT_NT) void k_bt_attention(LlmDims d, const float *q_norm, const float *k_norm,
+                                                         const float *bqkv, _Float16 *kcache, _Float16 *vcache,
+                                                         PrefillBuffers pb) {
+    using C = AttCfg<HD>;
+    constexpr int PER = HD / 64;
+    __shared__ float qs[G][HD];
+    __shared__ float knew[HD], vnew[HD];
+    __shared__ float wres[ATT_NW][G][HD + 2];
+    const int kvh = blockIdx.x % d.n_kv, t = blockIdx.x / d.n_kv, ch = blockIdx.y;
+    const int pos = pb.pos[t * pb.pos_stride];
+    const int t0 = ch * ATT_CHUNK;
+    if (t0 > pos) return;
+    const size_t kvo = (size_t)pb.seq[t * pb.seq_stride] * pb.seq_kv + (size_t)kvh * d.n_ctx * HD;
+    _Float16 *kc = kcache + kvo, *vc = vcache + kvo;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const float2 *rope = pb.rope + (size_t)pos * (HD / 2);
+    h8 kr[C::IT], vr[C::IT];
+    load_kv_rows<HD>(kc, vc, t0, pos, kr, vr);  // row pos comes from LDS below
+    const float *qkv = pb.qkv + (size_t)t * (d.n_head + 2 * d.n_kv) * HD;
+    const bool owner = pos < t0 + ATT_CHUNK;
+    for (int hh = wave; hh < G + (owner ? 1 : 0); hh += ATT_NW) {
+        const bool isk = hh == G;
+        float vv[PER];
+        if (isk) {
+            const size_t vo = (size_t)(d.n_head + d.n_kv + kvh) * HD;
+#pragma unroll
+            for (int i = 0; i < PER; ++i) {
+                vv[i] = qkv[vo + lane + 64 * i];
+                if (bqkv) vv[i] = vv[i] + bqkv[vo + lane + 64 * i];
+            }
+        }
+        const size_t so = isk ? (size_t)(d.n_head + kvh) * HD : (size_t)(kvh * G + hh) * HD;
+        prep_head<HD>(qkv + so, bqkv ? bqkv + so : nullptr, isk ? k_norm : q_norm, rope, d, isk ? knew : qs[hh]);
+        if (isk) {
+#pragma unroll
+            for (int i = 0; i < PER; ++i) {
+                const int p = lane + 64 * i;
+                const float vr16 = f16r(vv[i]);
+                vnew[p] = vr16;
+                kc[(size_t)pos * HD + p] = (_Float16)knew[p];
+                vc[(size_t)pos * HD + p] = (_Float16)vr16;
+            }
+        }
+    }
+    lds_barrier();
+    if (owner) {
+        const int sl = threadIdx.x / C::LP, lp = lane % C::LP, r = pos - t0;
+        if (sl == r % C::NS) {
+            h8 kn, vn;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) kn[i] = (_Float16)knew[lp * 8 + i], vn[i] = (_Float16)vnew[lp * 8 + i];
+#pragma unroll
+            for (int it = 0; it < C::IT; ++it)
+                if (it == r / C::NS) kr[it] = kn, vr[it] = vn;
+        }
+    }
+    attend_chunk<HD, G>(qs, kr, vr, t0, pos, d.scale, wres,
+                        pb.part + (((size_t)t * d.n_head + kvh * G) * d.max_splits + ch) * C::REC,
+                        (size_t)d.max_splits * C::REC);
+}
+
 template <int NP, int T>
 __global__ __launch_bounds__(MT) void k_pf_attn_out(LlmDims d, QMat wo, PrefillBuffers pb, int nt, int rpw) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -396,21 +547,22 @@ __global__ __launch_bounds__(MT) void k_pf_attn_out(LlmDims d, QMat wo, PrefillB
 
 template <int NP, int T>
 __global__ __launch_bounds__(MT) void k_pf_ffn_in(LlmDims d, const float *norm_w, QMat gate, QMat up,
-                                                  PrefillBuffers pb, int nt) {
+                                                  PrefillBuffers pb, int nt, int fq) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int K = d.n_embd;
     int lo, hi;
     wave_range(d, gate.rows, lo, hi);
     Frag ga[CfgB<NP, 2>::U], gb[CfgB<NP, 2>::U];
     load_first_b<T, NP, 2>(gate, up, lo, hi, ga, gb);
-    prologue_copy(pb.act, K, smem, nt);
+    prologue_act<NP>(fq, pb.x, norm_w, K, d.eps, T != 8, pb.act, smem, nt);
     stream_rows_b<T, NP, 2>(gate, up, lo, hi, ga, gb, smem, nt, [&](int row, int t, float g, float u) {
         if ((threadIdx.x & 63) == 0) pb.h[(size_t)t * d.n_ff + row] = silu_f(g) * u;
     });
 }
 
 template <int NP, int T>
-__global__ __launch_bounds__(MT) void k_pf_ffn_down(LlmDims d, QMat down, PrefillBuffers pb, int nt, int rpw) {
+__global__ __launch_bounds__(MT) void k_pf_ffn_down(LlmDims d, QMat down, PrefillBuffers pb, int nt, int rpw,
+                                                    int fq) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int K = down.k, E = d.n_embd;
     int lo, hi;
@@ -420,7 +572,7 @@ __global__ __launch_bounds__(MT) void k_pf_ffn_down(LlmDims d, QMat down, Prefil
     load_first_b<T, NP, 1>(down, down, lo, hi, ga, gb);
     float *res = resid_lds(smem, K, nt, rpw);
     store_resid_b(rr, res, nt, rpw);
-    prologue_copy(pb.act, K, smem, nt);
+    prologue_act<NP>(fq, pb.h, nullptr, K, d.eps, T != 8, pb.act, smem, nt);
     stream_rows_b<T, NP, 1>(down, down, lo, hi, ga, gb, smem, nt, [&](int row, int t, float v, float) {
         const float r = res[t * rpw + row - lo];
         if ((threadIdx.x & 63) == 0) pb.x[(size_t)t * E + row] = v + r;
@@ -550,6 +702,20 @@ __global__ __launch_bounds__(ST) void k_bt_embed(LlmDims d, QMat emb, PrefillBuf
 }
 
 template <int HD>
+void launch_bt_attention(int G, dim3 grid, hipStream_t s, const LlmDims &d, const LayerW &L, _Float16 *kc,
+                         _Float16 *vc, const PrefillBuffers &pb) {
+    const float *qn = L.q_norm, *kn = L.k_norm, *bi = L.bqkv;
+    switch (G) {
+        case 1: hipLaunchKernelGGL((k_bt_attention<HD, 1>), grid, dim3(ATT_NT), 0, s, d, qn, kn, bi, kc, vc, pb); break;
+        case 2: hipLaunchKernelGGL((k_bt_attention<HD, 2>), grid, dim3(ATT_NT), 0, s, d, qn, kn, bi, kc, vc, pb); break;
+        case 3: hipLaunchKernelGGL((k_bt_attention<HD, 3>), grid, dim3(ATT_NT), 0, s, d, qn, kn, bi, kc, vc, pb); break;
+        case 4: hipLaunchKernelGGL((k_bt_attention<HD, 4>), grid, dim3(ATT_NT), 0, s, d, qn, kn, bi, kc, vc, pb); break;
+        case 8: hipLaunchKernelGGL((k_bt_attention<HD, 8>), grid, dim3(ATT_NT), 0, s, d, qn, kn, bi, kc, vc, pb); break;
+        default: break;
+    }
+}
+
+template <int HD>
 void launch_pf_attention(int G, dim3 grid, hipStream_t s, const LlmDims &d, const _Float16 *kc, const _Float16 *vc,
                          const PrefillBuffers &pb) {
     switch (G) {
@@ -630,8 +796,10 @@ void launch_quant(const LlmDims &d, int mode, const float *src, int K, const flo
 // Every layer for nt tokens of pb (residual streams pb.x in, out): one weight pass per
 // matvec launch (sub-launches only where a token range does not fit LDS), each preceded by
 // the launch that quantizes its activations once (k_bt_quant).
+// decode: every token is its own sequence (the batched decode step): attention per token
+// with the RoPE / KV append inside (k_bt_attention).
 void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16 *kcache, _Float16 *vcache,
-                   const PrefillBuffers &pb, int nt, int n_chunks, hipStream_t s) {
+                   const PrefillBuffers &pb, int nt, int n_chunks, bool decode, hipStream_t s) {
     const size_t layer_kv = (size_t)d.n_kv * d.n_ctx * d.hd;
     const int G = d.n_head / d.n_kv;
     // sub-launches over token ranges that fit LDS: f(t_off, n, shifted buffers)
@@ -646,6 +814,10 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
     // MIO_MMQ=0 / 1 forces one engine.
     static const int mmq_env = getenv("MIO_MMQ") ? atoi(getenv("MIO_MMQ")) : -1;
     const bool mmq = mmq_env >= 0 ? mmq_env != 0 : nt > 8;
+    // dot4 launches of <= 16 tokens quantize their RMSNorm / plain inputs themselves (one wave
+    // per token, wave_quant) instead of behind a k_bt_quant launch; MIO_FUSED_QUANT=0: off
+    static const bool fq_env = !(getenv("MIO_FUSED_QUANT") && getenv("MIO_FUSED_QUANT")[0] == '0');
+    const int fq = (!mmq && fq_env && nt <= 16) ? 1 : 0;
     const int QD = (d.n_head + 2 * d.n_kv) * d.hd;
     for (int il = 0; il < n_layer; ++il) {
         const LayerW &L = layers[il];
@@ -671,7 +843,7 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
             launch_mmq(&so, &L.out_proj.type, 1, MMQ_RESID, MmqArgs{pb.act, act_bytes(n), n, nt, pb.x, n, {}}, s);
         } else {
             _Float16 *kc = kcache + il * layer_kv, *vc = vcache + il * layer_kv;
-            launch_quant(d, 0, pb.x, d.n_embd, L.attn_norm, L.wq.type != 8, pb, nt, s);
+            if (!fq) launch_quant(d, 0, pb.x, d.n_embd, L.attn_norm, L.wq.type != 8, pb, nt, s);
             if (mmq) {
                 const MmqSeg sg[3] = {{L.wq, mmq_tiles(L.wq.rows), 0}, {L.wk, mmq_tiles(L.wk.rows), L.wq.rows},
                                       {L.wv, mmq_tiles(L.wv.rows), L.wq.rows + L.wk.rows}};
@@ -686,7 +858,7 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
                         auto go = [&]<int TV>() {
                             allow_lds(k_pf_attn_in<NP, TQ, TV>);
                             hipLaunchKernelGGL((k_pf_attn_in<NP, TQ, TV>), dim3(GW), dim3(MT), lds, s, d, L.attn_norm,
-                                               L.wq, L.wk, L.wv, g_qk, q, n);
+                                               L.wq, L.wk, L.wv, g_qk, q, n, fq);
                         };
                         if constexpr (TQ == 8) {
                             go.template operator()<8>();
@@ -699,14 +871,22 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
                     });
                 });
             }
-            {
-                const dim3 grid(d.n_head + d.n_kv, nt);
+            if (decode) {
+                const dim3 grid(d.n_kv * nt, n_chunks);
                 if (d.hd == 128)
-                    hipLaunchKernelGGL((k_pf_rope<128>), grid, dim3(64), 0, s, d, L.q_norm, L.k_norm, L.bqkv, kc, vc, pb);
+                    launch_bt_attention<128>(G, grid, s, d, L, kc, vc, pb);
                 else
-                    hipLaunchKernelGGL((k_pf_rope<64>), grid, dim3(64), 0, s, d, L.q_norm, L.k_norm, L.bqkv, kc, vc, pb);
-            }
-            {
+                    launch_bt_attention<64>(G, grid, s, d, L, kc, vc, pb);
+            } else {
+                {
+                    const dim3 grid(d.n_head + d.n_kv, nt);
+                    if (d.hd == 128)
+                        hipLaunchKernelGGL((k_pf_rope<128>), grid, dim3(64), 0, s, d, L.q_norm, L.k_norm, L.bqkv, kc,
+                                           vc, pb);
+                    else
+                        hipLaunchKernelGGL((k_pf_rope<64>), grid, dim3(64), 0, s, d, L.q_norm, L.k_norm, L.bqkv, kc,
+                                           vc, pb);
+                }
                 const dim3 grid(d.n_kv * nt, n_chunks);
                 if (d.hd == 128)
                     launch_pf_attention<128>(G, grid, s, d, kc, vc, pb);
@@ -729,7 +909,7 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
                 });
             }
         }
-        launch_quant(d, 0, pb.x, d.n_embd, L.ffn_norm, L.gate.type != 8, pb, nt, s);
+        if (!fq) launch_quant(d, 0, pb.x, d.n_embd, L.ffn_norm, L.gate.type != 8, pb, nt, s);
         if (mmq) {
             const MmqSeg sg{L.gate, mmq_tiles(L.gate.rows), 0};
             launch_mmq(&sg, &L.gate.type, 1, MMQ_SWIGLU,
@@ -740,11 +920,11 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
                 dispatch_nt(d.n_embd, L.gate.type, [&]<int NP, int T>() {
                     allow_lds(k_pf_ffn_in<NP, T>);
                     hipLaunchKernelGGL((k_pf_ffn_in<NP, T>), dim3(grid), dim3(MT), pf_lds_bytes(d.n_embd, n, 0), s, d,
-                                       L.ffn_norm, L.gate, L.up, q, n);
+                                       L.ffn_norm, L.gate, L.up, q, n, fq);
                 });
             });
         }
-        launch_quant(d, 1, pb.h, L.down.k, nullptr, L.down.type != 8, pb, nt, s);
+        if (!fq) launch_quant(d, 1, pb.h, L.down.k, nullptr, L.down.type != 8, pb, nt, s);
         if (mmq) {
             const MmqSeg sg{L.down, mmq_tiles(L.down.rows), 0};
             launch_mmq(&sg, &L.down.type, 1, MMQ_RESID,
@@ -755,7 +935,7 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
                 dispatch_nt(L.down.k, L.down.type, [&]<int NP, int T>() {
                     allow_lds(k_pf_ffn_down<NP, T>);
                     hipLaunchKernelGGL((k_pf_ffn_down<NP, T>), dim3(grid), dim3(MT), pf_lds_bytes(L.down.k, n, rpw),
-                                       s, d, L.down, q, n, rpw);
+                                       s, d, L.down, q, n, rpw, fq);
                 });
             });
         }
@@ -769,7 +949,7 @@ void launch_prefill_chunk(const LlmDims &d, const LayerW *layers, int n_layer, _
                           int n_chunks, hipStream_t s) {
     if (nt <= 0) return;
     hipLaunchKernelGGL(k_pf_embed, dim3(nt), dim3(ST), 0, s, d, tok_embd, pb, p0);
-    launch_layers(d, layers, n_layer, kcache, vcache, pb, nt, n_chunks, s);
+    launch_layers(d, layers, n_layer, kcache, vcache, pb, nt, n_chunks, false, s);
 }
 
 size_t prefill_act_bytes(int k_max) { return act_bytes(k_max) * kPrefillB; }
@@ -796,7 +976,7 @@ bool batch_supported(const LlmDims &d, int B) {
 void launch_batch_step(const LlmDims &d, const LayerW *layers, int n_layer, _Float16 *kcache, _Float16 *vcache,
                        const float *out_norm, const QMat &lm, const QMat &tok_embd, const PrefillBuffers &pb,
                        const BatchBuffers &bb, int B, hipStream_t s) {
-    launch_layers(d, layers, n_layer, kcache, vcache, pb, B, d.max_splits, s);
+    launch_layers(d, layers, n_layer, kcache, vcache, pb, B, d.max_splits, true, s);
     launch_quant(d, 0, pb.x, d.n_embd, out_norm, lm.type != 8, pb, B, s);
     const int nblk = matvec_grid(d, d.n_vocab);  // the batched lm_head keeps one workgroup per CU
     dispatch_nt(d.n_embd, lm.type, [&]<int NP, int T>() {

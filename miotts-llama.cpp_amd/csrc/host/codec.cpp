@@ -90,6 +90,7 @@ struct mio_hip_codec {
     int pc_cap = 0, pc_exact = 0;
     std::vector<int32_t> pc_codes;
     int pc_last_reused = 0;  // rows the last decode took from the cache (diagnostic)
+    double last_flops = 0.0;  // algorithmic FLOPs of the last decode_pcm (codec_roofline)
 
     ~mio_hip_codec() {
         if (d) hipSetDevice(d->dev);
@@ -104,6 +105,30 @@ struct mio_hip_codec {
 };
 
 namespace {
+
+// Algorithmic FLOPs of the decode being issued (2 per multiply-add of every GEMM, conv and
+// banded-attention dot product), read back by mio_hip_codec_last_flops for bench.py's
+// codec_roofline. Counted at issue, so an incremental re-decode counts only what it runs.
+thread_local double t_flops = 0.0;
+void gemm_launch(const mio::GemmArgs &a, int epi, hipStream_t s) {
+    t_flops += 2.0 * a.M * a.N * a.K;
+    mio::launch_gemm_f32(a, epi, s);
+}
+void conv_launch(const mio::ConvArgs &a, hipStream_t s) {
+    t_flops += 2.0 * a.L * a.Cout * a.taps * a.Cin;
+    mio::launch_conv_f16(a, s);
+}
+void band_launch(const float *qkv, float *out, int S, int H, int win, const float2 *rope, hipStream_t s) {
+    const int h = win / 2;
+    double pairs = 0;
+    for (int i = 0; i < S; ++i) pairs += std::min(S - 1, i + h) - std::max(0, i - h) + 1;
+    t_flops += 4.0 * pairs * H * 64;  // q.k and p.v over the band, head dim 64
+    mio::launch_band_attention(qkv, out, S, H, win, rope, s);
+}
+void cond_launch(const float *W, const float *b, const float *e, int R, int A, float *y, int e_f16, hipStream_t s) {
+    t_flops += 2.0 * R * A;
+    mio::launch_cond_gemv(W, b, e, R, A, y, e_f16, s);
+}
 
 struct Loader {
     mio_hip_codec *c;
@@ -362,11 +387,11 @@ void resnet(mio_hip_codec *c, const ResW &r, float *x, float *t, int L, int C, c
     // t = conv1(silu(GN1(x))) + b1
     mio::launch_groupnorm_apply(x, L, C, c->groups, c->gn_eps, r.gn1_w, r.gn1_b, w.gns, w.xa, s);
     a.B = r.w1, a.bias = r.b1, a.Y = t, a.resid = nullptr;
-    mio::launch_conv_f16(a, s);
+    conv_launch(a, s);
     // x = conv2(silu(GN2(t))) + b2 + x
     mio::launch_groupnorm_apply(t, L, C, c->groups, c->gn_eps, r.gn2_w, r.gn2_b, w.gns, w.xa, s);
     a.B = r.w2, a.bias = r.b2, a.Y = x, a.resid = x;
-    mio::launch_conv_f16(a, s);
+    conv_launch(a, s);
 }
 
 // Prenet receptive field in codes: each layer's banded attention reaches pre_win/2 each way.
@@ -397,18 +422,18 @@ int run_decode(mio_hip_codec *c, Ws &w, hipStream_t s, int stop_stage, const flo
     for (int i = 0; i < c->pre_layers; ++i) {
         const PreW &p = c->pre[i];
         mio::launch_rownorm(w.xT, w.hT, Tw, Dp, c->eps, 1, p.ln1_w, p.ln1_b, s);
-        mio::launch_gemm_f32(gemm(w.hT, Dp, Tw, p.qkv, 3 * Dp, w.qkvT, 3 * Dp, p.h16_qkv), mio::EPI_STORE, s);
-        mio::launch_band_attention(w.qkvT, w.aT, Tw, c->pre_heads, c->pre_win, rope_w, s);
-        mio::launch_gemm_f32(gemm(w.aT, Dp, Tw, p.wo, Dp, w.xT, Dp, p.h16_wo), mio::EPI_RESID, s);
+        gemm_launch(gemm(w.hT, Dp, Tw, p.qkv, 3 * Dp, w.qkvT, 3 * Dp, p.h16_qkv), mio::EPI_STORE, s);
+        band_launch(w.qkvT, w.aT, Tw, c->pre_heads, c->pre_win, rope_w, s);
+        gemm_launch(gemm(w.aT, Dp, Tw, p.wo, Dp, w.xT, Dp, p.h16_wo), mio::EPI_RESID, s);
         mio::launch_rownorm(w.xT, w.hT, Tw, Dp, c->eps, 1, p.ln2_w, p.ln2_b, s);
-        mio::launch_gemm_f32(gemm(w.hT, Dp, Tw, p.gu, 2 * c->pre_ff, w.fT, c->pre_ff, p.h16_gu), mio::EPI_SWIGLU, s);
-        mio::launch_gemm_f32(gemm(w.fT, c->pre_ff, Tw, p.wd, Dp, w.xT, Dp, p.h16_wd), mio::EPI_RESID, s);
+        gemm_launch(gemm(w.hT, Dp, Tw, p.gu, 2 * c->pre_ff, w.fT, c->pre_ff, p.h16_gu), mio::EPI_SWIGLU, s);
+        gemm_launch(gemm(w.fT, c->pre_ff, Tw, p.wd, Dp, w.xT, Dp, p.h16_wd), mio::EPI_RESID, s);
     }
     mio::launch_rownorm(w.xT, w.hT, Tw, Dp, c->eps, 1, c->pre_norm_w, c->pre_norm_b, s);
     {
         mio::GemmArgs g = gemm(w.hT, Dp, Tw, c->pre_out_w, Dd, w.yT + (size_t)s0 * Dd, Dd, c->h16_pre_out);
         g.bias = c->pre_out_b;
-        mio::launch_gemm_f32(g, mio::EPI_STORE, s);
+        gemm_launch(g, mio::EPI_STORE, s);
     }
     // the cached rows replace the window's left edge (whose context was cut)
     if (cached > 0)
@@ -418,31 +443,31 @@ int run_decode(mio_hip_codec *c, Ws &w, hipStream_t s, int stop_stage, const flo
     {
         mio::GemmArgs g = gemm(w.yT, Dd, T, c->ups_w, 2 * Dd, w.xS, Dd, c->h16_ups);
         g.bias = c->ups_b, g.f = 2, g.trim = 0, g.cout = Dd, g.rows_out = S;
-        mio::launch_gemm_f32(g, mio::EPI_CONVT, s);
+        gemm_launch(g, mio::EPI_CONVT, s);
     }
     if (done(w.xS, S, Dd)) return MIO_OK;
     // 4. wave_prior (:629-637)
     for (auto &r : c->prior) resnet(c, r, w.xS, w.hS, S, Dd, w, s);
     if (done(w.xS, S, Dd)) return MIO_OK;
     // 5. AdaLN-Zero decoder (:640-660); all conditioning vectors in one GEMV
-    mio::launch_cond_gemv(c->cond_w, c->cond_b, w.emb, c->cond_rows, c->adaln, w.cond, c->h16_cond, s);
+    cond_launch(c->cond_w, c->cond_b, w.emb, c->cond_rows, c->adaln, w.cond, c->h16_cond, s);
     for (int i = 0; i < c->dec_layers; ++i) {
         const DecW &p = c->dec[i];
         const float *ca = w.cond + (size_t)i * 6 * Dd, *cf = ca + 3 * Dd;
         mio::launch_rownorm(w.xS, w.hS, S, Dd, c->eps, 2, ca, ca + Dd, s);
-        mio::launch_gemm_f32(gemm(w.hS, Dd, S, p.qkv, 3 * Dd, w.qkvS, 3 * Dd, p.h16_qkv), mio::EPI_STORE, s);
-        mio::launch_band_attention(w.qkvS, w.aS, S, c->dec_heads, c->dec_win, c->rope, s);
+        gemm_launch(gemm(w.hS, Dd, S, p.qkv, 3 * Dd, w.qkvS, 3 * Dd, p.h16_qkv), mio::EPI_STORE, s);
+        band_launch(w.qkvS, w.aS, S, c->dec_heads, c->dec_win, c->rope, s);
         {
             mio::GemmArgs g = gemm(w.aS, Dd, S, p.wo, Dd, w.xS, Dd, p.h16_wo);
             g.aux = ca + 2 * Dd;
-            mio::launch_gemm_f32(g, mio::EPI_GATED, s);
+            gemm_launch(g, mio::EPI_GATED, s);
         }
         mio::launch_rownorm(w.xS, w.hS, S, Dd, c->eps, 2, cf, cf + Dd, s);
-        mio::launch_gemm_f32(gemm(w.hS, Dd, S, p.gu, 2 * c->dec_ff, w.fS, c->dec_ff, p.h16_gu), mio::EPI_SWIGLU, s);
+        gemm_launch(gemm(w.hS, Dd, S, p.gu, 2 * c->dec_ff, w.fS, c->dec_ff, p.h16_gu), mio::EPI_SWIGLU, s);
         {
             mio::GemmArgs g = gemm(w.fS, c->dec_ff, S, p.wd, Dd, w.xS, Dd, p.h16_wd);
             g.aux = cf + 2 * Dd;
-            mio::launch_gemm_f32(g, mio::EPI_GATED, s);
+            gemm_launch(g, mio::EPI_GATED, s);
         }
     }
     {
@@ -465,7 +490,7 @@ int run_decode(mio_hip_codec *c, Ws &w, hipStream_t s, int stop_stage, const flo
         g.B = u.w, g.M = M, g.N = u.f * u.Cout, g.K = u.taps * u.Cin;
         g.C = w.u[st], g.ldc = u.Cout, g.bias = u.b, g.aux = u.alpha_e, g.aux2 = u.beta_e;
         g.f = u.f, g.trim = u.trim, g.cout = u.Cout, g.rows_out = Lout, g.a_f16 = u.h16;
-        mio::launch_gemm_f32(g, mio::EPI_CONVT_SNAKE, s);
+        gemm_launch(g, mio::EPI_CONVT_SNAKE, s);
         resnet(c, u.res, w.u[st], w.t[st], Lout, u.Cout, w, s);
         src = w.u[st];
         Lin = Lout;
@@ -476,14 +501,14 @@ int run_decode(mio_hip_codec *c, Ws &w, hipStream_t s, int stop_stage, const flo
     {
         mio::GemmArgs g = gemm(src, c->c_last, L, c->op_w, Dd, w.op, Dd, c->h16_op);
         g.bias = c->op_b, g.aux = c->op_ae, g.aux2 = c->op_be;
-        mio::launch_gemm_f32(g, mio::EPI_SNAKE, s);
+        gemm_launch(g, mio::EPI_SNAKE, s);
     }
     if (done(w.op, L, Dd)) return MIO_OK;
     // 9. iSTFT head (:728-737) written as [frame][bin][re,im] (:801-808)
     {
         mio::GemmArgs g = gemm(w.op, Dd, L, c->head_w, 2 * c->nfp, w.spec, 2 * c->n_freq, c->h16_head);
         g.bias = c->head_b, g.cout = c->n_freq;
-        mio::launch_gemm_f32(g, mio::EPI_HEAD, s);
+        gemm_launch(g, mio::EPI_HEAD, s);
     }
     if (done(w.spec, L, 2 * c->n_freq)) return MIO_OK;
     return MIO_OK;
@@ -827,7 +852,9 @@ extern "C" int mio_hip_codec_decode_pcm(mio_hip_codec *c, const int32_t *codes, 
     }
     c->pc_last_reused = cached;
     MIO_HIP_CHECK(hipEventRecord(c->ev[0], s));
+    t_flops = 0.0;
     if ((rc = run_decode(c, w, s, 1 << 20, &buf, &r, &cc, cached))) return rc;
+    c->last_flops = t_flops;
     if (incr) {  // rows whose receptive field this decode held completely become the cache
         const int exact = std::max(0, n_codes - prenet_radius(c));
         if (exact > cached)
@@ -856,6 +883,12 @@ extern "C" int mio_hip_codec_decode_pcm(mio_hip_codec *c, const int32_t *codes, 
 extern "C" int mio_hip_codec_last_reused(const mio_hip_codec *c, int *rows) {
     MIO_REQUIRE(c && rows, MIO_ERR_INVALID, "codec_last_reused: null");
     *rows = c->pc_last_reused;
+    return MIO_OK;
+}
+
+extern "C" int mio_hip_codec_last_flops(const mio_hip_codec *c, double *flops) {
+    MIO_REQUIRE(c && flops, MIO_ERR_INVALID, "codec_last_flops: null");
+    *flops = c->last_flops;
     return MIO_OK;
 }
 

@@ -211,9 +211,10 @@ bool upload_qmat(mio_hip_llm *m, const mio::GgufTensor *t, mio::QMat &q) {
     return true;
 }
 
-float *upload_f32(mio_hip_llm *m, const mio::GgufTensor *t, int64_t n) {
+float *upload_f32(mio_hip_llm *m, const mio::GgufFile &g, const std::string &name, int64_t n) {
+    const mio::GgufTensor *t = g.tensor(name);
     if (!t || t->type != mio::GGML_F32 || t->nelements() != n) {
-        mio::set_error("llm: norm tensor %s missing or not f32[%lld]", t ? t->name.c_str() : "?", (long long)n);
+        mio::set_error("llm: norm tensor %s missing or not f32[%lld]", name.c_str(), (long long)n);
         return nullptr;
     }
     const auto it = m->arena_off.find(t->name);
@@ -640,15 +641,15 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
         m->weight_bytes += embd_bytes;
     }
     // lfm2's final norm is token_embd_norm (llama.cpp model.tok_norm)
-    if (!(m->out_norm = upload_f32(m, g.tensor(lfm2 ? "token_embd_norm.weight" : "output_norm.weight"), D.n_embd)))
+    if (!(m->out_norm = upload_f32(m, g, lfm2 ? "token_embd_norm.weight" : "output_norm.weight", D.n_embd)))
         return fail(MIO_ERR_FORMAT);
     bool any_conv = false;
     auto fam = [](int t) { return t == mio::GGML_Q8_0 ? 0 : 1; };
     for (int i = 0; i < m->n_layer; ++i) {
         const std::string p = "blk." + std::to_string(i) + ".";
         mio::LayerW L{};
-        if (!(L.attn_norm = upload_f32(m, g.tensor(p + "attn_norm.weight"), D.n_embd)) ||
-            !(L.ffn_norm = upload_f32(m, g.tensor(p + "ffn_norm.weight"), D.n_embd)))
+        if (!(L.attn_norm = upload_f32(m, g, p + "attn_norm.weight", D.n_embd)) ||
+            !(L.ffn_norm = upload_f32(m, g, p + "ffn_norm.weight", D.n_embd)))
             return fail(MIO_ERR_FORMAT);
         L.conv = g.tensor(p + "shortconv.in_proj.weight") ? 1 : 0;
         if (lfm2 && (size_t)i < kv_arr.size() && (kv_arr[i] == 0) != (L.conv != 0)) {
@@ -665,7 +666,7 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
                                mio::kConvL);
                 return fail(MIO_ERR_FORMAT);
             }
-            if (!(L.conv_w = upload_f32(m, tc, (int64_t)D.n_embd * mio::kConvL)) ||
+            if (!(L.conv_w = upload_f32(m, g, p + "shortconv.conv.weight", (int64_t)D.n_embd * mio::kConvL)) ||
                 !upload_qmat(m, g.tensor(p + "shortconv.in_proj.weight"), L.in_proj) ||
                 !upload_qmat(m, g.tensor(p + "shortconv.out_proj.weight"), L.out_proj) ||
                 !upload_qmat(m, g.tensor(p + "ffn_gate.weight"), L.gate) ||
@@ -683,8 +684,8 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
             continue;
         }
         if (D.qk_norm) {
-            if (!(L.q_norm = upload_f32(m, g.tensor(p + "attn_q_norm.weight"), D.hd)) ||
-                !(L.k_norm = upload_f32(m, g.tensor(p + "attn_k_norm.weight"), D.hd)))
+            if (!(L.q_norm = upload_f32(m, g, p + "attn_q_norm.weight", D.hd)) ||
+                !(L.k_norm = upload_f32(m, g, p + "attn_k_norm.weight", D.hd)))
                 return fail(MIO_ERR_FORMAT);
         }
         if (!upload_qmat(m, g.tensor(p + "attn_q.weight"), L.wq) || !upload_qmat(m, g.tensor(p + "attn_k.weight"), L.wk) ||

@@ -567,6 +567,8 @@ bool TestToSpeech::synthesize_stream_profiled(const VoiceModel &voice, const std
             return false;
         profile.decode_calls++;
         profile.decoded_codes += codes.size();
+        if (int reused = 0; mio_hip_codec_last_reused(I.codec->codec, &reused) == MIO_OK)
+            profile.prenet_rows_reused += (size_t)reused;
         const double per_code = (double)len / (double)codes.size();
         const size_t b = (size_t)std::llround((double)committed * per_code);
         const size_t e = std::min((size_t)std::llround((double)target * per_code), (size_t)len);

@@ -85,6 +85,7 @@ int main(int argc, char **argv) {
     std::printf("stream_bench.llm_tokens=%d\n", p.llm_tokens);
     std::printf("stream_bench.decode_calls=%d\n", p.decode_calls);
     std::printf("stream_bench.decoded_codes=%zu\n", p.decoded_codes);
+    std::printf("stream_bench.prenet_rows_reused=%zu\n", p.prenet_rows_reused);
     std::printf("stream_bench.emitted_samples=%zu\n", p.emitted_samples);
     auto stage = [&](const char *k, double v) {
         std::printf("stream_bench.stage.%s=%.6f (%.2f%%)\n", k, v, 100.0 * v / total);

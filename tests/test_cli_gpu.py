@@ -133,10 +133,12 @@ def test_stream_benchmark_1p7b_700_tokens(files, synth_llm_path):
     print({k: r[k] for k in r if k.startswith("stream_bench.")})
 
 
-@pytest.mark.parametrize("n,chunk", [(100, 4096), (141, 1000)])
+@pytest.mark.parametrize("n,chunk", [(100, 4096), (141, 1000), (320, 4096)])
 def test_stream_emission_matches_restatement(files, n, chunk):
     """Everything synthesize_stream hands its callback (LLM speech-only, tiny codec) against
-    oracle/stream_ref.c over the same codes: identical chunk sizes, samples within 1e-4 RMS."""
+    oracle/stream_ref.c over the same codes: identical chunk sizes, samples within 1e-4 RMS.
+    At 320 tokens the later re-decodes take prenet rows from the previous decode
+    (MIO_CODEC_INCREMENTAL: rows whose receptive field was complete), checked to happen."""
     prefix = str(files["dir"] / f"stream_{n}_{chunk}")
     out = run(["miotts-stream-benchmark", "-m", files["llm"], "-c", files["codec_tiny"], "-v", files["voice"],
                "-p", "こんにちは、今日はいい天気ですね。", "--max-tokens", n, "--speech-only", "--ignore-eos",
@@ -154,3 +156,5 @@ def test_stream_emission_matches_restatement(files, n, chunk):
     d = got.astype(np.float64) - ref
     rms = float(np.sqrt(np.mean(d * d)))
     assert rms <= 1e-4 and float(np.abs(d).max()) <= 1e-3, (rms, float(np.abs(d).max()))
+    if n >= 300:
+        assert int(r["stream_bench.prenet_rows_reused"]) > 0, r

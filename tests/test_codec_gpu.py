@@ -37,13 +37,13 @@ def emb(files):
     return m.read_voice(files["voice"])
 
 
-def _stage_close(g, o, name):
+def _stage_close(g, o, name, rms_bound=1e-3, max_bound=5e-3):
     assert g.shape == o.shape, (name, g.shape, o.shape)
     d = g.astype(np.float64) - o.astype(np.float64)
     rms_ref = np.sqrt(np.mean(o.astype(np.float64) ** 2)) + 1e-30
     rel_rms = np.sqrt(np.mean(d * d)) / rms_ref
     rel_max = np.abs(d).max() / (np.abs(o).max() + 1e-30)
-    assert rel_rms <= 1e-3 and rel_max <= 5e-3, f"{name}: rel_rms={rel_rms:.3g} rel_max={rel_max:.3g}"
+    assert rel_rms <= rms_bound and rel_max <= max_bound, f"{name}: rel_rms={rel_rms:.3g} rel_max={rel_max:.3g}"
 
 
 def _pcm_close(g, o):
@@ -147,8 +147,11 @@ def test_codec_f16_weights(device, tmp_path, emb, preset, T):
     F16): ggml's mul_mat and conv_transpose_1d then convert the activation to the F16
     vec_dot_type (miocodec.cpp:205-209 linear, :624 / :685 ConvT), which the GPU GEMMs do in
     their operand staging (GemmArgs::a_f16) and the oracle before its dot products (whose F16
-    path tests/test_np_codec.py checks against the numpy restatement). Stages before the
-    spectrogram: the F32 codec's bounds. The spectrogram head rounds its input to f16 and then
+    path tests/test_np_codec.py checks against the numpy restatement). Every F16 linear rounds
+    its input, so last-bit differences upstream that cross an f16 rounding boundary move a
+    value by one f16 ulp (5e-4 relative) and the chained stages drift further than in the F32
+    codec (measured 1.0e-3 rms at stage 8, T=33): stages before the spectrogram within 3e-3
+    rms / 1e-2 max. The spectrogram head rounds its input to f16 and then
     exponentiates, so one-ulp input flips (last-bit differences upstream crossing an f16
     rounding boundary) grow into ~1e-3 of the output: there the GPU is checked teacher-forced
     (numpy head with f16 rounding on the GPU's own stage input: tight; without the rounding:
@@ -166,7 +169,7 @@ def test_codec_f16_weights(device, tmp_path, emb, preset, T):
     last = oc.n_stages - 1
     for st in range(last):
         _stage_close(gc.decode_stage(codes, emb, st, cap), oc.decode_stage(codes, emb, st, cap),
-                     f"f16 preset {preset} T={T} stage {st}")
+                     f"f16 preset {preset} T={T} stage {st}", 3e-3, 1e-2)
     g_in = gc.decode_stage(codes, emb, last - 1, cap).astype(np.float64)
     g_spec = gc.decode_stage(codes, emb, last, cap).astype(np.float64)
     nc = np_codec.Codec(path)
