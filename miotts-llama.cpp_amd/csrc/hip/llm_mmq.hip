@@ -214,39 +214,83 @@ __device__ v16f slot_kq(const QMat &W, int row, int k, const int8_t *aq, const f
 }
 
 // Q8_0: lane group k = slots 8k .. 8k+7 (block b = p * 64 + slot), each slot's pass sum,
-// then sum8_f's tree over the group
+// then sum8_f's tree over the group. With one pass (K <= 2048) the 8 slots' weight /
+// activation / scale loads are all issued before the first MFMA (one memory round trip, not
+// eight); longer K goes four slots at a time (register budget). Same arithmetic and order
+// either way.
 __device__ v16f slot_q80(const QMat &W, int row, int k, const int8_t *aq, const float *da_lds) {
     const int lane = threadIdx.x & 63, h = lane >> 5;
     const int nb = W.k >> 5, NP = (nb + 63) / 64;
     const int8_t *qrow = (const int8_t *)W.p0 + (size_t)row * W.k;
     const uint16_t *drow = (const uint16_t *)W.p1 + (size_t)row * nb;
     Tree<3> inner;
-    auto slot = [&]<int i>() {
-        const int lam = 8 * k + i;
-        v16f acc = {};
-        for (int p = 0; p < NP; ++p) {
-            const int b = p * 64 + lam;
-            v16f v = {};
-            if (b < nb) {
-                const v4i w = *reinterpret_cast<const v4i *>(qrow + (size_t)b * 32 + 16 * h);
-                const v4i a = act16(aq, b * 32 + 16 * h);
-                const v16i c = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, w, v16i{}, 0, 0, 0);
-                const float dw = h2f(drow[b]);
+    if (NP == 1) {
+        v4i w[8], a[8];
+        float dw[8];
 #pragma unroll
-                for (int r = 0; r < 16; ++r) v[r] = (float)c[r] * (dw * da_lds[b * TT + tok_of(lane, r)]);
-            }
-            acc = acc + v;
+        for (int i = 0; i < 8; ++i) {
+            const int b = min(8 * k + i, nb - 1);  // clamped: every load in flight at once
+            w[i] = *reinterpret_cast<const v4i *>(qrow + (size_t)b * 32 + 16 * h);
+            a[i] = act16(aq, b * 32 + 16 * h);
+            dw[i] = h2f(drow[b]);
         }
-        inner.template push<i>(acc);
+        auto slot1 = [&]<int i>() {
+            const int b = 8 * k + i;
+            v16f v = {};
+            if (b < nb) {  // wave-uniform: the MFMA runs with the full EXEC
+                const v16i c = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[i], w[i], v16i{}, 0, 0, 0);
+#pragma unroll
+                for (int r = 0; r < 16; ++r) v[r] = (float)c[r] * (dw[i] * da_lds[b * TT + tok_of(lane, r)]);
+            }
+            const v16f acc = v16f{} + v;
+            inner.template push<i>(acc);
+        };
+        slot1.template operator()<0>();
+        slot1.template operator()<1>();
+        slot1.template operator()<2>();
+        slot1.template operator()<3>();
+        slot1.template operator()<4>();
+        slot1.template operator()<5>();
+        slot1.template operator()<6>();
+        slot1.template operator()<7>();
+        return inner.result;
+    }
+    // several passes (K > 2048): four slots at a time, each pass's loads of the four issued
+    // together (two round trips per pass instead of eight); slot i still accumulates its
+    // passes in order and enters the tree in slot order
+    auto half = [&]<int H>() {
+        v16f acc[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[i] = v16f{};
+        for (int p = 0; p < NP; ++p) {
+            v4i w[4], a[4];
+            float dw[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int b = min(p * 64 + 8 * k + 4 * H + i, nb - 1);
+                w[i] = *reinterpret_cast<const v4i *>(qrow + (size_t)b * 32 + 16 * h);
+                a[i] = act16(aq, b * 32 + 16 * h);
+                dw[i] = h2f(drow[b]);
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int b = p * 64 + 8 * k + 4 * H + i;
+                v16f v = {};
+                if (b < nb) {
+                    const v16i c = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[i], w[i], v16i{}, 0, 0, 0);
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) v[r] = (float)c[r] * (dw[i] * da_lds[b * TT + tok_of(lane, r)]);
+                }
+                acc[i] = acc[i] + v;
+            }
+        }
+        inner.template push<4 * H + 0>(acc[0]);
+        inner.template push<4 * H + 1>(acc[1]);
+        inner.template push<4 * H + 2>(acc[2]);
+        inner.template push<4 * H + 3>(acc[3]);
     };
-    slot.template operator()<0>();
-    slot.template operator()<1>();
-    slot.template operator()<2>();
-    slot.template operator()<3>();
-    slot.template operator()<4>();
-    slot.template operator()<5>();
-    slot.template operator()<6>();
-    slot.template operator()<7>();
+    half.template operator()<0>();
+    half.template operator()<1>();
     return inner.result;
 }
 

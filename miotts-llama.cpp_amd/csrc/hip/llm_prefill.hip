@@ -65,9 +65,13 @@ __device__ inline float *resid_lds(char *base, int K, int nt, int rpw) {
 // A register group holds RU whole rows (all NM matrices, all NP passes): every fragment is
 // loaded once and dotted with each token's activation; row totals per token as in the
 // decode engine (acc over passes in order, then row_total).
+// MIO_BT_UNITS (compile-time, A/B builds): weight units per row group (4 default)
+#ifndef MIO_BT_UNITS
+#define MIO_BT_UNITS 4
+#endif
 template <int NP, int NM>
 struct CfgB {
-    static constexpr int RU = NP * NM >= 4 ? 1 : 4 / (NP * NM);
+    static constexpr int RU = NP * NM >= MIO_BT_UNITS ? 1 : MIO_BT_UNITS / (NP * NM);
     static constexpr int U = RU * NP * NM;
 };
 
@@ -813,11 +817,30 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
     // 16 streams 2.6B Q8_0 134 / 144; a 64-token prefill chunk 10.4 / 2.7 ms.
     // MIO_MMQ=0 / 1 forces one engine.
     static const int mmq_env = getenv("MIO_MMQ") ? atoi(getenv("MIO_MMQ")) : -1;
-    const bool mmq = mmq_env >= 0 ? mmq_env != 0 : nt > 8;
-    // dot4 launches of <= 16 tokens quantize their RMSNorm / plain inputs themselves (one wave
-    // per token, wave_quant) instead of behind a k_bt_quant launch; MIO_FUSED_QUANT=0: off
-    static const bool fq_env = !(getenv("MIO_FUSED_QUANT") && getenv("MIO_FUSED_QUANT")[0] == '0');
+    const bool mmq_all = mmq_env >= 0 ? mmq_env != 0 : nt > 8;
+    // At <= 8 tokens the engine is chosen per launch kind (bit 0 attn_in, 1 attn_out, 2 ffn_in,
+    // 3 ffn_down set = int8 MFMA): q|k|v on the matrix cores, gate|up too for the K-quants,
+    // the O and down matvecs (n_embd rows = 64 tiles of 32 rows: a quarter of the CUs) on
+    // dot4. Eager per-kernel times at 8 tokens (profiles/r03_batch8_mmq_vs_dot4.txt): 1.7B
+    // Q4_K_M gate|up 11.0 vs 25.1 us, q|k|v 6.6-11.8 vs 13.1-13.8, down (Q6_K) 32.5 vs 12.2;
+    // 8-stream steps (graph) 1.7B 1.91 ms with q|k|v + gate|up on MFMA vs 2.22 all dot4; 2.6B
+    // Q8_0 3.04 with q|k|v only, 3.22 adding gate|up, 3.10 all dot4 (profiles/r03_batch8_masks.txt).
+    // MIO_MMQ_MASK overrides the set for every type (A/B).
+    static const int mmq_mask = getenv("MIO_MMQ_MASK") ? atoi(getenv("MIO_MMQ_MASK")) : -1;
+    auto use_mmq = [&](int kind, int type) {
+        const int mask = mmq_mask >= 0 ? mmq_mask : (type == 8 ? 1 : 5);
+        return mmq_all || (nt <= 8 && mmq_env < 0 && ((mask >> kind) & 1));
+    };
+    const bool mmq = mmq_all;
+    // MIO_FUSED_QUANT=1: dot4 launches of <= 16 tokens quantize their RMSNorm / plain inputs
+    // themselves (one wave per token, wave_quant) instead of behind a k_bt_quant launch. Off:
+    // measured slower (8 streams, 1.7B: 2.47 vs 2.23 ms per step; every workgroup re-reads all
+    // tokens' inputs twice)
+    static const bool fq_env = getenv("MIO_FUSED_QUANT") && getenv("MIO_FUSED_QUANT")[0] == '1';
     const int fq = (!mmq && fq_env && nt <= 16) ? 1 : 0;
+    // MIO_BT_ATT=0: the batched decode step uses k_pf_rope + k_pf_attention (A/B)
+    static const bool bt_att = !(getenv("MIO_BT_ATT") && getenv("MIO_BT_ATT")[0] == '0');
+    decode = decode && bt_att;
     const int QD = (d.n_head + 2 * d.n_kv) * d.hd;
     for (int il = 0; il < n_layer; ++il) {
         const LayerW &L = layers[il];
@@ -843,8 +866,8 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
             launch_mmq(&so, &L.out_proj.type, 1, MMQ_RESID, MmqArgs{pb.act, act_bytes(n), n, nt, pb.x, n, {}}, s);
         } else {
             _Float16 *kc = kcache + il * layer_kv, *vc = vcache + il * layer_kv;
-            if (!fq) launch_quant(d, 0, pb.x, d.n_embd, L.attn_norm, L.wq.type != 8, pb, nt, s);
-            if (mmq) {
+            if (!fq || use_mmq(0, L.wq.type)) launch_quant(d, 0, pb.x, d.n_embd, L.attn_norm, L.wq.type != 8, pb, nt, s);
+            if (use_mmq(0, L.wq.type)) {
                 const MmqSeg sg[3] = {{L.wq, mmq_tiles(L.wq.rows), 0}, {L.wk, mmq_tiles(L.wk.rows), L.wq.rows},
                                       {L.wv, mmq_tiles(L.wv.rows), L.wq.rows + L.wk.rows}};
                 const int ty[3] = {L.wq.type, L.wk.type, L.wv.type};
@@ -894,7 +917,7 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
                     launch_pf_attention<64>(G, grid, s, d, kc, vc, pb);
             }
             launch_quant(d, 2, nullptr, L.wo.k, nullptr, L.wo.type != 8, pb, nt, s);
-            if (mmq) {
+            if (use_mmq(1, L.wo.type)) {
                 const MmqSeg sg{L.wo, mmq_tiles(L.wo.rows), 0};
                 launch_mmq(&sg, &L.wo.type, 1, MMQ_RESID, MmqArgs{pb.act, act_bytes(L.wo.k), L.wo.k, nt, pb.x, d.n_embd, {}},
                            s);
@@ -909,8 +932,8 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
                 });
             }
         }
-        if (!fq) launch_quant(d, 0, pb.x, d.n_embd, L.ffn_norm, L.gate.type != 8, pb, nt, s);
-        if (mmq) {
+        if (!fq || use_mmq(2, L.gate.type)) launch_quant(d, 0, pb.x, d.n_embd, L.ffn_norm, L.gate.type != 8, pb, nt, s);
+        if (use_mmq(2, L.gate.type)) {
             const MmqSeg sg{L.gate, mmq_tiles(L.gate.rows), 0};
             launch_mmq(&sg, &L.gate.type, 1, MMQ_SWIGLU,
                        MmqArgs{pb.act, act_bytes(d.n_embd), d.n_embd, nt, pb.h, d.n_ff, L.up}, s);
@@ -924,8 +947,8 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
                 });
             });
         }
-        if (!fq) launch_quant(d, 1, pb.h, L.down.k, nullptr, L.down.type != 8, pb, nt, s);
-        if (mmq) {
+        if (!fq || use_mmq(3, L.down.type)) launch_quant(d, 1, pb.h, L.down.k, nullptr, L.down.type != 8, pb, nt, s);
+        if (use_mmq(3, L.down.type)) {
             const MmqSeg sg{L.down, mmq_tiles(L.down.rows), 0};
             launch_mmq(&sg, &L.down.type, 1, MMQ_RESID,
                        MmqArgs{pb.act, act_bytes(L.down.k), L.down.k, nt, pb.x, d.n_embd, {}}, s);

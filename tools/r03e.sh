@@ -1,23 +1,30 @@
 set -e
-# per-kernel times of the batched decode step, dot4 (fused quant) vs int8 MFMA, B=8
 out=gpurun_out/r03_e
 mkdir -p $out
 export TMPDIR=/tmp
-export MIO_NO_GRAPH=1
-for p in 3 4; do
-  for mm in 0 1; do
-    MIO_MMQ=$mm timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $out/p${p}_mmq${mm} -o b -- python3 tools/batch_prof.py 8 48 $p > $out/p${p}_mmq${mm}.txt 2>&1
-  done
-done
-unset MIO_NO_GRAPH
-# lm_head LDS pad A/B (at most two lm_head workgroups per CU): timeline + time_kernel
+T="python -u -m pytest -x -v -s --timeout 300 --timeout-method thread"
+# split-bf16 codec GEMMs (default now): stage / PCM parity
+timeout -k 10 600 $T tests/test_codec_gpu.py tests/test_llm_batch_gpu.py > $out/tests.log 2>&1
+# codec time: split-bf16 vs exact-f32 chain
+timeout -k 10 120 python3 -u tools/codec_time.py > $out/codec_x3.txt 2>&1
+MIO_CODEC_GEMM=f32 timeout -k 10 120 python3 -u tools/codec_time.py > $out/codec_f32.txt 2>&1
+# batched decode: fused RoPE attention vs rope + attention
+timeout -k 10 200 python3 -u tools/batch_prof.py 8 200 3 > $out/b8_btatt.txt 2>&1
+MIO_BT_ATT=0 timeout -k 10 200 python3 -u tools/batch_prof.py 8 200 3 > $out/b8_pfatt.txt 2>&1
+# lm_head LDS pad A/B (at most two lm_head workgroups per CU): step timelines
 timeout -k 10 200 python3 -u tools/step_timeline.py --pos 400 > $out/tl_lm0.txt 2>&1
 MIO_LM_LDS_KB=56 timeout -k 10 200 python3 -u tools/step_timeline.py --pos 400 > $out/tl_lm56.txt 2>&1
+# per-kernel times of the batched decode step, dot4 vs int8 MFMA, B=8 (eager)
+for p in 3 4; do
+  for mm in 0 1; do
+    MIO_NO_GRAPH=1 MIO_MMQ=$mm timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $out/p${p}_mmq${mm} -o b -- python3 tools/batch_prof.py 8 48 $p > $out/p${p}_mmq${mm}.txt 2>&1
+  done
+done
+# codec MFMA-busy share (one PMC pass, kernel trace only beside it)
+timeout -s KILL 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d $out/pmcc -o codec -- python3 tools/codec_trace.py > $out/pmcc.txt 2>&1
 # one whole 700-token utterance through the C oracle on the box's CPU share (16 threads)
 timeout -k 10 400 python3 -u tools/cpu_full.py 16 3 700 > $out/cpu_full.json 2> $out/cpu_full.err
 # C1's shape (0.1B Q8_0) through the same CPU port
 timeout -k 10 300 python3 -u tools/cpu_full.py 16 2 700 > $out/cpu_full_c1.json 2> $out/cpu_full_c1.err
-# codec MFMA-busy share (one PMC pass, kernel trace only beside it)
-timeout -s KILL 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d $out/pmcc -o codec -- python3 tools/codec_trace.py > $out/pmcc.txt 2>&1
 # last: the graph-replay profiler probe (a profiler crash ends the script here)
 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $out/gprobe -o g -- python3 tools/graph_replay_probe.py 30000 1 > $out/gprobe.txt 2>&1 || echo "probe exit $?" >> $out/gprobe.txt
