@@ -50,6 +50,9 @@ struct ConvArgs {
 };
 
 void launch_gemm_f32(const GemmArgs &a, int epi, hipStream_t s);
+// One forced tile configuration (micro-benchmark): kg K-groups (1, 2, 4), wt = 10 WTM + WTN
+// (11, 21, 12, 22; WTM x WTN 32 x 32 accumulators per wave). Returns -1 for an unbuilt pair.
+int launch_gemm_f32_cfg(const GemmArgs &a, int epi, int kg, int wt, hipStream_t s);
 void launch_conv_f16(const ConvArgs &a, hipStream_t s);
 
 // Row norms, one wave per row. mode 0: plain, 1: affine (w,b; b may be null),

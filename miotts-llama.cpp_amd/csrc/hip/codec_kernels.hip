@@ -41,7 +41,8 @@ __device__ __forceinline__ float snake_f(float v, float a, float b) {
 }
 
 // ---------------------------------------------------------------- f32 GEMM
-// 64 x 64 output tile per block, 2 x 2 waves of 32 x 32, times KG K-groups (256*KG threads).
+// (64 WTM) x (64 WTN) output tile per block, 2 x 2 waves of (32 WTM) x (32 WTN) (WTM x WTN
+// independent 32 x 32 accumulators per wave), times KG K-groups (256*KG threads).
 // A stage is BK = 32*KG deep; K-group kg owns k in [32kg, 32kg + 32) of every stage, so each
 // wave runs one exact f32 fma chain (16 v_mfma_f32_32x32x2_f32 per stage) and the KG chains
 // are added once, in K-group order, in the epilogue. KG grows as the tile count shrinks so
@@ -108,9 +109,9 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs &g, const f32x16 &a
 }
 
 
-template <int KG, int EPI>
+template <int KG, int EPI, int WTM, int WTN>
 __global__ __launch_bounds__(256 * KG) void gemm_f32_kernel(GemmArgs g) {
-    constexpr int BM = GF_T, BN = GF_T, BK = GF_KD * KG, LDK = BK + 4, NT = 256 * KG;
+    constexpr int BM = GF_T * WTM, BN = GF_T * WTN, BK = GF_KD * KG, LDK = BK + 4, NT = 256 * KG;
     constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 32, TN = WN / 32;
     constexpr int AV = BM * BK / 4 / NT, BV = BN * BK / 4 / NT;
     static_assert(AV >= 1 && BV >= 1, "tile");
@@ -537,7 +538,15 @@ __global__ __launch_bounds__(256) void rownorm_kernel(const float *x, float *y, 
     if (row >= M) return;
     const float *xr = x + (long)row * D;
     const int npl = D / 64;
-    float v[RN_MAXPL];
+    float v[RN_MAXPL], pa[RN_MAXPL], pb[RN_MAXPL];
+    // the affine / AdaLN parameters are loaded with the row (not after the two reductions:
+    // one memory round trip less on the kernel's critical path)
+#pragma unroll
+    for (int i = 0; i < RN_MAXPL; ++i) {
+        const int d = i * 64 + lane;
+        pa[i] = (mode != 0 && i < npl) ? p0[d] : 0.0f;
+        pb[i] = (mode != 0 && p1 && i < npl) ? p1[d] : 0.0f;
+    }
     double s = 0.0;
 #pragma unroll
     for (int i = 0; i < RN_MAXPL; ++i)
@@ -566,12 +575,12 @@ __global__ __launch_bounds__(256) void rownorm_kernel(const float *x, float *y, 
             const int d = i * 64 + lane;
             float t = v[i] * scale;
             if (mode == 1) {
-                t = t * p0[d];
-                if (p1) t = t + p1[d];
+                t = t * pa[i];
+                if (p1) t = t + pb[i];
             } else if (mode == 2) {
-                const float sc = 1.0f + p1[d];
+                const float sc = 1.0f + pb[i];
                 t = t * sc;
-                t = t + p0[d];
+                t = t + pa[i];
             }
             yr[d] = t;
         }
@@ -808,9 +817,10 @@ __global__ __launch_bounds__(256) void cond_gemv_kernel(const float *W, const fl
     if (lane == 0) y[r] = a + b[r];
 }
 
-template <int KG, bool X3>
+template <int KG, bool X3, int WTM = 1, int WTN = 1>
 void launch_gemm_kg(const GemmArgs &a, int epi, hipStream_t s) {
-    const long nb = (long)((a.M + GF_T - 1) / GF_T) * ((a.N + GF_T - 1) / GF_T);
+    const int bm = GF_T * WTM, bn = GF_T * WTN;
+    const long nb = (long)((a.M + bm - 1) / bm) * ((a.N + bn - 1) / bn);
     dim3 grid((unsigned)(8 * ((nb + 7) / 8)));
     switch (epi) {
 #define CASE(E)                                                                                  \
@@ -818,7 +828,7 @@ void launch_gemm_kg(const GemmArgs &a, int epi, hipStream_t s) {
         if constexpr (X3)                                                                        \
             hipLaunchKernelGGL((gemm_x3_kernel<KG, E>), grid, dim3(256 * KG), 0, s, a);          \
         else                                                                                     \
-            hipLaunchKernelGGL((gemm_f32_kernel<KG, E>), grid, dim3(256 * KG), 0, s, a);         \
+            hipLaunchKernelGGL((gemm_f32_kernel<KG, E, WTM, WTN>), grid, dim3(256 * KG), 0, s, a); \
         break;
         CASE(EPI_STORE)
         CASE(EPI_RESID)
@@ -869,6 +879,25 @@ void launch_gemm_f32(const GemmArgs &a0, int epi, hipStream_t s) {
         case 2: launch_gemm_kg<2, false>(a, epi, s); break;
         default: launch_gemm_kg<4, false>(a, epi, s); break;
     }
+}
+
+// One tile configuration, forced (tools/micro/gemm_probe): kg K-groups, wt = 10 WTM + WTN.
+int launch_gemm_f32_cfg(const GemmArgs &a0, int epi, int kg, int wt, hipStream_t s) {
+    GemmArgs a = a0;
+    a.m_major = (long)a.M * a.K > (long)a.N * a.K * 2 ? 1 : 0;
+    switch (wt * 10 + kg) {
+        case 111: launch_gemm_kg<1, false, 1, 1>(a, epi, s); break;
+        case 112: launch_gemm_kg<2, false, 1, 1>(a, epi, s); break;
+        case 114: launch_gemm_kg<4, false, 1, 1>(a, epi, s); break;
+        case 211: launch_gemm_kg<1, false, 2, 1>(a, epi, s); break;
+        case 212: launch_gemm_kg<2, false, 2, 1>(a, epi, s); break;
+        case 121: launch_gemm_kg<1, false, 1, 2>(a, epi, s); break;
+        case 122: launch_gemm_kg<2, false, 1, 2>(a, epi, s); break;
+        case 221: launch_gemm_kg<1, false, 2, 2>(a, epi, s); break;
+        case 222: launch_gemm_kg<2, false, 2, 2>(a, epi, s); break;
+        default: return -1;
+    }
+    return 0;
 }
 
 void launch_conv_f16(const ConvArgs &a, hipStream_t s) {

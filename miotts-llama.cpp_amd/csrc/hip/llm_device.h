@@ -210,7 +210,7 @@ __device__ inline Smem carve(char *base, int K) {
 }
 
 // Workgroup sum (8 waves). No trailing barrier: every caller writes `red` again only
-// after a later workgroup barrier (rmsnorm_quant's staging barrier).
+// after a later workgroup barrier (the quantizer's closing barrier).
 __device__ double block_sum(double v, double *red) {
     v = wave_sum_d(v);
     if ((MIO_TIDX & 63) == 0) red[MIO_TIDX >> 6] = v;
@@ -377,6 +377,36 @@ __device__ inline void load_x(const float *x, const float *w, int K, XRegs<XV> &
     }
 }
 
+// Quantization straight from the registers a prologue loaded: thread t holds elements
+// e = (t + i MT) * 4 .. +3, i.e. wave w lane l holds 256 w + 4 l + 2048 i — exactly superblock
+// w + 8 i at lane offset 4 l (quant_q8k's layout) and, for Q8_0, block 8 w + (l >> 3) + 64 i
+// at position 4 (l & 7) (quant_q80's layout). So the LDS staging row and its barrier of the
+// staged quantizer are not needed; the records are the same bits. One barrier at the end
+// makes them visible to every wave.
+template <int XV>
+__device__ __forceinline__ void quant_regs(const float4 (&v)[XV], int K, bool kquant, const ActL &a) {
+    const int lane = MIO_TIDX & 63, wave = __builtin_amdgcn_readfirstlane(MIO_TIDX >> 6);
+    if (kquant) {
+        const int nsb = K >> 8;
+#pragma unroll
+        for (int j = 0; j < XV; ++j) {
+            const int b = wave + MW * j;
+            if (b >= nsb) break;
+            const float vv[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
+            q8k_store(vv, abs_max4(vv), b, a);
+        }
+    } else {
+        const int nb = K / 32;
+#pragma unroll
+        for (int j = 0; j < XV; ++j) {
+            const int b = wave * 8 + MW * 8 * j + (lane >> 3);
+            const float vv[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
+            q80_store(vv, b, b < nb, a);
+        }
+    }
+    lds_barrier();
+}
+
 // ggml: mean = sum / ne00 in double; a power-of-two K divides exactly by a multiply
 __device__ __forceinline__ float rms_scale(double tot, int K, float eps) {
     const float mean = (float)((K & (K - 1)) == 0 ? tot * (1.0 / K) : tot / K);
@@ -420,34 +450,25 @@ __device__ void rmsnorm_quant(const XRegs<XV> &xr, int K, float eps, bool kquant
     const double tot = block_sum(acc, s.red);
     MIO_DIAG_STAMP(diag, 4, tot);  // reduced over the workgroup
     const float scale = rms_scale(tot, K, eps);
+    float4 y[XV];
 #pragma unroll
     for (int i = 0; i < XV; ++i) {
-        const int e = (MIO_TIDX + i * MT) * 4;
-        if (e < K) {
-            const float4 v = xr.v[i], ww = xr.w[i];
-            float t;
-            t = v.x * scale, s.xs[e + 0] = t * ww.x;
-            t = v.y * scale, s.xs[e + 1] = t * ww.y;
-            t = v.z * scale, s.xs[e + 2] = t * ww.z;
-            t = v.w * scale, s.xs[e + 3] = t * ww.w;
-        }
+        const float4 v = xr.v[i], ww = xr.w[i];
+        float t;
+        t = v.x * scale, y[i].x = t * ww.x;
+        t = v.y * scale, y[i].y = t * ww.y;
+        t = v.z * scale, y[i].z = t * ww.z;
+        t = v.w * scale, y[i].w = t * ww.w;
     }
-    lds_barrier();
-    MIO_DIAG_STAMP(diag, 5, scale);  // normalized activation staged in LDS
-    quantize<XV>(s.xs, K, kquant, s.a);
+    MIO_DIAG_STAMP(diag, 5, scale);  // normalized activation in registers
+    quant_regs<XV>(y, K, kquant, s.a);
 }
 
 template <int XV>
 __device__ inline void plain_quant(const XRegs<XV> &xr, int K, bool kquant, const Smem &s,
                                    unsigned long long *diag = nullptr) {
-#pragma unroll
-    for (int i = 0; i < XV; ++i) {
-        const int e = (MIO_TIDX + i * MT) * 4;
-        if (e < K) *reinterpret_cast<float4 *>(s.xs + e) = xr.v[i];
-    }
-    lds_barrier();
-    MIO_DIAG_STAMP(diag, 5, 0);  // activation arrived and staged in LDS
-    quantize<XV>(s.xs, K, kquant, s.a);
+    MIO_DIAG_STAMP(diag, 5, 0);  // activation arrived
+    quant_regs<XV>(xr.v, K, kquant, s.a);
 }
 
 // ------------------------------------------------------------------ lfm2 gated short conv
@@ -488,14 +509,16 @@ __device__ inline void conv_load(const float *bcx, const ConvPrev &p1, const Con
         }
     }
 }
-// the conv output into s.xs (and, when bx_out is set, this token's bx row into it), then the
-// plain re-quantization of the out_proj activation
+// the conv output (and, when bx_out is set, this token's bx row into it), re-quantized from
+// registers as the out_proj activation
 template <int XV>
 __device__ inline void conv_quant(const ConvRegs<XV> &r, int K, bool kquant, const Smem &s, float *bx_out,
                                   unsigned long long *diag = nullptr) {
+    float4 y[XV];
 #pragma unroll
     for (int i = 0; i < XV; ++i) {
         const int e = (MIO_TIDX + i * MT) * 4;
+        y[i] = make_float4(0.f, 0.f, 0.f, 0.f);
         if (e < K) {
             const float4 bx = mul4(r.b[i], r.x[i]);
             const float v2[4] = {r.p2[i].x, r.p2[i].y, r.p2[i].z, r.p2[i].w};
@@ -505,20 +528,21 @@ __device__ inline void conv_quant(const ConvRegs<XV> &r, int K, bool kquant, con
             // taps of channels e..e+3: w[e + j][t] = flat[(e + j) * 3 + t] = 12 consecutive floats
             const float w[12] = {r.w[i][0].x, r.w[i][0].y, r.w[i][0].z, r.w[i][0].w, r.w[i][1].x, r.w[i][1].y,
                                  r.w[i][1].z, r.w[i][1].w, r.w[i][2].x, r.w[i][2].y, r.w[i][2].z, r.w[i][2].w};
+            float o[4];
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 float acc = 0.0f;
                 acc = acc + v2[j] * w[j * 3 + 0];
                 acc = acc + v1[j] * w[j * 3 + 1];
                 acc = acc + v0[j] * w[j * 3 + 2];
-                s.xs[e + j] = c[j] * acc;
+                o[j] = c[j] * acc;
             }
+            y[i] = make_float4(o[0], o[1], o[2], o[3]);
             if (bx_out) *reinterpret_cast<float4 *>(bx_out + e) = bx;
         }
     }
-    lds_barrier();
     MIO_DIAG_STAMP(diag, 5, 0);
-    quantize<XV>(s.xs, K, kquant, s.a);
+    quant_regs<XV>(y, K, kquant, s.a);
 }
 // keeps the conv operands' use below the first weight loads (x_after_weights)
 template <int XV>
@@ -1005,23 +1029,24 @@ __device__ __forceinline__ float4 merge_out4(const float *base, int nch, int rec
 }
 
 // Merge of the attention chunks' partial records (k_attention) for all heads: thread t
-// owns outputs 4(t + i*MT) .. +3 (merge_out4); normalized outputs -> s.xs, then
-// re-quantized into s.a.
+// owns outputs 4(t + i*MT) .. +3 (merge_out4), re-quantized from its registers into s.a
+// (quant_regs).
 template <int NP>
 __device__ void merge_attention(const LlmDims &d, const float *part, int nch, int K, bool kquant, const Smem &s,
                                 unsigned long long *diag = nullptr) {
     const int hd = d.hd, rec = part_rec(hd);
+    float4 y[NP];
 #pragma unroll
     for (int i = 0; i < NP; ++i) {
         const int e = (MIO_TIDX + i * MT) * 4;
+        y[i] = make_float4(0.f, 0.f, 0.f, 0.f);
         if (e < K) {
             const int h = e / hd, dd = e - h * hd;
-            *reinterpret_cast<float4 *>(s.xs + e) = merge_out4(part + (size_t)h * d.max_splits * rec, nch, rec, hd, dd);
+            y[i] = merge_out4(part + (size_t)h * d.max_splits * rec, nch, rec, hd, dd);
         }
     }
-    lds_barrier();
-    MIO_DIAG_STAMP(diag, 5, 0);  // chunks merged, staged in LDS
-    quantize<NP>(s.xs, K, kquant, s.a);
+    MIO_DIAG_STAMP(diag, 5, 0);  // chunks merged (in registers)
+    quant_regs<NP>(y, K, kquant, s.a);
 }
 
 __device__ inline float silu_f(float x) { return x / (1.0f + expf(-x)); }

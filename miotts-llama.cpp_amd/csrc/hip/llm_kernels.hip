@@ -192,7 +192,6 @@ __global__ __launch_bounds__(MT) void k_ffn_down(LlmDims d, QMat down, LlmBuffer
 template <int NP, int T, bool DG>
 __global__ __launch_bounds__(MT) void k_lm_head(LlmDims d, const float *norm_w, QMat lm, LlmBuffers b) {
     constexpr bool kDiag = DG;
-    const SampleCfg sc = *b.cfg;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __shared__ float bs_[MW];
     __shared__ int bi_[MW];
@@ -203,12 +202,16 @@ __global__ __launch_bounds__(MT) void k_lm_head(LlmDims d, const float *norm_w, 
     XRegs<NP> xr;
     load_x(b.x, norm_w, K, xr);
     x_gate();
-    const int step = b.st->step;
     int lo, hi;
     wave_range(d, lm.rows, lo, hi);
     Frag ga[Cfg<NP>::U], gb[Cfg<NP>::U];
     load_first<T, NP, 1, 0, MIO_LM_AUX>(lm, lm, lo, hi, ga, gb);
     x_after_weights(xr);
+    // the sampling configuration and step are needed only by the epilogue: loaded behind the
+    // first weight group (in front of it, their scalar-load wait held the weight stream back)
+    asm volatile("" ::: "memory");
+    const SampleCfg sc = *b.cfg;
+    const int step = b.st->step;
     MIO_TRACE(b, 1);
     MIO_TL_MARK1(b);
     rmsnorm_quant(xr, K, d.eps, T != 8, s, MIO_TL_DIAGSLOT(b));

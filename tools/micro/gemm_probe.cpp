@@ -44,15 +44,28 @@ int main(int argc, char **argv) {
         g.A = A, g.a_seg = s.K, g.a_row_off = 0, g.a_rows = s.M, g.B = B, g.M = s.M, g.N = s.N, g.K = s.K;
         g.C = C, g.ldc = s.N, g.aux = aux;
         const int reps = s.M >= 4096 && s.N >= 4096 ? 5 : 50;
-        for (int i = 0; i < 3; ++i) mio::launch_gemm_f32(g, s.epi, st);
-        hipEventRecord(e0, st);
-        for (int i = 0; i < reps; ++i) mio::launch_gemm_f32(g, s.epi, st);
-        hipEventRecord(e1, st);
-        hipEventSynchronize(e1);
-        float ms = 0;
-        hipEventElapsedTime(&ms, e0, e1);
-        const double us = ms * 1e3 / reps, tf = 2.0 * s.M * s.N * s.K / (us * 1e-6) / 1e12;
-        printf("%-14s M=%5d N=%5d K=%5d  %8.1f us  %6.1f TF/s\n", s.name, s.M, s.N, s.K, us, tf);
+        // cfg 0: the default choice (launch_gemm_f32); then every forced tile configuration
+        const int cfgs[][2] = {{0, 0}, {1, 11}, {2, 11}, {4, 11}, {1, 21}, {2, 21}, {1, 12}, {2, 12}, {1, 22}, {2, 22}};
+        for (auto &c : cfgs) {
+            auto run = [&] {
+                if (c[0] == 0)
+                    mio::launch_gemm_f32(g, s.epi, st);
+                else
+                    mio::launch_gemm_f32_cfg(g, s.epi, c[0], c[1], st);
+            };
+            for (int i = 0; i < 3; ++i) run();
+            hipEventRecord(e0, st);
+            for (int i = 0; i < reps; ++i) run();
+            hipEventRecord(e1, st);
+            hipEventSynchronize(e1);
+            float ms = 0;
+            hipEventElapsedTime(&ms, e0, e1);
+            const double us = ms * 1e3 / reps, tf = 2.0 * s.M * s.N * s.K / (us * 1e-6) / 1e12;
+            printf("%-14s M=%5d N=%5d K=%5d  kg %d wt %2d  %8.1f us  %6.1f TF/s\n", s.name, s.M, s.N, s.K, c[0], c[1],
+                   us, tf);
+        }
+        fflush(stdout);
     }
+    if (hipGetLastError() != hipSuccess) return 1;
     return 0;
 }
