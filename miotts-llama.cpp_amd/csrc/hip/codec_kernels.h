@@ -55,7 +55,7 @@ void launch_gemm_f32(const GemmArgs &a, int epi, hipStream_t s);
 int launch_gemm_f32_cfg(const GemmArgs &a, int epi, int kg, int wt, hipStream_t s);
 void launch_conv_f16(const ConvArgs &a, hipStream_t s);
 
-// Row norms, one wave per row. mode 0: plain, 1: affine (w,b; b may be null),
+// Row norms, one wave per row (D % 64 == 0, D <= 1024). mode 0: plain, 1: affine (w,b; b may be null),
 // 2: AdaLN (shift = p0, scale = p1: y*(1+scale)+shift). In-place (y == x) allowed.
 void launch_rownorm(const float *x, float *y, int M, int D, float eps, int mode, const float *p0,
                     const float *p1, hipStream_t s);

@@ -22,6 +22,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <string>
+#include <type_traits>
 
 #pragma clang fp contract(off)
 
@@ -53,9 +54,33 @@ constexpr int GF_T = 64, GF_KD = 32;
 
 // Epilogue of one 32 x 32 accumulator tile (C layout: col = lane&31, row = (r&3) + 8(r>>2) +
 // 4(lane>>5)) at rows [rowbase, +32), columns [colbase, +32).
+// Residual epilogues (RESID / GATED) read C and the per-column bias / gate: gemm_f32_kernel
+// loads them before its K loop (gemm_prefetch), so the epilogue does not open with a global
+// round trip after the last MFMA. pre == nullptr: read them here.
+struct EpiPre {
+    float c[16];
+    float col;  // bias[col] (RESID, 0 without bias) or gate[col] (GATED)
+};
+
+template <int EPI>
+__device__ __forceinline__ void gemm_prefetch(const GemmArgs &g, int rowbase, int colbase, int lane, EpiPre &p) {
+    const int col = min(colbase + (lane & 31), g.N - 1);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int row = min(rowbase + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5), g.M - 1);
+        p.c[r] = g.C[(long)row * g.ldc + col];
+    }
+    if constexpr (EPI == EPI_GATED) {
+        p.col = g.aux[col];
+    } else {
+        const float b = (g.bias ? g.bias : g.C)[col];
+        p.col = g.bias ? b : 0.0f;
+    }
+}
+
 template <int EPI>
 __device__ __forceinline__ void gemm_epilogue(const GemmArgs &g, const f32x16 &acc, int rowbase, int colbase,
-                                              int lane) {
+                                              int lane, const EpiPre *pre = nullptr) {
     const int col = colbase + (lane & 31);
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -94,11 +119,16 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs &g, const f32x16 &a
                 if constexpr (EPI == EPI_STORE) {
                     *o = g.bias ? v + g.bias[col] : v;
                 } else if constexpr (EPI == EPI_RESID) {
-                    if (g.bias) v = v + g.bias[col];
-                    *o = *o + v;
+                    if (pre) {
+                        if (g.bias) v = v + pre->col;
+                        *o = pre->c[r] + v;
+                    } else {
+                        if (g.bias) v = v + g.bias[col];
+                        *o = *o + v;
+                    }
                 } else if constexpr (EPI == EPI_GATED) {
-                    const float gh = v * g.aux[col];
-                    *o = *o + gh;
+                    const float gh = v * (pre ? pre->col : g.aux[col]);
+                    *o = (pre ? pre->c[r] : *o) + gh;
                 } else if constexpr (EPI == EPI_SNAKE) {
                     v = v + g.bias[col];
                     *o = snake_f(v, g.aux[col], g.aux2[col]);
@@ -141,40 +171,38 @@ __global__ __launch_bounds__(256 * KG) void gemm_f32_kernel(GemmArgs g) {
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
 
     float4 ra0[AV], rb0[BV], ra1[AV], rb1[BV];
-    // per-thread row bases, fixed over the K loop; a plain A (no tap window: every source row
-    // exists) skips the per-element source-row test and its division
-    const bool a_win = g.a_seg != g.K || g.a_row_off != 0 || g.a_rows < g.M;
-    const float *a_base[AV];
-    const float *b_base[BV];
-    bool a_ok[AV], b_ok[BV];
+    // Operands through buffer descriptors: an out-of-range load returns zeros in hardware, so
+    // a masked element (row past the operand, tap-window row outside [0, a_rows), k past K:
+    // its offset is pushed out of range by a select) needs no branch. Every load then issues
+    // unconditionally and in order, and the compiler's vmcnt waits for exactly the stage a
+    // store consumes instead of draining the stage issued just before (exec-masked loads).
+    const auto ra_src = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(g.A), 0,
+                                                          (int)((long)g.a_rows * g.a_seg * 4), 0x00020000);
+    const auto rb_src = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(g.B), 0,
+                                                          (int)((long)g.N * g.K * 4), 0x00020000);
+    int a_off[AV], a_c[AV], b_off[BV], b_c[BV];
 #pragma unroll
     for (int i = 0; i < AV; ++i) {
         const int e = tid + i * NT, m = m0 + e / (BK / 4);
-        a_ok[i] = m < g.M;
-        a_base[i] = g.A + (long)(m + g.a_row_off) * g.a_seg + (e % (BK / 4)) * 4;
+        a_c[i] = (e % (BK / 4)) * 4;
+        a_off[i] = ((m + g.a_row_off) * g.a_seg + a_c[i]) * 4;  // negative: out of range
     }
 #pragma unroll
     for (int i = 0; i < BV; ++i) {
         const int e = tid + i * NT, n = n0 + e / (BK / 4);
-        b_ok[i] = n < g.N;
-        b_base[i] = g.B + (long)n * g.K + (e % (BK / 4)) * 4;
+        b_c[i] = (e % (BK / 4)) * 4;
+        b_off[i] = (n * g.K + b_c[i]) * 4;
     }
     auto load = [&](int k0, float4 (&ra)[AV], float4 (&rb)[BV]) {
 #pragma unroll
         for (int i = 0; i < AV; ++i) {
-            const int e = tid + i * NT, m = m0 + e / (BK / 4), k = k0 + (e % (BK / 4)) * 4;
-            bool ok = a_ok[i] && k < g.K;
-            if (a_win && ok) {
-                const int src = m + g.a_row_off + k / g.a_seg;
-                ok = src >= 0 && src < g.a_rows;
-            }
-            ra[i] = ok ? *reinterpret_cast<const float4 *>(a_base[i] + k0) : make_float4(0.f, 0.f, 0.f, 0.f);
+            const int off = k0 + a_c[i] < g.K ? a_off[i] + k0 * 4 : (int)0x80000000;
+            ra[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(ra_src, off, 0, 0));
         }
 #pragma unroll
         for (int i = 0; i < BV; ++i) {
-            const int k = k0 + ((tid + i * NT) % (BK / 4)) * 4;
-            rb[i] = (b_ok[i] && k < g.K) ? *reinterpret_cast<const float4 *>(b_base[i] + k0)
-                                         : make_float4(0.f, 0.f, 0.f, 0.f);
+            const int off = k0 + b_c[i] < g.K ? b_off[i] + k0 * 4 : (int)0x80000000;
+            rb[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rb_src, off, 0, 0));
         }
     };
     auto store = [&](int buf, const float4 (&ra)[AV], const float4 (&rb)[BV]) {
@@ -218,22 +246,32 @@ __global__ __launch_bounds__(256 * KG) void gemm_f32_kernel(GemmArgs g) {
         }
     };
 
+    constexpr bool PRE = EPI == EPI_RESID || EPI == EPI_GATED;
+    EpiPre pre[PRE ? TM : 1][PRE ? TN : 1];
+    if constexpr (PRE) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) gemm_prefetch<EPI>(g, m0 + wm * WM + i * 32, n0 + wn * WN + j * 32, lane, pre[i][j]);
+    }
+
+    // stages past K load zeros (unconditional loads keep the vmcnt ring exact, see load)
     const int nk = (g.K + BK - 1) / BK;
     load(0, ra0, rb0);
-    if (nk > 1) load(BK, ra1, rb1);
+    load(BK, ra1, rb1);
     store(0, ra0, rb0);
     __syncthreads();
     for (int kt = 0; kt < nk; kt += 2) {
         // even stage: LDS buffer 0; registers 1 hold stage kt+1, registers 0 refill with kt+2
-        if (kt + 2 < nk) load((kt + 2) * BK, ra0, rb0);
+        load((kt + 2) * BK, ra0, rb0);
         compute(0);
-        if (kt + 1 < nk) store(1, ra1, rb1);
+        store(1, ra1, rb1);
         __syncthreads();
         if (kt + 1 >= nk) break;
         // odd stage: LDS buffer 1
-        if (kt + 3 < nk) load((kt + 3) * BK, ra1, rb1);
+        load((kt + 3) * BK, ra1, rb1);
         compute(1);
-        if (kt + 2 < nk) store(0, ra0, rb0);
+        store(0, ra0, rb0);
         __syncthreads();
     }
 
@@ -269,7 +307,9 @@ __global__ __launch_bounds__(256 * KG) void gemm_f32_kernel(GemmArgs g) {
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) gemm_epilogue<EPI>(g, acc[i][j], m0 + wm * WM + i * 32, n0 + wn * WN + j * 32, lane);
+        for (int j = 0; j < TN; ++j)
+            gemm_epilogue<EPI>(g, acc[i][j], m0 + wm * WM + i * 32, n0 + wn * WN + j * 32, lane,
+                               PRE ? &pre[PRE ? i : 0][PRE ? j : 0] : nullptr);
 }
 
 // ---------------------------------------------------------------- split-bf16 GEMM
@@ -458,26 +498,28 @@ __global__ __launch_bounds__(256) void conv_f16_kernel(ConvArgs c) {
     for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
 
     uint4 ra0[NV], rb0[NV], ra1[NV], rb1[NV];
+    // Buffer-descriptor loads as in gemm_f32_kernel: element (m, k = tap Cin + ci) of the tap
+    // window sits at Xa[(m - pad) Cin + k], valid exactly when that index is inside [0, L Cin)
+    // (the hardware returns zeros outside, the "same" padding); k past K is pushed out of
+    // range by a select. No branches around the loads: the vmcnt ring stays exact.
+    const auto xa_src = __builtin_amdgcn_make_buffer_rsrc(const_cast<_Float16 *>(c.Xa), 0,
+                                                          (int)((long)c.L * c.Cin * 2), 0x00020000);
+    const auto w_src = __builtin_amdgcn_make_buffer_rsrc(const_cast<_Float16 *>(c.B), 0,
+                                                         (int)((long)c.Cout * K * 2), 0x00020000);
     auto load = [&](int k0, uint4 (&ra)[NV], uint4 (&rb)[NV]) {
 #pragma unroll
         for (int i = 0; i < NV; ++i) {
             const int e = tid + i * 256, r = e / (CV_BK / 8), c8 = (e % (CV_BK / 8)) * 8;
-            const int m = m0 + r, k = k0 + c8;
-            uint4 v = make_uint4(0, 0, 0, 0);
-            if (m < c.L && k < K) {
-                const int tap = k / c.Cin, ci = k - tap * c.Cin;
-                const int src = m + tap - c.pad;
-                if (src >= 0 && src < c.L) v = *reinterpret_cast<const uint4 *>(c.Xa + (long)src * c.Cin + ci);
-            }
-            ra[i] = v;
+            const int k = k0 + c8;
+            const int off = k < K ? ((m0 + r - c.pad) * c.Cin + k) * 2 : (int)0x80000000;
+            ra[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xa_src, off, 0, 0));
         }
 #pragma unroll
         for (int i = 0; i < NV; ++i) {
             const int e = tid + i * 256, r = e / (CV_BK / 8), c8 = (e % (CV_BK / 8)) * 8;
-            const int n = n0 + r, k = k0 + c8;
-            uint4 v = make_uint4(0, 0, 0, 0);
-            if (n < c.Cout && k < K) v = *reinterpret_cast<const uint4 *>(c.B + (long)n * K + k);
-            rb[i] = v;
+            const int k = k0 + c8;
+            const int off = k < K ? ((n0 + r) * K + k) * 2 : (int)0x80000000;
+            rb[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(w_src, off, 0, 0));
         }
     };
     auto store = [&](int buf, const uint4 (&ra)[NV], const uint4 (&rb)[NV]) {
@@ -499,29 +541,39 @@ __global__ __launch_bounds__(256) void conv_f16_kernel(ConvArgs c) {
         }
     };
 
+    // epilogue operands (bias, residual) loaded before the K loop, off its critical path
+    const int col = n0 + wn * 32 + (lane & 31), colc = min(col, c.Cout - 1);
+    const float bias = c.bias[colc];
+    float res[16];
+    const float *rsrc = c.resid ? c.resid : c.bias;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int row = min(m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5), c.L - 1);
+        res[r] = rsrc[c.resid ? (long)row * c.Cout + colc : colc];
+    }
+
     const int nk = (K + CV_BK - 1) / CV_BK;
     load(0, ra0, rb0);
-    if (nk > 1) load(CV_BK, ra1, rb1);
+    load(CV_BK, ra1, rb1);
     store(0, ra0, rb0);
     __syncthreads();
     for (int kt = 0; kt < nk; kt += 2) {  // same two-stage register ring as gemm_f32_kernel
-        if (kt + 2 < nk) load((kt + 2) * CV_BK, ra0, rb0);
+        load((kt + 2) * CV_BK, ra0, rb0);
         compute(0);
-        if (kt + 1 < nk) store(1, ra1, rb1);
+        store(1, ra1, rb1);
         __syncthreads();
         if (kt + 1 >= nk) break;
-        if (kt + 3 < nk) load((kt + 3) * CV_BK, ra1, rb1);
+        load((kt + 3) * CV_BK, ra1, rb1);
         compute(1);
-        if (kt + 2 < nk) store(0, ra0, rb0);
+        store(0, ra0, rb0);
         __syncthreads();
     }
-    const int col = n0 + wn * 32 + (lane & 31);
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
         const int row = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
         if (row < c.L && col < c.Cout) {
-            float v = acc[r] + c.bias[col];
-            if (c.resid) v = v + c.resid[(long)row * c.Cout + col];
+            float v = acc[r] + bias;
+            if (c.resid) v = v + res[r];
             c.Y[(long)row * c.Cout + col] = v;
         }
     }
@@ -530,60 +582,76 @@ __global__ __launch_bounds__(256) void conv_f16_kernel(ConvArgs c) {
 // ---------------------------------------------------------------- row norms
 constexpr int RN_MAXPL = 16;  // D <= 1024
 
-__global__ __launch_bounds__(256) void rownorm_kernel(const float *x, float *y, int M, int D,
-                                                      float eps, int mode, const float *p0,
-                                                      const float *p1) {
+// Sum over the 64 lanes of a wave in double, the total in every lane: DPP steps within rows
+// (quad xor 1, 2, half-row and row mirrors), row broadcasts 15 / 31 into lane 63, one read.
+// ~6 VALU latencies instead of six ds_bpermute round trips per 32-bit half.
+template <int CTRL, int ROWS = 0xF>
+__device__ __forceinline__ double dpp_f64(double x) {
+    const int2 v = __builtin_bit_cast(int2, x);
+    const int lo = __builtin_amdgcn_update_dpp(0, v.x, CTRL, ROWS, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, v.y, CTRL, ROWS, 0xF, false);
+    return __builtin_bit_cast(double, make_int2(lo, hi));
+}
+__device__ __forceinline__ double wave_sum_f64(double s) {
+    s += dpp_f64<0xB1>(s);        // quad_perm [1,0,3,2]
+    s += dpp_f64<0x4E>(s);        // quad_perm [2,3,0,1]
+    s += dpp_f64<0x141>(s);       // row_half_mirror
+    s += dpp_f64<0x140>(s);       // row_mirror
+    s += dpp_f64<0x142, 0xA>(s);  // row_bcast:15 -> rows 1, 3
+    s += dpp_f64<0x143, 0xC>(s);  // row_bcast:31 -> rows 2, 3
+    const int2 v = __builtin_bit_cast(int2, s);
+    return __builtin_bit_cast(double, make_int2(__builtin_amdgcn_readlane(v.x, 63), __builtin_amdgcn_readlane(v.y, 63)));
+}
+
+// One wave per row; NPL = D / 64 values per lane, fixed at compile time so that every load
+// is unconditional (a runtime bound put each load behind a branch and a vmcnt(0) drain).
+template <int NPL>
+__global__ __launch_bounds__(256) void rownorm_kernel(const float *x, float *y, int M, float eps, int mode,
+                                                      const float *p0, const float *p1) {
+    constexpr int D = NPL * 64;
     const int lane = threadIdx.x & 63;
     const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (row >= M) return;
     const float *xr = x + (long)row * D;
-    const int npl = D / 64;
-    float v[RN_MAXPL], pa[RN_MAXPL], pb[RN_MAXPL];
+    float v[NPL], pa[NPL], pb[NPL];
     // the affine / AdaLN parameters are loaded with the row (not after the two reductions:
     // one memory round trip less on the kernel's critical path)
+    const float *q0 = mode != 0 ? p0 : xr, *q1 = (mode != 0 && p1) ? p1 : xr;
 #pragma unroll
-    for (int i = 0; i < RN_MAXPL; ++i) {
-        const int d = i * 64 + lane;
-        pa[i] = (mode != 0 && i < npl) ? p0[d] : 0.0f;
-        pb[i] = (mode != 0 && p1 && i < npl) ? p1[d] : 0.0f;
+    for (int i = 0; i < NPL; ++i) {
+        v[i] = xr[i * 64 + lane];
+        pa[i] = q0[i * 64 + lane];
+        pb[i] = q1[i * 64 + lane];
     }
     double s = 0.0;
 #pragma unroll
-    for (int i = 0; i < RN_MAXPL; ++i)
-        if (i < npl) {
-            v[i] = xr[i * 64 + lane];
-            s += (double)v[i];
-        }
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o);
+    for (int i = 0; i < NPL; ++i) s += (double)v[i];
+    s = wave_sum_f64(s);
     const float mean = (float)(s / D);
     double s2 = 0.0;
 #pragma unroll
-    for (int i = 0; i < RN_MAXPL; ++i)
-        if (i < npl) {
-            v[i] = v[i] - mean;
-            s2 += (double)(v[i] * v[i]);
-        }
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) s2 += __shfl_xor(s2, o);
+    for (int i = 0; i < NPL; ++i) {
+        v[i] = v[i] - mean;
+        s2 += (double)(v[i] * v[i]);
+    }
+    s2 = wave_sum_f64(s2);
     const float variance = (float)(s2 / D);
     const float scale = 1.0f / sqrtf(variance + eps);
     float *yr = y + (long)row * D;
 #pragma unroll
-    for (int i = 0; i < RN_MAXPL; ++i)
-        if (i < npl) {
-            const int d = i * 64 + lane;
-            float t = v[i] * scale;
-            if (mode == 1) {
-                t = t * pa[i];
-                if (p1) t = t + pb[i];
-            } else if (mode == 2) {
-                const float sc = 1.0f + pb[i];
-                t = t * sc;
-                t = t + pa[i];
-            }
-            yr[d] = t;
+    for (int i = 0; i < NPL; ++i) {
+        const int d = i * 64 + lane;
+        float t = v[i] * scale;
+        if (mode == 1) {
+            t = t * pa[i];
+            if (p1) t = t + pb[i];
+        } else if (mode == 2) {
+            const float sc = 1.0f + pb[i];
+            t = t * sc;
+            t = t + pa[i];
         }
+        yr[d] = t;
+    }
 }
 
 // ---------------------------------------------------------------- group norm
@@ -594,64 +662,75 @@ __global__ __launch_bounds__(256) void rownorm_kernel(const float *x, float *y, 
 // deviations and write rstd; gn_apply writes the f16 conv operand. Kernel boundaries order
 // the passes (no grid-wide fences: on 8 XCDs a device-scope release flushes the L2).
 // Requires C % 8 == 0, C <= 1024, G <= 64 and cpg | 64 (groups never straddle 64 lanes).
-constexpr int GN_MAXJ = 16, GN_PMAX = 256;
+constexpr int GN_PMAX = 256;
 
-template <int PASS>
+// NJ = ceil(C / 64) channel chunks per lane, fixed at compile time: the loads of a row issue
+// unconditionally (a runtime bound put every load behind a branch and a vmcnt(0) drain);
+// channels past C read an in-range address and are zeroed by a select.
+template <int PASS, int NJ>
 __global__ __launch_bounds__(256) void gn_partial_kernel(const float *x, int L, int C, int G, int cpg,
                                                          int rows, const float2 *stat, double *part) {
     __shared__ double wsum[4][64];
     const int p = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int r0 = p * rows, r1 = min(L, r0 + rows);
-    const int nj = (C + 63) / 64;
-    double acc[GN_MAXJ];
-    float mean[GN_MAXJ];
+    double acc[NJ];
+    float mean[NJ];
+    bool ok[NJ];
+    int ch[NJ];
 #pragma unroll
-    for (int j = 0; j < GN_MAXJ; ++j) {
+    for (int j = 0; j < NJ; ++j) {
+        ok[j] = j * 64 + lane < C;
+        ch[j] = ok[j] ? j * 64 + lane : 0;
         acc[j] = 0.0;
-        mean[j] = (PASS == 2 && j * 64 + lane < C) ? stat[(j * 64 + lane) / cpg].x : 0.0f;
+        mean[j] = PASS == 2 ? stat[ch[j] / cpg].x : 0.0f;
     }
-#pragma unroll 4
+#pragma unroll 2
     for (int r = r0 + wave; r < r1; r += 4) {
-        const float *xr = x + (long)r * C + lane;
+        const float *xr = x + (long)r * C;
+        float v[NJ];
 #pragma unroll
-        for (int j = 0; j < GN_MAXJ; ++j)
-            if (j < nj && j * 64 + lane < C) {
-                const float v = xr[j * 64];
-                if constexpr (PASS == 1) {
-                    acc[j] += (double)v;
-                } else {
-                    const float d = v - mean[j];
-                    acc[j] += (double)(d * d);
-                }
+        for (int j = 0; j < NJ; ++j) v[j] = xr[ch[j]];
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            if constexpr (PASS == 1) {
+                acc[j] += ok[j] ? (double)v[j] : 0.0;
+            } else {
+                const float d = v[j] - mean[j];
+                acc[j] += ok[j] ? (double)(d * d) : 0.0;
             }
+        }
     }
     // a group is cpg consecutive lanes of one 64-channel chunk
 #pragma unroll
-    for (int j = 0; j < GN_MAXJ; ++j)
-        if (j < nj) {
-            double s = acc[j];
-            for (int o = 1; o < cpg; o <<= 1) s += __shfl_xor(s, o);
-            if (lane % cpg == 0 && j * 64 + lane < C) wsum[wave][(j * 64 + lane) / cpg] = s;
-        }
+    for (int j = 0; j < NJ; ++j) {
+        double s = acc[j];
+        for (int o = 1; o < cpg; o <<= 1) s += __shfl_xor(s, o);
+        if (lane % cpg == 0 && ok[j]) wsum[wave][(j * 64 + lane) / cpg] = s;
+    }
     __syncthreads();
     for (int g = threadIdx.x; g < G; g += 256)
         part[(long)p * G + g] = ((wsum[0][g] + wsum[1][g]) + wsum[2][g]) + wsum[3][g];
 }
 
 // One block: stat[g].x = mean (PASS 1) or stat[g].y = rstd (PASS 2) from the P slice sums;
-// 32 lanes per group, lane s takes slices p = s mod 32, then a 5-level xor tree.
+// 32 lanes per group, lane s takes slices p = s mod 32, then a 5-level xor tree. The slice
+// loads issue unconditionally (clamped index, zeroed by a select).
 template <int PASS>
 __global__ __launch_bounds__(1024) void gn_final_kernel(const double *part, int P, int G, long n,
                                                         float eps, float2 *stat) {
     const int t = threadIdx.x, s32 = t & 31;
     for (int g0 = 0; g0 < G; g0 += 32) {
         const int g = g0 + (t >> 5), gg = g < G ? g : 0;
-        double sum = 0.0;
+        double v[GN_PMAX / 32];
 #pragma unroll
         for (int i = 0; i < GN_PMAX / 32; ++i) {
             const int q = s32 + 32 * i;
-            if (q < P) sum += part[(long)q * G + gg];
+            v[i] = part[(long)(q < P ? q : 0) * G + gg];
         }
+        double sum = 0.0;
+#pragma unroll
+        for (int i = 0; i < GN_PMAX / 32; ++i)
+            if (s32 + 32 * i < P) sum += v[i];
 #pragma unroll
         for (int o = 1; o < 32; o <<= 1) sum += __shfl_xor(sum, o);
         if (s32 == 0 && g < G) {
@@ -693,15 +772,24 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const float *x, int L, in
 }
 
 // ---------------------------------------------------------------- banded attention
-constexpr int BA_QB = 64;   // queries per block (4 threads per query)
+// 16 queries per block, 16 threads per query (thread t scores keys j0 + t + 16 n, then owns
+// output dims [4t, 4t + 4)): 4x the blocks of a 4-threads-per-query layout, so that the
+// 700 / 1400-row attentions spread over every CU instead of ~150 of them. K (roped) and V
+// rows of the block's key range and its roped queries are staged in LDS with float4 loads.
+// Each score is the same ascending-d fmaf chain as before; P V runs over ascending j.
+constexpr int BA_QB = 16;   // queries per block
+constexpr int BA_TQ = 16;   // threads per query
 constexpr int BA_HD = 64;   // head dim
 constexpr int BA_MAXHW = 32;
 constexpr int BA_KB = BA_QB + 2 * BA_MAXHW;
+constexpr int BA_LD = BA_HD + 4;  // K / Q row stride (floats): 16 B aligned, rows 4 banks apart
+constexpr int BA_NS = (2 * BA_MAXHW + 1 + BA_TQ - 1) / BA_TQ;  // scores per thread
 
 __global__ __launch_bounds__(256) void band_attention_kernel(const float *qkv, float *out, int S,
                                                              int H, int hw, const float2 *rope) {
-    __shared__ float Ks[BA_KB][BA_HD + 1];
+    __shared__ __attribute__((aligned(16))) float Ks[BA_KB][BA_LD];
     __shared__ __attribute__((aligned(16))) float Vs[BA_KB][BA_HD];
+    __shared__ __attribute__((aligned(16))) float Qs[BA_QB][BA_LD];
     __shared__ float Ps[BA_QB][2 * BA_MAXHW + 2];
     const int h = blockIdx.y, i0 = blockIdx.x * BA_QB, tid = threadIdx.x;
     const int D = H * BA_HD, ld = 3 * D;
@@ -710,87 +798,91 @@ __global__ __launch_bounds__(256) void band_attention_kernel(const float *qkv, f
     if (kend > S - 1) kend = S - 1;
     const int nk = kend - kbeg + 1;
 
-    // K (roped) and V rows of this head into LDS: one pair per thread-iteration
-    for (int e = tid; e < nk * (BA_HD / 2); e += 256) {
-        const int r = e / (BA_HD / 2), pi = e - r * (BA_HD / 2);
-        const int p = kbeg + r;
-        const float *kr = qkv + (long)p * ld + D + h * BA_HD;
-        const float *vr = qkv + (long)p * ld + 2 * D + h * BA_HD;
-        const float2 cs = rope[(long)p * (BA_HD / 2) + pi];
-        const float x0 = kr[2 * pi], x1 = kr[2 * pi + 1];
-        Ks[r][2 * pi] = x0 * cs.x - x1 * cs.y;
-        Ks[r][2 * pi + 1] = x0 * cs.y + x1 * cs.x;
-        Vs[r][2 * pi] = vr[2 * pi];
-        Vs[r][2 * pi + 1] = vr[2 * pi + 1];
+    // K (roped) and V rows, then the block's queries (roped): float4 = two rotation pairs
+    for (int e = tid; e < nk * (BA_HD / 4); e += 256) {
+        const int r = e / (BA_HD / 4), c = (e - r * (BA_HD / 4)) * 4;
+        const long p = kbeg + r;
+        const float4 k = *reinterpret_cast<const float4 *>(qkv + p * ld + D + h * BA_HD + c);
+        const float4 cs = *reinterpret_cast<const float4 *>(rope + p * (BA_HD / 2) + c / 2);
+        const float4 v = *reinterpret_cast<const float4 *>(qkv + p * ld + 2 * D + h * BA_HD + c);
+        *reinterpret_cast<float4 *>(&Ks[r][c]) =
+            make_float4(k.x * cs.x - k.y * cs.y, k.x * cs.y + k.y * cs.x, k.z * cs.z - k.w * cs.w, k.z * cs.w + k.w * cs.z);
+        *reinterpret_cast<float4 *>(&Vs[r][c]) = v;
+    }
+    for (int e = tid; e < BA_QB * (BA_HD / 4); e += 256) {
+        const int r = e / (BA_HD / 4), c = (e - r * (BA_HD / 4)) * 4;
+        const long p = i0 + r < S ? i0 + r : S - 1;
+        const float4 q = *reinterpret_cast<const float4 *>(qkv + p * ld + h * BA_HD + c);
+        const float4 cs = *reinterpret_cast<const float4 *>(rope + p * (BA_HD / 2) + c / 2);
+        *reinterpret_cast<float4 *>(&Qs[r][c]) =
+            make_float4(q.x * cs.x - q.y * cs.y, q.x * cs.y + q.y * cs.x, q.z * cs.z - q.w * cs.w, q.z * cs.w + q.w * cs.z);
     }
     __syncthreads();
 
-    const int ql = tid >> 2, t = tid & 3;
+    const int ql = tid / BA_TQ, t = tid % BA_TQ;
     const int i = i0 + ql;
     const bool active = i < S;
-    float q[BA_HD];
-    if (active) {
-        const float *qr = qkv + (long)i * ld + h * BA_HD;
-#pragma unroll
-        for (int pi = 0; pi < BA_HD / 2; ++pi) {
-            const float2 cs = rope[(long)i * (BA_HD / 2) + pi];
-            const float x0 = qr[2 * pi], x1 = qr[2 * pi + 1];
-            q[2 * pi] = x0 * cs.x - x1 * cs.y;
-            q[2 * pi + 1] = x0 * cs.y + x1 * cs.x;
-        }
-    }
     const int j0 = active ? (i - hw < 0 ? 0 : i - hw) : 0;
     const int j1 = active ? (i + hw > S - 1 ? S - 1 : i + hw) : -1;
     const float scale = 0.125f;  // 1/sqrt(64), exact
-    float mx = -INFINITY;
-    float sc[(2 * BA_MAXHW + 1 + 3) / 4];
+    float q[BA_HD];
 #pragma unroll
-    for (int n = 0; n < (2 * BA_MAXHW + 1 + 3) / 4; ++n) {
-        const int j = j0 + t + 4 * n;
+    for (int d = 0; d < BA_HD; d += 4) {
+        const float4 v = *reinterpret_cast<const float4 *>(&Qs[ql][d]);
+        q[d] = v.x, q[d + 1] = v.y, q[d + 2] = v.z, q[d + 3] = v.w;
+    }
+    float mx = -INFINITY;
+    float sc[BA_NS];
+#pragma unroll
+    for (int n = 0; n < BA_NS; ++n) {
+        const int j = j0 + t + BA_TQ * n;
         float s = -INFINITY;
         if (j <= j1) {
             const float *kr = Ks[j - kbeg];
             float a = 0.0f;
 #pragma unroll
-            for (int d = 0; d < BA_HD; ++d) a = fmaf(kr[d], q[d], a);
+            for (int d = 0; d < BA_HD; d += 4) {
+                const float4 k = *reinterpret_cast<const float4 *>(kr + d);
+                a = fmaf(k.x, q[d], a);
+                a = fmaf(k.y, q[d + 1], a);
+                a = fmaf(k.z, q[d + 2], a);
+                a = fmaf(k.w, q[d + 3], a);
+            }
             s = a * scale;
         }
         sc[n] = s;
         mx = fmaxf(mx, s);
     }
-    mx = fmaxf(mx, __shfl_xor(mx, 1));
-    mx = fmaxf(mx, __shfl_xor(mx, 2));
+#pragma unroll
+    for (int o = 1; o < BA_TQ; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
     float sum = 0.0f;
 #pragma unroll
-    for (int n = 0; n < (2 * BA_MAXHW + 1 + 3) / 4; ++n) {
-        const int j = j0 + t + 4 * n;
+    for (int n = 0; n < BA_NS; ++n) {
+        const int j = j0 + t + BA_TQ * n;
         const float e = (j <= j1) ? expf(sc[n] - mx) : 0.0f;
         sc[n] = e;
         sum += e;
     }
-    sum += __shfl_xor(sum, 1);
-    sum += __shfl_xor(sum, 2);
+#pragma unroll
+    for (int o = 1; o < BA_TQ; o <<= 1) sum += __shfl_xor(sum, o);
     const float inv = 1.0f / sum;
 #pragma unroll
-    for (int n = 0; n < (2 * BA_MAXHW + 1 + 3) / 4; ++n) {
-        const int j = j0 + t + 4 * n;
+    for (int n = 0; n < BA_NS; ++n) {
+        const int j = j0 + t + BA_TQ * n;
         if (j <= j1) Ps[ql][j - j0] = sc[n] * inv;
     }
     __syncthreads();
     if (!active) return;
-    float o[16];
-#pragma unroll
-    for (int d = 0; d < 16; ++d) o[d] = 0.0f;
+    float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
     for (int j = j0; j <= j1; ++j) {
         const float p = Ps[ql][j - j0];
-        const float *vr = &Vs[j - kbeg][16 * t];
-#pragma unroll
-        for (int d = 0; d < 16; ++d) o[d] = fmaf(p, vr[d], o[d]);
+        const float4 v = *reinterpret_cast<const float4 *>(&Vs[j - kbeg][4 * t]);
+        o.x = fmaf(p, v.x, o.x);
+        o.y = fmaf(p, v.y, o.y);
+        o.z = fmaf(p, v.z, o.z);
+        o.w = fmaf(p, v.w, o.w);
     }
-    float *orow = out + (long)i * D + h * BA_HD + 16 * t;
-#pragma unroll
-    for (int d = 0; d < 16; d += 4)
-        *reinterpret_cast<float4 *>(orow + d) = make_float4(o[d], o[d + 1], o[d + 2], o[d + 3]);
+    *reinterpret_cast<float4 *>(out + (long)i * D + h * BA_HD + 4 * t) = o;
 }
 
 // ---------------------------------------------------------------- small kernels
@@ -882,6 +974,8 @@ void launch_gemm_f32(const GemmArgs &a0, int epi, hipStream_t s) {
 }
 
 // One tile configuration, forced (tools/micro/gemm_probe): kg K-groups, wt = 10 WTM + WTN.
+// Larger wave tiles (21, 12, 22) measured no faster on any codec shape and are not built
+// (profiles/r03_codec_gemm_configs_bufload.txt).
 int launch_gemm_f32_cfg(const GemmArgs &a0, int epi, int kg, int wt, hipStream_t s) {
     GemmArgs a = a0;
     a.m_major = (long)a.M * a.K > (long)a.N * a.K * 2 ? 1 : 0;
@@ -889,12 +983,6 @@ int launch_gemm_f32_cfg(const GemmArgs &a0, int epi, int kg, int wt, hipStream_t
         case 111: launch_gemm_kg<1, false, 1, 1>(a, epi, s); break;
         case 112: launch_gemm_kg<2, false, 1, 1>(a, epi, s); break;
         case 114: launch_gemm_kg<4, false, 1, 1>(a, epi, s); break;
-        case 211: launch_gemm_kg<1, false, 2, 1>(a, epi, s); break;
-        case 212: launch_gemm_kg<2, false, 2, 1>(a, epi, s); break;
-        case 121: launch_gemm_kg<1, false, 1, 2>(a, epi, s); break;
-        case 122: launch_gemm_kg<2, false, 1, 2>(a, epi, s); break;
-        case 221: launch_gemm_kg<1, false, 2, 2>(a, epi, s); break;
-        case 222: launch_gemm_kg<2, false, 2, 2>(a, epi, s); break;
         default: return -1;
     }
     return 0;
@@ -907,7 +995,14 @@ void launch_conv_f16(const ConvArgs &a, hipStream_t s) {
 
 void launch_rownorm(const float *x, float *y, int M, int D, float eps, int mode, const float *p0,
                     const float *p1, hipStream_t s) {
-    hipLaunchKernelGGL(rownorm_kernel, dim3((M + 3) / 4), dim3(256), 0, s, x, y, M, D, eps, mode, p0, p1);
+    const dim3 grid((M + 3) / 4);
+    switch (D / 64) {
+#define RN(P)                                                                                             \
+    case P: hipLaunchKernelGGL(rownorm_kernel<P>, grid, dim3(256), 0, s, x, y, M, eps, mode, p0, p1); break;
+        RN(1) RN(2) RN(3) RN(4) RN(5) RN(6) RN(7) RN(8) RN(9) RN(10) RN(11) RN(12) RN(13) RN(14) RN(15) RN(16)
+#undef RN
+        default: break;  // refused at load (codec.cpp: D % 64 == 0, D <= 1024)
+    }
 }
 
 void launch_groupnorm_apply(const float *x, int L, int C, int G, float eps, const float *gamma,
@@ -917,12 +1012,23 @@ void launch_groupnorm_apply(const float *x, int L, int C, int G, float eps, cons
     if ((L + rows - 1) / rows > GN_PMAX) rows = (L + GN_PMAX - 1) / GN_PMAX;
     const int P = (L + rows - 1) / rows;
     const long n = (long)L * cpg;
-    hipLaunchKernelGGL(gn_partial_kernel<1>, dim3(P), dim3(256), 0, s, x, L, C, G, cpg, rows,
-                       (const float2 *)gs.stat, gs.part);
+    auto partial = [&](auto pass) {
+        constexpr int PS = decltype(pass)::value;
+        switch ((C + 63) / 64) {
+#define GP(J)                                                                                                  \
+    case J:                                                                                                    \
+        hipLaunchKernelGGL((gn_partial_kernel<PS, J>), dim3(P), dim3(256), 0, s, x, L, C, G, cpg, rows,        \
+                           (const float2 *)gs.stat, gs.part);                                                  \
+        break;
+            GP(1) GP(2) GP(3) GP(4) GP(5) GP(6) GP(7) GP(8) GP(9) GP(10) GP(11) GP(12) GP(13) GP(14) GP(15) GP(16)
+#undef GP
+            default: break;  // C <= 1024 (codec.cpp refuses larger)
+        }
+    };
+    partial(std::integral_constant<int, 1>{});
     hipLaunchKernelGGL(gn_final_kernel<1>, dim3(1), dim3(1024), 0, s, (const double *)gs.part, P, G, n, eps,
                        gs.stat);
-    hipLaunchKernelGGL(gn_partial_kernel<2>, dim3(P), dim3(256), 0, s, x, L, C, G, cpg, rows,
-                       (const float2 *)gs.stat, gs.part);
+    partial(std::integral_constant<int, 2>{});
     hipLaunchKernelGGL(gn_final_kernel<2>, dim3(1), dim3(1024), 0, s, (const double *)gs.part, P, G, n, eps,
                        gs.stat);
     const long n8 = (long)L * C / 8;

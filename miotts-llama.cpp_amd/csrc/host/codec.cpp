@@ -570,7 +570,7 @@ extern "C" int mio_hip_codec_load(mio_hip_device *d, const char *path, mio_hip_c
     // shapes this implementation supports (all MioCodec checkpoints: head_dim 64, window 65)
     if (c->pre_dim % c->pre_heads || c->pre_dim / c->pre_heads != 64 || c->dec_dim % c->dec_heads ||
         c->dec_dim / c->dec_heads != 64 || c->pre_win / 2 > 32 || c->dec_win / 2 > 32 ||
-        c->pre_dim % 64 || c->dec_dim % 64 || c->pre_ff % 16 || c->dec_ff % 16 || c->groups > 64 ||
+        c->pre_dim % 64 || c->dec_dim % 64 || c->pre_dim > 1024 || c->dec_dim > 1024 || c->pre_ff % 16 || c->dec_ff % 16 || c->groups > 64 ||
         c->head_out != 2 * c->n_freq || c->up_stages < 0 || c->up_stages > 4) {
         mio::set_error("miocodec: unsupported hyper-parameters (head_dim must be 64, window <= 65)");
         return fail(MIO_ERR_UNSUPPORTED);

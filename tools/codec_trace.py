@@ -23,6 +23,27 @@ if len(sys.argv) > 2 and sys.argv[1] == "--report":
         nm = r["Kernel_Name"][:70]
         print(f"{d:9.1f} us  grid {g:>14}  wg {r.get('Workgroup_Size_X', r.get('Workgroup_Size', '?'))}  {nm}")
     print(f"total {tot / 1e3:.3f} ms over {len(rows) - n} kernels")
+    # wall (first start -> last end of the second decode), gaps between kernels, totals per kind
+    # the second decode: everything after the last host copy (the codes upload)
+    last_copy = max(i for i, r in enumerate(rows) if "copyBuffer" in r["Kernel_Name"])
+    sec = [r for r in rows[last_copy + 1:]]
+    wall = (int(sec[-1]["End_Timestamp"]) - int(sec[0]["Start_Timestamp"])) / 1e3
+    gaps = [(int(b["Start_Timestamp"]) - int(a["End_Timestamp"])) / 1e3 for a, b in zip(sec, sec[1:])]
+    print(f"wall {wall / 1e3:.3f} ms, gaps {sum(gaps) / 1e3:.3f} ms (median {sorted(gaps)[len(gaps) // 2]:.2f} us)")
+    kinds = {}
+    for r in sec:
+        nm = r["Kernel_Name"].replace("void ", "").replace("(anonymous namespace)::", "")
+        k = nm.split("(")[0].split("<")[0].split("::")[-1]
+        if nm.startswith("_ZN"):
+            k = nm[nm.index("N_1") + 4:][:24]
+        if "gemm_f32_kernel" in nm:
+            k = "gemm_f32_kernel" + nm[nm.index("<"):nm.index(">") + 1]
+        d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+        c = kinds.setdefault(k, [0, 0.0])
+        c[0] += 1
+        c[1] += d
+    for k, (cnt, d) in sorted(kinds.items(), key=lambda x: -x[1][1]):
+        print(f"  {k:40s} {cnt:4d} x  {d:8.1f} us")
     sys.exit(0)
 
 import numpy as np  # noqa: E402
