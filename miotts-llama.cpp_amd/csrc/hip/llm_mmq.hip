@@ -28,6 +28,7 @@
 #include "llm_mmq.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <mutex>
 #include <utility>
 #include <vector>
@@ -218,6 +219,51 @@ __device__ v16f slot_kq(const QMat &W, int row, int k, const int8_t *aq, const f
 // activation / scale loads are all issued before the first MFMA (one memory round trip, not
 // eight); longer K goes four slots at a time (register budget). Same arithmetic and order
 // either way.
+// One-pass Q8_0 slot (K <= 2048) in registers: the loads are issued by q80_load before the
+// tile's activation-scale staging and its barrier (one memory round trip per workgroup, not
+// two), q80_sum runs after it.
+struct Q80Regs {
+    v4i w[8], a[8];
+    float dw[8];
+};
+__device__ __forceinline__ void q80_load(const QMat &W, int row, int k, const int8_t *aq, Q80Regs &q) {
+    const int h = (threadIdx.x & 63) >> 5;
+    const int nb = W.k >> 5;
+    const int8_t *qrow = (const int8_t *)W.p0 + (size_t)row * W.k;
+    const uint16_t *drow = (const uint16_t *)W.p1 + (size_t)row * nb;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int b = min(8 * k + i, nb - 1);  // clamped: every load in flight at once
+        q.w[i] = *reinterpret_cast<const v4i *>(qrow + (size_t)b * 32 + 16 * h);
+        q.a[i] = act16(aq, b * 32 + 16 * h);
+        q.dw[i] = h2f(drow[b]);
+    }
+}
+__device__ __forceinline__ v16f q80_sum(const Q80Regs &q, int nb, int k, const float *da_lds) {
+    const int lane = threadIdx.x & 63;
+    Tree<3> inner;
+    auto slot1 = [&]<int i>() {
+        const int b = 8 * k + i;
+        v16f v = {};
+        if (b < nb) {  // wave-uniform: the MFMA runs with the full EXEC
+            const v16i c = __builtin_amdgcn_mfma_i32_32x32x32_i8(q.a[i], q.w[i], v16i{}, 0, 0, 0);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) v[r] = (float)c[r] * (q.dw[i] * da_lds[b * TT + tok_of(lane, r)]);
+        }
+        const v16f acc = v16f{} + v;
+        inner.template push<i>(acc);
+    };
+    slot1.template operator()<0>();
+    slot1.template operator()<1>();
+    slot1.template operator()<2>();
+    slot1.template operator()<3>();
+    slot1.template operator()<4>();
+    slot1.template operator()<5>();
+    slot1.template operator()<6>();
+    slot1.template operator()<7>();
+    return inner.result;
+}
+
 __device__ v16f slot_q80(const QMat &W, int row, int k, const int8_t *aq, const float *da_lds) {
     const int lane = threadIdx.x & 63, h = lane >> 5;
     const int nb = W.k >> 5, NP = (nb + 63) / 64;
@@ -225,35 +271,9 @@ __device__ v16f slot_q80(const QMat &W, int row, int k, const int8_t *aq, const 
     const uint16_t *drow = (const uint16_t *)W.p1 + (size_t)row * nb;
     Tree<3> inner;
     if (NP == 1) {
-        v4i w[8], a[8];
-        float dw[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const int b = min(8 * k + i, nb - 1);  // clamped: every load in flight at once
-            w[i] = *reinterpret_cast<const v4i *>(qrow + (size_t)b * 32 + 16 * h);
-            a[i] = act16(aq, b * 32 + 16 * h);
-            dw[i] = h2f(drow[b]);
-        }
-        auto slot1 = [&]<int i>() {
-            const int b = 8 * k + i;
-            v16f v = {};
-            if (b < nb) {  // wave-uniform: the MFMA runs with the full EXEC
-                const v16i c = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[i], w[i], v16i{}, 0, 0, 0);
-#pragma unroll
-                for (int r = 0; r < 16; ++r) v[r] = (float)c[r] * (dw[i] * da_lds[b * TT + tok_of(lane, r)]);
-            }
-            const v16f acc = v16f{} + v;
-            inner.template push<i>(acc);
-        };
-        slot1.template operator()<0>();
-        slot1.template operator()<1>();
-        slot1.template operator()<2>();
-        slot1.template operator()<3>();
-        slot1.template operator()<4>();
-        slot1.template operator()<5>();
-        slot1.template operator()<6>();
-        slot1.template operator()<7>();
-        return inner.result;
+        Q80Regs q;
+        q80_load(W, row, k, aq, q);
+        return q80_sum(q, nb, k, da_lds);
     }
     // several passes (K > 2048): four slots at a time, each pass's loads of the four issued
     // together (two round trips per pass instead of eight); slot i still accumulates its
@@ -313,6 +333,11 @@ __device__ __forceinline__ const int8_t *stage_act(const MmqArgs &a, int t0, int
     __syncthreads();
     const int t = min(t0 + (threadIdx.x & 31), a.nt - 1);
     return reinterpret_cast<const int8_t *>(a.act + (size_t)t * ab);
+}
+// this lane's token's codes (no loads)
+__device__ __forceinline__ const int8_t *act_codes(const MmqArgs &a, int t0) {
+    const int t = min(t0 + (threadIdx.x & 31), a.nt - 1);
+    return reinterpret_cast<const int8_t *>(a.act + (size_t)t * a.act_stride);
 }
 
 // sum of the 8 waves' slot values with the decode's row_total tree (valid in wave 0): each
@@ -376,9 +401,27 @@ __global__ __launch_bounds__(MMQ_NT) void k_mmq(MmqSeg s0, MmqSeg s1, MmqSeg s2,
     // segment of this tile (uniform branch): q | k | v of the attention input, or one matrix
     auto run = [&]<int T>(const MmqSeg &sg, int ti) {
         const int row0 = ti * RT, row = min(row0 + (lane & 31), sg.w.rows - 1);
-        const int8_t *aq = stage_act<T>(a, t0, a.K, da);
         v16f y = {}, u = {};
-        all_slots<T, MODE == MMQ_SWIGLU ? 2 : 1>(sg.w, a.w_up, row, aq, da, red, y, u);
+        if (T == 8 && a.K <= 2048) {
+            // one pass: the slot's weight / code / scale loads go out before the activation
+            // scales' staging barrier (same values, same order of every float operation)
+            const int k = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+            const int8_t *aq = act_codes(a, t0);
+            Q80Regs qw, qu;
+            q80_load(sg.w, row, k, aq, qw);
+            if constexpr (MODE == MMQ_SWIGLU) q80_load(a.w_up, row, k, aq, qu);
+            stage_act<8>(a, t0, a.K, da);
+            slot_store(q80_sum(qw, sg.w.k >> 5, k, da), red);
+            if constexpr (MODE == MMQ_SWIGLU) slot_store(q80_sum(qu, a.w_up.k >> 5, k, da), red + MMQ_NT * 16);
+            __syncthreads();
+            if (k == 0) {
+                y = slot_sum(red);
+                if constexpr (MODE == MMQ_SWIGLU) u = slot_sum(red + MMQ_NT * 16);
+            }
+        } else {
+            const int8_t *aq = stage_act<T>(a, t0, a.K, da);
+            all_slots<T, MODE == MMQ_SWIGLU ? 2 : 1>(sg.w, a.w_up, row, aq, da, red, y, u);
+        }
         const int orow = row0 + (lane & 31);
         if (wave != 0 || orow >= sg.w.rows) return;
 #pragma unroll
@@ -399,6 +442,139 @@ __global__ __launch_bounds__(MMQ_NT) void k_mmq(MmqSeg s0, MmqSeg s1, MmqSeg s2,
     }
     if constexpr (T2 >= 0) {
         if (tile_id < s2.tiles) return run.template operator()<T2>(s2, tile_id);
+    }
+}
+
+// ---------------------------------------------------------------- persistent one-pass Q8_0
+// The batched decode (<= 32 tokens, one token tile) streams every weight once, so a launch is
+// bound by how many weight bytes each CU keeps in flight. k_mmq runs one 8-wave workgroup
+// per CU (its registers) and one tile per workgroup: after a tile's loads land nothing is in
+// flight until the next workgroup starts, ~1.5 TB/s. Here a workgroup stays resident and
+// walks tiles ti = blockIdx.x + j gridDim.x: the activation codes of slot k and the tile's
+// scales are loaded once; every weight register is refilled with the next tile's block right
+// after the MFMA that read it (and each scale after its multiply), so the next tile's weights
+// stream during this tile's float math, LDS reduction and epilogue. The slot partials use
+// two LDS buffers (one barrier per tile). Same per-slot arithmetic as q80_sum (bit-exact).
+struct Q80Tile {
+    const int8_t *q;     // weight codes of this lane's row (slot blocks at q + b * 32 + 16 h)
+    const uint16_t *d;   // its block scales
+    int nb;              // blocks per row
+};
+
+template <int NSEG>
+__device__ __forceinline__ Q80Tile q80_tile(const MmqSeg &s0, const MmqSeg &s1, const MmqSeg &s2, const QMat &up,
+                                            bool use_up, int ti, int &row0, int &rows, int &out_off) {
+    const MmqSeg *sg = &s0;
+    if constexpr (NSEG > 1) {
+        if (ti >= s0.tiles) {
+            ti -= s0.tiles, sg = &s1;
+            if constexpr (NSEG > 2)
+                if (ti >= s1.tiles) ti -= s1.tiles, sg = &s2;
+        }
+    }
+    const QMat &W = use_up ? up : sg->w;
+    row0 = ti * RT, rows = sg->w.rows, out_off = sg->out_off;
+    const int row = min(row0 + (int)(threadIdx.x & 31), rows - 1);
+    const int nb = W.k >> 5;
+    return Q80Tile{(const int8_t *)W.p0 + (size_t)row * W.k, (const uint16_t *)W.p1 + (size_t)row * nb, nb};
+}
+
+template <int NSEG, int MODE>
+__global__ __launch_bounds__(MMQ_NT) void k_mmq_q80p(MmqSeg s0, MmqSeg s1, MmqSeg s2, MmqArgs a) {
+    constexpr int NV = MODE == MMQ_SWIGLU ? 2 : 1;
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    float *red = reinterpret_cast<float *>(lds);   // [2 buffers][NV][8 waves][64][16]
+    float *da = red + 2 * NV * MMQ_NT * 16;         // [K / 32][32 tokens]
+    const int lane = threadIdx.x & 63, h = lane >> 5;
+    const int k = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    int tiles = s0.tiles;
+    if constexpr (NSEG > 1) tiles += s1.tiles;
+    if constexpr (NSEG > 2) tiles += s2.tiles;
+    int ti = blockIdx.x;
+    if (ti >= tiles) return;  // grid <= tiles (host), never taken
+
+    // slot k's activation codes: the same for every tile
+    const int8_t *aq = act_codes(a, 0);
+    const int nb = a.K >> 5;
+    v4i act[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) act[i] = act16(aq, min(8 * k + i, nb - 1) * 32 + 16 * h);
+    // the first tile's weights and scales
+    int row0, rows, out_off;
+    v4i w[NV][8];
+    float dw[NV][8];
+    // slot k's blocks of a tile: this lane's 16-byte pieces at (b * 32 + 16 h) from the row's
+    // codes base (b clamped), scales at b
+    auto fetch = [&](const Q80Tile &q, int v, int i) {
+        const int b = min(8 * k + i, q.nb - 1);
+        w[v][i] = *reinterpret_cast<const v4i *>(q.q + (size_t)b * 32 + 16 * h);
+        dw[v][i] = h2f(q.d[b]);
+    };
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        const Q80Tile q = q80_tile<NSEG>(s0, s1, s2, a.w_up, v == 1, ti, row0, rows, out_off);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) fetch(q, v, i);
+    }
+    stage_act<8>(a, 0, a.K, da);
+
+    for (int j = 0; ti < tiles; ti += gridDim.x, ++j) {
+        q80_tile<NSEG>(s0, s1, s2, a.w_up, false, ti, row0, rows, out_off);
+        const int tn = ti + (int)gridDim.x < tiles ? ti + (int)gridDim.x : ti;  // next tile (or a reload)
+        float *rb = red + (size_t)(j & 1) * NV * MMQ_NT * 16;
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+            int r0n, rsn, oon;
+            const Q80Tile qn = q80_tile<NSEG>(s0, s1, s2, a.w_up, v == 1, tn, r0n, rsn, oon);
+            Tree<3> inner;
+            auto slot1 = [&]<int i>() {
+                const int b = 8 * k + i;
+                v16f x = {};
+                if (b < nb) {  // wave-uniform
+                    const v16i c = __builtin_amdgcn_mfma_i32_32x32x32_i8(act[i], w[v][i], v16i{}, 0, 0, 0);
+                    const float d = dw[v][i];
+                    fetch(qn, v, i);  // refill: the next tile's block i streams from here on
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) x[r] = (float)c[r] * (d * da[b * TT + tok_of(lane, r)]);
+                } else {
+                    fetch(qn, v, i);
+                }
+                const v16f acc = v16f{} + x;
+                inner.template push<i>(acc);
+                // one slot at a time: hoisting the next slots' MFMAs (and keeping their results
+                // live) spilled the refill registers
+                __builtin_amdgcn_sched_barrier(0);
+            };
+            slot1.template operator()<0>();
+            slot1.template operator()<1>();
+            slot1.template operator()<2>();
+            slot1.template operator()<3>();
+            slot1.template operator()<4>();
+            slot1.template operator()<5>();
+            slot1.template operator()<6>();
+            slot1.template operator()<7>();
+            slot_store(inner.result, rb + (size_t)v * MMQ_NT * 16);
+        }
+        __syncthreads();  // slot partials of this tile visible; the other buffer is free again
+        // epilogue on every wave: wave k sums the 8 slots (row_total's tree, as slot_sum) of
+        // accumulator registers r = 2k, 2k + 1 and stores them
+        const int orow = row0 + (lane & 31);
+#pragma unroll
+        for (int rr = 0; rr < 2; ++rr) {
+            const int r = 2 * k + rr, t = tok_of(lane, r);
+            auto total = [&](const float *src) {
+                float sl[8];
+#pragma unroll
+                for (int q = 0; q < 8; ++q) sl[q] = src[((size_t)q * 64 + lane) * 16 + r];
+                return ((sl[0] + sl[1]) + (sl[2] + sl[3])) + ((sl[4] + sl[5]) + (sl[6] + sl[7]));
+            };
+            const float y = total(rb);
+            if (orow >= rows || t >= a.nt) continue;
+            float *o = a.out + (size_t)t * a.ld + out_off + orow;
+            if constexpr (MODE == MMQ_STORE) *o = y;
+            else if constexpr (MODE == MMQ_RESID) *o = y + *o;
+            else *o = silu_f(y) * total(rb + MMQ_NT * 16);
+        }
     }
 }
 
@@ -426,10 +602,40 @@ static void allow_lds_mmq(const void *kern) {
 int mmq_tiles(int rows) { return (rows + RT - 1) / RT; }
 
 // types: {T0, T1, T2} (-1 = segment unused); mode MMQ_*.
+// MIO_MMQ_PERSIST=1: k_mmq_q80p for the one-pass Q8_0 launches of <= 32 tokens. Off by
+// default: measured slower at 8 streams of the 2.6B Q8_0 (3.17 vs 2.99 ms per step with q|k|v
+// on the matrix cores, 3.54 vs 3.31 adding O and gate|up; profiles/r03_batch8_persist_ab.txt)
+static bool mmq_persist() {
+    static const bool on = getenv("MIO_MMQ_PERSIST") && getenv("MIO_MMQ_PERSIST")[0] == '1';
+    return on;
+}
+
 void launch_mmq(const MmqSeg *seg, const int *types, int nseg, int mode, const MmqArgs &a, hipStream_t s) {
     MmqSeg sg[3] = {seg[0], nseg > 1 ? seg[1] : MmqSeg{}, nseg > 2 ? seg[2] : MmqSeg{}};
     int tiles = 0;
     for (int i = 0; i < nseg; ++i) tiles += sg[i].tiles;
+    bool q80 = true;
+    for (int i = 0; i < nseg; ++i) q80 = q80 && types[i] == 8;
+    if (mmq_persist() && q80 && a.nt <= TT && a.K <= 2048) {
+        static int n_cu = [] {
+            int dev = 0, n = 0;
+            hipGetDevice(&dev);
+            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+            return n > 0 ? n : 256;
+        }();
+        const int NV = mode == MMQ_SWIGLU ? 2 : 1;
+        const size_t lds = (size_t)2 * NV * MMQ_NT * 16 * sizeof(float) + (size_t)(a.K / 32) * TT * sizeof(float);
+        const dim3 grid(std::min(tiles, n_cu));
+        auto launch = [&](auto kern) {
+            if (lds > 64 * 1024) allow_lds_mmq(reinterpret_cast<const void *>(kern));
+            hipLaunchKernelGGL(kern, grid, dim3(MMQ_NT), lds, s, sg[0], sg[1], sg[2], a);
+        };
+        if (nseg == 3) launch(k_mmq_q80p<3, MMQ_STORE>);
+        else if (mode == MMQ_STORE) launch(k_mmq_q80p<1, MMQ_STORE>);
+        else if (mode == MMQ_RESID) launch(k_mmq_q80p<1, MMQ_RESID>);
+        else launch(k_mmq_q80p<1, MMQ_SWIGLU>);
+        return;
+    }
     const dim3 grid(tiles, (a.nt + TT - 1) / TT);
     size_t lds = 0;
     for (int i = 0; i < nseg; ++i) lds = std::max(lds, mmq_lds(types[i], a.K, mode));
