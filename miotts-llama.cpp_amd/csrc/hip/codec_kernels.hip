@@ -744,6 +744,87 @@ __global__ __launch_bounds__(1024) void gn_final_kernel(const double *part, int 
     }
 }
 
+// GroupNorm + SiLU in ONE launch: one 1024-thread workgroup per group (its L x cpg values,
+// 4 channels per float4), three passes over them — the double sum and the mean, the double
+// sum of fl(fl(x - mean)^2) and rstd (ggml's two-pass formula), then the f16 conv operand —
+// the second and third re-reading the group from L2. Replaces the sliced five-launch path
+// (partials, final, partials, final, apply) when cpg % 4 == 0: the re-decodes of the
+// streaming path are launch-bound, and their GroupNorms were 60 of ~220 launches.
+__device__ __forceinline__ double block_sum_f64_1024(double v, double *red) {
+    v = wave_sum_f64(v);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0) red[wave] = v;
+    __syncthreads();
+    double t = 0.0;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) t += red[w];
+    __syncthreads();  // red is reused by the next reduction
+    return t;
+}
+
+__global__ __launch_bounds__(1024) void gn_fused_kernel(const float *x, int L, int C, int cpg, int qsh, float eps,
+                                                        const float *gamma, const float *beta, _Float16 *xa) {
+    __shared__ double red[16];
+    constexpr int U = 8;  // quads in flight per thread
+    const int g = blockIdx.x, tid = threadIdx.x;
+    const int qm = (1 << qsh) - 1;             // quads per row - 1 (cpg / 4 is a power of two)
+    const int nq = L << qsh;                   // quads of the group
+    const long n = (long)L * cpg;
+    const float *xg = x + (long)g * cpg;
+    auto at = [&](int e) { return (long)(e >> qsh) * C + 4 * (e & qm); };
+    // pass 1: mean
+    double s = 0.0;
+    for (int base = 0; base < nq; base += 1024 * U) {
+        float4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = *reinterpret_cast<const float4 *>(xg + at(min(base + tid + 1024 * u, nq - 1)));
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (base + tid + 1024 * u < nq) s += ((((double)v[u].x + (double)v[u].y) + (double)v[u].z) + (double)v[u].w);
+    }
+    const float mean = (float)(block_sum_f64_1024(s, red) / (double)n);
+    // pass 2: rstd
+    double s2 = 0.0;
+    for (int base = 0; base < nq; base += 1024 * U) {
+        float4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = *reinterpret_cast<const float4 *>(xg + at(min(base + tid + 1024 * u, nq - 1)));
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (base + tid + 1024 * u < nq) {
+                const float dx = v[u].x - mean, dy = v[u].y - mean, dz = v[u].z - mean, dw = v[u].w - mean;
+                s2 += ((((double)(dx * dx) + (double)(dy * dy)) + (double)(dz * dz)) + (double)(dw * dw));
+            }
+    }
+    const float variance = (float)(block_sum_f64_1024(s2, red) / (double)n);
+    const float rstd = 1.0f / sqrtf(variance + eps);
+    // pass 3: f16(silu((x - mean) * rstd * gamma + beta)), the op order of gn_apply_kernel
+    for (int base = 0; base < nq; base += 1024 * U) {
+        float4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = *reinterpret_cast<const float4 *>(xg + at(min(base + tid + 1024 * u, nq - 1)));
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int e = base + tid + 1024 * u;
+            if (e >= nq) continue;
+            const int c = g * cpg + 4 * (e & qm);
+            const float t[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+            _Float16 o[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                float y = t[q] - mean;
+                y = y * rstd;
+                y = y * gamma[c + q];
+                y = y + beta[c + q];
+                o[q] = (_Float16)silu_f(y);
+            }
+            uint2 pk;
+            __builtin_memcpy(&pk, o, 8);
+            *reinterpret_cast<uint2 *>(xa + (long)(e >> qsh) * C + c) = pk;
+        }
+    }
+}
+
 // xa[l][c] = f16(silu((x - mean) * rstd * gamma + beta)), 8 channels per thread.
 __global__ __launch_bounds__(256) void gn_apply_kernel(const float *x, int L, int C, int G, int cpg,
                                                        const float2 *stat, const float *gamma,
@@ -1008,6 +1089,15 @@ void launch_rownorm(const float *x, float *y, int M, int D, float eps, int mode,
 void launch_groupnorm_apply(const float *x, int L, int C, int G, float eps, const float *gamma,
                             const float *beta, GnScratch gs, _Float16 *xa, hipStream_t s) {
     const int cpg = C / G;
+    // one launch when the group is whole float4 quads (cpg = 4, 8, 16, 32, 64: cpg | 64);
+    // MIO_GN_SLICED=1 keeps the sliced five-launch path (A/B)
+    static const bool sliced = getenv("MIO_GN_SLICED") && getenv("MIO_GN_SLICED")[0] == '1';
+    if (!sliced && cpg % 4 == 0 && (cpg & (cpg - 1)) == 0 && (long)L * (cpg / 4) < (1L << 30)) {
+        int qsh = 0;
+        while ((4 << qsh) < cpg) ++qsh;
+        hipLaunchKernelGGL(gn_fused_kernel, dim3(G), dim3(1024), 0, s, x, L, C, cpg, qsh, eps, gamma, beta, xa);
+        return;
+    }
     int rows = 4;
     if ((L + rows - 1) / rows > GN_PMAX) rows = (L + GN_PMAX - 1) / GN_PMAX;
     const int P = (L + rows - 1) / rows;
