@@ -19,7 +19,7 @@ import sys
 from collections import defaultdict
 
 N_SIMD = 256 * 4
-CODEC = ("gemm_f32", "gemm_x3", "conv_f16", "band_attention", "rownorm", "gn_partial", "gn_final", "gn_apply", "cond_gemv",
+CODEC = ("gemm_f32", "gemm_x3", "conv_f16", "band_attention", "rownorm", "gn_partial", "gn_final", "gn_apply", "gn_fused", "cond_gemv",
          "embed_kernel", "istft_fused")
 
 
