@@ -103,11 +103,155 @@ __device__ __forceinline__ void load_first_b(const QMat W0, const QMat W1, int l
     load_rows<T, NP, NM>(W0, W1, lo + CfgB<NP, NM>::RU, hi, B, split);
 }
 
+// ------------------------------------------------------------------ transposed row totals
+// The decode's row_total is a balanced tree over the wave's lanes by lane bit 0, 1, ..., 5
+// (sum8_f's row_shr 1/2/4 prefix, then row_shr 8 and row_bcast 15/31; K-quants: bits 3..5 over
+// the superblock lanes 8k+7, their integer sums being exact). A multi-token group has N such
+// totals (token x row x matrix) per lane; reducing each on its own costs N full trees plus N
+// wave-uniform epilogues. Here the N trees run together as a reduce-scatter: at lane bit b the
+// lanes with the bit clear keep the lower half of their values and add the partner's copy of
+// it, the others the upper half, so every level halves the values per lane. Every value still
+// sums the same two subtrees at every level (float addition is commutative), so each total is
+// bitwise the decode's; at the end each lane holds its own totals and the epilogue runs once
+// per (row, token) on the lane that owns it instead of once per value on the whole wave.
+constexpr int ROW_SHL4 = 0x104, ROW_SHL8 = 0x108;
+// v(l) + v(l ^ 2^B) (every lane)
+template <int B>
+__device__ __forceinline__ float xpair_sum(float v) {
+    const int lane = threadIdx.x & 63;
+    if constexpr (B == 0) return v + dpp_f<0xB1>(v);
+    else if constexpr (B == 1) return v + dpp_f<0x4E>(v);
+    else if constexpr (B == 2 || B == 3) {
+        const float up = dpp_f<B == 2 ? ROW_SHL4 : ROW_SHL8>(v);  // lane l + 2^B
+        const float dn = dpp_f<B == 2 ? ROW_SHR4 : ROW_SHR8>(v);  // lane l - 2^B
+        return v + (((lane >> B) & 1) ? dn : up);
+    } else {
+        return v + xor_lane<(1 << B)>(v);
+    }
+}
+// one scatter level at lane bit B: lanes with the bit clear return a(l) + a(l ^ 2^B), the
+// others b(l) + b(l ^ 2^B)
+template <int B>
+__device__ __forceinline__ float xpair_scatter(float a, float b) {
+    const int lane = threadIdx.x & 63;
+    if constexpr (B == 4 || B == 5) {
+        // the permlane swap exchanges a's upper lanes with b's lower ones: afterwards each lane
+        // holds its own kept value in one register and the partner's copy in the other
+        const auto r = B == 4 ? __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b), false, false)
+                              : __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+        return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+    } else if constexpr (B == 0 || B == 1) {
+        const float sa = a + dpp_f<B == 0 ? 0xB1 : 0x4E>(a), sb = b + dpp_f<B == 0 ? 0xB1 : 0x4E>(b);
+        return ((lane >> B) & 1) ? sb : sa;
+    } else {
+        const float sa = a + dpp_f<B == 2 ? ROW_SHL4 : ROW_SHL8>(a);
+        const float sb = b + dpp_f<B == 2 ? ROW_SHR4 : ROW_SHR8>(b);
+        return ((lane >> B) & 1) ? sb : sa;
+    }
+}
+// Levels B..5 over the first N entries of v: scatter while more than R values remain, then
+// all-reduce; returns nothing, v[0 .. max(R, N >> (6 - B))) hold the lane's totals.
+template <int B, int N, int R, int NV>
+__device__ __forceinline__ void xreduce(float (&v)[NV]) {
+    if constexpr (B < 6) {
+        if constexpr (N > R) {
+            constexpr int H = N / 2;
+#pragma unroll
+            for (int i = 0; i < H; ++i) v[i] = xpair_scatter<B>(v[i], v[i + H]);
+            xreduce<B + 1, H, R>(v);
+        } else {
+#pragma unroll
+            for (int i = 0; i < N; ++i) v[i] = xpair_sum<B>(v[i]);
+            xreduce<B + 1, N, R>(v);
+        }
+    }
+}
+// tokens per reduce-scatter group (the dot loop still goes TT tokens at a time)
+template <int NP>
+struct XRedCfg {
+    static constexpr int TT = NP == 1 ? 4 : (NP == 3 ? 2 : 1);
+    static constexpr int TB = NP == 1 ? 8 : (NP == 3 ? 4 : 8);
+};
+#ifndef MIO_BT_XRED
+#define MIO_BT_XRED 1
+#endif
+
+// epi(row, t, dot0, dot1): once per (row, token); with MIO_BT_XRED on the lane that holds
+// the totals (lane-varying values), else wave-uniform values on every lane
+template <int T, int NP, int NM, class Epi>
+__device__ __forceinline__ void stream_rows_bx(const QMat W0, const QMat W1, int lo, int hi,
+                                               Frag (&A)[CfgB<NP, NM>::U], Frag (&B)[CfgB<NP, NM>::U], char *smem,
+                                               int nt, Epi &&epi, int split = INT_MAX) {
+    constexpr int RU = CfgB<NP, NM>::RU, U = CfgB<NP, NM>::U;
+    constexpr int TT = XRedCfg<NP>::TT, TB = XRedCfg<NP>::TB;
+    constexpr int N = TB * RU * NM;             // totals per group: index ((t * RU + ri) * NM + m)
+    constexpr int LB = T == 8 ? 0 : 3;          // first tree level (K-quants: lanes 8k+7)
+    constexpr int NF = N >> (6 - LB) > NM ? N >> (6 - LB) : NM;  // totals per lane at the end
+    constexpr int SL = __builtin_ctz(N / NF);   // scatter levels
+    const int K = W0.k;
+    const int lane = threadIdx.x & 63;
+    if (hi <= lo) return;
+    // the lane's first total after the scatter (level k at lane bit LB + k halves the index
+    // range), and whether it is the replica that runs the epilogue
+    int jb = 0;
+#pragma unroll
+    for (int k = 0; k < SL; ++k) jb += ((lane >> (LB + k)) & 1) * (N >> (k + 1));
+    const bool owner = (LB == 0 || (lane & 7) == 7) && (lane >> (LB + SL)) == 0;
+    auto consume = [&](const Frag (&F)[U], int r) {
+        const int nr = min(RU, hi - r);
+        for (int tb = 0; tb < nt; tb += TB) {
+            float acc[N];
+#pragma unroll
+            for (int i = 0; i < N; ++i) acc[i] = 0.0f;
+#pragma unroll
+            for (int t0 = 0; t0 < TB; t0 += TT) {
+                if (tb + t0 < nt) {
+#pragma unroll
+                    for (int p = 0; p < NP; ++p) {
+                        ALane al[TT];
+#pragma unroll
+                        for (int j = 0; j < TT; ++j)
+                            al[j] = load_alane<T>(carve_t(smem, K, min(tb + t0 + j, nt - 1)).a, K, p);
+#pragma unroll
+                        for (int ri = 0; ri < RU; ++ri) {
+                            if (ri < nr) {
+#pragma unroll
+                                for (int m = 0; m < NM; ++m)
+#pragma unroll
+                                    for (int j = 0; j < TT; ++j)
+                                        acc[((t0 + j) * RU + ri) * NM + m] += dot_frag<T>(F[(ri * NM + m) * NP + p], al[j], K, p);
+                            }
+                        }
+                    }
+                }
+            }
+            xreduce<LB, N, NF>(acc);
+            if (owner) {
+#pragma unroll
+                for (int i = 0; i < NF / NM; ++i) {
+                    const int q = jb / NM + i, t = tb + q / RU, ri = q % RU;
+                    if (t < nt && ri < nr) epi(r + ri, t, acc[i * NM], acc[i * NM + NM - 1]);
+                }
+            }
+        }
+    };
+    for (int r = lo;;) {
+        consume(A, r);
+        r += RU;
+        if (r >= hi) break;
+        load_rows<T, NP, NM>(W0, W1, r + RU, hi, A, split);
+        consume(B, r);
+        r += RU;
+        if (r >= hi) break;
+        load_rows<T, NP, NM>(W0, W1, r + RU, hi, B, split);
+    }
+}
+
 // epi(row, t, dot0, dot1): wave-uniform values, once per (row, token)
 template <int T, int NP, int NM, class Epi>
-__device__ __forceinline__ void stream_rows_b(const QMat W0, const QMat W1, int lo, int hi,
-                                              Frag (&A)[CfgB<NP, NM>::U], Frag (&B)[CfgB<NP, NM>::U], char *smem,
-                                              int nt, Epi &&epi, int split = INT_MAX) {
+__device__ __forceinline__ void stream_rows_bu(const QMat W0, const QMat W1, int lo, int hi,
+                                               Frag (&A)[CfgB<NP, NM>::U], Frag (&B)[CfgB<NP, NM>::U], char *smem,
+                                               int nt, Epi &&epi, int split = INT_MAX) {
     constexpr int RU = CfgB<NP, NM>::RU, U = CfgB<NP, NM>::U;
     const int K = W0.k;
     if (hi <= lo) return;
@@ -147,7 +291,7 @@ __device__ __forceinline__ void stream_rows_b(const QMat W0, const QMat W1, int 
                         if (ri < nr) {
                             const float v0 = row_total<T>(acc[j][ri * NM]);
                             const float v1 = NM == 2 ? row_total<T>(acc[j][ri * NM + NM - 1]) : 0.0f;
-                            epi(r + ri, t0 + j, v0, v1);
+                            if ((threadIdx.x & 63) == 0) epi(r + ri, t0 + j, v0, v1);
                         }
                     }
                 }
@@ -164,6 +308,18 @@ __device__ __forceinline__ void stream_rows_b(const QMat W0, const QMat W1, int 
         if (r >= hi) break;
         load_rows<T, NP, NM>(W0, W1, r + RU, hi, B, split);
     }
+}
+
+// The multi-token streaming rows: transposed totals (MIO_BT_XRED, default) or one wave-wide
+// tree per total (A/B build). Either way epi runs once per (row, token) on one lane.
+template <int T, int NP, int NM, class Epi>
+__device__ __forceinline__ void stream_rows_b(const QMat W0, const QMat W1, int lo, int hi,
+                                              Frag (&A)[CfgB<NP, NM>::U], Frag (&B)[CfgB<NP, NM>::U], char *smem,
+                                              int nt, Epi &&epi, int split = INT_MAX) {
+    if constexpr (MIO_BT_XRED)
+        stream_rows_bx<T, NP, NM>(W0, W1, lo, hi, A, B, smem, nt, epi, split);
+    else
+        stream_rows_bu<T, NP, NM>(W0, W1, lo, hi, A, B, smem, nt, epi, split);
 }
 
 // ------------------------------------------------------------------ multi-token prologues
@@ -381,14 +537,14 @@ __global__ __launch_bounds__(MT) void k_pf_attn_in(LlmDims d, const float *norm_
         load_first_b<TQ, NP, 1>(wq, wk, lo, hi, ga, gb, o1);
         prologue_act<NP>(fq, pb.x, norm_w, K, d.eps, TQ != 8, pb.act, smem, nt);
         stream_rows_b<TQ, NP, 1>(wq, wk, lo, hi, ga, gb, smem, nt, [&](int row, int t, float v, float) {
-            if (lane == 0) pb.qkv[(size_t)t * QD + row] = v;
+            pb.qkv[(size_t)t * QD + row] = v;
         }, o1);
     } else {
         wave_range(wv.rows, lo, hi, blockIdx.x - g_qk, gridDim.x - g_qk);
         load_first_b<TV, NP, 1>(wv, wv, lo, hi, ga, gb);
         prologue_act<NP>(fq, pb.x, norm_w, K, d.eps, TQ != 8, pb.act, smem, nt);
         stream_rows_b<TV, NP, 1>(wv, wv, lo, hi, ga, gb, smem, nt, [&](int row, int t, float v, float) {
-            if (lane == 0) pb.qkv[(size_t)t * QD + o2 + row] = v;
+            pb.qkv[(size_t)t * QD + o2 + row] = v;
         });
     }
 }
@@ -545,7 +701,7 @@ __global__ __launch_bounds__(MT) void k_pf_attn_out(LlmDims d, QMat wo, PrefillB
     prologue_copy(pb.act, K, smem, nt);
     stream_rows_b<T, NP, 1>(wo, wo, lo, hi, ga, gb, smem, nt, [&](int row, int t, float v, float) {
         const float r = res[t * rpw + row - lo];
-        if ((threadIdx.x & 63) == 0) pb.x[(size_t)t * E + row] = v + r;
+        pb.x[(size_t)t * E + row] = v + r;
     });
 }
 
@@ -560,7 +716,7 @@ __global__ __launch_bounds__(MT) void k_pf_ffn_in(LlmDims d, const float *norm_w
     load_first_b<T, NP, 2>(gate, up, lo, hi, ga, gb);
     prologue_act<NP>(fq, pb.x, norm_w, K, d.eps, T != 8, pb.act, smem, nt);
     stream_rows_b<T, NP, 2>(gate, up, lo, hi, ga, gb, smem, nt, [&](int row, int t, float g, float u) {
-        if ((threadIdx.x & 63) == 0) pb.h[(size_t)t * d.n_ff + row] = silu_f(g) * u;
+        pb.h[(size_t)t * d.n_ff + row] = silu_f(g) * u;
     });
 }
 
@@ -579,7 +735,7 @@ __global__ __launch_bounds__(MT) void k_pf_ffn_down(LlmDims d, QMat down, Prefil
     prologue_act<NP>(fq, pb.h, nullptr, K, d.eps, T != 8, pb.act, smem, nt);
     stream_rows_b<T, NP, 1>(down, down, lo, hi, ga, gb, smem, nt, [&](int row, int t, float v, float) {
         const float r = res[t * rpw + row - lo];
-        if ((threadIdx.x & 63) == 0) pb.x[(size_t)t * E + row] = v + r;
+        pb.x[(size_t)t * E + row] = v + r;
     });
 }
 
@@ -609,7 +765,7 @@ __global__ __launch_bounds__(MT) void k_bt_lm_head(LlmDims d, const float *norm_
     prologue_copy(pb.act, K, smem, nt);
     float *vals = reinterpret_cast<float *>(smem + pf_lds_bytes(K, nt, 0)) + (size_t)wave * nt * 128;
     stream_rows_b<T, NP, 1>(lm, lm, lo, hi, ga, gb, smem, nt, [&](int row, int t, float v, float) {
-        if (lane == 0) vals[t * 128 + row - lo] = v;
+        vals[t * 128 + row - lo] = v;
     });
     lds_barrier();
     for (int t = 0; t < nt; ++t) {
