@@ -328,7 +328,7 @@ __device__ __forceinline__ void stream_rows_b(const QMat W0, const QMat W1, int 
 // itself: rmsnorm_quant / plain_quant / merge_attention, so the values are the decode's bit
 // for bit) into pb.act, and each matvec workgroup copies the records into LDS with all its
 // loads in flight (one memory latency for all tokens).
-__device__ void prologue_copy(const char *act, int K, char *smem, int nt) {
+__device__ __forceinline__ void prologue_copy(const char *act, int K, char *smem, int nt) {
     constexpr int UN = 8;
     const int n16 = (int)(act_bytes(K) * nt / 16);
     const uint4 *src = reinterpret_cast<const uint4 *>(act);
@@ -371,7 +371,7 @@ __device__ __forceinline__ void wq_val4(const float *x, const float *norm_w, flo
 }
 
 template <int XV>
-__device__ void wave_quant(const float *x, const float *norm_w, int K, float eps, bool kq, const ActL &a) {
+__device__ __forceinline__ void wave_quant(const float *x, const float *norm_w, int K, float eps, bool kq, const ActL &a) {
     const int lane = threadIdx.x & 63;
     float scale = 1.0f;
     if (norm_w) {
@@ -417,7 +417,7 @@ __device__ void wave_quant(const float *x, const float *norm_w, int K, float eps
 // The prologue of a matvec launch over nt tokens: quantize in-launch (fq, wave_quant) or copy
 // the records k_bt_quant wrote.
 template <int XV>
-__device__ void prologue_act(int fq, const float *src, const float *norm_w, int K, float eps, bool kq,
+__device__ __forceinline__ void prologue_act(int fq, const float *src, const float *norm_w, int K, float eps, bool kq,
                              const char *act, char *smem, int nt) {
     if (!fq) {
         prologue_copy(act, K, smem, nt);

@@ -1,7 +1,7 @@
 set -e
 # transposed row totals in the multi-token dot4 engine: parity (batch == single, prefill ==
 # sequential) and the 8-stream step time of the 2.6B Q8_0 / 1.7B Q4_K_M
-out=gpurun_out/r04_b
+out=gpurun_out/${OUT:-r04_b}
 mkdir -p $out
 export TMPDIR=/tmp
 timeout -k 10 600 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_llm_batch_gpu.py tests/test_llm_gpu.py -k "batch or prefill or mmq" > $out/tests.txt 2>&1
