@@ -69,10 +69,14 @@ __device__ inline float *resid_lds(char *base, int K, int nt, int rpw) {
 #ifndef MIO_BT_UNITS
 #define MIO_BT_UNITS 4
 #endif
+// NG register groups in flight per wave: two (one loading while the other is dotted), or one
+// for NP = 6 (a 6-pass row is 13 KB per wave; 8 waves x one row already keep 100 KB per CU in
+// flight, and the registers go to the activation records, act_issue)
 template <int NP, int NM>
 struct CfgB {
     static constexpr int RU = NP * NM >= MIO_BT_UNITS ? 1 : MIO_BT_UNITS / (NP * NM);
     static constexpr int U = RU * NP * NM;
+    static constexpr int NG = NP >= 6 ? 1 : 2;
 };
 
 template <int T, int NP, int NM>
@@ -100,7 +104,7 @@ __device__ __forceinline__ void load_first_b(const QMat W0, const QMat W1, int l
                                              int split = INT_MAX) {
     if (hi <= lo) return;
     load_rows<T, NP, NM>(W0, W1, lo, hi, A, split);
-    load_rows<T, NP, NM>(W0, W1, lo + CfgB<NP, NM>::RU, hi, B, split);
+    if constexpr (CfgB<NP, NM>::NG == 2) load_rows<T, NP, NM>(W0, W1, lo + CfgB<NP, NM>::RU, hi, B, split);
 }
 
 // ------------------------------------------------------------------ transposed row totals
@@ -235,6 +239,15 @@ __device__ __forceinline__ void stream_rows_bx(const QMat W0, const QMat W1, int
             }
         }
     };
+    if constexpr (CfgB<NP, NM>::NG == 1) {
+        for (int r = lo;;) {
+            consume(A, r);
+            r += RU;
+            if (r >= hi) break;
+            load_rows<T, NP, NM>(W0, W1, r, hi, A, split);
+        }
+        return;
+    }
     for (int r = lo;;) {
         consume(A, r);
         r += RU;
@@ -298,6 +311,15 @@ __device__ __forceinline__ void stream_rows_bu(const QMat W0, const QMat W1, int
             }
         }
     };
+    if constexpr (CfgB<NP, NM>::NG == 1) {
+        for (int r = lo;;) {
+            consume(A, r);
+            r += RU;
+            if (r >= hi) break;
+            load_rows<T, NP, NM>(W0, W1, r, hi, A, split);
+        }
+        return;
+    }
     for (int r = lo;;) {
         consume(A, r);
         r += RU;
@@ -343,6 +365,38 @@ __device__ __forceinline__ void prologue_copy(const char *act, int K, char *smem
             if (i < n16) dst[i] = v[u];
         }
     }
+    lds_barrier();
+}
+
+// The records' loads issued AHEAD of the launch's weight loads: vmcnt retires in order, so a
+// copy issued after the first weight groups (prologue_copy) waits for all of them before its
+// LDS stores and barrier - the launch then streams weights, THEN copies, THEN dots. Issued
+// first, the copy (L2 / Infinity Cache resident) lands while the weights are still in flight.
+// CP uint4 per thread cover nt tokens when act_bytes(K) * nt <= CP * MT * 16; a larger batch
+// copies the rest after (act_store_rest).
+template <int NP>
+struct ActPre {
+    static constexpr int CP = NP == 1 ? 6 : (NP == 3 ? 10 : 14);
+    uint4 v[CP];
+};
+template <int NP>
+__device__ __forceinline__ void act_issue(const char *act, int K, int nt, ActPre<NP> &ap) {
+    const int n16 = (int)(act_bytes(K) * nt / 16);
+    const uint4 *src = reinterpret_cast<const uint4 *>(act);
+#pragma unroll
+    for (int u = 0; u < ActPre<NP>::CP; ++u) ap.v[u] = src[min((int)threadIdx.x + u * MT, n16 - 1)];
+}
+template <int NP>
+__device__ __forceinline__ void act_store(const ActPre<NP> &ap, const char *act, int K, char *smem, int nt) {
+    const int n16 = (int)(act_bytes(K) * nt / 16);
+    uint4 *dst = reinterpret_cast<uint4 *>(smem + act_base(K));
+#pragma unroll
+    for (int u = 0; u < ActPre<NP>::CP; ++u) {
+        const int i = (int)threadIdx.x + u * MT;
+        if (i < n16) dst[i] = ap.v[u];
+    }
+    const uint4 *src = reinterpret_cast<const uint4 *>(act);
+    for (int i = (int)threadIdx.x + ActPre<NP>::CP * MT; i < n16; i += MT) dst[i] = src[i];
     lds_barrier();
 }
 
@@ -694,11 +748,13 @@ __global__ __launch_bounds__(MT) void k_pf_attn_out(LlmDims d, QMat wo, PrefillB
     int lo, hi;
     wave_range(d, wo.rows, lo, hi);
     const Resid xr = load_resid_b(pb.x, E, lo, hi, nt, rpw);
+    ActPre<NP> ap;
+    act_issue<NP>(pb.act, K, nt, ap);
     Frag ga[CfgB<NP, 1>::U], gb[CfgB<NP, 1>::U];
     load_first_b<T, NP, 1>(wo, wo, lo, hi, ga, gb);
     float *res = resid_lds(smem, K, nt, rpw);
     store_resid_b(xr, res, nt, rpw);
-    prologue_copy(pb.act, K, smem, nt);
+    act_store<NP>(ap, pb.act, K, smem, nt);
     stream_rows_b<T, NP, 1>(wo, wo, lo, hi, ga, gb, smem, nt, [&](int row, int t, float v, float) {
         const float r = res[t * rpw + row - lo];
         pb.x[(size_t)t * E + row] = v + r;
@@ -712,9 +768,14 @@ __global__ __launch_bounds__(MT) void k_pf_ffn_in(LlmDims d, const float *norm_w
     const int K = d.n_embd;
     int lo, hi;
     wave_range(d, gate.rows, lo, hi);
+    ActPre<NP> ap;
+    act_issue<NP>(pb.act, K, nt, ap);  // unconditional (in bounds; unused with fq): keeps ap in registers
     Frag ga[CfgB<NP, 2>::U], gb[CfgB<NP, 2>::U];
     load_first_b<T, NP, 2>(gate, up, lo, hi, ga, gb);
-    prologue_act<NP>(fq, pb.x, norm_w, K, d.eps, T != 8, pb.act, smem, nt);
+    if (!fq)
+        act_store<NP>(ap, pb.act, K, smem, nt);
+    else
+        prologue_act<NP>(fq, pb.x, norm_w, K, d.eps, T != 8, pb.act, smem, nt);
     stream_rows_b<T, NP, 2>(gate, up, lo, hi, ga, gb, smem, nt, [&](int row, int t, float g, float u) {
         pb.h[(size_t)t * d.n_ff + row] = silu_f(g) * u;
     });
@@ -728,11 +789,16 @@ __global__ __launch_bounds__(MT) void k_pf_ffn_down(LlmDims d, QMat down, Prefil
     int lo, hi;
     wave_range(d, down.rows, lo, hi);
     const Resid rr = load_resid_b(pb.x, E, lo, hi, nt, rpw);
+    ActPre<NP> ap;
+    act_issue<NP>(pb.act, K, nt, ap);  // unconditional (in bounds; unused with fq): keeps ap in registers
     Frag ga[CfgB<NP, 1>::U], gb[CfgB<NP, 1>::U];
     load_first_b<T, NP, 1>(down, down, lo, hi, ga, gb);
     float *res = resid_lds(smem, K, nt, rpw);
     store_resid_b(rr, res, nt, rpw);
-    prologue_act<NP>(fq, pb.h, nullptr, K, d.eps, T != 8, pb.act, smem, nt);
+    if (!fq)
+        act_store<NP>(ap, pb.act, K, smem, nt);
+    else
+        prologue_act<NP>(fq, pb.h, nullptr, K, d.eps, T != 8, pb.act, smem, nt);
     stream_rows_b<T, NP, 1>(down, down, lo, hi, ga, gb, smem, nt, [&](int row, int t, float v, float) {
         const float r = res[t * rpw + row - lo];
         pb.x[(size_t)t * E + row] = v + r;
@@ -760,9 +826,11 @@ __global__ __launch_bounds__(MT) void k_bt_lm_head(LlmDims d, const float *norm_
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     int lo, hi;
     wave_range(d, lm.rows, lo, hi);
+    ActPre<NP> ap;
+    act_issue<NP>(pb.act, K, nt, ap);
     Frag ga[CfgB<NP, 1>::U], gb[CfgB<NP, 1>::U];
     load_first_b<T, NP, 1>(lm, lm, lo, hi, ga, gb);
-    prologue_copy(pb.act, K, smem, nt);
+    act_store<NP>(ap, pb.act, K, smem, nt);
     float *vals = reinterpret_cast<float *>(smem + pf_lds_bytes(K, nt, 0)) + (size_t)wave * nt * 128;
     stream_rows_b<T, NP, 1>(lm, lm, lo, hi, ga, gb, smem, nt, [&](int row, int t, float v, float) {
         vals[t * 128 + row - lo] = v;
