@@ -468,6 +468,78 @@ __device__ __forceinline__ void wave_quant(const float *x, const float *norm_w, 
     }
 }
 
+// In-launch RMSNorm + quantization with the inputs loaded AHEAD of the weights (batched
+// decode, K <= 2048, nt <= 8 tokens: wave t quantizes token t). The token row and the norm
+// weights sit in the registers wave_quant<1> reads them into (lane l, register vw: elements
+// vw * 256 + 4 l .. +3, i.e. superblock vw / Q8_0 blocks 8 vw .. 8 vw + 7), issued before the
+// first weight group, so the quantization waits only for them (in-order vmcnt) and never
+// re-reads the row; the arithmetic and order are wave_quant's, so the records equal
+// k_bt_quant's bit for bit. Saves the k_bt_quant launch in front of the matvec.
+struct XPre {
+    float4 x[MW], w[MW];
+};
+__device__ __forceinline__ void xpre_issue(const float *src, const float *norm_w, int K, int nt, XPre &xp) {
+    const int lane = threadIdx.x & 63;
+    const int t = min((int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6), nt - 1);
+    const float *x = src + (size_t)t * K;
+#pragma unroll
+    for (int vw = 0; vw < MW; ++vw) {
+        const int e = min(vw * 256 + 4 * lane, K - 4);
+        xp.x[vw] = ld4(x + e);
+        xp.w[vw] = ld4(norm_w + e);
+    }
+}
+__device__ __forceinline__ void xpre_quant(const XPre &xp, int K, float eps, bool kq, char *smem, int nt) {
+    const int lane = threadIdx.x & 63;
+    const int t = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (t < nt) {
+        const ActL a = carve_t(smem, K, t).a;
+        double tot = 0.0;
+#pragma unroll
+        for (int vw = 0; vw < MW; ++vw) {
+            const int e = vw * 256 + 4 * lane;
+            const float4 v = xp.x[vw];
+            double acc = 0.0;
+            if (e < K) {
+                acc += (double)(v.x * v.x);
+                acc += (double)(v.y * v.y);
+                acc += (double)(v.z * v.z);
+                acc += (double)(v.w * v.w);
+            }
+            tot += wave_sum_d(acc);
+        }
+        const float scale = rms_scale(tot, K, eps);
+        auto val4 = [&](int vw, float (&v)[4]) {
+            const float4 xv = xp.x[vw], w = xp.w[vw];
+            float q;
+            q = xv.x * scale, v[0] = q * w.x;
+            q = xv.y * scale, v[1] = q * w.y;
+            q = xv.z * scale, v[2] = q * w.z;
+            q = xv.w * scale, v[3] = q * w.w;
+        };
+        if (kq) {
+#pragma unroll
+            for (int b = 0; b < MW; ++b)
+                if (b < K / 256) {
+                    float v[4];
+                    val4(b, v);
+                    q8k_store(v, abs_max4(v), b, a);
+                }
+        } else {
+            const int nb = K / 32;
+#pragma unroll
+            for (int m = 0; m < MW; ++m)
+                if (8 * m < nb) {
+                    const int b = 8 * m + (lane >> 3);
+                    float v[4];
+                    val4(m, v);
+                    q80_store(v, b, b < nb, a);
+                }
+        }
+    }
+    lds_barrier();
+}
+
 // The prologue of a matvec launch over nt tokens: quantize in-launch (fq, wave_quant) or copy
 // the records k_bt_quant wrote.
 template <int XV>
@@ -577,7 +649,7 @@ __device__ inline void store_resid_b(const Resid &r, float *lds, int nt, int rpw
 }
 
 // ------------------------------------------------------------------ kernels
-template <int NP, int TQ, int TV>
+template <int NP, int TQ, int TV, int FQ = 0>
 __global__ __launch_bounds__(MT) void k_pf_attn_in(LlmDims d, const float *norm_w, QMat wq, QMat wk, QMat wv,
                                                    int g_qk, PrefillBuffers pb, int nt, int fq) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -585,18 +657,26 @@ __global__ __launch_bounds__(MT) void k_pf_attn_in(LlmDims d, const float *norm_
     const int lane = threadIdx.x & 63;
     const int o1 = wq.rows, o2 = wq.rows + wk.rows;
     Frag ga[CfgB<NP, 1>::U], gb[CfgB<NP, 1>::U];
+    XPre xp;
+    if constexpr (FQ == 2) xpre_issue(pb.x, norm_w, K, nt, xp);
+    auto prologue = [&]() {
+        if constexpr (FQ == 2)
+            xpre_quant(xp, K, d.eps, TQ != 8, smem, nt);
+        else
+            prologue_act<NP>(fq, pb.x, norm_w, K, d.eps, TQ != 8, pb.act, smem, nt);
+    };
     int lo, hi;
     if ((int)blockIdx.x < g_qk) {
         wave_range(o2, lo, hi, blockIdx.x, g_qk);
         load_first_b<TQ, NP, 1>(wq, wk, lo, hi, ga, gb, o1);
-        prologue_act<NP>(fq, pb.x, norm_w, K, d.eps, TQ != 8, pb.act, smem, nt);
+        prologue();
         stream_rows_b<TQ, NP, 1>(wq, wk, lo, hi, ga, gb, smem, nt, [&](int row, int t, float v, float) {
             pb.qkv[(size_t)t * QD + row] = v;
         }, o1);
     } else {
         wave_range(wv.rows, lo, hi, blockIdx.x - g_qk, gridDim.x - g_qk);
         load_first_b<TV, NP, 1>(wv, wv, lo, hi, ga, gb);
-        prologue_act<NP>(fq, pb.x, norm_w, K, d.eps, TQ != 8, pb.act, smem, nt);
+        prologue();
         stream_rows_b<TV, NP, 1>(wv, wv, lo, hi, ga, gb, smem, nt, [&](int row, int t, float v, float) {
             pb.qkv[(size_t)t * QD + o2 + row] = v;
         });
@@ -761,7 +841,8 @@ __global__ __launch_bounds__(MT) void k_pf_attn_out(LlmDims d, QMat wo, PrefillB
     });
 }
 
-template <int NP, int T>
+// FQ = 2: RMSNorm + quantization in the launch from inputs loaded ahead of the weights (xpre)
+template <int NP, int T, int FQ = 0>
 __global__ __launch_bounds__(MT) void k_pf_ffn_in(LlmDims d, const float *norm_w, QMat gate, QMat up,
                                                   PrefillBuffers pb, int nt, int fq) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -769,10 +850,16 @@ __global__ __launch_bounds__(MT) void k_pf_ffn_in(LlmDims d, const float *norm_w
     int lo, hi;
     wave_range(d, gate.rows, lo, hi);
     ActPre<NP> ap;
-    act_issue<NP>(pb.act, K, nt, ap);  // unconditional (in bounds; unused with fq): keeps ap in registers
+    XPre xp;
+    if constexpr (FQ == 2)
+        xpre_issue(pb.x, norm_w, K, nt, xp);
+    else
+        act_issue<NP>(pb.act, K, nt, ap);  // unconditional (in bounds; unused with fq): keeps ap in registers
     Frag ga[CfgB<NP, 2>::U], gb[CfgB<NP, 2>::U];
     load_first_b<T, NP, 2>(gate, up, lo, hi, ga, gb);
-    if (!fq)
+    if constexpr (FQ == 2)
+        xpre_quant(xp, K, d.eps, T != 8, smem, nt);
+    else if (!fq)
         act_store<NP>(ap, pb.act, K, smem, nt);
     else
         prologue_act<NP>(fq, pb.x, norm_w, K, d.eps, T != 8, pb.act, smem, nt);
@@ -1062,6 +1149,15 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
     // tokens' inputs twice)
     static const bool fq_env = getenv("MIO_FUSED_QUANT") && getenv("MIO_FUSED_QUANT")[0] == '1';
     const int fq = (!mmq && fq_env && nt <= 16) ? 1 : 0;
+    // MIO_BT_FQ (bits: 1 attn_in, 2 ffn_in; default 1): launches of <= 8 tokens over K <= 2048
+    // RMSNorm + quantize in the launch from inputs loaded ahead of the weights (xpre), on the
+    // dot4 engine, instead of behind a k_bt_quant launch (and, for q|k|v, on the matrix cores).
+    // 8-stream steps (graph; profiles/r04_fq_ab.txt): 2.6B Q8_0 2.354 ms with attn_in only,
+    // 2.362 both, 2.488 neither or ffn_in only; 1.7B Q4_K_M 1.837 / 1.881 / 1.843 / 1.891
+    static const int fq2_env = getenv("MIO_BT_FQ") ? atoi(getenv("MIO_BT_FQ")) : 1;
+    auto fq2 = [&](int kind) {
+        return !fq && !mmq && nt <= MW && pick_np(d.n_embd) == 1 && ((fq2_env >> kind) & 1);
+    };
     // MIO_BT_ATT=0: the batched decode step uses k_pf_rope + k_pf_attention (A/B)
     static const bool bt_att = !(getenv("MIO_BT_ATT") && getenv("MIO_BT_ATT")[0] == '0');
     decode = decode && bt_att;
@@ -1090,8 +1186,10 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
             launch_mmq(&so, &L.out_proj.type, 1, MMQ_RESID, MmqArgs{pb.act, act_bytes(n), n, nt, pb.x, n, {}}, s);
         } else {
             _Float16 *kc = kcache + il * layer_kv, *vc = vcache + il * layer_kv;
-            if (!fq || use_mmq(0, L.wq.type)) launch_quant(d, 0, pb.x, d.n_embd, L.attn_norm, L.wq.type != 8, pb, nt, s);
-            if (use_mmq(0, L.wq.type)) {
+            const bool fa = fq2(0);
+            if (!fa && (!fq || use_mmq(0, L.wq.type)))
+                launch_quant(d, 0, pb.x, d.n_embd, L.attn_norm, L.wq.type != 8, pb, nt, s);
+            if (!fa && use_mmq(0, L.wq.type)) {
                 const MmqSeg sg[3] = {{L.wq, mmq_tiles(L.wq.rows), 0}, {L.wk, mmq_tiles(L.wk.rows), L.wq.rows},
                                       {L.wv, mmq_tiles(L.wv.rows), L.wq.rows + L.wk.rows}};
                 const int ty[3] = {L.wq.type, L.wk.type, L.wv.type};
@@ -1103,6 +1201,14 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
                     const size_t lds = pf_lds_bytes(d.n_embd, n, 0);
                     dispatch_nt(d.n_embd, L.wq.type, [&]<int NP, int TQ>() {
                         auto go = [&]<int TV>() {
+                            if constexpr (NP == 1) {
+                                if (fa) {
+                                    allow_lds(k_pf_attn_in<NP, TQ, TV, 2>);
+                                    hipLaunchKernelGGL((k_pf_attn_in<NP, TQ, TV, 2>), dim3(GW), dim3(MT), lds, s, d,
+                                                       L.attn_norm, L.wq, L.wk, L.wv, g_qk, q, n, fq);
+                                    return;
+                                }
+                            }
                             allow_lds(k_pf_attn_in<NP, TQ, TV>);
                             hipLaunchKernelGGL((k_pf_attn_in<NP, TQ, TV>), dim3(GW), dim3(MT), lds, s, d, L.attn_norm,
                                                L.wq, L.wk, L.wv, g_qk, q, n, fq);
@@ -1156,8 +1262,10 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
                 });
             }
         }
-        if (!fq || use_mmq(2, L.gate.type)) launch_quant(d, 0, pb.x, d.n_embd, L.ffn_norm, L.gate.type != 8, pb, nt, s);
-        if (use_mmq(2, L.gate.type)) {
+        const bool ff = fq2(1);
+        if (!ff && (!fq || use_mmq(2, L.gate.type)))
+            launch_quant(d, 0, pb.x, d.n_embd, L.ffn_norm, L.gate.type != 8, pb, nt, s);
+        if (!ff && use_mmq(2, L.gate.type)) {
             const MmqSeg sg{L.gate, mmq_tiles(L.gate.rows), 0};
             launch_mmq(&sg, &L.gate.type, 1, MMQ_SWIGLU,
                        MmqArgs{pb.act, act_bytes(d.n_embd), d.n_embd, nt, pb.h, d.n_ff, L.up}, s);
@@ -1165,6 +1273,14 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
             const int grid = matvec_grid(d, L.gate.rows);
             over_tokens(d.n_embd, 0, [&](int, int n, const PrefillBuffers &q) {
                 dispatch_nt(d.n_embd, L.gate.type, [&]<int NP, int T>() {
+                    if constexpr (NP == 1) {
+                        if (ff) {
+                            allow_lds(k_pf_ffn_in<NP, T, 2>);
+                            hipLaunchKernelGGL((k_pf_ffn_in<NP, T, 2>), dim3(grid), dim3(MT), pf_lds_bytes(d.n_embd, n, 0),
+                                               s, d, L.ffn_norm, L.gate, L.up, q, n, fq);
+                            return;
+                        }
+                    }
                     allow_lds(k_pf_ffn_in<NP, T>);
                     hipLaunchKernelGGL((k_pf_ffn_in<NP, T>), dim3(grid), dim3(MT), pf_lds_bytes(d.n_embd, n, 0), s, d,
                                        L.ffn_norm, L.gate, L.up, q, n, fq);
