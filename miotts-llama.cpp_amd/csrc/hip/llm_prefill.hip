@@ -65,25 +65,32 @@ __device__ inline float *resid_lds(char *base, int K, int nt, int rpw) {
 // A register group holds RU whole rows (all NM matrices, all NP passes): every fragment is
 // loaded once and dotted with each token's activation; row totals per token as in the
 // decode engine (acc over passes in order, then row_total).
-// MIO_BT_UNITS (compile-time, A/B builds): weight units per row group (4 default)
+// MIO_BT_UNITS / MIO_BT_UNITS_Q8 (compile-time, A/B builds): weight units per row group for
+// K-quant / Q8_0 matrices. Smaller groups turn over faster (the next group's loads go out
+// sooner); 8-stream steps (graph, profiles/r04_bt_units_ab.txt): 2.6B Q8_0 2.36 / 2.23 / 2.20
+// ms at 4 / 2 / 1 units, 1.7B Q4_K_M 1.84 / 1.77 / 1.81 ms
 #ifndef MIO_BT_UNITS
-#define MIO_BT_UNITS 4
+#define MIO_BT_UNITS 2
+#endif
+#ifndef MIO_BT_UNITS_Q8
+#define MIO_BT_UNITS_Q8 1
 #endif
 // NG register groups in flight per wave: two (one loading while the other is dotted), or one
 // for NP = 6 (a 6-pass row is 13 KB per wave; 8 waves x one row already keep 100 KB per CU in
 // flight, and the registers go to the activation records, act_issue)
-template <int NP, int NM>
+template <int T, int NP, int NM>
 struct CfgB {
-    static constexpr int RU = NP * NM >= MIO_BT_UNITS ? 1 : MIO_BT_UNITS / (NP * NM);
+    static constexpr int UN = T == 8 ? MIO_BT_UNITS_Q8 : MIO_BT_UNITS;
+    static constexpr int RU = NP * NM >= UN ? 1 : UN / (NP * NM);
     static constexpr int U = RU * NP * NM;
     static constexpr int NG = NP >= 6 ? 1 : 2;
 };
 
 template <int T, int NP, int NM>
-__device__ __forceinline__ void load_rows(const QMat W0, const QMat W1, int r, int hi, Frag (&F)[CfgB<NP, NM>::U],
+__device__ __forceinline__ void load_rows(const QMat W0, const QMat W1, int r, int hi, Frag (&F)[CfgB<T, NP, NM>::U],
                                           int split) {
 #pragma unroll
-    for (int ri = 0; ri < CfgB<NP, NM>::RU; ++ri) {
+    for (int ri = 0; ri < CfgB<T, NP, NM>::RU; ++ri) {
         const int row = __builtin_amdgcn_readfirstlane(min(r + ri, hi - 1));  // wave-uniform
 #pragma unroll
         for (int m = 0; m < NM; ++m)
@@ -100,11 +107,11 @@ __device__ __forceinline__ void load_rows(const QMat W0, const QMat W1, int r, i
 
 template <int T, int NP, int NM>
 __device__ __forceinline__ void load_first_b(const QMat W0, const QMat W1, int lo, int hi,
-                                             Frag (&A)[CfgB<NP, NM>::U], Frag (&B)[CfgB<NP, NM>::U],
+                                             Frag (&A)[CfgB<T, NP, NM>::U], Frag (&B)[CfgB<T, NP, NM>::U],
                                              int split = INT_MAX) {
     if (hi <= lo) return;
     load_rows<T, NP, NM>(W0, W1, lo, hi, A, split);
-    if constexpr (CfgB<NP, NM>::NG == 2) load_rows<T, NP, NM>(W0, W1, lo + CfgB<NP, NM>::RU, hi, B, split);
+    if constexpr (CfgB<T, NP, NM>::NG == 2) load_rows<T, NP, NM>(W0, W1, lo + CfgB<T, NP, NM>::RU, hi, B, split);
 }
 
 // ------------------------------------------------------------------ transposed row totals
@@ -176,6 +183,11 @@ struct XRedCfg {
     static constexpr int TT = NP == 1 ? 4 : (NP == 3 ? 2 : 1);
     static constexpr int TB = NP == 1 ? 8 : (NP == 3 ? 4 : 8);
 };
+// MIO_BT_MINB (compile-time A/B): workgroups per CU the one-pass batched matvecs (attn_out,
+// ffn_in) are register-budgeted for; with MIO_BT_WGM=2 at run time their grids double
+#ifndef MIO_BT_MINB
+#define MIO_BT_MINB 1
+#endif
 #ifndef MIO_BT_XRED
 #define MIO_BT_XRED 1
 #endif
@@ -184,9 +196,9 @@ struct XRedCfg {
 // the totals (lane-varying values), else wave-uniform values on every lane
 template <int T, int NP, int NM, class Epi>
 __device__ __forceinline__ void stream_rows_bx(const QMat W0, const QMat W1, int lo, int hi,
-                                               Frag (&A)[CfgB<NP, NM>::U], Frag (&B)[CfgB<NP, NM>::U], char *smem,
+                                               Frag (&A)[CfgB<T, NP, NM>::U], Frag (&B)[CfgB<T, NP, NM>::U], char *smem,
                                                int nt, Epi &&epi, int split = INT_MAX) {
-    constexpr int RU = CfgB<NP, NM>::RU, U = CfgB<NP, NM>::U;
+    constexpr int RU = CfgB<T, NP, NM>::RU, U = CfgB<T, NP, NM>::U;
     constexpr int TT = XRedCfg<NP>::TT, TB = XRedCfg<NP>::TB;
     constexpr int N = TB * RU * NM;             // totals per group: index ((t * RU + ri) * NM + m)
     constexpr int LB = T == 8 ? 0 : 3;          // first tree level (K-quants: lanes 8k+7)
@@ -239,7 +251,7 @@ __device__ __forceinline__ void stream_rows_bx(const QMat W0, const QMat W1, int
             }
         }
     };
-    if constexpr (CfgB<NP, NM>::NG == 1) {
+    if constexpr (CfgB<T, NP, NM>::NG == 1) {
         for (int r = lo;;) {
             consume(A, r);
             r += RU;
@@ -263,9 +275,9 @@ __device__ __forceinline__ void stream_rows_bx(const QMat W0, const QMat W1, int
 // epi(row, t, dot0, dot1): wave-uniform values, once per (row, token)
 template <int T, int NP, int NM, class Epi>
 __device__ __forceinline__ void stream_rows_bu(const QMat W0, const QMat W1, int lo, int hi,
-                                               Frag (&A)[CfgB<NP, NM>::U], Frag (&B)[CfgB<NP, NM>::U], char *smem,
+                                               Frag (&A)[CfgB<T, NP, NM>::U], Frag (&B)[CfgB<T, NP, NM>::U], char *smem,
                                                int nt, Epi &&epi, int split = INT_MAX) {
-    constexpr int RU = CfgB<NP, NM>::RU, U = CfgB<NP, NM>::U;
+    constexpr int RU = CfgB<T, NP, NM>::RU, U = CfgB<T, NP, NM>::U;
     const int K = W0.k;
     if (hi <= lo) return;
     // TT tokens per iteration: their activation loads are in flight together and their dot
@@ -311,7 +323,7 @@ __device__ __forceinline__ void stream_rows_bu(const QMat W0, const QMat W1, int
             }
         }
     };
-    if constexpr (CfgB<NP, NM>::NG == 1) {
+    if constexpr (CfgB<T, NP, NM>::NG == 1) {
         for (int r = lo;;) {
             consume(A, r);
             r += RU;
@@ -336,7 +348,7 @@ __device__ __forceinline__ void stream_rows_bu(const QMat W0, const QMat W1, int
 // tree per total (A/B build). Either way epi runs once per (row, token) on one lane.
 template <int T, int NP, int NM, class Epi>
 __device__ __forceinline__ void stream_rows_b(const QMat W0, const QMat W1, int lo, int hi,
-                                              Frag (&A)[CfgB<NP, NM>::U], Frag (&B)[CfgB<NP, NM>::U], char *smem,
+                                              Frag (&A)[CfgB<T, NP, NM>::U], Frag (&B)[CfgB<T, NP, NM>::U], char *smem,
                                               int nt, Epi &&epi, int split = INT_MAX) {
     if constexpr (MIO_BT_XRED)
         stream_rows_bx<T, NP, NM>(W0, W1, lo, hi, A, B, smem, nt, epi, split);
@@ -656,7 +668,7 @@ __global__ __launch_bounds__(MT) void k_pf_attn_in(LlmDims d, const float *norm_
     const int K = d.n_embd, QD = (d.n_head + 2 * d.n_kv) * d.hd;
     const int lane = threadIdx.x & 63;
     const int o1 = wq.rows, o2 = wq.rows + wk.rows;
-    Frag ga[CfgB<NP, 1>::U], gb[CfgB<NP, 1>::U];
+    Frag ga[CfgB<TQ, NP, 1>::U], gb[CfgB<TQ, NP, 1>::U];
     XPre xp;
     if constexpr (FQ == 2) xpre_issue(pb.x, norm_w, K, nt, xp);
     auto prologue = [&]() {
@@ -822,7 +834,7 @@ __global__ __launch_bounds__(ATT_NT) void k_bt_attention(LlmDims d, const float 
 }
 
 template <int NP, int T>
-__global__ __launch_bounds__(MT) void k_pf_attn_out(LlmDims d, QMat wo, PrefillBuffers pb, int nt, int rpw) {
+__global__ __launch_bounds__(MT, MIO_BT_MINB) void k_pf_attn_out(LlmDims d, QMat wo, PrefillBuffers pb, int nt, int rpw) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int K = wo.k, E = d.n_embd;
     int lo, hi;
@@ -830,7 +842,7 @@ __global__ __launch_bounds__(MT) void k_pf_attn_out(LlmDims d, QMat wo, PrefillB
     const Resid xr = load_resid_b(pb.x, E, lo, hi, nt, rpw);
     ActPre<NP> ap;
     act_issue<NP>(pb.act, K, nt, ap);
-    Frag ga[CfgB<NP, 1>::U], gb[CfgB<NP, 1>::U];
+    Frag ga[CfgB<T, NP, 1>::U], gb[CfgB<T, NP, 1>::U];
     load_first_b<T, NP, 1>(wo, wo, lo, hi, ga, gb);
     float *res = resid_lds(smem, K, nt, rpw);
     store_resid_b(xr, res, nt, rpw);
@@ -843,7 +855,7 @@ __global__ __launch_bounds__(MT) void k_pf_attn_out(LlmDims d, QMat wo, PrefillB
 
 // FQ = 2: RMSNorm + quantization in the launch from inputs loaded ahead of the weights (xpre)
 template <int NP, int T, int FQ = 0>
-__global__ __launch_bounds__(MT) void k_pf_ffn_in(LlmDims d, const float *norm_w, QMat gate, QMat up,
+__global__ __launch_bounds__(MT, MIO_BT_MINB) void k_pf_ffn_in(LlmDims d, const float *norm_w, QMat gate, QMat up,
                                                   PrefillBuffers pb, int nt, int fq) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int K = d.n_embd;
@@ -855,7 +867,7 @@ __global__ __launch_bounds__(MT) void k_pf_ffn_in(LlmDims d, const float *norm_w
         xpre_issue(pb.x, norm_w, K, nt, xp);
     else
         act_issue<NP>(pb.act, K, nt, ap);  // unconditional (in bounds; unused with fq): keeps ap in registers
-    Frag ga[CfgB<NP, 2>::U], gb[CfgB<NP, 2>::U];
+    Frag ga[CfgB<T, NP, 2>::U], gb[CfgB<T, NP, 2>::U];
     load_first_b<T, NP, 2>(gate, up, lo, hi, ga, gb);
     if constexpr (FQ == 2)
         xpre_quant(xp, K, d.eps, T != 8, smem, nt);
@@ -878,7 +890,7 @@ __global__ __launch_bounds__(MT) void k_pf_ffn_down(LlmDims d, QMat down, Prefil
     const Resid rr = load_resid_b(pb.x, E, lo, hi, nt, rpw);
     ActPre<NP> ap;
     act_issue<NP>(pb.act, K, nt, ap);  // unconditional (in bounds; unused with fq): keeps ap in registers
-    Frag ga[CfgB<NP, 1>::U], gb[CfgB<NP, 1>::U];
+    Frag ga[CfgB<T, NP, 1>::U], gb[CfgB<T, NP, 1>::U];
     load_first_b<T, NP, 1>(down, down, lo, hi, ga, gb);
     float *res = resid_lds(smem, K, nt, rpw);
     store_resid_b(rr, res, nt, rpw);
@@ -915,7 +927,7 @@ __global__ __launch_bounds__(MT) void k_bt_lm_head(LlmDims d, const float *norm_
     wave_range(d, lm.rows, lo, hi);
     ActPre<NP> ap;
     act_issue<NP>(pb.act, K, nt, ap);
-    Frag ga[CfgB<NP, 1>::U], gb[CfgB<NP, 1>::U];
+    Frag ga[CfgB<T, NP, 1>::U], gb[CfgB<T, NP, 1>::U];
     load_first_b<T, NP, 1>(lm, lm, lo, hi, ga, gb);
     act_store<NP>(ap, pb.act, K, smem, nt);
     float *vals = reinterpret_cast<float *>(smem + pf_lds_bytes(K, nt, 0)) + (size_t)wave * nt * 128;
@@ -1113,6 +1125,15 @@ void launch_quant(const LlmDims &d, int mode, const float *src, int K, const flo
 // the launch that quantizes its activations once (k_bt_quant).
 // decode: every token is its own sequence (the batched decode step): attention per token
 // with the RoPE / KV append inside (k_bt_attention).
+// MIO_BT_WGM (A/B, default 1): grid multiplier of the one-pass batched matvecs (two workgroups
+// per CU need a MIO_BT_MINB=2 build: <= 128 VGPRs, and <= 80 KB of LDS)
+static LlmDims bt_wgm(const LlmDims &d, int K) {
+    static const int m = getenv("MIO_BT_WGM") ? atoi(getenv("MIO_BT_WGM")) : 1;
+    LlmDims r = d;
+    if (m > 1 && pick_np(K) == 1) r.n_wg = d.n_wg * m;
+    return r;
+}
+
 void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16 *kcache, _Float16 *vcache,
                    const PrefillBuffers &pb, int nt, int n_chunks, bool decode, hipStream_t s) {
     const size_t layer_kv = (size_t)d.n_kv * d.n_ctx * d.hd;
@@ -1252,12 +1273,13 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
                 launch_mmq(&sg, &L.wo.type, 1, MMQ_RESID, MmqArgs{pb.act, act_bytes(L.wo.k), L.wo.k, nt, pb.x, d.n_embd, {}},
                            s);
             } else {
-                const int grid = matvec_grid(d, L.wo.rows), rpw = rows_per_wave(L.wo.rows, grid);
+                const LlmDims dw = bt_wgm(d, L.wo.k);
+                const int grid = matvec_grid(dw, L.wo.rows), rpw = rows_per_wave(L.wo.rows, grid);
                 over_tokens(L.wo.k, rpw, [&](int, int n, const PrefillBuffers &q) {
                     dispatch_nt(L.wo.k, L.wo.type, [&]<int NP, int T>() {
                         allow_lds(k_pf_attn_out<NP, T>);
                         hipLaunchKernelGGL((k_pf_attn_out<NP, T>), dim3(grid), dim3(MT), pf_lds_bytes(L.wo.k, n, rpw), s,
-                                           d, L.wo, q, n, rpw);
+                                           dw, L.wo, q, n, rpw);
                     });
                 });
             }
@@ -1270,19 +1292,20 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
             launch_mmq(&sg, &L.gate.type, 1, MMQ_SWIGLU,
                        MmqArgs{pb.act, act_bytes(d.n_embd), d.n_embd, nt, pb.h, d.n_ff, L.up}, s);
         } else {
-            const int grid = matvec_grid(d, L.gate.rows);
+            const LlmDims dw = bt_wgm(d, d.n_embd);
+            const int grid = matvec_grid(dw, L.gate.rows);
             over_tokens(d.n_embd, 0, [&](int, int n, const PrefillBuffers &q) {
                 dispatch_nt(d.n_embd, L.gate.type, [&]<int NP, int T>() {
                     if constexpr (NP == 1) {
                         if (ff) {
                             allow_lds(k_pf_ffn_in<NP, T, 2>);
                             hipLaunchKernelGGL((k_pf_ffn_in<NP, T, 2>), dim3(grid), dim3(MT), pf_lds_bytes(d.n_embd, n, 0),
-                                               s, d, L.ffn_norm, L.gate, L.up, q, n, fq);
+                                               s, dw, L.ffn_norm, L.gate, L.up, q, n, fq);
                             return;
                         }
                     }
                     allow_lds(k_pf_ffn_in<NP, T>);
-                    hipLaunchKernelGGL((k_pf_ffn_in<NP, T>), dim3(grid), dim3(MT), pf_lds_bytes(d.n_embd, n, 0), s, d,
+                    hipLaunchKernelGGL((k_pf_ffn_in<NP, T>), dim3(grid), dim3(MT), pf_lds_bytes(d.n_embd, n, 0), s, dw,
                                        L.ffn_norm, L.gate, L.up, q, n, fq);
                 });
             });
