@@ -1170,14 +1170,18 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
     // tokens' inputs twice)
     static const bool fq_env = getenv("MIO_FUSED_QUANT") && getenv("MIO_FUSED_QUANT")[0] == '1';
     const int fq = (!mmq && fq_env && nt <= 16) ? 1 : 0;
-    // MIO_BT_FQ (bits: 1 attn_in, 2 ffn_in; default 1): launches of <= 8 tokens over K <= 2048
+    // MIO_BT_FQ (bits: 1 attn_in, 2 ffn_in; default below): launches of <= 8 tokens over K <= 2048
     // RMSNorm + quantize in the launch from inputs loaded ahead of the weights (xpre), on the
     // dot4 engine, instead of behind a k_bt_quant launch (and, for q|k|v, on the matrix cores).
     // 8-stream steps (graph; profiles/r04_fq_ab.txt): 2.6B Q8_0 2.354 ms with attn_in only,
     // 2.362 both, 2.488 neither or ffn_in only; 1.7B Q4_K_M 1.837 / 1.881 / 1.843 / 1.891
-    static const int fq2_env = getenv("MIO_BT_FQ") ? atoi(getenv("MIO_BT_FQ")) : 1;
-    auto fq2 = [&](int kind) {
-        return !fq && !mmq && nt <= MW && pick_np(d.n_embd) == 1 && ((fq2_env >> kind) & 1);
+    // r04 engine A/B (profiles/r04_engine_choice_ab.txt): gate|up in-launch as well is 1% faster
+    // for Q8_0 (2.183 vs 2.202 ms) and 2% slower for K-quants (1.800 vs 1.769): default = attn_in
+    // always, ffn_in for Q8_0 gate|up
+    static const int fq2_env = getenv("MIO_BT_FQ") ? atoi(getenv("MIO_BT_FQ")) : -1;
+    auto fq2 = [&](int kind, int type) {
+        const bool on = fq2_env >= 0 ? ((fq2_env >> kind) & 1) != 0 : (kind == 0 || type == 8);
+        return !fq && !mmq && nt <= MW && pick_np(d.n_embd) == 1 && on;
     };
     // MIO_BT_ATT=0: the batched decode step uses k_pf_rope + k_pf_attention (A/B)
     static const bool bt_att = !(getenv("MIO_BT_ATT") && getenv("MIO_BT_ATT")[0] == '0');
@@ -1207,7 +1211,7 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
             launch_mmq(&so, &L.out_proj.type, 1, MMQ_RESID, MmqArgs{pb.act, act_bytes(n), n, nt, pb.x, n, {}}, s);
         } else {
             _Float16 *kc = kcache + il * layer_kv, *vc = vcache + il * layer_kv;
-            const bool fa = fq2(0);
+            const bool fa = fq2(0, L.wq.type);
             if (!fa && (!fq || use_mmq(0, L.wq.type)))
                 launch_quant(d, 0, pb.x, d.n_embd, L.attn_norm, L.wq.type != 8, pb, nt, s);
             if (!fa && use_mmq(0, L.wq.type)) {
@@ -1284,7 +1288,7 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
                 });
             }
         }
-        const bool ff = fq2(1);
+        const bool ff = fq2(1, L.gate.type);
         if (!ff && (!fq || use_mmq(2, L.gate.type)))
             launch_quant(d, 0, pb.x, d.n_embd, L.ffn_norm, L.gate.type != 8, pb, nt, s);
         if (!ff && use_mmq(2, L.gate.type)) {
