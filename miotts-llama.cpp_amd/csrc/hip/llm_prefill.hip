@@ -573,7 +573,10 @@ __global__ __launch_bounds__(MT) void k_bt_quant(LlmDims d, const float *src, in
                                                  PrefillBuffers pb) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int t = blockIdx.x;
-    const Smem s = carve(smem, K);
+    // the quantizers store straight into the token's global record (its layout is the LDS
+    // record's: qs | d | bs), no LDS staging + barrier + copy; LDS keeps the reduction scratch
+    Smem s = carve(smem, K);
+    s.a = carve_t(pb.act, K, t).a;
     if constexpr (MODE == 2) {
         const size_t tstride = (size_t)d.n_head * d.max_splits * part_rec(d.hd);
         merge_attention<NP>(d, pb.part + t * tstride, pb.pos[t * pb.pos_stride] / ATT_CHUNK + 1, K, kq != 0, s);
@@ -585,11 +588,6 @@ __global__ __launch_bounds__(MT) void k_bt_quant(LlmDims d, const float *src, in
         else
             plain_quant(xr, K, kq != 0, s);
     }
-    // LDS act {qs | d | bs} is contiguous from s.a.qs (carve) -> this token's global record
-    const int n16 = (int)(act_bytes(K) / 16);
-    const uint4 *l = reinterpret_cast<const uint4 *>(s.a.qs);
-    uint4 *g = reinterpret_cast<uint4 *>(pb.act + (size_t)t * act_bytes(K));
-    for (int i = threadIdx.x; i < n16; i += MT) g[i] = l[i];
 }
 
 // lfm2 short-conv layer, one workgroup per token t: the gated conv of t (conv_load /
