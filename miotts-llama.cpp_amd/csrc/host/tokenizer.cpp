@@ -114,9 +114,18 @@ bool BpeTokenizer::load(const GgufFile &g) {
     bos_ = (int32_t)g.get_int("tokenizer.ggml.bos_token_id", -1);
     const GgufValue *ab = g.get("tokenizer.ggml.add_bos_token");
     add_bos_ = ab ? ab->u != 0 : false;
-    // llama.cpp's tokenizer.ggml.pre names (llama-vocab.cpp) of the families implemented here
+    // llama.cpp's tokenizer.ggml.pre names (llama-vocab.cpp) of the families implemented here.
+    // convert_hf_to_gguf.py writes "gpt-2" for the GPT-2 regex; llama-vocab.cpp maps the
+    // other names below onto the same regex (its GPT2 / MPT / OLMO / JAIS pre types).
+    // "gpt2" is kept for GGUFs written by hand with the tokenizer.ggml.model spelling.
     const std::string pre = g.get_str("tokenizer.ggml.pre", "default");
-    if (pre == "gpt2" || pre == "mpt" || pre == "olmo" || pre == "jais")
+    static const char *const kGpt2Names[] = {"gpt-2",      "gpt2",       "phi-2",        "jina-es",  "jina-de",
+                                             "jina-v1-en", "jina-v2-es", "jina-v2-de",   "jina-v2-code",
+                                             "roberta-bpe", "gigachat",  "a.x-4.0",      "mellum",   "mpt",
+                                             "olmo",       "jais"};
+    bool gpt2_name = false;
+    for (const char *n : kGpt2Names) gpt2_name = gpt2_name || pre == n;
+    if (gpt2_name)
         pre_ = Pre::Gpt2;
     else if (pre == "default")
         pre_ = Pre::Default;
@@ -129,7 +138,7 @@ bool BpeTokenizer::load(const GgufFile &g) {
              pre == "exaone" || pre == "minerva-7b")
         pre_ = Pre::Smollm;
     else {
-        set_error("tokenizer: pre-tokenizer '%s' is not implemented (gpt2, default, qwen2, llama3 / llama-bpe / "
+        set_error("tokenizer: pre-tokenizer '%s' is not implemented (gpt-2, default, qwen2, llama3 / llama-bpe / "
                   "lfm2, smollm families)", pre.c_str());
         return false;
     }

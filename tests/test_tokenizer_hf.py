@@ -81,7 +81,7 @@ def _trained(pre, vocab_size, seed):
         tok.pre_tokenizer = pre_tokenizers.Sequence([
             pre_tokenizers.Digits(individual_digits=True),
             pre_tokenizers.ByteLevel(add_prefix_space=False, use_regex=True)])
-    else:  # gpt2
+    else:  # gpt-2 (llama.cpp's converter name) and its aliases
         tok.pre_tokenizer = pre_tokenizers.ByteLevel(add_prefix_space=False, use_regex=True)
     rng = random.Random(seed)
     corpus = [_text(rng, 200) for _ in range(600)] + _WORDS * 20
@@ -114,9 +114,9 @@ def _to_gguf(tok, path, pre):
     return len(merges)
 
 
-@pytest.mark.parametrize("pre,vocab_size,seed", [("qwen2", 1200, 1), ("qwen2", 3000, 2), ("gpt2", 1200, 3),
+@pytest.mark.parametrize("pre,vocab_size,seed", [("qwen2", 1200, 1), ("qwen2", 3000, 2), ("gpt-2", 1200, 3),
                                                   ("default", 1500, 4), ("llama3", 1500, 5), ("lfm2", 3000, 6),
-                                                  ("smollm", 1500, 7)])
+                                                  ("smollm", 1500, 7), ("gpt2", 1200, 8), ("phi-2", 1200, 9)])
 def test_tokenize_matches_hf_tokenizers(tmp_path, pre, vocab_size, seed):
     hf = _trained(pre, vocab_size, seed)
     path = str(tmp_path / f"hf_{pre}_{seed}.gguf")
