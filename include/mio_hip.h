@@ -205,6 +205,11 @@ int mio_hip_llm_conv_ring(mio_hip_llm *m, int il, float *ring, int set);
 /* Wall time (ms) of mio_hip_llm_load: GGUF mmap, re-layout into pinned staging buffers,
  * asynchronous copies into the HBM weight arena (double-buffered). */
 int mio_hip_llm_load_ms(const mio_hip_llm *m, double *ms);
+/* Decode steps (one sampled token each) issued since the last generate began, look-ahead
+ * included: generate keeps one check interval queued ahead of its end-token poll, so a run
+ * that stops at an end token after n_out tokens issued *steps - n_out - 1 steps for nothing
+ * (at most check_interval; 0 when it stops at max_tokens). */
+int mio_hip_llm_steps_issued(const mio_hip_llm *m, int *steps);
 /* Prenet rows the last mio_hip_codec_decode_pcm took from the incremental cache. */
 int mio_hip_codec_last_reused(const mio_hip_codec *c, int *rows);
 /* Algorithmic FLOPs of the last mio_hip_codec_decode_pcm (2 per multiply-add of every GEMM,

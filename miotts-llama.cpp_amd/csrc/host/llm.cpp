@@ -344,9 +344,11 @@ int prefill_issue(mio_hip_llm *m, int n) {
 // Batched prefill of positions [0, n): every launch reads only device buffers whose addresses
 // depend on n alone (prompt tokens in m->d_prompt), so one graph per prompt length replays it.
 // The first prefill of a length runs eagerly (its launches set the kernels' LDS attributes
-// outside any capture), then is captured for the next utterance. MIO_PREFILL_GRAPH=0: eager.
+// outside any capture), then is captured for the next utterance. MIO_PREFILL_GRAPH=0 or
+// MIO_NO_GRAPH=1 (every launch eager, for kernel tracing): eager.
 int prefill(mio_hip_llm *m, int n) {
-    static const bool use_graph = !(getenv("MIO_PREFILL_GRAPH") && getenv("MIO_PREFILL_GRAPH")[0] == '0');
+    static const bool use_graph = !(getenv("MIO_PREFILL_GRAPH") && getenv("MIO_PREFILL_GRAPH")[0] == '0') &&
+                                  !(getenv("MIO_NO_GRAPH") && getenv("MIO_NO_GRAPH")[0] == '1');
     if (n <= 0) return MIO_OK;
     const auto it = m->prefill_graphs.find(n);
     if (use_graph && it != m->prefill_graphs.end()) {
@@ -355,16 +357,25 @@ int prefill(mio_hip_llm *m, int n) {
     }
     int rc = prefill_issue(m, n);
     if (rc || !use_graph || m->prefill_graphs.size() >= 16) return rc;
+    // capture a second issue for the next utterance of this length; the prefill above already
+    // ran eagerly, so a failed capture or instantiation only leaves this length uncached
     hipStream_t s = m->d->stream;
     hipGraph_t g = nullptr;
     hipGraphExec_t ge = nullptr;
-    MIO_HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
-    rc = prefill_issue(m, n);
-    MIO_HIP_CHECK(hipStreamEndCapture(s, &g));
-    if (rc) return rc;
-    MIO_HIP_CHECK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
-    hipGraphDestroy(g);
-    m->prefill_graphs[n] = ge;
+    if (hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal) != hipSuccess) {
+        (void)hipGetLastError();
+        return MIO_OK;
+    }
+    const int crc = prefill_issue(m, n);
+    const hipError_t ec = hipStreamEndCapture(s, &g);
+    const bool ok = crc == MIO_OK && ec == hipSuccess && g &&
+                    hipGraphInstantiate(&ge, g, nullptr, nullptr, 0) == hipSuccess;
+    if (g) hipGraphDestroy(g);
+    (void)hipGetLastError();
+    if (ok)
+        m->prefill_graphs[n] = ge;
+    else if (ge)
+        hipGraphExecDestroy(ge);
     return MIO_OK;
 }
 
@@ -875,6 +886,12 @@ extern "C" int mio_hip_llm_load_ms(const mio_hip_llm *m, double *ms) {
     return MIO_OK;
 }
 
+extern "C" int mio_hip_llm_steps_issued(const mio_hip_llm *m, int *steps) {
+    MIO_REQUIRE(m && steps, MIO_ERR_INVALID, "llm_steps_issued: null");
+    *steps = std::max(0, m->steps_issued - (m->n_prompt - 1));
+    return MIO_OK;
+}
+
 extern "C" void mio_hip_llm_free(mio_hip_llm *m) { delete m; }
 
 extern "C" int mio_hip_llm_info(const mio_hip_llm *m, int *info) {
@@ -1312,6 +1329,38 @@ static int kernel_layer(const mio_hip_llm *m, int which) {
     return -1;
 }
 
+// Decode state a diagnostic launch may change, saved at entry and put back on exit: the
+// StepState (k_lm_head sets `pending`, layer 0's k_ffn_in folds it into pos) and the
+// residual x (attn_out / ffn_down / conv_out add into it; after a flush it holds the next
+// token's embedding). The other buffers a launch writes are rewritten by the next real step
+// before anything reads them: the K/V row and the short-conv ring slot of cur_pos (the
+// owner stores them first), q|k|v, h, the chunk partials and the lm_head partials (the same
+// inputs give the same values).
+struct DiagStateGuard {
+    mio_hip_llm *m;
+    mio::StepState st{};
+    float *x = nullptr;
+    int rc = MIO_OK;
+    explicit DiagStateGuard(mio_hip_llm *mm) : m(mm) {
+        const size_t xb = (size_t)m->dims.n_embd * sizeof(float);
+        if (hipStreamSynchronize(m->d->stream) != hipSuccess ||
+            hipMemcpy(&st, m->buf.st, sizeof(st), hipMemcpyDeviceToHost) != hipSuccess ||
+            hipMalloc(&x, xb) != hipSuccess || hipMemcpy(x, m->buf.x, xb, hipMemcpyDeviceToDevice) != hipSuccess)
+        {
+            mio::set_error("llm diagnostic: saving the decode state failed");
+            rc = MIO_ERR_HIP;
+        }
+    }
+    ~DiagStateGuard() {
+        hipStreamSynchronize(m->d->stream);
+        if (x) {
+            hipMemcpy(m->buf.x, x, (size_t)m->dims.n_embd * sizeof(float), hipMemcpyDeviceToDevice);
+            hipFree(x);
+        }
+        if (rc == MIO_OK) hipMemcpy(m->buf.st, &st, sizeof(st), hipMemcpyHostToDevice);
+    }
+};
+
 // Live timing of one kernel of the decode step (bench.py roofline): launches kernel
 // `which` (0 attn_in, 1 attention, 2 attn_out, 3 ffn_in, 4 ffn_down, 6 lm_head, 8 conv_in,
 // 9 conv_out) of layer kernel_layer() `iters` times on the runner's stream between HIP events, with the buffers and
@@ -1333,12 +1382,11 @@ extern "C" int mio_hip_llm_time_kernel(mio_hip_llm *m, int which, int iters, flo
         return (uint64_t)mio::ggml_row_bytes(q.type, q.k) * (uint64_t)q.rows;
     };
     const mio::LlmDims &D = m->dims;
-    // attention reads the K/V rows of positions <= pos of the current decode state
-    // the state at entry is restored on exit (k_lm_head sets `pending`, k_ffn_in of layer 0
-    // folds it into pos): diagnostic launches leave the decode state as they found it
-    mio::StepState st{};
-    MIO_HIP_CHECK(hipStreamSynchronize(m->d->stream));
-    MIO_HIP_CHECK(hipMemcpy(&st, m->buf.st, sizeof(st), hipMemcpyDeviceToHost));
+    // attention reads the K/V rows of positions <= pos of the current decode state; the
+    // decode state is put back on exit (DiagStateGuard)
+    DiagStateGuard guard(m);
+    if (guard.rc) return guard.rc;
+    const mio::StepState &st = guard.st;
     // the position the attention kernels work at (cur_pos: pos + pending)
     const uint64_t pos = (uint64_t)std::max(0, std::min(st.pos + st.pending, D.n_ctx - 1));
     const uint64_t nch = pos / mio::kAttChunk + 1, qkv = (uint64_t)(D.n_head + 2 * D.n_kv) * D.hd;
@@ -1375,7 +1423,6 @@ extern "C" int mio_hip_llm_time_kernel(mio_hip_llm *m, int which, int iters, flo
     float ms = 0;
     MIO_HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
     hipEventDestroy(e0), hipEventDestroy(e1);
-    MIO_HIP_CHECK(hipMemcpy(m->buf.st, &st, sizeof(st), hipMemcpyHostToDevice));
     *avg_ms = ms / iters;
     *bytes = b;
     return MIO_OK;
@@ -1392,9 +1439,8 @@ extern "C" int mio_hip_llm_trace_kernel(mio_hip_llm *m, int which, uint64_t *out
     int rc = mio::bind(m->d);
     if (rc) return rc;
     hipStream_t s = m->d->stream;
-    mio::StepState st0{};  // restored on exit, as in mio_hip_llm_time_kernel
-    MIO_HIP_CHECK(hipStreamSynchronize(s));
-    MIO_HIP_CHECK(hipMemcpy(&st0, m->buf.st, sizeof(st0), hipMemcpyDeviceToHost));
+    DiagStateGuard guard(m);  // the decode state is put back on exit
+    if (guard.rc) return guard.rc;
     unsigned long long *dt = nullptr;
     MIO_HIP_CHECK(hipMalloc(&dt, 32 * sizeof(unsigned long long)));
     MIO_HIP_CHECK(hipMemsetAsync(dt, 0, 32 * sizeof(unsigned long long), s));
@@ -1421,7 +1467,6 @@ extern "C" int mio_hip_llm_trace_kernel(mio_hip_llm *m, int which, uint64_t *out
     MIO_HIP_CHECK(hipStreamSynchronize(s));
     hipFree(dt);
     if (flush) hipFree(flush);
-    MIO_HIP_CHECK(hipMemcpy(m->buf.st, &st0, sizeof(st0), hipMemcpyHostToDevice));
     return MIO_OK;
 }
 

@@ -101,6 +101,7 @@ def _declare(L: ctypes.CDLL) -> None:
         "mio_hip_codec_last_reused": (c_int, [_vp, ctypes.POINTER(c_int)]),
         "mio_hip_codec_last_flops": (c_int, [_vp, ctypes.POINTER(ctypes.c_double)]),
         "mio_hip_llm_load_ms": (c_int, [_vp, ctypes.POINTER(ctypes.c_double)]),
+        "mio_hip_llm_steps_issued": (c_int, [_vp, ctypes.POINTER(c_int)]),
         "mio_hip_llm_step_kinds": (c_int, [_vp, _vp, c_int, ctypes.POINTER(c_int)]),
         "mio_hip_llm_conv_ring": (c_int, [_vp, c_int, _vp, c_int]),
         "mio_hip_debug_graph_replay": (c_int, [_vp, c_int, c_int, ctypes.POINTER(ctypes.c_double)]),
@@ -438,6 +439,12 @@ class Llm:
         """Wall time of the load (GGUF mmap -> pinned staging -> HBM arena)."""
         v = ctypes.c_double(0)
         check(lib().mio_hip_llm_load_ms(self.h, ctypes.byref(v)))
+        return v.value
+
+    def steps_issued(self) -> int:
+        """Decode steps issued by the last generate, look-ahead past an end token included."""
+        v = ctypes.c_int(0)
+        check(lib().mio_hip_llm_steps_issued(self.h, ctypes.byref(v)))
         return v.value
 
     def eval(self, token: int, pos: int) -> np.ndarray:
