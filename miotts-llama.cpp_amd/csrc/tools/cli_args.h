@@ -90,12 +90,15 @@ inline bool cli_parse(int argc, char **argv, const std::vector<CliFlag> &flags, 
     return true;
 }
 
-// the reference tools' required-argument checks; returns an error text or empty
-inline std::string cli_check(const CliArgs &a) {
+// the reference tools' required-argument checks; returns an error text or empty.
+// path_words: main.cpp:109-121 says "--codec path is required" where the examples
+// (stream-benchmark.cpp:93-105, stream-compare.cpp:174-186) say "--codec is required".
+inline std::string cli_check(const CliArgs &a, bool path_words = false) {
+    const std::string p = path_words ? " path" : "";
     if (a.prompt.empty()) return "--prompt is required";
-    if (a.codec_path.empty()) return "--codec is required";
-    if (a.voice_path.empty()) return "--voice is required";
-    if (!a.skip_llm && a.model_path.empty()) return "--model is required (or use --skip-llm)";
+    if (a.codec_path.empty()) return "--codec" + p + " is required";
+    if (a.voice_path.empty()) return "--voice" + p + " is required";
+    if (!a.skip_llm && a.model_path.empty()) return "--model" + p + " is required (or use --skip-llm)";
     return "";
 }
 

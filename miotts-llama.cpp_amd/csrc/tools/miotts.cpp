@@ -22,7 +22,7 @@ int main(int argc, char **argv) {
         miocodec_print_tensors(a.codec_path);
         return 0;
     }
-    const std::string err = cli_check(a);
+    const std::string err = cli_check(a, true);
     if (!err.empty()) {
         std::fprintf(stderr, "Error: %s\n", err.c_str());
         return 1;
