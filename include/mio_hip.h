@@ -189,13 +189,8 @@ int mio_hip_llm_trace_kernel(mio_hip_llm *m, int which, uint64_t *out);
  * prepared; 3-6 = prologue steps in -DMIO_TL_DIAG builds.
  * Advances the decode state. */
 int mio_hip_llm_timeline(mio_hip_llm *m, uint64_t *out, int max_launches, int *n_launches);
-/* Diagnostic: a graph of `nodes` empty one-workgroup launches, captured on the device's
- * stream and replayed `replays` times; *wall_ms = host wall time of the replays (synchronized).
- * Separates graph-replay machinery (and profilers intercepting it) from the decode kernels. */
-int mio_hip_debug_graph_replay(mio_hip_device *d, int replays, int nodes, double *wall_ms);
 /* The launches of one decode step in order, as the `which` of mio_hip_llm_time_kernel: per
- * layer 0 attn_in, 1 attention (absent when it runs inside attn_in, MIO_ATT_FUSED=1 at load),
- * 2 attn_out, or for an lfm2 short-conv layer 8 conv_in, 9 conv_out; then 3 ffn_in, 4
+ * layer 0 attn_in, 1 attention, 2 attn_out, or for an lfm2 short-conv layer 8 conv_in, 9 conv_out; then 3 ffn_in, 4
  * ffn_down; last 6 lm_head. *n = the count; kinds may be null (count only), else it needs
  * cap >= *n entries. */
 int mio_hip_llm_step_kinds(const mio_hip_llm *m, int *kinds, int cap, int *n);
@@ -208,7 +203,8 @@ int mio_hip_llm_load_ms(const mio_hip_llm *m, double *ms);
 /* Decode steps (one sampled token each) issued since the last generate began, look-ahead
  * included: generate keeps one check interval queued ahead of its end-token poll, so a run
  * that stops at an end token after n_out tokens issued *steps - n_out - 1 steps for nothing
- * (at most check_interval; 0 when it stops at max_tokens). */
+ * (the rest of the end token's interval plus one more: < 2 * check_interval; 0 when it stops
+ * at max_tokens). */
 int mio_hip_llm_steps_issued(const mio_hip_llm *m, int *steps);
 /* Prenet rows the last mio_hip_codec_decode_pcm took from the incremental cache. */
 int mio_hip_codec_last_reused(const mio_hip_codec *c, int *rows);

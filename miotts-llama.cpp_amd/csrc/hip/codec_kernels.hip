@@ -312,171 +312,6 @@ __global__ __launch_bounds__(256 * KG) void gemm_f32_kernel(GemmArgs g) {
                                PRE ? &pre[PRE ? i : 0][PRE ? j : 0] : nullptr);
 }
 
-// ---------------------------------------------------------------- split-bf16 GEMM
-// The same GEMM on the bf16 matrix cores at f32 accuracy: every f32 operand is split
-// exactly into three bf16 pieces x = x0 + x1 + x2 (truncation: x0 keeps the top 8
-// significant bits, x1 the next 8, x2 the last 8 — each remainder is exact in f32), and
-// C += A0 B0 + A0 B1 + A1 B0 + A0 B2 + A1 B1 + A2 B0 (v_mfma_f32_32x32x16_bf16, products exact,
-// f32 sums). The three dropped terms are below 2^-24 of |a b|: f32-level results, a different
-// summation order from the f32 chain. Six bf16 MFMAs (32 cycles each) replace eight f32 ones
-// (64 cycles each) per 16 k. Same tiles, K-groups, staging, tile order and epilogues as
-// gemm_f32_kernel; the operands are split when staged into LDS (3 bf16 planes per operand).
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-
-__device__ __forceinline__ void split3(float x, uint32_t &h0, uint32_t &h1, uint32_t &h2) {
-    const uint32_t u0 = __float_as_uint(x) & 0xFFFF0000u;
-    const float r1 = x - __uint_as_float(u0);
-    const uint32_t u1 = __float_as_uint(r1) & 0xFFFF0000u;
-    const float r2 = r1 - __uint_as_float(u1);
-    h0 = u0 >> 16, h1 = u1 >> 16, h2 = __float_as_uint(r2) >> 16;
-}
-
-template <int KG, int EPI>
-__global__ __launch_bounds__(256 * KG) void gemm_x3_kernel(GemmArgs g) {
-    constexpr int BM = GF_T, BN = GF_T, BK = GF_KD * KG, LDH = BK + 8, NT = 256 * KG;
-    constexpr int AV = BM * BK / 4 / NT, BV = BN * BK / 4 / NT;
-    constexpr int PLANE = (BM + BN) * LDH;  // one bf16 plane of both operands
-    static_assert(AV >= 1 && BV >= 1, "tile");
-    static_assert(2 * 3 * PLANE * 2 >= (KG - 1) * 4 * 16 * 64 * 4, "reduction area");
-    __shared__ __attribute__((aligned(16))) uint16_t smem[2 * 3 * PLANE];
-
-    const int nM = (g.M + BM - 1) / BM, nN = (g.N + BN - 1) / BN, nb = nM * nN, per = (nb + 7) / 8;
-    const int t = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
-    if (t >= nb) return;
-    const int mt = g.m_major ? t / nN : t % nM, nt = g.m_major ? t % nN : t / nM;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int kg = wave >> 2, wm = (wave >> 1) & 1, wn = wave & 1;
-    const int m0 = mt * BM, n0 = nt * BN;
-
-    f32x16 acc;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
-
-    float4 ra0[AV], rb0[BV], ra1[AV], rb1[BV];
-    const bool a_win = g.a_seg != g.K || g.a_row_off != 0 || g.a_rows < g.M;
-    const float *a_base[AV];
-    const float *b_base[BV];
-    bool a_ok[AV], b_ok[BV];
-#pragma unroll
-    for (int i = 0; i < AV; ++i) {
-        const int e = tid + i * NT, m = m0 + e / (BK / 4);
-        a_ok[i] = m < g.M;
-        a_base[i] = g.A + (long)(m + g.a_row_off) * g.a_seg + (e % (BK / 4)) * 4;
-    }
-#pragma unroll
-    for (int i = 0; i < BV; ++i) {
-        const int e = tid + i * NT, n = n0 + e / (BK / 4);
-        b_ok[i] = n < g.N;
-        b_base[i] = g.B + (long)n * g.K + (e % (BK / 4)) * 4;
-    }
-    auto load = [&](int k0, float4 (&ra)[AV], float4 (&rb)[BV]) {
-#pragma unroll
-        for (int i = 0; i < AV; ++i) {
-            const int e = tid + i * NT, m = m0 + e / (BK / 4), k = k0 + (e % (BK / 4)) * 4;
-            bool ok = a_ok[i] && k < g.K;
-            if (a_win && ok) {
-                const int src = m + g.a_row_off + k / g.a_seg;
-                ok = src >= 0 && src < g.a_rows;
-            }
-            ra[i] = ok ? *reinterpret_cast<const float4 *>(a_base[i] + k0) : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-#pragma unroll
-        for (int i = 0; i < BV; ++i) {
-            const int k = k0 + ((tid + i * NT) % (BK / 4)) * 4;
-            rb[i] = (b_ok[i] && k < g.K) ? *reinterpret_cast<const float4 *>(b_base[i] + k0)
-                                         : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-    };
-    // 4 consecutive k of one row -> three 8-byte bf16 quads, one per plane
-    auto put = [&](uint16_t *base, int r, int c4, float4 v) {
-        uint32_t p[3][4];
-        split3(v.x, p[0][0], p[1][0], p[2][0]);
-        split3(v.y, p[0][1], p[1][1], p[2][1]);
-        split3(v.z, p[0][2], p[1][2], p[2][2]);
-        split3(v.w, p[0][3], p[1][3], p[2][3]);
-#pragma unroll
-        for (int q = 0; q < 3; ++q)
-            *reinterpret_cast<uint2 *>(base + q * PLANE + r * LDH + c4 * 4) =
-                make_uint2(p[q][0] | (p[q][1] << 16), p[q][2] | (p[q][3] << 16));
-    };
-    auto store = [&](int buf, const float4 (&ra)[AV], const float4 (&rb)[BV]) {
-        uint16_t *base = smem + buf * 3 * PLANE;
-#pragma unroll
-        for (int i = 0; i < AV; ++i) {
-            const int e = tid + i * NT, r = e / (BK / 4), c4 = e % (BK / 4);
-            float4 v = ra[i];
-            if (g.a_f16) {  // F16 weight: ggml rounds the activation to f16 (exact products)
-                v.x = (float)(_Float16)v.x, v.y = (float)(_Float16)v.y;
-                v.z = (float)(_Float16)v.z, v.w = (float)(_Float16)v.w;
-            }
-            put(base, r, c4, v);
-        }
-#pragma unroll
-        for (int i = 0; i < BV; ++i) {
-            const int e = tid + i * NT, r = e / (BK / 4), c4 = e % (BK / 4);
-            put(base, BM + r, c4, rb[i]);
-        }
-    };
-    auto compute = [&](int buf) {
-        const uint16_t *base = smem + buf * 3 * PLANE;
-        const int ar = (wm * 32 + (lane & 31)) * LDH, br = (BM + wn * 32 + (lane & 31)) * LDH;
-#pragma unroll
-        for (int st = 0; st < GF_KD / 16; ++st) {
-            const int kc = kg * GF_KD + st * 16 + 8 * (lane >> 5);
-            bf16x8 a[3], b[3];
-#pragma unroll
-            for (int q = 0; q < 3; ++q) {
-                a[q] = *reinterpret_cast<const bf16x8 *>(base + q * PLANE + ar + kc);
-                b[q] = *reinterpret_cast<const bf16x8 *>(base + q * PLANE + br + kc);
-            }
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[0], acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1], acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[2], acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0], acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1], acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], acc, 0, 0, 0);
-        }
-    };
-
-    const int nk = (g.K + BK - 1) / BK;
-    load(0, ra0, rb0);
-    if (nk > 1) load(BK, ra1, rb1);
-    store(0, ra0, rb0);
-    __syncthreads();
-    for (int kt = 0; kt < nk; kt += 2) {
-        if (kt + 2 < nk) load((kt + 2) * BK, ra0, rb0);
-        compute(0);
-        if (kt + 1 < nk) store(1, ra1, rb1);
-        __syncthreads();
-        if (kt + 1 >= nk) break;
-        if (kt + 3 < nk) load((kt + 3) * BK, ra1, rb1);
-        compute(1);
-        if (kt + 2 < nk) store(0, ra0, rb0);
-        __syncthreads();
-    }
-
-    if constexpr (KG > 1) {
-        constexpr int SLOT = 16 * 64;
-        float *redbase = reinterpret_cast<float *>(smem);
-        const int sp = wave & 3;
-        if (kg > 0) {
-            float *red = redbase + ((kg - 1) * 4 + sp) * SLOT;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) red[r * 64 + lane] = acc[r];
-        }
-        __syncthreads();
-        if (kg > 0) return;
-#pragma unroll
-        for (int q = 1; q < KG; ++q) {
-            const float *red = redbase + ((q - 1) * 4 + sp) * SLOT;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[r] = acc[r] + red[r * 64 + lane];
-        }
-    }
-    gemm_epilogue<EPI>(g, acc, m0 + wm * 32, n0 + wn * 32, lane);
-}
-
 // ---------------------------------------------------------------- conv1d f16
 // The A operand is the GroupNorm+SiLU activation already rounded to f16 by gn_apply_kernel
 // ([L][Cin], one pass instead of once per tap and per column tile), so staging is a plain
@@ -990,7 +825,7 @@ __global__ __launch_bounds__(256) void cond_gemv_kernel(const float *W, const fl
     if (lane == 0) y[r] = a + b[r];
 }
 
-template <int KG, bool X3, int WTM = 1, int WTN = 1>
+template <int KG, int WTM = 1, int WTN = 1>
 void launch_gemm_kg(const GemmArgs &a, int epi, hipStream_t s) {
     const int bm = GF_T * WTM, bn = GF_T * WTN;
     const long nb = (long)((a.M + bm - 1) / bm) * ((a.N + bn - 1) / bn);
@@ -998,10 +833,7 @@ void launch_gemm_kg(const GemmArgs &a, int epi, hipStream_t s) {
     switch (epi) {
 #define CASE(E)                                                                                  \
     case E:                                                                                      \
-        if constexpr (X3)                                                                        \
-            hipLaunchKernelGGL((gemm_x3_kernel<KG, E>), grid, dim3(256 * KG), 0, s, a);          \
-        else                                                                                     \
-            hipLaunchKernelGGL((gemm_f32_kernel<KG, E, WTM, WTN>), grid, dim3(256 * KG), 0, s, a); \
+        hipLaunchKernelGGL((gemm_f32_kernel<KG, E, WTM, WTN>), grid, dim3(256 * KG), 0, s, a);   \
         break;
         CASE(EPI_STORE)
         CASE(EPI_RESID)
@@ -1027,30 +859,15 @@ int gemm_kgroups(long tiles) {
     return tiles >= 512 ? 1 : tiles >= 256 ? 2 : 4;
 }
 
-// MIO_CODEC_GEMM=x3: split-bf16 matrix cores at f32 accuracy (gemm_x3_kernel); default the
-// exact f32 MFMA chain. Measured at T = 700: codec 5.12 ms with x3 against 3.82 ms (the split
-// staging and its three LDS planes cost more than the matrix cores save at these shapes)
-bool gemm_split_bf16() {
-    static const bool x3 = getenv("MIO_CODEC_GEMM") && std::string(getenv("MIO_CODEC_GEMM")) == "x3";
-    return x3;
-}
-
 void launch_gemm_f32(const GemmArgs &a0, int epi, hipStream_t s) {
     GemmArgs a = a0;
     a.m_major = (long)a.M * a.K > (long)a.N * a.K * 2 ? 1 : 0;  // slab the larger operand
     const long tiles = (long)((a.M + GF_T - 1) / GF_T) * ((a.N + GF_T - 1) / GF_T);
     const int kgs = gemm_kgroups(tiles);
-    if (gemm_split_bf16()) {  // 3 bf16 planes per operand: K-groups 1 and 2 fit the LDS
-        if (kgs == 1)
-            launch_gemm_kg<1, true>(a, epi, s);
-        else
-            launch_gemm_kg<2, true>(a, epi, s);
-        return;
-    }
     switch (kgs) {
-        case 1: launch_gemm_kg<1, false>(a, epi, s); break;
-        case 2: launch_gemm_kg<2, false>(a, epi, s); break;
-        default: launch_gemm_kg<4, false>(a, epi, s); break;
+        case 1: launch_gemm_kg<1>(a, epi, s); break;
+        case 2: launch_gemm_kg<2>(a, epi, s); break;
+        default: launch_gemm_kg<4>(a, epi, s); break;
     }
 }
 
@@ -1061,9 +878,9 @@ int launch_gemm_f32_cfg(const GemmArgs &a0, int epi, int kg, int wt, hipStream_t
     GemmArgs a = a0;
     a.m_major = (long)a.M * a.K > (long)a.N * a.K * 2 ? 1 : 0;
     switch (wt * 10 + kg) {
-        case 111: launch_gemm_kg<1, false, 1, 1>(a, epi, s); break;
-        case 112: launch_gemm_kg<2, false, 1, 1>(a, epi, s); break;
-        case 114: launch_gemm_kg<4, false, 1, 1>(a, epi, s); break;
+        case 111: launch_gemm_kg<1, 1, 1>(a, epi, s); break;
+        case 112: launch_gemm_kg<2, 1, 1>(a, epi, s); break;
+        case 114: launch_gemm_kg<4, 1, 1>(a, epi, s); break;
         default: return -1;
     }
     return 0;

@@ -1,23 +1,13 @@
 // First launch of a decoder layer in the single-token decode step (llama_decode for one
-// token, test-to-speech.cpp:178-185 / :589-596): RMSNorm(x) -> q|k|v dequant-matvec, and,
-// in the same launch, the layer's attention (RoPE, F16 KV append, chunked softmax).
+// token, test-to-speech.cpp:178-185 / :589-596): RMSNorm(x) -> q|k|v dequant-matvec.
 //
-// Matvec workgroups [0, GW): q|k rows (type TQ) on the first g_qk workgroups, v rows (type
-// TV) on the rest; each branch is WG-uniform and runs its own prologue, so neither path
-// merges load counts. FS (layer 0 only): the previous step's sampler runs here when
-// st->pending. Every workgroup reduces the lm_head partials to the same token and
-// dequantizes its embedding row into its x registers while its first weight group is in
-// flight; workgroup 0 also stores x (attn_out's residual) and the token / token ring / EOS
-// flag. pos and step are advanced by layer 0's ffn_in (no kernel before it writes a
-// StepState field it reads).
-//
-// Attention workgroups [GW, GW + n_kv * max_splits) when b.qkv_g is set (the fused launch,
-// attention_role in llm_device.h): they issue their K/V row loads at launch start and wait
-// for their kv head's q|k|v rows, which the matvec workgroups store as data-tagged
-// write-through granules (put_granule). The separate k_attention launch and its boundary
-// disappear from the step, and the K/V load latency hides under the q|k|v weight stream.
-// Attention workgroups come after every matvec workgroup in dispatch order, so a waiting
-// consumer never holds a CU a producer still needs.
+// Matvec workgroups: q|k rows (type TQ) on the first g_qk workgroups, v rows (type TV) on the
+// rest; each branch is WG-uniform and runs its own prologue, so neither path merges load
+// counts. FS (layer 0 only): the previous step's sampler runs here when st->pending. Every
+// workgroup reduces the lm_head partials to the same token and dequantizes its embedding
+// row into its x registers while its first weight group is in flight; workgroup 0 also
+// stores x (attn_out's residual) and the token / token ring / EOS flag. pos and step are
+// advanced by layer 0's ffn_in (no kernel before it writes a StepState field it reads).
 #include "llm_device.h"
 
 #pragma clang fp contract(off)
@@ -25,30 +15,12 @@
 namespace mio {
 namespace {
 
-struct AttArgs {
-    const float *q_norm, *k_norm, *bqkv;
-    _Float16 *kc, *vc;  // this layer's caches
-    int il;
-};
-
 template <int NP, int TQ, int TV, int SU, bool DG, bool FS>
 __global__ __launch_bounds__(MT) void k_attn_in(LlmDims d, const float *norm_w, QMat wq, QMat wk, QMat wv,
-                                                int g_qk, LlmBuffers b, QMat emb, int nblk, AttArgs at) {
+                                                int g_qk, LlmBuffers b, QMat emb, int nblk) {
     constexpr bool kDiag = DG;
     const int o1 = wq.rows, o2 = wq.rows + wk.rows;
     const int GW = matvec_grid_n(d.n_wg, o2 + wv.rows);
-#ifndef MIO_NO_ROLE
-    if ((int)blockIdx.x >= GW) {
-        MIO_TL_BEGIN(b);
-        const int a = (int)blockIdx.x - GW;
-        if (d.hd == 128)
-            attention_role<128>(d, a, at.il, at.q_norm, at.k_norm, at.bqkv, at.kc, at.vc, b);
-        else
-            attention_role<64>(d, a, at.il, at.q_norm, at.k_norm, at.bqkv, at.kc, at.vc, b);
-        MIO_TL_END(b);
-        return;
-    }
-#endif
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __shared__ float rs_[MW];
     __shared__ int ri_[MW];
@@ -85,15 +57,8 @@ __global__ __launch_bounds__(MT) void k_attn_in(LlmDims d, const float *norm_w, 
             }
         }
     };
-    // q|k|v rows: plain (k_attention of the unfused step, diagnostics) and, for the attention
-    // workgroups of this launch, as tagged write-through granules
-    uint32_t tag = 0;
-    if (b.qkv_g) tag = qkv_tag(*b.cfg, b.st, at.il);
     auto put = [&](int row, float v) {
-        if ((threadIdx.x & 63) == 0) {
-            b.qkv[row] = v;
-            if (b.qkv_g) put_granule(b.qkv_g + row, v, tag);
-        }
+        if ((threadIdx.x & 63) == 0) b.qkv[row] = v;
     };
     Frag ga[Cfg<NP, SU>::U], gb[Cfg<NP, SU>::U];
     int lo, hi;
@@ -127,8 +92,7 @@ __global__ __launch_bounds__(MT) void k_attn_in(LlmDims d, const float *norm_w, 
 }
 
 template <bool DG>
-void launch(const LlmDims &d, const LayerW &L, int il, const AttArgs &at, const QMat &tok_embd, const LlmBuffers &b,
-            hipStream_t s) {
+void launch(const LlmDims &d, const LayerW &L, int il, const QMat &tok_embd, const LlmBuffers &b, hipStream_t s) {
     int GW, g_qk;
     attn_in_grid(d, L, GW, g_qk);
     const size_t lds = matvec_lds(d.n_embd);
@@ -136,16 +100,16 @@ void launch(const LlmDims &d, const LayerW &L, int il, const AttArgs &at, const 
     const int un = std::max(max_wave_units(L.wq.rows + L.wk.rows, g_qk, np, 1),
                             max_wave_units(L.wv.rows, GW - g_qk, np, 1));
     const int nblk = lm_head_blocks(d);
-    const int grid = GW + (b.qkv_g ? d.n_kv * d.max_splits : 0);
+    const int grid = GW;
     dispatch_nt(d.n_embd, L.wq.type, [&]<int NP, int TQ>() {
         auto go = [&]<int TV>() {
             dispatch_su<NP>(pick_su(un, NP), [&]<int SU>() {
                 if (il == 0)
                     hipLaunchKernelGGL((k_attn_in<NP, TQ, TV, SU, DG, true>), dim3(grid), dim3(MT), lds, s, d,
-                                       L.attn_norm, L.wq, L.wk, L.wv, g_qk, b, tok_embd, nblk, at);
+                                       L.attn_norm, L.wq, L.wk, L.wv, g_qk, b, tok_embd, nblk);
                 else
                     hipLaunchKernelGGL((k_attn_in<NP, TQ, TV, SU, DG, false>), dim3(grid), dim3(MT), lds, s, d,
-                                       L.attn_norm, L.wq, L.wk, L.wv, g_qk, b, tok_embd, nblk, at);
+                                       L.attn_norm, L.wq, L.wk, L.wv, g_qk, b, tok_embd, nblk);
             });
         };
         if constexpr (TQ == 8) {
@@ -161,13 +125,12 @@ void launch(const LlmDims &d, const LayerW &L, int il, const AttArgs &at, const 
 
 }  // namespace
 
-void launch_attn_in(const LlmDims &d, const LayerW &L, int il, _Float16 *kc, _Float16 *vc, const QMat &tok_embd,
-                    const LlmBuffers &b, bool dg, hipStream_t s) {
-    const AttArgs at{L.q_norm, L.k_norm, L.bqkv, kc, vc, il};
+void launch_attn_in(const LlmDims &d, const LayerW &L, int il, const QMat &tok_embd, const LlmBuffers &b, bool dg,
+                    hipStream_t s) {
     if (dg)
-        launch<true>(d, L, il, at, tok_embd, b, s);
+        launch<true>(d, L, il, tok_embd, b, s);
     else
-        launch<false>(d, L, il, at, tok_embd, b, s);
+        launch<false>(d, L, il, tok_embd, b, s);
 }
 
 }  // namespace mio

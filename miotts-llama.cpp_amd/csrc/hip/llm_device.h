@@ -1169,17 +1169,7 @@ __device__ __forceinline__ float xor_lane(float v) {
 // row: wave-private LDS scratch [HD]; the prepared head is left in row.
 // bias (may be null): the projection bias added in f32 before anything else (qwen2,
 // llama.cpp build_attn_mha's Qcur = ggml_add(Qcur, bq)).
-// SC1: src is read with agent-scope (L1-bypassing) loads: rows handed off inside the launch
-// (the fused attn_in launch's attention workgroups, attention_role).
-template <bool SC1>
-__device__ __forceinline__ float ldf(const float *p) {
-    if constexpr (SC1)
-        return __hip_atomic_load(const_cast<float *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else
-        return *p;
-}
-
-template <int HD, bool SC1 = false>
+template <int HD>
 __device__ void prep_head(const float *src, const float *bias, const float *nw, const float2 *rope,
                           const LlmDims &d, float *row) {
     constexpr int PER = HD / 64;
@@ -1189,7 +1179,7 @@ __device__ void prep_head(const float *src, const float *bias, const float *nw, 
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
         const int p = lane + 64 * i;
-        v[i] = ldf<SC1>(src + p);
+        v[i] = src[p];
         if (bias) v[i] = v[i] + bias[p];
         w[i] = d.qk_norm ? nw[p] : 1.0f;
         cs[i] = p < HD / 2 ? rope[p] : make_float2(0.0f, 0.0f);
@@ -1376,141 +1366,6 @@ __device__ void attend_chunk(const float (*qs)[HD], const h8 (&kr)[AttCfg<HD>::I
         float *o = dst + g * g_stride;
         o[dd] = O;
         if (dd == 0) o[HD] = M[g], o[HD + 1] = L;
-    }
-}
-
-// ------------------------------------------------------------------ fused attention role
-// s_memrealtime ticks (100 MHz) a consumer waits for its rows before it gives up and flags
-// StepState.fault (100 ms; a step takes < 1 ms): a broken hand-off ends the launch instead
-// of hanging the GPU.
-constexpr uint64_t kHandoffTimeout = 10000000ull;
-
-// Tag of the q|k|v granules one attn_in launch writes: unique among consecutive launches
-// (every launch rewrites every granule, so a granule's stale tag is always the previous
-// launch's): generation epoch (SampleCfg.epoch, >= 1, bumped by every llm_begin / eval),
-// decode step (st->step + pending: constant over the layers of a step), layer.
-__device__ __forceinline__ uint32_t qkv_tag(const SampleCfg &sc, const StepState *st, int il) {
-    const uint32_t step = (uint32_t)(st->step + st->pending);
-    return ((sc.epoch & 0x7FFu) << 21) | ((step & 0x7FFFu) << 6) | ((uint32_t)il & 63u);
-}
-// One q|k|v row value as a data-tagged granule {value, tag}: ONE 8-byte write-through store
-// (no separate flag, no wait for the store before any signal).
-__device__ __forceinline__ void put_granule(uint2 *g, float v, uint32_t tag) {
-    const uint64_t w = ((uint64_t)tag << 32) | __float_as_uint(v);
-    __hip_atomic_store(reinterpret_cast<uint64_t *>(g), w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Attention role of the fused attn_in launch: the workgroups past the matvec grid, a ->
-// (chunk a / n_kv, kv head a % n_kv), chunks past the decode position exit at once. The K/V
-// rows of the chunk are loaded first (they do not depend on this launch); then the
-// workgroup's threads load the (G + 2) * hd q|k|v granules of its kv head with agent-scope
-// (L1-bypassing) loads, each re-polling its own until the tag is this launch's, stage the
-// values in LDS and run k_attention's head preparation, K/V append and chunk softmax: the
-// same arithmetic, the same partial records for k_attn_out. G is a run-time value: heads are
-// swept two at a time by one attend_chunk<HD, 2> instantiation (an odd G's last head paired
-// with its own copy), per-head arithmetic unchanged.
-template <int HD>
-__device__ void attention_role(const LlmDims &d, int a, int il, const float *q_norm, const float *k_norm,
-                               const float *bqkv, _Float16 *kc, _Float16 *vc, const LlmBuffers &b) {
-    using C = AttCfg<HD>;
-    constexpr int PER = HD / 64, GMAX = 8;
-    __shared__ float qs[GMAX + 1][HD];
-    __shared__ float knew[HD], vnew[HD];
-    __shared__ float wres[ATT_NW * 2 * (HD + 2)];
-    __shared__ float rows[(GMAX + 2) * HD];  // the kv head's q rows | k row | v row
-    __shared__ int fault_;
-    const int G = d.n_head / d.n_kv;
-    const int kvh = a % d.n_kv, ch = a / d.n_kv;
-    const int pos = cur_pos(b.st, d);
-    const int t0 = ch * ATT_CHUNK;
-    if (t0 > pos) return;
-    const int lane = MIO_TIDX & 63, wave = MIO_TIDX >> 6;
-    h8 kr[C::IT], vr[C::IT];
-    load_kv_rows<HD>(kc + (size_t)kvh * d.n_ctx * HD, vc + (size_t)kvh * d.n_ctx * HD, t0, pos, kr, vr);
-    const uint32_t tag = qkv_tag(*b.cfg, b.st, il);
-    if (MIO_TIDX == 0) fault_ = 0;
-    {
-        const int Q = d.n_head * HD, nr = (G + 2) * HD;
-        const uint64_t start = __builtin_amdgcn_s_memrealtime();
-        for (int e = MIO_TIDX; e < nr; e += ATT_NT) {
-            // granule index: q rows of this kv head's G heads, then its k row, then its v row
-            const int gi = e < G * HD ? kvh * G * HD + e
-                                      : (e < (G + 1) * HD ? Q + kvh * HD + (e - G * HD)
-                                                          : Q + d.n_kv * HD + kvh * HD + (e - (G + 1) * HD));
-            uint64_t *src = reinterpret_cast<uint64_t *>(b.qkv_g + gi);
-            uint64_t w = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            while ((uint32_t)(w >> 32) != tag) {
-                __builtin_amdgcn_s_sleep(1);
-                if (__builtin_amdgcn_s_memrealtime() - start > kHandoffTimeout) {
-                    fault_ = 1;
-                    break;
-                }
-                w = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            rows[e] = __uint_as_float((uint32_t)w);
-        }
-    }
-    lds_barrier();
-    if (fault_) {
-        if (MIO_TIDX == 0) __hip_atomic_store(&b.st->fault, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return;
-    }
-    const float2 *rope = b.rope + (size_t)pos * (HD / 2);
-    const bool owner = pos < t0 + ATT_CHUNK;
-    for (int hh = wave; hh < G + (owner ? 1 : 0); hh += ATT_NW) {
-        const bool isk = hh == G;
-        float vv[PER];
-        if (isk) {
-            const size_t vo = (size_t)(d.n_head + d.n_kv + kvh) * HD;
-#pragma unroll
-            for (int i = 0; i < PER; ++i) {
-                vv[i] = rows[(G + 1) * HD + lane + 64 * i];
-                if (bqkv) vv[i] = vv[i] + bqkv[vo + lane + 64 * i];
-            }
-        }
-        const size_t so = isk ? (size_t)(d.n_head + kvh) * HD : (size_t)(kvh * G + hh) * HD;
-        prep_head<HD>(rows + (size_t)hh * HD, bqkv ? bqkv + so : nullptr, isk ? k_norm : q_norm, rope, d,
-                      isk ? knew : qs[hh]);
-        if (isk) {
-            _Float16 *kd = kc + ((size_t)kvh * d.n_ctx + pos) * HD;
-            _Float16 *vd = vc + ((size_t)kvh * d.n_ctx + pos) * HD;
-#pragma unroll
-            for (int i = 0; i < PER; ++i) {
-                const int p = lane + 64 * i;
-                const float vr16 = f16r(vv[i]);
-                vnew[p] = vr16;
-                kd[p] = (_Float16)knew[p];
-                vd[p] = (_Float16)vr16;
-            }
-        }
-    }
-    lds_barrier();
-    if (G & 1) {
-        for (int e = MIO_TIDX; e < HD; e += ATT_NT) qs[G][e] = qs[G - 1][e];
-        lds_barrier();
-    }
-    if (owner) {
-        const int sl = MIO_TIDX / C::LP, lp = lane % C::LP, r = pos - t0;
-        if (sl == r % C::NS) {
-            h8 kn, vn;
-#pragma unroll
-            for (int i = 0; i < 8; ++i) kn[i] = (_Float16)knew[lp * 8 + i], vn[i] = (_Float16)vnew[lp * 8 + i];
-#pragma unroll
-            for (int it = 0; it < C::IT; ++it)
-                if (it == r / C::NS) kr[it] = kn, vr[it] = vn;
-        }
-    }
-    float *dst = b.part + ((size_t)(kvh * G) * d.max_splits + ch) * C::REC;
-    const size_t gs = (size_t)d.max_splits * C::REC;
-    for (int g0 = 0; g0 < G; g0 += 2) {
-        // opaque to the optimizer: otherwise the f16 -> f32 conversions of every K/V row are
-        // hoisted out of this loop (64 more live registers, two workgroups no longer fit a CU)
-#pragma unroll
-        for (int it = 0; it < C::IT; ++it) asm volatile("" : "+v"(kr[it]), "+v"(vr[it]));
-        // an odd G's last head runs as a pair with its copy (qs[G] = qs[G - 1]) writing the same
-        // record twice (g_stride 0; equal values): one attend_chunk instantiation only
-        attend_chunk<HD, 2>(qs + g0, kr, vr, t0, pos, d.scale, reinterpret_cast<float (*)[2][HD + 2]>(wres),
-                            dst + g0 * gs, g0 + 1 < G ? gs : 0);
     }
 }
 

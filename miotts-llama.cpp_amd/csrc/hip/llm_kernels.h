@@ -44,7 +44,6 @@ struct StepState {
     int token;    // token being decoded
     int done;     // set once an end token was sampled
     int pending;  // 1: lm_head partials of this step await the sampler
-    int fault;    // != 0: a kernel gave up waiting for an in-launch hand-off (never expected)
 };
 
 struct SampleCfg {
@@ -56,7 +55,6 @@ struct SampleCfg {
     int n_force;
     int *out_tokens;     // [max_steps] sampled/forced next token per step
     int max_steps;
-    uint32_t epoch;      // >= 1, new for every generation / eval (q|k|v granule tags)
 };
 
 // lfm2 gated short conv: kernel width (shortconv.l_cache) and the ring of bx values kept per
@@ -98,8 +96,6 @@ struct LlmBuffers {
     unsigned long long *trace;  // optional: per-kernel checkpoint timestamps (workgroup 0, thread 0)
     unsigned long long *tl;     // optional: step timeline {min start, max end} per launch (s_memrealtime)
     int seq;                    // launch index within the step (timeline slot)
-    uint2 *qkv_g;  // q|k|v rows as data-tagged granules {value, tag} for the attention workgroups
-                   // of the fused attn_in launch, or null: attention is a launch of its own
     float *ring;   // lfm2: [n_layer][kConvSlots][n_embd] short-conv inputs bx by position
 };
 
@@ -188,10 +184,10 @@ size_t matvec_lds(int K);
 // and the single-group size that covers them (0 = streaming groups)
 int max_wave_units(int rows, int grid, int np, int nm);
 int pick_su(int units, int np);
-// Layer il's first launch (llm_attn_in.hip): RMSNorm + q|k|v matvec, plus the attention
-// workgroups when b.qkv_g is set; kc / vc: this layer's caches.
-void launch_attn_in(const LlmDims &d, const LayerW &L, int il, _Float16 *kc, _Float16 *vc, const QMat &tok_embd,
-                    const LlmBuffers &b, bool dg, hipStream_t s);
+// Layer il's first launch (llm_attn_in.hip): RMSNorm + q|k|v matvec (+ layer 0: the
+// previous step's sampler).
+void launch_attn_in(const LlmDims &d, const LayerW &L, int il, const QMat &tok_embd, const LlmBuffers &b, bool dg,
+                    hipStream_t s);
 // y = W x with x re-quantized to the vec_dot_type (parity test of the matvec kernels).
 void launch_debug_matvec(const QMat &W, const float *x, float *y, int n_wg, hipStream_t s);
 // y[t][rows] = W x[t] for nt tokens on the int8-MFMA multi-token matmul (act: scratch of

@@ -42,8 +42,8 @@ namespace mio {
 namespace {
 
 
-// k_attn_in (RMSNorm + q|k|v matvec, with the attention workgroups of the fused launch)
-// lives in llm_attn_in.hip.
+// k_attn_in (RMSNorm + q|k|v matvec, + layer 0: the previous step's sampler) lives in
+// llm_attn_in.hip.
 
 // residual rows of this wave (<= 64) in one register: lane i holds x[lo + i]
 __device__ inline float load_resid(const float *x, int lo, int hi) {
@@ -463,7 +463,7 @@ void launch_step_kernel(int which, const LlmDims &d, const LayerW *layers, int i
     auto go_dg = [&]<bool DG>() {
     switch (which) {
         case 0: {
-            launch_attn_in(d, layers[il], il, kcache + il * layer_kv, vcache + il * layer_kv, tok_embd, b, DG, s);
+            launch_attn_in(d, layers[il], il, tok_embd, b, DG, s);
             break;
         }
         case 1: {
@@ -515,9 +515,7 @@ void launch_step_kernel(int which, const LlmDims &d, const LayerW *layers, int i
             V.wk = qmat_rows(L.in_proj, 2 * n, 0);
             V.wv = qmat_rows(L.in_proj, 2 * n, n);
             V.q_norm = V.k_norm = V.bqkv = nullptr;
-            LlmBuffers bv = b;
-            bv.qkv_g = nullptr;  // no attention workgroups
-            launch_attn_in(d, V, il, nullptr, nullptr, tok_embd, bv, DG, s);
+            launch_attn_in(d, V, il, tok_embd, b, DG, s);
             break;
         }
         case 9: {

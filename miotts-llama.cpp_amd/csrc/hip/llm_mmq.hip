@@ -445,139 +445,6 @@ __global__ __launch_bounds__(MMQ_NT) void k_mmq(MmqSeg s0, MmqSeg s1, MmqSeg s2,
     }
 }
 
-// ---------------------------------------------------------------- persistent one-pass Q8_0
-// The batched decode (<= 32 tokens, one token tile) streams every weight once, so a launch is
-// bound by how many weight bytes each CU keeps in flight. k_mmq runs one 8-wave workgroup
-// per CU (its registers) and one tile per workgroup: after a tile's loads land nothing is in
-// flight until the next workgroup starts, ~1.5 TB/s. Here a workgroup stays resident and
-// walks tiles ti = blockIdx.x + j gridDim.x: the activation codes of slot k and the tile's
-// scales are loaded once; every weight register is refilled with the next tile's block right
-// after the MFMA that read it (and each scale after its multiply), so the next tile's weights
-// stream during this tile's float math, LDS reduction and epilogue. The slot partials use
-// two LDS buffers (one barrier per tile). Same per-slot arithmetic as q80_sum (bit-exact).
-struct Q80Tile {
-    const int8_t *q;     // weight codes of this lane's row (slot blocks at q + b * 32 + 16 h)
-    const uint16_t *d;   // its block scales
-    int nb;              // blocks per row
-};
-
-template <int NSEG>
-__device__ __forceinline__ Q80Tile q80_tile(const MmqSeg &s0, const MmqSeg &s1, const MmqSeg &s2, const QMat &up,
-                                            bool use_up, int ti, int &row0, int &rows, int &out_off) {
-    const MmqSeg *sg = &s0;
-    if constexpr (NSEG > 1) {
-        if (ti >= s0.tiles) {
-            ti -= s0.tiles, sg = &s1;
-            if constexpr (NSEG > 2)
-                if (ti >= s1.tiles) ti -= s1.tiles, sg = &s2;
-        }
-    }
-    const QMat &W = use_up ? up : sg->w;
-    row0 = ti * RT, rows = sg->w.rows, out_off = sg->out_off;
-    const int row = min(row0 + (int)(threadIdx.x & 31), rows - 1);
-    const int nb = W.k >> 5;
-    return Q80Tile{(const int8_t *)W.p0 + (size_t)row * W.k, (const uint16_t *)W.p1 + (size_t)row * nb, nb};
-}
-
-template <int NSEG, int MODE>
-__global__ __launch_bounds__(MMQ_NT) void k_mmq_q80p(MmqSeg s0, MmqSeg s1, MmqSeg s2, MmqArgs a) {
-    constexpr int NV = MODE == MMQ_SWIGLU ? 2 : 1;
-    extern __shared__ __attribute__((aligned(16))) char lds[];
-    float *red = reinterpret_cast<float *>(lds);   // [2 buffers][NV][8 waves][64][16]
-    float *da = red + 2 * NV * MMQ_NT * 16;         // [K / 32][32 tokens]
-    const int lane = threadIdx.x & 63, h = lane >> 5;
-    const int k = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    int tiles = s0.tiles;
-    if constexpr (NSEG > 1) tiles += s1.tiles;
-    if constexpr (NSEG > 2) tiles += s2.tiles;
-    int ti = blockIdx.x;
-    if (ti >= tiles) return;  // grid <= tiles (host), never taken
-
-    // slot k's activation codes: the same for every tile
-    const int8_t *aq = act_codes(a, 0);
-    const int nb = a.K >> 5;
-    v4i act[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) act[i] = act16(aq, min(8 * k + i, nb - 1) * 32 + 16 * h);
-    // the first tile's weights and scales
-    int row0, rows, out_off;
-    v4i w[NV][8];
-    float dw[NV][8];
-    // slot k's blocks of a tile: this lane's 16-byte pieces at (b * 32 + 16 h) from the row's
-    // codes base (b clamped), scales at b
-    auto fetch = [&](const Q80Tile &q, int v, int i) {
-        const int b = min(8 * k + i, q.nb - 1);
-        w[v][i] = *reinterpret_cast<const v4i *>(q.q + (size_t)b * 32 + 16 * h);
-        dw[v][i] = h2f(q.d[b]);
-    };
-#pragma unroll
-    for (int v = 0; v < NV; ++v) {
-        const Q80Tile q = q80_tile<NSEG>(s0, s1, s2, a.w_up, v == 1, ti, row0, rows, out_off);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) fetch(q, v, i);
-    }
-    stage_act<8>(a, 0, a.K, da);
-
-    for (int j = 0; ti < tiles; ti += gridDim.x, ++j) {
-        q80_tile<NSEG>(s0, s1, s2, a.w_up, false, ti, row0, rows, out_off);
-        const int tn = ti + (int)gridDim.x < tiles ? ti + (int)gridDim.x : ti;  // next tile (or a reload)
-        float *rb = red + (size_t)(j & 1) * NV * MMQ_NT * 16;
-#pragma unroll
-        for (int v = 0; v < NV; ++v) {
-            int r0n, rsn, oon;
-            const Q80Tile qn = q80_tile<NSEG>(s0, s1, s2, a.w_up, v == 1, tn, r0n, rsn, oon);
-            Tree<3> inner;
-            auto slot1 = [&]<int i>() {
-                const int b = 8 * k + i;
-                v16f x = {};
-                if (b < nb) {  // wave-uniform
-                    const v16i c = __builtin_amdgcn_mfma_i32_32x32x32_i8(act[i], w[v][i], v16i{}, 0, 0, 0);
-                    const float d = dw[v][i];
-                    fetch(qn, v, i);  // refill: the next tile's block i streams from here on
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) x[r] = (float)c[r] * (d * da[b * TT + tok_of(lane, r)]);
-                } else {
-                    fetch(qn, v, i);
-                }
-                const v16f acc = v16f{} + x;
-                inner.template push<i>(acc);
-                // one slot at a time: hoisting the next slots' MFMAs (and keeping their results
-                // live) spilled the refill registers
-                __builtin_amdgcn_sched_barrier(0);
-            };
-            slot1.template operator()<0>();
-            slot1.template operator()<1>();
-            slot1.template operator()<2>();
-            slot1.template operator()<3>();
-            slot1.template operator()<4>();
-            slot1.template operator()<5>();
-            slot1.template operator()<6>();
-            slot1.template operator()<7>();
-            slot_store(inner.result, rb + (size_t)v * MMQ_NT * 16);
-        }
-        __syncthreads();  // slot partials of this tile visible; the other buffer is free again
-        // epilogue on every wave: wave k sums the 8 slots (row_total's tree, as slot_sum) of
-        // accumulator registers r = 2k, 2k + 1 and stores them
-        const int orow = row0 + (lane & 31);
-#pragma unroll
-        for (int rr = 0; rr < 2; ++rr) {
-            const int r = 2 * k + rr, t = tok_of(lane, r);
-            auto total = [&](const float *src) {
-                float sl[8];
-#pragma unroll
-                for (int q = 0; q < 8; ++q) sl[q] = src[((size_t)q * 64 + lane) * 16 + r];
-                return ((sl[0] + sl[1]) + (sl[2] + sl[3])) + ((sl[4] + sl[5]) + (sl[6] + sl[7]));
-            };
-            const float y = total(rb);
-            if (orow >= rows || t >= a.nt) continue;
-            float *o = a.out + (size_t)t * a.ld + out_off + orow;
-            if constexpr (MODE == MMQ_STORE) *o = y;
-            else if constexpr (MODE == MMQ_RESID) *o = y + *o;
-            else *o = silu_f(y) * total(rb + MMQ_NT * 16);
-        }
-    }
-}
-
 }  // namespace
 
 size_t mmq_lds(int type, int K, int mode) {
@@ -602,40 +469,10 @@ static void allow_lds_mmq(const void *kern) {
 int mmq_tiles(int rows) { return (rows + RT - 1) / RT; }
 
 // types: {T0, T1, T2} (-1 = segment unused); mode MMQ_*.
-// MIO_MMQ_PERSIST=1: k_mmq_q80p for the one-pass Q8_0 launches of <= 32 tokens. Off by
-// default: measured slower at 8 streams of the 2.6B Q8_0 (3.17 vs 2.99 ms per step with q|k|v
-// on the matrix cores, 3.54 vs 3.31 adding O and gate|up; profiles/r03_batch8_persist_ab.txt)
-static bool mmq_persist() {
-    static const bool on = getenv("MIO_MMQ_PERSIST") && getenv("MIO_MMQ_PERSIST")[0] == '1';
-    return on;
-}
-
 void launch_mmq(const MmqSeg *seg, const int *types, int nseg, int mode, const MmqArgs &a, hipStream_t s) {
     MmqSeg sg[3] = {seg[0], nseg > 1 ? seg[1] : MmqSeg{}, nseg > 2 ? seg[2] : MmqSeg{}};
     int tiles = 0;
     for (int i = 0; i < nseg; ++i) tiles += sg[i].tiles;
-    bool q80 = true;
-    for (int i = 0; i < nseg; ++i) q80 = q80 && types[i] == 8;
-    if (mmq_persist() && q80 && a.nt <= TT && a.K <= 2048) {
-        static int n_cu = [] {
-            int dev = 0, n = 0;
-            hipGetDevice(&dev);
-            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
-            return n > 0 ? n : 256;
-        }();
-        const int NV = mode == MMQ_SWIGLU ? 2 : 1;
-        const size_t lds = (size_t)2 * NV * MMQ_NT * 16 * sizeof(float) + (size_t)(a.K / 32) * TT * sizeof(float);
-        const dim3 grid(std::min(tiles, n_cu));
-        auto launch = [&](auto kern) {
-            if (lds > 64 * 1024) allow_lds_mmq(reinterpret_cast<const void *>(kern));
-            hipLaunchKernelGGL(kern, grid, dim3(MMQ_NT), lds, s, sg[0], sg[1], sg[2], a);
-        };
-        if (nseg == 3) launch(k_mmq_q80p<3, MMQ_STORE>);
-        else if (mode == MMQ_STORE) launch(k_mmq_q80p<1, MMQ_STORE>);
-        else if (mode == MMQ_RESID) launch(k_mmq_q80p<1, MMQ_RESID>);
-        else launch(k_mmq_q80p<1, MMQ_SWIGLU>);
-        return;
-    }
     const dim3 grid(tiles, (a.nt + TT - 1) / TT);
     size_t lds = 0;
     for (int i = 0; i < nseg; ++i) lds = std::max(lds, mmq_lds(types[i], a.K, mode));

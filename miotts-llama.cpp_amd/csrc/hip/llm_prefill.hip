@@ -412,80 +412,16 @@ __device__ __forceinline__ void act_store(const ActPre<NP> &ap, const char *act,
     lds_barrier();
 }
 
-// The same records produced inside a matvec launch, ONE WAVE PER TOKEN (batched decode and
-// short prefill chunks: no k_bt_quant launch, no boundary before the matvec): wave w quantizes
-// tokens w, w + 8, ... of src (RMSNorm * norm_w first when norm_w is set) straight into the
-// token's LDS record while the workgroup's first weight rows are in flight. The arithmetic is
-// the workgroup prologue's (rmsnorm_quant / plain_quant), replayed by one wave: the sum of
-// squares accumulates per virtual thread tid = 64 vw + lane over its elements (tid + i MT) * 4
-// in order, each virtual wave reduces by the same DPP tree (wave_sum_d) and the 8 partial sums
-// add in wave order as block_sum does; each superblock / block is quantized by q8k_store /
-// q80_store as any wave of the workgroup would. Records equal k_bt_quant's bit for bit.
-// elements e..e+3 of the quantizer input: (x * scale) * w, or x
-__device__ __forceinline__ void wq_val4(const float *x, const float *norm_w, float scale, int e, float (&v)[4]) {
-    const float4 xv = ld4(x + e);
-    if (norm_w) {
-        const float4 w = ld4(norm_w + e);
-        float t;
-        t = xv.x * scale, v[0] = t * w.x;
-        t = xv.y * scale, v[1] = t * w.y;
-        t = xv.z * scale, v[2] = t * w.z;
-        t = xv.w * scale, v[3] = t * w.w;
-    } else {
-        v[0] = xv.x, v[1] = xv.y, v[2] = xv.z, v[3] = xv.w;
-    }
-}
-
-template <int XV>
-__device__ __forceinline__ void wave_quant(const float *x, const float *norm_w, int K, float eps, bool kq, const ActL &a) {
-    const int lane = threadIdx.x & 63;
-    float scale = 1.0f;
-    if (norm_w) {
-        // branch-free loads (clamped address, zeroed past K) so all 8 x XV sit in one block
-        double tot = 0.0;
-#pragma unroll
-        for (int vw = 0; vw < MW; ++vw) {
-            double acc = 0.0;
-#pragma unroll
-            for (int i = 0; i < XV; ++i) {
-                const int e = (vw * 64 + lane + i * MT) * 4;
-                const float4 l = ld4(x + min(e, K - 4));
-                const float4 v = e < K ? l : make_float4(0.f, 0.f, 0.f, 0.f);
-                if (e < K) {
-                    acc += (double)(v.x * v.x);
-                    acc += (double)(v.y * v.y);
-                    acc += (double)(v.z * v.z);
-                    acc += (double)(v.w * v.w);
-                }
-            }
-            tot += wave_sum_d(acc);
-        }
-        scale = rms_scale(tot, K, eps);
-    }
-    if (kq) {
-        for (int b = 0; b < K / 256; ++b) {
-            float v[4];
-            wq_val4(x, norm_w, scale, b * 256 + 4 * lane, v);
-            q8k_store(v, abs_max4(v), b, a);
-        }
-    } else {
-        const int nb = K / 32;
-        for (int b0 = 0; b0 < nb; b0 += 8) {
-            const int b = b0 + (lane >> 3);
-            const bool ok = b < nb;
-            float v[4];
-            wq_val4(x, norm_w, scale, min(b, nb - 1) * 32 + 4 * (lane & 7), v);
-            q80_store(v, b, ok, a);
-        }
-    }
-}
-
 // In-launch RMSNorm + quantization with the inputs loaded AHEAD of the weights (batched
 // decode, K <= 2048, nt <= 8 tokens: wave t quantizes token t). The token row and the norm
-// weights sit in the registers wave_quant<1> reads them into (lane l, register vw: elements
+// weights sit in registers (lane l, register vw: elements
 // vw * 256 + 4 l .. +3, i.e. superblock vw / Q8_0 blocks 8 vw .. 8 vw + 7), issued before the
 // first weight group, so the quantization waits only for them (in-order vmcnt) and never
-// re-reads the row; the arithmetic and order are wave_quant's, so the records equal
+// re-reads the row. The arithmetic is the workgroup prologue's (rmsnorm_quant), replayed by one
+// wave: the sum of squares accumulates per virtual thread tid = 64 vw + lane over its elements
+// (tid + i MT) * 4 in order, each virtual wave reduces by the same DPP tree (wave_sum_d) and
+// the 8 partial sums add in wave order as block_sum does; each superblock / block is quantized
+// by q8k_store / q80_store as any wave of the workgroup would, so the records equal
 // k_bt_quant's bit for bit. Saves the k_bt_quant launch in front of the matvec.
 struct XPre {
     float4 x[MW], w[MW];
@@ -549,20 +485,6 @@ __device__ __forceinline__ void xpre_quant(const XPre &xp, int K, float eps, boo
                 }
         }
     }
-    lds_barrier();
-}
-
-// The prologue of a matvec launch over nt tokens: quantize in-launch (fq, wave_quant) or copy
-// the records k_bt_quant wrote.
-template <int XV>
-__device__ __forceinline__ void prologue_act(int fq, const float *src, const float *norm_w, int K, float eps, bool kq,
-                             const char *act, char *smem, int nt) {
-    if (!fq) {
-        prologue_copy(act, K, smem, nt);
-        return;
-    }
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    for (int t = w; t < nt; t += MW) wave_quant<XV>(src + (size_t)t * K, norm_w, K, eps, kq, carve_t(smem, K, t).a);
     lds_barrier();
 }
 
@@ -661,7 +583,7 @@ __device__ inline void store_resid_b(const Resid &r, float *lds, int nt, int rpw
 // ------------------------------------------------------------------ kernels
 template <int NP, int TQ, int TV, int FQ = 0>
 __global__ __launch_bounds__(MT) void k_pf_attn_in(LlmDims d, const float *norm_w, QMat wq, QMat wk, QMat wv,
-                                                   int g_qk, PrefillBuffers pb, int nt, int fq) {
+                                                   int g_qk, PrefillBuffers pb, int nt) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int K = d.n_embd, QD = (d.n_head + 2 * d.n_kv) * d.hd;
     const int lane = threadIdx.x & 63;
@@ -673,7 +595,7 @@ __global__ __launch_bounds__(MT) void k_pf_attn_in(LlmDims d, const float *norm_
         if constexpr (FQ == 2)
             xpre_quant(xp, K, d.eps, TQ != 8, smem, nt);
         else
-            prologue_act<NP>(fq, pb.x, norm_w, K, d.eps, TQ != 8, pb.act, smem, nt);
+            prologue_copy(pb.act, K, smem, nt);
     };
     int lo, hi;
     if ((int)blockIdx.x < g_qk) {
@@ -854,7 +776,7 @@ __global__ __launch_bounds__(MT, MIO_BT_MINB) void k_pf_attn_out(LlmDims d, QMat
 // FQ = 2: RMSNorm + quantization in the launch from inputs loaded ahead of the weights (xpre)
 template <int NP, int T, int FQ = 0>
 __global__ __launch_bounds__(MT, MIO_BT_MINB) void k_pf_ffn_in(LlmDims d, const float *norm_w, QMat gate, QMat up,
-                                                  PrefillBuffers pb, int nt, int fq) {
+                                                  PrefillBuffers pb, int nt) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int K = d.n_embd;
     int lo, hi;
@@ -864,38 +786,32 @@ __global__ __launch_bounds__(MT, MIO_BT_MINB) void k_pf_ffn_in(LlmDims d, const 
     if constexpr (FQ == 2)
         xpre_issue(pb.x, norm_w, K, nt, xp);
     else
-        act_issue<NP>(pb.act, K, nt, ap);  // unconditional (in bounds; unused with fq): keeps ap in registers
+        act_issue<NP>(pb.act, K, nt, ap);
     Frag ga[CfgB<T, NP, 2>::U], gb[CfgB<T, NP, 2>::U];
     load_first_b<T, NP, 2>(gate, up, lo, hi, ga, gb);
     if constexpr (FQ == 2)
         xpre_quant(xp, K, d.eps, T != 8, smem, nt);
-    else if (!fq)
-        act_store<NP>(ap, pb.act, K, smem, nt);
     else
-        prologue_act<NP>(fq, pb.x, norm_w, K, d.eps, T != 8, pb.act, smem, nt);
+        act_store<NP>(ap, pb.act, K, smem, nt);
     stream_rows_b<T, NP, 2>(gate, up, lo, hi, ga, gb, smem, nt, [&](int row, int t, float g, float u) {
         pb.h[(size_t)t * d.n_ff + row] = silu_f(g) * u;
     });
 }
 
 template <int NP, int T>
-__global__ __launch_bounds__(MT) void k_pf_ffn_down(LlmDims d, QMat down, PrefillBuffers pb, int nt, int rpw,
-                                                    int fq) {
+__global__ __launch_bounds__(MT) void k_pf_ffn_down(LlmDims d, QMat down, PrefillBuffers pb, int nt, int rpw) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int K = down.k, E = d.n_embd;
     int lo, hi;
     wave_range(d, down.rows, lo, hi);
     const Resid rr = load_resid_b(pb.x, E, lo, hi, nt, rpw);
     ActPre<NP> ap;
-    act_issue<NP>(pb.act, K, nt, ap);  // unconditional (in bounds; unused with fq): keeps ap in registers
+    act_issue<NP>(pb.act, K, nt, ap);
     Frag ga[CfgB<T, NP, 1>::U], gb[CfgB<T, NP, 1>::U];
     load_first_b<T, NP, 1>(down, down, lo, hi, ga, gb);
     float *res = resid_lds(smem, K, nt, rpw);
     store_resid_b(rr, res, nt, rpw);
-    if (!fq)
-        act_store<NP>(ap, pb.act, K, smem, nt);
-    else
-        prologue_act<NP>(fq, pb.h, nullptr, K, d.eps, T != 8, pb.act, smem, nt);
+    act_store<NP>(ap, pb.act, K, smem, nt);
     stream_rows_b<T, NP, 1>(down, down, lo, hi, ga, gb, smem, nt, [&](int row, int t, float v, float) {
         const float r = res[t * rpw + row - lo];
         pb.x[(size_t)t * E + row] = v + r;
@@ -1162,12 +1078,6 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
         return mmq_all || (nt <= 8 && mmq_env < 0 && ((mask >> kind) & 1));
     };
     const bool mmq = mmq_all;
-    // MIO_FUSED_QUANT=1: dot4 launches of <= 16 tokens quantize their RMSNorm / plain inputs
-    // themselves (one wave per token, wave_quant) instead of behind a k_bt_quant launch. Off:
-    // measured slower (8 streams, 1.7B: 2.47 vs 2.23 ms per step; every workgroup re-reads all
-    // tokens' inputs twice)
-    static const bool fq_env = getenv("MIO_FUSED_QUANT") && getenv("MIO_FUSED_QUANT")[0] == '1';
-    const int fq = (!mmq && fq_env && nt <= 16) ? 1 : 0;
     // MIO_BT_FQ (bits: 1 attn_in, 2 ffn_in; default below): launches of <= 8 tokens over K <= 2048
     // RMSNorm + quantize in the launch from inputs loaded ahead of the weights (xpre), on the
     // dot4 engine, instead of behind a k_bt_quant launch (and, for q|k|v, on the matrix cores).
@@ -1179,7 +1089,7 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
     static const int fq2_env = getenv("MIO_BT_FQ") ? atoi(getenv("MIO_BT_FQ")) : -1;
     auto fq2 = [&](int kind, int type) {
         const bool on = fq2_env >= 0 ? ((fq2_env >> kind) & 1) != 0 : (kind == 0 || type == 8);
-        return !fq && !mmq && nt <= MW && pick_np(d.n_embd) == 1 && on;
+        return !mmq && nt <= MW && pick_np(d.n_embd) == 1 && on;
     };
     // MIO_BT_ATT=0: the batched decode step uses k_pf_rope + k_pf_attention (A/B)
     static const bool bt_att = !(getenv("MIO_BT_ATT") && getenv("MIO_BT_ATT")[0] == '0');
@@ -1210,7 +1120,7 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
         } else {
             _Float16 *kc = kcache + il * layer_kv, *vc = vcache + il * layer_kv;
             const bool fa = fq2(0, L.wq.type);
-            if (!fa && (!fq || use_mmq(0, L.wq.type)))
+            if (!fa)
                 launch_quant(d, 0, pb.x, d.n_embd, L.attn_norm, L.wq.type != 8, pb, nt, s);
             if (!fa && use_mmq(0, L.wq.type)) {
                 const MmqSeg sg[3] = {{L.wq, mmq_tiles(L.wq.rows), 0}, {L.wk, mmq_tiles(L.wk.rows), L.wq.rows},
@@ -1228,13 +1138,13 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
                                 if (fa) {
                                     allow_lds(k_pf_attn_in<NP, TQ, TV, 2>);
                                     hipLaunchKernelGGL((k_pf_attn_in<NP, TQ, TV, 2>), dim3(GW), dim3(MT), lds, s, d,
-                                                       L.attn_norm, L.wq, L.wk, L.wv, g_qk, q, n, fq);
+                                                       L.attn_norm, L.wq, L.wk, L.wv, g_qk, q, n);
                                     return;
                                 }
                             }
                             allow_lds(k_pf_attn_in<NP, TQ, TV>);
                             hipLaunchKernelGGL((k_pf_attn_in<NP, TQ, TV>), dim3(GW), dim3(MT), lds, s, d, L.attn_norm,
-                                               L.wq, L.wk, L.wv, g_qk, q, n, fq);
+                                               L.wq, L.wk, L.wv, g_qk, q, n);
                         };
                         if constexpr (TQ == 8) {
                             go.template operator()<8>();
@@ -1287,7 +1197,7 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
             }
         }
         const bool ff = fq2(1, L.gate.type);
-        if (!ff && (!fq || use_mmq(2, L.gate.type)))
+        if (!ff)
             launch_quant(d, 0, pb.x, d.n_embd, L.ffn_norm, L.gate.type != 8, pb, nt, s);
         if (!ff && use_mmq(2, L.gate.type)) {
             const MmqSeg sg{L.gate, mmq_tiles(L.gate.rows), 0};
@@ -1302,17 +1212,17 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
                         if (ff) {
                             allow_lds(k_pf_ffn_in<NP, T, 2>);
                             hipLaunchKernelGGL((k_pf_ffn_in<NP, T, 2>), dim3(grid), dim3(MT), pf_lds_bytes(d.n_embd, n, 0),
-                                               s, dw, L.ffn_norm, L.gate, L.up, q, n, fq);
+                                               s, dw, L.ffn_norm, L.gate, L.up, q, n);
                             return;
                         }
                     }
                     allow_lds(k_pf_ffn_in<NP, T>);
                     hipLaunchKernelGGL((k_pf_ffn_in<NP, T>), dim3(grid), dim3(MT), pf_lds_bytes(d.n_embd, n, 0), s, dw,
-                                       L.ffn_norm, L.gate, L.up, q, n, fq);
+                                       L.ffn_norm, L.gate, L.up, q, n);
                 });
             });
         }
-        if (!fq || use_mmq(3, L.down.type)) launch_quant(d, 1, pb.h, L.down.k, nullptr, L.down.type != 8, pb, nt, s);
+        launch_quant(d, 1, pb.h, L.down.k, nullptr, L.down.type != 8, pb, nt, s);
         if (use_mmq(3, L.down.type)) {
             const MmqSeg sg{L.down, mmq_tiles(L.down.rows), 0};
             launch_mmq(&sg, &L.down.type, 1, MMQ_RESID,
@@ -1323,7 +1233,7 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
                 dispatch_nt(L.down.k, L.down.type, [&]<int NP, int T>() {
                     allow_lds(k_pf_ffn_down<NP, T>);
                     hipLaunchKernelGGL((k_pf_ffn_down<NP, T>), dim3(grid), dim3(MT), pf_lds_bytes(L.down.k, n, rpw),
-                                       s, d, L.down, q, n, rpw, fq);
+                                       s, d, L.down, q, n, rpw);
                 });
             });
         }

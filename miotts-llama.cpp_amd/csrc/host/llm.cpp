@@ -18,7 +18,6 @@
 #include "common.h"
 #include "gguf.h"
 #include "llm_kernels.h"
-#include "prefetch.h"
 #include "quant.h"
 
 struct Stager;
@@ -69,7 +68,6 @@ struct mio_hip_llm {
     // eagerly and is captured: ~280 launches that eager issue makes host-bound)
     std::map<int, hipGraphExec_t> prefill_graphs;
     mio::SampleCfg *d_cfg = nullptr;
-    uint32_t epoch = 0;  // SampleCfg.epoch of the last put_cfg
     float *d_layers = nullptr;  // mio_hip_llm_eval_layers' residual snapshots (parity tests)
     // generation state
     int n_prompt = 0, max_new = 0, steps_total = 0, steps_issued = 0;
@@ -234,17 +232,15 @@ int graph_steps() {
     return n;
 }
 
-// Launches of layer il in step order (launch_step_kernel's `which`): attn_in (+ attention
-// when fused), [attention], attn_out, or an lfm2 short-conv layer's conv_in, conv_out; then
-// ffn_in, ffn_down. Returns the count (<= 5).
+// Launches of layer il in step order (launch_step_kernel's `which`): attn_in, attention,
+// attn_out, or an lfm2 short-conv layer's conv_in, conv_out; then ffn_in, ffn_down. Returns
+// the count (<= 5).
 int layer_kinds(const mio_hip_llm *m, int il, int *w) {
     int n = 0;
     if (m->layers[il].conv) {
         w[n++] = 8, w[n++] = 9;
     } else {
-        w[n++] = 0;
-        if (!m->buf.qkv_g) w[n++] = 1;
-        w[n++] = 2;
+        w[n++] = 0, w[n++] = 1, w[n++] = 2;
     }
     w[n++] = 3, w[n++] = 4;
     return n;
@@ -308,9 +304,6 @@ int ensure_graph(mio_hip_llm *m) {
 }
 
 int put_cfg(mio_hip_llm *m, mio::SampleCfg c) {
-    // a new generation epoch (q|k|v granule tags): 11 bits, never 0
-    m->epoch = m->epoch % 2047 + 1;
-    c.epoch = m->epoch;
     m->cfg = c;
     MIO_HIP_CHECK(hipMemcpyAsync(m->d_cfg, &c, sizeof(c), hipMemcpyHostToDevice, m->d->stream));
     return MIO_OK;
@@ -500,8 +493,6 @@ int llm_poll(mio_hip_llm *m, std::vector<int32_t> &out, bool *done) {
     --m->snap_n;
     const int first = m->n_prompt - 1;
     const StepState st = *sn.st;
-    MIO_REQUIRE(!st.fault, MIO_ERR_HIP, "llm: a decode step timed out waiting for its q/k/v rows (fault %d)",
-                st.fault);
     const int n = std::min(st.step, sn.hi) > first ? std::min(st.step, sn.hi) - first : 0;
     out.assign(sn.tok + first, sn.tok + first + n);
     bool d = false;
@@ -777,11 +768,6 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
     want(m->buf.smp, 2 * std::max(mio::lm_head_blocks(D), 4 * D.n_wg) + 16);
     want(m->buf.st, 1);
     want(m->d_cfg, 1);
-    // MIO_ATT_FUSED=1: attention inside the attn_in launch (tagged-granule hand-off);
-    // default: a launch of its own
-    uint2 *qkv_g = nullptr;
-    const bool fused = getenv("MIO_ATT_FUSED") && getenv("MIO_ATT_FUSED")[0] == '1';
-    if (fused) want(qkv_g, (size_t)qkv);
     m->max_steps = n_ctx;
     for (mio_hip_llm::Snap &sn : m->snaps)
         if (hipHostMalloc((void **)&sn.st, sizeof(mio::StepState), hipHostMallocDefault) != hipSuccess ||
@@ -811,7 +797,6 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
         }
     }
     m->buf.cfg = m->d_cfg;
-    m->buf.qkv_g = qkv_g;  // zeroed with the carve (dalloc): tag 0 is never a launch's
     m->pf.tokens = m->d_prompt;
     m->pf.ring = m->buf.ring;  // the single-stream prefill is sequence 0 of the decode rings
     m->pf.seq_ring = 0;
@@ -1006,7 +991,8 @@ extern "C" int mio_hip_llm_generate(mio_hip_llm *m, const int32_t *prompt, int n
     // (llm_begin prefilled the prompt) check every `check_interval` generated tokens (the
     // streaming cadence, test-to-speech.cpp:499,608) for an end token. The next interval is
     // enqueued before the previous one is checked: the GPU never waits for the host; after
-    // an end token at most one interval of steps runs for nothing (its tokens are dropped).
+    // an end token the rest of its interval and one more run for nothing (their tokens are
+    // dropped; mio_hip_llm_steps_issued counts them).
     if ((rc = mio::llm_run(m, check_interval))) return rc;
     while (!done) {
         if (m->steps_issued < m->steps_total && (rc = mio::llm_run(m, check_interval))) return rc;
@@ -1394,10 +1380,7 @@ extern "C" int mio_hip_llm_time_kernel(mio_hip_llm *m, int which, int iters, flo
     uint64_t b = 0;
     const uint64_t att_bytes = 2ull * 2 * D.n_kv * D.hd * (pos + 1) + 4ull * qkv + 8ull * (D.hd / 2) + part;
     switch (which) {
-        case 0:  // the fused launch also moves the attention's bytes (its q|k|v read stays on-chip)
-            b = qbytes(L.wq) + qbytes(L.wk) + qbytes(L.wv) + 4ull * D.n_embd + 4ull * qkv +
-                (m->buf.qkv_g ? att_bytes - 4ull * qkv : 0);
-            break;
+        case 0: b = qbytes(L.wq) + qbytes(L.wk) + qbytes(L.wv) + 4ull * D.n_embd + 4ull * qkv; break;
         case 1: b = att_bytes; break;
         case 2: b = qbytes(L.wo) + part + 4ull * D.n_embd * 2; break;
         case 3: b = qbytes(L.gate) + qbytes(L.up) + 4ull * (D.n_embd * 2 + D.n_ff); break;
@@ -1452,12 +1435,6 @@ extern "C" int mio_hip_llm_trace_kernel(mio_hip_llm *m, int which, uint64_t *out
     if (hipMalloc(&flush, flush_bytes) == hipSuccess) {
         hipMemsetAsync(flush, 1, flush_bytes, s);
         hipMemsetAsync(flush, 2, flush_bytes, s);
-    }
-    // MIO_TRACE_PREFETCH=1: the launch's weights are swept into the Infinity Cache first
-    if (getenv("MIO_TRACE_PREFETCH") && getenv("MIO_TRACE_PREFETCH")[0] == '1') {
-        const int wr = which == 8 ? 0 : (which == 9 ? 2 : which);
-        const size_t ri = which == 6 ? m->ranges.size() - 1 : (size_t)il * 5 + wr;
-        if (ri < m->ranges.size()) mio::launch_touch(m->ranges[ri].p, m->ranges[ri].bytes, m->dims.n_wg, s);
     }
     mio::LlmBuffers tb = m->buf;
     tb.trace = dt;

@@ -104,7 +104,6 @@ def _declare(L: ctypes.CDLL) -> None:
         "mio_hip_llm_steps_issued": (c_int, [_vp, ctypes.POINTER(c_int)]),
         "mio_hip_llm_step_kinds": (c_int, [_vp, _vp, c_int, ctypes.POINTER(c_int)]),
         "mio_hip_llm_conv_ring": (c_int, [_vp, c_int, _vp, c_int]),
-        "mio_hip_debug_graph_replay": (c_int, [_vp, c_int, c_int, ctypes.POINTER(ctypes.c_double)]),
         "mio_hip_llm_eval_layers": (c_int, [_vp, ctypes.c_int32, c_int, _vp, _vp]),
         "mio_hip_llm_kv_rows": (c_int, [_vp, c_int, c_int, _vp, _vp]),
         "mio_hip_debug_matvec": (c_int, [_vp, ctypes.c_uint32, _vp, c_int, c_int, _vp, _vp]),
@@ -172,13 +171,6 @@ class Device:
 
     def sync(self) -> None:
         check(lib().mio_hip_device_sync(self.h))
-
-    def graph_replay(self, replays: int, nodes: int = 1) -> float:
-        """Diagnostic (mio_hip_debug_graph_replay): wall ms of `replays` replays of a graph of
-        `nodes` empty launches."""
-        ms = ctypes.c_double(0)
-        check(lib().mio_hip_debug_graph_replay(self.h, replays, nodes, ctypes.byref(ms)))
-        return ms.value
 
     def cu_count(self) -> int:
         n = ctypes.c_int(0)
