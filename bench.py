@@ -152,7 +152,15 @@ def cpu_baseline(llm_path, codec_path, voice_path, n_tok, n_codes, utt_tokens, t
         pyoracle.set_threads(prev)
     wall = utt_tokens * t_tok + utt_tokens * t_code
     audio = utt_tokens * 1764 / 44100.0
+    host = os.cpu_count() or 1
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = host
     return {"value": round(audio / wall, 4), "unit": "x realtime (audio s / wall s)", "cores": threads,
+            "host_cpus": host, "affinity_cpus": affinity,
+            "cores_note": f"{threads} OpenMP threads = this job's CPU share (OMP_NUM_THREADS, else min(16, host "
+                          f"CPUs)); the host reports {host} CPUs ({affinity} in this process's affinity mask)",
             "kind": "port",
             "sample": f"oracle decode of {n_tok} tokens at positions 0..{utt_tokens - 1} "
                       f"({t_tok * 1e3:.1f} ms/token) + codec+iSTFT of {n_codes} codes "

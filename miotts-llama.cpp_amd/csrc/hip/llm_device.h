@@ -988,67 +988,6 @@ __device__ __forceinline__ float group_sum(float v) {
     return v;
 }
 
-// Online-softmax merge of nch chunk partial records {O[hd], m, l} for the 4 outputs
-// dd .. dd+3 of one head (base = that head's record array): 8 chunks' loads in flight per
-// batch; a missing chunk of a batch is {m = -inf, l = 0, O = 0}, which leaves the max and
-// the sums unchanged (only real chunks are loaded: every vector load instruction costs the
-// CU's address path the same, used or not).
-__device__ __forceinline__ float4 merge_out4(const float *base, int nch, int rec, int hd, int dd) {
-    float M = -INFINITY, L = 0.0f;
-    float4 O = make_float4(0.f, 0.f, 0.f, 0.f);
-    constexpr int CB = 8;  // chunks per batch of loads
-    for (int c0 = 0; c0 < nch; c0 += CB) {
-        float2 ml[CB];
-        float4 oc[CB];
-#pragma unroll
-        for (int j = 0; j < CB; ++j) {
-            const int c = c0 + j;
-            if (c < nch) {
-                ml[j] = *reinterpret_cast<const float2 *>(base + (size_t)c * rec + hd);
-                oc[j] = *reinterpret_cast<const float4 *>(base + (size_t)c * rec + dd);
-            } else {
-                ml[j] = make_float2(-INFINITY, 0.0f);
-                oc[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-            }
-        }
-        float mb = M;
-#pragma unroll
-        for (int j = 0; j < CB; ++j) mb = fmaxf(mb, ml[j].x);
-        const float a = M == -INFINITY ? 0.0f : expf(M - mb);
-        L *= a;
-        O.x *= a, O.y *= a, O.z *= a, O.w *= a;
-#pragma unroll
-        for (int j = 0; j < CB; ++j) {
-            const float w = c0 + j < nch ? expf(ml[j].x - mb) : 0.0f;
-            L += w * ml[j].y;
-            O.x += w * oc[j].x, O.y += w * oc[j].y, O.z += w * oc[j].z, O.w += w * oc[j].w;
-        }
-        M = mb;
-    }
-    return make_float4(O.x / L, O.y / L, O.z / L, O.w / L);
-}
-
-// Merge of the attention chunks' partial records (k_attention) for all heads: thread t
-// owns outputs 4(t + i*MT) .. +3 (merge_out4), re-quantized from its registers into s.a
-// (quant_regs).
-template <int NP>
-__device__ void merge_attention(const LlmDims &d, const float *part, int nch, int K, bool kquant, const Smem &s,
-                                unsigned long long *diag = nullptr) {
-    const int hd = d.hd, rec = part_rec(hd);
-    float4 y[NP];
-#pragma unroll
-    for (int i = 0; i < NP; ++i) {
-        const int e = (MIO_TIDX + i * MT) * 4;
-        y[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (e < K) {
-            const int h = e / hd, dd = e - h * hd;
-            y[i] = merge_out4(part + (size_t)h * d.max_splits * rec, nch, rec, hd, dd);
-        }
-    }
-    MIO_DIAG_STAMP(diag, 5, 0);  // chunks merged (in registers)
-    quant_regs<NP>(y, K, kquant, s.a);
-}
-
 __device__ inline float silu_f(float x) { return x / (1.0f + expf(-x)); }
 
 __device__ inline uint64_t mix64(uint64_t x) {
@@ -1134,19 +1073,80 @@ void dispatch_nt(int K, int type, F &&f) {
 
 
 // ------------------------------------------------------------------ attention chunk sweep
-// Shared by the decode step (k_attention) and the batched prefill (k_pf_attention), so the
-// two produce bit-identical partial records.
-constexpr int ATT_NT = 512;  // threads of an attention workgroup (2 waves per SIMD)
-constexpr int ATT_NW = ATT_NT / 64;
+// Shared by the decode step (k_attention), the batched decode (k_bt_attention) and the
+// prefill (k_pf_attention), so all three produce bit-identical partial records and outputs.
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 
+// One workgroup per (ATT_CHUNK positions, kv head [, token]): a position slot is LP lanes
+// holding 8 dims each; NT = ATT_CHUNK * LP threads (at most 512), so at 32-position chunks
+// every thread owns one position (IT = 1) and the K/V rows of a chunk arrive in one load
+// round trip per lane.
 template <int HD>
 struct AttCfg {
-    static constexpr int LP = HD / 8;             // lanes per position slot (8 dims each)
-    static constexpr int NS = ATT_NT / LP;        // position slots per workgroup
-    static constexpr int IT = ATT_CHUNK / NS;     // positions per slot
+    static constexpr int LP = HD / 8;                                        // lanes per slot
+    static constexpr int NT = ATT_CHUNK * LP < 512 ? ATT_CHUNK * LP : 512;   // threads
+    static constexpr int NW = NT / 64;                                       // waves
+    static constexpr int NS = NT / LP;                                       // position slots
+    static constexpr int IT = ATT_CHUNK / NS;                                // positions per slot
     static constexpr int REC = part_rec(HD);
 };
+
+// Agent-scope (sc1: write-through / L1-bypassing) accesses of the chunk records handed from
+// the attention workgroups of a launch to the one that merges them (attn_merge_last):
+// buffer instructions on a wave-uniform base with per-lane byte offsets (aux 16 = sc1).
+__device__ __forceinline__ void st1_sc1(float *base, uint32_t off, float v) {
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rsrc(base, 0x7FFFFFF0u), off, 0, 16);
+}
+__device__ __forceinline__ float4 ld4_sc1(const float *base, uint32_t off) {
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rsrc(base, 0x7FFFFFF0u), off, 0, 16);
+    return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
+}
+__device__ __forceinline__ float2 ld2_sc1(const float *base, uint32_t off) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b64(rsrc(base, 0x7FFFFFF0u), off, 0, 16);
+    return make_float2(__uint_as_float(v[0]), __uint_as_float(v[1]));
+}
+
+// Online-softmax merge of nch chunk partial records {O[hd], m, l} for the 4 outputs
+// dd .. dd+3 of one head whose record array starts at element `head` of the wave-uniform base
+// `part` (sc1 loads: records other workgroups of the launch wrote): 8 chunks' loads in flight
+// per batch; a missing chunk of a batch is {m = -inf, l = 0, O = 0}, which leaves the max and
+// the sums unchanged (only real chunks are loaded: every vector load instruction costs the
+// CU's address path the same, used or not). The float order does not depend on which
+// workgroup merges, so every path's outputs are the same bits.
+__device__ __forceinline__ float4 merge_out4(const float *part, uint32_t head, int nch, int rec, int hd, int dd) {
+    float M = -INFINITY, L = 0.0f;
+    float4 O = make_float4(0.f, 0.f, 0.f, 0.f);
+    constexpr int CB = 8;  // chunks per batch of loads
+    for (int c0 = 0; c0 < nch; c0 += CB) {
+        float2 ml[CB];
+        float4 oc[CB];
+#pragma unroll
+        for (int j = 0; j < CB; ++j) {
+            const int c = c0 + j;
+            if (c < nch) {
+                ml[j] = ld2_sc1(part, (head + (uint32_t)(c * rec + hd)) * 4u);
+                oc[j] = ld4_sc1(part, (head + (uint32_t)(c * rec + dd)) * 4u);
+            } else {
+                ml[j] = make_float2(-INFINITY, 0.0f);
+                oc[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+        }
+        float mb = M;
+#pragma unroll
+        for (int j = 0; j < CB; ++j) mb = fmaxf(mb, ml[j].x);
+        const float a = M == -INFINITY ? 0.0f : expf(M - mb);
+        L *= a;
+        O.x *= a, O.y *= a, O.z *= a, O.w *= a;
+#pragma unroll
+        for (int j = 0; j < CB; ++j) {
+            const float w = c0 + j < nch ? expf(ml[j].x - mb) : 0.0f;
+            L += w * ml[j].y;
+            O.x += w * oc[j].x, O.y += w * oc[j].y, O.z += w * oc[j].z, O.w += w * oc[j].w;
+        }
+        M = mb;
+    }
+    return make_float4(O.x / L, O.y / L, O.z / L, O.w / L);
+}
 
 // value of lane ^ O (O = 16 or 32 by the gfx950 permlane swaps, VALU; smaller O by bpermute)
 template <int O>
@@ -1252,8 +1252,9 @@ template <int HD, int G>
 __device__ void attend_chunk(const float (*qs)[HD], const h8 (&kr)[AttCfg<HD>::IT], const h8 (&vr)[AttCfg<HD>::IT],
                              int t0, int pos, float scale, float (*wres)[G][HD + 2], float *dst, size_t g_stride,
                              unsigned long long *trace = nullptr, unsigned long long *diag = nullptr) {
-    constexpr int LP = AttCfg<HD>::LP, NS = AttCfg<HD>::NS, IT = AttCfg<HD>::IT;
-    __shared__ float wmax[ATT_NW][G];
+    constexpr int LP = AttCfg<HD>::LP, NS = AttCfg<HD>::NS, IT = AttCfg<HD>::IT, NT = AttCfg<HD>::NT,
+                  NW = AttCfg<HD>::NW;
+    __shared__ float wmax[NW][G];
     const int tid = MIO_TIDX, lane = tid & 63, wave = tid >> 6;
     const int lp = lane % LP, sl = tid / LP;
     auto mark = [&](int k) {  // checkpoints of mio_hip_llm_trace_kernel (diagnostic)
@@ -1303,7 +1304,7 @@ __device__ void attend_chunk(const float (*qs)[HD], const h8 (&kr)[AttCfg<HD>::I
     for (int g = 0; g < G; ++g) {
         M[g] = wmax[0][g];
 #pragma unroll
-        for (int w = 1; w < ATT_NW; ++w) M[g] = fmaxf(M[g], wmax[w][g]);
+        for (int w = 1; w < NW; ++w) M[g] = fmaxf(M[g], wmax[w][g]);
     }
     mark(3);
     MIO_DIAG_STAMP(diag, 3, M[0]);  // scores and chunk max done
@@ -1354,18 +1355,51 @@ __device__ void attend_chunk(const float (*qs)[HD], const h8 (&kr)[AttCfg<HD>::I
     lds_barrier();
     mark(5);
     MIO_DIAG_STAMP(diag, 5, 0);  // wave results in LDS
-    // the waves -> this chunk's partial record per q head
-    for (int e = tid; e < G * HD; e += ATT_NT) {
+    // the waves -> this chunk's partial record per q head, stored write-through (sc1) for
+    // the workgroup of this launch that merges the chunks (attn_merge_last)
+    for (int e = tid; e < G * HD; e += NT) {
         const int g = e / HD, dd = e - g * HD;
         float O = 0.0f, L = 0.0f;
 #pragma unroll
-        for (int w = 0; w < ATT_NW; ++w) {
+        for (int w = 0; w < NW; ++w) {
             O += wres[w][g][dd];
             L += wres[w][g][HD];
         }
-        float *o = dst + g * g_stride;
-        o[dd] = O;
-        if (dd == 0) o[HD] = M[g], o[HD + 1] = L;
+        const uint32_t o = (uint32_t)(g * g_stride) * 4u;
+        st1_sc1(dst, o + 4u * dd, O);
+        if (dd == 0) st1_sc1(dst, o + 4u * HD, M[g]), st1_sc1(dst, o + 4u * (HD + 1), L);
+    }
+}
+
+// After attend_chunk: the chunk workgroups of one (kv head [, token]) take arrival tickets;
+// the last of the nch arrivals merges every chunk's records (merge_out4) into the G heads'
+// outputs out[G][HD] (plain stores: read by the next launch). Hand-off (MI355X_MICROARCH
+// "Valid forms", first row): every record byte was stored sc1 (attend_chunk), each wave
+// drains its stores (vmcnt(0)) before the workgroup barrier, then ONE lane adds to the
+// unsharded ticket with an agent-scope atomic; the workgroup whose add returned nch - 1 loads
+// the records only after that add returned (its other waves after the barrier that follows),
+// and every load of them is an sc1 load. The last arriver also resets the ticket to 0 for the
+// next launch (kernel boundaries order that store before any later add). part / head0: the
+// wave-uniform record base and the element offset of head g = 0's record array (head g at
+// head0 + g * g_stride).
+template <int HD, int G>
+__device__ void attn_merge_last(const float *part, uint32_t head0, uint32_t g_stride, int nch, int *cnt, float *out) {
+    constexpr int NT = AttCfg<HD>::NT, REC = AttCfg<HD>::REC;
+    __shared__ int last_;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (MIO_TIDX == 0) {
+        auto *c = (__attribute__((address_space(1))) int *)cnt;
+        const int old = __hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last_ = old == nch - 1;
+        if (old == nch - 1) __hip_atomic_store(c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (!last_) return;
+    for (int e = 4 * (int)MIO_TIDX; e < G * HD; e += 4 * NT) {
+        const int g = e / HD, dd = e - g * HD;
+        const float4 y = merge_out4(part, head0 + (uint32_t)g * g_stride, nch, REC, HD, dd);
+        *reinterpret_cast<float4 *>(out + e) = y;
     }
 }
 

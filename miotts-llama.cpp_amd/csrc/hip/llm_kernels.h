@@ -7,8 +7,14 @@
 
 namespace mio {
 
-// attention positions per chunk (k_attention workgroup), = LlmDims::split
-constexpr int kAttChunk = 128;
+// attention positions per chunk (one attention workgroup), = LlmDims::split. Every path
+// (decode step, batched decode, prefill) uses the same chunks and the same merge, so their
+// results are bit-identical. MIO_ATT_CHUNK: A/B builds (32, 64 or 128).
+#ifndef MIO_ATT_CHUNK
+#define MIO_ATT_CHUNK 32
+#endif
+constexpr int kAttChunk = MIO_ATT_CHUNK;
+static_assert(kAttChunk == 32 || kAttChunk == 64 || kAttChunk == 128, "attention chunk");
 
 // One quantized matrix in the split layout (csrc/host/quant.h), rows x k.
 struct QMat {
@@ -89,6 +95,8 @@ struct LlmBuffers {
     float *h;          // [n_ff] ffn activation
     float *logits;     // [n_vocab]
     float *part;       // [H][max_splits][hd + 4] attention chunk partials {O, m, l}
+    float *att;        // [H * hd] attention output (chunks merged by the last chunk workgroup)
+    int *att_cnt;      // [Hkv] chunk arrival tickets (0 between launches)
     float *smp;        // sampler partials [2 * n_lm_blocks]
     const float2 *rope;  // [n_ctx][hd/2] (cos, sin)
     StepState *st;
@@ -119,6 +127,8 @@ struct PrefillBuffers {
                          // layers: [kPrefillB][3 n_embd] B | C | X rows)
     float *h;            // [kPrefillB][n_ff]
     float *part;         // [kPrefillB][H][max_splits][hd + 4] attention chunk partials
+    float *att;          // [kPrefillB][H * hd] attention outputs (merged in the attention launch)
+    int *att_cnt;        // [kPrefillB][Hkv] chunk arrival tickets (0 between launches)
     const float2 *rope;  // [n_ctx][hd/2]
     const int *tokens;   // device token ids (embedded token t of a chunk at tokens[p0 + t])
     const int *pos;      // position of token t: pos[t * pos_stride] (device-resident)

@@ -64,12 +64,16 @@ __global__ __launch_bounds__(MT) void k_attn_out(LlmDims d, QMat wo, LlmBuffers 
     const Smem s = carve(smem, K);
     int lo, hi;
     wave_range(d, wo.rows, lo, hi);
+    XRegs<NP> xr;
+    load_x(b.att, nullptr, K, xr);
     const float xres = load_resid(b.x, lo, hi);
+    x_gate();
     Frag ga[Cfg<NP, SU>::U], gb[Cfg<NP, SU>::U];
     load_first<T, NP, 1, SU, MIO_SMALL_AUX>(wo, wo, lo, hi, ga, gb);
+    x_after_weights(xr);
     MIO_TRACE(b, 1);
     MIO_TL_MARK1(b);
-    merge_attention<NP>(d, b.part, cur_pos(b.st, d) / ATT_CHUNK + 1, K, T != 8, s, MIO_TL_DIAGSLOT(b));
+    plain_quant(xr, K, T != 8, s, MIO_TL_DIAGSLOT(b));
     MIO_TRACE(b, 2);
     MIO_TL_MARK(b, 2);
     stream_rows<T, NP, 1, SU, MIO_SMALL_AUX>(wo, wo, lo, hi, ga, gb, s.a, [&](int row, float v, float) {
@@ -261,20 +265,21 @@ __global__ __launch_bounds__(MT) void k_lm_head(LlmDims d, const float *norm_w, 
 }
 
 // ------------------------------------------------------------------ attention
-// One 256-thread workgroup per (chunk of ATT_CHUNK = 128 positions, kv head): q/k RMSNorm
-// (qwen3) + RoPE + f16 rounding, the chunk owning `pos` appends the new k/v row to the F16
-// cache, then an online softmax over the chunk for the G q heads sharing the kv head. Its
-// partial record {O[HD], m, l} per q head is merged with the other chunks' in the prologue
-// of k_attn_out (the launch-boundary reduce: no extra launch, no in-kernel hand-off).
+// One workgroup per (chunk of ATT_CHUNK positions, kv head): q/k RMSNorm (qwen3) + RoPE +
+// f16 rounding, the chunk owning `pos` appends the new k/v row to the F16 cache, then a
+// softmax over the chunk for the G q heads sharing the kv head, whose partial records
+// {O[HD], m, l} the last chunk workgroup to arrive merges into b.att (attn_merge_last): 32-
+// position chunks spread the K/V rows of position ~400 over 13 x n_kv workgroups (16 KB each
+// at hd 128) instead of 4 x n_kv, and k_attn_out reads the n_head * hd merged values.
 template <int HD, int G, bool DG>
-__global__ __launch_bounds__(ATT_NT) void k_attention(LlmDims d, const float *q_norm, const float *k_norm,
+__global__ __launch_bounds__(AttCfg<HD>::NT) void k_attention(LlmDims d, const float *q_norm, const float *k_norm,
                                                       const float *bqkv, _Float16 *kc, _Float16 *vc, LlmBuffers b) {
     constexpr bool kDiag = DG;
     using C = AttCfg<HD>;
     constexpr int PER = HD / 64;
     __shared__ float qs[G][HD];
     __shared__ float knew[HD], vnew[HD];
-    __shared__ float wres[ATT_NW][G][HD + 2];
+    __shared__ float wres[C::NW][G][HD + 2];
 
     MIO_TRACE(b, 0);
     MIO_TL_BEGIN(b);
@@ -283,7 +288,7 @@ __global__ __launch_bounds__(ATT_NT) void k_attention(LlmDims d, const float *q_
     // b.st (without this the compiler sinks them below the pos-dependent exit: a third
     // scalar-load round trip before the first K/V load)
     asm volatile("" ::"s"(kc), "s"(vc), "s"(d.n_ctx), "s"(b.qkv), "s"(b.rope), "s"(q_norm), "s"(k_norm),
-                 "s"(b.part), "s"(d.max_splits), "s"(bqkv));
+                 "s"(b.part), "s"(d.max_splits), "s"(bqkv), "s"(b.att), "s"(b.att_cnt));
     const int pos = cur_pos(b.st, d);
     const int t0 = ch * ATT_CHUNK;
     if (t0 > pos) return;
@@ -296,7 +301,7 @@ __global__ __launch_bounds__(ATT_NT) void k_attention(LlmDims d, const float *q_
     MIO_TL_MARK1(b);
     // q heads (waves 0..G-1) and, for the chunk owning `pos`, the new k/v row
     const bool owner = pos < t0 + ATT_CHUNK;
-    for (int hh = wave; hh < G + (owner ? 1 : 0); hh += ATT_NW) {
+    for (int hh = wave; hh < G + (owner ? 1 : 0); hh += C::NW) {
         const bool isk = hh == G;
         float vv[PER];
         if (isk) {
@@ -337,9 +342,10 @@ __global__ __launch_bounds__(ATT_NT) void k_attention(LlmDims d, const float *q_
                 if (it == r / C::NS) kr[it] = kn, vr[it] = vn;
         }
     }
-    attend_chunk<HD, G>(qs, kr, vr, t0, pos, d.scale, wres,
-                        b.part + ((size_t)(kvh * G) * d.max_splits + ch) * C::REC, (size_t)d.max_splits * C::REC,
+    const uint32_t gs = (uint32_t)(d.max_splits * C::REC), head0 = (uint32_t)(kvh * G) * gs;
+    attend_chunk<HD, G>(qs, kr, vr, t0, pos, d.scale, wres, b.part + head0 + (uint32_t)ch * C::REC, gs,
                         DG ? b.trace : nullptr, MIO_TL_DIAGSLOT(b));
+    attn_merge_last<HD, G>(b.part, head0, gs, pos / ATT_CHUNK + 1, b.att_cnt + kvh, b.att + (size_t)kvh * G * HD);
     MIO_TL_END(b);
     MIO_TRACE(b, 15);
 }
@@ -349,11 +355,11 @@ void launch_attention(int G, dim3 grid, hipStream_t s, const LlmDims &d, const L
                       _Float16 *vc, const LlmBuffers &b) {
     const float *qn = L.q_norm, *kn = L.k_norm, *bi = L.bqkv;
     switch (G) {
-        case 1: hipLaunchKernelGGL((k_attention<HD, 1, DG>), grid, dim3(ATT_NT), 0, s, d, qn, kn, bi, kc, vc, b); break;
-        case 2: hipLaunchKernelGGL((k_attention<HD, 2, DG>), grid, dim3(ATT_NT), 0, s, d, qn, kn, bi, kc, vc, b); break;
-        case 3: hipLaunchKernelGGL((k_attention<HD, 3, DG>), grid, dim3(ATT_NT), 0, s, d, qn, kn, bi, kc, vc, b); break;
-        case 4: hipLaunchKernelGGL((k_attention<HD, 4, DG>), grid, dim3(ATT_NT), 0, s, d, qn, kn, bi, kc, vc, b); break;
-        case 8: hipLaunchKernelGGL((k_attention<HD, 8, DG>), grid, dim3(ATT_NT), 0, s, d, qn, kn, bi, kc, vc, b); break;
+        case 1: hipLaunchKernelGGL((k_attention<HD, 1, DG>), grid, dim3(AttCfg<HD>::NT), 0, s, d, qn, kn, bi, kc, vc, b); break;
+        case 2: hipLaunchKernelGGL((k_attention<HD, 2, DG>), grid, dim3(AttCfg<HD>::NT), 0, s, d, qn, kn, bi, kc, vc, b); break;
+        case 3: hipLaunchKernelGGL((k_attention<HD, 3, DG>), grid, dim3(AttCfg<HD>::NT), 0, s, d, qn, kn, bi, kc, vc, b); break;
+        case 4: hipLaunchKernelGGL((k_attention<HD, 4, DG>), grid, dim3(AttCfg<HD>::NT), 0, s, d, qn, kn, bi, kc, vc, b); break;
+        case 8: hipLaunchKernelGGL((k_attention<HD, 8, DG>), grid, dim3(AttCfg<HD>::NT), 0, s, d, qn, kn, bi, kc, vc, b); break;
         default: break;
     }
 }

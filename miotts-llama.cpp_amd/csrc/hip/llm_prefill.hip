@@ -359,7 +359,7 @@ __device__ __forceinline__ void stream_rows_b(const QMat W0, const QMat W1, int 
 // ------------------------------------------------------------------ multi-token prologues
 // Every matvec workgroup needs every token's quantized activation. It is produced ONCE per
 // launch by k_bt_quant (one workgroup per token, running the single-token decode prologue
-// itself: rmsnorm_quant / plain_quant / merge_attention, so the values are the decode's bit
+// itself: rmsnorm_quant / plain_quant, so the values are the decode's bit
 // for bit) into pb.act, and each matvec workgroup copies the records into LDS with all its
 // loads in flight (one memory latency for all tokens).
 __device__ __forceinline__ void prologue_copy(const char *act, int K, char *smem, int nt) {
@@ -488,8 +488,8 @@ __device__ __forceinline__ void xpre_quant(const XPre &xp, int K, float eps, boo
     lds_barrier();
 }
 
-// One workgroup per token t: MODE 0 RMSNorm(src[t]) * norm_w, 1 src[t] as is, 2 the
-// attention chunk merge of token t; quantized (Q8_K / Q8_0) into the token's act record.
+// One workgroup per token t: MODE 0 RMSNorm(src[t]) * norm_w, 1 src[t] as is (the attention
+// output pb.att, h); quantized (Q8_K / Q8_0) into the token's act record.
 template <int NP, int MODE>
 __global__ __launch_bounds__(MT) void k_bt_quant(LlmDims d, const float *src, int K, const float *norm_w, int kq,
                                                  PrefillBuffers pb) {
@@ -499,17 +499,12 @@ __global__ __launch_bounds__(MT) void k_bt_quant(LlmDims d, const float *src, in
     // record's: qs | d | bs), no LDS staging + barrier + copy; LDS keeps the reduction scratch
     Smem s = carve(smem, K);
     s.a = carve_t(pb.act, K, t).a;
-    if constexpr (MODE == 2) {
-        const size_t tstride = (size_t)d.n_head * d.max_splits * part_rec(d.hd);
-        merge_attention<NP>(d, pb.part + t * tstride, pb.pos[t * pb.pos_stride] / ATT_CHUNK + 1, K, kq != 0, s);
-    } else {
-        XRegs<NP> xr;
-        load_x(src + (size_t)t * K, MODE == 0 ? norm_w : nullptr, K, xr);
-        if constexpr (MODE == 0)
-            rmsnorm_quant(xr, K, d.eps, kq != 0, s);
-        else
-            plain_quant(xr, K, kq != 0, s);
-    }
+    XRegs<NP> xr;
+    load_x(src + (size_t)t * K, MODE == 0 ? norm_w : nullptr, K, xr);
+    if constexpr (MODE == 0)
+        rmsnorm_quant(xr, K, d.eps, kq != 0, s);
+    else
+        plain_quant(xr, K, kq != 0, s);
 }
 
 // lfm2 short-conv layer, one workgroup per token t: the gated conv of t (conv_load /
@@ -656,18 +651,35 @@ __global__ __launch_bounds__(64) void k_pf_rope(LlmDims d, const float *q_norm, 
     }
 }
 
-// One workgroup per (128-position chunk, kv head, token): causal online softmax over the
-// chunk's positions <= the token's position in the token's own sequence, all rows read from
-// the cache (this launch's own rows were written by k_pf_rope); attend_chunk is the decode
-// step's sweep. Chunks past the token's position exit at once. Grid (n_kv * nt, chunks):
-// consecutive workgroup ids are different (kv head, token) pairs of one chunk, so the
-// workgroups with work (the low chunks) spread over all XCDs instead of one.
+// attend_chunk + attn_merge_last of token t's (kv head, chunk): records in pb.part
+// [t][H][max_splits][REC], tickets pb.att_cnt[t][Hkv], outputs pb.att[t][H * hd].
 template <int HD, int G>
-__global__ __launch_bounds__(ATT_NT) void k_pf_attention(LlmDims d, const _Float16 *kc, const _Float16 *vc,
-                                                         PrefillBuffers pb) {
+__device__ __forceinline__ void attend_and_merge(const LlmDims &d, const float (*qs)[HD],
+                                                 const h8 (&kr)[AttCfg<HD>::IT], const h8 (&vr)[AttCfg<HD>::IT],
+                                                 int t0, int pos, int ch, int t, int kvh,
+                                                 float (*wres)[G][HD + 2], const PrefillBuffers &pb) {
+    using C = AttCfg<HD>;
+    const uint32_t gs = (uint32_t)(d.max_splits * C::REC);
+    float *part = pb.part + (size_t)t * d.n_head * gs;  // token t's records (wave-uniform)
+    const uint32_t head0 = (uint32_t)(kvh * G) * gs;
+    attend_chunk<HD, G>(qs, kr, vr, t0, pos, d.scale, wres, part + head0 + (uint32_t)ch * C::REC, gs);
+    attn_merge_last<HD, G>(part, head0, gs, pos / ATT_CHUNK + 1, pb.att_cnt + (size_t)t * d.n_kv + kvh,
+                           pb.att + (size_t)t * d.n_head * HD + (size_t)kvh * G * HD);
+}
+
+// One workgroup per (ATT_CHUNK-position chunk, kv head, token): causal softmax over the
+// chunk's positions <= the token's position in the token's own sequence, all rows read from
+// the cache (this launch's own rows were written by k_pf_rope); attend_chunk and
+// attn_merge_last are the decode step's, so pb.att holds the decode's outputs bit for bit.
+// Chunks past the token's position exit at once. Grid (n_kv * nt, chunks): consecutive
+// workgroup ids are different (kv head, token) pairs of one chunk, so the workgroups with
+// work (the low chunks) spread over all XCDs instead of one.
+template <int HD, int G>
+__global__ __launch_bounds__(AttCfg<HD>::NT) void k_pf_attention(LlmDims d, const _Float16 *kc, const _Float16 *vc,
+                                                                 PrefillBuffers pb) {
     using C = AttCfg<HD>;
     __shared__ float qs[G][HD];
-    __shared__ float wres[ATT_NW][G][HD + 2];
+    __shared__ float wres[C::NW][G][HD + 2];
     const int kvh = blockIdx.x % d.n_kv, t = blockIdx.x / d.n_kv, ch = blockIdx.y;
     const int pos = pb.pos[t * pb.pos_stride];
     const int t0 = ch * ATT_CHUNK;
@@ -677,11 +689,9 @@ __global__ __launch_bounds__(ATT_NT) void k_pf_attention(LlmDims d, const _Float
     load_kv_rows<HD>(kc + kvo, vc + kvo, t0, pos, kr, vr);
     const int QD = (d.n_head + 2 * d.n_kv) * HD;
     const float *qsrc = pb.qkv + (size_t)t * QD + (size_t)kvh * G * HD;
-    for (int e = threadIdx.x; e < G * HD; e += ATT_NT) qs[e / HD][e % HD] = qsrc[e];
+    for (int e = threadIdx.x; e < G * HD; e += C::NT) qs[e / HD][e % HD] = qsrc[e];
     lds_barrier();
-    attend_chunk<HD, G>(qs, kr, vr, t0, pos, d.scale, wres,
-                        pb.part + (((size_t)t * d.n_head + kvh * G) * d.max_splits + ch) * C::REC,
-                        (size_t)d.max_splits * C::REC);
+    attend_and_merge<HD, G>(d, qs, kr, vr, t0, pos, ch, t, kvh, wres, pb);
 }
 
 // Batched decode attention (one token per sequence, so no token of the launch reads a row
@@ -689,17 +699,17 @@ __global__ __launch_bounds__(ATT_NT) void k_pf_attention(LlmDims d, const _Float
 // token's q heads (and, in the chunk owning its position, its k / v row) get q/k RMSNorm +
 // bias + RoPE + f16 rounding in LDS, the owner appends the row to the sequence's cache and
 // takes it from LDS, then the chunk's softmax partials. Replaces k_pf_rope + k_pf_attention
-// (one launch less per layer; the same prep_head / attend_chunk arithmetic, so the partial
-// records equal theirs bit for bit).
+// (one launch less per layer; the same prep_head / attend_chunk / attn_merge_last
+// arithmetic, so the outputs equal theirs bit for bit).
 template <int HD, int G>
-__global__ __launch_bounds__(ATT_NT) void k_bt_attention(LlmDims d, const float *q_norm, const float *k_norm,
+__global__ __launch_bounds__(AttCfg<HD>::NT) void k_bt_attention(LlmDims d, const float *q_norm, const float *k_norm,
                                                          const float *bqkv, _Float16 *kcache, _Float16 *vcache,
                                                          PrefillBuffers pb) {
     using C = AttCfg<HD>;
     constexpr int PER = HD / 64;
     __shared__ float qs[G][HD];
     __shared__ float knew[HD], vnew[HD];
-    __shared__ float wres[ATT_NW][G][HD + 2];
+    __shared__ float wres[C::NW][G][HD + 2];
     const int kvh = blockIdx.x % d.n_kv, t = blockIdx.x / d.n_kv, ch = blockIdx.y;
     const int pos = pb.pos[t * pb.pos_stride];
     const int t0 = ch * ATT_CHUNK;
@@ -712,7 +722,7 @@ __global__ __launch_bounds__(ATT_NT) void k_bt_attention(LlmDims d, const float 
     load_kv_rows<HD>(kc, vc, t0, pos, kr, vr);  // row pos comes from LDS below
     const float *qkv = pb.qkv + (size_t)t * (d.n_head + 2 * d.n_kv) * HD;
     const bool owner = pos < t0 + ATT_CHUNK;
-    for (int hh = wave; hh < G + (owner ? 1 : 0); hh += ATT_NW) {
+    for (int hh = wave; hh < G + (owner ? 1 : 0); hh += C::NW) {
         const bool isk = hh == G;
         float vv[PER];
         if (isk) {
@@ -748,9 +758,7 @@ __global__ __launch_bounds__(ATT_NT) void k_bt_attention(LlmDims d, const float 
                 if (it == r / C::NS) kr[it] = kn, vr[it] = vn;
         }
     }
-    attend_chunk<HD, G>(qs, kr, vr, t0, pos, d.scale, wres,
-                        pb.part + (((size_t)t * d.n_head + kvh * G) * d.max_splits + ch) * C::REC,
-                        (size_t)d.max_splits * C::REC);
+    attend_and_merge<HD, G>(d, qs, kr, vr, t0, pos, ch, t, kvh, wres, pb);
 }
 
 template <int NP, int T>
@@ -947,11 +955,11 @@ void launch_bt_attention(int G, dim3 grid, hipStream_t s, const LlmDims &d, cons
                          _Float16 *vc, const PrefillBuffers &pb) {
     const float *qn = L.q_norm, *kn = L.k_norm, *bi = L.bqkv;
     switch (G) {
-        case 1: hipLaunchKernelGGL((k_bt_attention<HD, 1>), grid, dim3(ATT_NT), 0, s, d, qn, kn, bi, kc, vc, pb); break;
-        case 2: hipLaunchKernelGGL((k_bt_attention<HD, 2>), grid, dim3(ATT_NT), 0, s, d, qn, kn, bi, kc, vc, pb); break;
-        case 3: hipLaunchKernelGGL((k_bt_attention<HD, 3>), grid, dim3(ATT_NT), 0, s, d, qn, kn, bi, kc, vc, pb); break;
-        case 4: hipLaunchKernelGGL((k_bt_attention<HD, 4>), grid, dim3(ATT_NT), 0, s, d, qn, kn, bi, kc, vc, pb); break;
-        case 8: hipLaunchKernelGGL((k_bt_attention<HD, 8>), grid, dim3(ATT_NT), 0, s, d, qn, kn, bi, kc, vc, pb); break;
+        case 1: hipLaunchKernelGGL((k_bt_attention<HD, 1>), grid, dim3(AttCfg<HD>::NT), 0, s, d, qn, kn, bi, kc, vc, pb); break;
+        case 2: hipLaunchKernelGGL((k_bt_attention<HD, 2>), grid, dim3(AttCfg<HD>::NT), 0, s, d, qn, kn, bi, kc, vc, pb); break;
+        case 3: hipLaunchKernelGGL((k_bt_attention<HD, 3>), grid, dim3(AttCfg<HD>::NT), 0, s, d, qn, kn, bi, kc, vc, pb); break;
+        case 4: hipLaunchKernelGGL((k_bt_attention<HD, 4>), grid, dim3(AttCfg<HD>::NT), 0, s, d, qn, kn, bi, kc, vc, pb); break;
+        case 8: hipLaunchKernelGGL((k_bt_attention<HD, 8>), grid, dim3(AttCfg<HD>::NT), 0, s, d, qn, kn, bi, kc, vc, pb); break;
         default: break;
     }
 }
@@ -960,11 +968,11 @@ template <int HD>
 void launch_pf_attention(int G, dim3 grid, hipStream_t s, const LlmDims &d, const _Float16 *kc, const _Float16 *vc,
                          const PrefillBuffers &pb) {
     switch (G) {
-        case 1: hipLaunchKernelGGL((k_pf_attention<HD, 1>), grid, dim3(ATT_NT), 0, s, d, kc, vc, pb); break;
-        case 2: hipLaunchKernelGGL((k_pf_attention<HD, 2>), grid, dim3(ATT_NT), 0, s, d, kc, vc, pb); break;
-        case 3: hipLaunchKernelGGL((k_pf_attention<HD, 3>), grid, dim3(ATT_NT), 0, s, d, kc, vc, pb); break;
-        case 4: hipLaunchKernelGGL((k_pf_attention<HD, 4>), grid, dim3(ATT_NT), 0, s, d, kc, vc, pb); break;
-        case 8: hipLaunchKernelGGL((k_pf_attention<HD, 8>), grid, dim3(ATT_NT), 0, s, d, kc, vc, pb); break;
+        case 1: hipLaunchKernelGGL((k_pf_attention<HD, 1>), grid, dim3(AttCfg<HD>::NT), 0, s, d, kc, vc, pb); break;
+        case 2: hipLaunchKernelGGL((k_pf_attention<HD, 2>), grid, dim3(AttCfg<HD>::NT), 0, s, d, kc, vc, pb); break;
+        case 3: hipLaunchKernelGGL((k_pf_attention<HD, 3>), grid, dim3(AttCfg<HD>::NT), 0, s, d, kc, vc, pb); break;
+        case 4: hipLaunchKernelGGL((k_pf_attention<HD, 4>), grid, dim3(AttCfg<HD>::NT), 0, s, d, kc, vc, pb); break;
+        case 8: hipLaunchKernelGGL((k_pf_attention<HD, 8>), grid, dim3(AttCfg<HD>::NT), 0, s, d, kc, vc, pb); break;
         default: break;
     }
 }
@@ -1008,12 +1016,14 @@ PrefillBuffers shifted(const LlmDims &d, const PrefillBuffers &pb, int t, int K)
     q.qkv += (size_t)t * (d.n_head + 2 * d.n_kv) * d.hd;
     q.h += (size_t)t * d.n_ff;
     q.part += (size_t)t * d.n_head * d.max_splits * part_rec(d.hd);
+    q.att += (size_t)t * d.n_head * d.hd;
+    q.att_cnt += (size_t)t * d.n_kv;
     q.pos += (size_t)t * pb.pos_stride;
     q.seq += (size_t)t * pb.seq_stride;
     return q;
 }
 
-// act records of nt tokens (k_bt_quant): mode 0 RMSNorm(src) * w, 1 src, 2 attention merge
+// act records of nt tokens (k_bt_quant): mode 0 RMSNorm(src) * w, 1 src
 void launch_quant(const LlmDims &d, int mode, const float *src, int K, const float *w, bool kq,
                   const PrefillBuffers &pb, int nt, hipStream_t s) {
     const int np = pick_np(K);
@@ -1021,10 +1031,8 @@ void launch_quant(const LlmDims &d, int mode, const float *src, int K, const flo
         const size_t lds = smem_bytes(K);
         if (mode == 0)
             hipLaunchKernelGGL((k_bt_quant<NP, 0>), dim3(nt), dim3(MT), lds, s, d, src, K, w, (int)kq, pb);
-        else if (mode == 1)
-            hipLaunchKernelGGL((k_bt_quant<NP, 1>), dim3(nt), dim3(MT), lds, s, d, src, K, w, (int)kq, pb);
         else
-            hipLaunchKernelGGL((k_bt_quant<NP, 2>), dim3(nt), dim3(MT), lds, s, d, src, K, w, (int)kq, pb);
+            hipLaunchKernelGGL((k_bt_quant<NP, 1>), dim3(nt), dim3(MT), lds, s, d, src, K, w, (int)kq, pb);
     };
     if (np == 1)
         go.template operator()<1>();
@@ -1179,7 +1187,7 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
                 else
                     launch_pf_attention<64>(G, grid, s, d, kc, vc, pb);
             }
-            launch_quant(d, 2, nullptr, L.wo.k, nullptr, L.wo.type != 8, pb, nt, s);
+            launch_quant(d, 1, pb.att, L.wo.k, nullptr, L.wo.type != 8, pb, nt, s);
             if (use_mmq(1, L.wo.type)) {
                 const MmqSeg sg{L.wo, mmq_tiles(L.wo.rows), 0};
                 launch_mmq(&sg, &L.wo.type, 1, MMQ_RESID, MmqArgs{pb.act, act_bytes(L.wo.k), L.wo.k, nt, pb.x, d.n_embd, {}},

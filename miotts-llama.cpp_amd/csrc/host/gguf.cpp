@@ -15,6 +15,7 @@ namespace mio {
 size_t ggml_type_block_elems(uint32_t t) {
     switch (t) {
         case GGML_Q4_0:
+        case GGML_Q5_0:
         case GGML_Q8_0: return 32;
         case GGML_Q4_K:
         case GGML_Q6_K:
@@ -32,6 +33,7 @@ size_t ggml_type_block_bytes(uint32_t t) {
         case GGML_I16: return 2;
         case GGML_I32: return 4;
         case GGML_Q4_0: return 18;
+        case GGML_Q5_0: return 22;
         case GGML_Q8_0: return 34;
         case GGML_Q4_K: return 144;
         case GGML_Q6_K: return 210;
@@ -55,6 +57,7 @@ const char *ggml_type_name(uint32_t t) {
         case GGML_I16: return "i16";
         case GGML_I32: return "i32";
         case GGML_Q4_0: return "q4_0";
+        case GGML_Q5_0: return "q5_0";
         case GGML_Q8_0: return "q8_0";
         case GGML_Q4_K: return "q4_K";
         case GGML_Q6_K: return "q6_K";

@@ -18,6 +18,7 @@ enum GgmlType : uint32_t {
     GGML_F32 = 0,
     GGML_F16 = 1,
     GGML_Q4_0 = 2,
+    GGML_Q5_0 = 6,
     GGML_Q8_0 = 8,
     GGML_Q4_K = 12,
     GGML_Q6_K = 14,

@@ -54,12 +54,6 @@ struct mio_hip_llm {
     // all quantized matrices live in one arena, in the order a step streams them
     uint8_t *arena = nullptr;
     std::map<std::string, size_t> arena_off;
-    // weight byte range streamed by each launch: [il * 5 + which] (which 0/2/3/4), lm_head last
-    struct Range {
-        const uint8_t *p = nullptr;
-        uint64_t bytes = 0;
-    };
-    std::vector<Range> ranges;
 
     // decode-step graphs, captured once (the sampling config is device-resident):
     // one step, and graph_steps() steps back to back (fewer graph launches per token)
@@ -177,12 +171,26 @@ bool upload_qmat(mio_hip_llm *m, const mio::GgufTensor *t, mio::QMat &q) {
         mio::set_error("llm: matrix tensor %s missing or not 2-D", t ? t->name.c_str() : "?");
         return false;
     }
-    if (t->type != mio::GGML_Q8_0 && t->type != mio::GGML_Q4_K && t->type != mio::GGML_Q6_K) {
-        mio::set_error("llm: tensor %s has type %s; supported: q8_0, q4_K, q6_K", t->name.c_str(),
-                       mio::ggml_type_name(t->type));
+    const bool repack = mio::repacks_to_q8_0(t->type);
+    if (t->type != mio::GGML_Q8_0 && t->type != mio::GGML_Q4_K && t->type != mio::GGML_Q6_K && !repack) {
+        mio::set_error("llm: tensor %s has type %s; supported: q8_0, q4_K, q6_K, q5_0 / q4_0 (run as q8_0)",
+                       t->name.c_str(), mio::ggml_type_name(t->type));
         return false;
     }
-    const mio::SplitLayout L = mio::split_layout(t->type, t->ne[1], t->ne[0]);
+    // Q5_0 (llama-quantize's Q4_K fallback for rows not a multiple of 256) and Q4_0 rows run as
+    // the Q8_0 rows they equal exactly (quant.h repack_to_q8_0)
+    const uint32_t type = repack ? (uint32_t)mio::GGML_Q8_0 : t->type;
+    std::vector<uint8_t> q80;
+    const void *src = t->data;
+    if (repack) {
+        q80.resize((size_t)t->ne[1] * (size_t)(t->ne[0] / 32) * sizeof(mio::BlockQ8_0));
+        if (!mio::repack_to_q8_0(t->type, t->data, t->ne[1], t->ne[0], q80.data())) {
+            mio::set_error("llm: repacking %s (%s) as q8_0 failed", t->name.c_str(), mio::ggml_type_name(t->type));
+            return false;
+        }
+        src = q80.data();
+    }
+    const mio::SplitLayout L = mio::split_layout(type, t->ne[1], t->ne[0]);
     const auto it = m->arena_off.find(t->name);
     uint8_t *dp = (m->arena && it != m->arena_off.end()) ? m->arena + it->second : dalloc<uint8_t>(m, L.bytes);
     uint8_t *host = dp && m->stager ? m->stager->acquire(L.bytes) : nullptr;
@@ -190,7 +198,7 @@ bool upload_qmat(mio_hip_llm *m, const mio::GgufTensor *t, mio::QMat &q) {
         mio::set_error("llm: staging / device buffer for %s failed", t->name.c_str());
         return false;
     }
-    if (!mio::to_split(t->type, t->data, t->ne[1], t->ne[0], host)) {
+    if (!mio::to_split(type, src, t->ne[1], t->ne[0], host)) {
         mio::set_error("llm: re-layout of %s failed", t->name.c_str());
         return false;
     }
@@ -198,7 +206,7 @@ bool upload_qmat(mio_hip_llm *m, const mio::GgufTensor *t, mio::QMat &q) {
         mio::set_error("llm: upload of %s failed", t->name.c_str());
         return false;
     }
-    q.type = (int)t->type;
+    q.type = (int)type;
     q.rows = (int)t->ne[1];
     q.k = (int)t->ne[0];
     q.p0 = dp + L.off[0];
@@ -372,7 +380,12 @@ int prefill(mio_hip_llm *m, int n) {
     return MIO_OK;
 }
 
+// Every prompt upload starts a new prefill / generation: the attention chunk tickets are
+// zeroed in stream order first (the last chunk workgroup of every attention launch resets its
+// ticket, so they are 0 here anyway; this keeps an interrupted run from carrying a count over).
 int upload_prompt(mio_hip_llm *m, const int32_t *prompt, int n) {
+    MIO_HIP_CHECK(hipMemsetAsync(m->buf.att_cnt, 0, (size_t)m->dims.n_kv * sizeof(int), m->d->stream));
+    MIO_HIP_CHECK(hipMemsetAsync(m->pf.att_cnt, 0, (size_t)mio::kPrefillB * m->dims.n_kv * sizeof(int), m->d->stream));
     MIO_HIP_CHECK(hipMemcpyAsync(m->d_prompt, prompt, (size_t)n * 4, hipMemcpyHostToDevice, m->d->stream));
     return MIO_OK;
 }
@@ -610,7 +623,8 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
             if (!t) continue;
             size_t bytes = 0;
             if (t->n_dims == 2 && t->type != mio::GGML_F32) {
-                bytes = mio::split_layout(t->type, t->ne[1], t->ne[0]).bytes;
+                const uint32_t ty = mio::repacks_to_q8_0(t->type) ? (uint32_t)mio::GGML_Q8_0 : t->type;
+                bytes = mio::split_layout(ty, t->ne[1], t->ne[0]).bytes;
             } else if (t->type == mio::GGML_F32) {
                 bytes = (size_t)t->nelements() * 4;
             }
@@ -731,19 +745,6 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
         }
         m->layers.push_back(L);
     }
-    // per-launch weight ranges (trace_kernel cache-warm diagnostic)
-    auto span = [&](const mio::QMat &a, const mio::QMat &z) {
-        const mio::SplitLayout L = mio::split_layout(z.type, z.rows, z.k);
-        return mio_hip_llm::Range{a.p0, (uint64_t)(z.p0 + L.bytes - a.p0)};
-    };
-    for (const mio::LayerW &L : m->layers) {
-        m->ranges.push_back(L.conv ? span(L.in_proj, L.in_proj) : span(L.wq, L.wv));
-        m->ranges.push_back({});
-        m->ranges.push_back(L.conv ? span(L.out_proj, L.out_proj) : span(L.wo, L.wo));
-        m->ranges.push_back(span(L.gate, L.up));
-        m->ranges.push_back(span(L.down, L.down));
-    }
-    m->ranges.push_back(span(m->lm, m->lm));
     // buffers
     const int qkv = (D.n_head + 2 * D.n_kv) * D.hd;
     // q|k|v rows, or an lfm2 short-conv layer's B | C | X rows
@@ -765,6 +766,8 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
     want(m->buf.h, D.n_ff);
     want(m->buf.logits, D.n_vocab);
     want(m->buf.part, (size_t)D.n_head * D.max_splits * (D.hd + 4));
+    want(m->buf.att, (size_t)D.n_head * D.hd);
+    want(m->buf.att_cnt, (size_t)D.n_kv);
     want(m->buf.smp, 2 * std::max(mio::lm_head_blocks(D), 4 * D.n_wg) + 16);
     want(m->buf.st, 1);
     want(m->d_cfg, 1);
@@ -783,6 +786,8 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
     want(m->pf.qkv, (size_t)mio::kPrefillB * qkv_rows);
     want(m->pf.h, (size_t)mio::kPrefillB * D.n_ff);
     want(m->pf.part, (size_t)mio::kPrefillB * D.n_head * D.max_splits * (D.hd + 4));
+    want(m->pf.att, (size_t)mio::kPrefillB * D.n_head * D.hd);
+    want(m->pf.att_cnt, (size_t)mio::kPrefillB * D.n_kv);
     want(m->pf.act, mio::prefill_act_bytes(std::max(std::max(D.n_embd, D.n_ff), D.n_head * D.hd)));
     want(dr, (size_t)n_ctx * (D.hd / 2));
     want(m->d_iota, (size_t)n_ctx + mio::kPrefillB);
@@ -811,7 +816,7 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
         }
     }
     if (!m->kc || !m->vc || !m->buf.x || !m->buf.qkv || !m->buf.h || !m->buf.logits ||
-        !m->buf.part || !m->buf.smp || !m->buf.st || !m->d_cfg || !m->d_tokens || !m->d_force || !dr ||
+        !m->buf.part || !m->buf.att || !m->buf.att_cnt || !m->pf.att || !m->pf.att_cnt || !m->buf.smp || !m->buf.st || !m->d_cfg || !m->d_tokens || !m->d_force || !dr ||
         !m->d_prompt || !m->pf.x || !m->pf.qkv || !m->pf.h || !m->pf.part || !m->pf.act || !m->d_iota ||
         (any_conv && !m->buf.ring)) {
         mio::set_error("llm_load: device allocation failed");
@@ -1232,11 +1237,21 @@ extern "C" int mio_hip_llm_logits(mio_hip_llm *m, float *logits) {
 extern "C" int mio_hip_debug_matvec(mio_hip_device *d, uint32_t type, const void *gguf_rows, int rows, int k,
                                     const float *x, float *y) {
     MIO_REQUIRE(d && gguf_rows && x && y && rows > 0 && k > 0, MIO_ERR_INVALID, "debug_matvec: bad args");
-    MIO_REQUIRE(type == mio::GGML_Q8_0 || type == mio::GGML_Q4_K || type == mio::GGML_Q6_K, MIO_ERR_UNSUPPORTED,
-                "debug_matvec: type %u", type);
-    MIO_REQUIRE(k % (type == mio::GGML_Q8_0 ? 32 : 256) == 0, MIO_ERR_INVALID, "debug_matvec: k %d", k);
+    MIO_REQUIRE(type == mio::GGML_Q8_0 || type == mio::GGML_Q4_K || type == mio::GGML_Q6_K ||
+                    mio::repacks_to_q8_0(type),
+                MIO_ERR_UNSUPPORTED, "debug_matvec: type %u", type);
+    const bool k32 = type == mio::GGML_Q8_0 || mio::repacks_to_q8_0(type);
+    MIO_REQUIRE(k % (k32 ? 32 : 256) == 0, MIO_ERR_INVALID, "debug_matvec: k %d", k);
     int rc = mio::bind(d);
     if (rc) return rc;
+    // Q4_0 / Q5_0 run as the Q8_0 rows they equal (llm_load does the same)
+    std::vector<uint8_t> q80;
+    if (mio::repacks_to_q8_0(type)) {
+        q80.resize((size_t)rows * (k / 32) * sizeof(mio::BlockQ8_0));
+        mio::repack_to_q8_0(type, gguf_rows, rows, k, q80.data());
+        gguf_rows = q80.data();
+        type = mio::GGML_Q8_0;
+    }
     const mio::SplitLayout L = mio::split_layout(type, rows, k);
     std::vector<uint8_t> host(L.bytes);
     mio::to_split(type, gguf_rows, rows, k, host.data());
@@ -1376,13 +1391,16 @@ extern "C" int mio_hip_llm_time_kernel(mio_hip_llm *m, int which, int iters, flo
     // the position the attention kernels work at (cur_pos: pos + pending)
     const uint64_t pos = (uint64_t)std::max(0, std::min(st.pos + st.pending, D.n_ctx - 1));
     const uint64_t nch = pos / mio::kAttChunk + 1, qkv = (uint64_t)(D.n_head + 2 * D.n_kv) * D.hd;
-    const uint64_t part = 4ull * D.n_head * nch * (D.hd + 2);  // chunk partial records {O, m, l}
+    // chunk partial records {O, m, l}: written by the chunk workgroups, read back by the
+    // merging one (attn_merge_last), which writes the n_head * hd outputs
+    const uint64_t part = 4ull * D.n_head * nch * (D.hd + 2);
     uint64_t b = 0;
-    const uint64_t att_bytes = 2ull * 2 * D.n_kv * D.hd * (pos + 1) + 4ull * qkv + 8ull * (D.hd / 2) + part;
+    const uint64_t att_bytes = 2ull * 2 * D.n_kv * D.hd * (pos + 1) + 4ull * qkv + 8ull * (D.hd / 2) + 2 * part +
+                               4ull * D.n_head * D.hd;
     switch (which) {
         case 0: b = qbytes(L.wq) + qbytes(L.wk) + qbytes(L.wv) + 4ull * D.n_embd + 4ull * qkv; break;
         case 1: b = att_bytes; break;
-        case 2: b = qbytes(L.wo) + part + 4ull * D.n_embd * 2; break;
+        case 2: b = qbytes(L.wo) + 4ull * D.n_head * D.hd + 4ull * D.n_embd * 2; break;
         case 3: b = qbytes(L.gate) + qbytes(L.up) + 4ull * (D.n_embd * 2 + D.n_ff); break;
         case 4: b = qbytes(L.down) + 4ull * (D.n_ff + 2 * D.n_embd); break;
         case 6: b = qbytes(m->lm) + 4ull * D.n_vocab; break;

@@ -42,6 +42,83 @@ void quantize_row_q8_0(const float *x, void *vy, int64_t k) {
     }
 }
 
+// ggml quantize_row_q4_0_ref / quantize_row_q5_0_ref: d = max / -8 (-16) with max the
+// signed value of largest magnitude, codes min(15 (31), (int8)(x / d + 8.5 (16.5))); Q5_0's
+// fifth bits packed into qh (bit j: element j, bit j + 16: element j + 16)
+static int64_t block_signed_max(const float *x, int n, float &amax) {
+    amax = 0.0f;
+    int64_t at = 0;
+    for (int j = 0; j < n; ++j)
+        if (std::fabs(x[j]) > amax) amax = std::fabs(x[j]), at = j;
+    return at;
+}
+void quantize_row_q4_0(const float *x, void *vy, int64_t k) {
+    BlockQ4_0 *y = (BlockQ4_0 *)vy;
+    for (int64_t i = 0; i < k / 32; ++i) {
+        const float *xb = x + i * 32;
+        float amax;
+        const float mx = xb[block_signed_max(xb, 32, amax)];
+        const float d = mx / -8.0f, id = d ? 1.0f / d : 0.0f;
+        y[i].d = f32_to_fp16(d);
+        for (int j = 0; j < 16; ++j) {
+            const uint8_t a = (uint8_t)std::min(15, (int)(int8_t)(xb[j] * id + 8.5f));
+            const uint8_t b = (uint8_t)std::min(15, (int)(int8_t)(xb[16 + j] * id + 8.5f));
+            y[i].qs[j] = a | (uint8_t)(b << 4);
+        }
+    }
+}
+void quantize_row_q5_0(const float *x, void *vy, int64_t k) {
+    BlockQ5_0 *y = (BlockQ5_0 *)vy;
+    for (int64_t i = 0; i < k / 32; ++i) {
+        const float *xb = x + i * 32;
+        float amax;
+        const float mx = xb[block_signed_max(xb, 32, amax)];
+        const float d = mx / -16.0f, id = d ? 1.0f / d : 0.0f;
+        y[i].d = f32_to_fp16(d);
+        uint32_t qh = 0;
+        for (int j = 0; j < 16; ++j) {
+            const uint8_t a = (uint8_t)std::min(31, (int)(int8_t)(xb[j] * id + 16.5f));
+            const uint8_t b = (uint8_t)std::min(31, (int)(int8_t)(xb[16 + j] * id + 16.5f));
+            y[i].qs[j] = (uint8_t)((a & 0x0F) | ((b & 0x0F) << 4));
+            qh |= ((uint32_t)(a & 0x10) >> 4) << j;
+            qh |= ((uint32_t)(b & 0x10) >> 4) << (j + 16);
+        }
+        std::memcpy(y[i].qh, &qh, 4);
+    }
+}
+
+// the signed codes of one Q4_0 / Q5_0 block (ggml dequantize_row_q4_0 / _q5_0 before * d)
+static void block_codes_4_5(uint32_t type, const uint8_t *blk, int8_t (&q)[32], uint16_t &d) {
+    std::memcpy(&d, blk, 2);
+    if (type == GGML_Q4_0) {
+        const uint8_t *qs = blk + 2;
+        for (int j = 0; j < 16; ++j) q[j] = (int8_t)((qs[j] & 0x0F) - 8), q[j + 16] = (int8_t)((qs[j] >> 4) - 8);
+    } else {
+        uint32_t qh;
+        std::memcpy(&qh, blk + 2, 4);
+        const uint8_t *qs = blk + 6;
+        for (int j = 0; j < 16; ++j) {
+            q[j] = (int8_t)(((qs[j] & 0x0F) | (((qh >> j) << 4) & 0x10)) - 16);
+            q[j + 16] = (int8_t)(((qs[j] >> 4) | ((qh >> (j + 12)) & 0x10)) - 16);
+        }
+    }
+}
+
+bool repacks_to_q8_0(uint32_t type) { return type == GGML_Q4_0 || type == GGML_Q5_0; }
+
+bool repack_to_q8_0(uint32_t type, const void *src, int64_t R, int64_t K, void *dst) {
+    if (!repacks_to_q8_0(type) || K % 32) return false;
+    const size_t bb = type == GGML_Q4_0 ? sizeof(BlockQ4_0) : sizeof(BlockQ5_0);
+    const uint8_t *s = (const uint8_t *)src;
+    BlockQ8_0 *y = (BlockQ8_0 *)dst;
+    for (int64_t i = 0; i < R * (K / 32); ++i) {
+        int8_t q[32];
+        block_codes_4_5(type, s + (size_t)i * bb, q, y[i].d);
+        std::memcpy(y[i].qs, q, 32);
+    }
+    return true;
+}
+
 // Simplified K-quant quantizers (one pass, min/max scales). Any byte pattern of the
 // right layout is a valid model for the synthetic benchmark; these keep the
 // dequantized weights close to the generating N(0, s) values.
@@ -148,6 +225,8 @@ bool quantize_row(uint32_t type, const float *x, void *y, int64_t k) {
             for (int64_t i = 0; i < k; ++i) ((uint16_t *)y)[i] = f32_to_fp16(x[i]);
             return true;
         case GGML_Q8_0: quantize_row_q8_0(x, y, k); return true;
+        case GGML_Q4_0: quantize_row_q4_0(x, y, k); return true;
+        case GGML_Q5_0: quantize_row_q5_0(x, y, k); return true;
         case GGML_Q4_K: quantize_row_q4_K(x, y, k); return true;
         case GGML_Q6_K: quantize_row_q6_K(x, y, k); return true;
         default: return false;
@@ -166,6 +245,18 @@ bool dequantize_row(uint32_t type, const void *vx, float *y, int64_t k) {
             for (int64_t i = 0; i < k / 32; ++i) {
                 const float d = fp16_to_f32(x[i].d);
                 for (int j = 0; j < 32; ++j) y[i * 32 + j] = x[i].qs[j] * d;
+            }
+            return true;
+        }
+        case GGML_Q4_0:
+        case GGML_Q5_0: {
+            const size_t bb = type == GGML_Q4_0 ? sizeof(BlockQ4_0) : sizeof(BlockQ5_0);
+            for (int64_t i = 0; i < k / 32; ++i) {
+                int8_t q[32];
+                uint16_t dh;
+                block_codes_4_5(type, (const uint8_t *)vx + (size_t)i * bb, q, dh);
+                const float d = fp16_to_f32(dh);
+                for (int j = 0; j < 32; ++j) y[i * 32 + j] = q[j] * d;
             }
             return true;
         }

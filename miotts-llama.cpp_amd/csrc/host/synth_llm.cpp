@@ -64,6 +64,13 @@ SynthLlmCfg synth_llm_preset(int p) {
             c.name = "tiny-lfm2-q4km", c.arch = "lfm2", c.n_layer = 5, c.attn_mod = 3, c.attn_at0 = 1, c.qtype = 15;
             c.rope_base = 1000000.f, c.rms_eps = 1e-5f;
             break;
+        case 9:
+            c.name = "tiny-q4km-576", c.arch = "qwen3", c.n_embd = 576, c.n_layer = 3, c.n_head = 9,
+            c.n_head_kv = 3, c.head_dim = 64, c.n_ff = 1536, c.qtype = 15, c.rope_base = 1000000.f;
+            break;
+        case 10:
+            c.name = "tiny-q4_0", c.qtype = 2;
+            break;
         default: break;
     }
     return c;
@@ -103,7 +110,7 @@ bool synth_write_llm(const std::string &path, const SynthLlmCfg &c) {
     const bool lfm2 = a == "lfm2";
     w.kv_str("general.architecture", a);
     w.kv_str("general.name", c.name);
-    w.kv_u32("general.file_type", c.qtype == 15 ? 15 : 7);
+    w.kv_u32("general.file_type", c.qtype == 15 ? 15 : (c.qtype == 2 ? 2 : 7));
     w.kv_u32(a + ".context_length", c.n_ctx);
     w.kv_u32(a + ".embedding_length", c.n_embd);
     w.kv_u32(a + ".block_count", c.n_layer);
@@ -147,10 +154,11 @@ bool synth_write_llm(const std::string &path, const SynthLlmCfg &c) {
         int fill;  // 0 quantized N(0, w_std) rows, 1 ones, 2 f32 N(0, 0.5) (biases / conv taps)
     };
     std::vector<T> ts;
-    const uint32_t base = c.qtype == 15 ? GGML_Q4_K : GGML_Q8_0;
-    const uint32_t more = c.qtype == 15 ? GGML_Q6_K : GGML_Q8_0;
+    const uint32_t base = c.qtype == 15 ? GGML_Q4_K : (c.qtype == 2 ? GGML_Q4_0 : GGML_Q8_0);
+    const uint32_t more = c.qtype == 15 ? GGML_Q6_K : (c.qtype == 2 ? GGML_Q4_0 : GGML_Q8_0);
     const int q_dim = c.n_head * c.head_dim, kv_dim = c.n_head_kv * c.head_dim;
-    ts.push_back({"token_embd.weight", c.qtype == 15 ? GGML_Q6_K : GGML_Q8_0, c.n_embd, c.n_vocab, false});
+    const uint32_t emb = c.qtype == 15 ? GGML_Q6_K : (c.qtype == 2 ? GGML_Q4_0 : GGML_Q8_0);
+    ts.push_back({"token_embd.weight", emb, c.n_embd, c.n_vocab, false});
     for (int i = 0; i < c.n_layer; ++i) {
         const std::string p = "blk." + std::to_string(i) + ".";
         const bool mb = use_more_bits(i, c.n_layer);
@@ -183,6 +191,13 @@ bool synth_write_llm(const std::string &path, const SynthLlmCfg &c) {
     // lfm2's final norm is token_embd_norm (llama.cpp model.tok_norm)
     ts.push_back({lfm2 ? "token_embd_norm.weight" : "output_norm.weight", GGML_F32, c.n_embd, 1, true});
     if (!c.tied) ts.push_back({"output.weight", more, c.n_embd, c.n_vocab, false});
+    // llama-quantize: a K-quant needs rows of whole 256-element super-blocks
+    if (c.kq_fallback)
+        for (auto &t : ts)
+            if (t.k % 256 != 0) {
+                if (t.type == GGML_Q4_K) t.type = GGML_Q5_0;
+                if (t.type == GGML_Q6_K) t.type = GGML_Q8_0;
+            }
     for (auto &t : ts) {
         if (t.rows == 1)
             w.add_tensor(t.name, t.type, {t.k});

@@ -15,7 +15,7 @@ import numpy as np
 _SCALAR = {0: "<B", 1: "<b", 2: "<H", 3: "<h", 4: "<I", 5: "<i", 6: "<f", 7: "<?",
            10: "<Q", 11: "<q", 12: "<d"}
 _TYPE_BLOCK = {0: (1, 4), 1: (1, 2), 30: (1, 2), 24: (1, 1), 25: (1, 2), 26: (1, 4),
-               2: (32, 18), 8: (32, 34), 12: (256, 144), 14: (256, 210), 15: (256, 292)}
+               2: (32, 18), 6: (32, 22), 8: (32, 34), 12: (256, 144), 14: (256, 210), 15: (256, 292)}
 
 
 @dataclass

@@ -11,6 +11,9 @@
  *       Q4_K / Q6_K  -> Q8_K activations (quantize_row_q8_K_ref: iscale = -127/max_signed,
  *                       q = min(127, nearest_int(iscale*x)), d = 1/iscale f32, bsums/16)
  *   - vec_dot_q8_0_q8_0 : sum_b (float)isum_b * (dw_b * da_b)
+ *   - vec_dot_q4_0_q8_0 / vec_dot_q5_0_q8_0 (vec_dot_type Q8_0): per block
+ *       (dw_b * da_b) * (isum over the low 16 codes + isum over the high 16), codes
+ *       (nibble - 8) / (nibble | fifth bit from qh) - 16
  *   - vec_dot_q4_K_q8_K : per superblock d*da*sum_j sc_j*dot_j - dmin*da*sum_j m_j*bsum_j
  *   - vec_dot_q6_K_q8_K : per superblock d*da*sum_j sc_j*dot_j  (q6 - 32)
  * Integer parts are exact; the GPU reproduces them bit-for-bit per superblock.
@@ -106,6 +109,44 @@ void mo_quantize_q8_K(const float *x, int64_t k, float *d, int8_t *qs, int16_t *
         }
         d[i] = 1 / iscale;
     }
+}
+
+/* codes of element j and j + 16 of a Q4_0 (18-byte) / Q5_0 (22-byte) block (ggml
+ * dequantize_row_q4_0 / _q5_0 before the scale) */
+static void q45_codes(uint32_t type, const uint8_t *blk, int j, int *x0, int *x1) {
+    if (type == 2) {
+        const uint8_t q = blk[2 + j];
+        *x0 = (q & 0x0F) - 8;
+        *x1 = (q >> 4) - 8;
+    } else {
+        uint32_t qh;
+        memcpy(&qh, blk + 2, 4);
+        const uint8_t q = blk[6 + j];
+        const uint32_t h0 = ((qh & (1u << j)) >> j) << 4;
+        const uint32_t h1 = (qh & (1u << (j + 16))) >> (j + 12);
+        *x0 = (int)((q & 0x0F) | h0) - 16;
+        *x1 = (int)((q >> 4) | h1) - 16;
+    }
+}
+
+/* vec_dot_q4_0_q8_0 / vec_dot_q5_0_q8_0 */
+float mo_vec_dot_q45_0(uint32_t type, const uint8_t *row, int64_t k, const uint16_t *ad, const int8_t *aq) {
+    const int bb = type == 2 ? 18 : 22;
+    float sumf = 0;
+    for (int64_t b = 0; b < k / 32; b++) {
+        const uint8_t *blk = row + b * bb;
+        uint16_t dw;
+        memcpy(&dw, blk, 2);
+        int sumi0 = 0, sumi1 = 0;
+        for (int j = 0; j < 16; j++) {
+            int x0, x1;
+            q45_codes(type, blk, j, &x0, &x1);
+            sumi0 += x0 * aq[b * 32 + j];
+            sumi1 += x1 * aq[b * 32 + j + 16];
+        }
+        sumf += (mo_fp16_to_f32(dw) * mo_fp16_to_f32(ad[b])) * (float)(sumi0 + sumi1);
+    }
+    return sumf;
 }
 
 /* row dot products; x = one weight row in GGUF block layout */
@@ -225,6 +266,19 @@ int mo_dequantize_row(uint32_t type, const uint8_t *row, int64_t k, float *y) {
             const int8_t *q = (const int8_t *)(row + 34 * b + 2);
             for (int j = 0; j < 32; j++) y[b * 32 + j] = q[j] * d;
         }
+    } else if (type == 2 || type == 6) {
+        const int bb = type == 2 ? 18 : 22;
+        for (int64_t b = 0; b < k / 32; b++) {
+            uint16_t dh;
+            memcpy(&dh, row + bb * b, 2);
+            const float d = mo_fp16_to_f32(dh);
+            for (int j = 0; j < 16; j++) {
+                int x0, x1;
+                q45_codes(type, row + bb * b, j, &x0, &x1);
+                y[b * 32 + j] = x0 * d;
+                y[b * 32 + j + 16] = x1 * d;
+            }
+        }
     } else if (type == 12) {
         for (int64_t b = 0; b < k / 256; b++) {
             const uint8_t *blk = row + 144 * b;
@@ -289,6 +343,10 @@ int mo_matvec(uint32_t type, const uint8_t *w, int rows, int64_t k, const float 
         rb = (size_t)k / 32 * 34;
         mo_quantize_q8_0(x, k, d0, qs);
         for (int r = 0; r < rows; r++) y[r] = mo_vec_dot_q8_0(w + r * rb, k, d0, qs);
+    } else if (type == 2 || type == 6) {
+        rb = (size_t)k / 32 * (type == 2 ? 18 : 22);
+        mo_quantize_q8_0(x, k, d0, qs);
+        for (int r = 0; r < rows; r++) y[r] = mo_vec_dot_q45_0(type, w + r * rb, k, d0, qs);
     } else if (type == 12 || type == 14) {
         rb = (size_t)k / 256 * (type == 12 ? 144 : 210);
         mo_quantize_q8_K(x, k, dk, qs, bs);

@@ -1,6 +1,7 @@
 """GPU parity: HIP LLM decode step (csrc/hip/llm_kernels.hip) vs the oracle.
 
-1. Single matvec per quant type (Q8_0 / Q4_K / Q6_K) on random data: the GPU's per-
+1. Single matvec per quant type (Q8_0 / Q4_K / Q6_K, and Q5_0 / Q4_0, which run as the Q8_0
+   rows they equal exactly) on random data: the GPU's per-
    superblock integer sums are exact, only the float sum over superblocks is reordered:
    |y_gpu - y_ref| <= 1e-5 * sum_b |partial_b| (bounded here by 2e-5 * max|y| + 1e-6).
 2. Teacher-forced logits: tiny models over 80 positions, the 1.7B model over 300 positions
@@ -31,10 +32,11 @@ pytestmark = pytest.mark.gpu
 @pytest.fixture(scope="module")
 def llm_files(tmp_path_factory):
     d = tmp_path_factory.mktemp("llm_gpu")
-    return {p: m.synth_llm(str(d / f"llm{p}.gguf"), p, 1) for p in (0, 1)}
+    return {p: m.synth_llm(str(d / f"llm{p}.gguf"), p, 1) for p in (0, 1, 9, 10)}
 
 
-@pytest.mark.parametrize("qtype,k", [(8, 576), (8, 2048), (12, 2048), (12, 6144), (14, 2048), (14, 768)])
+@pytest.mark.parametrize("qtype,k", [(8, 576), (8, 2048), (12, 2048), (12, 6144), (14, 2048), (14, 768),
+                                     (6, 576), (6, 2048), (2, 2048)])
 def test_matvec_exact_per_type(device, qtype, k):
     rng = np.random.default_rng(qtype * 1000 + k)
     rows = 37
@@ -51,7 +53,9 @@ def test_matvec_exact_per_type(device, qtype, k):
     assert np.abs(y - yo).max() <= 2e-5 * np.abs(yo).max() + 1e-6, np.abs(y - yo).max()
 
 
-@pytest.mark.parametrize("preset", [0, 1])
+# 9: Q4_K_M at the 0.1B width, whose q/k/v, O, gate/up and embedding rows (576 long) are
+# llama-quantize's Q5_0 / Q8_0 fallbacks; 10: Q4_0 (Q5_0 and Q4_0 run as the equal Q8_0 rows)
+@pytest.mark.parametrize("preset", [0, 1, 9, 10])
 def test_teacher_forced_logits_tiny(device, llm_files, preset):
     g = m.Llm(device, llm_files[preset], 256)
     o = pyoracle.Llm(llm_files[preset], 256)
@@ -68,7 +72,7 @@ def test_teacher_forced_logits_tiny(device, llm_files, preset):
     assert agree >= 76
 
 
-@pytest.mark.parametrize("preset", [0, 1])
+@pytest.mark.parametrize("preset", [0, 1, 9])
 def test_generate_matches_oracle(device, llm_files, preset):
     g = m.Llm(device, llm_files[preset], 256)
     o = pyoracle.Llm(llm_files[preset], 256)
@@ -243,7 +247,7 @@ def test_loader_rejects_unknown_biases_and_incomplete_lfm2(device, tmp_path):
 # token in the same order, so the last token's logits (and therefore the KV cache rows they
 # read) equal a token-by-token decode BIT FOR BIT; vs the oracle the teacher-forced bound
 # above applies.
-@pytest.mark.parametrize("preset,n", [(0, 2), (0, 17), (1, 40), (0, 150)])
+@pytest.mark.parametrize("preset,n", [(0, 2), (0, 17), (1, 40), (0, 150), (9, 70)])
 def test_batched_prefill_matches_sequential(device, llm_files, preset, n):
     g = m.Llm(device, llm_files[preset], 256)
     toks = np.random.default_rng(100 + n).integers(0, g.n_vocab, n)

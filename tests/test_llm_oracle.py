@@ -139,3 +139,58 @@ def test_qwen2_bias_oracle_and_rewrite(tmp_path):
     lf = str(tmp_path / "lfm2.gguf")
     gguf_np.rewrite(src, lf, arch="lfm2")
     assert gguf_np.GGUFReader(lf).kv["general.architecture"] == "lfm2"
+
+
+def _np_q45_codes(qtype, blocks):
+    """numpy restatement of ggml dequantize_row_q4_0 / _q5_0 codes (before * d): blocks
+    [n][18 | 22] bytes -> [n][32] int codes and the f16 scales."""
+    d = blocks[:, 0:2].copy().view(np.float16).astype(np.float32)[:, 0]
+    if qtype == 2:
+        qs = blocks[:, 2:18].astype(np.int32)
+        lo, hi = (qs & 0x0F) - 8, (qs >> 4) - 8
+    else:
+        qh = blocks[:, 2:6].copy().view(np.uint32)[:, 0].astype(np.int64)
+        qs = blocks[:, 6:22].astype(np.int32)
+        j = np.arange(16)
+        lo = (qs & 0x0F) | ((((qh[:, None] >> j) << 4) & 0x10)).astype(np.int32)
+        hi = (qs >> 4) | ((qh[:, None] >> (j + 12)) & 0x10).astype(np.int32)
+        lo, hi = lo - 16, hi - 16
+    return np.concatenate([lo, hi], axis=1), d
+
+
+@pytest.mark.parametrize("qtype", [2, 6])
+def test_q4_0_q5_0_rows(qtype):
+    """llama-quantize's Q4_K fallback (Q5_0) and Q4_0: the host quantizer's blocks decode to
+    the same values in the oracle (mo_dequantize_row) and in a numpy restatement of ggml's
+    dequantizer, within the format's step of the input; the oracle's vec_dot_q5_0_q8_0 /
+    q4_0_q8_0 equals the numpy block sum over Q8_0 activations (the GPU runs these rows as
+    the equal Q8_0 rows, tests/test_llm_gpu.py)."""
+    rng = np.random.default_rng(40 + qtype)
+    k = 576
+    x = (rng.standard_normal((5, k)) * 0.02).astype(np.float32)
+    x[1, 7] = 0.3  # a positive block max (d < 0)
+    q = m.quantize_rows(qtype, x)
+    bb = 18 if qtype == 2 else 22
+    codes, d = _np_q45_codes(qtype, q.reshape(-1, bb))
+    lo = -8 if qtype == 2 else -16
+    assert codes.min() >= lo and codes.max() <= -lo - 1
+    want = (codes.astype(np.float32) * d[:, None]).reshape(5, k)
+    got = _dequant(qtype, q, k)
+    assert np.array_equal(got, want)
+    step = 1.0 / (8 if qtype == 2 else 16)
+    blk = np.abs(x.reshape(-1, 32)).max(1, keepdims=True)
+    assert (np.abs(got - x).reshape(-1, 32) <= step * blk * 1.01 + 1e-7).all()
+    # vec_dot against Q8_0 activations (ggml vec_dot_type)
+    a = rng.standard_normal(k).astype(np.float32)
+    o = pyoracle.oracle()
+    o.mo_matvec.argtypes = [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_void_p,
+                            ctypes.c_void_p]
+    y = np.zeros(5, np.float32)
+    assert o.mo_matvec(qtype, q.ctypes.data, 5, k, a.ctypes.data, y.ctypes.data) == 0
+    aq = a.reshape(-1, 32)
+    da = (np.abs(aq).max(1) / 127).astype(np.float16).astype(np.float32)
+    ida = np.where(da > 0, 1.0 / (np.abs(aq).max(1) / 127), 0).astype(np.float32)
+    qa = np.round(aq * ida[:, None]).astype(np.int32)
+    c = codes.reshape(5, -1, 32)
+    ref = ((d.reshape(5, -1) * da[None]) * (c * qa[None]).sum(2)).sum(1)
+    assert np.allclose(y, ref, rtol=1e-5, atol=1e-6)
