@@ -17,7 +17,7 @@ extern "C" int mio_synth_voice_gguf(const char *path, uint64_t seed) {
 }
 
 extern "C" int mio_synth_llm_gguf(const char *path, int preset, uint64_t seed) {
-    MIO_REQUIRE(path && preset >= 0 && preset <= 10, MIO_ERR_INVALID, "synth_llm: bad args");
+    MIO_REQUIRE(path && preset >= 0 && preset <= 12, MIO_ERR_INVALID, "synth_llm: bad args");
     mio::SynthLlmCfg c = mio::synth_llm_preset(preset);
     c.seed = seed;
     MIO_REQUIRE(mio::synth_write_llm(path, c), MIO_ERR_IO, "synth_llm: cannot write %s", path);

@@ -69,7 +69,7 @@ __global__ __launch_bounds__(MT) void k_attn_in(LlmDims d, const float *norm_w, 
         x_after_weights(xr);
         MIO_TRACE(b, 1);
         MIO_TL_MARK1(b);
-        rmsnorm_quant(xr, K, d.eps, TQ != 8, s, MIO_TL_DIAGSLOT(b));
+        rmsnorm_quant(xr, K, d.eps, akind(TQ), s, MIO_TL_DIAGSLOT(b));
         MIO_TRACE(b, 2);
         MIO_TL_MARK(b, 2);
         stream_rows<TQ, NP, 1, SU, MIO_SMALL_AUX>(wq, wk, lo, hi, ga, gb, s.a, [&](int row, float v, float) {
@@ -83,7 +83,7 @@ __global__ __launch_bounds__(MT) void k_attn_in(LlmDims d, const float *norm_w, 
         load_first<TV, NP, 1, SU, MIO_SMALL_AUX>(wv, wv, lo, hi, ga, gb);
         sample_prologue();
         x_after_weights(xr);
-        rmsnorm_quant(xr, K, d.eps, TQ != 8, s, MIO_TL_DIAGSLOT(b));
+        rmsnorm_quant(xr, K, d.eps, akind(TV), s, MIO_TL_DIAGSLOT(b));
         stream_rows<TV, NP, 1, SU, MIO_SMALL_AUX>(wv, wv, lo, hi, ga, gb, s.a, [&](int row, float v, float) {
             put(o2 + row, v);
         });
@@ -112,8 +112,8 @@ void launch(const LlmDims &d, const LayerW &L, int il, const QMat &tok_embd, con
                                        L.attn_norm, L.wq, L.wk, L.wv, g_qk, b, tok_embd, nblk);
             });
         };
-        if constexpr (TQ == 8) {
-            go.template operator()<8>();
+        if constexpr (TQ == 8 || TQ == 30) {
+            go.template operator()<TQ>();
         } else {
             if (L.wv.type == 14)
                 go.template operator()<14>();

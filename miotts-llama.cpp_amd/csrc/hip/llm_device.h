@@ -189,22 +189,21 @@ struct ActL {
 };
 
 struct Smem {
-    float *xs;   // [K] float staging
     ActL a;
     double *red; // [16]
 };
 
-// LDS layout: xs f32[K] | qs i8[K] | d f32[K/32+8] | bs i16[K/16+8] | red
+// LDS layout: qs [2K bytes: int8 codes (Q8_0 / Q8_K) or bf16 values (BF16 weights)] |
+// d f32[K/32+8] | bs i16[K/16+8] | red
 __host__ __device__ inline size_t smem_bytes(int K) {
-    return (size_t)K * 4 + (size_t)K + (size_t)(K / 32 + 8) * 4 + (size_t)(K / 16 + 8) * 2 + 128;
+    return (size_t)K * 2 + (size_t)(K / 32 + 8) * 4 + (size_t)(K / 16 + 8) * 2 + 128;
 }
 
 __device__ inline Smem carve(char *base, int K) {
     Smem s;
-    s.xs = (float *)base;
-    s.a.qs = (int8_t *)(base + (size_t)K * 4);
-    s.a.d = (float *)(base + (size_t)K * 5);
-    s.a.bs = (int16_t *)(base + (size_t)K * 5 + (size_t)(K / 32 + 8) * 4);
+    s.a.qs = (int8_t *)base;
+    s.a.d = (float *)(base + (size_t)K * 2);
+    s.a.bs = (int16_t *)(base + (size_t)K * 2 + (size_t)(K / 32 + 8) * 4);
     s.red = (double *)(base + smem_bytes(K) - 128);
     return s;
 }
@@ -256,30 +255,6 @@ __device__ __forceinline__ float abs_max4(const float (&v)[4]) {
     return wave_max_f(fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))), 0.0f);
 }
 
-// One superblock per wave and pass (4 values per lane), NI passes (K <= NI * 2048) unrolled
-// so their reduction chains interleave.
-template <int NI>
-__device__ void quant_q8k(const float *xs, int K, const ActL &a) {
-    const int lane = MIO_TIDX & 63, wave = MIO_TIDX >> 6;
-    const int nsb = K >> 8;
-    float v[NI][4], am[NI];
-#pragma unroll
-    for (int j = 0; j < NI; ++j) {
-        const int b = wave + MW * j;
-        float4 v4 = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (b < nsb) v4 = *reinterpret_cast<const float4 *>(xs + b * 256 + 4 * lane);
-        v[j][0] = v4.x, v[j][1] = v4.y, v[j][2] = v4.z, v[j][3] = v4.w;
-    }
-#pragma unroll
-    for (int j = 0; j < NI; ++j) am[j] = abs_max4(v[j]);
-#pragma unroll
-    for (int j = 0; j < NI; ++j) {
-        const int b = wave + MW * j;
-        if (b >= nsb) break;
-        q8k_store(v[j], am[j], b, a);
-    }
-}
-
 // quantize_row_q8_0_ref semantics (d = amax/127 stored as f16, q = roundf(x * 1/d)) of
 // block b held by the 8-lane group of this lane (4 values per lane, lane & 7 = position)
 __device__ __forceinline__ void q80_store(const float (&v)[4], int b, bool ok, const ActL &a) {
@@ -298,32 +273,6 @@ __device__ __forceinline__ void q80_store(const float (&v)[4], int b, bool ok, c
             (q[0] & 0xFF) | ((q[1] & 0xFF) << 8) | ((q[2] & 0xFF) << 16) | ((q[3] & 0xFF) << 24);
         if ((lane & 7) == 0) a.d[b] = f16r(dd);
     }
-}
-
-// 8 blocks per wave and pass, NI passes unrolled
-template <int NI>
-__device__ void quant_q80(const float *xs, int K, const ActL &a) {
-    const int lane = MIO_TIDX & 63, wave = MIO_TIDX >> 6;
-    const int nb = K / 32;
-#pragma unroll
-    for (int j = 0; j < NI; ++j) {
-        const int b = wave * 8 + MW * 8 * j + (lane >> 3);
-        const bool ok = b < nb;
-        float v[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = ok ? xs[b * 32 + 4 * (lane & 7) + i] : 0.0f;
-        q80_store(v, b, ok, a);
-    }
-}
-
-// K <= NI * 2048
-template <int NI>
-__device__ inline void quantize(const float *xs, int K, bool kquant, const ActL &a) {
-    if (kquant)
-        quant_q8k<NI>(xs, K, a);
-    else
-        quant_q80<NI>(xs, K, a);
-    lds_barrier();
 }
 
 // MIO_X_FIRST=1: a matvec launch waits for its activation loads before issuing any weight
@@ -377,16 +326,28 @@ __device__ inline void load_x(const float *x, const float *w, int K, XRegs<XV> &
     }
 }
 
+// Activation kind of a weight type (ggml's vec_dot_type): 0 Q8_0 (Q8_0 weights), 1 Q8_K
+// (Q4_K / Q6_K), 2 BF16 (BF16 weights: the activation rounded to bf16, ggml_fp32_to_bf16).
+__host__ __device__ constexpr int akind(int T) { return T == 30 ? 2 : (T == 8 ? 0 : 1); }
+
+// ggml_compute_fp32_to_bf16: round to nearest even, NaN kept quiet
+__device__ __forceinline__ uint32_t f32_to_bf16(float f) {
+    const uint32_t u = __float_as_uint(f);
+    if ((u & 0x7fffffffu) > 0x7f800000u) return (u >> 16) | 64u;
+    return (u + (0x7fffu + ((u >> 16) & 1u))) >> 16;
+}
+
 // Quantization straight from the registers a prologue loaded: thread t holds elements
-// e = (t + i MT) * 4 .. +3, i.e. wave w lane l holds 256 w + 4 l + 2048 i — exactly superblock
+// e = (t + i*MT) * 4 .. +3, i.e. wave w lane l holds 256 w + 4 l + 2048 i — exactly superblock
 // w + 8 i at lane offset 4 l (quant_q8k's layout) and, for Q8_0, block 8 w + (l >> 3) + 64 i
 // at position 4 (l & 7) (quant_q80's layout). So the LDS staging row and its barrier of the
 // staged quantizer are not needed; the records are the same bits. One barrier at the end
-// makes them visible to every wave.
+// makes them visible to every wave. ak = akind(weight type); BF16 stores the rounded values
+// (2 bytes each) at a.qs + 2e.
 template <int XV>
-__device__ __forceinline__ void quant_regs(const float4 (&v)[XV], int K, bool kquant, const ActL &a) {
+__device__ __forceinline__ void quant_regs(const float4 (&v)[XV], int K, int ak, const ActL &a) {
     const int lane = MIO_TIDX & 63, wave = __builtin_amdgcn_readfirstlane(MIO_TIDX >> 6);
-    if (kquant) {
+    if (ak == 1) {
         const int nsb = K >> 8;
 #pragma unroll
         for (int j = 0; j < XV; ++j) {
@@ -394,6 +355,15 @@ __device__ __forceinline__ void quant_regs(const float4 (&v)[XV], int K, bool kq
             if (b >= nsb) break;
             const float vv[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
             q8k_store(vv, abs_max4(vv), b, a);
+        }
+    } else if (ak == 2) {
+#pragma unroll
+        for (int j = 0; j < XV; ++j) {
+            const int e = (MIO_TIDX + j * MT) * 4;
+            if (e < K)
+                *reinterpret_cast<uint2 *>(a.qs + 2 * e) =
+                    make_uint2(f32_to_bf16(v[j].x) | (f32_to_bf16(v[j].y) << 16),
+                               f32_to_bf16(v[j].z) | (f32_to_bf16(v[j].w) << 16));
         }
     } else {
         const int nb = K / 32;
@@ -415,7 +385,7 @@ __device__ __forceinline__ float rms_scale(double tot, int K, float eps) {
 
 // ggml_rms_norm + mul(weight): xs = (x * 1/sqrtf(mean(x^2) + eps)) * w, then quantize.
 template <int XV>
-__device__ void rmsnorm_quant(const XRegs<XV> &xr, int K, float eps, bool kquant, const Smem &s,
+__device__ void rmsnorm_quant(const XRegs<XV> &xr, int K, float eps, int kquant, const Smem &s,
                               unsigned long long *diag = nullptr) {
     double acc = 0.0;
 #pragma unroll
@@ -465,7 +435,7 @@ __device__ void rmsnorm_quant(const XRegs<XV> &xr, int K, float eps, bool kquant
 }
 
 template <int XV>
-__device__ inline void plain_quant(const XRegs<XV> &xr, int K, bool kquant, const Smem &s,
+__device__ inline void plain_quant(const XRegs<XV> &xr, int K, int kquant, const Smem &s,
                                    unsigned long long *diag = nullptr) {
     MIO_DIAG_STAMP(diag, 5, 0);  // activation arrived
     quant_regs<XV>(xr.v, K, kquant, s.a);
@@ -512,7 +482,7 @@ __device__ inline void conv_load(const float *bcx, const ConvPrev &p1, const Con
 // the conv output (and, when bx_out is set, this token's bx row into it), re-quantized from
 // registers as the out_proj activation
 template <int XV>
-__device__ inline void conv_quant(const ConvRegs<XV> &r, int K, bool kquant, const Smem &s, float *bx_out,
+__device__ inline void conv_quant(const ConvRegs<XV> &r, int K, int kquant, const Smem &s, float *bx_out,
                                   unsigned long long *diag = nullptr) {
     float4 y[XV];
 #pragma unroll
@@ -589,9 +559,12 @@ constexpr uint32_t M4 = 0x0F0F0F0Fu, M2 = 0x03030303u;
 //         4 x 24-bit scale pairs}
 //   Q6_K: a = 16 B of ql, b = 16 B of qh, c = the lane's two int8 sub-block scales, e = d
 //   Q8_0: a, b = the lane's 32 codes, e = d
+//   BF16: a, b, a2, b2 = the lane's 32 weights (bf16 pairs), one contiguous KB per register
+//         over the wave (weights pass*2048 + 512 i + 8 l .. +8 for register i = a, b, a2, b2)
 struct Frag {
     uint4 a, b;
     uint32_t c, e;
+    uint4 a2, b2;
 };
 
 // One unit's activation registers (the lane's 32 int8 values, two bsums, the scale).
@@ -599,6 +572,7 @@ struct ALane {
     int4 lo, hi;
     int b0, b1;
     float d;
+    int4 lo2, hi2;  // BF16: the activations of registers a2, b2
 };
 
 // Lane mapping per pass: K-quants - 8 superblocks x 8 lanes (lane>>3 = superblock,
@@ -666,6 +640,16 @@ __device__ __forceinline__ Frag load_frag(const QMat W, int row, int pass) {
         f.b = bld16<AUX>(W.p1, R * hb, sb * 64 + 32 * (pc >> 2) + 16 * (pc & 1), r * hb);
         f.c = bld2<AUX>(W.p2, R * sbb, sb * 16 + 2 * pc, r * sbb);
         f.e = bld2<AUX>(W.p3, R * db, sb * 2, r * db);
+    } else if constexpr (T == 30) {
+        // element offsets clamped into the row (past K: another valid piece, zeroed in dot_frag)
+        const uint32_t rb = (uint32_t)W.k * 2;
+        auto off = [&](int i) { return (uint32_t)min(pass * 2048 + 512 * i + 8 * lane, W.k - 8) * 2u; };
+        f.a = bld16<AUX>(W.p0, R * rb, off(0), r * rb);
+        f.b = bld16<AUX>(W.p0, R * rb, off(1), r * rb);
+        f.a2 = bld16<AUX>(W.p0, R * rb, off(2), r * rb);
+        f.b2 = bld16<AUX>(W.p0, R * rb, off(3), r * rb);
+        f.c = 0;
+        f.e = 0;
     } else {
         const int nb = W.k >> 5, b = min(pass * 64 + lane, nb - 1);
         const uint32_t qb = (uint32_t)W.k, db = (uint32_t)nb * 2;
@@ -698,6 +682,14 @@ __device__ __forceinline__ ALane load_alane(const ActL &a, int K, int pass) {
         r.b0 = a.bs[e >> 4];
         r.b1 = a.bs[e2 >> 4];
         r.d = a.d[sbc];
+    } else if constexpr (T == 30) {
+        auto at = [&](int i) {
+            const int e = min(pass * 2048 + 512 * i + 8 * lane, K - 8);
+            return *reinterpret_cast<const int4 *>(a.qs + 2 * e);
+        };
+        r.lo = at(0), r.hi = at(1), r.lo2 = at(2), r.hi2 = at(3);
+        r.b0 = r.b1 = 0;
+        r.d = 0.0f;
     } else {
         const int nb = K >> 5, b = pass * 64 + lane, bc = b < nb ? b : 0;
         r.lo = *reinterpret_cast<const int4 *>(a.qs + 32 * bc);
@@ -765,6 +757,27 @@ __device__ __forceinline__ float dot_frag(const Frag &f, const ALane &al, int K,
         const float d = h2f(f.e) * al.d;
         const float v = d * (float)isum;
         return pass * 8 + (lane >> 3) < (K >> 8) ? v : 0.0f;
+    } else if constexpr (T == 30) {
+        // ggml_vec_dot_bf16 on the bf16-rounded activation: products of bf16 pairs are exact
+        // in f32; 8 weights per register, summed by v_dot2 in register order (pieces past K
+        // zeroed on both sides)
+        typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
+        float acc = 0.0f;
+        auto dot8 = [&](const uint4 &w, const int4 &x, int i) {
+            const bool ok = pass * 2048 + 512 * i + 8 * lane < K;
+            const uint4 ww = ok ? w : make_uint4(0, 0, 0, 0);
+            const uint4 xx = ok ? make_uint4((uint32_t)x.x, (uint32_t)x.y, (uint32_t)x.z, (uint32_t)x.w)
+                                : make_uint4(0, 0, 0, 0);
+            acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf2, ww.x), __builtin_bit_cast(bf2, xx.x), acc, false);
+            acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf2, ww.y), __builtin_bit_cast(bf2, xx.y), acc, false);
+            acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf2, ww.z), __builtin_bit_cast(bf2, xx.z), acc, false);
+            acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf2, ww.w), __builtin_bit_cast(bf2, xx.w), acc, false);
+        };
+        dot8(f.a, al.lo, 0);
+        dot8(f.b, al.hi, 1);
+        dot8(f.a2, al.lo2, 2);
+        dot8(f.b2, al.hi2, 3);
+        return acc;
     } else {
         int s = 0;
         s = sdot4((int)f.a.x, al.lo.x, s);
@@ -783,7 +796,7 @@ __device__ __forceinline__ float dot_frag(const Frag &f, const ALane &al, int K,
 // Row total of the per-lane partials (accumulated over the row's passes), wave-uniform.
 template <int T>
 __device__ __forceinline__ float row_total(float acc) {
-    if constexpr (T == 8) acc = sum8_f(acc);
+    if constexpr (T == 8 || T == 30) acc = sum8_f(acc);
     return sum_lanes7(acc);
 }
 
@@ -942,6 +955,9 @@ __device__ float dequant_elem(const QMat &W, int row, int e) {
         const int sc = ((const int8_t *)W.p2)[(size_t)row * (W.k / 16) + sb * 16 + 2 * (4 * sn + (sw & 3)) + (sw >> 2)];
         const float dd = h2f(((const uint16_t *)W.p3)[(size_t)row * nsb + sb]);
         return dd * (float)sc * (float)q;
+    } else if (W.type == 30) {
+        const uint16_t h = ((const uint16_t *)W.p0)[(size_t)row * W.k + e];
+        return __uint_as_float((uint32_t)h << 16);
     } else {
         const int nb = W.k >> 5;
         const int8_t q = ((const int8_t *)W.p0)[(size_t)row * W.k + e];
@@ -1060,14 +1076,18 @@ __device__ inline void embed_regs(const QMat &emb, int tok, int K, XRegs<XV> &xr
     }
 }
 
-// Calls f.template operator()<NP, T>() for the matrix's pass count and weight type.
-template <class F>
+// Calls f.template operator()<NP, T>() for the matrix's pass count and weight type. BF = false:
+// the int8 types only (the multi-token engine: BF16 models prefill token by token).
+template <bool BF = true, class F>
 void dispatch_nt(int K, int type, F &&f) {
     const int np = pick_np(K);
 #define NT_CASE(NPV, TV) \
     if (np == NPV && type == TV) return f.template operator()<NPV, TV>();
     NT_CASE(1, 8) NT_CASE(1, 12) NT_CASE(1, 14) NT_CASE(3, 8) NT_CASE(3, 12) NT_CASE(3, 14)
     NT_CASE(6, 8) NT_CASE(6, 12) NT_CASE(6, 14)
+    if constexpr (BF) {
+        NT_CASE(1, 30) NT_CASE(3, 30) NT_CASE(6, 30)
+    }
 #undef NT_CASE
 }
 

@@ -73,7 +73,7 @@ __global__ __launch_bounds__(MT) void k_attn_out(LlmDims d, QMat wo, LlmBuffers 
     x_after_weights(xr);
     MIO_TRACE(b, 1);
     MIO_TL_MARK1(b);
-    plain_quant(xr, K, T != 8, s, MIO_TL_DIAGSLOT(b));
+    plain_quant(xr, K, akind(T), s, MIO_TL_DIAGSLOT(b));
     MIO_TRACE(b, 2);
     MIO_TL_MARK(b, 2);
     stream_rows<T, NP, 1, SU, MIO_SMALL_AUX>(wo, wo, lo, hi, ga, gb, s.a, [&](int row, float v, float) {
@@ -111,7 +111,7 @@ __global__ __launch_bounds__(MT) void k_conv_out(LlmDims d, QMat wo, const float
     conv_after_weights(cr);
     MIO_TRACE(b, 1);
     MIO_TL_MARK1(b);
-    conv_quant(cr, K, T != 8, s, blockIdx.x == 0 ? ring + (size_t)(pos & (kConvSlots - 1)) * K : nullptr,
+    conv_quant(cr, K, akind(T), s, blockIdx.x == 0 ? ring + (size_t)(pos & (kConvSlots - 1)) * K : nullptr,
                MIO_TL_DIAGSLOT(b));
     MIO_TRACE(b, 2);
     MIO_TL_MARK(b, 2);
@@ -143,7 +143,7 @@ __global__ __launch_bounds__(MT) void k_ffn_in(LlmDims d, const float *norm_w, Q
     x_after_weights(xr);
     MIO_TRACE(b, 1);
     MIO_TL_MARK1(b);
-    rmsnorm_quant(xr, K, d.eps, T != 8, s, MIO_TL_DIAGSLOT(b));
+    rmsnorm_quant(xr, K, d.eps, akind(T), s, MIO_TL_DIAGSLOT(b));
     MIO_TRACE(b, 2);
     MIO_TL_MARK(b, 2);
     stream_rows<T, NP, 2, SU>(gate, up, lo, hi, ga, gb, s.a, [&](int row, float g, float u) {
@@ -179,7 +179,7 @@ __global__ __launch_bounds__(MT) void k_ffn_down(LlmDims d, QMat down, LlmBuffer
     x_after_weights(xr);
     MIO_TRACE(b, 1);
     MIO_TL_MARK1(b);
-    plain_quant(xr, K, T != 8, s, MIO_TL_DIAGSLOT(b));
+    plain_quant(xr, K, akind(T), s, MIO_TL_DIAGSLOT(b));
     MIO_TRACE(b, 2);
     MIO_TL_MARK(b, 2);
     stream_rows<T, NP, 1, SU>(down, down, lo, hi, ga, gb, s.a, [&](int row, float v, float) {
@@ -218,7 +218,7 @@ __global__ __launch_bounds__(MT) void k_lm_head(LlmDims d, const float *norm_w, 
     const int step = b.st->step;
     MIO_TRACE(b, 1);
     MIO_TL_MARK1(b);
-    rmsnorm_quant(xr, K, d.eps, T != 8, s, MIO_TL_DIAGSLOT(b));
+    rmsnorm_quant(xr, K, d.eps, akind(T), s, MIO_TL_DIAGSLOT(b));
     MIO_TRACE(b, 2);
     MIO_TL_MARK(b, 2);
     const int lane = threadIdx.x & 63;
@@ -570,7 +570,7 @@ __global__ __launch_bounds__(MT) void k_debug_matvec(QMat W, const float *x, flo
     wave_range(W.rows, lo, hi, blockIdx.x, gridDim.x);
     Frag ga[Cfg<NP>::U], gb[Cfg<NP>::U];
     load_first<T, NP, 1>(W, W, lo, hi, ga, gb);
-    plain_quant(xr, K, T != 8, s);
+    plain_quant(xr, K, akind(T), s);
     stream_rows<T, NP, 1>(W, W, lo, hi, ga, gb, s.a, [&](int row, float v, float) {
         if ((threadIdx.x & 63) == 0) y[row] = v;
     });

@@ -48,7 +48,6 @@ __host__ __device__ inline size_t pf_lds_bytes(int K, int nt, int rpw) {
 
 __device__ inline Smem carve_t(char *base, int K, int t) {
     Smem s;
-    s.xs = nullptr;
     s.red = nullptr;
     char *a = base + act_base(K) + act_bytes(K) * t;
     s.a.qs = (int8_t *)a;
@@ -1140,7 +1139,7 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
                 attn_in_grid(d, L, GW, g_qk);
                 over_tokens(d.n_embd, 0, [&](int, int n, const PrefillBuffers &q) {
                     const size_t lds = pf_lds_bytes(d.n_embd, n, 0);
-                    dispatch_nt(d.n_embd, L.wq.type, [&]<int NP, int TQ>() {
+                    dispatch_nt<false>(d.n_embd, L.wq.type, [&]<int NP, int TQ>() {
                         auto go = [&]<int TV>() {
                             if constexpr (NP == 1) {
                                 if (fa) {
@@ -1196,7 +1195,7 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
                 const LlmDims dw = bt_wgm(d, L.wo.k);
                 const int grid = matvec_grid(dw, L.wo.rows), rpw = rows_per_wave(L.wo.rows, grid);
                 over_tokens(L.wo.k, rpw, [&](int, int n, const PrefillBuffers &q) {
-                    dispatch_nt(L.wo.k, L.wo.type, [&]<int NP, int T>() {
+                    dispatch_nt<false>(L.wo.k, L.wo.type, [&]<int NP, int T>() {
                         allow_lds(k_pf_attn_out<NP, T>);
                         hipLaunchKernelGGL((k_pf_attn_out<NP, T>), dim3(grid), dim3(MT), pf_lds_bytes(L.wo.k, n, rpw), s,
                                            dw, L.wo, q, n, rpw);
@@ -1215,7 +1214,7 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
             const LlmDims dw = bt_wgm(d, d.n_embd);
             const int grid = matvec_grid(dw, L.gate.rows);
             over_tokens(d.n_embd, 0, [&](int, int n, const PrefillBuffers &q) {
-                dispatch_nt(d.n_embd, L.gate.type, [&]<int NP, int T>() {
+                dispatch_nt<false>(d.n_embd, L.gate.type, [&]<int NP, int T>() {
                     if constexpr (NP == 1) {
                         if (ff) {
                             allow_lds(k_pf_ffn_in<NP, T, 2>);
@@ -1238,7 +1237,7 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
         } else {
             const int grid = matvec_grid(d, L.down.rows), rpw = rows_per_wave(L.down.rows, grid);
             over_tokens(L.down.k, rpw, [&](int, int n, const PrefillBuffers &q) {
-                dispatch_nt(L.down.k, L.down.type, [&]<int NP, int T>() {
+                dispatch_nt<false>(L.down.k, L.down.type, [&]<int NP, int T>() {
                     allow_lds(k_pf_ffn_down<NP, T>);
                     hipLaunchKernelGGL((k_pf_ffn_down<NP, T>), dim3(grid), dim3(MT), pf_lds_bytes(L.down.k, n, rpw),
                                        s, d, L.down, q, n, rpw);
@@ -1285,7 +1284,7 @@ void launch_batch_step(const LlmDims &d, const LayerW *layers, int n_layer, _Flo
     launch_layers(d, layers, n_layer, kcache, vcache, pb, B, d.max_splits, true, s);
     launch_quant(d, 0, pb.x, d.n_embd, out_norm, lm.type != 8, pb, B, s);
     const int nblk = matvec_grid(d, d.n_vocab);  // the batched lm_head keeps one workgroup per CU
-    dispatch_nt(d.n_embd, lm.type, [&]<int NP, int T>() {
+    dispatch_nt<false>(d.n_embd, lm.type, [&]<int NP, int T>() {
         allow_lds(k_bt_lm_head<NP, T>);
         hipLaunchKernelGGL((k_bt_lm_head<NP, T>), dim3(nblk), dim3(MT), batch_lm_head_lds(d, B), s, d, out_norm, lm,
                            pb, bb, B);

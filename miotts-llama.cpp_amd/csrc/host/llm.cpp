@@ -51,6 +51,9 @@ struct mio_hip_llm {
     int max_steps = 0;
     std::vector<void *> allocs;
     uint64_t weight_bytes = 0;
+    // some matrix is BF16: the multi-token engine (int8 records) does not take it, so the
+    // prompt is prefilled as forced decode steps and batched decode is refused
+    bool bf16 = false;
     // all quantized matrices live in one arena, in the order a step streams them
     uint8_t *arena = nullptr;
     std::map<std::string, size_t> arena_off;
@@ -172,9 +175,15 @@ bool upload_qmat(mio_hip_llm *m, const mio::GgufTensor *t, mio::QMat &q) {
         return false;
     }
     const bool repack = mio::repacks_to_q8_0(t->type);
-    if (t->type != mio::GGML_Q8_0 && t->type != mio::GGML_Q4_K && t->type != mio::GGML_Q6_K && !repack) {
-        mio::set_error("llm: tensor %s has type %s; supported: q8_0, q4_K, q6_K, q5_0 / q4_0 (run as q8_0)",
+    if (t->type != mio::GGML_Q8_0 && t->type != mio::GGML_Q4_K && t->type != mio::GGML_Q6_K &&
+        t->type != mio::GGML_BF16 && !repack) {
+        mio::set_error("llm: tensor %s has type %s; supported: bf16, q8_0, q4_K, q6_K, q5_0 / q4_0 (run as q8_0)",
                        t->name.c_str(), mio::ggml_type_name(t->type));
+        return false;
+    }
+    if (t->type == mio::GGML_BF16 && t->ne[0] % 32) {
+        mio::set_error("llm: bf16 tensor %s: row length %lld is not a multiple of 32", t->name.c_str(),
+                       (long long)t->ne[0]);
         return false;
     }
     // Q5_0 (llama-quantize's Q4_K fallback for rows not a multiple of 256) and Q4_0 rows run as
@@ -207,6 +216,7 @@ bool upload_qmat(mio_hip_llm *m, const mio::GgufTensor *t, mio::QMat &q) {
         return false;
     }
     q.type = (int)type;
+    if (type == mio::GGML_BF16) m->bf16 = true;
     q.rows = (int)t->ne[1];
     q.k = (int)t->ne[0];
     q.p0 = dp + L.off[0];
@@ -317,7 +327,10 @@ int put_cfg(mio_hip_llm *m, mio::SampleCfg c) {
     return MIO_OK;
 }
 
+int reset_tickets(mio_hip_llm *m);
+
 int set_state(mio_hip_llm *m, int pos, int token, int step = 0) {
+    if (int rc = reset_tickets(m)) return rc;
     mio::StepState st{pos, step, token, 0};
     MIO_HIP_CHECK(hipMemcpyAsync(m->buf.st, &st, sizeof(st), hipMemcpyHostToDevice, m->d->stream));
     mio::launch_embed_token(m->dims, m->tok, m->buf, m->d->stream);
@@ -380,12 +393,17 @@ int prefill(mio_hip_llm *m, int n) {
     return MIO_OK;
 }
 
-// Every prompt upload starts a new prefill / generation: the attention chunk tickets are
-// zeroed in stream order first (the last chunk workgroup of every attention launch resets its
-// ticket, so they are 0 here anyway; this keeps an interrupted run from carrying a count over).
-int upload_prompt(mio_hip_llm *m, const int32_t *prompt, int n) {
+// The attention chunk tickets (attn_merge_last) are zeroed in stream order before every
+// prefill and every decode start (the last chunk workgroup of each attention launch resets
+// its ticket, so they are 0 here anyway; this keeps an interrupted run from carrying a count).
+int reset_tickets(mio_hip_llm *m) {
     MIO_HIP_CHECK(hipMemsetAsync(m->buf.att_cnt, 0, (size_t)m->dims.n_kv * sizeof(int), m->d->stream));
     MIO_HIP_CHECK(hipMemsetAsync(m->pf.att_cnt, 0, (size_t)mio::kPrefillB * m->dims.n_kv * sizeof(int), m->d->stream));
+    return MIO_OK;
+}
+
+int upload_prompt(mio_hip_llm *m, const int32_t *prompt, int n) {
+    if (int rc = reset_tickets(m)) return rc;
     MIO_HIP_CHECK(hipMemcpyAsync(m->d_prompt, prompt, (size_t)n * 4, hipMemcpyHostToDevice, m->d->stream));
     return MIO_OK;
 }
@@ -466,7 +484,7 @@ int llm_begin(mio_hip_llm *m, const int32_t *prompt, int n_prompt, int max_new, 
     // kPrefillB tokens), or, with MIO_SEQ_PREFILL=1, as P forced decode steps; decoding
     // then starts at position P with the step counter at P either way (same sampler stream)
     const int P = n_prompt - 1;
-    if (sequential_prefill()) {
+    if (sequential_prefill() || m->bf16) {
         m->steps_issued = 0;
         if ((rc = set_state(m, 0, prompt[0]))) return rc;
         return llm_run(m, P);
@@ -660,7 +678,7 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
     if (!(m->out_norm = upload_f32(m, g, lfm2 ? "token_embd_norm.weight" : "output_norm.weight", D.n_embd)))
         return fail(MIO_ERR_FORMAT);
     bool any_conv = false;
-    auto fam = [](int t) { return t == mio::GGML_Q8_0 ? 0 : 1; };
+    auto fam = [](int t) { return t == mio::GGML_Q8_0 ? 0 : (t == mio::GGML_BF16 ? 2 : 1); };
     for (int i = 0; i < m->n_layer; ++i) {
         const std::string p = "blk." + std::to_string(i) + ".";
         mio::LayerW L{};
@@ -1121,6 +1139,8 @@ extern "C" int mio_hip_llm_generate_batch(mio_hip_llm *m, const int32_t *prompts
                 "llm_generate_batch: bad args");
     MIO_REQUIRE(mio::batch_supported(m->dims, B), MIO_ERR_UNSUPPORTED,
                 "llm_generate_batch: %d streams not supported (1..%d, lm_head LDS)", B, mio::kBatchMax);
+    MIO_REQUIRE(!m->bf16, MIO_ERR_UNSUPPORTED,
+                "llm_generate_batch: BF16 weights run on the single-stream decode only (mio_hip_llm_generate)");
     const mio::LlmDims &D = m->dims;
     std::vector<int> off(B + 1, 0);
     for (int b = 0; b < B; ++b) {
@@ -1220,7 +1240,12 @@ extern "C" int mio_hip_llm_prefill(mio_hip_llm *m, const int32_t *tokens, int n_
                     tokens[i]);
     int rc = mio::bind(m->d);
     if (rc) return rc;
-    if ((rc = upload_prompt(m, tokens, n_tokens)) || (rc = prefill(m, n_tokens - 1))) return rc;
+    if (m->bf16) {  // forced decode steps (the multi-token engine is int8-only)
+        for (int i = 0; i + 1 < n_tokens; ++i)
+            if ((rc = mio_hip_llm_eval(m, tokens[i], i, nullptr))) return rc;
+    } else if ((rc = upload_prompt(m, tokens, n_tokens)) || (rc = prefill(m, n_tokens - 1))) {
+        return rc;
+    }
     return mio_hip_llm_eval(m, tokens[n_tokens - 1], n_tokens - 1, logits);
 }
 

@@ -15,6 +15,14 @@ float fp16_to_f32(uint16_t h) {
     return (float)v;
 }
 
+// ggml_compute_fp32_to_bf16: round to nearest even, NaN kept quiet
+uint16_t f32_to_bf16(float f) {
+    uint32_t u;
+    std::memcpy(&u, &f, 4);
+    if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 64u);
+    return (uint16_t)((u + (0x7fffu + ((u >> 16) & 1u))) >> 16);
+}
+
 uint16_t f32_to_fp16(float f) {
     _Float16 v = (_Float16)f;
     uint16_t h;
@@ -224,6 +232,9 @@ bool quantize_row(uint32_t type, const float *x, void *y, int64_t k) {
         case GGML_F16:
             for (int64_t i = 0; i < k; ++i) ((uint16_t *)y)[i] = f32_to_fp16(x[i]);
             return true;
+        case GGML_BF16:
+            for (int64_t i = 0; i < k; ++i) ((uint16_t *)y)[i] = f32_to_bf16(x[i]);
+            return true;
         case GGML_Q8_0: quantize_row_q8_0(x, y, k); return true;
         case GGML_Q4_0: quantize_row_q4_0(x, y, k); return true;
         case GGML_Q5_0: quantize_row_q5_0(x, y, k); return true;
@@ -248,6 +259,12 @@ bool dequantize_row(uint32_t type, const void *vx, float *y, int64_t k) {
             }
             return true;
         }
+        case GGML_BF16:
+            for (int64_t i = 0; i < k; ++i) {
+                const uint32_t u = (uint32_t)((const uint16_t *)vx)[i] << 16;
+                std::memcpy(&y[i], &u, 4);
+            }
+            return true;
         case GGML_Q4_0:
         case GGML_Q5_0: {
             const size_t bb = type == GGML_Q4_0 ? sizeof(BlockQ4_0) : sizeof(BlockQ5_0);
@@ -338,7 +355,8 @@ SplitLayout split_layout(uint32_t type, int64_t R, int64_t K) {
                 take(3, (size_t)R * (K / 256) * 2);
             break;
         case GGML_F32: take(0, (size_t)R * K * 4); break;
-        case GGML_F16: take(0, (size_t)R * K * 2); break;
+        case GGML_F16:
+        case GGML_BF16: take(0, (size_t)R * K * 2); break;
         default: return L;
     }
     L.bytes = o;
@@ -348,7 +366,7 @@ SplitLayout split_layout(uint32_t type, int64_t R, int64_t K) {
 bool to_split(uint32_t type, const void *src, int64_t R, int64_t K, uint8_t *dst) {
     const SplitLayout L = split_layout(type, R, K);
     if (!L.bytes) return false;
-    if (type == GGML_F32 || type == GGML_F16) {
+    if (type == GGML_F32 || type == GGML_F16 || type == GGML_BF16) {
         std::memcpy(dst, src, (size_t)R * K * (type == GGML_F32 ? 4 : 2));
         return true;
     }

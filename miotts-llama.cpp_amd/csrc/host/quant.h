@@ -53,6 +53,7 @@ static_assert(sizeof(BlockQ6_K) == 210, "q6_K");
 
 float fp16_to_f32(uint16_t h);
 uint16_t f32_to_fp16(float f);  // round to nearest even
+uint16_t f32_to_bf16(float f);  // ggml_compute_fp32_to_bf16
 
 void quantize_row_q8_0(const float *x, void *y, int64_t k);
 void quantize_row_q4_0(const float *x, void *y, int64_t k);

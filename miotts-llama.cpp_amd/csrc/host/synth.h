@@ -33,7 +33,7 @@ struct SynthLlmCfg {
     int n_embd = 256, n_layer = 2, n_head = 4, n_head_kv = 2, head_dim = 64, n_ff = 512;
     int n_vocab = 13312, n_ctx = 4096;
     float rope_base = 10000.f, rms_eps = 1e-6f, w_std = 0.02f;
-    int qtype = 8;   // 8 = all Q8_0; 15 = Q4_K_M mix (Q4_K + Q6_K); 2 = Q4_0 (+ Q6_K output)
+    int qtype = 8;   // 8 = all Q8_0; 15 = Q4_K_M mix (Q4_K + Q6_K); 2 = Q4_0; 30 = all BF16
     // llama-quantize's fallback for rows whose length is not a multiple of 256: Q4_K -> Q5_0,
     // Q6_K -> Q8_0 (llama-quant.cpp); Q4_K_M files of the 0.1B model (n_embd 576) carry them
     bool kq_fallback = true;
@@ -48,7 +48,8 @@ struct SynthLlmCfg {
 //         5 tiny Q8_0 qwen2 with q/k/v projection biases, 6 "2.6B" Q8_0 as lfm2 (the LFM2-2.6B
 //         width, FFN, vocab and GQA; short-conv / attention layer hybrid), 7 tiny Q8_0 lfm2,
 //         8 tiny Q4_K_M lfm2, 9 tiny Q4_K_M at the 0.1B width (n_embd 576: q/k/v, O, gate/up and
-//         the embedding fall back to Q5_0 / Q8_0 as llama-quantize does), 10 tiny Q4_0
+//         the embedding fall back to Q5_0 / Q8_0 as llama-quantize does), 10 tiny Q4_0,
+//         11 tiny BF16 (qwen3), 12 "1.7B" BF16
 SynthLlmCfg synth_llm_preset(int preset);
 bool synth_write_llm(const std::string &path, const SynthLlmCfg &cfg);
 // Token ids of the synthetic vocabulary.

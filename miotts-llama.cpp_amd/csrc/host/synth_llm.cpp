@@ -71,6 +71,14 @@ SynthLlmCfg synth_llm_preset(int p) {
         case 10:
             c.name = "tiny-q4_0", c.qtype = 2;
             break;
+        case 11:
+            c.name = "tiny-bf16", c.arch = "qwen3", c.n_layer = 3, c.n_ff = 768, c.qtype = 30;
+            c.rope_base = 1000000.f;
+            break;
+        case 12:  // the 1.7B shape as the published BF16 file (README.md:196)
+            c = synth_llm_preset(3);
+            c.name = "MioTTS-1.7B-bf16-synthetic", c.qtype = 30;
+            break;
         default: break;
     }
     return c;
@@ -110,7 +118,8 @@ bool synth_write_llm(const std::string &path, const SynthLlmCfg &c) {
     const bool lfm2 = a == "lfm2";
     w.kv_str("general.architecture", a);
     w.kv_str("general.name", c.name);
-    w.kv_u32("general.file_type", c.qtype == 15 ? 15 : (c.qtype == 2 ? 2 : 7));
+    // llama_ftype: 7 MOSTLY_Q8_0, 15 MOSTLY_Q4_K_M, 2 MOSTLY_Q4_0, 32 MOSTLY_BF16
+    w.kv_u32("general.file_type", c.qtype == 15 ? 15 : (c.qtype == 2 ? 2 : (c.qtype == 30 ? 32 : 7)));
     w.kv_u32(a + ".context_length", c.n_ctx);
     w.kv_u32(a + ".embedding_length", c.n_embd);
     w.kv_u32(a + ".block_count", c.n_layer);
@@ -154,10 +163,12 @@ bool synth_write_llm(const std::string &path, const SynthLlmCfg &c) {
         int fill;  // 0 quantized N(0, w_std) rows, 1 ones, 2 f32 N(0, 0.5) (biases / conv taps)
     };
     std::vector<T> ts;
-    const uint32_t base = c.qtype == 15 ? GGML_Q4_K : (c.qtype == 2 ? GGML_Q4_0 : GGML_Q8_0);
-    const uint32_t more = c.qtype == 15 ? GGML_Q6_K : (c.qtype == 2 ? GGML_Q4_0 : GGML_Q8_0);
+    auto pick = [&](uint32_t k_mix, uint32_t q4) -> uint32_t {
+        return c.qtype == 15 ? k_mix : (c.qtype == 2 ? q4 : (c.qtype == 30 ? (uint32_t)GGML_BF16 : GGML_Q8_0));
+    };
+    const uint32_t base = pick(GGML_Q4_K, GGML_Q4_0), more = pick(GGML_Q6_K, GGML_Q4_0);
     const int q_dim = c.n_head * c.head_dim, kv_dim = c.n_head_kv * c.head_dim;
-    const uint32_t emb = c.qtype == 15 ? GGML_Q6_K : (c.qtype == 2 ? GGML_Q4_0 : GGML_Q8_0);
+    const uint32_t emb = pick(GGML_Q6_K, GGML_Q4_0);
     ts.push_back({"token_embd.weight", emb, c.n_embd, c.n_vocab, false});
     for (int i = 0; i < c.n_layer; ++i) {
         const std::string p = "blk." + std::to_string(i) + ".";

@@ -541,7 +541,7 @@ class Llm:
         return [out[b, : n[b]].copy() for b in range(B)]
 
 
-GGML_BLOCK = {2: (32, 18), 6: (32, 22), 8: (32, 34), 12: (256, 144), 14: (256, 210)}
+GGML_BLOCK = {2: (32, 18), 6: (32, 22), 8: (32, 34), 12: (256, 144), 14: (256, 210), 30: (1, 2)}
 
 
 def quantize_rows(qtype: int, x: np.ndarray) -> np.ndarray:

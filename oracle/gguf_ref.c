@@ -57,6 +57,7 @@ size_t mo_type_size(uint32_t type, int64_t n) {
         case 0: return 4 * n;           /* f32 */
         case 1: return 2 * n;           /* f16 */
         case 26: return 4 * n;          /* i32 */
+        case 30: return n * 2;          /* bf16 */
         case 2: return n / 32 * 18;     /* q4_0 */
         case 6: return n / 32 * 22;     /* q5_0 */
         case 8: return n / 32 * 34;     /* q8_0 */

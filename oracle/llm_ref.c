@@ -37,6 +37,8 @@ void mo_quantize_q8_0(const float *x, int64_t k, uint16_t *d, int8_t *qs);
 void mo_quantize_q8_K(const float *x, int64_t k, float *d, int8_t *qs, int16_t *bsums);
 float mo_vec_dot_q8_0(const uint8_t *row, int64_t k, const uint16_t *ad, const int8_t *aq);
 float mo_vec_dot_q45_0(uint32_t type, const uint8_t *row, int64_t k, const uint16_t *ad, const int8_t *aq);
+float mo_vec_dot_bf16(const uint8_t *row, int64_t k, const uint16_t *xb);
+uint16_t mo_f32_to_bf16(float f);
 float mo_vec_dot_q4_K(const uint8_t *row, int64_t k, const float *ad, const int8_t *aq, const int16_t *bsums);
 float mo_vec_dot_q6_K(const uint8_t *row, int64_t k, const float *ad, const int8_t *aq);
 int mo_dequantize_row(uint32_t type, const uint8_t *row, int64_t k, float *y);
@@ -192,6 +194,12 @@ static void matvec(mo_llm *m, const mo_tensor *W, const float *x, float *y) {
         mo_quantize_q8_0(x, K, m->q80d, m->q8qs);
 #pragma omp parallel for schedule(static)
         for (int64_t r = 0; r < R; r++) y[r] = mo_vec_dot_q8_0(W->data + r * rb, K, m->q80d, m->q8qs);
+    } else if (W->type == 30) {  /* BF16: vec_dot_type BF16 */
+        uint16_t *xh = (uint16_t *)malloc(sizeof(uint16_t) * K);
+        for (int64_t i = 0; i < K; i++) xh[i] = mo_f32_to_bf16(x[i]);
+#pragma omp parallel for schedule(static)
+        for (int64_t r = 0; r < R; r++) y[r] = mo_vec_dot_bf16(W->data + r * rb, K, xh);
+        free(xh);
     } else if (W->type == 2 || W->type == 6) {  /* Q4_0 / Q5_0: vec_dot_type Q8_0 */
         mo_quantize_q8_0(x, K, m->q80d, m->q8qs);
 #pragma omp parallel for schedule(static)

@@ -11,6 +11,9 @@
  *       Q4_K / Q6_K  -> Q8_K activations (quantize_row_q8_K_ref: iscale = -127/max_signed,
  *                       q = min(127, nearest_int(iscale*x)), d = 1/iscale f32, bsums/16)
  *   - vec_dot_q8_0_q8_0 : sum_b (float)isum_b * (dw_b * da_b)
+ *   - vec_dot_bf16 (vec_dot_type BF16): the activation rounded to bf16
+ *       (ggml_compute_fp32_to_bf16, nearest even), sum_i of the f32 products w_i * x_i
+ *       accumulated in double (ggml_float) in element order
  *   - vec_dot_q4_0_q8_0 / vec_dot_q5_0_q8_0 (vec_dot_type Q8_0): per block
  *       (dw_b * da_b) * (isum over the low 16 codes + isum over the high 16), codes
  *       (nibble - 8) / (nibble | fifth bit from qh) - 16
@@ -149,6 +152,31 @@ float mo_vec_dot_q45_0(uint32_t type, const uint8_t *row, int64_t k, const uint1
     return sumf;
 }
 
+/* ggml_compute_fp32_to_bf16 / GGML_BF16_TO_FP32 */
+uint16_t mo_f32_to_bf16(float f) {
+    uint32_t u;
+    memcpy(&u, &f, 4);
+    if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 64u);
+    return (uint16_t)((u + (0x7fffu + ((u >> 16) & 1u))) >> 16);
+}
+static float bf16_to_f32(uint16_t h) {
+    const uint32_t u = (uint32_t)h << 16;
+    float f;
+    memcpy(&f, &u, 4);
+    return f;
+}
+
+/* vec_dot_bf16 over a bf16 weight row and the bf16-rounded activation xb */
+float mo_vec_dot_bf16(const uint8_t *row, int64_t k, const uint16_t *xb) {
+    double sumf = 0;
+    for (int64_t i = 0; i < k; i++) {
+        uint16_t w;
+        memcpy(&w, row + 2 * i, 2);
+        sumf += (double)(bf16_to_f32(w) * bf16_to_f32(xb[i]));
+    }
+    return (float)sumf;
+}
+
 /* row dot products; x = one weight row in GGUF block layout */
 float mo_vec_dot_q8_0(const uint8_t *row, int64_t k, const uint16_t *ad, const int8_t *aq) {
     float sumf = 0;
@@ -266,6 +294,12 @@ int mo_dequantize_row(uint32_t type, const uint8_t *row, int64_t k, float *y) {
             const int8_t *q = (const int8_t *)(row + 34 * b + 2);
             for (int j = 0; j < 32; j++) y[b * 32 + j] = q[j] * d;
         }
+    } else if (type == 30) {
+        for (int64_t i = 0; i < k; i++) {
+            uint16_t h;
+            memcpy(&h, row + 2 * i, 2);
+            y[i] = bf16_to_f32(h);
+        }
     } else if (type == 2 || type == 6) {
         const int bb = type == 2 ? 18 : 22;
         for (int64_t b = 0; b < k / 32; b++) {
@@ -343,6 +377,12 @@ int mo_matvec(uint32_t type, const uint8_t *w, int rows, int64_t k, const float 
         rb = (size_t)k / 32 * 34;
         mo_quantize_q8_0(x, k, d0, qs);
         for (int r = 0; r < rows; r++) y[r] = mo_vec_dot_q8_0(w + r * rb, k, d0, qs);
+    } else if (type == 30) {
+        rb = (size_t)k * 2;
+        uint16_t *xb = (uint16_t *)malloc(sizeof(uint16_t) * k);
+        for (int64_t i = 0; i < k; i++) xb[i] = mo_f32_to_bf16(x[i]);
+        for (int r = 0; r < rows; r++) y[r] = mo_vec_dot_bf16(w + r * rb, k, xb);
+        free(xb);
     } else if (type == 2 || type == 6) {
         rb = (size_t)k / 32 * (type == 2 ? 18 : 22);
         mo_quantize_q8_0(x, k, d0, qs);

@@ -73,6 +73,15 @@ def test_batch_stops_at_eos(device, llm_files):
         assert len(got[b]) < 200 and (got[b] != m.SYNTH_EOT).all()
 
 
+def test_batch_refuses_bf16(device, tmp_path):
+    """BF16 weights run on the single-stream decode only; the batched engine (int8 records)
+    refuses them with a message instead of computing with the wrong activation type."""
+    g = m.Llm(device, m.synth_llm(str(tmp_path / "bf16.gguf"), 11, 1), 256)
+    with pytest.raises(Exception, match="BF16"):
+        g.generate_batch([[256, 257, 65]] * 2, 4, 0.8, seeds=[1, 2])
+    assert len(g.generate([256, 257, 65], 4, 0.8, 1)) == 4
+
+
 def test_batch_rejects_bad_shapes(device, llm_files):
     g = m.Llm(device, llm_files[0], 64)
     with pytest.raises(m.HipError):

@@ -1,7 +1,8 @@
 """GPU parity: HIP LLM decode step (csrc/hip/llm_kernels.hip) vs the oracle.
 
 1. Single matvec per quant type (Q8_0 / Q4_K / Q6_K, and Q5_0 / Q4_0, which run as the Q8_0
-   rows they equal exactly) on random data: the GPU's per-
+   rows they equal exactly; BF16 within the same bound, its f32 sums reordered) on random
+   data: the GPU's per-
    superblock integer sums are exact, only the float sum over superblocks is reordered:
    |y_gpu - y_ref| <= 1e-5 * sum_b |partial_b| (bounded here by 2e-5 * max|y| + 1e-6).
 2. Teacher-forced logits: tiny models over 80 positions, the 1.7B model over 300 positions
@@ -32,11 +33,11 @@ pytestmark = pytest.mark.gpu
 @pytest.fixture(scope="module")
 def llm_files(tmp_path_factory):
     d = tmp_path_factory.mktemp("llm_gpu")
-    return {p: m.synth_llm(str(d / f"llm{p}.gguf"), p, 1) for p in (0, 1, 9, 10)}
+    return {p: m.synth_llm(str(d / f"llm{p}.gguf"), p, 1) for p in (0, 1, 9, 10, 11)}
 
 
 @pytest.mark.parametrize("qtype,k", [(8, 576), (8, 2048), (12, 2048), (12, 6144), (14, 2048), (14, 768),
-                                     (6, 576), (6, 2048), (2, 2048)])
+                                     (6, 576), (6, 2048), (2, 2048), (30, 576), (30, 2048), (30, 6144)])
 def test_matvec_exact_per_type(device, qtype, k):
     rng = np.random.default_rng(qtype * 1000 + k)
     rows = 37
@@ -54,8 +55,9 @@ def test_matvec_exact_per_type(device, qtype, k):
 
 
 # 9: Q4_K_M at the 0.1B width, whose q/k/v, O, gate/up and embedding rows (576 long) are
-# llama-quantize's Q5_0 / Q8_0 fallbacks; 10: Q4_0 (Q5_0 and Q4_0 run as the equal Q8_0 rows)
-@pytest.mark.parametrize("preset", [0, 1, 9, 10])
+# llama-quantize's Q5_0 / Q8_0 fallbacks; 10: Q4_0 (Q5_0 and Q4_0 run as the equal Q8_0 rows);
+# 11: BF16 (v_dot2 over the bf16-rounded activation, ggml's vec_dot_bf16)
+@pytest.mark.parametrize("preset", [0, 1, 9, 10, 11])
 def test_teacher_forced_logits_tiny(device, llm_files, preset):
     g = m.Llm(device, llm_files[preset], 256)
     o = pyoracle.Llm(llm_files[preset], 256)
@@ -72,7 +74,7 @@ def test_teacher_forced_logits_tiny(device, llm_files, preset):
     assert agree >= 76
 
 
-@pytest.mark.parametrize("preset", [0, 1, 9])
+@pytest.mark.parametrize("preset", [0, 1, 9, 11])
 def test_generate_matches_oracle(device, llm_files, preset):
     g = m.Llm(device, llm_files[preset], 256)
     o = pyoracle.Llm(llm_files[preset], 256)
@@ -247,7 +249,7 @@ def test_loader_rejects_unknown_biases_and_incomplete_lfm2(device, tmp_path):
 # token in the same order, so the last token's logits (and therefore the KV cache rows they
 # read) equal a token-by-token decode BIT FOR BIT; vs the oracle the teacher-forced bound
 # above applies.
-@pytest.mark.parametrize("preset,n", [(0, 2), (0, 17), (1, 40), (0, 150), (9, 70)])
+@pytest.mark.parametrize("preset,n", [(0, 2), (0, 17), (1, 40), (0, 150), (9, 70), (11, 30)])
 def test_batched_prefill_matches_sequential(device, llm_files, preset, n):
     g = m.Llm(device, llm_files[preset], 256)
     toks = np.random.default_rng(100 + n).integers(0, g.n_vocab, n)

@@ -44,7 +44,7 @@ def _rel(a, b):
     return float(np.sqrt(np.mean((a - b) ** 2)) / max(np.sqrt(np.mean(b ** 2)), 1e-30))
 
 
-@pytest.mark.parametrize("preset", [3, 4, 2, 7, 8, 6, 9])
+@pytest.mark.parametrize("preset", [3, 4, 2, 7, 8, 6, 9, 11])
 def test_layers_match_oracle_on_gpu_inputs(device, synth_llm_path, preset):
     path = synth_llm_path(preset)
     g = m.Llm(device, path, 2048)

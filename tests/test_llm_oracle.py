@@ -194,3 +194,35 @@ def test_q4_0_q5_0_rows(qtype):
     c = codes.reshape(5, -1, 32)
     ref = ((d.reshape(5, -1) * da[None]) * (c * qa[None]).sum(2)).sum(1)
     assert np.allclose(y, ref, rtol=1e-5, atol=1e-6)
+
+
+def test_bf16_rows_and_vec_dot():
+    """BF16 weights (the published MioTTS BF16 GGUFs): the host quantizer rounds to nearest
+    even (ggml_compute_fp32_to_bf16, checked on a tie and a NaN), the oracle decodes the
+    rows exactly, and its vec_dot_bf16 equals a numpy sum (double) of the f32 products of the
+    weights with the bf16-rounded activation."""
+    def bf16(x):
+        u = np.asarray(x, np.float32).view(np.uint32).astype(np.uint64)
+        r = ((u + (0x7FFF + ((u >> 16) & 1))) >> 16).astype(np.uint16)
+        nan = (u & 0x7FFFFFFF) > 0x7F800000
+        return np.where(nan, ((u >> 16) | 64).astype(np.uint16), r)
+    rng = np.random.default_rng(30)
+    k = 576
+    x = (rng.standard_normal((4, k)) * 0.05).astype(np.float32)
+    x[0, 0] = np.float32(1.0 + 2.0 ** -8)  # a tie: rounds to even (1.0)
+    x[0, 1] = np.float32(1.0 + 3 * 2.0 ** -8)  # a tie: rounds up to even
+    q = m.quantize_rows(30, x)
+    h = q.view(np.uint16).reshape(4, k)
+    assert np.array_equal(h, bf16(x))
+    assert h[0, 0] == 0x3F80 and h[0, 1] == 0x3F82
+    got = _dequant(30, q, k)
+    assert np.array_equal(got, (h.astype(np.uint32) << 16).view(np.float32))
+    a = rng.standard_normal(k).astype(np.float32)
+    o = pyoracle.oracle()
+    o.mo_matvec.argtypes = [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_void_p,
+                            ctypes.c_void_p]
+    y = np.zeros(4, np.float32)
+    assert o.mo_matvec(30, q.ctypes.data, 4, k, a.ctypes.data, y.ctypes.data) == 0
+    ab = (bf16(a).astype(np.uint32) << 16).view(np.float32)
+    ref = np.array([np.sum((got[r] * ab).astype(np.float64)) for r in range(4)], np.float32)
+    assert np.array_equal(y, ref)
