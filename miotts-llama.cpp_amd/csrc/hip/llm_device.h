@@ -1402,8 +1402,14 @@ __device__ void attend_chunk(const float (*qs)[HD], const h8 (&kr)[AttCfg<HD>::I
 // next launch (kernel boundaries order that store before any later add). part / head0: the
 // wave-uniform record base and the element offset of head g = 0's record array (head g at
 // head0 + g * g_stride).
+// ak >= 0 (multi-token launches): the merger also writes the outputs' activation record for
+// the O matvec (ak = akind of W_o: 1 Q8_K, 0 Q8_0) into rec, blocks from blk0 on: wave w of
+// the merger holds outputs 256 w .. 256 w + 255 in quant_regs' layout, so the records are
+// k_bt_quant's bits and its launch is not needed (host: (G * HD) % 256 == 0 for Q8_K, % 32
+// for Q8_0).
 template <int HD, int G>
-__device__ void attn_merge_last(const float *part, uint32_t head0, uint32_t g_stride, int nch, int *cnt, float *out) {
+__device__ void attn_merge_last(const float *part, uint32_t head0, uint32_t g_stride, int nch, int *cnt, float *out,
+                                int ak = -1, ActL rec = {}, int blk0 = 0) {
     constexpr int NT = AttCfg<HD>::NT, REC = AttCfg<HD>::REC;
     __shared__ int last_;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1416,10 +1422,23 @@ __device__ void attn_merge_last(const float *part, uint32_t head0, uint32_t g_st
     }
     __syncthreads();
     if (!last_) return;
-    for (int e = 4 * (int)MIO_TIDX; e < G * HD; e += 4 * NT) {
+    static_assert(G * HD <= 4 * NT, "one float4 of outputs per thread");
+    const int e = 4 * (int)MIO_TIDX;
+    float4 y = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (e < G * HD) {
         const int g = e / HD, dd = e - g * HD;
-        const float4 y = merge_out4(part, head0 + (uint32_t)g * g_stride, nch, REC, HD, dd);
+        y = merge_out4(part, head0 + (uint32_t)g * g_stride, nch, REC, HD, dd);
         *reinterpret_cast<float4 *>(out + e) = y;
+    }
+    if (ak >= 0) {
+        const int wave = __builtin_amdgcn_readfirstlane(MIO_TIDX >> 6), lane = MIO_TIDX & 63;
+        if (wave * 256 < G * HD) {
+            const float vv[4] = {y.x, y.y, y.z, y.w};
+            if (ak == 1)
+                q8k_store(vv, abs_max4(vv), blk0 + wave, rec);
+            else
+                q80_store(vv, blk0 + wave * 8 + (lane >> 3), e < G * HD, rec);
+        }
     }
 }
 

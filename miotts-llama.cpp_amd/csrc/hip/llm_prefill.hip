@@ -652,18 +652,21 @@ __global__ __launch_bounds__(64) void k_pf_rope(LlmDims d, const float *q_norm, 
 
 // attend_chunk + attn_merge_last of token t's (kv head, chunk): records in pb.part
 // [t][H][max_splits][REC], tickets pb.att_cnt[t][Hkv], outputs pb.att[t][H * hd].
+// att_q >= 0: the merger also writes token t's O-matvec activation record (attn_merge_last).
 template <int HD, int G>
 __device__ __forceinline__ void attend_and_merge(const LlmDims &d, const float (*qs)[HD],
                                                  const h8 (&kr)[AttCfg<HD>::IT], const h8 (&vr)[AttCfg<HD>::IT],
                                                  int t0, int pos, int ch, int t, int kvh,
-                                                 float (*wres)[G][HD + 2], const PrefillBuffers &pb) {
+                                                 float (*wres)[G][HD + 2], const PrefillBuffers &pb, int att_q) {
     using C = AttCfg<HD>;
     const uint32_t gs = (uint32_t)(d.max_splits * C::REC);
     float *part = pb.part + (size_t)t * d.n_head * gs;  // token t's records (wave-uniform)
     const uint32_t head0 = (uint32_t)(kvh * G) * gs;
     attend_chunk<HD, G>(qs, kr, vr, t0, pos, d.scale, wres, part + head0 + (uint32_t)ch * C::REC, gs);
+    const int KO = d.n_head * HD;
     attn_merge_last<HD, G>(part, head0, gs, pos / ATT_CHUNK + 1, pb.att_cnt + (size_t)t * d.n_kv + kvh,
-                           pb.att + (size_t)t * d.n_head * HD + (size_t)kvh * G * HD);
+                           pb.att + (size_t)t * KO + (size_t)kvh * G * HD, att_q, carve_t(pb.act, KO, t).a,
+                           att_q == 1 ? kvh * G * HD / 256 : kvh * G * HD / 32);
 }
 
 // One workgroup per (ATT_CHUNK-position chunk, kv head, token): causal softmax over the
@@ -675,7 +678,7 @@ __device__ __forceinline__ void attend_and_merge(const LlmDims &d, const float (
 // work (the low chunks) spread over all XCDs instead of one.
 template <int HD, int G>
 __global__ __launch_bounds__(AttCfg<HD>::NT) void k_pf_attention(LlmDims d, const _Float16 *kc, const _Float16 *vc,
-                                                                 PrefillBuffers pb) {
+                                                                 PrefillBuffers pb, int att_q) {
     using C = AttCfg<HD>;
     __shared__ float qs[G][HD];
     __shared__ float wres[C::NW][G][HD + 2];
@@ -690,7 +693,7 @@ __global__ __launch_bounds__(AttCfg<HD>::NT) void k_pf_attention(LlmDims d, cons
     const float *qsrc = pb.qkv + (size_t)t * QD + (size_t)kvh * G * HD;
     for (int e = threadIdx.x; e < G * HD; e += C::NT) qs[e / HD][e % HD] = qsrc[e];
     lds_barrier();
-    attend_and_merge<HD, G>(d, qs, kr, vr, t0, pos, ch, t, kvh, wres, pb);
+    attend_and_merge<HD, G>(d, qs, kr, vr, t0, pos, ch, t, kvh, wres, pb, att_q);
 }
 
 // Batched decode attention (one token per sequence, so no token of the launch reads a row
@@ -703,7 +706,7 @@ __global__ __launch_bounds__(AttCfg<HD>::NT) void k_pf_attention(LlmDims d, cons
 template <int HD, int G>
 __global__ __launch_bounds__(AttCfg<HD>::NT) void k_bt_attention(LlmDims d, const float *q_norm, const float *k_norm,
                                                          const float *bqkv, _Float16 *kcache, _Float16 *vcache,
-                                                         PrefillBuffers pb) {
+                                                         PrefillBuffers pb, int att_q) {
     using C = AttCfg<HD>;
     constexpr int PER = HD / 64;
     __shared__ float qs[G][HD];
@@ -757,7 +760,7 @@ __global__ __launch_bounds__(AttCfg<HD>::NT) void k_bt_attention(LlmDims d, cons
                 if (it == r / C::NS) kr[it] = kn, vr[it] = vn;
         }
     }
-    attend_and_merge<HD, G>(d, qs, kr, vr, t0, pos, ch, t, kvh, wres, pb);
+    attend_and_merge<HD, G>(d, qs, kr, vr, t0, pos, ch, t, kvh, wres, pb, att_q);
 }
 
 template <int NP, int T>
@@ -951,27 +954,27 @@ __global__ __launch_bounds__(ST) void k_bt_embed(LlmDims d, QMat emb, PrefillBuf
 
 template <int HD>
 void launch_bt_attention(int G, dim3 grid, hipStream_t s, const LlmDims &d, const LayerW &L, _Float16 *kc,
-                         _Float16 *vc, const PrefillBuffers &pb) {
+                         _Float16 *vc, const PrefillBuffers &pb, int att_q) {
     const float *qn = L.q_norm, *kn = L.k_norm, *bi = L.bqkv;
     switch (G) {
-        case 1: hipLaunchKernelGGL((k_bt_attention<HD, 1>), grid, dim3(AttCfg<HD>::NT), 0, s, d, qn, kn, bi, kc, vc, pb); break;
-        case 2: hipLaunchKernelGGL((k_bt_attention<HD, 2>), grid, dim3(AttCfg<HD>::NT), 0, s, d, qn, kn, bi, kc, vc, pb); break;
-        case 3: hipLaunchKernelGGL((k_bt_attention<HD, 3>), grid, dim3(AttCfg<HD>::NT), 0, s, d, qn, kn, bi, kc, vc, pb); break;
-        case 4: hipLaunchKernelGGL((k_bt_attention<HD, 4>), grid, dim3(AttCfg<HD>::NT), 0, s, d, qn, kn, bi, kc, vc, pb); break;
-        case 8: hipLaunchKernelGGL((k_bt_attention<HD, 8>), grid, dim3(AttCfg<HD>::NT), 0, s, d, qn, kn, bi, kc, vc, pb); break;
+        case 1: hipLaunchKernelGGL((k_bt_attention<HD, 1>), grid, dim3(AttCfg<HD>::NT), 0, s, d, qn, kn, bi, kc, vc, pb, att_q); break;
+        case 2: hipLaunchKernelGGL((k_bt_attention<HD, 2>), grid, dim3(AttCfg<HD>::NT), 0, s, d, qn, kn, bi, kc, vc, pb, att_q); break;
+        case 3: hipLaunchKernelGGL((k_bt_attention<HD, 3>), grid, dim3(AttCfg<HD>::NT), 0, s, d, qn, kn, bi, kc, vc, pb, att_q); break;
+        case 4: hipLaunchKernelGGL((k_bt_attention<HD, 4>), grid, dim3(AttCfg<HD>::NT), 0, s, d, qn, kn, bi, kc, vc, pb, att_q); break;
+        case 8: hipLaunchKernelGGL((k_bt_attention<HD, 8>), grid, dim3(AttCfg<HD>::NT), 0, s, d, qn, kn, bi, kc, vc, pb, att_q); break;
         default: break;
     }
 }
 
 template <int HD>
 void launch_pf_attention(int G, dim3 grid, hipStream_t s, const LlmDims &d, const _Float16 *kc, const _Float16 *vc,
-                         const PrefillBuffers &pb) {
+                         const PrefillBuffers &pb, int att_q) {
     switch (G) {
-        case 1: hipLaunchKernelGGL((k_pf_attention<HD, 1>), grid, dim3(AttCfg<HD>::NT), 0, s, d, kc, vc, pb); break;
-        case 2: hipLaunchKernelGGL((k_pf_attention<HD, 2>), grid, dim3(AttCfg<HD>::NT), 0, s, d, kc, vc, pb); break;
-        case 3: hipLaunchKernelGGL((k_pf_attention<HD, 3>), grid, dim3(AttCfg<HD>::NT), 0, s, d, kc, vc, pb); break;
-        case 4: hipLaunchKernelGGL((k_pf_attention<HD, 4>), grid, dim3(AttCfg<HD>::NT), 0, s, d, kc, vc, pb); break;
-        case 8: hipLaunchKernelGGL((k_pf_attention<HD, 8>), grid, dim3(AttCfg<HD>::NT), 0, s, d, kc, vc, pb); break;
+        case 1: hipLaunchKernelGGL((k_pf_attention<HD, 1>), grid, dim3(AttCfg<HD>::NT), 0, s, d, kc, vc, pb, att_q); break;
+        case 2: hipLaunchKernelGGL((k_pf_attention<HD, 2>), grid, dim3(AttCfg<HD>::NT), 0, s, d, kc, vc, pb, att_q); break;
+        case 3: hipLaunchKernelGGL((k_pf_attention<HD, 3>), grid, dim3(AttCfg<HD>::NT), 0, s, d, kc, vc, pb, att_q); break;
+        case 4: hipLaunchKernelGGL((k_pf_attention<HD, 4>), grid, dim3(AttCfg<HD>::NT), 0, s, d, kc, vc, pb, att_q); break;
+        case 8: hipLaunchKernelGGL((k_pf_attention<HD, 8>), grid, dim3(AttCfg<HD>::NT), 0, s, d, kc, vc, pb, att_q); break;
         default: break;
     }
 }
@@ -1098,6 +1101,7 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
         const bool on = fq2_env >= 0 ? ((fq2_env >> kind) & 1) != 0 : (kind == 0 || type == 8);
         return !mmq && nt <= MW && pick_np(d.n_embd) == 1 && on;
     };
+    static const bool att_q_env = !(getenv("MIO_ATT_Q") && getenv("MIO_ATT_Q")[0] == '0');
     // MIO_BT_ATT=0: the batched decode step uses k_pf_rope + k_pf_attention (A/B)
     static const bool bt_att = !(getenv("MIO_BT_ATT") && getenv("MIO_BT_ATT")[0] == '0');
     decode = decode && bt_att;
@@ -1126,6 +1130,11 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
             launch_mmq(&so, &L.out_proj.type, 1, MMQ_RESID, MmqArgs{pb.act, act_bytes(n), n, nt, pb.x, n, {}}, s);
         } else {
             _Float16 *kc = kcache + il * layer_kv, *vc = vcache + il * layer_kv;
+            // the attention merger writes the O matvec's activation records when every kv head's
+            // G * hd outputs are whole quantization blocks (MIO_ATT_Q=0: a k_bt_quant launch)
+            const int gh = G * d.hd;
+            const int att_q = !att_q_env ? -1
+                              : (L.wo.type == 8 ? (gh % 32 == 0 ? 0 : -1) : (gh % 256 == 0 ? 1 : -1));
             const bool fa = fq2(0, L.wq.type);
             if (!fa)
                 launch_quant(d, 0, pb.x, d.n_embd, L.attn_norm, L.wq.type != 8, pb, nt, s);
@@ -1167,9 +1176,9 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
             if (decode) {
                 const dim3 grid(d.n_kv * nt, n_chunks);
                 if (d.hd == 128)
-                    launch_bt_attention<128>(G, grid, s, d, L, kc, vc, pb);
+                    launch_bt_attention<128>(G, grid, s, d, L, kc, vc, pb, att_q);
                 else
-                    launch_bt_attention<64>(G, grid, s, d, L, kc, vc, pb);
+                    launch_bt_attention<64>(G, grid, s, d, L, kc, vc, pb, att_q);
             } else {
                 {
                     const dim3 grid(d.n_head + d.n_kv, nt);
@@ -1182,11 +1191,11 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
                 }
                 const dim3 grid(d.n_kv * nt, n_chunks);
                 if (d.hd == 128)
-                    launch_pf_attention<128>(G, grid, s, d, kc, vc, pb);
+                    launch_pf_attention<128>(G, grid, s, d, kc, vc, pb, att_q);
                 else
-                    launch_pf_attention<64>(G, grid, s, d, kc, vc, pb);
+                    launch_pf_attention<64>(G, grid, s, d, kc, vc, pb, att_q);
             }
-            launch_quant(d, 1, pb.att, L.wo.k, nullptr, L.wo.type != 8, pb, nt, s);
+            if (att_q < 0) launch_quant(d, 1, pb.att, L.wo.k, nullptr, L.wo.type != 8, pb, nt, s);
             if (use_mmq(1, L.wo.type)) {
                 const MmqSeg sg{L.wo, mmq_tiles(L.wo.rows), 0};
                 launch_mmq(&sg, &L.wo.type, 1, MMQ_RESID, MmqArgs{pb.act, act_bytes(L.wo.k), L.wo.k, nt, pb.x, d.n_embd, {}},
