@@ -86,6 +86,22 @@ def dequant(qtype: int, raw: np.ndarray, rows: int, k: int) -> np.ndarray:
                 s = np.repeat(S[..., [2 * n, 2 * n + 1]], 16, axis=-1)  # sub-blocks of 16
                 out[:, :, 128 * h + 32 * n:128 * h + 32 * n + 32] = d * s * q
         return out.reshape(rows, k)
+    if qtype in (2, 6):  # Q4_0 / Q5_0: 32 codes per block, x - 8 / (nibble | fifth bit) - 16
+        bb = 18 if qtype == 2 else 22
+        b = raw.reshape(rows, k // 32, bb)
+        d = _f16(b[:, :, 0:2].copy()).reshape(rows, -1, 1)
+        qs = b[:, :, bb - 16:].astype(np.int64)
+        lo, hi = qs & 0xF, qs >> 4
+        if qtype == 2:
+            lo, hi = lo - 8, hi - 8
+        else:
+            qh = b[:, :, 2:6].copy().view(np.uint32).astype(np.int64)  # [rows, blocks, 1]
+            j = np.arange(16)
+            lo = (lo | (((qh >> j) & 1) << 4)) - 16
+            hi = (hi | (((qh >> (j + 16)) & 1) << 4)) - 16
+        return (d * np.concatenate([lo, hi], axis=2)).reshape(rows, k)
+    if qtype == 30:  # BF16: the high half of an f32
+        return (raw.view(np.uint16).astype(np.uint32) << 16).view(np.float32).reshape(rows, k).astype(np.float64)
     raise ValueError(f"np_ref: weight type {qtype}")
 
 
@@ -101,6 +117,13 @@ def act_q8_0(x: np.ndarray) -> np.ndarray:
     idv = np.where(d != 0, np.float32(1) / np.where(d != 0, d, 1), 0).astype(np.float32)
     q = _roundf((x * idv).astype(np.float32).astype(np.float64))
     return (d.astype(np.float16).astype(np.float64) * q).reshape(-1)
+
+
+def act_bf16(x: np.ndarray) -> np.ndarray:
+    """ggml_compute_fp32_to_bf16 (nearest even), returned as float64."""
+    u = np.asarray(x, np.float32).view(np.uint32).astype(np.uint64)
+    h = ((u + (0x7FFF + ((u >> 16) & 1))) >> 16).astype(np.uint32)
+    return (h << 16).view(np.float32).astype(np.float64)
 
 
 def act_q8_k(x: np.ndarray) -> np.ndarray:
@@ -123,7 +146,15 @@ class Mat:
         self.w = dequant(t.type, t.raw(), self.rows, self.k)
 
     def __matmul__(self, x: np.ndarray) -> np.ndarray:
-        a = act_q8_0(x) if self.type == 8 else (act_q8_k(x) if self.type in (12, 14) else x.astype(np.float64))
+        # the vec_dot_type: Q8_0 for Q8_0 / Q5_0 / Q4_0, Q8_K for the K-quants, BF16 for BF16
+        if self.type in (2, 6, 8):
+            a = act_q8_0(x)
+        elif self.type in (12, 14):
+            a = act_q8_k(x)
+        elif self.type == 30:
+            a = act_bf16(x)
+        else:
+            a = x.astype(np.float64)
         return (self.w @ a).astype(np.float32)
 
 

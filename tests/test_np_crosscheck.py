@@ -36,7 +36,7 @@ def _rel(a, b):
 @pytest.fixture(scope="module")
 def llms(tmp_path_factory):
     d = tmp_path_factory.mktemp("npllm")
-    return {p: m.synth_llm(str(d / f"llm{p}.gguf"), p, 1) for p in (0, 1, 5, 7, 8)}
+    return {p: m.synth_llm(str(d / f"llm{p}.gguf"), p, 1) for p in (0, 1, 5, 7, 8, 9, 10, 11)}
 
 
 def _sweep(o, n, toks):
@@ -65,7 +65,7 @@ def _sweep(o, n, toks):
     return flips, worst
 
 
-@pytest.mark.parametrize("preset", [0, 1, 5, 7, 8])
+@pytest.mark.parametrize("preset", [0, 1, 5, 7, 8, 9, 10, 11])
 def test_layers_match_numpy_restatement(llms, preset):
     path = llms[preset]
     n_pos = 40
