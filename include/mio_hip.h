@@ -206,6 +206,10 @@ int mio_hip_llm_load_ms(const mio_hip_llm *m, double *ms);
  * (the rest of the end token's interval plus one more: < 2 * check_interval; 0 when it stops
  * at max_tokens). */
 int mio_hip_llm_steps_issued(const mio_hip_llm *m, int *steps);
+/* Allocates now the device memory decodes of up to n_codes codes need (workspace, RoPE
+ * table, incremental prenet cache), as miocodec_load's graph-allocator reserve
+ * (miocodec.cpp:424-516); later decodes of at most n_codes allocate nothing. */
+int mio_hip_codec_reserve(mio_hip_codec *c, int n_codes);
 /* Prenet rows the last mio_hip_codec_decode_pcm took from the incremental cache. */
 int mio_hip_codec_last_reused(const mio_hip_codec *c, int *rows);
 /* Algorithmic FLOPs of the last mio_hip_codec_decode_pcm (2 per multiply-add of every GEMM,

@@ -880,6 +880,34 @@ extern "C" int mio_hip_codec_decode_pcm(mio_hip_codec *c, const int32_t *codes, 
     return MIO_OK;
 }
 
+// Device memory a decode of up to n_codes codes needs (workspace, RoPE table, the
+// incremental prenet cache, timing events), allocated now: the ggml_gallocr reserve of
+// miocodec_load (miocodec.cpp:424-516) happens at load too, so no decode pays a hipMalloc
+// (and a hipFree that waits for the whole device) in its own time.
+extern "C" int mio_hip_codec_reserve(mio_hip_codec *c, int n_codes) {
+    MIO_REQUIRE(c && n_codes > 0, MIO_ERR_INVALID, "codec_reserve: bad args");
+    int rc = mio::bind(c->d);
+    if (rc) return rc;
+    Ws w;
+    if ((rc = plan_ws(c, n_codes, w, true))) return rc;
+    if (!c->ev[0])
+        for (auto &e : c->ev) MIO_HIP_CHECK(hipEventCreate(&e));
+    if (n_codes > c->pc_cap) {
+        const int cap = std::max(2 * n_codes, 1024);
+        float *np = nullptr;
+        MIO_HIP_CHECK(hipMalloc(&np, (size_t)cap * c->dec_dim * 4));
+        if (c->pc) {
+            MIO_HIP_CHECK(hipDeviceSynchronize());
+            hipFree(c->pc);
+        }
+        c->pc = np;
+        c->pc_cap = cap;
+        c->pc_exact = 0;
+        c->pc_codes.clear();
+    }
+    return MIO_OK;
+}
+
 extern "C" int mio_hip_codec_last_reused(const mio_hip_codec *c, int *rows) {
     MIO_REQUIRE(c && rows, MIO_ERR_INVALID, "codec_last_reused: null");
     *rows = c->pc_last_reused;

@@ -64,6 +64,7 @@ struct mio_hip_llm {
     // prompt prefills replayed as graphs, by prompt length (the first prefill of a length runs
     // eagerly and is captured: ~280 launches that eager issue makes host-bound)
     std::map<int, hipGraphExec_t> prefill_graphs;
+    std::map<int, int> prefill_seen;  // eager prefills per prompt length (capture on the second)
     mio::SampleCfg *d_cfg = nullptr;
     float *d_layers = nullptr;  // mio_hip_llm_eval_layers' residual snapshots (parity tests)
     // generation state
@@ -358,7 +359,7 @@ int prefill_issue(mio_hip_llm *m, int n) {
 // Batched prefill of positions [0, n): every launch reads only device buffers whose addresses
 // depend on n alone (prompt tokens in m->d_prompt), so one graph per prompt length replays it.
 // The first prefill of a length runs eagerly (its launches set the kernels' LDS attributes
-// outside any capture), then is captured for the next utterance. MIO_PREFILL_GRAPH=0 or
+// outside any capture), the second too and is captured, later ones replay the graph. MIO_PREFILL_GRAPH=0 or
 // MIO_NO_GRAPH=1 (every launch eager, for kernel tracing): eager.
 int prefill(mio_hip_llm *m, int n) {
     static const bool use_graph = !(getenv("MIO_PREFILL_GRAPH") && getenv("MIO_PREFILL_GRAPH")[0] == '0') &&
@@ -370,7 +371,9 @@ int prefill(mio_hip_llm *m, int n) {
         return MIO_OK;
     }
     int rc = prefill_issue(m, n);
-    if (rc || !use_graph || m->prefill_graphs.size() >= 16) return rc;
+    // a length is captured when it comes back (the second prefill of that length): a one-off
+    // prompt does not pay for a capture it never replays
+    if (rc || !use_graph || m->prefill_graphs.size() >= 16 || m->prefill_seen[n]++ == 0) return rc;
     // capture a second issue for the next utterance of this length; the prefill above already
     // ran eagerly, so a failed capture or instantiation only leaves this length uncached
     hipStream_t s = m->d->stream;
@@ -856,6 +859,9 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
     }
     delete m->stager;
     m->stager = nullptr;
+    // the decode-step graphs are captured here, as llama_init_from_model reserves its compute
+    // graphs at context creation: the first generate replays them instead of capturing
+    if ((rc = ensure_graph(m))) return fail(rc);
     m->load_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_load0).count();
     *out = m;
     return MIO_OK;

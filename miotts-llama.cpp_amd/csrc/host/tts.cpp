@@ -326,6 +326,16 @@ struct TestToSpeech::Impl {
     }
 };
 
+static int cstream_priority() {
+    int least = 0, greatest = 0;
+    hipDeviceGetStreamPriorityRange(&least, &greatest);
+    const char *e = getenv("MIO_CSTREAM_PRIO");
+    const std::string v = e ? e : "normal";
+    if (v == "low") return least;
+    if (v == "high") return greatest;
+    return 0;
+}
+
 TestToSpeech::TestToSpeech(const Config &config) : config_(config), impl_(std::make_unique<Impl>()) {
     Impl &I = *impl_;
     I.dev = mio::default_device(config_.device);
@@ -356,6 +366,24 @@ TestToSpeech::TestToSpeech(const Config &config) : config_(config), impl_(std::m
     I.n_fft = miocodec_n_fft(I.codec);
     I.hop = miocodec_hop_length(I.codec);
     I.spt = miocodec_samples_per_token(I.codec);
+    // device memory for utterances of up to max_tokens codes, allocated with the models (as
+    // llama_init_from_model / miocodec_load reserve theirs): codec workspace and prenet cache,
+    // the PCM and PCM16 buffers; a synthesis then allocates nothing on the device
+    const int reserve = config_.max_tokens > 0 ? config_.max_tokens : 700;
+    if (mio_hip_codec_reserve(I.codec->codec, reserve) != MIO_OK ||
+        (I.spt > 0 && (!I.ensure(I.d_pcm, I.pcm_cap, (size_t)reserve * I.spt * sizeof(float) + 64) ||
+                       !I.ensure(I.d_pcm16, I.pcm16_cap, (size_t)reserve * I.spt * 2 + 64)))) {
+        fprintf(stderr, "TestToSpeech: device buffers for %d codes failed: %s\n", reserve, mio_hip_last_error());
+        miocodec_free(I.codec);
+        I.codec = nullptr;
+        return;
+    }
+    // the streaming path's codec stream (MIO_CSTREAM_PRIO=low|normal|high: its priority
+    // relative to the LLM's normal-priority stream)
+    if (hipStreamCreateWithPriority(&I.cstream, hipStreamNonBlocking, cstream_priority()) != hipSuccess) {
+        fprintf(stderr, "TestToSpeech: codec stream creation failed\n");
+        I.cstream = nullptr;
+    }
 }
 
 TestToSpeech::~TestToSpeech() = default;
@@ -465,16 +493,6 @@ bool TestToSpeech::synthesize_stream(const VoiceModel &voice, const std::string 
 bool TestToSpeech::synthesize_stream(const VoiceModel &voice, const std::string &text, const StreamCallback &callback,
                                      size_t chunk_samples) {
     return synthesize_stream(voice, text, callback, chunk_samples, Options{});
-}
-
-static int cstream_priority() {
-    int least = 0, greatest = 0;
-    hipDeviceGetStreamPriorityRange(&least, &greatest);
-    const char *e = getenv("MIO_CSTREAM_PRIO");
-    const std::string v = e ? e : "normal";
-    if (v == "low") return least;
-    if (v == "high") return greatest;
-    return 0;
 }
 
 // Streaming (test-to-speech.cpp:435-614): the LLM runs 20 steps per check on the GPU
