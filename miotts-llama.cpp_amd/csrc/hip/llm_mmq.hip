@@ -54,11 +54,11 @@ __device__ __forceinline__ int tok_of(int lane, int r) { return (r & 3) + 8 * (r
 
 // Balanced pairwise sum over a stream of 2^L values pushed in order (the decode's DPP trees:
 // ((s7+s6)+(s5+s4))+((s3+s2)+(s1+s0)) for L = 3), 16 tokens per lane.
-template <int L>
+template <int L, class V = v16f>
 struct Tree {
-    v16f lv[L];
+    V lv[L];
     template <int I>
-    __device__ __forceinline__ void push(v16f x) {
+    __device__ __forceinline__ void push(V x) {
         // carry chain of the binary counter at index I (compile-time)
         if constexpr (L >= 1 && (I & 1)) x = lv[0] + x;
         if constexpr (L >= 2 && (I & 3) == 3) x = lv[1] + x;
@@ -71,7 +71,7 @@ struct Tree {
         if constexpr (lvl < L) lv[lvl] = x;
         else result = x;
     }
-    v16f result;
+    V result;
 };
 
 // 16 int8 activations of token row `t` (record base) at byte offset e.. e+15
@@ -445,6 +445,283 @@ __global__ __launch_bounds__(MMQ_NT) void k_mmq(MmqSeg s0, MmqSeg s1, MmqSeg s2,
     }
 }
 
+// ---------------------------------------------------------------- 16-row x 16-token tiles
+// The same matmul for launches of at most 16 tokens (the batched decode of up to 16
+// utterances) on v_mfma_i32_16x16x32_i8: a 32x32 tile pads 8 tokens to 32 (75 % of every
+// MFMA and of its float epilogue wasted) and gives a 2048-row matrix 64 tiles; 16 x 16 tiles
+// pad to 16 and give it 128. Operands (8 bytes per lane): lane l holds token / weight row
+// l & 15 and the 8 K elements 8 (l >> 4) .. +7 of the 32-element group; the result: lane l,
+// weight row l & 15, tokens 4 (l >> 4) + i (tools/micro/mfma_i8_probe, 16x16x32_i8 hyp 1).
+// Per group the integer dot is exact and the scales, per-lane pass accumulation and the
+// decode's trees are applied exactly as in the 32 x 32 kernel above: every (row, token)
+// equals the single-token decode step bit for bit.
+constexpr int RT16 = 16, TT16 = 16;
+typedef float v4f __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ int tok16(int lane, int i) { return 4 * (lane >> 4) + i; }
+__device__ __forceinline__ long act8(const int8_t *qs, int e) { return *reinterpret_cast<const long *>(qs + e); }
+__device__ __forceinline__ v4i mfma16(long a, long b, v4i c) {
+    return __builtin_amdgcn_mfma_i32_16x16x32_i8(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ long lo_nib(uint2 q) {
+    return (long)(uint32_t)(q.x & M4) | ((long)(uint32_t)(q.y & M4) << 32);
+}
+__device__ __forceinline__ long hi_nib(uint2 q) {
+    return (long)(uint32_t)((q.x >> 4) & M4) | ((long)(uint32_t)((q.y >> 4) & M4) << 32);
+}
+
+// Q4_K superblock s: v = d * isum - dmin * imin per token (ggml vec_dot_q4_K_q8_K)
+__device__ __forceinline__ v4f sb16_q4k(const uint8_t *qrow, const uint8_t *hrow, int s, const int8_t *aq,
+                                        const float *da_lds) {
+    const int lane = threadIdx.x & 63, g = lane >> 4;
+    const uint4 hd = *reinterpret_cast<const uint4 *>(hrow + (size_t)s * 16);
+    uint2 nb[4];
+    long al[4], ah[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        nb[c] = *reinterpret_cast<const uint2 *>(qrow + (size_t)s * 128 + 32 * c + 8 * g);
+        al[c] = act8(aq, s * 256 + 64 * c + 8 * g);
+        ah[c] = act8(aq, s * 256 + 64 * c + 32 + 8 * g);
+    }
+    v4i isum = {}, imin = {};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const uint32_t wlo = c < 2 ? hd.y : (c == 2 ? hd.z : hd.w);
+        const uint32_t whi = c < 2 ? hd.z : hd.w;
+        const uint32_t F = __builtin_amdgcn_alignbit(whi, wlo, (24 * c) & 31);
+        const int sc0 = F & 63, m0 = (F >> 6) & 63, sc1 = (F >> 12) & 63, m1 = (F >> 18) & 63;
+        const v4i clo = mfma16(al[c], lo_nib(nb[c]), v4i{});
+        const v4i chi = mfma16(ah[c], hi_nib(nb[c]), v4i{});
+        const long mb0 = (long)(uint32_t)(m0 * 0x01010101) * 0x100000001l;
+        const long mb1 = (long)(uint32_t)(m1 * 0x01010101) * 0x100000001l;
+        imin = mfma16(al[c], mb0, imin);
+        imin = mfma16(ah[c], mb1, imin);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) isum[i] += __mul24(sc0, clo[i]) + __mul24(sc1, chi[i]);
+    }
+    const float dw = h2f(hd.x & 0xFFFF), dmw = h2f(hd.x >> 16);
+    v4f v;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const float da = da_lds[s * TT16 + tok16(lane, i)];
+        const float d = dw * da, dmin = dmw * da;
+        float x = d * (float)isum[i];
+        x = x - dmin * (float)imin[i];
+        v[i] = x;
+    }
+    return v;
+}
+
+// Q6_K superblock s: 16 sub-blocks of 16 values; sub-block j in K elements 0..15 of one MFMA
+// (lane groups 0, 1), lane groups 2, 3 contribute zeros; v = d * sum_j sc_j * C_j
+__device__ __forceinline__ v4f sb16_q6k(const QMat &W, int row, int s, const int8_t *aq, const float *da_lds) {
+    const int lane = threadIdx.x & 63, g = lane >> 4, h = g & 1;
+    const bool live = g < 2;
+    const int nsb = W.k >> 8;
+    const uint8_t *qlrow = W.p0 + (size_t)row * (W.k / 2);
+    const uint8_t *qhrow = W.p1 + (size_t)row * (W.k / 4);
+    const int8_t *screw = (const int8_t *)W.p2 + (size_t)row * (W.k / 16);
+    const uint16_t *drow = (const uint16_t *)W.p3 + (size_t)row * nsb;
+    const uint4 scr = *reinterpret_cast<const uint4 *>(screw + (size_t)s * 16);
+    int8_t sc[16];
+    __builtin_memcpy(sc, &scr, 16);
+    uint2 qh[2][2], ql[2][2][2];
+    long aa[16];
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            qh[n][b] = *reinterpret_cast<const uint2 *>(qhrow + (size_t)s * 64 + 32 * n + 16 * b + 8 * h);
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+                ql[n][a][b] = *reinterpret_cast<const uint2 *>(qlrow + (size_t)s * 128 + 64 * n + 32 * a + 16 * b + 8 * h);
+        }
+#pragma unroll
+    for (int j = 0; j < 16; ++j) aa[j] = live ? act8(aq, s * 256 + 16 * j + 8 * h) : 0l;
+    v4i isum = {};
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+                for (int hi = 0; hi < 2; ++hi) {
+                    const int gg = 2 * hi + a;
+                    const int j = 8 * n + 2 * gg + b;
+                    const uint2 l8 = ql[n][a][b], h8v = qh[n][b];
+                    const uint32_t lx = hi ? (l8.x >> 4) & M4 : l8.x & M4;
+                    const uint32_t ly = hi ? (l8.y >> 4) & M4 : l8.y & M4;
+                    const uint32_t hx = ((h8v.x >> (2 * gg)) & M2) << 4, hy = ((h8v.y >> (2 * gg)) & M2) << 4;
+                    const long bq = live ? ((long)(uint32_t)q6s(lx | hx) | ((long)(uint32_t)q6s(ly | hy) << 32)) : 0l;
+                    const v4i c = mfma16(aa[j], bq, v4i{});
+                    const int nn = j >> 3, rr = j & 7;
+                    const int scj = rr < 4 ? sc[2 * (4 * nn + rr)] : sc[2 * (4 * nn + rr - 4) + 1];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) isum[i] += __mul24(scj, c[i]);
+                }
+    const float dw = h2f(drow[s]);
+    v4f v;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const float d = dw * da_lds[s * TT16 + tok16(lane, i)];
+        v[i] = d * (float)isum[i];
+    }
+    return v;
+}
+
+template <int T>
+__device__ v4f slot16_kq(const QMat &W, int row, int k, const int8_t *aq, const float *da_lds) {
+    const int nsb = W.k >> 8, NP = (nsb + 7) / 8;
+    v4f acc = {};
+    for (int p = 0; p < NP; ++p) {
+        const int s = p * 8 + k;
+        v4f v = {};
+        if (s < nsb) {
+            if constexpr (T == 12)
+                v = sb16_q4k(W.p0 + (size_t)row * (W.k / 2), W.p1 + (size_t)row * nsb * 16, s, aq, da_lds);
+            else
+                v = sb16_q6k(W, row, s, aq, da_lds);
+        }
+        acc = acc + v;  // the decode lane's pass accumulation (0 + v0 + v1 ...)
+    }
+    return acc;
+}
+
+// Q8_0: slots 8k .. 8k+7 of lane group k (block b = p * 64 + slot), each slot's pass sum in
+// order, then sum8_f's tree over the 8 slots; per pass the 8 blocks' loads go out together
+__device__ v4f slot16_q80(const QMat &W, int row, int k, const int8_t *aq, const float *da_lds) {
+    const int lane = threadIdx.x & 63, g = lane >> 4;
+    const int nb = W.k >> 5, NP = (nb + 63) / 64;
+    const int8_t *qrow = (const int8_t *)W.p0 + (size_t)row * W.k;
+    const uint16_t *drow = (const uint16_t *)W.p1 + (size_t)row * nb;
+    v4f acc[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[i] = v4f{};
+    for (int p = 0; p < NP; ++p) {
+        long w[8], a[8];
+        float dw[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int b = min(p * 64 + 8 * k + i, nb - 1);  // clamped: every load in flight at once
+            w[i] = *reinterpret_cast<const long *>(qrow + (size_t)b * 32 + 8 * g);
+            a[i] = act8(aq, b * 32 + 8 * g);
+            dw[i] = h2f(drow[b]);
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int b = p * 64 + 8 * k + i;
+            v4f v = {};
+            if (b < nb) {  // wave-uniform
+                const v4i c = mfma16(a[i], w[i], v4i{});
+#pragma unroll
+                for (int j = 0; j < 4; ++j) v[j] = (float)c[j] * (dw[i] * da_lds[b * TT16 + tok16(lane, j)]);
+            }
+            acc[i] = acc[i] + v;
+        }
+    }
+    Tree<3, v4f> inner;
+    inner.template push<0>(acc[0]);
+    inner.template push<1>(acc[1]);
+    inner.template push<2>(acc[2]);
+    inner.template push<3>(acc[3]);
+    inner.template push<4>(acc[4]);
+    inner.template push<5>(acc[5]);
+    inner.template push<6>(acc[6]);
+    inner.template push<7>(acc[7]);
+    return inner.result;
+}
+
+template <int T>
+__device__ __forceinline__ v4f slot16_val(const QMat &W, int row, int k, const int8_t *aq, const float *da_lds) {
+    if constexpr (T == 8) return slot16_q80(W, row, k, aq, da_lds);
+    else return slot16_kq<T>(W, row, k, aq, da_lds);
+}
+
+// activation scales of the tile's 16 tokens -> LDS [group][token]; returns this lane's
+// token's codes (A operand: token lane & 15)
+template <int T>
+__device__ __forceinline__ const int8_t *stage_act16(const MmqArgs &a, int t0, int K, float *da_lds) {
+    const int ng = T == 8 ? K >> 5 : K >> 8;
+    const size_t ab = a.act_stride;
+    for (int e = threadIdx.x; e < ng * TT16; e += MMQ_NT) {
+        const int g = e / TT16, t = min(t0 + e % TT16, a.nt - 1);
+        da_lds[e] = reinterpret_cast<const float *>(a.act + (size_t)t * ab + K)[g];
+    }
+    __syncthreads();
+    const int t = min(t0 + (threadIdx.x & 15), a.nt - 1);
+    return reinterpret_cast<const int8_t *>(a.act + (size_t)t * ab);
+}
+
+__device__ __forceinline__ void slot16_store(const v4f &mine, float *red) {
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    *reinterpret_cast<float4 *>(red + ((size_t)wave * 64 + lane) * 4) = make_float4(mine[0], mine[1], mine[2], mine[3]);
+}
+__device__ __forceinline__ v4f slot16_sum(const float *red) {
+    const int lane = threadIdx.x & 63;
+    Tree<3, v4f> t;
+    auto leaf = [&]<int k>() {
+        const float4 f = *reinterpret_cast<const float4 *>(red + ((size_t)k * 64 + lane) * 4);
+        t.template push<k>(v4f{f.x, f.y, f.z, f.w});
+    };
+    leaf.template operator()<0>();
+    leaf.template operator()<1>();
+    leaf.template operator()<2>();
+    leaf.template operator()<3>();
+    leaf.template operator()<4>();
+    leaf.template operator()<5>();
+    leaf.template operator()<6>();
+    leaf.template operator()<7>();
+    return t.result;
+}
+
+template <int T0, int T1, int T2, int MODE>
+__global__ __launch_bounds__(MMQ_NT) void k_mmq16(MmqSeg s0, MmqSeg s1, MmqSeg s2, MmqArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    constexpr int NV = MODE == MMQ_SWIGLU ? 2 : 1;
+    float *red = reinterpret_cast<float *>(lds);  // [NV][8 waves][64][4]
+    float *da = red + NV * MMQ_NT * 4;           // [groups][16 tokens]
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int t0 = blockIdx.y * TT16;
+    int tile_id = blockIdx.x;
+    auto run = [&]<int T>(const MmqSeg &sg, int ti) {
+        const int row0 = ti * RT16, row = min(row0 + (lane & 15), sg.w.rows - 1);
+        // the slot index must be wave-uniform (divergent branches around the MFMAs would run
+        // them with a partial EXEC)
+        const int k = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+        const int8_t *aq = stage_act16<T>(a, t0, a.K, da);
+        slot16_store(slot16_val<T>(sg.w, row, k, aq, da), red);
+        if constexpr (NV == 2) slot16_store(slot16_val<T>(a.w_up, row, k, aq, da), red + MMQ_NT * 4);
+        __syncthreads();
+        if (wave != 0) return;
+        const v4f y = slot16_sum(red);
+        v4f u = {};
+        if constexpr (NV == 2) u = slot16_sum(red + MMQ_NT * 4);
+        const int orow = row0 + (lane & 15);
+        if (orow >= sg.w.rows) return;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int t = t0 + tok16(lane, i);
+            if (t >= a.nt) continue;
+            float *o = a.out + (size_t)t * a.ld + sg.out_off + orow;
+            if constexpr (MODE == MMQ_STORE) *o = y[i];
+            else if constexpr (MODE == MMQ_RESID) *o = y[i] + *o;
+            else *o = silu_f(y[i]) * u[i];
+        }
+    };
+    const int n0 = (s0.w.rows + RT16 - 1) / RT16;
+    if (tile_id < n0) return run.template operator()<T0>(s0, tile_id);
+    tile_id -= n0;
+    if constexpr (T1 >= 0) {
+        const int n1 = (s1.w.rows + RT16 - 1) / RT16;
+        if (tile_id < n1) return run.template operator()<T1>(s1, tile_id);
+        tile_id -= n1;
+    }
+    if constexpr (T2 >= 0) {
+        if (tile_id < (s2.w.rows + RT16 - 1) / RT16) return run.template operator()<T2>(s2, tile_id);
+    }
+}
+
 }  // namespace
 
 size_t mmq_lds(int type, int K, int mode) {
@@ -469,18 +746,37 @@ static void allow_lds_mmq(const void *kern) {
 int mmq_tiles(int rows) { return (rows + RT - 1) / RT; }
 
 // types: {T0, T1, T2} (-1 = segment unused); mode MMQ_*.
+// 16 x 16 tiles (k_mmq16) for launches of at most 16 tokens; MIO_MMQ16=0: 32 x 32 tiles always
+bool mmq16_on(int nt) {
+    static const bool on = !(getenv("MIO_MMQ16") && getenv("MIO_MMQ16")[0] == '0');
+    return on && nt <= TT16;
+}
+
 void launch_mmq(const MmqSeg *seg, const int *types, int nseg, int mode, const MmqArgs &a, hipStream_t s) {
     MmqSeg sg[3] = {seg[0], nseg > 1 ? seg[1] : MmqSeg{}, nseg > 2 ? seg[2] : MmqSeg{}};
+    const bool t16 = mmq16_on(a.nt);
     int tiles = 0;
-    for (int i = 0; i < nseg; ++i) tiles += sg[i].tiles;
-    const dim3 grid(tiles, (a.nt + TT - 1) / TT);
+    for (int i = 0; i < nseg; ++i) tiles += t16 ? (sg[i].w.rows + RT16 - 1) / RT16 : sg[i].tiles;
+    const dim3 grid(tiles, t16 ? 1 : (a.nt + TT - 1) / TT);
     size_t lds = 0;
-    for (int i = 0; i < nseg; ++i) lds = std::max(lds, mmq_lds(types[i], a.K, mode));
+    for (int i = 0; i < nseg; ++i)
+        lds = std::max(lds, t16 ? (size_t)(mode == MMQ_SWIGLU ? 2 : 1) * MMQ_NT * 4 * sizeof(float) +
+                                      (size_t)(types[i] == 8 ? a.K / 32 : a.K / 256) * TT16 * sizeof(float)
+                                : mmq_lds(types[i], a.K, mode));
     auto go = [&]<int A, int B, int C>() {
         auto launch = [&](auto kern) {
             if (lds > 64 * 1024) allow_lds_mmq(reinterpret_cast<const void *>(kern));
             hipLaunchKernelGGL(kern, grid, dim3(MMQ_NT), lds, s, sg[0], sg[1], sg[2], a);
         };
+        if (t16) {
+            if (mode == MMQ_STORE)
+                launch(k_mmq16<A, B, C, MMQ_STORE>);
+            else if (mode == MMQ_RESID)
+                launch(k_mmq16<A, B, C, MMQ_RESID>);
+            else
+                launch(k_mmq16<A, B, C, MMQ_SWIGLU>);
+            return;
+        }
         if (mode == MMQ_STORE)
             launch(k_mmq<A, B, C, MMQ_STORE>);
         else if (mode == MMQ_RESID)

@@ -289,7 +289,10 @@ def test_batched_prefill_1p7b_q4km(device, tmp_path):
 @pytest.mark.parametrize("qtype,k,rows,nt", [(8, 256, 40, 1), (8, 576, 37, 5), (8, 2048, 64, 33), (8, 10752, 33, 17),
                                            (12, 256, 50, 3), (14, 768, 33, 2),
                                            (12, 2048, 70, 32), (12, 6144, 32, 64), (14, 2048, 45, 9),
-                                           (14, 6144, 96, 40)])
+                                           (14, 6144, 96, 40),
+                                           # <= 16 tokens: the 16 x 16 tiles (k_mmq16)
+                                           (8, 2048, 70, 8), (8, 10752, 40, 16), (12, 2048, 70, 8),
+                                           (12, 6144, 33, 16), (14, 2048, 45, 8), (14, 6144, 37, 12)])
 def test_mmq_equals_single_token_matvec(device, qtype, k, rows, nt):
     """The batched matmul on the int8 matrix cores (llm_mmq.hip: prefill and batched decode)
     returns, for every token, the single-token decode matvec's value BIT FOR BIT (same exact
