@@ -1269,9 +1269,9 @@ extern "C" int mio_hip_debug_matvec(mio_hip_device *d, uint32_t type, const void
                                     const float *x, float *y) {
     MIO_REQUIRE(d && gguf_rows && x && y && rows > 0 && k > 0, MIO_ERR_INVALID, "debug_matvec: bad args");
     MIO_REQUIRE(type == mio::GGML_Q8_0 || type == mio::GGML_Q4_K || type == mio::GGML_Q6_K ||
-                    mio::repacks_to_q8_0(type),
+                    type == mio::GGML_BF16 || mio::repacks_to_q8_0(type),
                 MIO_ERR_UNSUPPORTED, "debug_matvec: type %u", type);
-    const bool k32 = type == mio::GGML_Q8_0 || mio::repacks_to_q8_0(type);
+    const bool k32 = type == mio::GGML_Q8_0 || type == mio::GGML_BF16 || mio::repacks_to_q8_0(type);
     MIO_REQUIRE(k % (k32 ? 32 : 256) == 0, MIO_ERR_INVALID, "debug_matvec: k %d", k);
     int rc = mio::bind(d);
     if (rc) return rc;
