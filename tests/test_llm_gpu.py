@@ -69,8 +69,10 @@ def test_teacher_forced_logits_tiny(device, llm_files, preset):
         rel = np.abs(lg - lo).max() / np.abs(lo).max()
         # preset 9's 576-wide rows re-quantize to Q8_0 blocks (Q5_0 / Q8_0 fallbacks) with G = 3
         # heads per kv head, like the 0.1B model, whose flips start at position 0-1 too
-        # (test_teacher_forced_large_models); the per-layer test pins its layers
-        if pos < (1 if preset == 9 else 2):
+        # (test_teacher_forced_large_models); BF16 (11) rounds every matvec input to 8
+        # mantissa bits, so an f32-ulp difference of a sum flips a rounding much sooner. The
+        # per-layer test (test_llm_layers_gpu.py) pins both presets' layers.
+        if pos < {9: 1, 11: 0}.get(preset, 2):
             assert rel <= 1e-5, (pos, rel)
         assert rel <= 5e-2, (pos, rel)
         agree += int(lg.argmax() == lo.argmax())
