@@ -9,9 +9,10 @@ namespace mio {
 
 // attention positions per chunk (one attention workgroup), = LlmDims::split. Every path
 // (decode step, batched decode, prefill) uses the same chunks and the same merge, so their
-// results are bit-identical. MIO_ATT_CHUNK: A/B builds (32, 64 or 128).
+// results are bit-identical. MIO_ATT_CHUNK: A/B builds (32, 64 or 128); 64 by default
+// (profiles/r04_att_chunk_ab.txt: 1.7B decode 0.823 / 0.773 / 0.775 ms per token at 32 / 64 / 128).
 #ifndef MIO_ATT_CHUNK
-#define MIO_ATT_CHUNK 32
+#define MIO_ATT_CHUNK 64
 #endif
 constexpr int kAttChunk = MIO_ATT_CHUNK;
 static_assert(kAttChunk == 32 || kAttChunk == 64 || kAttChunk == 128, "attention chunk");

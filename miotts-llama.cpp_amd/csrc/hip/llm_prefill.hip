@@ -517,7 +517,10 @@ __global__ __launch_bounds__(MT) void k_bt_conv(LlmDims d, const float *conv_w, 
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int t = blockIdx.x, K = d.n_embd;
     const size_t CW = (size_t)3 * K;
-    const Smem s = carve(smem, K);
+    // quantized straight into the token's global record (k_bt_quant's way); LDS keeps the
+    // reduction scratch
+    Smem s = carve(smem, K);
+    s.a = carve_t(pb.act, K, t).a;
     const int pos = pb.pos[t * pb.pos_stride], sq = pb.seq[t * pb.seq_stride];
     const float *rs = ring + (size_t)sq * pb.seq_ring;
     ConvPrev pv[2];
@@ -534,10 +537,6 @@ __global__ __launch_bounds__(MT) void k_bt_conv(LlmDims d, const float *conv_w, 
     ConvRegs<NP> cr;
     conv_load(pb.qkv + t * CW, pv[0], pv[1], conv_w, K, cr);
     conv_quant(cr, K, kq != 0, s, nullptr);
-    const int n16 = (int)(act_bytes(K) / 16);
-    const uint4 *l = reinterpret_cast<const uint4 *>(s.a.qs);
-    uint4 *g = reinterpret_cast<uint4 *>(pb.act + (size_t)t * act_bytes(K));
-    for (int i = threadIdx.x; i < n16; i += MT) g[i] = l[i];
 }
 
 // After k_bt_conv: the bx rows of each sequence's last two positions in this launch go to
