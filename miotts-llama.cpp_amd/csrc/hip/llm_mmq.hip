@@ -470,19 +470,41 @@ __device__ __forceinline__ long hi_nib(uint2 q) {
     return (long)(uint32_t)((q.x >> 4) & M4) | ((long)(uint32_t)((q.y >> 4) & M4) << 32);
 }
 
-// Q4_K superblock s: v = d * isum - dmin * imin per token (ggml vec_dot_q4_K_q8_K)
+// Q8_0 with 16-B loads (K % 256 == 0): lane (row / token l & 15, group g = l >> 4) loads 16 B
+// at byte 16 g of a 64-B block pair (b, b + 1) - groups 0, 1 hold block b, groups 2, 3 block
+// b + 1 - and one v_permlane32_swap per dword swaps the high 8 B of lanes 0-31 with the low
+// 8 B of lanes 32-63: the low halves of the 4 groups are then block b's bytes {0-7, 16-23,
+// 8-15, 24-31}, the high halves block b + 1's, in the weights and in the activations alike, so
+// one 16x16x32 MFMA per block gives the same exact integer dot. A wave's 8 weight scales of a
+// pass are one 16-B load. Per wave and pass: 4 weight loads per matrix, 4 activation loads,
+// one scale load per matrix, instead of 8 + 8 + 8 (8-B weights / activations, 2-B scales):
+// the vector-memory instruction count is what bounds these launches at 8 tokens
+// (tools/micro/mmq_probe.hip: 2 x 10752 x 2048 gate|up 28.7 -> 13.7 us, bit-equal).
+__device__ __forceinline__ void swap_halves(v4i &x) {
+    const auto p = __builtin_amdgcn_permlane32_swap(x.x, x.z, false, false);
+    const auto q = __builtin_amdgcn_permlane32_swap(x.y, x.w, false, false);
+    x.x = p[0], x.z = p[1], x.y = q[0], x.w = q[1];
+}
+__device__ __forceinline__ long lo8(const v4i &x) { return (long)(uint32_t)x.x | ((long)(uint32_t)x.y << 32); }
+__device__ __forceinline__ long hi8(const v4i &x) { return (long)(uint32_t)x.z | ((long)(uint32_t)x.w << 32); }
+
+// Q4_K superblock s: v = d * isum - dmin * imin per token (ggml vec_dot_q4_K_q8_K). Loads as
+// in the Q8_0 pair path (swap_halves): the 32-B nibble runs of sub-block pairs c, c + 1 are
+// one 16-B load per lane, the 64 activation bytes of sub-blocks 2c, 2c + 1 another; after the
+// swaps the low / high halves hold one run / one sub-block each in the same K order.
 __device__ __forceinline__ v4f sb16_q4k(const uint8_t *qrow, const uint8_t *hrow, int s, const int8_t *aq,
                                         const float *da_lds) {
     const int lane = threadIdx.x & 63, g = lane >> 4;
     const uint4 hd = *reinterpret_cast<const uint4 *>(hrow + (size_t)s * 16);
-    uint2 nb[4];
-    long al[4], ah[4];
+    v4i w[2], x[4];
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        nb[c] = *reinterpret_cast<const uint2 *>(qrow + (size_t)s * 128 + 32 * c + 8 * g);
-        al[c] = act8(aq, s * 256 + 64 * c + 8 * g);
-        ah[c] = act8(aq, s * 256 + 64 * c + 32 + 8 * g);
-    }
+    for (int i = 0; i < 2; ++i) w[i] = *reinterpret_cast<const v4i *>(qrow + (size_t)s * 128 + 64 * i + 16 * g);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) x[c] = *reinterpret_cast<const v4i *>(aq + s * 256 + 64 * c + 16 * g);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) swap_halves(w[i]);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) swap_halves(x[c]);
     v4i isum = {}, imin = {};
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
@@ -490,12 +512,14 @@ __device__ __forceinline__ v4f sb16_q4k(const uint8_t *qrow, const uint8_t *hrow
         const uint32_t whi = c < 2 ? hd.z : hd.w;
         const uint32_t F = __builtin_amdgcn_alignbit(whi, wlo, (24 * c) & 31);
         const int sc0 = F & 63, m0 = (F >> 6) & 63, sc1 = (F >> 12) & 63, m1 = (F >> 18) & 63;
-        const v4i clo = mfma16(al[c], lo_nib(nb[c]), v4i{});
-        const v4i chi = mfma16(ah[c], hi_nib(nb[c]), v4i{});
+        const long q = (c & 1) ? hi8(w[c >> 1]) : lo8(w[c >> 1]);
+        const long al = lo8(x[c]), ah = hi8(x[c]);
+        const v4i clo = mfma16(al, q & 0x0F0F0F0F0F0F0F0Fl, v4i{});
+        const v4i chi = mfma16(ah, (q >> 4) & 0x0F0F0F0F0F0F0F0Fl, v4i{});
         const long mb0 = (long)(uint32_t)(m0 * 0x01010101) * 0x100000001l;
         const long mb1 = (long)(uint32_t)(m1 * 0x01010101) * 0x100000001l;
-        imin = mfma16(al[c], mb0, imin);
-        imin = mfma16(ah[c], mb1, imin);
+        imin = mfma16(al, mb0, imin);
+        imin = mfma16(ah, mb1, imin);
 #pragma unroll
         for (int i = 0; i < 4; ++i) isum[i] += __mul24(sc0, clo[i]) + __mul24(sc1, chi[i]);
     }
@@ -505,62 +529,73 @@ __device__ __forceinline__ v4f sb16_q4k(const uint8_t *qrow, const uint8_t *hrow
     for (int i = 0; i < 4; ++i) {
         const float da = da_lds[s * TT16 + tok16(lane, i)];
         const float d = dw * da, dmin = dmw * da;
-        float x = d * (float)isum[i];
-        x = x - dmin * (float)imin[i];
-        v[i] = x;
+        float xx = d * (float)isum[i];
+        xx = xx - dmin * (float)imin[i];
+        v[i] = xx;
     }
     return v;
 }
 
-// Q6_K superblock s: 16 sub-blocks of 16 values; sub-block j in K elements 0..15 of one MFMA
-// (lane groups 0, 1), lane groups 2, 3 contribute zeros; v = d * sum_j sc_j * C_j
+// Q6_K superblock s: v = d * sum_j sc_j * dot_j over its 16 sub-blocks of 16 (ggml
+// vec_dot_q6_K_q8_K). A q-group (n, g4) = values 128 n + 32 g4 + l, l < 32: low (g4 0, 1) or
+// high (g4 2, 3) nibbles of ql[64 n + 32 (g4 & 1) + l] with bits 2 g4 of qh[32 n + l], i.e.
+// sub-blocks 8 n + 2 g4 and + 1. Loads as in the Q8_0 pair path (swap_halves): ql's 64 B of
+// half n, qh's 64 B and the 64 activation bytes of q-groups (n, 2i), (n, 2i + 1) are one 16-B
+// load per lane each; after the swaps every lane holds 8 values l in {0-7, 16-23, 8-15, 24-31}
+// of its group g, so sub-block 8 n + 2 g4 lies in groups 0, 2 and the next one in groups 1, 3:
+// two 16x16x32 MFMAs per q-group, each on one sub-block's lanes (the others zero).
 __device__ __forceinline__ v4f sb16_q6k(const QMat &W, int row, int s, const int8_t *aq, const float *da_lds) {
-    const int lane = threadIdx.x & 63, g = lane >> 4, h = g & 1;
-    const bool live = g < 2;
+    const int lane = threadIdx.x & 63, g = lane >> 4;
+    const bool first = (g & 1) == 0;  // groups 0, 2: the q-group's first sub-block
     const int nsb = W.k >> 8;
     const uint8_t *qlrow = W.p0 + (size_t)row * (W.k / 2);
     const uint8_t *qhrow = W.p1 + (size_t)row * (W.k / 4);
     const int8_t *screw = (const int8_t *)W.p2 + (size_t)row * (W.k / 16);
     const uint16_t *drow = (const uint16_t *)W.p3 + (size_t)row * nsb;
+    // split-layout scales: pair p2 = 4n + r -> {scales[8n + r], scales[8n + r + 4]}
     const uint4 scr = *reinterpret_cast<const uint4 *>(screw + (size_t)s * 16);
     int8_t sc[16];
     __builtin_memcpy(sc, &scr, 16);
-    uint2 qh[2][2], ql[2][2][2];
-    long aa[16];
+    v4i ql[2], qh, x[4];
 #pragma unroll
-    for (int n = 0; n < 2; ++n)
+    for (int n = 0; n < 2; ++n) ql[n] = *reinterpret_cast<const v4i *>(qlrow + (size_t)s * 128 + 64 * n + 16 * g);
+    qh = *reinterpret_cast<const v4i *>(qhrow + (size_t)s * 64 + 16 * g);
 #pragma unroll
-        for (int b = 0; b < 2; ++b) {
-            qh[n][b] = *reinterpret_cast<const uint2 *>(qhrow + (size_t)s * 64 + 32 * n + 16 * b + 8 * h);
+    for (int i = 0; i < 4; ++i) x[i] = *reinterpret_cast<const v4i *>(aq + s * 256 + 64 * i + 16 * g);
+    const float dw = h2f(drow[s]);
+    swap_halves(ql[0]);
+    swap_halves(ql[1]);
+    swap_halves(qh);
 #pragma unroll
-            for (int a = 0; a < 2; ++a)
-                ql[n][a][b] = *reinterpret_cast<const uint2 *>(qlrow + (size_t)s * 128 + 64 * n + 32 * a + 16 * b + 8 * h);
-        }
-#pragma unroll
-    for (int j = 0; j < 16; ++j) aa[j] = live ? act8(aq, s * 256 + 16 * j + 8 * h) : 0l;
+    for (int i = 0; i < 4; ++i) swap_halves(x[i]);
     v4i isum = {};
 #pragma unroll
-    for (int n = 0; n < 2; ++n)
+    for (int n = 0; n < 2; ++n) {
+        const uint32_t hw0 = n ? (uint32_t)qh.z : (uint32_t)qh.x, hw1 = n ? (uint32_t)qh.w : (uint32_t)qh.y;
 #pragma unroll
-        for (int b = 0; b < 2; ++b)
+        for (int g4 = 0; g4 < 4; ++g4) {
+            // ql bytes 32 (g4 & 1) + l of half n: the low (g4 & 1 == 0) or high halves after the swap
+            const uint32_t lw0 = (g4 & 1) ? (uint32_t)ql[n].z : (uint32_t)ql[n].x;
+            const uint32_t lw1 = (g4 & 1) ? (uint32_t)ql[n].w : (uint32_t)ql[n].y;
+            const int sh = 4 * (g4 >> 1);
+            const uint32_t b0 = q6s(((lw0 >> sh) & M4) | (((hw0 >> (2 * g4)) & M2) << 4));
+            const uint32_t b1 = q6s(((lw1 >> sh) & M4) | (((hw1 >> (2 * g4)) & M2) << 4));
+            const long bq = (long)b0 | ((long)b1 << 32);
+            const v4i &xa = x[2 * n + (g4 >> 1)];
+            const long a = (g4 & 1) ? hi8(xa) : lo8(xa);
+            const v4i c0 = mfma16(first ? a : 0l, bq, v4i{});
+            const v4i c1 = mfma16(first ? 0l : a, bq, v4i{});
 #pragma unroll
-            for (int a = 0; a < 2; ++a)
+            for (int h = 0; h < 2; ++h) {
+                const int j = 8 * n + 2 * g4 + h;  // sub-block
+                const int nn = j >> 3, rr = j & 7;
+                const int scj = rr < 4 ? sc[2 * (4 * nn + rr)] : sc[2 * (4 * nn + rr - 4) + 1];
+                const v4i &c = h ? c1 : c0;
 #pragma unroll
-                for (int hi = 0; hi < 2; ++hi) {
-                    const int gg = 2 * hi + a;
-                    const int j = 8 * n + 2 * gg + b;
-                    const uint2 l8 = ql[n][a][b], h8v = qh[n][b];
-                    const uint32_t lx = hi ? (l8.x >> 4) & M4 : l8.x & M4;
-                    const uint32_t ly = hi ? (l8.y >> 4) & M4 : l8.y & M4;
-                    const uint32_t hx = ((h8v.x >> (2 * gg)) & M2) << 4, hy = ((h8v.y >> (2 * gg)) & M2) << 4;
-                    const long bq = live ? ((long)(uint32_t)q6s(lx | hx) | ((long)(uint32_t)q6s(ly | hy) << 32)) : 0l;
-                    const v4i c = mfma16(aa[j], bq, v4i{});
-                    const int nn = j >> 3, rr = j & 7;
-                    const int scj = rr < 4 ? sc[2 * (4 * nn + rr)] : sc[2 * (4 * nn + rr - 4) + 1];
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) isum[i] += __mul24(scj, c[i]);
-                }
-    const float dw = h2f(drow[s]);
+                for (int i = 0; i < 4; ++i) isum[i] += __mul24(scj, c[i]);
+            }
+        }
+    }
     v4f v;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -632,6 +667,82 @@ __device__ v4f slot16_q80(const QMat &W, int row, int k, const int8_t *aq, const
     return inner.result;
 }
 
+struct Q80Pass {
+    v4i w[4];
+    v4i ds;  // the 8 blocks' f16 scales
+};
+// pass p of slot group k (blocks p * 64 + 8 k .. + 7; the group is wave-uniform, and with
+// K % 256 == 0 either all of its blocks exist or none: clamped loads, values skipped)
+__device__ __forceinline__ void q80p_load(const QMat &W, int row, int p, int k, Q80Pass &q) {
+    const int g = (threadIdx.x & 63) >> 4, nb = W.k >> 5;
+    const int b0 = min(p * 64 + 8 * k, nb - 8);
+    const int8_t *qrow = (const int8_t *)W.p0 + (size_t)row * W.k;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) q.w[i] = *reinterpret_cast<const v4i *>(qrow + (size_t)(b0 + 2 * i) * 32 + 16 * g);
+    q.ds = *reinterpret_cast<const v4i *>((const uint16_t *)W.p1 + (size_t)row * nb + b0);
+}
+__device__ __forceinline__ void act_load(const int8_t *aq, int K, int p, int k, v4i (&a)[4]) {
+    const int g = (threadIdx.x & 63) >> 4;
+    const int b0 = min(p * 64 + 8 * k, (K >> 5) - 8);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a[i] = *reinterpret_cast<const v4i *>(aq + (b0 + 2 * i) * 32 + 16 * g);
+}
+// the 8 slots' values of one pass added to acc (a: the pass's activations, already swapped)
+__device__ __forceinline__ void q80p_acc(Q80Pass &q, const v4i (&a)[4], int p, int k, int nb, const float *da_lds,
+                                         v4f (&acc)[8]) {
+    const int lane = threadIdx.x & 63;
+    const int b0 = p * 64 + 8 * k;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) swap_halves(q.w[i]);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        v4f v = {};
+        if (b0 < nb) {  // wave-uniform
+            const v4i &w = q.w[i >> 1], &x = a[i >> 1];
+            const v4i c = (i & 1) ? mfma16(hi8(x), hi8(w), v4i{}) : mfma16(lo8(x), lo8(w), v4i{});
+            const uint32_t dd = (uint32_t)q.ds[i >> 1];
+            const float dw = h2f((i & 1) ? dd >> 16 : dd & 0xFFFF);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = (float)c[j] * (dw * da_lds[(b0 + i) * TT16 + tok16(lane, j)]);
+        }
+        acc[i] = acc[i] + v;
+    }
+}
+__device__ __forceinline__ v4f tree8(const v4f (&acc)[8]) {
+    Tree<3, v4f> t;
+    t.template push<0>(acc[0]);
+    t.template push<1>(acc[1]);
+    t.template push<2>(acc[2]);
+    t.template push<3>(acc[3]);
+    t.template push<4>(acc[4]);
+    t.template push<5>(acc[5]);
+    t.template push<6>(acc[6]);
+    t.template push<7>(acc[7]);
+    return t.result;
+}
+// NV matrices (W, then U) over the same activations, one pass at a time
+template <int NV>
+__device__ __forceinline__ void slot16_q80p(const QMat &W, const QMat &U, int row, int k, const int8_t *aq,
+                                            const float *da_lds, v4f &y, v4f &u) {
+    const int nb = W.k >> 5, NP = (nb + 63) / 64;
+    v4f aw[8], au[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) aw[i] = v4f{}, au[i] = v4f{};
+    for (int p = 0; p < NP; ++p) {
+        Q80Pass qw, qu;
+        v4i x[4];
+        q80p_load(W, row, p, k, qw);
+        if constexpr (NV == 2) q80p_load(U, row, p, k, qu);
+        act_load(aq, W.k, p, k, x);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) swap_halves(x[i]);
+        q80p_acc(qw, x, p, k, nb, da_lds, aw);
+        if constexpr (NV == 2) q80p_acc(qu, x, p, k, nb, da_lds, au);
+    }
+    y = tree8(aw);
+    if constexpr (NV == 2) u = tree8(au);
+}
+
 template <int T>
 __device__ __forceinline__ v4f slot16_val(const QMat &W, int row, int k, const int8_t *aq, const float *da_lds) {
     if constexpr (T == 8) return slot16_q80(W, row, k, aq, da_lds);
@@ -644,13 +755,20 @@ template <int T>
 __device__ __forceinline__ const int8_t *stage_act16(const MmqArgs &a, int t0, int K, float *da_lds) {
     const int ng = T == 8 ? K >> 5 : K >> 8;
     const size_t ab = a.act_stride;
+    // token-major walk: consecutive threads read consecutive scales of one record
     for (int e = threadIdx.x; e < ng * TT16; e += MMQ_NT) {
-        const int g = e / TT16, t = min(t0 + e % TT16, a.nt - 1);
-        da_lds[e] = reinterpret_cast<const float *>(a.act + (size_t)t * ab + K)[g];
+        const int tt = e / ng, g = e - tt * ng, t = min(t0 + tt, a.nt - 1);
+        da_lds[g * TT16 + tt] = reinterpret_cast<const float *>(a.act + (size_t)t * ab + K)[g];
     }
     __syncthreads();
     const int t = min(t0 + (threadIdx.x & 15), a.nt - 1);
     return reinterpret_cast<const int8_t *>(a.act + (size_t)t * ab);
+}
+
+// this lane's token's codes (A operand: token lane & 15; no loads)
+__device__ __forceinline__ const int8_t *act16_codes(const MmqArgs &a, int t0) {
+    const int t = min(t0 + (threadIdx.x & 15), a.nt - 1);
+    return reinterpret_cast<const int8_t *>(a.act + (size_t)t * a.act_stride);
 }
 
 __device__ __forceinline__ void slot16_store(const v4f &mine, float *red) {
@@ -689,9 +807,41 @@ __global__ __launch_bounds__(MMQ_NT) void k_mmq16(MmqSeg s0, MmqSeg s1, MmqSeg s
         // the slot index must be wave-uniform (divergent branches around the MFMAs would run
         // them with a partial EXEC)
         const int k = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-        const int8_t *aq = stage_act16<T>(a, t0, a.K, da);
-        slot16_store(slot16_val<T>(sg.w, row, k, aq, da), red);
-        if constexpr (NV == 2) slot16_store(slot16_val<T>(a.w_up, row, k, aq, da), red + MMQ_NT * 4);
+        if (T == 8 && a.K % 256 == 0) {
+            const int8_t *aq = act16_codes(a, t0);
+            v4f y = {}, u = {};
+            if (a.K <= 2048) {
+                // one pass: every weight / activation / scale load goes out before the
+                // activation scales' staging barrier
+                const int nb = a.K >> 5;
+                Q80Pass qw, qu;
+                v4i x[4];
+                q80p_load(sg.w, row, 0, k, qw);
+                if constexpr (NV == 2) q80p_load(a.w_up, row, 0, k, qu);
+                act_load(aq, a.K, 0, k, x);
+                stage_act16<8>(a, t0, a.K, da);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) swap_halves(x[i]);
+                v4f aw[8], au[8];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) aw[i] = v4f{}, au[i] = v4f{};
+                q80p_acc(qw, x, 0, k, nb, da, aw);
+                y = tree8(aw);
+                if constexpr (NV == 2) {
+                    q80p_acc(qu, x, 0, k, nb, da, au);
+                    u = tree8(au);
+                }
+            } else {
+                stage_act16<8>(a, t0, a.K, da);
+                slot16_q80p<NV>(sg.w, a.w_up, row, k, aq, da, y, u);
+            }
+            slot16_store(y, red);
+            if constexpr (NV == 2) slot16_store(u, red + MMQ_NT * 4);
+        } else {
+            const int8_t *aq = stage_act16<T>(a, t0, a.K, da);
+            slot16_store(slot16_val<T>(sg.w, row, k, aq, da), red);
+            if constexpr (NV == 2) slot16_store(slot16_val<T>(a.w_up, row, k, aq, da), red + MMQ_NT * 4);
+        }
         __syncthreads();
         if (wave != 0) return;
         const v4f y = slot16_sum(red);

@@ -1074,16 +1074,15 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
     static const int mmq_env = getenv("MIO_MMQ") ? atoi(getenv("MIO_MMQ")) : -1;
     const bool mmq_all = mmq_env >= 0 ? mmq_env != 0 : nt > 8;
     // At <= 8 tokens the engine is chosen per launch kind (bit 0 attn_in, 1 attn_out, 2 ffn_in,
-    // 3 ffn_down set = int8 MFMA): q|k|v on the matrix cores, gate|up too for the K-quants,
-    // the O and down matvecs (n_embd rows = 64 tiles of 32 rows: a quarter of the CUs) on
-    // dot4. Eager per-kernel times at 8 tokens (profiles/r03_batch8_mmq_vs_dot4.txt): 1.7B
-    // Q4_K_M gate|up 11.0 vs 25.1 us, q|k|v 6.6-11.8 vs 13.1-13.8, down (Q6_K) 32.5 vs 12.2;
-    // 8-stream steps (graph) 1.7B 1.91 ms with q|k|v + gate|up on MFMA vs 2.22 all dot4; 2.6B
-    // Q8_0 3.04 with q|k|v only, 3.22 adding gate|up, 3.10 all dot4 (profiles/r03_batch8_masks.txt).
+    // 3 ffn_down set = int8 MFMA). r04: the 16x16 MFMA tiles load 16 B per lane (llm_mmq.hip,
+    // swap_halves) and every K-quant matvec runs on the matrix cores (8-stream 1.7B Q4_K_M step
+    // 1.516 ms vs 1.640 with q|k|v + gate|up only and 1.676 before the 16-B loads,
+    // profiles/r04_batch8_mmq16_ab.txt); Q8_0 keeps q|k|v only: its O and down at 8 tokens on
+    // MFMA 2.155 vs 2.074 ms (the dot4 streams read longer runs per row).
     // MIO_MMQ_MASK overrides the set for every type (A/B).
     static const int mmq_mask = getenv("MIO_MMQ_MASK") ? atoi(getenv("MIO_MMQ_MASK")) : -1;
     auto use_mmq = [&](int kind, int type) {
-        const int mask = mmq_mask >= 0 ? mmq_mask : (type == 8 ? 1 : 5);
+        const int mask = mmq_mask >= 0 ? mmq_mask : (type == 8 ? 1 : 15);
         return mmq_all || (nt <= 8 && mmq_env < 0 && ((mask >> kind) & 1));
     };
     const bool mmq = mmq_all;
@@ -1092,12 +1091,12 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
     // dot4 engine, instead of behind a k_bt_quant launch (and, for q|k|v, on the matrix cores).
     // 8-stream steps (graph; profiles/r04_fq_ab.txt): 2.6B Q8_0 2.354 ms with attn_in only,
     // 2.362 both, 2.488 neither or ffn_in only; 1.7B Q4_K_M 1.837 / 1.881 / 1.843 / 1.891
-    // r04 engine A/B (profiles/r04_engine_choice_ab.txt): gate|up in-launch as well is 1% faster
-    // for Q8_0 (2.183 vs 2.202 ms) and 2% slower for K-quants (1.800 vs 1.769): default = attn_in
-    // always, ffn_in for Q8_0 gate|up
+    // r03 engine A/B (profiles/r03s2_engine_choice_ab.txt): gate|up in-launch as well is 1% faster
+    // for Q8_0 (2.183 vs 2.202 ms); default = both in-launch for Q8_0, none for the K-quants
+    // (their matvecs are all on the matrix cores, above)
     static const int fq2_env = getenv("MIO_BT_FQ") ? atoi(getenv("MIO_BT_FQ")) : -1;
     auto fq2 = [&](int kind, int type) {
-        const bool on = fq2_env >= 0 ? ((fq2_env >> kind) & 1) != 0 : (kind == 0 || type == 8);
+        const bool on = fq2_env >= 0 ? ((fq2_env >> kind) & 1) != 0 : type == 8;
         return !mmq && nt <= MW && pick_np(d.n_embd) == 1 && on;
     };
     static const bool att_q_env = !(getenv("MIO_ATT_Q") && getenv("MIO_ATT_Q")[0] == '0');
