@@ -1098,13 +1098,18 @@ void dispatch_nt(int K, int type, F &&f) {
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 
 // One workgroup per (ATT_CHUNK positions, kv head [, token]): a position slot is LP lanes
-// holding 8 dims each; NT = ATT_CHUNK * LP threads (at most 512), so at 32-position chunks
-// every thread owns one position (IT = 1) and the K/V rows of a chunk arrive in one load
-// round trip per lane.
+// holding 8 dims each; NT = ATT_CHUNK * LP threads (at most MIO_ATT_NT), IT positions per
+// slot, and the K/V rows of a chunk arrive in one load round trip per lane.
+// MIO_ATT_NT: threads per attention chunk workgroup at most. 256 (4 positions per slot at
+// 64-position chunks): 0.763-0.766 vs 0.775 ms per token with 512 (profiles/r04_att_nt_ab.txt);
+// 128 would need the merge to cover more than one float4 of outputs per thread at G * hd = 1024
+#ifndef MIO_ATT_NT
+#define MIO_ATT_NT 256
+#endif
 template <int HD>
 struct AttCfg {
     static constexpr int LP = HD / 8;                                        // lanes per slot
-    static constexpr int NT = ATT_CHUNK * LP < 512 ? ATT_CHUNK * LP : 512;   // threads
+    static constexpr int NT = ATT_CHUNK * LP < MIO_ATT_NT ? ATT_CHUNK * LP : MIO_ATT_NT;  // threads
     static constexpr int NW = NT / 64;                                       // waves
     static constexpr int NS = NT / LP;                                       // position slots
     static constexpr int IT = ATT_CHUNK / NS;                                // positions per slot
