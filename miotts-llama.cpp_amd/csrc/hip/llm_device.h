@@ -1427,22 +1427,27 @@ __device__ void attn_merge_last(const float *part, uint32_t head0, uint32_t g_st
     }
     __syncthreads();
     if (!last_) return;
-    static_assert(G * HD <= 4 * NT, "one float4 of outputs per thread");
-    const int e = 4 * (int)MIO_TIDX;
-    float4 y = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (e < G * HD) {
-        const int g = e / HD, dd = e - g * HD;
-        y = merge_out4(part, head0 + (uint32_t)g * g_stride, nch, REC, HD, dd);
-        *reinterpret_cast<float4 *>(out + e) = y;
-    }
-    if (ak >= 0) {
-        const int wave = __builtin_amdgcn_readfirstlane(MIO_TIDX >> 6), lane = MIO_TIDX & 63;
-        if (wave * 256 < G * HD) {
-            const float vv[4] = {y.x, y.y, y.z, y.w};
-            if (ak == 1)
-                q8k_store(vv, abs_max4(vv), blk0 + wave, rec);
-            else
-                q80_store(vv, blk0 + wave * 8 + (lane >> 3), e < G * HD, rec);
+    // one float4 of outputs per thread and pass (G * hd > 4 NT: several passes); in pass b,
+    // wave w holds outputs 4 NT b + 256 w .. + 255 (one Q8_K superblock / eight Q8_0 blocks)
+#pragma unroll
+    for (int b = 0; b < (G * HD + 4 * NT - 1) / (4 * NT); ++b) {
+        const int e = 4 * NT * b + 4 * (int)MIO_TIDX;
+        float4 y = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (e < G * HD) {
+            const int g = e / HD, dd = e - g * HD;
+            y = merge_out4(part, head0 + (uint32_t)g * g_stride, nch, REC, HD, dd);
+            *reinterpret_cast<float4 *>(out + e) = y;
+        }
+        if (ak >= 0) {
+            const int wave = __builtin_amdgcn_readfirstlane(MIO_TIDX >> 6), lane = MIO_TIDX & 63;
+            const int sb = (4 * NT * b) / 256 + wave;
+            if (sb * 256 < G * HD) {
+                const float vv[4] = {y.x, y.y, y.z, y.w};
+                if (ak == 1)
+                    q8k_store(vv, abs_max4(vv), blk0 + sb, rec);
+                else
+                    q80_store(vv, blk0 + sb * 8 + (lane >> 3), e < G * HD, rec);
+            }
         }
     }
 }
