@@ -793,7 +793,10 @@ __device__ __forceinline__ v4f slot16_sum(const float *red) {
     return t.result;
 }
 
-template <int T0, int T1, int T2, int MODE>
+// KP: the launch is Q8_0 with K % 256 == 0 and (1) K <= 2048 or (2) K > 2048 (host-checked),
+// so only that pair path is compiled into it: the generic kernel (KP 0) carries three Q8_0
+// paths, and its size alone cost the 2.6B gate|up launch 19.2 vs 14.4 us
+template <int T0, int T1, int T2, int MODE, int KP = 0>
 __global__ __launch_bounds__(MMQ_NT) void k_mmq16(MmqSeg s0, MmqSeg s1, MmqSeg s2, MmqArgs a) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     constexpr int NV = MODE == MMQ_SWIGLU ? 2 : 1;
@@ -807,10 +810,10 @@ __global__ __launch_bounds__(MMQ_NT) void k_mmq16(MmqSeg s0, MmqSeg s1, MmqSeg s
         // the slot index must be wave-uniform (divergent branches around the MFMAs would run
         // them with a partial EXEC)
         const int k = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-        if (T == 8 && a.K % 256 == 0) {
+        if (T == 8 && (KP != 0 || a.K % 256 == 0)) {
             const int8_t *aq = act16_codes(a, t0);
             v4f y = {}, u = {};
-            if (a.K <= 2048) {
+            if (KP == 1 || (KP == 0 && a.K <= 2048)) {
                 // one pass: every weight / activation / scale load goes out before the
                 // activation scales' staging barrier
                 const int nb = a.K >> 5;
@@ -919,12 +922,19 @@ void launch_mmq(const MmqSeg *seg, const int *types, int nseg, int mode, const M
             hipLaunchKernelGGL(kern, grid, dim3(MMQ_NT), lds, s, sg[0], sg[1], sg[2], a);
         };
         if (t16) {
+            const bool q8 = A == 8 && (B < 0 || B == 8) && (C < 0 || C == 8) && a.K % 256 == 0;
+            const int kp = q8 ? (a.K <= 2048 ? 1 : 2) : 0;
+            auto kpl = [&]<int M>() {
+                if (kp == 1) launch(k_mmq16<A, B, C, M, 1>);
+                else if (kp == 2) launch(k_mmq16<A, B, C, M, 2>);
+                else launch(k_mmq16<A, B, C, M, 0>);
+            };
             if (mode == MMQ_STORE)
-                launch(k_mmq16<A, B, C, MMQ_STORE>);
+                kpl.template operator()<MMQ_STORE>();
             else if (mode == MMQ_RESID)
-                launch(k_mmq16<A, B, C, MMQ_RESID>);
+                kpl.template operator()<MMQ_RESID>();
             else
-                launch(k_mmq16<A, B, C, MMQ_SWIGLU>);
+                kpl.template operator()<MMQ_SWIGLU>();
             return;
         }
         if (mode == MMQ_STORE)

@@ -1077,12 +1077,14 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
     // 3 ffn_down set = int8 MFMA). r04: the 16x16 MFMA tiles load 16 B per lane (llm_mmq.hip,
     // swap_halves) and every K-quant matvec runs on the matrix cores (8-stream 1.7B Q4_K_M step
     // 1.516 ms vs 1.640 with q|k|v + gate|up only and 1.676 before the 16-B loads,
-    // profiles/r04_batch8_mmq16_ab.txt); Q8_0 keeps q|k|v only: its O and down at 8 tokens on
-    // MFMA 2.155 vs 2.074 ms (the dot4 streams read longer runs per row).
+    // profiles/r04_batch8_mmq16_ab.txt); Q8_0 (one-pass kernels compiled with the pair path
+    // alone, k_mmq16 P1): O and gate|up on MFMA too, q|k|v on the dot4 engine quantizing in the
+    // launch, down on dot4 (2.6B 8-stream step 2.026 ms vs 2.059 with q|k|v only, 2.061 adding
+    // down).
     // MIO_MMQ_MASK overrides the set for every type (A/B).
     static const int mmq_mask = getenv("MIO_MMQ_MASK") ? atoi(getenv("MIO_MMQ_MASK")) : -1;
     auto use_mmq = [&](int kind, int type) {
-        const int mask = mmq_mask >= 0 ? mmq_mask : (type == 8 ? 1 : 15);
+        const int mask = mmq_mask >= 0 ? mmq_mask : (type == 8 ? 7 : 15);
         return mmq_all || (nt <= 8 && mmq_env < 0 && ((mask >> kind) & 1));
     };
     const bool mmq = mmq_all;
@@ -1091,12 +1093,11 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
     // dot4 engine, instead of behind a k_bt_quant launch (and, for q|k|v, on the matrix cores).
     // 8-stream steps (graph; profiles/r04_fq_ab.txt): 2.6B Q8_0 2.354 ms with attn_in only,
     // 2.362 both, 2.488 neither or ffn_in only; 1.7B Q4_K_M 1.837 / 1.881 / 1.843 / 1.891
-    // r03 engine A/B (profiles/r03s2_engine_choice_ab.txt): gate|up in-launch as well is 1% faster
-    // for Q8_0 (2.183 vs 2.202 ms); default = both in-launch for Q8_0, none for the K-quants
-    // (their matvecs are all on the matrix cores, above)
+    // default: attn_in in-launch for Q8_0 (its gate|up runs on the matrix cores, above), none for
+    // the K-quants (every matvec on the matrix cores)
     static const int fq2_env = getenv("MIO_BT_FQ") ? atoi(getenv("MIO_BT_FQ")) : -1;
     auto fq2 = [&](int kind, int type) {
-        const bool on = fq2_env >= 0 ? ((fq2_env >> kind) & 1) != 0 : type == 8;
+        const bool on = fq2_env >= 0 ? ((fq2_env >> kind) & 1) != 0 : (type == 8 && kind == 0);
         return !mmq && nt <= MW && pick_np(d.n_embd) == 1 && on;
     };
     static const bool att_q_env = !(getenv("MIO_ATT_Q") && getenv("MIO_ATT_Q")[0] == '0');
