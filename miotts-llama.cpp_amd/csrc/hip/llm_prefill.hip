@@ -1084,7 +1084,10 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
     // MIO_MMQ_MASK overrides the set for every type (A/B).
     static const int mmq_mask = getenv("MIO_MMQ_MASK") ? atoi(getenv("MIO_MMQ_MASK")) : -1;
     auto use_mmq = [&](int kind, int type) {
-        const int mask = mmq_mask >= 0 ? mmq_mask : (type == 8 ? 7 : 15);
+        // Q8_0 O and gate|up only where their 16-B pair kernels apply (K % 256 == 0, one pass)
+        const bool q8_pair = d.n_embd % 256 == 0 && d.n_embd <= 2048 && (d.n_head * d.hd) % 256 == 0 &&
+                             d.n_head * d.hd <= 2048;
+        const int mask = mmq_mask >= 0 ? mmq_mask : (type == 8 ? (q8_pair ? 7 : 1) : 15);
         return mmq_all || (nt <= 8 && mmq_env < 0 && ((mask >> kind) & 1));
     };
     const bool mmq = mmq_all;
@@ -1097,7 +1100,8 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
     // the K-quants (every matvec on the matrix cores)
     static const int fq2_env = getenv("MIO_BT_FQ") ? atoi(getenv("MIO_BT_FQ")) : -1;
     auto fq2 = [&](int kind, int type) {
-        const bool on = fq2_env >= 0 ? ((fq2_env >> kind) & 1) != 0 : (type == 8 && kind == 0);
+        const bool q8_pair = d.n_embd % 256 == 0 && d.n_embd <= 2048;
+        const bool on = fq2_env >= 0 ? ((fq2_env >> kind) & 1) != 0 : (type == 8 && (kind == 0 || !q8_pair));
         return !mmq && nt <= MW && pick_np(d.n_embd) == 1 && on;
     };
     static const bool att_q_env = !(getenv("MIO_ATT_Q") && getenv("MIO_ATT_Q")[0] == '0');
