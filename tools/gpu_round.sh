@@ -1,7 +1,9 @@
 # One GPU-box pass: GPU tests, the default bench line (with the CPU baseline), the eager
 # bench under rocprofv3 kernel trace + stats (graph replays crash rocprofiler-sdk 7.2's
 # queue intercept), and the two PMC passes at decode position ~400.
-# Outputs under gpurun_out/$TAG/.   usage: bash tools/gpu_round.sh TAG [skip-tests]
+# With "configs" as the third argument, also smoke() and the BASELINE config lines C2 (0.1B
+# Q8_0), C4 (2.6B Q8_0, 8 utterances per GPU) and C5 (stream benchmark, 3 runs).
+# Outputs under gpurun_out/$TAG/.   usage: bash tools/gpu_round.sh TAG [skip-tests|tests] [configs]
 set -e
 tag=${1:-run}
 out=gpurun_out/$tag
@@ -18,4 +20,10 @@ MIO_NO_GRAPH=1 timeout -k 10 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --out
 MIO_NO_GRAPH=1 timeout -k 10 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $out/pmc -o write -- python3 tools/pmc_run.py > $out/pmc_write.out 2>&1
 python3 tools/pmc_traffic.py $(find $out/pmc -name 'fetch_counter_collection.csv') $(find $out/pmc -name 'write_counter_collection.csv') 3 > $out/pmc_traffic.json
 find $out/pmc -name '*kernel_trace.csv' -delete
+if [ "$3" = "configs" ]; then
+  timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $out/smoke.txt 2>&1
+  timeout -k 10 400 python -u bench.py --preset 2 --no-cpu-baseline > $out/c2.json 2> $out/c2.err
+  timeout -k 10 400 python -u bench.py --preset 4 --utts-per-gpu 8 --no-cpu-baseline --batch 0 > $out/c4.json 2> $out/c4.err
+  AB_K=3 timeout -k 10 400 python -u tools/stream_ab.py > $out/c5.json 2> $out/c5.err
+fi
 echo done
