@@ -506,6 +506,23 @@ __global__ __launch_bounds__(MT) void k_bt_quant(LlmDims d, const float *src, in
         plain_quant(xr, K, kq != 0, s);
 }
 
+// MODE 1 (plain rows, K % 256 == 0) split over 2048-element chunks: grid (nt, chunks). Q8_K
+// superblocks / Q8_0 blocks are quantized independently of each other, so each chunk
+// workgroup's records are k_bt_quant's bits (quant_regs: thread tid of chunk c holds elements
+// c * 2048 + 4 tid .. + 3, i.e. wave w holds superblock 8 c + w / blocks 64 c + 8 w ..).
+__global__ __launch_bounds__(MT) void k_bt_quant_split(const float *src, int K, int kq, PrefillBuffers pb) {
+    const int t = blockIdx.x, c = blockIdx.y;
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (c * 2048 + wave * 256 >= K) return;  // wave-uniform
+    const ActL a = carve_t(pb.act, K, t).a;
+    const float4 x = *reinterpret_cast<const float4 *>(src + (size_t)t * K + c * 2048 + 4 * (int)threadIdx.x);
+    const float v[4] = {x.x, x.y, x.z, x.w};
+    if (kq)
+        q8k_store(v, abs_max4(v), c * 8 + wave, a);
+    else
+        q80_store(v, c * 64 + wave * 8 + (lane >> 3), true, a);
+}
+
 // lfm2 short-conv layer, one workgroup per token t: the gated conv of t (conv_load /
 // conv_quant, the decode step's prologue) quantized into t's act record. Window inputs of
 // positions pos - 1, pos - 2: the bcx rows of the tokens before t in this launch when they are
@@ -1027,6 +1044,13 @@ PrefillBuffers shifted(const LlmDims &d, const PrefillBuffers &pb, int t, int K)
 // act records of nt tokens (k_bt_quant): mode 0 RMSNorm(src) * w, 1 src
 void launch_quant(const LlmDims &d, int mode, const float *src, int K, const float *w, bool kq,
                   const PrefillBuffers &pb, int nt, hipStream_t s) {
+    // plain rows: one workgroup per (token, 2048 elements) instead of per token (MIO_QSPLIT=0:
+    // per token, for A/B)
+    static const bool qsplit = !(getenv("MIO_QSPLIT") && getenv("MIO_QSPLIT")[0] == '0');
+    if (mode == 1 && qsplit && K % 256 == 0) {
+        hipLaunchKernelGGL(k_bt_quant_split, dim3(nt, (K + 2047) / 2048), dim3(MT), 0, s, src, K, (int)kq, pb);
+        return;
+    }
     const int np = pick_np(K);
     auto go = [&]<int NP>() {
         const size_t lds = smem_bytes(K);
