@@ -66,6 +66,7 @@ def parse_args(argv=None):
     p.add_argument("--workdir", default=os.environ.get("MIOTTS_BENCH_DIR", "/tmp/miotts_bench"))
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-tokens", type=int, default=64)
+    p.add_argument("--no-cpu-c1", action="store_true", help="skip the C1 leg (0.1B Q8_0 CPU utterance)")
     p.add_argument("--cpu-codes", type=int, default=40)
     p.add_argument("--batch", type=int, default=8,
                    help="also time B utterances decoded together per GPU (N=1 only; 0 = skip)")
@@ -165,6 +166,62 @@ def cpu_baseline(llm_path, codec_path, voice_path, n_tok, n_codes, utt_tokens, t
             "sample": f"oracle decode of {n_tok} tokens at positions 0..{utt_tokens - 1} "
                       f"({t_tok * 1e3:.1f} ms/token) + codec+iSTFT of {n_codes} codes "
                       f"({t_code * 1e3:.2f} ms/code), extrapolated to {utt_tokens} tokens"}
+
+
+def cpu_baseline_c1(workdir, tokens, threads):
+    """BASELINE configs[0] (C1: MioTTS-0.1B Q8_0, the CPU path of miotts-stream-benchmark,
+    stream-benchmark.cpp:148-166): one whole utterance through the C oracle ("port"; the
+    reference's own CPU path needs the absent ggml) on `threads` OpenMP threads,
+    NOT extrapolated: the chat-template prompt prefilled token by token, `tokens` sampled speech
+    tokens, MioCodec + iSTFT of the codes, timed end to end (tools/cpu_full.py's run)."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import numpy as np
+    import miotts_amd as m
+    import pyoracle
+    llm_path, codec_path, voice_path = ensure_files(workdir, 2, 0, lambda: None)
+    prompt = prompt_tokens(PROMPT)
+    allow = (m.SYNTH_SPEECH0, m.SYNTH_SPEECH0 + 12800)
+    prev = pyoracle.set_threads(threads)
+    try:
+        o = pyoracle.Llm(llm_path, len(prompt) + tokens + 8)
+        c = pyoracle.Codec(codec_path)
+        emb = m.read_voice(voice_path)
+        o.eval(prompt[0], 0)  # page the weights in (not timed)
+        o.reset()
+        t0 = time.perf_counter()
+        ids = o.generate(prompt, tokens, 0.8, 42, allow=allow)
+        t1 = time.perf_counter()
+        pcm = c.decode_pcm(np.asarray(ids, np.int64) - m.SYNTH_SPEECH0, emb)
+        t2 = time.perf_counter()
+    finally:
+        pyoracle.set_threads(prev)
+    audio = pcm.size / 44100.0
+    return {"value": round(audio / (t2 - t0), 4), "unit": "x realtime (audio s / wall s)", "cores": threads,
+            "kind": "port", "model": PRESETS[2], "tokens": len(ids), "prompt_tokens": len(prompt),
+            "llm_s": round(t1 - t0, 3), "codec_istft_s": round(t2 - t1, 3), "wall_s": round(t2 - t0, 3),
+            "sample": f"one whole utterance, not extrapolated: {len(prompt)}-token prompt + {len(ids)} tokens "
+                      f"+ codec/iSTFT of {len(ids)} codes ({audio:.1f} s audio)"}
+
+
+def eos_tail(llm, prompt, tokens_per_step_us):
+    """Cost of the decode steps queued past an end token (test-to-speech.cpp:168-170 breaks
+    before the next llama_decode): an EOS-ending run (1 in 4 allowed ids is the end token,
+    temperature 2), then mio_hip_llm_tail: steps issued after the end token and the GPU time of
+    the whole check intervals queued behind the poll that found it."""
+    import miotts_amd as m
+    for seed in range(11, 40):
+        toks = llm.generate(prompt, 400, 2.0, seed, allow=(m.SYNTH_EOT, m.SYNTH_SPEECH0 + 3),
+                            eos=(m.SYNTH_EOT, m.SYNTH_IM_END), check_interval=32)
+        wasted, timed, ms = llm.tail()
+        if timed:
+            break
+    r = {"tokens_before_eos": len(toks), "steps_after_eos": wasted, "timed_steps": timed,
+         "timed_ms": round(ms, 3), "check_interval": 32}
+    if timed:
+        r["us_per_step_after_eos"] = round(ms * 1e3 / timed, 2)
+        r["us_per_step_decoding"] = round(tokens_per_step_us, 2)
+        r["launches_per_step"] = len(llm.step_kinds())
+    return r
 
 
 def batched_line(a, llm, codec, dev, prompt, allow, d_emb, d_pcm):
@@ -443,6 +500,9 @@ def main():
         # position of the PMC passes (tools/pmc_run.py)
         llm.generate(prompt, max(1, ROOF_POS + 2 - len(prompt)), 0.8, 7, allow=allow, check_interval=1000)
         roof = roofline(llm, a.preset)
+    tail = None
+    if rank == 0 and B == 1 and stage["llm_ms"] > 0:
+        tail = eos_tail(llm, prompt, stage["llm_ms"] / utt_per_rank / a.tokens * 1e3)
 
     steps_total = utt_per_rank
     model = PRESETS[a.preset]
@@ -474,6 +534,7 @@ def main():
         "roofline": roof,
         "value_pcie_inclusive": round(value_pcie, 3),
         "cpu_baseline": None,
+        "eos_tail": tail,
     }
     if codec_flops and stage["codec_ms"] > 0:
         out["codec_roofline"] = codec_roofline(sum(codec_flops) / len(codec_flops), stage["codec_ms"] / steps_total,
@@ -498,6 +559,8 @@ def main():
                                            share)
         out["cpu_baseline_4_threads"] = cpu_baseline(llm_path, codec_path, voice_path, max(16, a.cpu_tokens // 4),
                                                      a.cpu_codes // 2, a.tokens, 4)
+        if not a.no_cpu_c1:
+            out["cpu_baseline_c1"] = cpu_baseline_c1(a.workdir, a.tokens, share)
     if rank == 0:
         print(json.dumps(out, ensure_ascii=False), flush=True)
     if dist is not None:

@@ -206,6 +206,13 @@ int mio_hip_llm_load_ms(const mio_hip_llm *m, double *ms);
  * (the rest of the end token's interval plus one more: < 2 * check_interval; 0 when it stops
  * at max_tokens). */
 int mio_hip_llm_steps_issued(const mio_hip_llm *m, int *steps);
+/* Cost of those steps after the last mio_hip_llm_generate that stopped at an end token
+ * (test-to-speech.cpp:168-170 decodes nothing after it): every decode launch after the end
+ * token returns at entry (StepState.done), so such a step costs about its launch boundaries.
+ * *steps = steps issued after the end token's step (0 when the run stopped at max_tokens);
+ * *timed_steps / *timed_ms = the whole check intervals queued behind the poll that found it and
+ * their GPU time (HIP events; 0 when none was queued). */
+int mio_hip_llm_tail(const mio_hip_llm *m, int *steps, int *timed_steps, float *timed_ms);
 /* Allocates now the device memory decodes of up to n_codes codes need (workspace, RoPE
  * table, incremental prenet cache), as miocodec_load's graph-allocator reserve
  * (miocodec.cpp:424-516); later decodes of at most n_codes allocate nothing. */

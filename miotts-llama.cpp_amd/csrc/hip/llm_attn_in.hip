@@ -30,13 +30,17 @@ __global__ __launch_bounds__(MT) void k_attn_in(LlmDims d, const float *norm_w, 
     MIO_TL_BEGIN(b);
     int pend = 0, step = 0;
     if constexpr (FS) {
+        // after an end token every decode launch returns at entry (test-to-speech.cpp:168-170
+        // breaks before the next llama_decode); layer 0 reads the flag with pending / step
         pend = b.st->pending;
         step = b.st->step;
+        if (b.st->done) return;
     }
     XRegs<NP> xr;
     load_x(pend ? nullptr : b.x, norm_w, K, xr);
     x_gate();
-    auto sample_prologue = [&]() {
+    // returns true when the sampled token ends generation (the rest of the step is skipped)
+    auto sample_prologue = [&]() -> bool {
         if constexpr (FS) {
             if (pend) {
                 const SampleCfg sc = *b.cfg;
@@ -54,8 +58,10 @@ __global__ __launch_bounds__(MT) void k_attn_in(LlmDims d, const float *norm_w, 
                         b.st->token = tok;
                     }
                 }
+                return tok == sc.eos0 || tok == sc.eos1;
             }
         }
+        return false;
     };
     auto put = [&](int row, float v) {
         if ((threadIdx.x & 63) == 0) b.qkv[row] = v;
@@ -65,8 +71,9 @@ __global__ __launch_bounds__(MT) void k_attn_in(LlmDims d, const float *norm_w, 
     if ((int)blockIdx.x < g_qk) {
         wave_range(o2, lo, hi, blockIdx.x, g_qk);
         load_first<TQ, NP, 1, SU, MIO_SMALL_AUX>(wq, wk, lo, hi, ga, gb, o1);
-        sample_prologue();
+        if (sample_prologue()) return;
         x_after_weights(xr);
+        if (!FS && step_done(b)) return;
         MIO_TRACE(b, 1);
         MIO_TL_MARK1(b);
         rmsnorm_quant(xr, K, d.eps, akind(TQ), s, MIO_TL_DIAGSLOT(b));
@@ -81,8 +88,9 @@ __global__ __launch_bounds__(MT) void k_attn_in(LlmDims d, const float *norm_w, 
         const int bv = (int)blockIdx.x - g_qk, gv = GW - g_qk;
         wave_range(wv.rows, lo, hi, bv, gv);
         load_first<TV, NP, 1, SU, MIO_SMALL_AUX>(wv, wv, lo, hi, ga, gb);
-        sample_prologue();
+        if (sample_prologue()) return;
         x_after_weights(xr);
+        if (!FS && step_done(b)) return;
         rmsnorm_quant(xr, K, d.eps, akind(TV), s, MIO_TL_DIAGSLOT(b));
         stream_rows<TV, NP, 1, SU, MIO_SMALL_AUX>(wv, wv, lo, hi, ga, gb, s.a, [&](int row, float v, float) {
             put(o2 + row, v);

@@ -1029,6 +1029,16 @@ __device__ __forceinline__ int cur_pos(const StepState *st, const LlmDims &d) {
     return min(st->pos + st->pending, d.n_ctx - 1);
 }
 
+// An end token was sampled: the rest of the step and every later step return at entry (the
+// reference breaks before the next llama_decode, test-to-speech.cpp:168-170). The matvec
+// launches read the flag behind their first weight group and x, so its scalar round trip
+// overlaps theirs instead of holding the weight stream back.
+template <class B>
+__device__ __forceinline__ bool step_done(const B &b) {
+    asm volatile("" ::: "memory");
+    return b.st->done != 0;
+}
+
 // The pending sample's token: Gumbel-max winner (ties -> lowest id) over the lm_head
 // workgroups' partials {smp[2i] value, smp[2i+1] id bits}, sc.lo when no id was allowed, the
 // forced token of this step if any. Whole workgroup of NTH threads (multiple of 64, <= 1024);

@@ -71,6 +71,7 @@ __global__ __launch_bounds__(MT) void k_attn_out(LlmDims d, QMat wo, LlmBuffers 
     Frag ga[Cfg<NP, SU>::U], gb[Cfg<NP, SU>::U];
     load_first<T, NP, 1, SU, MIO_SMALL_AUX>(wo, wo, lo, hi, ga, gb);
     x_after_weights(xr);
+    if (step_done(b)) return;
     MIO_TRACE(b, 1);
     MIO_TL_MARK1(b);
     plain_quant(xr, K, akind(T), s, MIO_TL_DIAGSLOT(b));
@@ -109,6 +110,7 @@ __global__ __launch_bounds__(MT) void k_conv_out(LlmDims d, QMat wo, const float
     Frag ga[Cfg<NP, SU>::U], gb[Cfg<NP, SU>::U];
     load_first<T, NP, 1, SU>(wo, wo, lo, hi, ga, gb);
     conv_after_weights(cr);
+    if (step_done(b)) return;
     MIO_TRACE(b, 1);
     MIO_TL_MARK1(b);
     conv_quant(cr, K, akind(T), s, blockIdx.x == 0 ? ring + (size_t)(pos & (kConvSlots - 1)) * K : nullptr,
@@ -124,6 +126,13 @@ __global__ __launch_bounds__(MT) void k_conv_out(LlmDims d, QMat wo, const float
 }
 
 // adv (layer 0): folds a sampled-in-attn_in token into pos / step (StepState.pending).
+__device__ __forceinline__ void advance_state(StepState *st, const LlmDims &d) {
+    const int p = st->pending;
+    st->pos = min(st->pos + p, d.n_ctx - 1);
+    st->step = st->step + p;
+    st->pending = 0;
+}
+
 template <int NP, int T, int SU, bool DG>
 __global__ __launch_bounds__(MT) void k_ffn_in(LlmDims d, const float *norm_w, QMat gate, QMat up,
                                                LlmBuffers b, int adv) {
@@ -141,6 +150,10 @@ __global__ __launch_bounds__(MT) void k_ffn_in(LlmDims d, const float *norm_w, Q
     Frag ga[Cfg<NP, SU>::U], gb[Cfg<NP, SU>::U];
     load_first<T, NP, 2, SU>(gate, up, lo, hi, ga, gb);
     x_after_weights(xr);
+    if (step_done(b)) {  // layer 0 still folds the end token's step (the host counts it)
+        if (adv && blockIdx.x == 0 && MIO_TIDX == 0) advance_state(b.st, d);
+        return;
+    }
     MIO_TRACE(b, 1);
     MIO_TL_MARK1(b);
     rmsnorm_quant(xr, K, d.eps, akind(T), s, MIO_TL_DIAGSLOT(b));
@@ -149,13 +162,7 @@ __global__ __launch_bounds__(MT) void k_ffn_in(LlmDims d, const float *norm_w, Q
     stream_rows<T, NP, 2, SU>(gate, up, lo, hi, ga, gb, s.a, [&](int row, float g, float u) {
         if ((threadIdx.x & 63) == 0) b.h[row] = silu_f(g) * u;
     }, INT_MAX, DG ? b.trace : nullptr);
-    if (adv && blockIdx.x == 0 && MIO_TIDX == 0) {
-        StepState *st = b.st;
-        const int p = st->pending;
-        st->pos = min(st->pos + p, d.n_ctx - 1);
-        st->step = st->step + p;
-        st->pending = 0;
-    }
+    if (adv && blockIdx.x == 0 && MIO_TIDX == 0) advance_state(b.st, d);
     MIO_TL_END(b);
     MIO_TRACE(b, 15);
 }
@@ -177,6 +184,7 @@ __global__ __launch_bounds__(MT) void k_ffn_down(LlmDims d, QMat down, LlmBuffer
     Frag ga[Cfg<NP, SU>::U], gb[Cfg<NP, SU>::U];
     load_first<T, NP, 1, SU>(down, down, lo, hi, ga, gb);
     x_after_weights(xr);
+    if (step_done(b)) return;
     MIO_TRACE(b, 1);
     MIO_TL_MARK1(b);
     plain_quant(xr, K, akind(T), s, MIO_TL_DIAGSLOT(b));
@@ -216,6 +224,7 @@ __global__ __launch_bounds__(MT) void k_lm_head(LlmDims d, const float *norm_w, 
     asm volatile("" ::: "memory");
     const SampleCfg sc = *b.cfg;
     const int step = b.st->step;
+    if (b.st->done) return;  // no pending sample: the next step's attn_in returns too
     MIO_TRACE(b, 1);
     MIO_TL_MARK1(b);
     rmsnorm_quant(xr, K, d.eps, akind(T), s, MIO_TL_DIAGSLOT(b));
@@ -291,7 +300,7 @@ __global__ __launch_bounds__(AttCfg<HD>::NT) void k_attention(LlmDims d, const f
                  "s"(b.part), "s"(d.max_splits), "s"(bqkv), "s"(b.att), "s"(b.att_cnt));
     const int pos = cur_pos(b.st, d);
     const int t0 = ch * ATT_CHUNK;
-    if (t0 > pos) return;
+    if (t0 > pos || b.st->done) return;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const float2 *rope = b.rope + (size_t)pos * (HD / 2);
     // K/V rows of this slot first (row `pos` is never consumed from the cache)

@@ -701,7 +701,10 @@ __global__ __launch_bounds__(AttCfg<HD>::NT) void k_pf_attention(LlmDims d, cons
     const int kvh = blockIdx.x % d.n_kv, t = blockIdx.x / d.n_kv, ch = blockIdx.y;
     const int pos = pb.pos[t * pb.pos_stride];
     const int t0 = ch * ATT_CHUNK;
-    if (t0 > pos) return;
+    // a stream that sampled its end token is frozen (k_bt_sample): its attention is skipped
+    // (pb.pos points at StepState.pos of each stream in the batched decode)
+    static_assert(offsetof(StepState, done) - offsetof(StepState, pos) == 3 * sizeof(int), "StepState layout");
+    if (t0 > pos || pb.pos[t * pb.pos_stride + 3]) return;
     const size_t kvo = (size_t)pb.seq[t * pb.seq_stride] * pb.seq_kv + (size_t)kvh * d.n_ctx * HD;
     h8 kr[C::IT], vr[C::IT];
     load_kv_rows<HD>(kc + kvo, vc + kvo, t0, pos, kr, vr);
@@ -914,8 +917,8 @@ __global__ __launch_bounds__(MT) void k_bt_lm_head(LlmDims d, const float *norm_
 
 // One workgroup per stream b: the lm_head partials -> the sampled token (k_sample's
 // selection rule), the token ring, end-token flag, the next embedding into pb.x[b], and the
-// state advance. A stream whose step budget (cfg.max_steps) is spent is frozen: nothing is
-// recorded and its position no longer advances.
+// state advance. A stream whose step budget (cfg.max_steps) is spent, or that sampled an end
+// token, is frozen: nothing is recorded and its position no longer advances.
 __global__ __launch_bounds__(ST) void k_bt_sample(LlmDims d, QMat emb, int nblk, PrefillBuffers pb,
                                                   BatchBuffers bb) {
     __shared__ float bs_[ST / 64];
@@ -951,7 +954,9 @@ __global__ __launch_bounds__(ST) void k_bt_sample(LlmDims d, QMat emb, int nblk,
     }
     lds_barrier();
     const int tok = tok_s;
-    const bool live = step < sc.max_steps;
+    // a stream whose step budget is spent or that sampled its end token stays frozen
+    // (test-to-speech.cpp:168-170: the reference decodes nothing after the end token)
+    const bool live = step < sc.max_steps && !st->done;
     if (live) embed_row(emb, tok, d.n_embd, pb.x + (size_t)t * d.n_embd);
     if (tid == 0 && live) {
         sc.out_tokens[step] = tok;

@@ -84,6 +84,11 @@ struct mio_hip_llm {
     static constexpr int kSnaps = 2;
     Snap snaps[kSnaps];
     int snap_head = 0, snap_n = 0;  // oldest outstanding snapshot, number outstanding
+    // steps run after the end token of the last generate (mio_hip_llm_tail): slot of the
+    // snapshot whose poll found it (-1: none), steps issued in total after it, and the GPU
+    // time of the whole intervals queued behind that snapshot
+    int eos_snap = -1, tail_steps = 0, tail_timed_steps = 0;
+    float tail_ms = 0.0f;
 
     ~mio_hip_llm() {
         if (d) hipSetDevice(d->dev);
@@ -397,8 +402,9 @@ int prefill(mio_hip_llm *m, int n) {
 }
 
 // The attention chunk tickets (attn_merge_last) are zeroed in stream order before every
-// prefill and every decode start (the last chunk workgroup of each attention launch resets
-// its ticket, so they are 0 here anyway; this keeps an interrupted run from carrying a count).
+// prefill, every decode start and every batched generate (the last chunk workgroup of each
+// attention launch resets its ticket, so they are 0 here anyway; this keeps an interrupted
+// run from carrying a count).
 int reset_tickets(mio_hip_llm *m) {
     MIO_HIP_CHECK(hipMemsetAsync(m->buf.att_cnt, 0, (size_t)m->dims.n_kv * sizeof(int), m->d->stream));
     MIO_HIP_CHECK(hipMemsetAsync(m->pf.att_cnt, 0, (size_t)mio::kPrefillB * m->dims.n_kv * sizeof(int), m->d->stream));
@@ -521,7 +527,8 @@ int llm_poll(mio_hip_llm *m, std::vector<int32_t> &out, bool *done) {
     if (rc) return rc;
     if (m->snap_n == 0 && (rc = snap_push(m))) return rc;
     // the oldest outstanding snapshot: steps enqueued after it keep the GPU busy meanwhile
-    const mio_hip_llm::Snap &sn = m->snaps[m->snap_head];
+    const int slot = m->snap_head;
+    const mio_hip_llm::Snap &sn = m->snaps[slot];
     MIO_HIP_CHECK(hipEventSynchronize(sn.ev));
     m->snap_head = (m->snap_head + 1) % mio_hip_llm::kSnaps;
     --m->snap_n;
@@ -534,6 +541,7 @@ int llm_poll(mio_hip_llm *m, std::vector<int32_t> &out, bool *done) {
         if (out[i] == m->cfg.eos0 || out[i] == m->cfg.eos1) {
             out.resize(i);  // the reference stops before appending the end token (:168-170)
             d = true;
+            m->eos_snap = slot;
             break;
         }
     if (done) *done = d || sn.issued >= m->steps_total;
@@ -796,7 +804,7 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
     for (mio_hip_llm::Snap &sn : m->snaps)
         if (hipHostMalloc((void **)&sn.st, sizeof(mio::StepState), hipHostMallocDefault) != hipSuccess ||
             hipHostMalloc((void **)&sn.tok, (size_t)m->max_steps * 4, hipHostMallocDefault) != hipSuccess ||
-            hipEventCreateWithFlags(&sn.ev, hipEventDisableTiming) != hipSuccess) {
+            hipEventCreate(&sn.ev) != hipSuccess) {
             mio::set_error("llm_load: pinned host buffers / events failed");
             return fail(MIO_ERR_OOM);
         }
@@ -1003,6 +1011,12 @@ extern "C" int mio_hip_llm_kv_rows(mio_hip_llm *m, int il, int n_pos, uint16_t *
     return MIO_OK;
 }
 
+extern "C" int mio_hip_llm_tail(const mio_hip_llm *m, int *steps, int *timed_steps, float *timed_ms) {
+    MIO_REQUIRE(m && steps && timed_steps && timed_ms, MIO_ERR_INVALID, "llm_tail: null argument");
+    *steps = m->tail_steps, *timed_steps = m->tail_timed_steps, *timed_ms = m->tail_ms;
+    return MIO_OK;
+}
+
 extern "C" int mio_hip_llm_generate(mio_hip_llm *m, const int32_t *prompt, int n_prompt, int max_tokens,
                                     float temperature, uint64_t seed, int32_t allow_lo, int32_t allow_hi,
                                     int32_t eos0, int32_t eos1, int32_t check_interval, int32_t *out_tokens,
@@ -1022,10 +1036,24 @@ extern "C" int mio_hip_llm_generate(mio_hip_llm *m, const int32_t *prompt, int n
     // enqueued before the previous one is checked: the GPU never waits for the host; after
     // an end token the rest of its interval and one more run for nothing (their tokens are
     // dropped; mio_hip_llm_steps_issued counts them).
+    m->eos_snap = -1, m->tail_steps = 0, m->tail_timed_steps = 0, m->tail_ms = 0.0f;
     if ((rc = mio::llm_run(m, check_interval))) return rc;
     while (!done) {
         if (m->steps_issued < m->steps_total && (rc = mio::llm_run(m, check_interval))) return rc;
         if ((rc = mio::llm_poll(m, toks, &done))) return rc;
+    }
+    if (m->eos_snap >= 0) {
+        // steps after the end token's: they return at entry (StepState.done); the whole
+        // intervals queued behind the snapshot that found it are timed by its event and the
+        // last one's
+        m->tail_steps = m->steps_issued - (n_prompt - 1) - (int)toks.size() - 1;
+        if (m->snap_n > 0) {
+            const auto &a = m->snaps[m->eos_snap];
+            const auto &z = m->snaps[(m->snap_head + m->snap_n - 1) % mio_hip_llm::kSnaps];
+            MIO_HIP_CHECK(hipEventSynchronize(z.ev));
+            MIO_HIP_CHECK(hipEventElapsedTime(&m->tail_ms, a.ev, z.ev));
+            m->tail_timed_steps = z.issued - a.issued;
+        }
     }
     const int n = (int)toks.size() < max_tokens ? (int)toks.size() : max_tokens;
     std::memcpy(out_tokens, toks.data(), (size_t)n * 4);
@@ -1158,7 +1186,7 @@ extern "C" int mio_hip_llm_generate_batch(mio_hip_llm *m, const int32_t *prompts
         MIO_REQUIRE(prompts[i] >= 0 && prompts[i] < D.n_vocab, MIO_ERR_INVALID,
                     "llm_generate_batch: token %d out of vocab", prompts[i]);
     int rc = mio::bind(m->d);
-    if (rc || (rc = batch_ensure(m, B))) return rc;
+    if (rc || (rc = batch_ensure(m, B)) || (rc = reset_tickets(m))) return rc;
     auto &bt = m->bt;
     hipStream_t s = m->d->stream;
     // prompt positions [0, P_b) of every stream: one flattened list, kPrefillB tokens per

@@ -102,6 +102,7 @@ def _declare(L: ctypes.CDLL) -> None:
         "mio_hip_codec_last_flops": (c_int, [_vp, ctypes.POINTER(ctypes.c_double)]),
         "mio_hip_llm_load_ms": (c_int, [_vp, ctypes.POINTER(ctypes.c_double)]),
         "mio_hip_llm_steps_issued": (c_int, [_vp, ctypes.POINTER(c_int)]),
+        "mio_hip_llm_tail": (c_int, [_vp, ctypes.POINTER(c_int), ctypes.POINTER(c_int), ctypes.POINTER(ctypes.c_float)]),
         "mio_hip_llm_step_kinds": (c_int, [_vp, _vp, c_int, ctypes.POINTER(c_int)]),
         "mio_hip_llm_conv_ring": (c_int, [_vp, c_int, _vp, c_int]),
         "mio_hip_llm_eval_layers": (c_int, [_vp, ctypes.c_int32, c_int, _vp, _vp]),
@@ -438,6 +439,13 @@ class Llm:
         v = ctypes.c_int(0)
         check(lib().mio_hip_llm_steps_issued(self.h, ctypes.byref(v)))
         return v.value
+
+    def tail(self):
+        """(steps after the end token, whole intervals' steps timed, their GPU ms) of the last
+        generate that stopped at an end token (mio_hip_llm_tail)."""
+        a, b, ms = ctypes.c_int(0), ctypes.c_int(0), ctypes.c_float(0)
+        check(lib().mio_hip_llm_tail(self.h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(ms)))
+        return a.value, b.value, ms.value
 
     def eval(self, token: int, pos: int) -> np.ndarray:
         out = np.empty(self.n_vocab, np.float32)

@@ -133,6 +133,28 @@ def test_stream_benchmark_1p7b_700_tokens(files, synth_llm_path):
     print({k: r[k] for k in r if k.startswith("stream_bench.")})
 
 
+def test_stream_benchmark_c1_0p1b_700_tokens(files, synth_llm_path):
+    """BASELINE configs[0] (C1): MioTTS-0.1B Q8_0 (preset 2) through miotts-stream-benchmark,
+    the reference's harness (stream-benchmark.cpp:148-166): every stream_bench.* key, the
+    18 / 7160 re-decode cadence of a 700-token utterance, every sample emitted. The reference
+    runs this config on its CPU path (ggml, absent here); the product has no CPU
+    fallback, so this is the same workload on the GPU path (bench.py's cpu_baseline_c1 times
+    the C oracle on it)."""
+    out = run(["miotts-stream-benchmark", "-m", synth_llm_path(2), "-c", files["codec"], "-v", files["voice"],
+               "-p", "こんにちは、今日はいい天気ですね。", "--max-tokens", 700, "--speech-only", "--ignore-eos"],
+              timeout=600)
+    r = kv(out)
+    for k in ["total_sec", "audio_sec", "rtf", "x_realtime", "llm_tokens", "decode_calls", "decoded_codes",
+              "emitted_samples", "stage.llm_sec", "stage.codec_sec", "stage.istft_sec", "stage.callback_sec"]:
+        assert f"stream_bench.{k}" in r, k
+    assert int(r["stream_bench.llm_tokens"]) == 700
+    assert int(r["stream_bench.decode_calls"]) == 18
+    assert int(r["stream_bench.decoded_codes"]) == 7160
+    assert int(r["stream_bench.emitted_samples"]) == 700 * 1764
+    assert float(r["stream_bench.audio_sec"]) == pytest.approx(28.0, abs=1e-3)
+    print({k: r[k] for k in r if k.startswith("stream_bench.")})
+
+
 @pytest.mark.parametrize("n,chunk", [(100, 4096), (141, 1000), (320, 4096)])
 def test_stream_emission_matches_restatement(files, n, chunk):
     """Everything synthesize_stream hands its callback (LLM speech-only, tiny codec) against

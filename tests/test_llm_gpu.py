@@ -104,9 +104,30 @@ def test_generate_stops_at_eos(device, llm_files):
     # ahead of the poll that found it
     wasted = g.steps_issued() - len(toks) - 1
     assert 0 <= wasted < 2 * 20, wasted
+    assert g.tail()[0] == wasted
     # a run that stops at max_tokens issues exactly max_tokens steps
     toks = g.generate(prompt, 50, 0.8, 7, allow=(m.SYNTH_SPEECH0, m.SYNTH_SPEECH0 + 3), check_interval=20)
-    assert len(toks) == 50 and g.steps_issued() == 50
+    assert len(toks) == 50 and g.steps_issued() == 50 and g.tail() == (0, 0, 0.0)
+
+
+# After an end token every decode launch returns at entry (StepState.done; the reference breaks
+# before the next llama_decode, test-to-speech.cpp:168-170): a step queued past it costs about
+# its launch boundaries (~1.5 us each) instead of streaming the weights. 1.7B Q4_K_M: 141
+# launches per step, 0.77 ms per real step = 5.4 us per launch.
+@pytest.mark.parametrize("preset", [3, 2])
+def test_steps_after_eos_return_at_entry(device, synth_llm_path, preset):
+    g = m.Llm(device, synth_llm_path(preset), 512)
+    prompt = [256, 257, 65, 258, 257]
+    toks = g.generate(prompt, 400, 2.0, 11, allow=(m.SYNTH_EOT, m.SYNTH_SPEECH0 + 3),
+                      eos=(m.SYNTH_EOT, m.SYNTH_IM_END), check_interval=20)
+    assert len(toks) < 20, len(toks)  # 1 in 4 allowed ids ends the run
+    wasted, timed, ms = g.tail()
+    assert wasted == g.steps_issued() - len(toks) - 1 and timed == 20, (wasted, timed)
+    us_per_launch = ms * 1e3 / timed / len(g.step_kinds())
+    print(f"preset {preset}: {wasted} steps after the end token, {ms * 1e3 / timed:.1f} us per step "
+          f"({us_per_launch:.2f} us per launch)")
+    assert us_per_launch <= 2.5, us_per_launch
+    g.close()
 
 
 def _teacher_forced(device, path, n_pos, seed):
