@@ -701,10 +701,7 @@ __global__ __launch_bounds__(AttCfg<HD>::NT) void k_pf_attention(LlmDims d, cons
     const int kvh = blockIdx.x % d.n_kv, t = blockIdx.x / d.n_kv, ch = blockIdx.y;
     const int pos = pb.pos[t * pb.pos_stride];
     const int t0 = ch * ATT_CHUNK;
-    // a stream that sampled its end token is frozen (k_bt_sample): its attention is skipped
-    // (pb.pos points at StepState.pos of each stream in the batched decode)
-    static_assert(offsetof(StepState, done) - offsetof(StepState, pos) == 3 * sizeof(int), "StepState layout");
-    if (t0 > pos || pb.pos[t * pb.pos_stride + 3]) return;
+    if (t0 > pos) return;
     const size_t kvo = (size_t)pb.seq[t * pb.seq_stride] * pb.seq_kv + (size_t)kvh * d.n_ctx * HD;
     h8 kr[C::IT], vr[C::IT];
     load_kv_rows<HD>(kc + kvo, vc + kvo, t0, pos, kr, vr);
@@ -734,7 +731,10 @@ __global__ __launch_bounds__(AttCfg<HD>::NT) void k_bt_attention(LlmDims d, cons
     const int kvh = blockIdx.x % d.n_kv, t = blockIdx.x / d.n_kv, ch = blockIdx.y;
     const int pos = pb.pos[t * pb.pos_stride];
     const int t0 = ch * ATT_CHUNK;
-    if (t0 > pos) return;
+    // a stream that sampled its end token is frozen (k_bt_sample): its attention is skipped
+    // (in the batched decode pb.pos points at StepState.pos of each stream)
+    static_assert(offsetof(StepState, done) - offsetof(StepState, pos) == 3 * sizeof(int), "StepState layout");
+    if (t0 > pos || pb.pos[t * pb.pos_stride + 3]) return;
     const size_t kvo = (size_t)pb.seq[t * pb.seq_stride] * pb.seq_kv + (size_t)kvh * d.n_ctx * HD;
     _Float16 *kc = kcache + kvo, *vc = vcache + kvo;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
