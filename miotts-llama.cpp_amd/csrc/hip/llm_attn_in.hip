@@ -36,6 +36,8 @@ __global__ __launch_bounds__(MT) void k_attn_in(LlmDims d, const float *norm_w, 
         step = b.st->step;
         if (b.st->done) return;
     }
+    uint32_t dn = 0;
+    if constexpr (!FS) dn = done_issue(b);
     XRegs<NP> xr;
     load_x(pend ? nullptr : b.x, norm_w, K, xr);
     x_gate();
@@ -73,7 +75,7 @@ __global__ __launch_bounds__(MT) void k_attn_in(LlmDims d, const float *norm_w, 
         load_first<TQ, NP, 1, SU, MIO_SMALL_AUX>(wq, wk, lo, hi, ga, gb, o1);
         if (sample_prologue()) return;
         x_after_weights(xr);
-        if (!FS && step_done(b)) return;
+        if (!FS && done_now(dn)) return;
         MIO_TRACE(b, 1);
         MIO_TL_MARK1(b);
         rmsnorm_quant(xr, K, d.eps, akind(TQ), s, MIO_TL_DIAGSLOT(b));
@@ -90,7 +92,7 @@ __global__ __launch_bounds__(MT) void k_attn_in(LlmDims d, const float *norm_w, 
         load_first<TV, NP, 1, SU, MIO_SMALL_AUX>(wv, wv, lo, hi, ga, gb);
         if (sample_prologue()) return;
         x_after_weights(xr);
-        if (!FS && step_done(b)) return;
+        if (!FS && done_now(dn)) return;
         rmsnorm_quant(xr, K, d.eps, akind(TV), s, MIO_TL_DIAGSLOT(b));
         stream_rows<TV, NP, 1, SU, MIO_SMALL_AUX>(wv, wv, lo, hi, ga, gb, s.a, [&](int row, float v, float) {
             put(o2 + row, v);

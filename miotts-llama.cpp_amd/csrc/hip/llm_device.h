@@ -1031,13 +1031,14 @@ __device__ __forceinline__ int cur_pos(const StepState *st, const LlmDims &d) {
 
 // An end token was sampled: the rest of the step and every later step return at entry (the
 // reference breaks before the next llama_decode, test-to-speech.cpp:168-170). The matvec
-// launches read the flag behind their first weight group and x, so its scalar round trip
-// overlaps theirs instead of holding the weight stream back.
+// launches read the flag with a VECTOR load issued in front of their activation loads:
+// vmcnt retires in order, so the wait for x covers it and a decoding step pays no extra
+// round trip (a scalar load of the flag behind the weight group cost 82 us per 1.7B token).
 template <class B>
-__device__ __forceinline__ bool step_done(const B &b) {
-    asm volatile("" ::: "memory");
-    return b.st->done != 0;
+__device__ __forceinline__ uint32_t done_issue(const B &b) {
+    return __builtin_amdgcn_raw_buffer_load_b32(rsrc(&b.st->done, 4), 0, 0, 0);
 }
+__device__ __forceinline__ bool done_now(uint32_t v) { return __builtin_amdgcn_readfirstlane(v) != 0; }
 
 // The pending sample's token: Gumbel-max winner (ties -> lowest id) over the lm_head
 // workgroups' partials {smp[2i] value, smp[2i+1] id bits}, sc.lo when no id was allowed, the
@@ -1404,6 +1405,253 @@ __device__ void attend_chunk(const float (*qs)[HD], const h8 (&kr)[AttCfg<HD>::I
         st1_sc1(dst, o + 4u * dd, O);
         if (dd == 0) st1_sc1(dst, o + 4u * HD, M[g]), st1_sc1(dst, o + 4u * (HD + 1), L);
     }
+}
+
+// ------------------------------------------------------------------ attention chunk on the matrix cores
+// MIO_ATT_MFMA (default 1; 0 = the VALU attend_chunk above, for A/B builds): the chunk's
+// Q.K^T and P.V on v_mfma_f32_16x16x32_f16, shared by the decode step, the batched decode and
+// the prefill, so their outputs stay equal bit for bit.
+//  * K and V rows are staged once per workgroup into two LDS images (one 16-B chunk per lane
+//    and load; a chunk's physical slot is XOR-swizzled per row, AttM::fk / fv, so the
+//    fragment reads below are bank-conflict-free);
+//  * every wave computes S^T = K Q^T for the WHOLE chunk (PT x KS MFMAs: A = a 16-position K
+//    tile read from the image, B = Q^T, the G heads padded to 16 columns with zeros), so the
+//    chunk max and sum of each head are wave-local: no workgroup barrier after the staging;
+//  * S^T's accumulator has the position on the registers and the head on the lane, so P (as
+//    f16 hi + lo parts: P = hi + lo to 2^-22, the f32 probabilities to within rounding of the
+//    residual) is the A operand of the P.V MFMA with no lane movement; V's 16-dim column tiles
+//    come from the image by ds_read_b64_tr_b16 (4 positions x 16 dims per 16-lane group) in
+//    the same permuted k order (positions 32 s + 4 h + j and 32 s + 16 + 4 h + j of lane half
+//    h: cdna_hip_programming.md §3 "An accumulator tile as the next MFMA's operand");
+//  * wave w owns output dims [HD / 4 * w, HD / 4 * (w + 1)): DTW tiles of 16.
+// Numerics: q and the cache rows are f16-exact, so every product is exact and only the f32
+// summation order differs from the VALU sweep (scores by 32-dim MFMA k-steps, p.v by 32
+// positions); records {O[hd] = sum p v, m, l = sum p} as attend_chunk's.
+#ifndef MIO_ATT_MFMA
+#define MIO_ATT_MFMA 1
+#endif
+// MIO_ATT_FASTEXP (default 1): p by the hardware exp (v_exp_f32 of x log2 e) instead of expf
+// (0 for A/B: 0.768 vs 0.759 ms per 1.7B token, profiles/r05_att_ab.txt)
+#ifndef MIO_ATT_FASTEXP
+#define MIO_ATT_FASTEXP 1
+#endif
+typedef _Float16 h4v __attribute__((ext_vector_type(4)));
+typedef short s4v __attribute__((ext_vector_type(4)));
+typedef float f4v __attribute__((ext_vector_type(4)));
+
+template <int HD>
+struct AttM {
+    static constexpr int NT = 256, NW = 4;
+    static constexpr int CH = HD / 8;               // 16-byte chunks per K / V row
+    static constexpr int VI = ATT_CHUNK * CH / NT;  // chunks of K (and of V) each thread stages
+    static constexpr int PT = ATT_CHUNK / 16;       // 16-position tiles of S^T
+    static constexpr int KS = HD / 32;              // 32-dim k-steps of Q.K^T
+    static constexpr int PS = ATT_CHUNK / 32;       // 32-position k-steps of P.V
+    static constexpr int DTW = HD / 16 / NW;        // 16-dim output tiles per wave
+    static constexpr int RB = HD * 2;               // bytes per image row
+    static constexpr int IMG = ATT_CHUNK * RB;      // bytes per image
+    // physical chunk of logical chunk c of row r = c ^ f(r).
+    // fk: the K fragment read (ds_read_b128, lane (h, i) reads chunk 4 j + h of row 16 tau + i)
+    //     puts each 16-lane bank group on 16 distinct slots (HD 128: slots = chunks; HD 64: 8
+    //     chunks x 2 row parities);
+    // fv: the transposed read (lane 4 q + p of group h: row base + 4 h + q, dims col0 + 4 p ..)
+    //     puts the 8 rows x 2 chunks of a 32-lane half on 16 distinct slots.
+    // Both keep the 8-lane groups of the image stores (ds_write_b128, 8 consecutive chunks of a
+    // row) on distinct banks.
+    __device__ static int fk(int r) { return HD == 128 ? (r & 15) : ((r >> 1) & 7); }
+    __device__ static int fv(int r) { return HD == 128 ? ((r & 7) << 1) : (((r >> 1) & 3) << 1); }
+};
+static_assert(ATT_CHUNK % 32 == 0, "attention chunk: whole 32-position k-steps");
+
+// This thread's K / V chunks of the chunk's rows t0 .. t0 + ATT_CHUNK - 1 (rows past pos read
+// row pos: finite values under a zero probability), issued early.
+template <int HD>
+__device__ __forceinline__ void kv_issue(const _Float16 *kb, const _Float16 *vb, int t0, int pos,
+                                         h8 (&kr)[AttM<HD>::VI], h8 (&vr)[AttM<HD>::VI]) {
+    using A = AttM<HD>;
+#pragma unroll
+    for (int it = 0; it < A::VI; ++it) {
+        const int c = it * A::NT + (int)MIO_TIDX, row = c / A::CH, ch = c % A::CH;
+        const size_t o = (size_t)min(t0 + row, pos) * HD + ch * 8;
+        kr[it] = *reinterpret_cast<const h8 *>(kb + o);
+        vr[it] = *reinterpret_cast<const h8 *>(vb + o);
+    }
+}
+
+// The chunks into the images; row `skip` (the position being decoded, whose cache row this
+// launch writes) is staged from LDS by the wave that prepared it (kv_stage_row).
+template <int HD>
+__device__ __forceinline__ void kv_stage(const h8 (&kr)[AttM<HD>::VI], const h8 (&vr)[AttM<HD>::VI], int skip,
+                                         char *kimg, char *vimg) {
+    using A = AttM<HD>;
+#pragma unroll
+    for (int it = 0; it < A::VI; ++it) {
+        const int c = it * A::NT + (int)MIO_TIDX, row = c / A::CH, ch = c % A::CH;
+        if (row != skip) {
+            *reinterpret_cast<h8 *>(kimg + row * A::RB + 16 * (ch ^ A::fk(row))) = kr[it];
+            *reinterpret_cast<h8 *>(vimg + row * A::RB + 16 * (ch ^ A::fv(row))) = vr[it];
+        }
+    }
+}
+
+// One wave: row r of both images from the prepared f16-exact k / v values (LDS floats).
+template <int HD>
+__device__ __forceinline__ void kv_stage_row(const float *kn, const float *vn, int r, char *kimg, char *vimg) {
+    using A = AttM<HD>;
+    const int lane = MIO_TIDX & 63;
+    if (lane < 2 * A::CH) {
+        const bool isv = lane >= A::CH;
+        const int ch = lane % A::CH;
+        const float *src = (isv ? vn : kn) + ch * 8;
+        h8 v;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = (_Float16)src[e];
+        char *img = isv ? vimg : kimg;
+        *reinterpret_cast<h8 *>(img + r * A::RB + 16 * (ch ^ (isv ? A::fv(r) : A::fk(r)))) = v;
+    }
+}
+
+// The chunk's partial records {O[HD], m, l} of the G heads qh (LDS, f16) over positions
+// [t0, min(t0 + ATT_CHUNK, pos + 1)) from the staged images, stored write-through (sc1) at
+// dst + g * g_stride for attn_merge_last. Whole workgroup (AttM::NT threads); the images and
+// qh must be visible (a barrier after staging).
+template <int HD, int G>
+__device__ __forceinline__ void attend_chunk_mfma(const _Float16 (*qh)[HD], const char *kimg, const char *vimg, int t0,
+                                                  int pos, float scale, float *dst, uint32_t g_stride,
+                                                  unsigned long long *trace = nullptr) {
+    using A = AttM<HD>;
+    static_assert(G <= 16, "heads per kv head");
+    const int lane = MIO_TIDX & 63, wave = MIO_TIDX >> 6, h = lane >> 4, i = lane & 15;
+    auto mark = [&](int k, float v) {  // checkpoints of mio_hip_llm_trace_kernel (diagnostic)
+        if (trace && blockIdx.x == 0 && blockIdx.y == 0 && MIO_TIDX == 0) {
+            asm volatile("" ::"v"(v) : "memory");
+            trace[k] = __builtin_readcyclecounter();
+        }
+    };
+    // every LDS read of the chunk is issued up front (one round trip, not one per fragment):
+    // the K tiles (A operand: lane (h, i) reads position 16 tau + i, dims 32 j + 8 h .. + 7) ...
+    h8 kf[A::PT][A::KS];
+#pragma unroll
+    for (int tau = 0; tau < A::PT; ++tau)
+#pragma unroll
+        for (int j = 0; j < A::KS; ++j) {
+            const int r = 16 * tau + i;
+            kf[tau][j] = *reinterpret_cast<const h8 *>(kimg + r * A::RB + 16 * ((4 * j + h) ^ A::fk(r)));
+        }
+    // ... Q^T (B operand: head i's dims 32 j + 8 h .. + 7, zero past G) ...
+    h8 qf[A::KS];
+    const int gq = i < G ? i : G - 1;
+#pragma unroll
+    for (int j = 0; j < A::KS; ++j) {
+        const h8 q = *reinterpret_cast<const h8 *>(&qh[gq][32 * j + 8 * h]);
+        qf[j] = i < G ? q : h8{};
+    }
+    // ... and this wave's V^T tiles by transposed reads (lane 4 q + p of group h: row
+    // 32 s + 16 r2 + 4 h + q, dims col0 + 4 p .. + 3)
+    const int q4 = i >> 2, p4 = i & 3;
+    h4v vb[A::PS][A::DTW][2];
+#pragma unroll
+    for (int s2 = 0; s2 < A::PS; ++s2)
+#pragma unroll
+        for (int n = 0; n < A::DTW; ++n) {
+            const int lch = 2 * (wave * A::DTW + n) + (p4 >> 1);
+#pragma unroll
+            for (int r2 = 0; r2 < 2; ++r2) {
+                const int row = 32 * s2 + 16 * r2 + 4 * h + q4;
+                const char *a = vimg + row * A::RB + 16 * (lch ^ A::fv(row)) + 8 * (p4 & 1);
+                vb[s2][n][r2] = __builtin_bit_cast(
+                    h4v, __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4v *)(const_cast<char *>(a))));
+            }
+        }
+    // S^T tiles: s[tau][e] = q_i . k(t0 + 16 tau + 4 h + e)
+    f4v s[A::PT];
+#pragma unroll
+    for (int tau = 0; tau < A::PT; ++tau) {
+        s[tau] = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int j = 0; j < A::KS; ++j) s[tau] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf[tau][j], qf[j], s[tau], 0, 0, 0);
+    }
+    // scaled scores, positions past pos masked (only the chunk holding pos has any), and head
+    // i's chunk max over this lane's 4 PT positions, then the 4 lanes (h) holding head i
+    float M = -INFINITY;
+    if (t0 + ATT_CHUNK - 1 <= pos) {
+#pragma unroll
+        for (int tau = 0; tau < A::PT; ++tau)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                s[tau][e] = s[tau][e] * scale;
+                M = fmaxf(M, s[tau][e]);
+            }
+    } else {
+#pragma unroll
+        for (int tau = 0; tau < A::PT; ++tau)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const bool valid = t0 + 16 * tau + 4 * h + e <= pos;
+                s[tau][e] = valid ? s[tau][e] * scale : -INFINITY;
+                M = fmaxf(M, s[tau][e]);
+            }
+    }
+    M = fmaxf(M, xor_lane<16>(M));
+    M = fmaxf(M, xor_lane<32>(M));
+    mark(3, M);
+    // p = exp(s - M) as the P.V A operand (hi + lo f16 parts), l = sum p (the chunk holds
+    // position t0 <= pos, so M is finite; exp(-inf) = 0 for the masked positions)
+    float L = 0.0f;
+    h8 ph[A::PS], pl[A::PS];
+#pragma unroll
+    for (int tau = 0; tau < A::PT; ++tau)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+#if MIO_ATT_FASTEXP
+            // exp(x) = 2^(x log2 e) on v_exp_f32 (relative error ~ |x| 2^-24 + 1 ulp)
+            const float p = __builtin_amdgcn_exp2f((s[tau][e] - M) * 1.44269504088896341f);
+#else
+            const float p = expf(s[tau][e] - M);
+#endif
+            L += p;
+            const _Float16 hi = (_Float16)p;
+            ph[tau >> 1][(tau & 1) * 4 + e] = hi;
+            pl[tau >> 1][(tau & 1) * 4 + e] = (_Float16)(p - (float)hi);
+        }
+    L += xor_lane<16>(L);
+    L += xor_lane<32>(L);
+    mark(4, L);
+    // P.V for this wave's dims
+    f4v o[A::DTW];
+#pragma unroll
+    for (int n = 0; n < A::DTW; ++n) o[n] = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s2 = 0; s2 < A::PS; ++s2)
+#pragma unroll
+        for (int n = 0; n < A::DTW; ++n) {
+            const h4v *b2 = vb[s2][n];
+            const h8 vf = h8{b2[0][0], b2[0][1], b2[0][2], b2[0][3], b2[1][0], b2[1][1], b2[1][2], b2[1][3]};
+            o[n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ph[s2], vf, o[n], 0, 0, 0);
+            o[n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pl[s2], vf, o[n], 0, 0, 0);
+        }
+    mark(5, o[0][0]);
+    // o[n][e] = O[head 4 h + e][dim 16 (wave DTW + n) + i]
+#pragma unroll
+    for (int n = 0; n < A::DTW; ++n)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int g = 4 * h + e;
+            if (g < G) st1_sc1(dst, ((uint32_t)g * g_stride + 16 * (wave * A::DTW + n) + i) * 4u, o[n][e]);
+        }
+    if (wave == 0 && h == 0 && i < G) {
+        st1_sc1(dst, ((uint32_t)i * g_stride + HD) * 4u, M);
+        st1_sc1(dst, ((uint32_t)i * g_stride + HD + 1) * 4u, L);
+    }
+}
+
+// q heads as f16 (the f16-exact prepared values) for attend_chunk_mfma's B operand: one wave,
+// head row src (HD floats) -> dst
+template <int HD>
+__device__ __forceinline__ void q_to_f16(const float *src, _Float16 *dst) {
+    const int lane = MIO_TIDX & 63;
+#pragma unroll
+    for (int e = lane; e < HD; e += 64) dst[e] = (_Float16)src[e];
 }
 
 // After attend_chunk: the chunk workgroups of one (kv head [, token]) take arrival tickets;

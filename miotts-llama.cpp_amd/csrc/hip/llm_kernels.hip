@@ -64,6 +64,7 @@ __global__ __launch_bounds__(MT) void k_attn_out(LlmDims d, QMat wo, LlmBuffers 
     const Smem s = carve(smem, K);
     int lo, hi;
     wave_range(d, wo.rows, lo, hi);
+    const uint32_t dn = done_issue(b);
     XRegs<NP> xr;
     load_x(b.att, nullptr, K, xr);
     const float xres = load_resid(b.x, lo, hi);
@@ -71,7 +72,7 @@ __global__ __launch_bounds__(MT) void k_attn_out(LlmDims d, QMat wo, LlmBuffers 
     Frag ga[Cfg<NP, SU>::U], gb[Cfg<NP, SU>::U];
     load_first<T, NP, 1, SU, MIO_SMALL_AUX>(wo, wo, lo, hi, ga, gb);
     x_after_weights(xr);
-    if (step_done(b)) return;
+    if (done_now(dn)) return;
     MIO_TRACE(b, 1);
     MIO_TL_MARK1(b);
     plain_quant(xr, K, akind(T), s, MIO_TL_DIAGSLOT(b));
@@ -98,6 +99,7 @@ __global__ __launch_bounds__(MT) void k_conv_out(LlmDims d, QMat wo, const float
     MIO_TL_BEGIN(b);
     const int K = wo.k;
     const Smem s = carve(smem, K);
+    const uint32_t dn = done_issue(b);
     const int pos = cur_pos(b.st, d);
     const ConvPrev p1{pos >= 1 ? ring + (size_t)((pos - 1) & (kConvSlots - 1)) * K : nullptr, 0};
     const ConvPrev p2{pos >= 2 ? ring + (size_t)((pos - 2) & (kConvSlots - 1)) * K : nullptr, 0};
@@ -110,7 +112,7 @@ __global__ __launch_bounds__(MT) void k_conv_out(LlmDims d, QMat wo, const float
     Frag ga[Cfg<NP, SU>::U], gb[Cfg<NP, SU>::U];
     load_first<T, NP, 1, SU>(wo, wo, lo, hi, ga, gb);
     conv_after_weights(cr);
-    if (step_done(b)) return;
+    if (done_now(dn)) return;
     MIO_TRACE(b, 1);
     MIO_TL_MARK1(b);
     conv_quant(cr, K, akind(T), s, blockIdx.x == 0 ? ring + (size_t)(pos & (kConvSlots - 1)) * K : nullptr,
@@ -142,6 +144,7 @@ __global__ __launch_bounds__(MT) void k_ffn_in(LlmDims d, const float *norm_w, Q
     MIO_TL_BEGIN(b);
     const int K = d.n_embd;
     const Smem s = carve(smem, K);
+    const uint32_t dn = done_issue(b);
     XRegs<NP> xr;
     load_x(b.x, norm_w, K, xr);
     x_gate();
@@ -150,7 +153,7 @@ __global__ __launch_bounds__(MT) void k_ffn_in(LlmDims d, const float *norm_w, Q
     Frag ga[Cfg<NP, SU>::U], gb[Cfg<NP, SU>::U];
     load_first<T, NP, 2, SU>(gate, up, lo, hi, ga, gb);
     x_after_weights(xr);
-    if (step_done(b)) {  // layer 0 still folds the end token's step (the host counts it)
+    if (done_now(dn)) {  // layer 0 still folds the end token's step (the host counts it)
         if (adv && blockIdx.x == 0 && MIO_TIDX == 0) advance_state(b.st, d);
         return;
     }
@@ -175,6 +178,7 @@ __global__ __launch_bounds__(MT) void k_ffn_down(LlmDims d, QMat down, LlmBuffer
     MIO_TL_BEGIN(b);
     const int K = down.k;
     const Smem s = carve(smem, K);
+    const uint32_t dn = done_issue(b);
     XRegs<NP> xr;
     load_x(b.h, nullptr, K, xr);
     int lo, hi;
@@ -184,7 +188,7 @@ __global__ __launch_bounds__(MT) void k_ffn_down(LlmDims d, QMat down, LlmBuffer
     Frag ga[Cfg<NP, SU>::U], gb[Cfg<NP, SU>::U];
     load_first<T, NP, 1, SU>(down, down, lo, hi, ga, gb);
     x_after_weights(xr);
-    if (step_done(b)) return;
+    if (done_now(dn)) return;
     MIO_TRACE(b, 1);
     MIO_TL_MARK1(b);
     plain_quant(xr, K, akind(T), s, MIO_TL_DIAGSLOT(b));
@@ -288,7 +292,14 @@ __global__ __launch_bounds__(AttCfg<HD>::NT) void k_attention(LlmDims d, const f
     constexpr int PER = HD / 64;
     __shared__ float qs[G][HD];
     __shared__ float knew[HD], vnew[HD];
+#if MIO_ATT_MFMA
+    using A = AttM<HD>;
+    static_assert(C::NT == A::NT, "attention workgroup size");
+    __shared__ __attribute__((aligned(16))) char img[2 * A::IMG];
+    __shared__ __attribute__((aligned(16))) _Float16 qh[G][HD];
+#else
     __shared__ float wres[C::NW][G][HD + 2];
+#endif
 
     MIO_TRACE(b, 0);
     MIO_TL_BEGIN(b);
@@ -303,9 +314,14 @@ __global__ __launch_bounds__(AttCfg<HD>::NT) void k_attention(LlmDims d, const f
     if (t0 > pos || b.st->done) return;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const float2 *rope = b.rope + (size_t)pos * (HD / 2);
-    // K/V rows of this slot first (row `pos` is never consumed from the cache)
+    // K/V rows of this thread first (row `pos` is never consumed from the cache)
+#if MIO_ATT_MFMA
+    h8 kr[A::VI], vr[A::VI];
+    kv_issue<HD>(kc + (size_t)kvh * d.n_ctx * HD, vc + (size_t)kvh * d.n_ctx * HD, t0, pos, kr, vr);
+#else
     h8 kr[C::IT], vr[C::IT];
     load_kv_rows<HD>(kc + (size_t)kvh * d.n_ctx * HD, vc + (size_t)kvh * d.n_ctx * HD, t0, pos, kr, vr);
+#endif
     MIO_TRACE(b, 1);
     MIO_TL_MARK1(b);
     // q heads (waves 0..G-1) and, for the chunk owning `pos`, the new k/v row
@@ -334,8 +350,27 @@ __global__ __launch_bounds__(AttCfg<HD>::NT) void k_attention(LlmDims d, const f
                 kd[p] = (_Float16)knew[p];
                 vd[p] = (_Float16)vr16;
             }
+#if MIO_ATT_MFMA
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            kv_stage_row<HD>(knew, vnew, pos - t0, img, img + A::IMG);
+#endif
         }
+#if MIO_ATT_MFMA
+        else {
+            q_to_f16<HD>(qs[hh], qh[hh]);
+        }
+#endif
     }
+#if MIO_ATT_MFMA
+    kv_stage<HD>(kr, vr, owner ? pos - t0 : -1, img, img + A::IMG);
+    lds_barrier();
+    MIO_TRACE(b, 2);
+    MIO_TL_MARK(b, 2);
+    const uint32_t gs = (uint32_t)(d.max_splits * C::REC), head0 = (uint32_t)(kvh * G) * gs;
+    attend_chunk_mfma<HD, G>(qh, img, img + A::IMG, t0, pos, d.scale, b.part + head0 + (uint32_t)ch * C::REC, gs,
+                             DG ? b.trace : nullptr);
+#else
     lds_barrier();
     MIO_TRACE(b, 2);
     MIO_TL_MARK(b, 2);
@@ -354,6 +389,7 @@ __global__ __launch_bounds__(AttCfg<HD>::NT) void k_attention(LlmDims d, const f
     const uint32_t gs = (uint32_t)(d.max_splits * C::REC), head0 = (uint32_t)(kvh * G) * gs;
     attend_chunk<HD, G>(qs, kr, vr, t0, pos, d.scale, wres, b.part + head0 + (uint32_t)ch * C::REC, gs,
                         DG ? b.trace : nullptr, MIO_TL_DIAGSLOT(b));
+#endif
     attn_merge_last<HD, G>(b.part, head0, gs, pos / ATT_CHUNK + 1, b.att_cnt + kvh, b.att + (size_t)kvh * G * HD);
     MIO_TL_END(b);
     MIO_TRACE(b, 15);

@@ -666,9 +666,29 @@ __global__ __launch_bounds__(64) void k_pf_rope(LlmDims d, const float *q_norm, 
     }
 }
 
-// attend_chunk + attn_merge_last of token t's (kv head, chunk): records in pb.part
+// attend_chunk(_mfma) + attn_merge_last of token t's (kv head, chunk): records in pb.part
 // [t][H][max_splits][REC], tickets pb.att_cnt[t][Hkv], outputs pb.att[t][H * hd].
 // att_q >= 0: the merger also writes token t's O-matvec activation record (attn_merge_last).
+template <int HD, int G>
+__device__ __forceinline__ void merge_token(const LlmDims &d, int pos, int t, int kvh, const PrefillBuffers &pb,
+                                            int att_q, float *part, uint32_t head0, uint32_t gs) {
+    const int KO = d.n_head * HD;
+    attn_merge_last<HD, G>(part, head0, gs, pos / ATT_CHUNK + 1, pb.att_cnt + (size_t)t * d.n_kv + kvh,
+                           pb.att + (size_t)t * KO + (size_t)kvh * G * HD, att_q, carve_t(pb.act, KO, t).a,
+                           att_q == 1 ? kvh * G * HD / 256 : kvh * G * HD / 32);
+}
+#if MIO_ATT_MFMA
+template <int HD, int G>
+__device__ __forceinline__ void attend_and_merge(const LlmDims &d, const _Float16 (*qh)[HD], const char *img, int t0,
+                                                 int pos, int ch, int t, int kvh, const PrefillBuffers &pb, int att_q) {
+    using C = AttCfg<HD>;
+    const uint32_t gs = (uint32_t)(d.max_splits * C::REC);
+    float *part = pb.part + (size_t)t * d.n_head * gs;  // token t's records (wave-uniform)
+    const uint32_t head0 = (uint32_t)(kvh * G) * gs;
+    attend_chunk_mfma<HD, G>(qh, img, img + AttM<HD>::IMG, t0, pos, d.scale, part + head0 + (uint32_t)ch * C::REC, gs);
+    merge_token<HD, G>(d, pos, t, kvh, pb, att_q, part, head0, gs);
+}
+#else
 template <int HD, int G>
 __device__ __forceinline__ void attend_and_merge(const LlmDims &d, const float (*qs)[HD],
                                                  const h8 (&kr)[AttCfg<HD>::IT], const h8 (&vr)[AttCfg<HD>::IT],
@@ -679,15 +699,13 @@ __device__ __forceinline__ void attend_and_merge(const LlmDims &d, const float (
     float *part = pb.part + (size_t)t * d.n_head * gs;  // token t's records (wave-uniform)
     const uint32_t head0 = (uint32_t)(kvh * G) * gs;
     attend_chunk<HD, G>(qs, kr, vr, t0, pos, d.scale, wres, part + head0 + (uint32_t)ch * C::REC, gs);
-    const int KO = d.n_head * HD;
-    attn_merge_last<HD, G>(part, head0, gs, pos / ATT_CHUNK + 1, pb.att_cnt + (size_t)t * d.n_kv + kvh,
-                           pb.att + (size_t)t * KO + (size_t)kvh * G * HD, att_q, carve_t(pb.act, KO, t).a,
-                           att_q == 1 ? kvh * G * HD / 256 : kvh * G * HD / 32);
+    merge_token<HD, G>(d, pos, t, kvh, pb, att_q, part, head0, gs);
 }
+#endif
 
 // One workgroup per (ATT_CHUNK-position chunk, kv head, token): causal softmax over the
 // chunk's positions <= the token's position in the token's own sequence, all rows read from
-// the cache (this launch's own rows were written by k_pf_rope); attend_chunk and
+// the cache (this launch's own rows were written by k_pf_rope); the attention and
 // attn_merge_last are the decode step's, so pb.att holds the decode's outputs bit for bit.
 // Chunks past the token's position exit at once. Grid (n_kv * nt, chunks): consecutive
 // workgroup ids are different (kv head, token) pairs of one chunk, so the workgroups with
@@ -697,28 +715,40 @@ __global__ __launch_bounds__(AttCfg<HD>::NT) void k_pf_attention(LlmDims d, cons
                                                                  PrefillBuffers pb, int att_q) {
     using C = AttCfg<HD>;
     __shared__ float qs[G][HD];
-    __shared__ float wres[C::NW][G][HD + 2];
     const int kvh = blockIdx.x % d.n_kv, t = blockIdx.x / d.n_kv, ch = blockIdx.y;
     const int pos = pb.pos[t * pb.pos_stride];
     const int t0 = ch * ATT_CHUNK;
     if (t0 > pos) return;
     const size_t kvo = (size_t)pb.seq[t * pb.seq_stride] * pb.seq_kv + (size_t)kvh * d.n_ctx * HD;
-    h8 kr[C::IT], vr[C::IT];
-    load_kv_rows<HD>(kc + kvo, vc + kvo, t0, pos, kr, vr);
     const int QD = (d.n_head + 2 * d.n_kv) * HD;
     const float *qsrc = pb.qkv + (size_t)t * QD + (size_t)kvh * G * HD;
+#if MIO_ATT_MFMA
+    using A = AttM<HD>;
+    __shared__ __attribute__((aligned(16))) char img[2 * A::IMG];
+    __shared__ __attribute__((aligned(16))) _Float16 qh[G][HD];
+    h8 kr[A::VI], vr[A::VI];
+    kv_issue<HD>(kc + kvo, vc + kvo, t0, pos, kr, vr);
+    for (int e = threadIdx.x; e < G * HD; e += C::NT) qh[e / HD][e % HD] = (_Float16)qsrc[e];
+    kv_stage<HD>(kr, vr, -1, img, img + A::IMG);
+    lds_barrier();
+    attend_and_merge<HD, G>(d, qh, img, t0, pos, ch, t, kvh, pb, att_q);
+#else
+    __shared__ float wres[C::NW][G][HD + 2];
+    h8 kr[C::IT], vr[C::IT];
+    load_kv_rows<HD>(kc + kvo, vc + kvo, t0, pos, kr, vr);
     for (int e = threadIdx.x; e < G * HD; e += C::NT) qs[e / HD][e % HD] = qsrc[e];
     lds_barrier();
     attend_and_merge<HD, G>(d, qs, kr, vr, t0, pos, ch, t, kvh, wres, pb, att_q);
+#endif
 }
 
 // Batched decode attention (one token per sequence, so no token of the launch reads a row
 // another one writes): per (kv head, token, chunk) the decode step's k_attention — the
 // token's q heads (and, in the chunk owning its position, its k / v row) get q/k RMSNorm +
 // bias + RoPE + f16 rounding in LDS, the owner appends the row to the sequence's cache and
-// takes it from LDS, then the chunk's softmax partials. Replaces k_pf_rope + k_pf_attention
-// (one launch less per layer; the same prep_head / attend_chunk / attn_merge_last
-// arithmetic, so the outputs equal theirs bit for bit).
+// stages it from LDS, then the chunk's softmax partials. Replaces k_pf_rope + k_pf_attention
+// (one launch less per layer; the same prep_head / attention / attn_merge_last arithmetic,
+// so the outputs equal theirs bit for bit).
 template <int HD, int G>
 __global__ __launch_bounds__(AttCfg<HD>::NT) void k_bt_attention(LlmDims d, const float *q_norm, const float *k_norm,
                                                          const float *bqkv, _Float16 *kcache, _Float16 *vcache,
@@ -727,7 +757,13 @@ __global__ __launch_bounds__(AttCfg<HD>::NT) void k_bt_attention(LlmDims d, cons
     constexpr int PER = HD / 64;
     __shared__ float qs[G][HD];
     __shared__ float knew[HD], vnew[HD];
+#if MIO_ATT_MFMA
+    using A = AttM<HD>;
+    __shared__ __attribute__((aligned(16))) char img[2 * A::IMG];
+    __shared__ __attribute__((aligned(16))) _Float16 qh[G][HD];
+#else
     __shared__ float wres[C::NW][G][HD + 2];
+#endif
     const int kvh = blockIdx.x % d.n_kv, t = blockIdx.x / d.n_kv, ch = blockIdx.y;
     const int pos = pb.pos[t * pb.pos_stride];
     const int t0 = ch * ATT_CHUNK;
@@ -739,8 +775,13 @@ __global__ __launch_bounds__(AttCfg<HD>::NT) void k_bt_attention(LlmDims d, cons
     _Float16 *kc = kcache + kvo, *vc = vcache + kvo;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const float2 *rope = pb.rope + (size_t)pos * (HD / 2);
+#if MIO_ATT_MFMA
+    h8 kr[A::VI], vr[A::VI];
+    kv_issue<HD>(kc, vc, t0, pos, kr, vr);  // row pos is staged from LDS below
+#else
     h8 kr[C::IT], vr[C::IT];
     load_kv_rows<HD>(kc, vc, t0, pos, kr, vr);  // row pos comes from LDS below
+#endif
     const float *qkv = pb.qkv + (size_t)t * (d.n_head + 2 * d.n_kv) * HD;
     const bool owner = pos < t0 + ATT_CHUNK;
     for (int hh = wave; hh < G + (owner ? 1 : 0); hh += C::NW) {
@@ -765,8 +806,23 @@ __global__ __launch_bounds__(AttCfg<HD>::NT) void k_bt_attention(LlmDims d, cons
                 kc[(size_t)pos * HD + p] = (_Float16)knew[p];
                 vc[(size_t)pos * HD + p] = (_Float16)vr16;
             }
+#if MIO_ATT_MFMA
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            kv_stage_row<HD>(knew, vnew, pos - t0, img, img + A::IMG);
+#endif
         }
+#if MIO_ATT_MFMA
+        else {
+            q_to_f16<HD>(qs[hh], qh[hh]);
+        }
+#endif
     }
+#if MIO_ATT_MFMA
+    kv_stage<HD>(kr, vr, owner ? pos - t0 : -1, img, img + A::IMG);
+    lds_barrier();
+    attend_and_merge<HD, G>(d, qh, img, t0, pos, ch, t, kvh, pb, att_q);
+#else
     lds_barrier();
     if (owner) {
         const int sl = threadIdx.x / C::LP, lp = lane % C::LP, r = pos - t0;
@@ -780,6 +836,7 @@ __global__ __launch_bounds__(AttCfg<HD>::NT) void k_bt_attention(LlmDims d, cons
         }
     }
     attend_and_merge<HD, G>(d, qs, kr, vr, t0, pos, ch, t, kvh, wres, pb, att_q);
+#endif
 }
 
 template <int NP, int T>

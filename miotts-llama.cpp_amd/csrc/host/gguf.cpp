@@ -6,6 +6,7 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <cmath>
 #include <cstring>
 
 #include "common.h"
@@ -111,7 +112,9 @@ bool read_scalar(Cursor &c, uint32_t type, GgufValue &v) {
         default: return false;
     }
     if (type != GGUF_F32 && type != GGUF_F64 && type != GGUF_STR) v.f = (double)(int64_t)v.u;
-    if (type == GGUF_F32 || type == GGUF_F64) v.u = (uint64_t)(int64_t)v.f;
+    // the integer view of a float value: only where it is representable (NaN / inf / huge -> 0)
+    if (type == GGUF_F32 || type == GGUF_F64)
+        v.u = std::isfinite(v.f) && std::fabs(v.f) < 9.0e18 ? (uint64_t)(int64_t)v.f : 0;
     return c.ok;
 }
 
@@ -199,10 +202,22 @@ bool GgufFile::open(const std::string &path) {
             c.ok = false;
             break;
         }
-        for (int d = 0; d < t.n_dims; ++d) t.ne[d] = (int64_t)c.rd<uint64_t>();
+        // every dimension in [0, 2^40) and the byte count without overflow (a hostile file
+        // must not wrap the bounds check below)
+        bool shape_ok = true;
+        for (int d = 0; d < t.n_dims; ++d) {
+            const uint64_t v = c.rd<uint64_t>();
+            shape_ok = shape_ok && v < (1ull << 40);
+            t.ne[d] = shape_ok ? (int64_t)v : 0;
+        }
         t.type = c.rd<uint32_t>();
         t.offset = c.rd<uint64_t>();
-        t.nbytes = ggml_row_bytes(t.type, t.ne[0]) * (size_t)(t.ne[1] * t.ne[2] * t.ne[3]);
+        uint64_t rows = 0, nb = 0;
+        if (shape_ok && !__builtin_mul_overflow((uint64_t)t.ne[1], (uint64_t)t.ne[2], &rows) &&
+            !__builtin_mul_overflow(rows, (uint64_t)t.ne[3], &rows) &&
+            !__builtin_mul_overflow((uint64_t)ggml_row_bytes(t.type, t.ne[0]), rows, &nb))
+            t.nbytes = (size_t)nb;
+        if (!c.ok) break;
         if (!t.nbytes) {
             set_error("gguf: tensor %s has unsupported type %u / shape", t.name.c_str(), t.type);
             close();
@@ -216,11 +231,18 @@ bool GgufFile::open(const std::string &path) {
         close();
         return false;
     }
-    const size_t align = (size_t)get_int("general.alignment", 32);
+    const int64_t align = get_int("general.alignment", 32);
+    if (align < 1 || align > (1 << 20) || (align & (align - 1))) {
+        set_error("gguf: %s has general.alignment %lld (a power of two is required)", path.c_str(), (long long)align);
+        close();
+        return false;
+    }
     size_t off = (size_t)(c.p - base);
-    data_offset_ = (off + align - 1) / align * align;
+    data_offset_ = (off + (size_t)align - 1) / (size_t)align * (size_t)align;
     for (auto &t : tensors_) {
-        if (data_offset_ + t.offset + t.nbytes > map_size_) {
+        // overflow-safe: data_offset_ + offset + nbytes <= map_size_
+        if (data_offset_ > map_size_ || t.offset > map_size_ - data_offset_ ||
+            t.nbytes > map_size_ - data_offset_ - t.offset) {
             set_error("gguf: tensor %s data out of file bounds", t.name.c_str());
             close();
             return false;

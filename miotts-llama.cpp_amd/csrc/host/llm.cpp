@@ -1274,9 +1274,20 @@ extern "C" int mio_hip_llm_prefill(mio_hip_llm *m, const int32_t *tokens, int n_
                     tokens[i]);
     int rc = mio::bind(m->d);
     if (rc) return rc;
-    if (m->bf16) {  // forced decode steps (the multi-token engine is int8-only)
-        for (int i = 0; i + 1 < n_tokens; ++i)
-            if ((rc = mio_hip_llm_eval(m, tokens[i], i, nullptr))) return rc;
+    if (m->bf16) {
+        // forced decode steps as llm_begin runs them (the multi-token engine is int8-only):
+        // step j decodes tokens[j] at position j and its sampler is forced to tokens[j + 1]
+        if (n_tokens > 1) {
+            mio::SampleCfg c{};
+            c.temp = 0.0f, c.lo = 0, c.hi = m->dims.n_vocab, c.eos0 = c.eos1 = -1;
+            c.force = m->d_force, c.n_force = m->max_steps, c.out_tokens = m->d_tokens, c.max_steps = m->max_steps;
+            std::vector<int> force(m->max_steps, -1);
+            for (int j = 0; j + 1 < n_tokens && j < m->max_steps; ++j) force[j] = tokens[j + 1];
+            MIO_HIP_CHECK(hipMemcpyAsync(m->d_force, force.data(), force.size() * 4, hipMemcpyHostToDevice,
+                                         m->d->stream));
+            if ((rc = put_cfg(m, c)) || (rc = ensure_graph(m)) || (rc = set_state(m, 0, tokens[0]))) return rc;
+            for (int j = 0; j + 1 < n_tokens; ++j) MIO_HIP_CHECK(hipGraphLaunch(m->graph, m->d->stream));
+        }
     } else if ((rc = upload_prompt(m, tokens, n_tokens)) || (rc = prefill(m, n_tokens - 1))) {
         return rc;
     }
