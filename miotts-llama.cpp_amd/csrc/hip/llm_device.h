@@ -1205,21 +1205,48 @@ __device__ __forceinline__ float xor_lane(float v) {
 // row: wave-private LDS scratch [HD]; the prepared head is left in row.
 // bias (may be null): the projection bias added in f32 before anything else (qwen2,
 // llama.cpp build_attn_mha's Qcur = ggml_add(Qcur, bq)).
+// The loads of one head's preparation (prep_head), issued on their own so a caller can put
+// them in front of its K/V row loads (vmcnt retires in order: a head load behind 8 K/V loads
+// waits for all of them). val: the head's values (+ bias), w: norm weight, cs: RoPE cos/sin;
+// vv (optional, the new v row of the owner's k head): value + bias.
 template <int HD>
-__device__ void prep_head(const float *src, const float *bias, const float *nw, const float2 *rope,
-                          const LlmDims &d, float *row) {
+struct HeadIn {
+    static constexpr int PER = HD / 64;
+    float v[PER], w[PER], vv[PER];
+    float2 cs[PER];
+};
+template <int HD>
+__device__ __forceinline__ void head_load(const float *src, const float *bias, const float *nw, const float2 *rope,
+                                          const LlmDims &d, HeadIn<HD> &in, const float *vsrc = nullptr,
+                                          const float *vbias = nullptr) {
     constexpr int PER = HD / 64;
     const int lane = MIO_TIDX & 63;
-    float v[PER], w[PER];
-    float2 cs[PER];
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
         const int p = lane + 64 * i;
-        v[i] = src[p];
-        if (bias) v[i] = v[i] + bias[p];
-        w[i] = d.qk_norm ? nw[p] : 1.0f;
-        cs[i] = p < HD / 2 ? rope[p] : make_float2(0.0f, 0.0f);
+        in.v[i] = src[p];
+        if (bias) in.v[i] = in.v[i] + bias[p];
+        in.w[i] = d.qk_norm ? nw[p] : 1.0f;
+        in.cs[i] = p < HD / 2 ? rope[p] : make_float2(0.0f, 0.0f);
+        if (vsrc) {
+            in.vv[i] = vsrc[p];
+            if (vbias) in.vv[i] = in.vv[i] + vbias[p];
+        }
     }
+}
+
+// q/k head preparation by one wave from head_load's registers: optional RMSNorm with weight w
+// (qwen3 attn_q_norm / attn_k_norm), RoPE on (i, i + HD/2) pairs (NEOX) or (2i, 2i+1) (NORM)
+// with the ggml rope-cache cos/sin, f16 rounding (the F16 cache / ggml's f16 K operand).
+// The projection bias was added in f32 before anything else (qwen2, llama.cpp build_attn_mha's
+// Qcur = ggml_add(Qcur, bq)). row: wave-private LDS scratch [HD]; the prepared head is left in row.
+template <int HD>
+__device__ void head_prep(const HeadIn<HD> &in, const LlmDims &d, float *row) {
+    constexpr int PER = HD / 64;
+    const int lane = MIO_TIDX & 63;
+    float v[PER];
+#pragma unroll
+    for (int i = 0; i < PER; ++i) v[i] = in.v[i];
     if (d.qk_norm) {
         double ss = 0.0;
 #pragma unroll
@@ -1230,7 +1257,7 @@ __device__ void prep_head(const float *src, const float *bias, const float *nw, 
 #pragma unroll
         for (int i = 0; i < PER; ++i) {
             const float t = v[i] * scale;
-            v[i] = t * w[i];
+            v[i] = t * in.w[i];
         }
     }
 #pragma unroll
@@ -1246,8 +1273,8 @@ __device__ void prep_head(const float *src, const float *bias, const float *nw, 
         if (p < HD / 2) {
             const int i0 = d.neox ? p : 2 * p, i1 = d.neox ? p + HD / 2 : 2 * p + 1;
             const float x0 = row[i0], x1 = row[i1];
-            o0[i] = x0 * cs[i].x - x1 * cs[i].y;
-            o1[i] = x0 * cs[i].y + x1 * cs[i].x;
+            o0[i] = x0 * in.cs[i].x - x1 * in.cs[i].y;
+            o1[i] = x0 * in.cs[i].y + x1 * in.cs[i].x;
             i0s[i] = i0, i1s[i] = i1;
         }
     }
@@ -1261,6 +1288,15 @@ __device__ void prep_head(const float *src, const float *bias, const float *nw, 
         }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+}
+
+// head_load + head_prep (HD values at src; bias may be null)
+template <int HD>
+__device__ void prep_head(const float *src, const float *bias, const float *nw, const float2 *rope,
+                          const LlmDims &d, float *row) {
+    HeadIn<HD> in;
+    head_load<HD>(src, bias, nw, rope, d, in);
+    head_prep<HD>(in, d, row);
 }
 
 // K/V rows of this thread's slot (positions t0 + sl + NS*it, clamped to pos), issued early.

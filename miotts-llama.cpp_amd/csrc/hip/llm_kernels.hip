@@ -314,7 +314,19 @@ __global__ __launch_bounds__(AttCfg<HD>::NT) void k_attention(LlmDims d, const f
     if (t0 > pos || b.st->done) return;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const float2 *rope = b.rope + (size_t)pos * (HD / 2);
-    // K/V rows of this thread first (row `pos` is never consumed from the cache)
+    // q heads (waves 0..G-1) and, for the chunk owning `pos`, the new k/v row (wave G); the
+    // loads of each wave's first head go out before its K/V rows (row `pos` is never consumed
+    // from the cache)
+    const bool owner = pos < t0 + ATT_CHUNK;
+    auto head_src = [&](int hh, HeadIn<HD> &in) {
+        const bool isk = hh == G;
+        const size_t so = isk ? (size_t)(d.n_head + kvh) * HD : (size_t)(kvh * G + hh) * HD;
+        const size_t vo = (size_t)(d.n_head + d.n_kv + kvh) * HD;
+        head_load<HD>(b.qkv + so, bqkv ? bqkv + so : nullptr, isk ? k_norm : q_norm, rope, d, in,
+                      isk ? b.qkv + vo : nullptr, isk && bqkv ? bqkv + vo : nullptr);
+    };
+    HeadIn<HD> hin;
+    if (wave < G + (owner ? 1 : 0)) head_src(wave, hin);
 #if MIO_ATT_MFMA
     h8 kr[A::VI], vr[A::VI];
     kv_issue<HD>(kc + (size_t)kvh * d.n_ctx * HD, vc + (size_t)kvh * d.n_ctx * HD, t0, pos, kr, vr);
@@ -324,28 +336,17 @@ __global__ __launch_bounds__(AttCfg<HD>::NT) void k_attention(LlmDims d, const f
 #endif
     MIO_TRACE(b, 1);
     MIO_TL_MARK1(b);
-    // q heads (waves 0..G-1) and, for the chunk owning `pos`, the new k/v row
-    const bool owner = pos < t0 + ATT_CHUNK;
     for (int hh = wave; hh < G + (owner ? 1 : 0); hh += C::NW) {
         const bool isk = hh == G;
-        float vv[PER];
-        if (isk) {
-            const size_t vo = (size_t)(d.n_head + d.n_kv + kvh) * HD;
-#pragma unroll
-            for (int i = 0; i < PER; ++i) {
-                vv[i] = b.qkv[vo + lane + 64 * i];
-                if (bqkv) vv[i] = vv[i] + bqkv[vo + lane + 64 * i];
-            }
-        }
-        const size_t so = isk ? (size_t)(d.n_head + kvh) * HD : (size_t)(kvh * G + hh) * HD;
-        prep_head<HD>(b.qkv + so, bqkv ? bqkv + so : nullptr, isk ? k_norm : q_norm, rope, d, isk ? knew : qs[hh]);
+        if (hh != wave) head_src(hh, hin);
+        head_prep<HD>(hin, d, isk ? knew : qs[hh]);
         if (isk) {
             _Float16 *kd = kc + ((size_t)kvh * d.n_ctx + pos) * HD;
             _Float16 *vd = vc + ((size_t)kvh * d.n_ctx + pos) * HD;
 #pragma unroll
             for (int i = 0; i < PER; ++i) {
                 const int p = lane + 64 * i;
-                const float vr16 = f16r(vv[i]);
+                const float vr16 = f16r(hin.vv[i]);
                 vnew[p] = vr16;
                 kd[p] = (_Float16)knew[p];
                 vd[p] = (_Float16)vr16;
@@ -363,7 +364,9 @@ __global__ __launch_bounds__(AttCfg<HD>::NT) void k_attention(LlmDims d, const f
 #endif
     }
 #if MIO_ATT_MFMA
+    MIO_TRACE(b, 6);  // this wave's head prepared
     kv_stage<HD>(kr, vr, owner ? pos - t0 : -1, img, img + A::IMG);
+    MIO_TRACE(b, 7);  // this thread's K / V rows arrived and staged
     lds_barrier();
     MIO_TRACE(b, 2);
     MIO_TL_MARK(b, 2);

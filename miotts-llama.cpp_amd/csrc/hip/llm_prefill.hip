@@ -775,6 +775,18 @@ __global__ __launch_bounds__(AttCfg<HD>::NT) void k_bt_attention(LlmDims d, cons
     _Float16 *kc = kcache + kvo, *vc = vcache + kvo;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const float2 *rope = pb.rope + (size_t)pos * (HD / 2);
+    const float *qkv = pb.qkv + (size_t)t * (d.n_head + 2 * d.n_kv) * HD;
+    const bool owner = pos < t0 + ATT_CHUNK;
+    // the loads of each wave's first head go out before its K/V rows (as k_attention)
+    auto head_src = [&](int hh, HeadIn<HD> &in) {
+        const bool isk = hh == G;
+        const size_t so = isk ? (size_t)(d.n_head + kvh) * HD : (size_t)(kvh * G + hh) * HD;
+        const size_t vo = (size_t)(d.n_head + d.n_kv + kvh) * HD;
+        head_load<HD>(qkv + so, bqkv ? bqkv + so : nullptr, isk ? k_norm : q_norm, rope, d, in,
+                      isk ? qkv + vo : nullptr, isk && bqkv ? bqkv + vo : nullptr);
+    };
+    HeadIn<HD> hin;
+    if (wave < G + (owner ? 1 : 0)) head_src(wave, hin);
 #if MIO_ATT_MFMA
     h8 kr[A::VI], vr[A::VI];
     kv_issue<HD>(kc, vc, t0, pos, kr, vr);  // row pos is staged from LDS below
@@ -782,26 +794,15 @@ __global__ __launch_bounds__(AttCfg<HD>::NT) void k_bt_attention(LlmDims d, cons
     h8 kr[C::IT], vr[C::IT];
     load_kv_rows<HD>(kc, vc, t0, pos, kr, vr);  // row pos comes from LDS below
 #endif
-    const float *qkv = pb.qkv + (size_t)t * (d.n_head + 2 * d.n_kv) * HD;
-    const bool owner = pos < t0 + ATT_CHUNK;
     for (int hh = wave; hh < G + (owner ? 1 : 0); hh += C::NW) {
         const bool isk = hh == G;
-        float vv[PER];
-        if (isk) {
-            const size_t vo = (size_t)(d.n_head + d.n_kv + kvh) * HD;
-#pragma unroll
-            for (int i = 0; i < PER; ++i) {
-                vv[i] = qkv[vo + lane + 64 * i];
-                if (bqkv) vv[i] = vv[i] + bqkv[vo + lane + 64 * i];
-            }
-        }
-        const size_t so = isk ? (size_t)(d.n_head + kvh) * HD : (size_t)(kvh * G + hh) * HD;
-        prep_head<HD>(qkv + so, bqkv ? bqkv + so : nullptr, isk ? k_norm : q_norm, rope, d, isk ? knew : qs[hh]);
+        if (hh != wave) head_src(hh, hin);
+        head_prep<HD>(hin, d, isk ? knew : qs[hh]);
         if (isk) {
 #pragma unroll
             for (int i = 0; i < PER; ++i) {
                 const int p = lane + 64 * i;
-                const float vr16 = f16r(vv[i]);
+                const float vr16 = f16r(hin.vv[i]);
                 vnew[p] = vr16;
                 kc[(size_t)pos * HD + p] = (_Float16)knew[p];
                 vc[(size_t)pos * HD + p] = (_Float16)vr16;
