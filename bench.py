@@ -48,7 +48,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 ROOF_POS = 400  # decode position of the roofline timeline / kernel timings (and of the PMC run)
 KERNEL_NAMES = {0: "k_attn_in", 1: "k_attention", 2: "k_attn_out", 3: "k_ffn_in", 4: "k_ffn_down",
                 6: "k_lm_head", 8: "k_conv_in", 9: "k_conv_out"}
-PRESETS = {2: "MioTTS-0.1B Q8_0", 3: "MioTTS-1.7B Q4_K_M", 4: "MioTTS-2.6B Q8_0"}
+PRESETS = {2: "MioTTS-0.1B Q8_0", 3: "MioTTS-1.7B Q4_K_M", 4: "MioTTS-2.6B Q8_0", 12: "MioTTS-1.7B BF16"}
 PROMPT = "こんにちは、今日はいい天気ですね。"  # README.md:83, SURVEY 8(d)
 
 
@@ -518,7 +518,9 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": ("int8-dot (q8_0 x q8_0)" if "Q8_0" in model else "int8-dot (q4_K/q6_K x q8_K)")
+        "dtype": ("int8-dot (q8_0 x q8_0)" if "Q8_0" in model
+                  else ("bf16-dot2 (bf16 x bf16-rounded activation, f32 sums)" if "BF16" in model
+                        else "int8-dot (q4_K/q6_K x q8_K)"))
                  + " + f32/f16 codec",
         "data": "synthetic",
         "config": {"workload": (f"{model} {'single utterance' if B == 1 else f'{B} utterances decoded together'}"

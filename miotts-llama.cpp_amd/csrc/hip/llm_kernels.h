@@ -114,8 +114,9 @@ struct LlmBuffers {
 // chat-template prompts of the benchmarks (≈70 tokens) in one chunk: a 64-token chunk left
 // their last few tokens to a second, dot4 weight pass (+1.5 ms per 68-token prompt).
 // Memory: the chunk's attention partials (PrefillBuffers.part) are kPrefillB x n_head x
-// ceil(n_ctx / kAttChunk) x (hd + 4) floats: 17 MB for the 1.7B model at n_ctx 2048, 277 MB at
-// the 32768 maximum (of 288 GB).
+// ceil(n_ctx / kAttChunk) x (hd + 4) floats: at the default 64-position chunks 35 MB for the 1.7B
+// model at n_ctx 2048 and 554 MB at the 32768 maximum (of 288 GB); the merged outputs pb.att
+// add kPrefillB x n_head x hd floats (1 MB) and the tickets pb.att_cnt kPrefillB x n_kv ints.
 constexpr int kPrefillB = 128;
 // The same multi-token layers run the batched decode step of up to kBatchMax utterances.
 constexpr int kBatchMax = 16;
@@ -140,8 +141,10 @@ struct PrefillBuffers {
     size_t seq_ring;     // ring elements per sequence
     char *act;           // [kPrefillB] quantized activation records of the next matvec
 };
-// bytes of the act records (pb.act) for K up to k_max
+// bytes of the act records (pb.act) for K up to k_max (BF16 weights: pass prefill_rec_k)
 size_t prefill_act_bytes(int k_max);
+// K of the act record layout for a weight type (2K for BF16: K bf16 values)
+int prefill_rec_k(int K, int type);
 
 // One chunk of nt <= kPrefillB tokens (ids at tokens[p0 + t], positions/sequences from
 // pb.pos / pb.seq) through every layer: embedding, K/V rows, residual streams in pb.x.
@@ -164,8 +167,8 @@ struct BatchBuffers {
 void launch_batch_step(const LlmDims &d, const LayerW *layers, int n_layer, _Float16 *kcache, _Float16 *vcache,
                        const float *out_norm, const QMat &lm, const QMat &tok_embd, const PrefillBuffers &pb,
                        const BatchBuffers &bb, int B, hipStream_t s);
-// B streams fit one batched step (B <= kBatchMax and the lm_head's LDS)
-bool batch_supported(const LlmDims &d, int B);
+// B streams fit one batched step (B <= kBatchMax and the lm_head's LDS for its weight type)
+bool batch_supported(const LlmDims &d, int B, int lm_type);
 // Embedding of st[b].token into pb.x[b] for every sequence (decode start).
 void launch_batch_embed(const LlmDims &d, const QMat &tok_embd, const PrefillBuffers &pb, const BatchBuffers &bb,
                         int B, hipStream_t s);

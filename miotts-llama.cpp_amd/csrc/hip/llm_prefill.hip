@@ -42,6 +42,10 @@ __host__ __device__ inline size_t act_bytes(int K) {
     return ((size_t)K + (size_t)(K / 32 + 8) * 4 + (size_t)(K / 16 + 8) * 2 + 15) & ~(size_t)15;
 }
 __host__ __device__ inline size_t act_base(int) { return 0; }
+// K of the act record layout for a weight type: BF16 weights take the activation as K bf16
+// values (ggml's vec_dot_bf16 operand, 2 bytes each), stored in the qs area of a record laid out
+// for 2K (the d / bs areas then go unused)
+__host__ __device__ constexpr int rec_k(int K, int type) { return type == 30 ? 2 * K : K; }
 __host__ __device__ inline size_t pf_lds_bytes(int K, int nt, int rpw) {
     return act_base(K) + act_bytes(K) * nt + (size_t)MW * nt * rpw * 4;
 }
@@ -200,10 +204,10 @@ __device__ __forceinline__ void stream_rows_bx(const QMat W0, const QMat W1, int
     constexpr int RU = CfgB<T, NP, NM>::RU, U = CfgB<T, NP, NM>::U;
     constexpr int TT = XRedCfg<NP>::TT, TB = XRedCfg<NP>::TB;
     constexpr int N = TB * RU * NM;             // totals per group: index ((t * RU + ri) * NM + m)
-    constexpr int LB = T == 8 ? 0 : 3;          // first tree level (K-quants: lanes 8k+7)
+    constexpr int LB = (T == 8 || T == 30) ? 0 : 3;  // first tree level (K-quants: lanes 8k+7)
     constexpr int NF = N >> (6 - LB) > NM ? N >> (6 - LB) : NM;  // totals per lane at the end
     constexpr int SL = __builtin_ctz(N / NF);   // scatter levels
-    const int K = W0.k;
+    const int K = W0.k, KR = rec_k(K, T);
     const int lane = threadIdx.x & 63;
     if (hi <= lo) return;
     // the lane's first total after the scatter (level k at lane bit LB + k halves the index
@@ -226,7 +230,7 @@ __device__ __forceinline__ void stream_rows_bx(const QMat W0, const QMat W1, int
                         ALane al[TT];
 #pragma unroll
                         for (int j = 0; j < TT; ++j)
-                            al[j] = load_alane<T>(carve_t(smem, K, min(tb + t0 + j, nt - 1)).a, K, p);
+                            al[j] = load_alane<T>(carve_t(smem, KR, min(tb + t0 + j, nt - 1)).a, K, p);
 #pragma unroll
                         for (int ri = 0; ri < RU; ++ri) {
                             if (ri < nr) {
@@ -277,7 +281,7 @@ __device__ __forceinline__ void stream_rows_bu(const QMat W0, const QMat W1, int
                                                Frag (&A)[CfgB<T, NP, NM>::U], Frag (&B)[CfgB<T, NP, NM>::U], char *smem,
                                                int nt, Epi &&epi, int split = INT_MAX) {
     constexpr int RU = CfgB<T, NP, NM>::RU, U = CfgB<T, NP, NM>::U;
-    const int K = W0.k;
+    const int K = W0.k, KR = rec_k(K, T);
     if (hi <= lo) return;
     // TT tokens per iteration: their activation loads are in flight together and their dot
     // / reduction chains interleave (the weight decode is shared); rows of the group past hi
@@ -295,7 +299,7 @@ __device__ __forceinline__ void stream_rows_bu(const QMat W0, const QMat W1, int
             for (int p = 0; p < NP; ++p) {
                 ALane al[TT];
 #pragma unroll
-                for (int j = 0; j < TT; ++j) al[j] = load_alane<T>(carve_t(smem, K, min(t0 + j, nt - 1)).a, K, p);
+                for (int j = 0; j < TT; ++j) al[j] = load_alane<T>(carve_t(smem, KR, min(t0 + j, nt - 1)).a, K, p);
 #pragma unroll
                 for (int ri = 0; ri < RU; ++ri) {
                     if (ri < nr) {
@@ -489,21 +493,23 @@ __device__ __forceinline__ void xpre_quant(const XPre &xp, int K, float eps, boo
 
 // One workgroup per token t: MODE 0 RMSNorm(src[t]) * norm_w, 1 src[t] as is (the attention
 // output pb.att, h); quantized (Q8_K / Q8_0) into the token's act record.
+// ak = akind of the consuming weights (0 Q8_0, 1 Q8_K, 2 BF16: the record then holds K bf16
+// values and is laid out for rec_k = 2K)
 template <int NP, int MODE>
-__global__ __launch_bounds__(MT) void k_bt_quant(LlmDims d, const float *src, int K, const float *norm_w, int kq,
+__global__ __launch_bounds__(MT) void k_bt_quant(LlmDims d, const float *src, int K, const float *norm_w, int ak,
                                                  PrefillBuffers pb) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int t = blockIdx.x;
     // the quantizers store straight into the token's global record (its layout is the LDS
     // record's: qs | d | bs), no LDS staging + barrier + copy; LDS keeps the reduction scratch
     Smem s = carve(smem, K);
-    s.a = carve_t(pb.act, K, t).a;
+    s.a = carve_t(pb.act, ak == 2 ? 2 * K : K, t).a;
     XRegs<NP> xr;
     load_x(src + (size_t)t * K, MODE == 0 ? norm_w : nullptr, K, xr);
     if constexpr (MODE == 0)
-        rmsnorm_quant(xr, K, d.eps, kq != 0, s);
+        rmsnorm_quant(xr, K, d.eps, ak, s);
     else
-        plain_quant(xr, K, kq != 0, s);
+        plain_quant(xr, K, ak, s);
 }
 
 // MODE 1 (plain rows, K % 256 == 0) split over 2048-element chunks: grid (nt, chunks). Q8_K
@@ -595,7 +601,7 @@ template <int NP, int TQ, int TV, int FQ = 0>
 __global__ __launch_bounds__(MT) void k_pf_attn_in(LlmDims d, const float *norm_w, QMat wq, QMat wk, QMat wv,
                                                    int g_qk, PrefillBuffers pb, int nt) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int K = d.n_embd, QD = (d.n_head + 2 * d.n_kv) * d.hd;
+    const int K = d.n_embd, QD = (d.n_head + 2 * d.n_kv) * d.hd, KR = rec_k(K, TQ);
     const int lane = threadIdx.x & 63;
     const int o1 = wq.rows, o2 = wq.rows + wk.rows;
     Frag ga[CfgB<TQ, NP, 1>::U], gb[CfgB<TQ, NP, 1>::U];
@@ -605,7 +611,7 @@ __global__ __launch_bounds__(MT) void k_pf_attn_in(LlmDims d, const float *norm_
         if constexpr (FQ == 2)
             xpre_quant(xp, K, d.eps, TQ != 8, smem, nt);
         else
-            prologue_copy(pb.act, K, smem, nt);
+            prologue_copy(pb.act, KR, smem, nt);
     };
     int lo, hi;
     if ((int)blockIdx.x < g_qk) {
@@ -843,17 +849,17 @@ __global__ __launch_bounds__(AttCfg<HD>::NT) void k_bt_attention(LlmDims d, cons
 template <int NP, int T>
 __global__ __launch_bounds__(MT, MIO_BT_MINB) void k_pf_attn_out(LlmDims d, QMat wo, PrefillBuffers pb, int nt, int rpw) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int K = wo.k, E = d.n_embd;
+    const int K = wo.k, E = d.n_embd, KR = rec_k(K, T);
     int lo, hi;
     wave_range(d, wo.rows, lo, hi);
     const Resid xr = load_resid_b(pb.x, E, lo, hi, nt, rpw);
     ActPre<NP> ap;
-    act_issue<NP>(pb.act, K, nt, ap);
+    act_issue<NP>(pb.act, KR, nt, ap);
     Frag ga[CfgB<T, NP, 1>::U], gb[CfgB<T, NP, 1>::U];
     load_first_b<T, NP, 1>(wo, wo, lo, hi, ga, gb);
-    float *res = resid_lds(smem, K, nt, rpw);
+    float *res = resid_lds(smem, KR, nt, rpw);
     store_resid_b(xr, res, nt, rpw);
-    act_store<NP>(ap, pb.act, K, smem, nt);
+    act_store<NP>(ap, pb.act, KR, smem, nt);
     stream_rows_b<T, NP, 1>(wo, wo, lo, hi, ga, gb, smem, nt, [&](int row, int t, float v, float) {
         const float r = res[t * rpw + row - lo];
         pb.x[(size_t)t * E + row] = v + r;
@@ -865,7 +871,7 @@ template <int NP, int T, int FQ = 0>
 __global__ __launch_bounds__(MT, MIO_BT_MINB) void k_pf_ffn_in(LlmDims d, const float *norm_w, QMat gate, QMat up,
                                                   PrefillBuffers pb, int nt) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int K = d.n_embd;
+    const int K = d.n_embd, KR = rec_k(K, T);
     int lo, hi;
     wave_range(d, gate.rows, lo, hi);
     ActPre<NP> ap;
@@ -873,13 +879,13 @@ __global__ __launch_bounds__(MT, MIO_BT_MINB) void k_pf_ffn_in(LlmDims d, const 
     if constexpr (FQ == 2)
         xpre_issue(pb.x, norm_w, K, nt, xp);
     else
-        act_issue<NP>(pb.act, K, nt, ap);
+        act_issue<NP>(pb.act, KR, nt, ap);
     Frag ga[CfgB<T, NP, 2>::U], gb[CfgB<T, NP, 2>::U];
     load_first_b<T, NP, 2>(gate, up, lo, hi, ga, gb);
     if constexpr (FQ == 2)
         xpre_quant(xp, K, d.eps, T != 8, smem, nt);
     else
-        act_store<NP>(ap, pb.act, K, smem, nt);
+        act_store<NP>(ap, pb.act, KR, smem, nt);
     stream_rows_b<T, NP, 2>(gate, up, lo, hi, ga, gb, smem, nt, [&](int row, int t, float g, float u) {
         pb.h[(size_t)t * d.n_ff + row] = silu_f(g) * u;
     });
@@ -888,17 +894,17 @@ __global__ __launch_bounds__(MT, MIO_BT_MINB) void k_pf_ffn_in(LlmDims d, const 
 template <int NP, int T>
 __global__ __launch_bounds__(MT) void k_pf_ffn_down(LlmDims d, QMat down, PrefillBuffers pb, int nt, int rpw) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int K = down.k, E = d.n_embd;
+    const int K = down.k, E = d.n_embd, KR = rec_k(K, T);
     int lo, hi;
     wave_range(d, down.rows, lo, hi);
     const Resid rr = load_resid_b(pb.x, E, lo, hi, nt, rpw);
     ActPre<NP> ap;
-    act_issue<NP>(pb.act, K, nt, ap);
+    act_issue<NP>(pb.act, KR, nt, ap);
     Frag ga[CfgB<T, NP, 1>::U], gb[CfgB<T, NP, 1>::U];
     load_first_b<T, NP, 1>(down, down, lo, hi, ga, gb);
-    float *res = resid_lds(smem, K, nt, rpw);
+    float *res = resid_lds(smem, KR, nt, rpw);
     store_resid_b(rr, res, nt, rpw);
-    act_store<NP>(ap, pb.act, K, smem, nt);
+    act_store<NP>(ap, pb.act, KR, smem, nt);
     stream_rows_b<T, NP, 1>(down, down, lo, hi, ga, gb, smem, nt, [&](int row, int t, float v, float) {
         const float r = res[t * rpw + row - lo];
         pb.x[(size_t)t * E + row] = v + r;
@@ -922,16 +928,16 @@ __global__ __launch_bounds__(MT) void k_bt_lm_head(LlmDims d, const float *norm_
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __shared__ float bs_[MW];
     __shared__ int bi_[MW];
-    const int K = d.n_embd;
+    const int K = d.n_embd, KR = rec_k(K, T);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     int lo, hi;
     wave_range(d, lm.rows, lo, hi);
     ActPre<NP> ap;
-    act_issue<NP>(pb.act, K, nt, ap);
+    act_issue<NP>(pb.act, KR, nt, ap);
     Frag ga[CfgB<T, NP, 1>::U], gb[CfgB<T, NP, 1>::U];
     load_first_b<T, NP, 1>(lm, lm, lo, hi, ga, gb);
-    act_store<NP>(ap, pb.act, K, smem, nt);
-    float *vals = reinterpret_cast<float *>(smem + pf_lds_bytes(K, nt, 0)) + (size_t)wave * nt * 128;
+    act_store<NP>(ap, pb.act, KR, smem, nt);
+    float *vals = reinterpret_cast<float *>(smem + pf_lds_bytes(KR, nt, 0)) + (size_t)wave * nt * 128;
     stream_rows_b<T, NP, 1>(lm, lm, lo, hi, ga, gb, smem, nt, [&](int row, int t, float v, float) {
         vals[t * 128 + row - lo] = v;
     });
@@ -1104,23 +1110,24 @@ PrefillBuffers shifted(const LlmDims &d, const PrefillBuffers &pb, int t, int K)
     return q;
 }
 
-// act records of nt tokens (k_bt_quant): mode 0 RMSNorm(src) * w, 1 src
-void launch_quant(const LlmDims &d, int mode, const float *src, int K, const float *w, bool kq,
+// act records of nt tokens (k_bt_quant): mode 0 RMSNorm(src) * w, 1 src; ak = akind of the
+// consuming weights (0 Q8_0, 1 Q8_K, 2 BF16)
+void launch_quant(const LlmDims &d, int mode, const float *src, int K, const float *w, int ak,
                   const PrefillBuffers &pb, int nt, hipStream_t s) {
     // plain rows: one workgroup per (token, 2048 elements) instead of per token (MIO_QSPLIT=0:
     // per token, for A/B)
     static const bool qsplit = !(getenv("MIO_QSPLIT") && getenv("MIO_QSPLIT")[0] == '0');
-    if (mode == 1 && qsplit && K % 256 == 0) {
-        hipLaunchKernelGGL(k_bt_quant_split, dim3(nt, (K + 2047) / 2048), dim3(MT), 0, s, src, K, (int)kq, pb);
+    if (mode == 1 && qsplit && K % 256 == 0 && ak != 2) {
+        hipLaunchKernelGGL(k_bt_quant_split, dim3(nt, (K + 2047) / 2048), dim3(MT), 0, s, src, K, ak, pb);
         return;
     }
     const int np = pick_np(K);
     auto go = [&]<int NP>() {
         const size_t lds = smem_bytes(K);
         if (mode == 0)
-            hipLaunchKernelGGL((k_bt_quant<NP, 0>), dim3(nt), dim3(MT), lds, s, d, src, K, w, (int)kq, pb);
+            hipLaunchKernelGGL((k_bt_quant<NP, 0>), dim3(nt), dim3(MT), lds, s, d, src, K, w, ak, pb);
         else
-            hipLaunchKernelGGL((k_bt_quant<NP, 1>), dim3(nt), dim3(MT), lds, s, d, src, K, w, (int)kq, pb);
+            hipLaunchKernelGGL((k_bt_quant<NP, 1>), dim3(nt), dim3(MT), lds, s, d, src, K, w, ak, pb);
     };
     if (np == 1)
         go.template operator()<1>();
@@ -1149,6 +1156,7 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
     const size_t layer_kv = (size_t)d.n_kv * d.n_ctx * d.hd;
     const int G = d.n_head / d.n_kv;
     // sub-launches over token ranges that fit LDS: f(t_off, n, shifted buffers)
+    // (K = the act record's K, rec_k: twice the row length for BF16 weights)
     auto over_tokens = [&](int K, int rpw, auto &&f) {
         const int per = tokens_per_launch(K, nt, rpw);
         for (int t = 0; t < nt; t += per) f(t, nt - t < per ? nt - t : per, shifted(d, pb, t, K));
@@ -1175,7 +1183,9 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
         const bool q8_pair = d.n_embd % 256 == 0 && d.n_embd <= 2048 && (d.n_head * d.hd) % 256 == 0 &&
                              d.n_head * d.hd <= 2048;
         const int mask = mmq_mask >= 0 ? mmq_mask : (type == 8 ? (q8_pair ? 7 : 1) : 15);
-        return mmq_all || (nt <= 8 && mmq_env < 0 && ((mask >> kind) & 1));
+        // BF16 weights: the streaming dot engine (v_dot2 in the decode's lane order) at any token
+        // count; the matrix-core matmuls are int8
+        return type != 30 && (mmq_all || (nt <= 8 && mmq_env < 0 && ((mask >> kind) & 1)));
     };
     const bool mmq = mmq_all;
     // MIO_BT_FQ (bits: 1 attn_in, 2 ffn_in; default below): launches of <= 8 tokens over K <= 2048
@@ -1189,7 +1199,7 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
     auto fq2 = [&](int kind, int type) {
         const bool q8_pair = d.n_embd % 256 == 0 && d.n_embd <= 2048;
         const bool on = fq2_env >= 0 ? ((fq2_env >> kind) & 1) != 0 : (type == 8 && (kind == 0 || !q8_pair));
-        return !mmq && nt <= MW && pick_np(d.n_embd) == 1 && on;
+        return !mmq && nt <= MW && pick_np(d.n_embd) == 1 && on && type != 30;
     };
     static const bool att_q_env = !(getenv("MIO_ATT_Q") && getenv("MIO_ATT_Q")[0] == '0');
     // MIO_BT_ATT=0: the batched decode step uses k_pf_rope + k_pf_attention (A/B)
@@ -1204,7 +1214,7 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
             // decode step's matvec at any token count).
             const int n = d.n_embd;
             float *ring = pb.ring + (size_t)il * kConvSlots * n;
-            launch_quant(d, 0, pb.x, n, L.attn_norm, L.in_proj.type != 8, pb, nt, s);
+            launch_quant(d, 0, pb.x, n, L.attn_norm, akind(L.in_proj.type), pb, nt, s);
             const MmqSeg sg{L.in_proj, mmq_tiles(L.in_proj.rows), 0};
             launch_mmq(&sg, &L.in_proj.type, 1, MMQ_STORE, MmqArgs{pb.act, act_bytes(n), n, nt, pb.qkv, 3 * n, {}}, s);
             const int np = pick_np(n);
@@ -1223,11 +1233,12 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
             // the attention merger writes the O matvec's activation records when every kv head's
             // G * hd outputs are whole quantization blocks (MIO_ATT_Q=0: a k_bt_quant launch)
             const int gh = G * d.hd;
-            const int att_q = !att_q_env ? -1
-                              : (L.wo.type == 8 ? (gh % 32 == 0 ? 0 : -1) : (gh % 256 == 0 ? 1 : -1));
+            const int att_q = !att_q_env || L.wo.type == 30
+                                  ? -1
+                                  : (L.wo.type == 8 ? (gh % 32 == 0 ? 0 : -1) : (gh % 256 == 0 ? 1 : -1));
             const bool fa = fq2(0, L.wq.type);
             if (!fa)
-                launch_quant(d, 0, pb.x, d.n_embd, L.attn_norm, L.wq.type != 8, pb, nt, s);
+                launch_quant(d, 0, pb.x, d.n_embd, L.attn_norm, akind(L.wq.type), pb, nt, s);
             if (!fa && use_mmq(0, L.wq.type)) {
                 const MmqSeg sg[3] = {{L.wq, mmq_tiles(L.wq.rows), 0}, {L.wk, mmq_tiles(L.wk.rows), L.wq.rows},
                                       {L.wv, mmq_tiles(L.wv.rows), L.wq.rows + L.wk.rows}};
@@ -1236,11 +1247,12 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
             } else {
                 int GW, g_qk;
                 attn_in_grid(d, L, GW, g_qk);
-                over_tokens(d.n_embd, 0, [&](int, int n, const PrefillBuffers &q) {
-                    const size_t lds = pf_lds_bytes(d.n_embd, n, 0);
-                    dispatch_nt<false>(d.n_embd, L.wq.type, [&]<int NP, int TQ>() {
+                const int KR = rec_k(d.n_embd, L.wq.type);
+                over_tokens(KR, 0, [&](int, int n, const PrefillBuffers &q) {
+                    const size_t lds = pf_lds_bytes(KR, n, 0);
+                    dispatch_nt<true>(d.n_embd, L.wq.type, [&]<int NP, int TQ>() {
                         auto go = [&]<int TV>() {
-                            if constexpr (NP == 1) {
+                            if constexpr (NP == 1 && TQ != 30) {
                                 if (fa) {
                                     allow_lds(k_pf_attn_in<NP, TQ, TV, 2>);
                                     hipLaunchKernelGGL((k_pf_attn_in<NP, TQ, TV, 2>), dim3(GW), dim3(MT), lds, s, d,
@@ -1252,8 +1264,8 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
                             hipLaunchKernelGGL((k_pf_attn_in<NP, TQ, TV>), dim3(GW), dim3(MT), lds, s, d, L.attn_norm,
                                                L.wq, L.wk, L.wv, g_qk, q, n);
                         };
-                        if constexpr (TQ == 8) {
-                            go.template operator()<8>();
+                        if constexpr (TQ == 8 || TQ == 30) {
+                            go.template operator()<TQ>();
                         } else {
                             if (L.wv.type == 14)
                                 go.template operator()<14>();
@@ -1285,7 +1297,7 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
                 else
                     launch_pf_attention<64>(G, grid, s, d, kc, vc, pb, att_q);
             }
-            if (att_q < 0) launch_quant(d, 1, pb.att, L.wo.k, nullptr, L.wo.type != 8, pb, nt, s);
+            if (att_q < 0) launch_quant(d, 1, pb.att, L.wo.k, nullptr, akind(L.wo.type), pb, nt, s);
             if (use_mmq(1, L.wo.type)) {
                 const MmqSeg sg{L.wo, mmq_tiles(L.wo.rows), 0};
                 launch_mmq(&sg, &L.wo.type, 1, MMQ_RESID, MmqArgs{pb.act, act_bytes(L.wo.k), L.wo.k, nt, pb.x, d.n_embd, {}},
@@ -1293,10 +1305,11 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
             } else {
                 const LlmDims dw = bt_wgm(d, L.wo.k);
                 const int grid = matvec_grid(dw, L.wo.rows), rpw = rows_per_wave(L.wo.rows, grid);
-                over_tokens(L.wo.k, rpw, [&](int, int n, const PrefillBuffers &q) {
-                    dispatch_nt<false>(L.wo.k, L.wo.type, [&]<int NP, int T>() {
+                const int KR = rec_k(L.wo.k, L.wo.type);
+                over_tokens(KR, rpw, [&](int, int n, const PrefillBuffers &q) {
+                    dispatch_nt<true>(L.wo.k, L.wo.type, [&]<int NP, int T>() {
                         allow_lds(k_pf_attn_out<NP, T>);
-                        hipLaunchKernelGGL((k_pf_attn_out<NP, T>), dim3(grid), dim3(MT), pf_lds_bytes(L.wo.k, n, rpw), s,
+                        hipLaunchKernelGGL((k_pf_attn_out<NP, T>), dim3(grid), dim3(MT), pf_lds_bytes(KR, n, rpw), s,
                                            dw, L.wo, q, n, rpw);
                     });
                 });
@@ -1304,7 +1317,7 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
         }
         const bool ff = fq2(1, L.gate.type);
         if (!ff)
-            launch_quant(d, 0, pb.x, d.n_embd, L.ffn_norm, L.gate.type != 8, pb, nt, s);
+            launch_quant(d, 0, pb.x, d.n_embd, L.ffn_norm, akind(L.gate.type), pb, nt, s);
         if (!ff && use_mmq(2, L.gate.type)) {
             const MmqSeg sg{L.gate, mmq_tiles(L.gate.rows), 0};
             launch_mmq(&sg, &L.gate.type, 1, MMQ_SWIGLU,
@@ -1312,9 +1325,10 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
         } else {
             const LlmDims dw = bt_wgm(d, d.n_embd);
             const int grid = matvec_grid(dw, L.gate.rows);
-            over_tokens(d.n_embd, 0, [&](int, int n, const PrefillBuffers &q) {
-                dispatch_nt<false>(d.n_embd, L.gate.type, [&]<int NP, int T>() {
-                    if constexpr (NP == 1) {
+            const int KR = rec_k(d.n_embd, L.gate.type);
+            over_tokens(KR, 0, [&](int, int n, const PrefillBuffers &q) {
+                dispatch_nt<true>(d.n_embd, L.gate.type, [&]<int NP, int T>() {
+                    if constexpr (NP == 1 && T != 30) {
                         if (ff) {
                             allow_lds(k_pf_ffn_in<NP, T, 2>);
                             hipLaunchKernelGGL((k_pf_ffn_in<NP, T, 2>), dim3(grid), dim3(MT), pf_lds_bytes(d.n_embd, n, 0),
@@ -1323,22 +1337,23 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
                         }
                     }
                     allow_lds(k_pf_ffn_in<NP, T>);
-                    hipLaunchKernelGGL((k_pf_ffn_in<NP, T>), dim3(grid), dim3(MT), pf_lds_bytes(d.n_embd, n, 0), s, dw,
+                    hipLaunchKernelGGL((k_pf_ffn_in<NP, T>), dim3(grid), dim3(MT), pf_lds_bytes(KR, n, 0), s, dw,
                                        L.ffn_norm, L.gate, L.up, q, n);
                 });
             });
         }
-        launch_quant(d, 1, pb.h, L.down.k, nullptr, L.down.type != 8, pb, nt, s);
+        launch_quant(d, 1, pb.h, L.down.k, nullptr, akind(L.down.type), pb, nt, s);
         if (use_mmq(3, L.down.type)) {
             const MmqSeg sg{L.down, mmq_tiles(L.down.rows), 0};
             launch_mmq(&sg, &L.down.type, 1, MMQ_RESID,
                        MmqArgs{pb.act, act_bytes(L.down.k), L.down.k, nt, pb.x, d.n_embd, {}}, s);
         } else {
             const int grid = matvec_grid(d, L.down.rows), rpw = rows_per_wave(L.down.rows, grid);
-            over_tokens(L.down.k, rpw, [&](int, int n, const PrefillBuffers &q) {
-                dispatch_nt<false>(L.down.k, L.down.type, [&]<int NP, int T>() {
+            const int KR = rec_k(L.down.k, L.down.type);
+            over_tokens(KR, rpw, [&](int, int n, const PrefillBuffers &q) {
+                dispatch_nt<true>(L.down.k, L.down.type, [&]<int NP, int T>() {
                     allow_lds(k_pf_ffn_down<NP, T>);
-                    hipLaunchKernelGGL((k_pf_ffn_down<NP, T>), dim3(grid), dim3(MT), pf_lds_bytes(L.down.k, n, rpw),
+                    hipLaunchKernelGGL((k_pf_ffn_down<NP, T>), dim3(grid), dim3(MT), pf_lds_bytes(KR, n, rpw),
                                        s, d, L.down, q, n, rpw);
                 });
             });
@@ -1357,6 +1372,7 @@ void launch_prefill_chunk(const LlmDims &d, const LayerW *layers, int n_layer, _
 }
 
 size_t prefill_act_bytes(int k_max) { return act_bytes(k_max) * kPrefillB; }
+int prefill_rec_k(int K, int type) { return rec_k(K, type); }
 
 // parity entry (mio_hip_debug_mmq): nt activation rows x[t][K] quantized as the decode does
 // (plain_quant), then y[t][rows] = W x[t] on the int8-MFMA matmul
@@ -1366,26 +1382,28 @@ void launch_debug_mmq(const QMat &W, const QMat &up, int mode, const float *x, i
     LlmDims d{};
     PrefillBuffers pb{};
     pb.act = act;
-    launch_quant(d, 1, x, W.k, nullptr, W.type != 8, pb, nt, s);
+    launch_quant(d, 1, x, W.k, nullptr, akind(W.type), pb, nt, s);
     const MmqSeg sg{W, mmq_tiles(W.rows), 0};
     launch_mmq(&sg, &W.type, 1, mode, MmqArgs{act, act_bytes(W.k), W.k, nt, y, W.rows, up}, s);
 }
 
-size_t batch_lm_head_lds(const LlmDims &d, int B) { return pf_lds_bytes(d.n_embd, B, 0) + (size_t)MW * B * 128 * 4; }
+size_t batch_lm_head_lds(const LlmDims &d, int B, int type) {
+    return pf_lds_bytes(rec_k(d.n_embd, type), B, 0) + (size_t)MW * B * 128 * 4;
+}
 
-bool batch_supported(const LlmDims &d, int B) {
-    return B >= 1 && B <= kBatchMax && batch_lm_head_lds(d, B) <= (size_t)LDS_DYN_MAX;
+bool batch_supported(const LlmDims &d, int B, int lm_type) {
+    return B >= 1 && B <= kBatchMax && batch_lm_head_lds(d, B, lm_type) <= (size_t)LDS_DYN_MAX;
 }
 
 void launch_batch_step(const LlmDims &d, const LayerW *layers, int n_layer, _Float16 *kcache, _Float16 *vcache,
                        const float *out_norm, const QMat &lm, const QMat &tok_embd, const PrefillBuffers &pb,
                        const BatchBuffers &bb, int B, hipStream_t s) {
     launch_layers(d, layers, n_layer, kcache, vcache, pb, B, d.max_splits, true, s);
-    launch_quant(d, 0, pb.x, d.n_embd, out_norm, lm.type != 8, pb, B, s);
+    launch_quant(d, 0, pb.x, d.n_embd, out_norm, akind(lm.type), pb, B, s);
     const int nblk = matvec_grid(d, d.n_vocab);  // the batched lm_head keeps one workgroup per CU
-    dispatch_nt<false>(d.n_embd, lm.type, [&]<int NP, int T>() {
+    dispatch_nt<true>(d.n_embd, lm.type, [&]<int NP, int T>() {
         allow_lds(k_bt_lm_head<NP, T>);
-        hipLaunchKernelGGL((k_bt_lm_head<NP, T>), dim3(nblk), dim3(MT), batch_lm_head_lds(d, B), s, d, out_norm, lm,
+        hipLaunchKernelGGL((k_bt_lm_head<NP, T>), dim3(nblk), dim3(MT), batch_lm_head_lds(d, B, T), s, d, out_norm, lm,
                            pb, bb, B);
     });
     hipLaunchKernelGGL(k_bt_sample, dim3(B), dim3(ST), 0, s, d, tok_embd, nblk, pb, bb);

@@ -51,9 +51,12 @@ struct mio_hip_llm {
     int max_steps = 0;
     std::vector<void *> allocs;
     uint64_t weight_bytes = 0;
-    // some matrix is BF16: the multi-token engine (int8 records) does not take it, so the
-    // prompt is prefilled as forced decode steps and batched decode is refused
-    bool bf16 = false;
+    // BF16 matrices: the multi-token engine runs them on its streaming dot engine with bf16
+    // act records (rec_k) when every matrix is BF16 and no layer is an lfm2 short conv (whose
+    // in_proj / out_proj are on the int8 matrix cores); otherwise (bf16_mt false) the prompt is
+    // prefilled as forced decode steps and batched decode is refused
+    bool bf16 = false, int8 = false, has_conv = false;
+    bool bf16_mt() const { return !bf16 || (!int8 && !has_conv); }
     // all quantized matrices live in one arena, in the order a step streams them
     uint8_t *arena = nullptr;
     std::map<std::string, size_t> arena_off;
@@ -222,7 +225,10 @@ bool upload_qmat(mio_hip_llm *m, const mio::GgufTensor *t, mio::QMat &q) {
         return false;
     }
     q.type = (int)type;
-    if (type == mio::GGML_BF16) m->bf16 = true;
+    if (type == mio::GGML_BF16)
+        m->bf16 = true;
+    else
+        m->int8 = true;
     q.rows = (int)t->ne[1];
     q.k = (int)t->ne[0];
     q.p0 = dp + L.off[0];
@@ -493,7 +499,7 @@ int llm_begin(mio_hip_llm *m, const int32_t *prompt, int n_prompt, int max_new, 
     // kPrefillB tokens), or, with MIO_SEQ_PREFILL=1, as P forced decode steps; decoding
     // then starts at position P with the step counter at P either way (same sampler stream)
     const int P = n_prompt - 1;
-    if (sequential_prefill() || m->bf16) {
+    if (sequential_prefill() || !m->bf16_mt()) {
         m->steps_issued = 0;
         if ((rc = set_state(m, 0, prompt[0]))) return rc;
         return llm_run(m, P);
@@ -725,6 +731,7 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
                 return fail(MIO_ERR_UNSUPPORTED);
             }
             any_conv = true;
+            m->has_conv = true;
             m->layers.push_back(L);
             continue;
         }
@@ -817,7 +824,8 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
     want(m->pf.part, (size_t)mio::kPrefillB * D.n_head * D.max_splits * (D.hd + 4));
     want(m->pf.att, (size_t)mio::kPrefillB * D.n_head * D.hd);
     want(m->pf.att_cnt, (size_t)mio::kPrefillB * D.n_kv);
-    want(m->pf.act, mio::prefill_act_bytes(std::max(std::max(D.n_embd, D.n_ff), D.n_head * D.hd)));
+    want(m->pf.act, mio::prefill_act_bytes(
+                        mio::prefill_rec_k(std::max(std::max(D.n_embd, D.n_ff), D.n_head * D.hd), m->bf16 ? 30 : 8)));
     want(dr, (size_t)n_ctx * (D.hd / 2));
     want(m->d_iota, (size_t)n_ctx + mio::kPrefillB);
     size_t io_bytes = 0;
@@ -1171,10 +1179,11 @@ extern "C" int mio_hip_llm_generate_batch(mio_hip_llm *m, const int32_t *prompts
                                           int32_t check_interval, int32_t *out_tokens, int32_t *n_out) {
     MIO_REQUIRE(m && prompts && prompt_lens && seeds && out_tokens && n_out && max_tokens >= 1, MIO_ERR_INVALID,
                 "llm_generate_batch: bad args");
-    MIO_REQUIRE(mio::batch_supported(m->dims, B), MIO_ERR_UNSUPPORTED,
+    MIO_REQUIRE(mio::batch_supported(m->dims, B, m->lm.type), MIO_ERR_UNSUPPORTED,
                 "llm_generate_batch: %d streams not supported (1..%d, lm_head LDS)", B, mio::kBatchMax);
-    MIO_REQUIRE(!m->bf16, MIO_ERR_UNSUPPORTED,
-                "llm_generate_batch: BF16 weights run on the single-stream decode only (mio_hip_llm_generate)");
+    MIO_REQUIRE(m->bf16_mt(), MIO_ERR_UNSUPPORTED,
+                "llm_generate_batch: BF16 weights mixed with quantized ones, or in an lfm2 model, run on the "
+                "single-stream decode only (mio_hip_llm_generate)");
     const mio::LlmDims &D = m->dims;
     std::vector<int> off(B + 1, 0);
     for (int b = 0; b < B; ++b) {
@@ -1274,7 +1283,7 @@ extern "C" int mio_hip_llm_prefill(mio_hip_llm *m, const int32_t *tokens, int n_
                     tokens[i]);
     int rc = mio::bind(m->d);
     if (rc) return rc;
-    if (m->bf16) {
+    if (!m->bf16_mt()) {
         // forced decode steps as llm_begin runs them (the multi-token engine is int8-only):
         // step j decodes tokens[j] at position j and its sampler is forced to tokens[j + 1]
         if (n_tokens > 1) {

@@ -289,7 +289,7 @@ def test_loader_rejects_unknown_biases_and_incomplete_lfm2(device, tmp_path):
 # token in the same order, so the last token's logits (and therefore the KV cache rows they
 # read) equal a token-by-token decode BIT FOR BIT; vs the oracle the teacher-forced bound
 # above applies.
-@pytest.mark.parametrize("preset,n", [(0, 2), (0, 17), (1, 40), (0, 150), (9, 70), (11, 30)])
+@pytest.mark.parametrize("preset,n", [(0, 2), (0, 17), (1, 40), (0, 150), (9, 70), (11, 30), (11, 150)])
 def test_batched_prefill_matches_sequential(device, llm_files, preset, n):
     g = m.Llm(device, llm_files[preset], 256)
     toks = np.random.default_rng(100 + n).integers(0, g.n_vocab, n)
@@ -315,9 +315,11 @@ def test_batched_prefill_then_generate(device, llm_files):
     assert len(tg) == 24 and (tg == to).sum() >= 22
 
 
-def test_batched_prefill_1p7b_q4km(device, tmp_path):
-    """1.7B Q4_K_M, 68-token prompt (the bench prompt length: one chunk, Q4_K + Q6_K)."""
-    path = m.synth_llm(str(tmp_path / "llm17.gguf"), 3, 1)
+@pytest.mark.parametrize("preset", [3, 12])
+def test_batched_prefill_1p7b(device, synth_llm_path, preset):
+    """1.7B, 68-token prompt (the bench prompt length: one chunk): Q4_K_M (Q4_K + Q6_K on the
+    int8 matrix cores) and BF16 (the streaming dot engine with bf16 records)."""
+    path = synth_llm_path(preset)
     g = m.Llm(device, path, 256)
     toks = np.random.default_rng(68).integers(0, 151936, 68)
     batched = g.prefill(toks)

@@ -44,7 +44,7 @@ def _rel(a, b):
     return float(np.sqrt(np.mean((a - b) ** 2)) / max(np.sqrt(np.mean(b ** 2)), 1e-30))
 
 
-@pytest.mark.parametrize("preset", [3, 4, 2, 7, 8, 6, 9, 11])
+@pytest.mark.parametrize("preset", [3, 4, 2, 7, 8, 6, 9, 11, 12])
 def test_layers_match_oracle_on_gpu_inputs(device, synth_llm_path, preset):
     path = synth_llm_path(preset)
     g = m.Llm(device, path, 2048)
@@ -98,9 +98,17 @@ def test_layers_match_oracle_on_gpu_inputs(device, synth_llm_path, preset):
     worst_pos = max((np.median(v), pos) for pos, v in by_pos.items())
     print(f"  worst per-layer median {worst_layer[0]:.3g} (layer {worst_layer[1]}), worst per-position median "
           f"{worst_pos[0]:.3g} (pos {worst_pos[1]})")
-    assert worst_layer[0] <= 1e-5 and worst_pos[0] <= 1e-5, (worst_layer, worst_pos)
-    assert (e > 1e-4).sum() <= 0.12 * len(e)
+    # BF16 weights (11, 12) round every matvec input to bf16 (8-bit mantissa): an f32-ulp
+    # difference of the GPU's summation order crosses a bf16 rounding midpoint far more often
+    # than it flips an int8 code, and each such flip moves the layer output by ~1e-4, so the
+    # flip evaluations are denser (1.7B BF16 measured: median 9.7e-8, 11.7% above 1e-4, worst
+    # per-layer median 1.5e-5, max 1.8e-3). A structural error still shows at >= 1e-2 in every
+    # evaluation of its layer or position, far above either bound.
+    bf16 = preset in (11, 12)
+    med_bound, frac_bound = (1e-4, 0.2) if bf16 else (1e-5, 0.12)
+    assert worst_layer[0] <= med_bound and worst_pos[0] <= med_bound, (worst_layer, worst_pos)
+    assert (e > 1e-4).sum() <= frac_bound * len(e)
     assert worst[0] <= 5e-2, worst
     # the appended K/V row: within one f16 ulp everywhere but in the flip evaluations
-    assert sum(1 for b in kv_bad if b) <= 0.12 * len(kv_bad), kv_bad
+    assert sum(1 for b in kv_bad if b) <= frac_bound * len(kv_bad), kv_bad
     assert np.median(head_errs) <= 1e-4 and max(head_errs) <= 5e-2
