@@ -81,12 +81,14 @@ __device__ inline float *resid_lds(char *base, int K, int nt, int rpw) {
 // NG register groups in flight per wave: two (one loading while the other is dotted), or one
 // for NP = 6 (a 6-pass row is 13 KB per wave; 8 waves x one row already keep 100 KB per CU in
 // flight, and the registers go to the activation records, act_issue)
+// BF16 units are 64 B per lane (4 registers of 8 weights): one unit per group, or the
+// batched kernels spill
 template <int T, int NP, int NM>
 struct CfgB {
-    static constexpr int UN = T == 8 ? MIO_BT_UNITS_Q8 : MIO_BT_UNITS;
+    static constexpr int UN = T == 8 ? MIO_BT_UNITS_Q8 : (T == 30 ? 1 : MIO_BT_UNITS);
     static constexpr int RU = NP * NM >= UN ? 1 : UN / (NP * NM);
     static constexpr int U = RU * NP * NM;
-    static constexpr int NG = NP >= 6 ? 1 : 2;
+    static constexpr int NG = (NP >= 6 || T == 30) ? 1 : 2;
 };
 
 template <int T, int NP, int NM>
@@ -286,7 +288,8 @@ __device__ __forceinline__ void stream_rows_bu(const QMat W0, const QMat W1, int
     // TT tokens per iteration: their activation loads are in flight together and their dot
     // / reduction chains interleave (the weight decode is shared); rows of the group past hi
     // (a wave owning fewer rows than RU) are not dotted
-    constexpr int TT = NP == 1 ? 4 : (NP == 3 ? 2 : 1);
+    // (BF16: one token at a time, its activation slice alone is 16 registers)
+    constexpr int TT = T == 30 ? 1 : (NP == 1 ? 4 : (NP == 3 ? 2 : 1));
     auto consume = [&](const Frag (&F)[U], int r) {
         const int nr = min(RU, hi - r);
         for (int t0 = 0; t0 < nt; t0 += TT) {
@@ -353,7 +356,9 @@ template <int T, int NP, int NM, class Epi>
 __device__ __forceinline__ void stream_rows_b(const QMat W0, const QMat W1, int lo, int hi,
                                               Frag (&A)[CfgB<T, NP, NM>::U], Frag (&B)[CfgB<T, NP, NM>::U], char *smem,
                                               int nt, Epi &&epi, int split = INT_MAX) {
-    if constexpr (MIO_BT_XRED)
+    // BF16: the per-total trees (its 64-B units and 16-register activation slices leave no
+    // room for the transposed reduction's token groups)
+    if constexpr (MIO_BT_XRED && T != 30)
         stream_rows_bx<T, NP, NM>(W0, W1, lo, hi, A, B, smem, nt, epi, split);
     else
         stream_rows_bu<T, NP, NM>(W0, W1, lo, hi, A, B, smem, nt, epi, split);
