@@ -312,14 +312,15 @@ __device__ __forceinline__ void x_after_weights(XRegs<XV> &xr) {
                      "+v"(xr.w[i].y), "+v"(xr.w[i].z), "+v"(xr.w[i].w));
 }
 
-template <int XV>
+// XAUX = 16 (sc1): x was stored write-through by another workgroup of the same launch
+template <int XV, int XAUX = 0>
 __device__ inline void load_x(const float *x, const float *w, int K, XRegs<XV> &xr) {
     const auto rx = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(x), 0, x ? K * 4 : 0, 0x00020000);
     const auto rw = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(w), 0, w ? K * 4 : 0, 0x00020000);
 #pragma unroll
     for (int i = 0; i < XV; ++i) {
         const int e = (MIO_TIDX + i * MT) * 4;
-        const u32x4 a = __builtin_amdgcn_raw_buffer_load_b128(rx, e * 4, 0, 0);
+        const u32x4 a = __builtin_amdgcn_raw_buffer_load_b128(rx, e * 4, 0, XAUX);
         const u32x4 c = __builtin_amdgcn_raw_buffer_load_b128(rw, e * 4, 0, 0);
         xr.v[i] = make_float4(__uint_as_float(a.x), __uint_as_float(a.y), __uint_as_float(a.z), __uint_as_float(a.w));
         xr.w[i] = make_float4(__uint_as_float(c.x), __uint_as_float(c.y), __uint_as_float(c.z), __uint_as_float(c.w));
@@ -1133,6 +1134,22 @@ struct AttCfg {
 __device__ __forceinline__ void st1_sc1(float *base, uint32_t off, float v) {
     __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rsrc(base, 0x7FFFFFF0u), off, 0, 16);
 }
+__device__ __forceinline__ void st4_sc1(float *base, uint32_t off, float4 v) {
+    u32x4 u;
+    u.x = __float_as_uint(v.x), u.y = __float_as_uint(v.y), u.z = __float_as_uint(v.z), u.w = __float_as_uint(v.w);
+    __builtin_amdgcn_raw_buffer_store_b128(u, rsrc(base, 0x7FFFFFF0u), off, 0, 16);
+}
+// One lane waits until the agent-scope counter *c reaches target (relaxed loads, s_sleep
+// between polls: MI355X_MICROARCH "polling-cost"). Bounded: after ~2^16 polls (tens of ms) it
+// gives up and raises *flag, so a lost signal ends the launch instead of hanging the GPU.
+__device__ __forceinline__ void wait_count(int *c, int target, int *flag) {
+    auto *p = (__attribute__((address_space(1))) int *)c;
+    for (int it = 0; it < (1 << 16); ++it) {
+        if (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) return;
+        __builtin_amdgcn_s_sleep(1);
+    }
+    __hip_atomic_store((__attribute__((address_space(1))) int *)flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 __device__ __forceinline__ float4 ld4_sc1(const float *base, uint32_t off) {
     const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rsrc(base, 0x7FFFFFF0u), off, 0, 16);
     return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
@@ -1706,9 +1723,13 @@ __device__ __forceinline__ void q_to_f16(const float *src, _Float16 *dst) {
 // the merger holds outputs 256 w .. 256 w + 255 in quant_regs' layout, so the records are
 // k_bt_quant's bits and its launch is not needed (host: (G * HD) % 256 == 0 for Q8_K, % 32
 // for Q8_0).
+// rdy != nullptr (the fused attention + O launch, k_att_o): the outputs are consumed by other
+// workgroups of the same launch, so they are stored sc1 (write-through), drained, and then
+// lanes 0..7 add 1 to each of the 8 counter shards rdy[64 i] (the O workgroups wait for n_kv
+// adds on theirs), the same hand-off form as the records'.
 template <int HD, int G>
 __device__ void attn_merge_last(const float *part, uint32_t head0, uint32_t g_stride, int nch, int *cnt, float *out,
-                                int ak = -1, ActL rec = {}, int blk0 = 0) {
+                                int ak = -1, ActL rec = {}, int blk0 = 0, int *rdy = nullptr) {
     constexpr int NT = AttCfg<HD>::NT, REC = AttCfg<HD>::REC;
     __shared__ int last_;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1730,7 +1751,10 @@ __device__ void attn_merge_last(const float *part, uint32_t head0, uint32_t g_st
         if (e < G * HD) {
             const int g = e / HD, dd = e - g * HD;
             y = merge_out4(part, head0 + (uint32_t)g * g_stride, nch, REC, HD, dd);
-            *reinterpret_cast<float4 *>(out + e) = y;
+            if (rdy)
+                st4_sc1(out, (uint32_t)e * 4, y);
+            else
+                *reinterpret_cast<float4 *>(out + e) = y;
         }
         if (ak >= 0) {
             const int wave = __builtin_amdgcn_readfirstlane(MIO_TIDX >> 6), lane = MIO_TIDX & 63;
@@ -1743,6 +1767,13 @@ __device__ void attn_merge_last(const float *part, uint32_t head0, uint32_t g_st
                     q80_store(vv, blk0 + sb * 8 + (lane >> 3), e < G * HD, rec);
             }
         }
+    }
+    if (rdy) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (MIO_TIDX < 8)
+            __hip_atomic_fetch_add((__attribute__((address_space(1))) int *)(rdy + 64 * MIO_TIDX), 1,
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 

@@ -97,7 +97,8 @@ struct LlmBuffers {
     float *logits;     // [n_vocab]
     float *part;       // [H][max_splits][hd + 4] attention chunk partials {O, m, l}
     float *att;        // [H * hd] attention output (chunks merged by the last chunk workgroup)
-    int *att_cnt;      // [Hkv] chunk arrival tickets (0 between launches)
+    int *att_cnt;      // [Hkv] chunk arrival tickets (0 between launches); k_att_o's merge
+                       // counters and wait-timeout flag at kRdyOff.. (kAttCntInts in all)
     float *smp;        // sampler partials [2 * n_lm_blocks]
     const float2 *rope;  // [n_ctx][hd/2] (cos, sin)
     StepState *st;
@@ -192,6 +193,14 @@ __host__ __device__ inline int matvec_grid_n(int n_wg, int rows) {
     return g < 2 ? 2 : g;
 }
 int matvec_grid(const LlmDims &d, int rows);
+// the fused attention + O launch (launch_step_kernel which = 10) exists for this head shape
+bool att_o_supported(int hd, int G);
+// k_att_o's merge counters in LlmBuffers.att_cnt: kRdyShards words kRdyStride ints (256 B)
+// apart from int kRdyOff on (one per XCD: an O workgroup polls shard blockIdx % 8, so no word
+// has more than 1/8 of the pollers; MI355X_MICROARCH "dequeue": one word saturates near 88
+// accesses per us), then the wait-timeout flag. Needs n_kv <= kRdyOff.
+constexpr int kRdyOff = 64, kRdyShards = 8, kRdyStride = 64;
+constexpr int kRdyFlag = kRdyOff + kRdyShards * kRdyStride, kAttCntInts = kRdyFlag + 1;
 int pick_np(int K);
 size_t matvec_lds(int K);
 // units (row passes) of the busiest wave of a matvec over `rows` rows on `grid` workgroups,

@@ -148,6 +148,10 @@ __global__ __launch_bounds__(MT) void k_ffn_in(LlmDims d, const float *norm_w, Q
     XRegs<NP> xr;
     load_x(b.x, norm_w, K, xr);
     x_gate();
+    // k_att_o's merge counters: zero again for the next layer's launch (kernel boundary)
+    if (blockIdx.x == 0 && MIO_TIDX < kRdyShards)
+        __hip_atomic_store((__attribute__((address_space(1))) int *)(b.att_cnt + kRdyOff + kRdyStride * MIO_TIDX), 0,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     int lo, hi;
     wave_range(d, gate.rows, lo, hi);
     Frag ga[Cfg<NP, SU>::U], gb[Cfg<NP, SU>::U];
@@ -281,12 +285,17 @@ __global__ __launch_bounds__(MT) void k_lm_head(LlmDims d, const float *norm_w, 
 // One workgroup per (chunk of ATT_CHUNK positions, kv head): q/k RMSNorm (qwen3) + RoPE +
 // f16 rounding, the chunk owning `pos` appends the new k/v row to the F16 cache, then a
 // softmax over the chunk for the G q heads sharing the kv head, whose partial records
-// {O[HD], m, l} the last chunk workgroup to arrive merges into b.att (attn_merge_last): 32-
-// position chunks spread the K/V rows of position ~400 over 13 x n_kv workgroups (16 KB each
-// at hd 128) instead of 4 x n_kv, and k_attn_out reads the n_head * hd merged values.
+// {O[HD], m, l} the last chunk workgroup to arrive merges into b.att (attn_merge_last):
+// ATT_CHUNK (64) -position chunks spread the K/V rows of position ~400 over 7 x n_kv
+// workgroups (32 KB each at hd 128), and k_attn_out (or the O workgroups of k_att_o) reads
+// the n_head * hd merged values.
+// The body of one (chunk ch, kv head kvh) workgroup at position pos (first AttCfg<HD>::NT
+// threads). rdy: the fused attention + O launch's merge counter (attn_merge_last), or null.
+// Returns false for a workgroup with no positions (or after an end token).
 template <int HD, int G, bool DG>
-__global__ __launch_bounds__(AttCfg<HD>::NT) void k_attention(LlmDims d, const float *q_norm, const float *k_norm,
-                                                      const float *bqkv, _Float16 *kc, _Float16 *vc, LlmBuffers b) {
+__device__ __forceinline__ bool attention_wg(const LlmDims &d, const float *q_norm, const float *k_norm,
+                                             const float *bqkv, _Float16 *kc, _Float16 *vc, const LlmBuffers &b,
+                                             int ch, int kvh, int pos, int *rdy) {
     constexpr bool kDiag = DG;
     using C = AttCfg<HD>;
     constexpr int PER = HD / 64;
@@ -301,17 +310,8 @@ __global__ __launch_bounds__(AttCfg<HD>::NT) void k_attention(LlmDims d, const f
     __shared__ float wres[C::NW][G][HD + 2];
 #endif
 
-    MIO_TRACE(b, 0);
-    MIO_TL_BEGIN(b);
-    const int kvh = blockIdx.y, ch = blockIdx.x;
-    // every kernel argument the workgroup uses is loaded in the round trip that fetches
-    // b.st (without this the compiler sinks them below the pos-dependent exit: a third
-    // scalar-load round trip before the first K/V load)
-    asm volatile("" ::"s"(kc), "s"(vc), "s"(d.n_ctx), "s"(b.qkv), "s"(b.rope), "s"(q_norm), "s"(k_norm),
-                 "s"(b.part), "s"(d.max_splits), "s"(bqkv), "s"(b.att), "s"(b.att_cnt));
-    const int pos = cur_pos(b.st, d);
     const int t0 = ch * ATT_CHUNK;
-    if (t0 > pos || b.st->done) return;
+    if (t0 > pos || b.st->done) return false;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const float2 *rope = b.rope + (size_t)pos * (HD / 2);
     // q heads (waves 0..G-1) and, for the chunk owning `pos`, the new k/v row (wave G); the
@@ -393,7 +393,24 @@ __global__ __launch_bounds__(AttCfg<HD>::NT) void k_attention(LlmDims d, const f
     attend_chunk<HD, G>(qs, kr, vr, t0, pos, d.scale, wres, b.part + head0 + (uint32_t)ch * C::REC, gs,
                         DG ? b.trace : nullptr, MIO_TL_DIAGSLOT(b));
 #endif
-    attn_merge_last<HD, G>(b.part, head0, gs, pos / ATT_CHUNK + 1, b.att_cnt + kvh, b.att + (size_t)kvh * G * HD);
+    attn_merge_last<HD, G>(b.part, head0, gs, pos / ATT_CHUNK + 1, b.att_cnt + kvh, b.att + (size_t)kvh * G * HD, -1,
+                           {}, 0, rdy);
+    return true;
+}
+
+template <int HD, int G, bool DG>
+__global__ __launch_bounds__(AttCfg<HD>::NT) void k_attention(LlmDims d, const float *q_norm, const float *k_norm,
+                                                      const float *bqkv, _Float16 *kc, _Float16 *vc, LlmBuffers b) {
+    constexpr bool kDiag = DG;
+    MIO_TRACE(b, 0);
+    MIO_TL_BEGIN(b);
+    // every kernel argument the workgroup uses is loaded in the round trip that fetches
+    // b.st (without this the compiler sinks them below the pos-dependent exit: a third
+    // scalar-load round trip before the first K/V load)
+    asm volatile("" ::"s"(kc), "s"(vc), "s"(d.n_ctx), "s"(b.qkv), "s"(b.rope), "s"(q_norm), "s"(k_norm),
+                 "s"(b.part), "s"(d.max_splits), "s"(bqkv), "s"(b.att), "s"(b.att_cnt));
+    const int pos = cur_pos(b.st, d);
+    if (!attention_wg<HD, G, DG>(d, q_norm, k_norm, bqkv, kc, vc, b, blockIdx.x, blockIdx.y, pos, nullptr)) return;
     MIO_TL_END(b);
     MIO_TRACE(b, 15);
 }
@@ -410,6 +427,84 @@ void launch_attention(int G, dim3 grid, hipStream_t s, const LlmDims &d, const L
         case 8: hipLaunchKernelGGL((k_attention<HD, 8, DG>), grid, dim3(AttCfg<HD>::NT), 0, s, d, qn, kn, bi, kc, vc, b); break;
         default: break;
     }
+}
+
+// ------------------------------------------------------------------ attention + O, one launch
+// k_att_o: the attention workgroups and the O-projection workgroups of a layer in ONE launch
+// (MI355X_MICROARCH "boundary": a dependent launch boundary costs ~1.2-1.5 us, and the O
+// workgroups' weights and residual rows are loaded while the attention runs). Roles are taken
+// from the position (every workgroup reads it): workgroups [0, n_act) with n_act =
+// (pos / ATT_CHUNK + 1) * n_kv are the attention chunks (chunk bid / n_kv, kv head bid % n_kv;
+// their first AttCfg::NT threads), the next matvec_grid(wo) are k_attn_out's workgroups, the
+// rest return. The n_kv merging workgroups store the head outputs write-through and add 1 to
+// each of the 8 counter shards at b.att_cnt + kRdyOff (attn_merge_last); an O workgroup issues
+// its weight group, waits for n_kv on its shard (one lane, wait_count), then loads the outputs
+// sc1. Deadlock-free by dispatch
+// order: every producer has a lower workgroup index than every consumer and never waits, so
+// it is dispatched (and finishes) whatever the residency. The counter is zeroed by the next
+// launch, k_ffn_in (kernel boundary ordered), and by reset_tickets.
+template <int NP, int T, int SU, bool DG>
+__device__ __forceinline__ void o_consumer(const LlmDims &d, const QMat &wo, const LlmBuffers &b, int ob, int no) {
+    constexpr bool kDiag = DG;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int K = wo.k;
+    const Smem s = carve(smem, K);
+    int lo, hi;
+    wave_range(wo.rows, lo, hi, ob, no);
+    const float xres = load_resid(b.x, lo, hi);
+    Frag ga[Cfg<NP, SU>::U], gb[Cfg<NP, SU>::U];
+    load_first<T, NP, 1, SU, MIO_SMALL_AUX>(wo, wo, lo, hi, ga, gb);
+    if (MIO_TIDX == 0)
+        wait_count(b.att_cnt + kRdyOff + kRdyStride * (blockIdx.x & (kRdyShards - 1)), d.n_kv, b.att_cnt + kRdyFlag);
+    asm volatile("s_barrier" ::: "memory");
+    MIO_TL_MARK(b, 3);
+    XRegs<NP> xr;
+    load_x<NP, 16>(b.att, nullptr, K, xr);
+    x_after_weights(xr);
+    MIO_TL_MARK1(b);
+    plain_quant(xr, K, akind(T), s, MIO_TL_DIAGSLOT(b));
+    MIO_TL_MARK(b, 2);
+    stream_rows<T, NP, 1, SU, MIO_SMALL_AUX>(wo, wo, lo, hi, ga, gb, s.a, [&](int row, float v, float) {
+        const float r = lane_value(xres, row - lo);
+        if ((threadIdx.x & 63) == 0) b.x[row] = v + r;
+    });
+}
+
+template <int HD, int G, int NP, int T, int SU, bool DG>
+__global__ __launch_bounds__(MT) void k_att_o(LlmDims d, const float *q_norm, const float *k_norm, const float *bqkv,
+                                              _Float16 *kc, _Float16 *vc, QMat wo, LlmBuffers b) {
+    constexpr bool kDiag = DG;
+    MIO_TRACE(b, 0);
+    MIO_TL_BEGIN(b);
+    asm volatile("" ::"s"(kc), "s"(vc), "s"(d.n_ctx), "s"(b.qkv), "s"(b.rope), "s"(q_norm), "s"(k_norm),
+                 "s"(b.part), "s"(d.max_splits), "s"(bqkv), "s"(b.att), "s"(b.att_cnt));
+    const int pos = cur_pos(b.st, d);
+    if (b.st->done) return;  // no merge is signalled after an end token: nobody may wait
+    const int bid = blockIdx.x, n_act = (pos / ATT_CHUNK + 1) * d.n_kv;
+    if (bid < n_act) {
+        if (MIO_TIDX >= AttCfg<HD>::NT) return;  // whole waves; s_barrier counts the live ones
+        if (!attention_wg<HD, G, DG>(d, q_norm, k_norm, bqkv, kc, vc, b, bid / d.n_kv, bid % d.n_kv, pos,
+                                     b.att_cnt + kRdyOff))
+            return;
+    } else {
+        const int no = matvec_grid_n(d.n_wg, wo.rows), ob = bid - n_act;
+        if (ob >= no) return;
+        o_consumer<NP, T, SU, DG>(d, wo, b, ob, no);
+    }
+    MIO_TL_END(b);
+    MIO_TRACE(b, 15);
+}
+
+template <int NP, int T, int SU, bool DG>
+void launch_att_o(int G, int grid, size_t lds, hipStream_t s, const LlmDims &d, const LayerW &L, _Float16 *kc,
+                  _Float16 *vc, const LlmBuffers &b) {
+    const float *qn = L.q_norm, *kn = L.k_norm, *bi = L.bqkv;
+#define MIO_ATT_O(HH, GG) \
+    hipLaunchKernelGGL((k_att_o<HH, GG, NP, T, SU, DG>), dim3(grid), dim3(MT), lds, s, d, qn, kn, bi, kc, vc, L.wo, b)
+    if (d.hd == 128 && G == 2) MIO_ATT_O(128, 2);
+    if (d.hd == 64 && G == 3) MIO_ATT_O(64, 3);
+    if (d.hd == 64 && G == 4) MIO_ATT_O(64, 4);
+#undef MIO_ATT_O
 }
 
 // ------------------------------------------------------------------ sampler / embedding
@@ -455,6 +550,10 @@ int pick_np(int K) { return K <= 2048 ? 1 : (K <= 6144 ? 3 : 6); }
 
 // at least MW rows per workgroup (every wave owns >= 1 row), at most one workgroup per CU
 static_assert(MW == 8, "matvec_grid_n assumes 8 waves per workgroup");
+// (hd, G) of the fused launch: 1.7B qwen3 (128, 2), 0.1B (64, 3), 2.6B (64, 4); other shapes
+// keep the two launches
+bool att_o_supported(int hd, int G) { return (hd == 128 && G == 2) || (hd == 64 && (G == 3 || G == 4)); }
+
 int matvec_grid(const LlmDims &d, int rows) { return matvec_grid_n(d.n_wg, rows); }
 
 // lm_head workgroups per CU (MIO_LM_WGM, 1..4): the lm_head launch sees n_wg scaled. Two
@@ -536,6 +635,18 @@ void launch_step_kernel(int which, const LlmDims &d, const LayerW *layers, int i
                 dispatch_su<NP>(pick_su(max_wave_units(L.wo.rows, grid, NP, 1), NP), [&]<int SU>() {
                     hipLaunchKernelGGL((k_attn_out<NP, T, SU, DG>), dim3(grid), dim3(MT), mv_lds(L.wo.k), s, d, L.wo, b);
                 });
+            });
+            break;
+        }
+        case 10: {  // attention + O in one launch (k_att_o)
+            const LayerW &L = layers[il];
+            const int grid = d.max_splits * d.n_kv + matvec_grid(d, L.wo.rows);
+            dispatch_nt(L.wo.k, L.wo.type, [&]<int NP, int T>() {
+                if constexpr (NP == 1)
+                    dispatch_su<NP>(pick_su(max_wave_units(L.wo.rows, matvec_grid(d, L.wo.rows), NP, 1), NP), [&]<int SU>() {
+                        launch_att_o<NP, T, SU, DG>(G, grid, mv_lds(L.wo.k), s, d, L, kcache + il * layer_kv,
+                                                    vcache + il * layer_kv, b);
+                    });
             });
             break;
         }

@@ -265,10 +265,38 @@ int graph_steps() {
 // Launches of layer il in step order (launch_step_kernel's `which`): attn_in, attention,
 // attn_out, or an lfm2 short-conv layer's conv_in, conv_out; then ffn_in, ffn_down. Returns
 // the count (<= 5).
+// MIO_ATT_FUSE_O (default 1): attention + O as one launch (k_att_o, which = 10) where the head
+// shape has it; 0 keeps the two launches (A/B).
+bool fuse_att_o(const mio_hip_llm *m) {
+    static const bool env = [] {
+        const char *e = getenv("MIO_ATT_FUSE_O");
+        return !(e && *e == '0');
+    }();
+    return env && m->dims.n_kv <= mio::kRdyOff && mio::att_o_supported(m->dims.hd, m->dims.n_head / m->dims.n_kv);
+}
+
+// k_att_o's bounded wait (wait_count) raises att_cnt[kRdyFlag] if a merge signal never came:
+// reported as an error instead of silently using stale attention outputs.
+int check_handoff(mio_hip_llm *m) {
+    if (!fuse_att_o(m)) return MIO_OK;
+    int flag = 0;
+    int *f = m->buf.att_cnt + mio::kRdyFlag;
+    MIO_HIP_CHECK(hipMemcpyAsync(&flag, f, sizeof(int), hipMemcpyDeviceToHost, m->d->stream));
+    MIO_HIP_CHECK(hipStreamSynchronize(m->d->stream));
+    if (flag) {
+        MIO_HIP_CHECK(hipMemsetAsync(f, 0, sizeof(int), m->d->stream));
+        mio::set_error("llm decode: the attention -> O hand-off wait timed out");
+        return MIO_ERR_HIP;
+    }
+    return MIO_OK;
+}
+
 int layer_kinds(const mio_hip_llm *m, int il, int *w) {
     int n = 0;
     if (m->layers[il].conv) {
         w[n++] = 8, w[n++] = 9;
+    } else if (fuse_att_o(m)) {
+        w[n++] = 0, w[n++] = 10;
     } else {
         w[n++] = 0, w[n++] = 1, w[n++] = 2;
     }
@@ -412,7 +440,7 @@ int prefill(mio_hip_llm *m, int n) {
 // attention launch resets its ticket, so they are 0 here anyway; this keeps an interrupted
 // run from carrying a count).
 int reset_tickets(mio_hip_llm *m) {
-    MIO_HIP_CHECK(hipMemsetAsync(m->buf.att_cnt, 0, (size_t)m->dims.n_kv * sizeof(int), m->d->stream));
+    MIO_HIP_CHECK(hipMemsetAsync(m->buf.att_cnt, 0, (size_t)mio::kAttCntInts * sizeof(int), m->d->stream));
     MIO_HIP_CHECK(hipMemsetAsync(m->pf.att_cnt, 0, (size_t)mio::kPrefillB * m->dims.n_kv * sizeof(int), m->d->stream));
     return MIO_OK;
 }
@@ -803,7 +831,7 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
     want(m->buf.logits, D.n_vocab);
     want(m->buf.part, (size_t)D.n_head * D.max_splits * (D.hd + 4));
     want(m->buf.att, (size_t)D.n_head * D.hd);
-    want(m->buf.att_cnt, (size_t)D.n_kv);
+    want(m->buf.att_cnt, (size_t)mio::kAttCntInts);  // + k_att_o's merge counters and timeout flag
     want(m->buf.smp, 2 * std::max(mio::lm_head_blocks(D), 4 * D.n_wg) + 16);
     want(m->buf.st, 1);
     want(m->d_cfg, 1);
@@ -957,7 +985,7 @@ extern "C" int mio_hip_llm_eval(mio_hip_llm *m, int32_t token, int pos, float *l
     // the step left its sample pending (k_lm_head): take it, so the state is a settled one
     if ((rc = flush_sample(m))) return rc;
     MIO_HIP_CHECK(hipStreamSynchronize(m->d->stream));
-    return MIO_OK;
+    return check_handoff(m);
 }
 
 // One decode step like mio_hip_llm_eval, launched kernel by kernel, with the residual stream
@@ -999,7 +1027,7 @@ extern "C" int mio_hip_llm_eval_layers(mio_hip_llm *m, int32_t token, int pos, f
         MIO_HIP_CHECK(hipMemcpyAsync(logits, m->buf.logits, (size_t)m->dims.n_vocab * 4, hipMemcpyDeviceToHost, s));
     if ((rc = flush_sample(m))) return rc;
     MIO_HIP_CHECK(hipStreamSynchronize(s));
-    return MIO_OK;
+    return check_handoff(m);
 }
 
 // F16 K / V cache rows [0, n_pos) of layer il as [n_kv][n_pos][head_dim] (parity tests).
@@ -1063,6 +1091,7 @@ extern "C" int mio_hip_llm_generate(mio_hip_llm *m, const int32_t *prompt, int n
             m->tail_timed_steps = z.issued - a.issued;
         }
     }
+    if ((rc = check_handoff(m))) return rc;
     const int n = (int)toks.size() < max_tokens ? (int)toks.size() : max_tokens;
     std::memcpy(out_tokens, toks.data(), (size_t)n * 4);
     *n_out = n;
@@ -1404,7 +1433,7 @@ static int kernel_layer(const mio_hip_llm *m, int which) {
     for (int i = 0; i < m->n_layer; ++i) {
         const int il = (m->n_layer / 2 + i) % m->n_layer;
         const bool conv = m->layers[il].conv != 0;
-        if (which <= 2 ? !conv : (which >= 8 ? conv : true)) return il;
+        if (which <= 2 || which == 10 ? !conv : (which >= 8 ? conv : true)) return il;
     }
     return -1;
 }
@@ -1451,8 +1480,9 @@ struct DiagStateGuard {
 extern "C" int mio_hip_llm_time_kernel(mio_hip_llm *m, int which, int iters, float *avg_ms, uint64_t *bytes) {
     MIO_REQUIRE(m && avg_ms && bytes && iters > 0 && m->graph, MIO_ERR_INVALID,
                 "llm_time_kernel: run generate/eval first");
-    MIO_REQUIRE(which >= 0 && which <= 9 && which != 5 && which != 7, MIO_ERR_INVALID, "llm_time_kernel: which %d",
-                which);
+    MIO_REQUIRE(which >= 0 && which <= 10 && which != 5 && which != 7, MIO_ERR_INVALID,
+                "llm_time_kernel: which %d", which);
+    MIO_REQUIRE(which != 10 || fuse_att_o(m), MIO_ERR_INVALID, "llm_time_kernel: no fused attention + O launch");
     const int il = kernel_layer(m, which);
     MIO_REQUIRE(il >= 0, MIO_ERR_INVALID, "llm_time_kernel: the model has no layer with kernel %d", which);
     int rc = mio::bind(m->d);
@@ -1480,6 +1510,7 @@ extern "C" int mio_hip_llm_time_kernel(mio_hip_llm *m, int which, int iters, flo
         case 0: b = qbytes(L.wq) + qbytes(L.wk) + qbytes(L.wv) + 4ull * D.n_embd + 4ull * qkv; break;
         case 1: b = att_bytes; break;
         case 2: b = qbytes(L.wo) + 4ull * D.n_head * D.hd + 4ull * D.n_embd * 2; break;
+        case 10: b = att_bytes + qbytes(L.wo) + 4ull * D.n_head * D.hd + 4ull * D.n_embd * 2; break;
         case 3: b = qbytes(L.gate) + qbytes(L.up) + 4ull * (D.n_embd * 2 + D.n_ff); break;
         case 4: b = qbytes(L.down) + 4ull * (D.n_ff + 2 * D.n_embd); break;
         case 6: b = qbytes(m->lm) + 4ull * D.n_vocab; break;
@@ -1491,17 +1522,32 @@ extern "C" int mio_hip_llm_time_kernel(mio_hip_llm *m, int which, int iters, flo
     MIO_HIP_CHECK(hipEventCreate(&e0));
     MIO_HIP_CHECK(hipEventCreate(&e1));
     hipStream_t s = m->d->stream;
-    // warm
-    mio::launch_step_kernel(which, D, m->layers.data(), il, m->kc, m->vc, m->out_norm, m->lm, m->tok, m->buf,
-                            s);
-    MIO_HIP_CHECK(hipEventRecord(e0, s));
-    for (int i = 0; i < iters; ++i)
-        mio::launch_step_kernel(which, D, m->layers.data(), il, m->kc, m->vc, m->out_norm, m->lm, m->tok, m->buf,
-                                s);
-    MIO_HIP_CHECK(hipEventRecord(e1, s));
-    MIO_HIP_CHECK(hipEventSynchronize(e1));
-    float ms = 0;
-    MIO_HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+    // k_att_o's merge counter is zeroed by the k_ffn_in that follows it in a step: here a
+    // memset does it before every launch, and a loop of the memsets alone is subtracted
+    int *rdy = m->buf.att_cnt + mio::kRdyOff;
+    auto launch = [&](bool fused, bool reset_only) {
+        if (fused) MIO_HIP_CHECK(hipMemsetAsync(rdy, 0, mio::kRdyShards * mio::kRdyStride * sizeof(int), s));
+        if (!reset_only)
+            mio::launch_step_kernel(which, D, m->layers.data(), il, m->kc, m->vc, m->out_norm, m->lm, m->tok, m->buf,
+                                    s);
+        return MIO_OK;
+    };
+    auto timed = [&](bool reset_only, float &ms) {
+        MIO_HIP_CHECK(hipEventRecord(e0, s));
+        for (int i = 0; i < iters; ++i)
+            if (int rc = launch(which == 10, reset_only)) return rc;
+        MIO_HIP_CHECK(hipEventRecord(e1, s));
+        MIO_HIP_CHECK(hipEventSynchronize(e1));
+        MIO_HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+        return MIO_OK;
+    };
+    if (int rc = launch(which == 10, false)) return rc;  // warm
+    float ms = 0, ms_reset = 0;
+    if (int rc = timed(false, ms)) return rc;
+    if (which == 10) {
+        if (int rc = timed(true, ms_reset)) return rc;
+        ms = std::max(0.0f, ms - ms_reset);
+    }
     hipEventDestroy(e0), hipEventDestroy(e1);
     *avg_ms = ms / iters;
     *bytes = b;
@@ -1513,7 +1559,8 @@ extern "C" int mio_hip_llm_time_kernel(mio_hip_llm *m, int which, int iters, flo
 // checkpoints 0 and 15 in out[16] / out[31]. Diagnostic only.
 extern "C" int mio_hip_llm_trace_kernel(mio_hip_llm *m, int which, uint64_t *out) {
     MIO_REQUIRE(m && out && m->graph, MIO_ERR_INVALID, "llm_trace_kernel: run generate/eval first");
-    MIO_REQUIRE(which >= 0 && which <= 9 && which != 5, MIO_ERR_INVALID, "llm_trace_kernel: which %d", which);
+    MIO_REQUIRE(which >= 0 && which <= 10 && which != 5, MIO_ERR_INVALID, "llm_trace_kernel: which %d", which);
+    MIO_REQUIRE(which != 10 || fuse_att_o(m), MIO_ERR_INVALID, "llm_trace_kernel: no fused attention + O launch");
     const int il = kernel_layer(m, which);
     MIO_REQUIRE(il >= 0, MIO_ERR_INVALID, "llm_trace_kernel: the model has no layer with kernel %d", which);
     int rc = mio::bind(m->d);
@@ -1524,6 +1571,8 @@ extern "C" int mio_hip_llm_trace_kernel(mio_hip_llm *m, int which, uint64_t *out
     unsigned long long *dt = nullptr;
     MIO_HIP_CHECK(hipMalloc(&dt, 32 * sizeof(unsigned long long)));
     MIO_HIP_CHECK(hipMemsetAsync(dt, 0, 32 * sizeof(unsigned long long), s));
+    if (which == 10)
+        MIO_HIP_CHECK(hipMemsetAsync(m->buf.att_cnt + mio::kRdyOff, 0, mio::kRdyShards * mio::kRdyStride * sizeof(int), s));
     mio::launch_step_kernel(which, m->dims, m->layers.data(), il, m->kc, m->vc, m->out_norm, m->lm, m->tok, m->buf,
                             s);
     // evict L2 / MALL so the traced launch streams its weights from HBM as in a real step
@@ -1535,6 +1584,8 @@ extern "C" int mio_hip_llm_trace_kernel(mio_hip_llm *m, int which, uint64_t *out
     }
     mio::LlmBuffers tb = m->buf;
     tb.trace = dt;
+    if (which == 10)
+        MIO_HIP_CHECK(hipMemsetAsync(m->buf.att_cnt + mio::kRdyOff, 0, mio::kRdyShards * mio::kRdyStride * sizeof(int), s));
     mio::launch_step_kernel(which, m->dims, m->layers.data(), il, m->kc, m->vc, m->out_norm, m->lm, m->tok, tb,
                             s);
     MIO_HIP_CHECK(hipMemcpyAsync(out, dt, 32 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));

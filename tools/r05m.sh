@@ -1,0 +1,6 @@
+# sharded merge counters for k_att_o: timeline, then bench (fused)
+export TMPDIR=/tmp; out=gpurun_out/r05_m; mkdir -p $out
+timeout -k 10 200 python -u tools/step_timeline.py > $out/timeline.txt 2>&1 || { echo timeline_failed; exit 1; }
+timeout -k 10 300 python -u -m pytest tests/test_llm_layers_gpu.py -x -q --timeout 120 --timeout-method thread > $out/layers.log 2>&1 || { echo layers_failed; exit 1; }
+timeout -k 10 400 python -u bench.py --no-cpu-baseline --no-cpu-c1 > $out/fused.json 2> $out/fused.err || { echo bench_failed; exit 1; }
+echo done

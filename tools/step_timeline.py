@@ -25,7 +25,7 @@ llm.generate([256, 257, 65, 258, 257], a.pos, 0.8, 1, allow=(m.SYNTH_SPEECH0, m.
 t = llm.timeline()
 nl = t.shape[0]
 KN = {0: "attn_in", 1: "attention", 2: "attn_out", 3: "ffn_in", 4: "ffn_down", 6: "lm_head", 8: "conv_in",
-      9: "conv_out"}
+      9: "conv_out", 10: "att_o"}
 names = [KN[k] for k in llm.step_kinds()]
 s0 = np.nanmin(t[:, :, 0], axis=1)
 s1 = np.nanmax(t[:, :, 0], axis=1)
@@ -56,3 +56,23 @@ for k in ["attn_in", "attention", "attn_out", "ffn_in", "ffn_down", "lm_head"]:
         v = t[idx, :, j] - t[idx, :, 0]
         cols.append(f"{np.nanmedian(v):6.2f}" if np.isfinite(v).any() else "     -")
     print(f"  {k:10s}  " + " ".join(cols))
+# the fused attention + O launch: attention workgroups end without mark 3, O workgroups mark 3
+# when their wait is over
+ia = [i for i, n in enumerate(names) if n == "att_o"]
+if ia:
+    T = t[ia]
+    base = s0[ia][:, None]
+    isO = np.isfinite(T[:, :, 3])
+    isA = np.isfinite(T[:, :, 7]) & ~isO
+
+    def med(x, msk):
+        return float(np.nanmedian(np.where(msk, x, np.nan)))
+
+    def lastv(x, msk):
+        return float(np.nanmedian(np.nanmax(np.where(msk, x, np.nan), axis=1)))
+    print(f"  att_o: {int(isA[0].sum())} attention workgroups: start {med(T[:, :, 0] - base, isA):.2f} end "
+          f"{med(T[:, :, 7] - base, isA):.2f} (last {lastv(T[:, :, 7] - base, isA):.2f}); {int(isO[0].sum())} O "
+          f"workgroups: start {med(T[:, :, 0] - base, isO):.2f} (last {lastv(T[:, :, 0] - base, isO):.2f}) wait done "
+          f"{med(T[:, :, 3] - base, isO):.2f} (first {-lastv(-(T[:, :, 3] - base), isO):.2f}) x in "
+          f"{med(T[:, :, 1] - base, isO):.2f} end {med(T[:, :, 7] - base, isO):.2f} "
+          f"(last {lastv(T[:, :, 7] - base, isO):.2f}) us after the launch's first start")
