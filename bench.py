@@ -47,7 +47,7 @@ sys.path.insert(0, os.path.join(REPO, "miotts-llama.cpp_amd", "python"))
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 ROOF_POS = 400  # decode position of the roofline timeline / kernel timings (and of the PMC run)
 KERNEL_NAMES = {0: "k_attn_in", 1: "k_attention", 2: "k_attn_out", 3: "k_ffn_in", 4: "k_ffn_down",
-                6: "k_lm_head", 8: "k_conv_in", 9: "k_conv_out", 10: "k_att_o"}
+                6: "k_lm_head", 8: "k_conv_in", 9: "k_conv_out", 10: "k_att_o", 11: "k_layer_att"}
 PRESETS = {2: "MioTTS-0.1B Q8_0", 3: "MioTTS-1.7B Q4_K_M", 4: "MioTTS-2.6B Q8_0", 12: "MioTTS-1.7B BF16"}
 PROMPT = "こんにちは、今日はいい天気ですね。"  # README.md:83, SURVEY 8(d)
 
@@ -315,7 +315,7 @@ def roofline(llm, preset):
     step = llm.step_kinds()
     assert len(step) == nl, (len(step), nl)
     names = [KERNEL_NAMES[k] for k in step]
-    fused = 10 in step
+    fused = 10 in step or 11 in step
     dur = np.nanmax(tl[:, :, 7], axis=1) - np.nanmin(tl[:, :, 0], axis=1)
     step_wall_us = float(np.nanmax(tl[-1, :, 7]) - np.nanmin(tl[0, :, 0]))
     per_kernel = {}
@@ -353,8 +353,9 @@ def roofline(llm, preset):
             "per_token_us": {k: round(sum(v), 1) for k, v in per_kernel.items()},
             "bytes_per_launch_all": bytes_of, "launches_per_step": nl,
             "note": ("timeline, events and attention bytes at decode position ~400 (as the PMC run)"
-                     + ("; k_att_o = attention + O projection in one launch (its bytes: K/V rows, q|k|v, "
-                        "chunk records, W_o, x); its event time excludes the counter reset a step's k_ffn_in "
+                     + ("; k_att_o = attention + O projection in one launch (layer 0; bytes: K/V rows, q|k|v, "
+                        "chunk records, W_o, x), k_layer_att = RMSNorm + q|k|v + attention + O in one launch "
+                        "(layers >= 1; + W_q|k|v); their event times exclude the counter reset a step's k_ffn_in "
                         "does" if fused else ""))}
 
 

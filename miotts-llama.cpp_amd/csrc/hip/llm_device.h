@@ -41,7 +41,7 @@ constexpr bool kDiag = true;
 // mark 1, mark 2, diagnostic marks 3-6, end}, s_memrealtime ticks (100 MHz), plain stores to
 // slot [seq][wg][8] (wg < 512). Marks: matvec kernels 1 = weight loads issued, 2 = activations quantized;
 // attention 1 = K/V loads issued, 2 = heads prepared; sampler 1 = token chosen.
-#define MIO_TL_SLOT(bufs) ((bufs).tl + 8 * ((size_t)(bufs).seq * 512 + ((blockIdx.x + blockIdx.y * gridDim.x) & 511)))
+#define MIO_TL_SLOT(bufs) ((bufs).tl + 8 * ((size_t)(bufs).seq * 1024 + ((blockIdx.x + blockIdx.y * gridDim.x) & 1023)))
 #define MIO_TL_AT(bufs, k)                                                                      \
     do {                                                                                        \
         if (kDiag && (bufs).tl && MIO_TIDX == 0) MIO_TL_SLOT(bufs)[k] = __builtin_amdgcn_s_memrealtime(); \
@@ -1232,21 +1232,26 @@ struct HeadIn {
     float v[PER], w[PER], vv[PER];
     float2 cs[PER];
 };
-template <int HD>
+// AUX = 16 (sc1): src / vsrc were stored write-through by other workgroups of the same launch
+template <int HD, int AUX = 0>
 __device__ __forceinline__ void head_load(const float *src, const float *bias, const float *nw, const float2 *rope,
                                           const LlmDims &d, HeadIn<HD> &in, const float *vsrc = nullptr,
                                           const float *vbias = nullptr) {
     constexpr int PER = HD / 64;
     const int lane = MIO_TIDX & 63;
+    auto ld = [&](const float *base, int p) {
+        if constexpr (AUX == 0) return base[p];
+        return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc(base, HD * 4), p * 4, 0, AUX));
+    };
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
         const int p = lane + 64 * i;
-        in.v[i] = src[p];
+        in.v[i] = ld(src, p);
         if (bias) in.v[i] = in.v[i] + bias[p];
         in.w[i] = d.qk_norm ? nw[p] : 1.0f;
         in.cs[i] = p < HD / 2 ? rope[p] : make_float2(0.0f, 0.0f);
         if (vsrc) {
-            in.vv[i] = vsrc[p];
+            in.vv[i] = ld(vsrc, p);
             if (vbias) in.vv[i] = in.vv[i] + vbias[p];
         }
     }
@@ -1729,7 +1734,8 @@ __device__ __forceinline__ void q_to_f16(const float *src, _Float16 *dst) {
 // adds on theirs), the same hand-off form as the records'.
 template <int HD, int G>
 __device__ void attn_merge_last(const float *part, uint32_t head0, uint32_t g_stride, int nch, int *cnt, float *out,
-                                int ak = -1, ActL rec = {}, int blk0 = 0, int *rdy = nullptr) {
+                                int ak = -1, ActL rec = {}, int blk0 = 0, int *rdy = nullptr,
+                                unsigned long long *tl = nullptr) {
     constexpr int NT = AttCfg<HD>::NT, REC = AttCfg<HD>::REC;
     __shared__ int last_;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1742,6 +1748,7 @@ __device__ void attn_merge_last(const float *part, uint32_t head0, uint32_t g_st
     }
     __syncthreads();
     if (!last_) return;
+    if (tl && MIO_TIDX == 0) tl[5] = __builtin_amdgcn_s_memrealtime();  // step timeline: merger's ticket
     // one float4 of outputs per thread and pass (G * hd > 4 NT: several passes); in pass b,
     // wave w holds outputs 4 NT b + 256 w .. + 255 (one Q8_K superblock / eight Q8_0 blocks)
 #pragma unroll
@@ -1771,6 +1778,7 @@ __device__ void attn_merge_last(const float *part, uint32_t head0, uint32_t g_st
     if (rdy) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
+        if (tl && MIO_TIDX == 0) tl[6] = __builtin_amdgcn_s_memrealtime();  // outputs written through
         if (MIO_TIDX < 8)
             __hip_atomic_fetch_add((__attribute__((address_space(1))) int *)(rdy + 64 * MIO_TIDX), 1,
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

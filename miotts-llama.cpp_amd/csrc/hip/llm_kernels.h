@@ -176,7 +176,8 @@ void launch_batch_embed(const LlmDims &d, const QMat &tok_embd, const PrefillBuf
 
 // Launch one kernel of a decode step (which: 0 attn_in, 1 attention, 2 attn_out, 3 ffn_in,
 // 4 ffn_down of layer il; 6 lm_head, 7 sampler; lfm2 short-conv layers: 8 conv_in, 9
-// conv_out in place of 0..2) on stream s.
+// conv_out in place of 0..2; 10 attention + O (k_att_o, for 1 + 2), 11 the whole attention
+// block (k_layer_att, for 0 + 1 + 2)) on stream s.
 void launch_step_kernel(int which, const LlmDims &d, const LayerW *layers, int il, _Float16 *kcache,
                         _Float16 *vcache, const float *out_norm, const QMat &lm, const QMat &tok_embd,
                         const LlmBuffers &b, hipStream_t s);
@@ -195,12 +196,20 @@ __host__ __device__ inline int matvec_grid_n(int n_wg, int rows) {
 int matvec_grid(const LlmDims &d, int rows);
 // the fused attention + O launch (launch_step_kernel which = 10) exists for this head shape
 bool att_o_supported(int hd, int G);
+// the whole attention block of layer L as one launch (llm_layer_att.hip, which = 11) exists for
+// its shapes and weight types
+bool layer_att_supported(const LlmDims &d, const LayerW &L);
+void launch_layer_att(const LlmDims &d, const LayerW &L, _Float16 *kc, _Float16 *vc, const LlmBuffers &b, bool dg,
+                      hipStream_t s);
 // k_att_o's merge counters in LlmBuffers.att_cnt: kRdyShards words kRdyStride ints (256 B)
 // apart from int kRdyOff on (one per XCD: an O workgroup polls shard blockIdx % 8, so no word
 // has more than 1/8 of the pollers; MI355X_MICROARCH "dequeue": one word saturates near 88
 // accesses per us), then the wait-timeout flag. Needs n_kv <= kRdyOff.
+// Then k_layer_att's q|k|v row counters, one per kv head (at most kQkvMax), kQkvStride apart.
 constexpr int kRdyOff = 64, kRdyShards = 8, kRdyStride = 64;
-constexpr int kRdyFlag = kRdyOff + kRdyShards * kRdyStride, kAttCntInts = kRdyFlag + 1;
+constexpr int kRdyFlag = kRdyOff + kRdyShards * kRdyStride;
+constexpr int kQkvOff = kRdyFlag + 64, kQkvStride = 64, kQkvMax = 64;
+constexpr int kAttCntInts = kQkvOff + kQkvStride * kQkvMax;
 int pick_np(int K);
 size_t matvec_lds(int K);
 // units (row passes) of the busiest wave of a matvec over `rows` rows on `grid` workgroups,

@@ -1,0 +1,194 @@
+// A decoder layer's attention block as ONE launch of the single-token decode step (layers >= 1;
+// llama_decode for one token, test-to-speech.cpp:178-185): RMSNorm + q|k|v matvec, the
+// attention chunks and their merge, and the O projection + residual, which are k_attn_in,
+// k_attention and k_attn_out's bodies as three workgroup roles of one grid:
+//   [0, GW)                q|k|v producers (k_attn_in's body; rows stored write-through, then
+//                          the rows each workgroup wrote per kv head added to that head's
+//                          counter at b.att_cnt + kQkvOff + kQkvStride * kvh)
+//   [GW, GW + n_act)       attention chunks (n_act = (pos / ATT_CHUNK + 1) * n_kv): K/V rows
+//                          of the chunk loaded and staged in LDS first, then one lane waits
+//                          for the kv head's (G + 2) * hd rows, the head rows are loaded sc1
+//                          (attention_wg<..., WQ = true>); the mergers signal the O counters
+//   [GW + n_act, + no)     O workgroups (o_consumer, as in k_att_o)
+// Every consumer has a higher workgroup index than the producers it waits for, and producers
+// never wait, so in-order dispatch makes progress whatever the residency (MI355X_MICROARCH
+// "Persistent kernels": hand-offs inside a launch instead of a ~1.2-1.5 us boundary each).
+// Layer 0 keeps k_attn_in (its sampler may end the step) + k_att_o. The counters are zeroed by
+// the next launch, k_ffn_in. Instantiated for the shipped head shapes and weight types only
+// (layer_att_supported); everything else runs the separate launches, whose math is the same.
+#include "llm_attention.h"
+
+#pragma clang fp contract(off)
+
+namespace mio {
+#if MIO_ATT_MFMA
+namespace {
+
+template <int NP, int TQ, int TV, int SU, int HD, int G, bool DG>
+__device__ __forceinline__ void qkv_producer(const LlmDims &d, const float *norm_w, const QMat &wq, const QMat &wk,
+                                             const QMat &wv, int g_qk, int GW, const LlmBuffers &b) {
+    constexpr bool kDiag = DG;
+    const int o1 = wq.rows, o2 = wq.rows + wk.rows;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int K = d.n_embd;
+    const Smem s = carve(smem, K);
+    const uint32_t dn = done_issue(b);
+    XRegs<NP> xr;
+    load_x(b.x, norm_w, K, xr);
+    x_gate();
+    auto put = [&](int row, float v) {
+        if ((threadIdx.x & 63) == 0) st1_sc1(b.qkv, (uint32_t)row * 4, v);
+    };
+    Frag ga[Cfg<NP, SU>::U], gb[Cfg<NP, SU>::U];
+    int lo, hi, ra, rb;
+    const int bid = blockIdx.x;
+    if (bid < g_qk) {
+        wave_range(o2, lo, hi, bid, g_qk);
+        ra = o2 * bid / g_qk, rb = o2 * (bid + 1) / g_qk;
+        load_first<TQ, NP, 1, SU, MIO_SMALL_AUX>(wq, wk, lo, hi, ga, gb, o1);
+        x_after_weights(xr);
+        if (done_now(dn)) return;
+        MIO_TL_MARK1(b);
+        rmsnorm_quant(xr, K, d.eps, akind(TQ), s, MIO_TL_DIAGSLOT(b));
+        MIO_TL_MARK(b, 2);
+        stream_rows<TQ, NP, 1, SU, MIO_SMALL_AUX>(wq, wk, lo, hi, ga, gb, s.a, [&](int row, float v, float) {
+            put(row, v);
+        }, o1);
+    } else {
+        const int bv = bid - g_qk, gv = GW - g_qk;
+        wave_range(wv.rows, lo, hi, bv, gv);
+        ra = o2 + wv.rows * bv / gv, rb = o2 + wv.rows * (bv + 1) / gv;
+        load_first<TV, NP, 1, SU, MIO_SMALL_AUX>(wv, wv, lo, hi, ga, gb);
+        x_after_weights(xr);
+        if (done_now(dn)) return;
+        MIO_TL_MARK1(b);
+        rmsnorm_quant(xr, K, d.eps, akind(TV), s, MIO_TL_DIAGSLOT(b));
+        MIO_TL_MARK(b, 2);
+        stream_rows<TV, NP, 1, SU, MIO_SMALL_AUX>(wv, wv, lo, hi, ga, gb, s.a, [&](int row, float v, float) {
+            put(o2 + row, v);
+        });
+    }
+    // every row of the workgroup written through, then per kv head ONE add of the workgroup's
+    // row count there (runs of equal heads over rows ra .. rb - 1 <= 64, host-checked)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (MIO_TIDX < 64) {
+        const int i = MIO_TIDX, r = ra + i;
+        auto head_of = [&](int rr) { return rr < o1 ? rr / (HD * G) : (rr < o2 ? (rr - o1) / HD : (rr - o2) / HD); };
+        const bool ok = r < rb;
+        const int h = ok ? head_of(r) : -1;
+        const bool start = ok && (i == 0 || head_of(r - 1) != h);
+        const uint64_t m = __ballot(start);
+        if (start) {
+            const uint64_t nx = i < 63 ? m >> (i + 1) : 0;
+            const int end = nx ? i + 1 + __builtin_ctzll(nx) : rb - ra;
+            __hip_atomic_fetch_add((__attribute__((address_space(1))) int *)(b.att_cnt + kQkvOff + kQkvStride * h),
+                                   end - i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+template <int NP, int TQ, int TV, int SU, int HD, int G, int TO, int SUO, bool DG>
+__global__ __launch_bounds__(MT) void k_layer_att(LlmDims d, const float *norm_w, QMat wq, QMat wk, QMat wv, int g_qk,
+                                                  int GW, const float *q_norm, const float *k_norm, const float *bqkv,
+                                                  _Float16 *kc, _Float16 *vc, QMat wo, LlmBuffers b) {
+    constexpr bool kDiag = DG;
+    MIO_TRACE(b, 0);
+    MIO_TL_BEGIN(b);
+    const int bid = blockIdx.x;
+    if (bid < GW) {
+        qkv_producer<NP, TQ, TV, SU, HD, G, DG>(d, norm_w, wq, wk, wv, g_qk, GW, b);
+    } else {
+        asm volatile("" ::"s"(kc), "s"(vc), "s"(d.n_ctx), "s"(b.qkv), "s"(b.rope), "s"(q_norm), "s"(k_norm),
+                     "s"(b.part), "s"(d.max_splits), "s"(bqkv), "s"(b.att), "s"(b.att_cnt));
+        const int pos = cur_pos(b.st, d);
+        if (b.st->done) return;  // the producers return too: nobody signals, nobody waits
+        const int ab = bid - GW, n_act = (pos / ATT_CHUNK + 1) * d.n_kv;
+        if (ab < n_act) {
+            if (MIO_TIDX >= AttCfg<HD>::NT) return;  // whole waves; s_barrier counts the live ones
+            if (!attention_wg<HD, G, DG, true>(d, q_norm, k_norm, bqkv, kc, vc, b, ab / d.n_kv, ab % d.n_kv, pos,
+                                               b.att_cnt + kRdyOff))
+                return;
+        } else {
+            const int no = matvec_grid_n(d.n_wg, wo.rows), ob = ab - n_act;
+            if (ob >= no) return;
+            o_consumer<1, TO, SUO, DG>(d, wo, b, ob, no);
+        }
+    }
+    MIO_TL_END(b);
+    MIO_TRACE(b, 15);
+}
+
+// the instantiated (np, q|k type, v type, su, hd, G, o type, o su): 1.7B Q4_K_M (v Q4_K or
+// Q6_K) and BF16, 0.1B Q8_0, 2.6B Q8_0 (and the LFM2-2.6B attention layers)
+#define MIO_LAYER_ATT_SHAPES(X)   \
+    X(1, 12, 12, 2, 128, 2, 12, 1) \
+    X(1, 12, 14, 2, 128, 2, 12, 1) \
+    X(1, 30, 30, 2, 128, 2, 30, 1) \
+    X(1, 8, 8, 1, 64, 3, 8, 1)     \
+    X(1, 8, 8, 2, 64, 4, 8, 1)
+
+struct Shape {
+    int np, tq, tv, su, hd, g, to, suo;
+    int GW, g_qk;
+};
+
+Shape shape_of(const LlmDims &d, const LayerW &L) {
+    Shape s{};
+    attn_in_grid(d, L, s.GW, s.g_qk);
+    s.np = pick_np(d.n_embd);
+    s.tq = L.wq.type, s.tv = L.wv.type, s.to = L.wo.type;
+    s.su = pick_su(std::max(max_wave_units(L.wq.rows + L.wk.rows, s.g_qk, s.np, 1),
+                            max_wave_units(L.wv.rows, s.GW - s.g_qk, s.np, 1)),
+                   s.np);
+    s.suo = pick_su(max_wave_units(L.wo.rows, matvec_grid(d, L.wo.rows), pick_np(L.wo.k), 1), pick_np(L.wo.k));
+    s.hd = d.hd, s.g = d.n_head / d.n_kv;
+    if (pick_np(L.wo.k) != 1) s.suo = -1;
+    return s;
+}
+
+template <bool DG>
+bool launch(const LlmDims &d, const LayerW &L, _Float16 *kc, _Float16 *vc, const LlmBuffers &b, hipStream_t st,
+            bool dry) {
+    const Shape s = shape_of(d, L);
+    const int rows = L.wq.rows + L.wk.rows + L.wv.rows;
+    // the producer's per-head signal covers <= 64 rows per workgroup
+    if ((L.wq.rows + L.wk.rows + s.g_qk - 1) / s.g_qk > 64 || (L.wv.rows + s.GW - s.g_qk - 1) / (s.GW - s.g_qk) > 64 ||
+        d.n_kv > kQkvMax || rows != (d.n_head + 2 * d.n_kv) * d.hd || L.conv)
+        return false;
+    const int grid = s.GW + d.max_splits * d.n_kv + matvec_grid(d, L.wo.rows);
+    const size_t lds = std::max(matvec_lds(d.n_embd), matvec_lds(L.wo.k));
+    bool found = false;
+#define MIO_LA_CASE(NP, TQ, TV, SU, HD, G, TO, SUO)                                                                   \
+    if (!found && s.np == NP && s.tq == TQ && s.tv == TV && s.su == SU && s.hd == HD && s.g == G && s.to == TO &&   \
+        s.suo == SUO) {                                                                                                \
+        found = true;                                                                                                  \
+        if (!dry)                                                                                                      \
+            hipLaunchKernelGGL((k_layer_att<NP, TQ, TV, SU, HD, G, TO, SUO, DG>), dim3(grid), dim3(MT), lds, st, d,   \
+                               L.attn_norm, L.wq, L.wk, L.wv, s.g_qk, s.GW, L.q_norm, L.k_norm, L.bqkv, kc, vc, L.wo, \
+                               b);                                                                                     \
+    }
+    MIO_LAYER_ATT_SHAPES(MIO_LA_CASE)
+#undef MIO_LA_CASE
+    return found;
+}
+
+}  // namespace
+
+bool layer_att_supported(const LlmDims &d, const LayerW &L) {
+    return launch<false>(d, L, nullptr, nullptr, LlmBuffers{}, nullptr, true);
+}
+
+void launch_layer_att(const LlmDims &d, const LayerW &L, _Float16 *kc, _Float16 *vc, const LlmBuffers &b, bool dg,
+                      hipStream_t s) {
+    if (dg)
+        launch<true>(d, L, kc, vc, b, s, false);
+    else
+        launch<false>(d, L, kc, vc, b, s, false);
+}
+#else
+bool layer_att_supported(const LlmDims &, const LayerW &) { return false; }
+void launch_layer_att(const LlmDims &, const LayerW &, _Float16 *, _Float16 *, const LlmBuffers &, bool, hipStream_t) {}
+#endif
+
+}  // namespace mio

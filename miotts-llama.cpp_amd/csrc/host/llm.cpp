@@ -291,10 +291,22 @@ int check_handoff(mio_hip_llm *m) {
     return MIO_OK;
 }
 
+// MIO_LAYER_ATT (default 1): layers >= 1 run their whole attention block as one launch
+// (k_layer_att, which = 11) where it is instantiated; 0 keeps attn_in + the k_att_o launch.
+bool fuse_layer_att(const mio_hip_llm *m, int il) {
+    static const bool env = [] {
+        const char *e = getenv("MIO_LAYER_ATT");
+        return !(e && *e == '0');
+    }();
+    return env && il > 0 && fuse_att_o(m) && mio::layer_att_supported(m->dims, m->layers[il]);
+}
+
 int layer_kinds(const mio_hip_llm *m, int il, int *w) {
     int n = 0;
     if (m->layers[il].conv) {
         w[n++] = 8, w[n++] = 9;
+    } else if (fuse_layer_att(m, il)) {
+        w[n++] = 11;
     } else if (fuse_att_o(m)) {
         w[n++] = 0, w[n++] = 10;
     } else {
@@ -1433,7 +1445,9 @@ static int kernel_layer(const mio_hip_llm *m, int which) {
     for (int i = 0; i < m->n_layer; ++i) {
         const int il = (m->n_layer / 2 + i) % m->n_layer;
         const bool conv = m->layers[il].conv != 0;
-        if (which <= 2 || which == 10 ? !conv : (which >= 8 ? conv : true)) return il;
+        if (which == 11 ? !conv && fuse_layer_att(m, il)
+                        : (which <= 2 || which == 10 ? !conv : (which >= 8 ? conv : true)))
+            return il;
     }
     return -1;
 }
@@ -1480,9 +1494,9 @@ struct DiagStateGuard {
 extern "C" int mio_hip_llm_time_kernel(mio_hip_llm *m, int which, int iters, float *avg_ms, uint64_t *bytes) {
     MIO_REQUIRE(m && avg_ms && bytes && iters > 0 && m->graph, MIO_ERR_INVALID,
                 "llm_time_kernel: run generate/eval first");
-    MIO_REQUIRE(which >= 0 && which <= 10 && which != 5 && which != 7, MIO_ERR_INVALID,
+    MIO_REQUIRE(which >= 0 && which <= 11 && which != 5 && which != 7, MIO_ERR_INVALID,
                 "llm_time_kernel: which %d", which);
-    MIO_REQUIRE(which != 10 || fuse_att_o(m), MIO_ERR_INVALID, "llm_time_kernel: no fused attention + O launch");
+    MIO_REQUIRE(which < 10 || fuse_att_o(m), MIO_ERR_INVALID, "llm_time_kernel: no fused attention launch");
     const int il = kernel_layer(m, which);
     MIO_REQUIRE(il >= 0, MIO_ERR_INVALID, "llm_time_kernel: the model has no layer with kernel %d", which);
     int rc = mio::bind(m->d);
@@ -1511,6 +1525,11 @@ extern "C" int mio_hip_llm_time_kernel(mio_hip_llm *m, int which, int iters, flo
         case 1: b = att_bytes; break;
         case 2: b = qbytes(L.wo) + 4ull * D.n_head * D.hd + 4ull * D.n_embd * 2; break;
         case 10: b = att_bytes + qbytes(L.wo) + 4ull * D.n_head * D.hd + 4ull * D.n_embd * 2; break;
+        // q|k|v written and read back by the attention workgroups: counted once each way
+        case 11:
+            b = qbytes(L.wq) + qbytes(L.wk) + qbytes(L.wv) + 4ull * D.n_embd + att_bytes + qbytes(L.wo) +
+                4ull * D.n_head * D.hd + 4ull * D.n_embd * 2;
+            break;
         case 3: b = qbytes(L.gate) + qbytes(L.up) + 4ull * (D.n_embd * 2 + D.n_ff); break;
         case 4: b = qbytes(L.down) + 4ull * (D.n_ff + 2 * D.n_embd); break;
         case 6: b = qbytes(m->lm) + 4ull * D.n_vocab; break;
@@ -1525,8 +1544,9 @@ extern "C" int mio_hip_llm_time_kernel(mio_hip_llm *m, int which, int iters, flo
     // k_att_o's merge counter is zeroed by the k_ffn_in that follows it in a step: here a
     // memset does it before every launch, and a loop of the memsets alone is subtracted
     int *rdy = m->buf.att_cnt + mio::kRdyOff;
+    const size_t rdy_bytes = (size_t)(mio::kAttCntInts - mio::kRdyOff) * sizeof(int);
     auto launch = [&](bool fused, bool reset_only) {
-        if (fused) MIO_HIP_CHECK(hipMemsetAsync(rdy, 0, mio::kRdyShards * mio::kRdyStride * sizeof(int), s));
+        if (fused) MIO_HIP_CHECK(hipMemsetAsync(rdy, 0, rdy_bytes, s));
         if (!reset_only)
             mio::launch_step_kernel(which, D, m->layers.data(), il, m->kc, m->vc, m->out_norm, m->lm, m->tok, m->buf,
                                     s);
@@ -1535,16 +1555,16 @@ extern "C" int mio_hip_llm_time_kernel(mio_hip_llm *m, int which, int iters, flo
     auto timed = [&](bool reset_only, float &ms) {
         MIO_HIP_CHECK(hipEventRecord(e0, s));
         for (int i = 0; i < iters; ++i)
-            if (int rc = launch(which == 10, reset_only)) return rc;
+            if (int rc = launch(which >= 10, reset_only)) return rc;
         MIO_HIP_CHECK(hipEventRecord(e1, s));
         MIO_HIP_CHECK(hipEventSynchronize(e1));
         MIO_HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
         return MIO_OK;
     };
-    if (int rc = launch(which == 10, false)) return rc;  // warm
+    if (int rc = launch(which >= 10, false)) return rc;  // warm
     float ms = 0, ms_reset = 0;
     if (int rc = timed(false, ms)) return rc;
-    if (which == 10) {
+    if (which >= 10) {
         if (int rc = timed(true, ms_reset)) return rc;
         ms = std::max(0.0f, ms - ms_reset);
     }
@@ -1559,8 +1579,8 @@ extern "C" int mio_hip_llm_time_kernel(mio_hip_llm *m, int which, int iters, flo
 // checkpoints 0 and 15 in out[16] / out[31]. Diagnostic only.
 extern "C" int mio_hip_llm_trace_kernel(mio_hip_llm *m, int which, uint64_t *out) {
     MIO_REQUIRE(m && out && m->graph, MIO_ERR_INVALID, "llm_trace_kernel: run generate/eval first");
-    MIO_REQUIRE(which >= 0 && which <= 10 && which != 5, MIO_ERR_INVALID, "llm_trace_kernel: which %d", which);
-    MIO_REQUIRE(which != 10 || fuse_att_o(m), MIO_ERR_INVALID, "llm_trace_kernel: no fused attention + O launch");
+    MIO_REQUIRE(which >= 0 && which <= 11 && which != 5, MIO_ERR_INVALID, "llm_trace_kernel: which %d", which);
+    MIO_REQUIRE(which < 10 || fuse_att_o(m), MIO_ERR_INVALID, "llm_trace_kernel: no fused attention launch");
     const int il = kernel_layer(m, which);
     MIO_REQUIRE(il >= 0, MIO_ERR_INVALID, "llm_trace_kernel: the model has no layer with kernel %d", which);
     int rc = mio::bind(m->d);
@@ -1571,8 +1591,9 @@ extern "C" int mio_hip_llm_trace_kernel(mio_hip_llm *m, int which, uint64_t *out
     unsigned long long *dt = nullptr;
     MIO_HIP_CHECK(hipMalloc(&dt, 32 * sizeof(unsigned long long)));
     MIO_HIP_CHECK(hipMemsetAsync(dt, 0, 32 * sizeof(unsigned long long), s));
-    if (which == 10)
-        MIO_HIP_CHECK(hipMemsetAsync(m->buf.att_cnt + mio::kRdyOff, 0, mio::kRdyShards * mio::kRdyStride * sizeof(int), s));
+    if (which >= 10)
+        MIO_HIP_CHECK(hipMemsetAsync(m->buf.att_cnt + mio::kRdyOff, 0,
+                                     (size_t)(mio::kAttCntInts - mio::kRdyOff) * sizeof(int), s));
     mio::launch_step_kernel(which, m->dims, m->layers.data(), il, m->kc, m->vc, m->out_norm, m->lm, m->tok, m->buf,
                             s);
     // evict L2 / MALL so the traced launch streams its weights from HBM as in a real step
@@ -1584,8 +1605,9 @@ extern "C" int mio_hip_llm_trace_kernel(mio_hip_llm *m, int which, uint64_t *out
     }
     mio::LlmBuffers tb = m->buf;
     tb.trace = dt;
-    if (which == 10)
-        MIO_HIP_CHECK(hipMemsetAsync(m->buf.att_cnt + mio::kRdyOff, 0, mio::kRdyShards * mio::kRdyStride * sizeof(int), s));
+    if (which >= 10)
+        MIO_HIP_CHECK(hipMemsetAsync(m->buf.att_cnt + mio::kRdyOff, 0,
+                                     (size_t)(mio::kAttCntInts - mio::kRdyOff) * sizeof(int), s));
     mio::launch_step_kernel(which, m->dims, m->layers.data(), il, m->kc, m->vc, m->out_norm, m->lm, m->tok, tb,
                             s);
     MIO_HIP_CHECK(hipMemcpyAsync(out, dt, 32 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
@@ -1605,7 +1627,7 @@ extern "C" int mio_hip_llm_timeline(mio_hip_llm *m, uint64_t *out, int max_launc
     const int nl = (int)step_kinds(m).size();
     MIO_REQUIRE(max_launches >= nl, MIO_ERR_INVALID, "llm_timeline: need %d launch slots", nl);
     hipStream_t s = m->d->stream;
-    const size_t nslot = (size_t)nl * 512 * 8;
+    const size_t nslot = (size_t)nl * 1024 * 8;  // MIO_TL_SLOT: 1024 workgroup slots per launch
     unsigned long long *tl = nullptr;
     MIO_HIP_CHECK(hipMalloc(&tl, sizeof(unsigned long long) * nslot));
     hipGraph_t g = nullptr;

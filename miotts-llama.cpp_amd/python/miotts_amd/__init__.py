@@ -481,10 +481,10 @@ class Llm:
         """Per-launch, per-workgroup [start, marks 1-6, end] (us from the step start, NaN =
         absent) of one graph-replayed step (diagnostic, mio_hip_llm_timeline; advances the
         decode state). Marks: see MIO_TL_MARK in csrc/hip/llm_device.h."""
-        out = np.zeros(1024 * 512 * 8, np.uint64)
+        out = np.zeros(512 * 1024 * 8, np.uint64)
         n = ctypes.c_int(0)
-        check(lib().mio_hip_llm_timeline(self.h, _ptr(out), 1024, ctypes.byref(n)))
-        t = out[: n.value * 4096].astype(np.float64).reshape(n.value, 512, 8)
+        check(lib().mio_hip_llm_timeline(self.h, _ptr(out), 512, ctypes.byref(n)))
+        t = out[: n.value * 8192].astype(np.float64).reshape(n.value, 1024, 8)
         t[t == 0] = np.nan
         return (t - np.nanmin(t[0, :, 0])) * 0.01
 

@@ -25,7 +25,7 @@ llm.generate([256, 257, 65, 258, 257], a.pos, 0.8, 1, allow=(m.SYNTH_SPEECH0, m.
 t = llm.timeline()
 nl = t.shape[0]
 KN = {0: "attn_in", 1: "attention", 2: "attn_out", 3: "ffn_in", 4: "ffn_down", 6: "lm_head", 8: "conv_in",
-      9: "conv_out", 10: "att_o"}
+      9: "conv_out", 10: "att_o", 11: "layer_att"}
 names = [KN[k] for k in llm.step_kinds()]
 s0 = np.nanmin(t[:, :, 0], axis=1)
 s1 = np.nanmax(t[:, :, 0], axis=1)
@@ -76,3 +76,28 @@ if ia:
           f"{med(T[:, :, 3] - base, isO):.2f} (first {-lastv(-(T[:, :, 3] - base), isO):.2f}) x in "
           f"{med(T[:, :, 1] - base, isO):.2f} end {med(T[:, :, 7] - base, isO):.2f} "
           f"(last {lastv(T[:, :, 7] - base, isO):.2f}) us after the launch's first start")
+# the whole attention block in one launch: producers (no mark 3), attention (mark 4 = K/V
+# staged, mark 3 = q|k|v ready), O workgroups (mark 3, no mark 4)
+il = [i for i, n in enumerate(names) if n == "layer_att"]
+if il:
+    T = t[il]
+    base = s0[il][:, None]
+    m3, m4 = np.isfinite(T[:, :, 3]), np.isfinite(T[:, :, 4])
+    isA, isO = m3 & m4, m3 & ~m4
+    isP = np.isfinite(T[:, :, 2]) & ~m3
+
+    def med(x, msk):
+        return float(np.nanmedian(np.where(msk, x, np.nan)))
+
+    def lastv(x, msk):
+        return float(np.nanmedian(np.nanmax(np.where(msk, x, np.nan), axis=1)))
+    print(f"  layer_att: {int(isP[0].sum())} producers end {med(T[:, :, 7] - base, isP):.2f} (last "
+          f"{lastv(T[:, :, 7] - base, isP):.2f}); {int(isA[0].sum())} attention: K/V staged "
+          f"{med(T[:, :, 4] - base, isA):.2f}, q|k|v ready {med(T[:, :, 3] - base, isA):.2f}, end "
+          f"{med(T[:, :, 7] - base, isA):.2f} (last {lastv(T[:, :, 7] - base, isA):.2f}); {int(isO[0].sum())} O: "
+          f"wait done {med(T[:, :, 3] - base, isO):.2f}, end {med(T[:, :, 7] - base, isO):.2f} (last "
+          f"{lastv(T[:, :, 7] - base, isO):.2f}) us after the launch's first start")
+    mg = np.isfinite(T[:, :, 5])
+    print(f"  layer_att mergers ({int(mg[0].sum())}): ticket {med(T[:, :, 5] - base, mg):.2f}, outputs written "
+          f"{med(T[:, :, 6] - base, mg):.2f}, end {med(T[:, :, 7] - base, mg):.2f}; chunk compute done (m2->end "
+          f"of non-mergers) {med(T[:, :, 7] - base, isA & ~mg):.2f} (last {lastv(T[:, :, 7] - base, isA & ~mg):.2f})")
