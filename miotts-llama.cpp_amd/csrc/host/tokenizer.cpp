@@ -3,6 +3,8 @@
 
 #include <algorithm>
 #include <climits>
+#include <functional>
+#include <queue>
 #include <set>
 
 #include "common.h"
@@ -91,8 +93,10 @@ uint32_t lower_ascii(uint32_t cp) { return cp >= 'A' && cp <= 'Z' ? cp + 32 : cp
 bool BpeTokenizer::load(const GgufFile &g) {
     const std::string model = g.get_str("tokenizer.ggml.model");
     const GgufValue *tv = g.get("tokenizer.ggml.tokens");
+    if (model == "llama" && tv && !tv->arr_s.empty()) return load_spm(g);
     if (model != "gpt2" || !tv || tv->arr_s.empty()) {
-        set_error("tokenizer: GGUF has no gpt2 (byte-level BPE) vocabulary (model '%s')", model.c_str());
+        set_error("tokenizer: GGUF has no gpt2 (byte-level BPE) or llama (SPM) vocabulary (model '%s')",
+                  model.c_str());
         return false;
     }
     tokens_ = tv->arr_s;
@@ -151,6 +155,119 @@ bool BpeTokenizer::load(const GgufFile &g) {
         byte_dec_[cp] = (uint8_t)b;
     }
     return true;
+}
+
+// SPM (tokenizer.ggml.model "llama"): tokens, scores, types; llama.cpp's defaults for this
+// vocabulary type: BOS added, EOS not, a space prefix on the first fragment
+bool BpeTokenizer::load_spm(const GgufFile &g) {
+    spm_ = true;
+    tokens_ = g.get("tokenizer.ggml.tokens")->arr_s;
+    const size_t n = tokens_.size();
+    types_.assign(n, 1);
+    if (const GgufValue *tt = g.get("tokenizer.ggml.token_type"))
+        for (size_t i = 0; i < tt->arr_i.size() && i < n; ++i) types_[i] = (int32_t)tt->arr_i[i];
+    scores_.assign(n, 0.0f);
+    if (const GgufValue *sc = g.get("tokenizer.ggml.scores"))
+        for (size_t i = 0; i < sc->arr_f.size() && i < n; ++i) scores_[i] = (float)sc->arr_f[i];
+    id_.reserve(n * 2);
+    for (size_t i = 0; i < n; ++i) id_.emplace(tokens_[i], (int32_t)i);
+    std::set<size_t, std::greater<size_t>> lens;
+    for (size_t i = 0; i < n; ++i)
+        if ((types_[i] == 3 || types_[i] == 4) && !tokens_[i].empty()) {  // CONTROL, USER_DEFINED
+            special_.emplace(tokens_[i], (int32_t)i);
+            lens.insert(tokens_[i].size());
+        }
+    special_lens_.assign(lens.begin(), lens.end());
+    eos_ = (int32_t)g.get_int("tokenizer.ggml.eos_token_id", -1);
+    bos_ = (int32_t)g.get_int("tokenizer.ggml.bos_token_id", -1);
+    unk_ = (int32_t)g.get_int("tokenizer.ggml.unknown_token_id", -1);
+    const GgufValue *ab = g.get("tokenizer.ggml.add_bos_token");
+    add_bos_ = ab ? ab->u != 0 : true;
+    const GgufValue *ae = g.get("tokenizer.ggml.add_eos_token");
+    add_eos_ = ae ? ae->u != 0 : false;
+    const GgufValue *sp = g.get("tokenizer.ggml.add_space_prefix");
+    add_space_prefix_ = sp ? sp->u != 0 : true;
+    // byte tokens "<0xXX>", else the byte itself as a token, else unk
+    static const char *hex = "0123456789ABCDEF";
+    for (int b = 0; b < 256; ++b) {
+        const char t[7] = {'<', '0', 'x', hex[b >> 4], hex[b & 15], '>', 0};
+        auto it = id_.find(t);
+        if (it == id_.end()) it = id_.find(std::string(1, (char)b));
+        byte_tok_[b] = it != id_.end() ? it->second : unk_;
+    }
+    if (bos_ >= (int32_t)n || eos_ >= (int32_t)n || unk_ >= (int32_t)n) {
+        set_error("tokenizer: SPM special token id out of range");
+        return false;
+    }
+    return true;
+}
+
+// ------------------------------------------------------------------ SPM
+void BpeTokenizer::spm(const std::string &text, std::vector<int32_t> &out) const {
+    struct Sym {
+        int prev, next;
+        size_t off, n;
+    };
+    std::vector<Sym> sym;
+    for (size_t off = 0; off < text.size();) {
+        size_t l = 1;
+        utf8_decode(text, off, &l);
+        l = std::min(l, text.size() - off);
+        const int idx = (int)sym.size();
+        sym.push_back({idx - 1, off + l == text.size() ? -1 : idx + 1, off, l});
+        off += l;
+    }
+    if (sym.empty()) return;
+    struct Bigram {
+        int left, right;
+        float score;
+        size_t size;
+    };
+    // highest score first; equal scores: the leftmost pair
+    auto worse = [](const Bigram &a, const Bigram &b) { return a.score < b.score || (a.score == b.score && a.left > b.left); };
+    std::priority_queue<Bigram, std::vector<Bigram>, decltype(worse)> q(worse);
+    std::unordered_map<std::string, std::pair<int, int>> rev;
+    auto add = [&](int l, int r) {
+        if (l < 0 || r < 0) return;
+        const std::string t = text.substr(sym[l].off, sym[l].n + sym[r].n);
+        const auto it = id_.find(t);
+        if (it == id_.end()) return;
+        q.push({l, r, scores_[it->second], t.size()});
+        rev[t] = {l, r};
+    };
+    for (int i = 1; i < (int)sym.size(); ++i) add(i - 1, i);
+    while (!q.empty()) {
+        const Bigram b = q.top();
+        q.pop();
+        Sym &L = sym[b.left], &R = sym[b.right];
+        if (L.n == 0 || R.n == 0 || L.n + R.n != b.size) continue;  // stale: a side was merged since
+        L.n += R.n;
+        R.n = 0;
+        L.next = R.next;
+        if (R.next >= 0) sym[R.next].prev = b.left;
+        add(L.prev, b.left);
+        add(b.left, L.next);
+    }
+    // a final symbol that is no token: the two symbols it was merged from (split at the right
+    // one's start: symbol starts never move), recursively; characters of no token -> bytes
+    std::function<void(size_t, size_t)> reseg;
+    reseg = [&](size_t off, size_t n) {
+        const std::string t = text.substr(off, n);
+        const auto it = id_.find(t);
+        if (it != id_.end()) {
+            out.push_back(it->second);
+            return;
+        }
+        const auto p = rev.find(t);
+        if (p == rev.end()) {
+            for (size_t j = 0; j < n; ++j) out.push_back(byte_tok_[(unsigned char)text[off + j]]);
+            return;
+        }
+        const size_t split = sym[p->second.second].off;
+        reseg(off, split - off);
+        reseg(split, off + n - split);
+    };
+    for (int i = 0; i != -1; i = sym[i].next) reseg(sym[i].off, sym[i].n);
 }
 
 int32_t BpeTokenizer::special_id(const std::string &text) const {
@@ -371,11 +488,25 @@ std::vector<int32_t> BpeTokenizer::tokenize(const std::string &text, bool add_sp
     std::vector<int32_t> out;
     if (add_special && add_bos_ && bos_ >= 0) out.push_back(bos_);
     std::string run;
+    bool prev_special = true;  // SPM: the space prefix goes on a fragment that opens the text or follows a special
     auto flush = [&]() {
         if (run.empty()) return;
-        std::vector<std::string> pieces;
-        pretokenize(run, pieces);
-        for (const std::string &p : pieces) bpe(p, out);
+        if (spm_) {
+            std::string t = add_space_prefix_ && prev_special ? " " + run : run;
+            std::string e;
+            for (char c : t) {
+                if (c == ' ')
+                    e += "\xe2\x96\x81";  // U+2581
+                else
+                    e += c;
+            }
+            spm(e, out);
+            prev_special = false;
+        } else {
+            std::vector<std::string> pieces;
+            pretokenize(run, pieces);
+            for (const std::string &p : pieces) bpe(p, out);
+        }
         run.clear();
     };
     for (size_t i = 0; i < text.size();) {
@@ -393,12 +524,14 @@ std::vector<int32_t> BpeTokenizer::tokenize(const std::string &text, bool add_sp
         if (sid >= 0) {
             flush();
             out.push_back(sid);
+            prev_special = true;
             i += slen;
         } else {
             run += text[i++];
         }
     }
     flush();
+    if (spm_ && add_special && add_eos_ && eos_ >= 0) out.push_back(eos_);
     return out;
 }
 
@@ -406,6 +539,27 @@ std::string BpeTokenizer::piece(int32_t id) const {
     if (id < 0 || id >= (int32_t)tokens_.size()) return "";
     const std::string &t = tokens_[id];
     if (types_[id] == 3 || types_[id] == 4) return t;  // special: rendered as text
+    if (spm_) {
+        // llama_token_to_piece(special = true): UNKNOWN as its text, NORMAL with U+2581 -> ' ',
+        // BYTE "<0xXX>" -> the byte, other types (UNUSED) nothing
+        if (types_[id] == 2) return t;
+        if (types_[id] == 6) {
+            if (t.size() == 6 && t.compare(0, 3, "<0x") == 0 && t[5] == '>')
+                return std::string(1, (char)std::stoi(t.substr(3, 2), nullptr, 16));
+            return t;
+        }
+        if (types_[id] != 1) return "";
+        std::string o;
+        for (size_t i = 0; i < t.size();) {
+            if (t.compare(i, 3, "\xe2\x96\x81") == 0) {
+                o += ' ';
+                i += 3;
+            } else {
+                o += t[i++];
+            }
+        }
+        return o;
+    }
     std::string o;
     for (size_t i = 0; i < t.size();) {
         size_t l = 1;

@@ -14,6 +14,17 @@
 //      rank order; pieces are then looked up in the vocabulary (bytes as a fallback).
 // Parity: llama.cpp is absent here; each pre-type is checked id for id against HuggingFace
 // `tokenizers` with the same regex sequence (tests/test_tokenizer_hf.py).
+//
+// SPM vocabularies (tokenizer.ggml.model == "llama": SentencePiece pieces with scores and
+// <0xXX> byte tokens, llama.cpp's llm_tokenizer_spm, restated): specials split as above; a
+// text fragment gets a leading " " when tokenizer.ggml.add_space_prefix (default true) and it
+// opens the text or follows a special token, every ' ' becomes U+2581; the fragment is split
+// into UTF-8 characters and adjacent symbols are merged greedily, highest vocabulary score
+// first (ties: leftmost), whenever their concatenation is a token; a final symbol that is not
+// a token is resegmented into the two symbols it was merged from, and characters that form no
+// token become their <0xXX> byte tokens. BOS is added by default (add_bos_token), EOS when
+// add_eos_token. Pieces: U+2581 -> ' ', byte tokens -> the byte. Checked id for id against
+// the `sentencepiece` package's BPE encoder on trained vocabularies (tests/test_tokenizer_spm.py).
 #pragma once
 
 #include <cstdint>
@@ -41,6 +52,8 @@ public:
 
 private:
     void bpe(const std::string &piece, std::vector<int32_t> &out) const;
+    void spm(const std::string &text, std::vector<int32_t> &out) const;
+    bool load_spm(const GgufFile &g);
     void pretokenize(const std::string &text, std::vector<std::string> &pieces) const;
 
     std::vector<std::string> tokens_;
@@ -51,8 +64,12 @@ private:
     std::vector<size_t> special_lens_;                  // distinct lengths, descending
     std::string byte_enc_[256];                          // byte -> UTF-8 of its unicode stand-in
     std::unordered_map<uint32_t, uint8_t> byte_dec_;     // stand-in code point -> byte
-    int32_t eos_ = -1, bos_ = -1;
-    bool add_bos_ = false;
+    int32_t eos_ = -1, bos_ = -1, unk_ = -1;
+    bool add_bos_ = false, add_eos_ = false;
+    // SPM vocabularies
+    bool spm_ = false, add_space_prefix_ = true;
+    std::vector<float> scores_;
+    int32_t byte_tok_[256];
     // pre-tokenizer family (llama.cpp LLAMA_VOCAB_PRE_TYPE_*): the regex sequence of step 2
     enum class Pre { Gpt2, Default, Qwen2, Llama3, Smollm };
     Pre pre_ = Pre::Gpt2;

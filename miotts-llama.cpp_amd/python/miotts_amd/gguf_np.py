@@ -105,7 +105,7 @@ class GGUFReader:
 
 def write_kv_gguf(path: str, kv: Dict[str, Any]) -> None:
     """Minimal GGUF v3 writer (metadata only, no tensors) for tokenizer tests.
-    Values: str, bool, int (u32), float (f32), list[str], list[int] (i32)."""
+    Values: str, bool, int (u32), float (f32), list[str], list[int] (i32), list[float] (f32)."""
     def s(x: str) -> bytes:
         b = x.encode("utf-8")
         return struct.pack("<Q", len(b)) + b
@@ -123,6 +123,8 @@ def write_kv_gguf(path: str, kv: Dict[str, Any]) -> None:
             out += struct.pack("<I", 8) + s(v)
         elif isinstance(v, list) and (not v or isinstance(v[0], str)):
             out += struct.pack("<IIQ", 9, 8, len(v)) + b"".join(s(x) for x in v)
+        elif isinstance(v, list) and isinstance(v[0], float):
+            out += struct.pack("<IIQ", 9, 6, len(v)) + b"".join(struct.pack("<f", x) for x in v)
         elif isinstance(v, list):
             out += struct.pack("<IIQ", 9, 5, len(v)) + b"".join(struct.pack("<i", x) for x in v)
         else:
