@@ -118,6 +118,15 @@ public:
                              const Options & options,
                              std::string & out_token_text);
 
+    // (extension) several utterances on this device: their LLM decodes run together (one
+    // weight pass per step for all of them, mio_hip_llm_generate_batch, up to 16 at a time),
+    // then each is written as synthesize_to_file writes it (the same bytes: every utterance
+    // samples with the seed synthesize_to_file uses)
+    bool synthesize_batch_to_files(const VoiceModel & voice,
+                                   const std::vector<std::string> & texts,
+                                   const std::vector<std::string> & output_paths,
+                                   const Options & options);
+
     struct Impl;  // GPU handles (device, LLM runner, codec, tokenizer)
 
 private:

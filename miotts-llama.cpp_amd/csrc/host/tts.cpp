@@ -484,6 +484,67 @@ bool TestToSpeech::synthesize_to_file(const VoiceModel &voice, const std::string
     return synthesize_to_file(voice, text, output_path, Options{});
 }
 
+// Batched synthesis (extension): prompts in groups of up to 16 through the batched decode
+// engine, then codec + iSTFT + the PCM epilogue per utterance as synthesize_to_file does it.
+// Every stream uses synthesize_to_file's seed, so each file has the bytes a single call writes
+// (mio_hip_llm_generate_batch's streams equal mio_hip_llm_generate of their prompts).
+bool TestToSpeech::synthesize_batch_to_files(const VoiceModel &voice, const std::vector<std::string> &texts,
+                                             const std::vector<std::string> &output_paths, const Options &options) {
+    if (!is_ready() || !voice.is_ready() || texts.size() != output_paths.size()) {
+        fprintf(stderr, "TestToSpeech: %s\n",
+                !is_ready() ? "not ready" : (!voice.is_ready() ? "voice model is not ready" : "texts / paths mismatch"));
+        return false;
+    }
+    Impl &I = *impl_;
+    if (options.skip_llm || !I.llm) {
+        for (size_t i = 0; i < texts.size(); ++i)
+            if (!synthesize_to_file(voice, texts[i], output_paths[i], options)) return false;
+        return true;
+    }
+    const float temp = options.temperature >= 0.0f ? options.temperature : config_.temperature;
+    const int max_tokens = options.max_tokens > 0 ? options.max_tokens : config_.max_tokens;
+    mio::SamplingParams sp;
+    sp.temperature = temp, sp.seed = 42, sp.eos0 = I.eos, sp.eos1 = I.im_end;
+    I.harness(options, sp);
+    constexpr size_t kGroup = 16;
+    for (size_t g0 = 0; g0 < texts.size(); g0 += kGroup) {
+        const int B = (int)std::min(kGroup, texts.size() - g0);
+        std::vector<int32_t> prompts, lens;
+        for (int b = 0; b < B; ++b) {
+            const std::vector<int32_t> p = I.prompt_tokens(texts[g0 + b]);
+            if (p.empty()) {
+                fprintf(stderr, "TestToSpeech: tokenization failed\n");
+                return false;
+            }
+            prompts.insert(prompts.end(), p.begin(), p.end());
+            lens.push_back((int32_t)p.size());
+        }
+        std::vector<uint64_t> seeds((size_t)B, sp.seed);
+        std::vector<int32_t> toks((size_t)B * max_tokens), n_out((size_t)B);
+        if (mio_hip_llm_generate_batch(I.llm, prompts.data(), lens.data(), B, max_tokens, temp, seeds.data(),
+                                       sp.allow_lo, sp.allow_hi, sp.eos0, sp.eos1, 32, toks.data(),
+                                       n_out.data()) != MIO_OK) {
+            // a model the batched engine does not take: one utterance at a time
+            for (int b = 0; b < B; ++b)
+                if (!synthesize_to_file(voice, texts[g0 + b], output_paths[g0 + b], options)) return false;
+            continue;
+        }
+        for (int b = 0; b < B; ++b) {
+            std::string text;
+            for (int i = 0; i < n_out[b]; ++i) text += I.tok.piece(toks[(size_t)b * max_tokens + i]);
+            if (!synthesize_to_file(voice, text, output_paths[g0 + b], [&] {
+                    Options o = options;
+                    o.skip_llm = true;
+                    return o;
+                }())) {
+                fprintf(stderr, "TestToSpeech: utterance %zu failed\n", g0 + b);
+                return false;
+            }
+        }
+    }
+    return true;
+}
+
 bool TestToSpeech::synthesize_stream(const VoiceModel &voice, const std::string &text, const StreamCallback &callback,
                                      size_t chunk_samples, const Options &options) {
     StreamProfile p;

@@ -15,6 +15,8 @@ struct CliArgs {
     std::string model_path, codec_path, voice_path, prompt;
     std::string output_path = "output.wav";
     std::string out_offline = "offline.wav", out_stream = "stream_concat.wav";
+    std::string batch_file;  // miotts --batch: one prompt per line
+    int gpus = 1;            // miotts --gpus: MI355Xs the batch is sharded over
     float temperature = 0.8f;
     int max_tokens = 700, n_threads = 4, n_gpu_layers = 0, device = -1;
     size_t chunk_samples = 4096;

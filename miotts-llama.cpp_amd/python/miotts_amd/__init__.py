@@ -17,13 +17,15 @@ REPO_ROOT = os.path.dirname(PKG_ROOT)
 # MIO_BUILD_DIR: an alternative in-tree build (A/B experiments of compile-time variants)
 BUILD_DIR = os.environ.get("MIO_BUILD_DIR") or os.path.join(PKG_ROOT, "build")
 LIB_PATH = os.path.join(BUILD_DIR, "libmiotts.so")
+# test-support library (include/mio_hip_test.h: synthetic GGUF writers, kernel parity entries)
+TEST_LIB_PATH = os.path.join(BUILD_DIR, "libmiotts_test.so")
 INCLUDE_DIR = os.path.join(REPO_ROOT, "include")
 
 MIO_IN_DEVICE = 1
 MIO_OUT_DEVICE = 2
 MIO_CODEC_INCREMENTAL = 4
 
-_lib: Optional[ctypes.CDLL] = None
+_lib = None
 
 _f32p = ctypes.POINTER(ctypes.c_float)
 _i32p = ctypes.POINTER(ctypes.c_int32)
@@ -34,8 +36,25 @@ class HipError(RuntimeError):
     pass
 
 
-def lib() -> ctypes.CDLL:
-    """Load libmiotts.so (built in-tree by __graft_entry__.build / `make`)."""
+class _Libs:
+    """The product library and, behind it, the test-support library: an entry point is looked
+    up in libmiotts.so first, then in libmiotts_test.so."""
+
+    def __init__(self, product: ctypes.CDLL, test: Optional[ctypes.CDLL]):
+        self.product, self.test = product, test
+
+    def __getattr__(self, name):
+        f = getattr(self.product, name, None)
+        if f is None and self.test is not None:
+            f = getattr(self.test, name, None)
+        if f is None:
+            raise AttributeError(name)
+        return f
+
+
+def lib() -> _Libs:
+    """Load libmiotts.so and libmiotts_test.so (built in-tree by __graft_entry__.build /
+    `make`)."""
     global _lib
     if _lib is None:
         if not os.path.exists(LIB_PATH):
@@ -43,8 +62,11 @@ def lib() -> ctypes.CDLL:
                 f"{LIB_PATH} not built: run `make -C miotts-llama.cpp_amd` "
                 "(or __graft_entry__.build()); there is no CPU fallback")
         L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        T = ctypes.CDLL(TEST_LIB_PATH, mode=ctypes.RTLD_GLOBAL) if os.path.exists(TEST_LIB_PATH) else None
         _declare(L)
-        _lib = L
+        if T is not None:
+            _declare(T)
+        _lib = _Libs(L, T)
     return _lib
 
 
@@ -389,7 +411,7 @@ class Codec:
 
 
 # ---------------------------------------------------------------- LLM
-SYNTH_SPEECH0 = 260      # id of <|s_0|> in the synthetic vocabulary (csrc/host/synth.h)
+SYNTH_SPEECH0 = 260      # id of <|s_0|> in the synthetic vocabulary (csrc/testlib/synth.h)
 SYNTH_IM_END = 258
 SYNTH_EOT = 259
 

@@ -83,6 +83,22 @@ def test_miotts_cli_writes_wav(files):
     assert abs(np.abs(x).max() - int(0.95 * 32767)) <= 1  # peak-normalised to 0.95
 
 
+def test_miotts_batch_equals_single_runs(files):
+    """`miotts --batch FILE` (extension): the lines decode together on the batched engine and
+    each OUTPUT_nnn.wav has the bytes a single `miotts -p LINE` run writes (every stream
+    samples with the single run's seed; mio_hip_llm_generate_batch's streams equal
+    mio_hip_llm_generate). --gpus 1 takes the sharding path with one device."""
+    d = files["dir"]
+    prompts = ["テストです。", "こんにちは。", "今日はいい天気ですね。"]
+    (d / "batch.txt").write_text("\n".join(prompts) + "\n", "utf-8")
+    common = ["-m", files["llm"], "-c", files["codec"], "-v", files["voice"], "--max-tokens", 40, "--speech-only",
+              "--ignore-eos"]
+    run(["miotts"] + common + ["--batch", d / "batch.txt", "-o", d / "b.wav", "--gpus", 1])
+    for i, p in enumerate(prompts):
+        run(["miotts"] + common + ["-p", p, "-o", d / f"s{i}.wav"])
+        assert (d / f"b_{i:03d}.wav").read_bytes() == (d / f"s{i}.wav").read_bytes(), i
+
+
 def test_miotts_usage_errors(files):
     p = subprocess.run([os.path.join(BIN, "miotts"), "-c", files["codec"]], capture_output=True, text=True)
     assert p.returncode == 1 and "--prompt is required" in p.stderr

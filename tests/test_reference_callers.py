@@ -99,3 +99,20 @@ def test_reference_cli_without_gpu_fails_loudly(callers, models, name, extra):
     assert rc_ref == rc_ours == 1
     assert out_ref == out_ours and err_ref == err_ours
     assert "no HIP device" in err_ref
+
+
+def test_miotts_batch_flags(tmp_path):
+    """The batch extension of `miotts` (--batch FILE, --gpus N): listed in
+    --help, --gpus without --batch and an unreadable or empty --batch file are usage errors
+    (exit 1 with a message) before any device is touched."""
+    exe = os.path.join(BIN, "miotts")
+    rc, out, err = _run(exe, ["--help"])
+    assert rc == 0 and "--batch" in out + err and "--gpus" in out + err
+    common = ["-c", "c.gguf", "-v", "v.gguf", "-m", "m.gguf"]
+    rc, _, err = _run(exe, common + ["-p", "x", "--gpus", "2"])
+    assert rc == 1 and "--gpus needs --batch" in err
+    rc, _, err = _run(exe, common + ["--batch", str(tmp_path / "missing.txt")])
+    assert rc == 1 and "cannot read --batch file" in err
+    (tmp_path / "empty.txt").write_text("\n\n")
+    rc, _, err = _run(exe, common + ["--batch", str(tmp_path / "empty.txt")])
+    assert rc == 1 and "has no prompts" in err

@@ -20,14 +20,15 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 H = os.path.join(REPO, "miotts-llama.cpp_amd", "csrc")
 CLANG = "/opt/rocm/lib/llvm/bin/clang++"  # g++ 11 has no _Float16 in C++ (quant.cpp)
 SRCS = [os.path.join(REPO, "tests", "sanitize", "host_fuzz.cpp")] + [
-    os.path.join(H, "host", f) for f in ("gguf.cpp", "tokenizer.cpp", "text.cpp", "quant.cpp", "synth.cpp",
-                                         "synth_llm.cpp")]
+    os.path.join(H, "host", f) for f in ("gguf.cpp", "tokenizer.cpp", "text.cpp", "quant.cpp")] + [
+    os.path.join(H, "testlib", f) for f in ("synth.cpp", "synth_llm.cpp")]
 
 
 def build(out):
     cmd = [CLANG, "-std=c++20", "-O1", "-g", "-fsanitize=address,undefined", "-fno-sanitize-recover=all",
            "-fno-omit-frame-pointer", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include",
-           "-I" + os.path.join(REPO, "include"), "-I" + H, "-I" + os.path.join(H, "host")] + SRCS + ["-o", out]
+           "-I" + os.path.join(REPO, "include"), "-I" + H, "-I" + os.path.join(H, "host"),
+           "-I" + os.path.join(H, "testlib")] + SRCS + ["-o", out]
     subprocess.run(cmd, check=True, capture_output=True, text=True, timeout=600)
 
 
