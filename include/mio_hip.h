@@ -236,7 +236,8 @@ int mio_wav_encode(const float *samples, int n, int sample_rate, uint8_t *out, i
 /* ---------------- GGUF tokenizer ----------------
  * Replaces llama_tokenize(vocab, text, add_special, parse_special) (test-to-speech.cpp:117-125),
  * llama_token_to_piece(..., special=true) (:173-176), llama_vocab_eos (:150) and the
- * "<|im_end|>" lookup (:151-159) for gpt2-type (byte-level BPE) GGUF vocabularies.
+ * "<|im_end|>" lookup (:151-159) for gpt2-type (byte-level BPE) and llama-type (SPM) GGUF
+ * vocabularies.
  * info[4] = {n_vocab, bos, eos, im_end (-1 if not a single token)}. */
 int mio_tokenizer_load(const char *gguf_path, mio_tokenizer **out);
 void mio_tokenizer_free(mio_tokenizer *t);

@@ -1489,7 +1489,7 @@ __device__ void attend_chunk(const float (*qs)[HD], const h8 (&kr)[AttCfg<HD>::I
 #define MIO_ATT_MFMA 1
 #endif
 // MIO_ATT_FASTEXP (default 1): p by the hardware exp (v_exp_f32 of x log2 e) instead of expf
-// (0 for A/B: 0.768 vs 0.759 ms per 1.7B token, profiles/r05_att_ab.txt)
+// (0 for A/B: 0.764 vs 0.754-0.758 ms per 1.7B token, profiles/r05_att_ab.txt)
 #ifndef MIO_ATT_FASTEXP
 #define MIO_ATT_FASTEXP 1
 #endif
