@@ -208,6 +208,22 @@ __device__ inline Smem carve(char *base, int K) {
     return s;
 }
 
+// A multi-token activation record (prefill / batched launches, llm_prefill.hip): act[t] =
+// {qs i8[K] | d f32[K/32+8] | bs i16[K/16+8]}, 16-B aligned, nt of them back to back.
+__host__ __device__ inline size_t act_bytes(int K) {
+    return ((size_t)K + (size_t)(K / 32 + 8) * 4 + (size_t)(K / 16 + 8) * 2 + 15) & ~(size_t)15;
+}
+__host__ __device__ inline size_t act_base(int) { return 0; }
+__device__ inline Smem carve_t(char *base, int K, int t) {
+    Smem s;
+    s.red = nullptr;
+    char *a = base + act_base(K) + act_bytes(K) * t;
+    s.a.qs = (int8_t *)a;
+    s.a.d = (float *)(a + K);
+    s.a.bs = (int16_t *)(a + K + (size_t)(K / 32 + 8) * 4);
+    return s;
+}
+
 // Workgroup sum (8 waves). No trailing barrier: every caller writes `red` again only
 // after a later workgroup barrier (the quantizer's closing barrier).
 __device__ double block_sum(double v, double *red) {

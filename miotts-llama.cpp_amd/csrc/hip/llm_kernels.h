@@ -141,7 +141,10 @@ struct PrefillBuffers {
     float *ring;         // lfm2 short-conv rings [seq][n_layer][kConvSlots][n_embd], or null
     size_t seq_ring;     // ring elements per sequence
     char *act;           // [kPrefillB] quantized activation records of the next matvec
+    int *qcnt;           // batched decode, in-launch quantization (launch_mmq_q): 2 sets of 8
+                         // counter shards 64 ints apart, then the wait-timeout flag (kQcntFlag)
 };
+constexpr int kQcntFlag = 1024, kQcntInts = kQcntFlag + 64;
 // bytes of the act records (pb.act) for K up to k_max (BF16 weights: pass prefill_rec_k)
 size_t prefill_act_bytes(int k_max);
 // K of the act record layout for a weight type (2K for BF16: K bf16 values)

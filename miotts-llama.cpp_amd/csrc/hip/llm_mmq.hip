@@ -391,7 +391,7 @@ __device__ __forceinline__ void all_slots(const QMat &W, const QMat &U, int row,
 }
 
 template <int T0, int T1, int T2, int MODE>
-__global__ __launch_bounds__(MMQ_NT) void k_mmq(MmqSeg s0, MmqSeg s1, MmqSeg s2, MmqArgs a) {
+__global__ __launch_bounds__(MMQ_NT) void k_mmq(MmqSeg s0, MmqSeg s1, MmqSeg s2, MmqArgs a, MmqQuant) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     float *red = reinterpret_cast<float *>(lds);                          // [8 waves][64][16] (x2 SWIGLU)
     float *da = red + (MODE == MMQ_SWIGLU ? 2 : 1) * MMQ_NT * 16;         // [groups][32 tokens]
@@ -796,15 +796,59 @@ __device__ __forceinline__ v4f slot16_sum(const float *red) {
 // KP: the launch is Q8_0 with K % 256 == 0 and (1) K <= 2048 or (2) K > 2048 (host-checked),
 // so only that pair path is compiled into it: the generic kernel (KP 0) carries three Q8_0
 // paths, and its size alone cost the 2.6B gate|up launch 19.2 vs 14.4 us
-template <int T0, int T1, int T2, int MODE, int KP = 0>
-__global__ __launch_bounds__(MMQ_NT) void k_mmq16(MmqSeg s0, MmqSeg s1, MmqSeg s2, MmqArgs a) {
+// QNP > 0 (k_mmq16q): the first a.nt workgroups are quantization producers (MmqQuant, XRegs
+// of QNP passes, QM = its mode), the tiles follow and wait before their activation reads.
+template <int T0, int T1, int T2, int MODE, int KP = 0, int QNP = 0, int QM = 0>
+__global__ __launch_bounds__(MMQ_NT) void k_mmq16(MmqSeg s0, MmqSeg s1, MmqSeg s2, MmqArgs a, MmqQuant q) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     constexpr int NV = MODE == MMQ_SWIGLU ? 2 : 1;
+    constexpr bool QF = QNP > 0;
+    if constexpr (QF) {
+        if ((int)blockIdx.x < a.nt) {
+            // producer: k_bt_quant's arithmetic into an LDS record laid out as the global one,
+            // then copied write-through (16-B sc1 stores), drained, and signalled
+            const int t = blockIdx.x;
+            const int ak = T0 == 8 ? 0 : 1;
+            if (blockIdx.x == 0 && threadIdx.x < 8) {
+                __hip_atomic_store((__attribute__((address_space(1))) int *)(q.other + 64 * threadIdx.x), 0,
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            Smem st = carve(lds + act_bytes(a.K), a.K);
+            st.a = carve_t(lds, a.K, 0).a;
+            XRegs<QNP> xr;
+            load_x(q.src + (size_t)t * a.K, QM == 0 ? q.norm_w : nullptr, a.K, xr);
+            if constexpr (QM == 0)
+                rmsnorm_quant(xr, a.K, q.eps, ak, st);
+            else
+                plain_quant(xr, a.K, ak, st);
+            const int n16 = (int)(act_bytes(a.K) / 16);
+            const auto dst = rsrc(a.act + (size_t)t * a.act_stride, (uint32_t)act_bytes(a.K));
+            for (int i = threadIdx.x; i < n16; i += MMQ_NT) {
+                const uint4 v = reinterpret_cast<const uint4 *>(lds)[i];
+                u32x4 u;
+                u.x = v.x, u.y = v.y, u.z = v.z, u.w = v.w;
+                __builtin_amdgcn_raw_buffer_store_b128(u, dst, i * 16, 0, 16);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (threadIdx.x < 8)
+                __hip_atomic_fetch_add((__attribute__((address_space(1))) int *)(q.cnt + 64 * threadIdx.x), 1,
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return;
+        }
+    }
     float *red = reinterpret_cast<float *>(lds);  // [NV][8 waves][64][4]
     float *da = red + NV * MMQ_NT * 4;           // [groups][16 tokens]
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int t0 = blockIdx.y * TT16;
-    int tile_id = blockIdx.x;
+    int tile_id = (int)blockIdx.x - (QF ? a.nt : 0);
+    // the producers' records are complete: one lane waits, the barrier releases the others
+    auto wait_act = [&]() {
+        if constexpr (QF) {
+            if (threadIdx.x == 0) wait_count(q.cnt + 64 * (blockIdx.x & 7), a.nt, q.flag);
+            asm volatile("s_barrier" ::: "memory");
+        }
+    };
     auto run = [&]<int T>(const MmqSeg &sg, int ti) {
         const int row0 = ti * RT16, row = min(row0 + (lane & 15), sg.w.rows - 1);
         // the slot index must be wave-uniform (divergent branches around the MFMAs would run
@@ -821,6 +865,7 @@ __global__ __launch_bounds__(MMQ_NT) void k_mmq16(MmqSeg s0, MmqSeg s1, MmqSeg s
                 v4i x[4];
                 q80p_load(sg.w, row, 0, k, qw);
                 if constexpr (NV == 2) q80p_load(a.w_up, row, 0, k, qu);
+                wait_act();
                 act_load(aq, a.K, 0, k, x);
                 stage_act16<8>(a, t0, a.K, da);
 #pragma unroll
@@ -835,12 +880,14 @@ __global__ __launch_bounds__(MMQ_NT) void k_mmq16(MmqSeg s0, MmqSeg s1, MmqSeg s
                     u = tree8(au);
                 }
             } else {
+                wait_act();
                 stage_act16<8>(a, t0, a.K, da);
                 slot16_q80p<NV>(sg.w, a.w_up, row, k, aq, da, y, u);
             }
             slot16_store(y, red);
             if constexpr (NV == 2) slot16_store(u, red + MMQ_NT * 4);
         } else {
+            wait_act();
             const int8_t *aq = stage_act16<T>(a, t0, a.K, da);
             slot16_store(slot16_val<T>(sg.w, row, k, aq, da), red);
             if constexpr (NV == 2) slot16_store(slot16_val<T>(a.w_up, row, k, aq, da), red + MMQ_NT * 4);
@@ -919,7 +966,7 @@ void launch_mmq(const MmqSeg *seg, const int *types, int nseg, int mode, const M
     auto go = [&]<int A, int B, int C>() {
         auto launch = [&](auto kern) {
             if (lds > 64 * 1024) allow_lds_mmq(reinterpret_cast<const void *>(kern));
-            hipLaunchKernelGGL(kern, grid, dim3(MMQ_NT), lds, s, sg[0], sg[1], sg[2], a);
+            hipLaunchKernelGGL(kern, grid, dim3(MMQ_NT), lds, s, sg[0], sg[1], sg[2], a, MmqQuant{});
         };
         if (t16) {
             const bool q8 = A == 8 && (B < 0 || B == 8) && (C < 0 || C == 8) && a.K % 256 == 0;
@@ -954,6 +1001,44 @@ void launch_mmq(const MmqSeg *seg, const int *types, int nseg, int mode, const M
     if (types[0] == 12) one.template operator()<12>();
     else if (types[0] == 14) one.template operator()<14>();
     else one.template operator()<8>();
+}
+
+
+// The fused shapes of the batched decode (launch_layers): q|k|v of the K-quant models (three
+// segments, RMSNorm input), gate|up (Q4_K, or Q8_0 one-pass pairs; RMSNorm input) and the
+// K-quant down matmul (plain h rows of 3 passes). Anything else: false.
+bool launch_mmq_q(const MmqSeg *seg, const int *types, int nseg, int mode, const MmqArgs &a, const MmqQuant &q,
+                  hipStream_t s) {
+    if (!mmq16_on(a.nt)) return false;
+    MmqSeg sg[3] = {seg[0], nseg > 1 ? seg[1] : MmqSeg{}, nseg > 2 ? seg[2] : MmqSeg{}};
+    int tiles = 0;
+    size_t lds = 0;
+    for (int i = 0; i < nseg; ++i) {
+        tiles += (sg[i].w.rows + RT16 - 1) / RT16;
+        lds = std::max(lds, (size_t)(mode == MMQ_SWIGLU ? 2 : 1) * MMQ_NT * 4 * sizeof(float) +
+                                (size_t)(types[i] == 8 ? a.K / 32 : a.K / 256) * TT16 * sizeof(float));
+    }
+    lds = std::max(lds, act_bytes(a.K) + smem_bytes(a.K));  // the producers' record + scratch
+    const dim3 grid(a.nt + tiles);
+    auto go = [&](auto kern) {
+        if (lds > 64 * 1024) allow_lds_mmq(reinterpret_cast<const void *>(kern));
+        hipLaunchKernelGGL(kern, grid, dim3(MMQ_NT), lds, s, sg[0], sg[1], sg[2], a, q);
+        return true;
+    };
+    const int np = pick_np(a.K);
+    if (mode == MMQ_STORE && nseg == 3 && q.mode == 0 && np == 1 && types[0] == 12 && types[1] == 12) {
+        if (types[2] == 12) return go(k_mmq16<12, 12, 12, MMQ_STORE, 0, 1, 0>);
+        if (types[2] == 14) return go(k_mmq16<12, 12, 14, MMQ_STORE, 0, 1, 0>);
+    }
+    if (mode == MMQ_SWIGLU && nseg == 1 && q.mode == 0 && np == 1) {
+        if (types[0] == 12) return go(k_mmq16<12, -1, -1, MMQ_SWIGLU, 0, 1, 0>);
+        if (types[0] == 8 && a.K % 256 == 0 && a.K <= 2048) return go(k_mmq16<8, -1, -1, MMQ_SWIGLU, 1, 1, 0>);
+    }
+    if (mode == MMQ_RESID && nseg == 1 && q.mode == 1 && np == 3) {
+        if (types[0] == 12) return go(k_mmq16<12, -1, -1, MMQ_RESID, 0, 3, 1>);
+        if (types[0] == 14) return go(k_mmq16<14, -1, -1, MMQ_RESID, 0, 3, 1>);
+    }
+    return false;
 }
 
 }  // namespace mio

@@ -37,11 +37,7 @@ constexpr int LDS_MAX = 160 * 1024;
 // ------------------------------------------------------------------ LDS layout
 // act[t] = {qs i8[K] | d f32[K/32+8] | bs i16[K/16+8]} x nt | resid f32[MW][nt * rpw] (the
 // wave's residual rows per token). The prologues quantize straight from registers (one wave
-// per token), so no f32 staging row is needed.
-__host__ __device__ inline size_t act_bytes(int K) {
-    return ((size_t)K + (size_t)(K / 32 + 8) * 4 + (size_t)(K / 16 + 8) * 2 + 15) & ~(size_t)15;
-}
-__host__ __device__ inline size_t act_base(int) { return 0; }
+// per token), so no f32 staging row is needed. (act_bytes / carve_t: llm_device.h)
 // K of the act record layout for a weight type: BF16 weights take the activation as K bf16
 // values (ggml's vec_dot_bf16 operand, 2 bytes each), stored in the qs area of a record laid out
 // for 2K (the d / bs areas then go unused)
@@ -50,15 +46,6 @@ __host__ __device__ inline size_t pf_lds_bytes(int K, int nt, int rpw) {
     return act_base(K) + act_bytes(K) * nt + (size_t)MW * nt * rpw * 4;
 }
 
-__device__ inline Smem carve_t(char *base, int K, int t) {
-    Smem s;
-    s.red = nullptr;
-    char *a = base + act_base(K) + act_bytes(K) * t;
-    s.a.qs = (int8_t *)a;
-    s.a.d = (float *)(a + K);
-    s.a.bs = (int16_t *)(a + K + (size_t)(K / 32 + 8) * 4);
-    return s;
-}
 __device__ inline float *resid_lds(char *base, int K, int nt, int rpw) {
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     return (float *)(base + act_base(K) + act_bytes(K) * nt) + (size_t)w * nt * rpw;
@@ -994,6 +981,11 @@ __global__ __launch_bounds__(ST) void k_bt_sample(LlmDims d, QMat emb, int nblk,
     __shared__ int bi_[ST / 64];
     __shared__ int tok_s;
     const int t = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // the step's last launch: both sets of the in-launch quantization counters start the next
+    // step at zero (launch_layers alternates them within a step)
+    if (t == 0 && tid < 16 && pb.qcnt)
+        __hip_atomic_store((__attribute__((address_space(1))) int *)(pb.qcnt + 64 * tid), 0, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
     const SampleCfg sc = bb.cfg[t];
     StepState *st = bb.st + t;
     const int step = st->step;
@@ -1210,6 +1202,21 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
     // MIO_BT_ATT=0: the batched decode step uses k_pf_rope + k_pf_attention (A/B)
     static const bool bt_att = !(getenv("MIO_BT_ATT") && getenv("MIO_BT_ATT")[0] == '0');
     decode = decode && bt_att;
+    // MIO_BT_QF (default 1): in the batched decode, the 16x16 matmuls quantize their input in
+    // the launch (launch_mmq_q: producer workgroups + counters) instead of behind a k_bt_quant
+    // launch; the counter sets alternate per fused launch (k_bt_sample zeroes both at the end of
+    // each step)
+    static const bool qf_env = !(getenv("MIO_BT_QF") && getenv("MIO_BT_QF")[0] == '0');
+    int qi = 0;
+    auto fused_q = [&](const MmqSeg *sg, const int *ty, int nseg, int mode, const MmqArgs &a, const float *src,
+                       const float *nw, int qmode) {
+        if (!decode || !qf_env || !pb.qcnt) return false;
+        const int set = qi & 1;
+        const MmqQuant q{src, nw, qmode, d.eps, pb.qcnt + 512 * set, pb.qcnt + 512 * (1 - set), pb.qcnt + kQcntFlag};
+        if (!launch_mmq_q(sg, ty, nseg, mode, a, q, s)) return false;
+        ++qi;
+        return true;
+    };
     const int QD = (d.n_head + 2 * d.n_kv) * d.hd;
     for (int il = 0; il < n_layer; ++il) {
         const LayerW &L = layers[il];
@@ -1242,13 +1249,17 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
                                   ? -1
                                   : (L.wo.type == 8 ? (gh % 32 == 0 ? 0 : -1) : (gh % 256 == 0 ? 1 : -1));
             const bool fa = fq2(0, L.wq.type);
-            if (!fa)
+            const bool mq0 = !fa && use_mmq(0, L.wq.type);
+            const MmqSeg sg0[3] = {{L.wq, mmq_tiles(L.wq.rows), 0}, {L.wk, mmq_tiles(L.wk.rows), L.wq.rows},
+                                   {L.wv, mmq_tiles(L.wv.rows), L.wq.rows + L.wk.rows}};
+            const int ty0[3] = {L.wq.type, L.wk.type, L.wv.type};
+            const MmqArgs a0{pb.act, act_bytes(d.n_embd), d.n_embd, nt, pb.qkv, QD, {}};
+            const bool q0 = mq0 && fused_q(sg0, ty0, 3, MMQ_STORE, a0, pb.x, L.attn_norm, 0);
+            if (!fa && !q0)
                 launch_quant(d, 0, pb.x, d.n_embd, L.attn_norm, akind(L.wq.type), pb, nt, s);
-            if (!fa && use_mmq(0, L.wq.type)) {
-                const MmqSeg sg[3] = {{L.wq, mmq_tiles(L.wq.rows), 0}, {L.wk, mmq_tiles(L.wk.rows), L.wq.rows},
-                                      {L.wv, mmq_tiles(L.wv.rows), L.wq.rows + L.wk.rows}};
-                const int ty[3] = {L.wq.type, L.wk.type, L.wv.type};
-                launch_mmq(sg, ty, 3, MMQ_STORE, MmqArgs{pb.act, act_bytes(d.n_embd), d.n_embd, nt, pb.qkv, QD, {}}, s);
+            if (q0) {
+            } else if (mq0) {
+                launch_mmq(sg0, ty0, 3, MMQ_STORE, a0, s);
             } else {
                 int GW, g_qk;
                 attn_in_grid(d, L, GW, g_qk);
@@ -1321,12 +1332,15 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
             }
         }
         const bool ff = fq2(1, L.gate.type);
-        if (!ff)
+        const bool mq2 = !ff && use_mmq(2, L.gate.type);
+        const MmqSeg sg2{L.gate, mmq_tiles(L.gate.rows), 0};
+        const MmqArgs a2{pb.act, act_bytes(d.n_embd), d.n_embd, nt, pb.h, d.n_ff, L.up};
+        const bool q2 = mq2 && fused_q(&sg2, &L.gate.type, 1, MMQ_SWIGLU, a2, pb.x, L.ffn_norm, 0);
+        if (!ff && !q2)
             launch_quant(d, 0, pb.x, d.n_embd, L.ffn_norm, akind(L.gate.type), pb, nt, s);
-        if (!ff && use_mmq(2, L.gate.type)) {
-            const MmqSeg sg{L.gate, mmq_tiles(L.gate.rows), 0};
-            launch_mmq(&sg, &L.gate.type, 1, MMQ_SWIGLU,
-                       MmqArgs{pb.act, act_bytes(d.n_embd), d.n_embd, nt, pb.h, d.n_ff, L.up}, s);
+        if (q2) {
+        } else if (mq2) {
+            launch_mmq(&sg2, &L.gate.type, 1, MMQ_SWIGLU, a2, s);
         } else {
             const LlmDims dw = bt_wgm(d, d.n_embd);
             const int grid = matvec_grid(dw, L.gate.rows);
@@ -1347,11 +1361,14 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
                 });
             });
         }
-        launch_quant(d, 1, pb.h, L.down.k, nullptr, akind(L.down.type), pb, nt, s);
-        if (use_mmq(3, L.down.type)) {
-            const MmqSeg sg{L.down, mmq_tiles(L.down.rows), 0};
-            launch_mmq(&sg, &L.down.type, 1, MMQ_RESID,
-                       MmqArgs{pb.act, act_bytes(L.down.k), L.down.k, nt, pb.x, d.n_embd, {}}, s);
+        const bool mq3 = use_mmq(3, L.down.type);
+        const MmqSeg sg3{L.down, mmq_tiles(L.down.rows), 0};
+        const MmqArgs a3{pb.act, act_bytes(L.down.k), L.down.k, nt, pb.x, d.n_embd, {}};
+        const bool q3 = mq3 && fused_q(&sg3, &L.down.type, 1, MMQ_RESID, a3, pb.h, nullptr, 1);
+        if (!q3) launch_quant(d, 1, pb.h, L.down.k, nullptr, akind(L.down.type), pb, nt, s);
+        if (q3) {
+        } else if (mq3) {
+            launch_mmq(&sg3, &L.down.type, 1, MMQ_RESID, a3, s);
         } else {
             const int grid = matvec_grid(d, L.down.rows), rpw = rows_per_wave(L.down.rows, grid);
             const int KR = rec_k(L.down.k, L.down.type);

@@ -454,6 +454,7 @@ int prefill(mio_hip_llm *m, int n) {
 int reset_tickets(mio_hip_llm *m) {
     MIO_HIP_CHECK(hipMemsetAsync(m->buf.att_cnt, 0, (size_t)mio::kAttCntInts * sizeof(int), m->d->stream));
     MIO_HIP_CHECK(hipMemsetAsync(m->pf.att_cnt, 0, (size_t)mio::kPrefillB * m->dims.n_kv * sizeof(int), m->d->stream));
+    MIO_HIP_CHECK(hipMemsetAsync(m->pf.qcnt, 0, (size_t)mio::kQcntInts * sizeof(int), m->d->stream));
     return MIO_OK;
 }
 
@@ -864,6 +865,7 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
     want(m->pf.part, (size_t)mio::kPrefillB * D.n_head * D.max_splits * (D.hd + 4));
     want(m->pf.att, (size_t)mio::kPrefillB * D.n_head * D.hd);
     want(m->pf.att_cnt, (size_t)mio::kPrefillB * D.n_kv);
+    want(m->pf.qcnt, (size_t)mio::kQcntInts);  // batched decode in-launch quantization counters
     want(m->pf.act, mio::prefill_act_bytes(
                         mio::prefill_rec_k(std::max(std::max(D.n_embd, D.n_ff), D.n_head * D.hd), m->bf16 ? 30 : 8)));
     want(dr, (size_t)n_ctx * (D.hd / 2));
@@ -893,7 +895,7 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
         }
     }
     if (!m->kc || !m->vc || !m->buf.x || !m->buf.qkv || !m->buf.h || !m->buf.logits ||
-        !m->buf.part || !m->buf.att || !m->buf.att_cnt || !m->pf.att || !m->pf.att_cnt || !m->buf.smp || !m->buf.st || !m->d_cfg || !m->d_tokens || !m->d_force || !dr ||
+        !m->buf.part || !m->buf.att || !m->buf.att_cnt || !m->pf.att || !m->pf.att_cnt || !m->pf.qcnt || !m->buf.smp || !m->buf.st || !m->d_cfg || !m->d_tokens || !m->d_force || !dr ||
         !m->d_prompt || !m->pf.x || !m->pf.qkv || !m->pf.h || !m->pf.part || !m->pf.act || !m->d_iota ||
         (any_conv && !m->buf.ring)) {
         mio::set_error("llm_load: device allocation failed");
@@ -1312,6 +1314,15 @@ extern "C" int mio_hip_llm_generate_batch(mio_hip_llm *m, const int32_t *prompts
         while (k < n && ring[k] != eos0 && ring[k] != eos1) ++k;
         std::memcpy(out_tokens + (size_t)b * max_tokens, ring.data(), (size_t)k * 4);
         n_out[b] = k;
+    }
+    // the in-launch quantization's bounded wait (launch_mmq_q) raises this flag if a producer's
+    // signal never came: an error instead of tokens computed from stale records
+    int qflag = 0;
+    MIO_HIP_CHECK(hipMemcpy(&qflag, m->pf.qcnt + mio::kQcntFlag, sizeof(int), hipMemcpyDeviceToHost));
+    if (qflag) {
+        MIO_HIP_CHECK(hipMemsetAsync(m->pf.qcnt + mio::kQcntFlag, 0, sizeof(int), m->d->stream));
+        mio::set_error("llm_generate_batch: the in-launch quantization hand-off wait timed out");
+        return MIO_ERR_HIP;
     }
     return MIO_OK;
 }
