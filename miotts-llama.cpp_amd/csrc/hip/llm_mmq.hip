@@ -1038,6 +1038,11 @@ bool launch_mmq_q(const MmqSeg *seg, const int *types, int nseg, int mode, const
         if (types[0] == 12) return go(k_mmq16<12, -1, -1, MMQ_RESID, 0, 3, 1>);
         if (types[0] == 14) return go(k_mmq16<14, -1, -1, MMQ_RESID, 0, 3, 1>);
     }
+    // Q8_0 down (multi-pass pair path) when MIO_MMQ_MASK puts it on the matrix cores
+    if (mode == MMQ_RESID && nseg == 1 && q.mode == 1 && types[0] == 8 && a.K % 256 == 0 && a.K > 2048) {
+        if (np == 3) return go(k_mmq16<8, -1, -1, MMQ_RESID, 2, 3, 1>);
+        if (np == 6) return go(k_mmq16<8, -1, -1, MMQ_RESID, 2, 6, 1>);
+    }
     return false;
 }
 

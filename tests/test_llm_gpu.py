@@ -54,6 +54,38 @@ def test_matvec_exact_per_type(device, qtype, k):
     assert np.abs(y - yo).max() <= 2e-5 * np.abs(yo).max() + 1e-6, np.abs(y - yo).max()
 
 
+def _bf16_round(x):
+    """ggml_compute_fp32_to_bf16: round to nearest even (finite inputs)."""
+    u = x.astype(np.float32).view(np.uint32).astype(np.uint64)
+    r = ((u + 0x7FFF + ((u >> 16) & 1)) >> 16).astype(np.uint32) << 16
+    return r.astype(np.uint32).view(np.float32)
+
+
+@pytest.mark.parametrize("k", [576, 2048, 6144])
+def test_bf16_matvec_derived_bound(device, k):
+    """BF16 rows (ggml vec_dot_bf16: the activation rounded to bf16, products of two bf16 exact
+    in f32, f32 sums): the GPU's v_dot2 matvec against the exact (float64) dot of the same
+    bf16 operands, within the f32 summation bound of its order — each lane sums its k / 64
+    products in sequence, then a 6-level lane tree and the pass sum: |err| <= (k / 64 + 8) *
+    2^-24 * sum_i |w_i x_i| per row (about 1e-6 of that sum at k = 2048). An f32 (unrounded)
+    activation breaks it by ~2^-9: checked to exceed the bound (teeth)."""
+    rng = np.random.default_rng(k + 30)
+    rows = 41
+    w = (rng.standard_normal((rows, k)) * 0.05).astype(np.float32)
+    wq = m.quantize_rows(30, w)  # bf16 bit patterns, ggml row layout
+    wb = (wq.view(np.uint16).reshape(rows, k).astype(np.uint32) << 16).view(np.float32)
+    x = rng.standard_normal(k).astype(np.float32)
+    y = m.debug_matvec(device, 30, wq, k, x).astype(np.float64)
+    xb = _bf16_round(x)
+    exact = wb.astype(np.float64) @ xb.astype(np.float64)
+    sabs = np.abs(wb.astype(np.float64)) @ np.abs(xb.astype(np.float64))
+    bound = (k / 64 + 8) * 2.0 ** -24 * sabs
+    err = np.abs(y - exact)
+    assert np.all(err <= bound), (float((err / sabs).max()), float((bound / sabs).max()))
+    unrounded = wb.astype(np.float64) @ x.astype(np.float64)
+    assert np.any(np.abs(y - unrounded) > bound), "bf16 rounding of the activation not observable"
+
+
 # 9: Q4_K_M at the 0.1B width, whose q/k/v, O, gate/up and embedding rows (576 long) are
 # llama-quantize's Q5_0 / Q8_0 fallbacks; 10: Q4_0 (Q5_0 and Q4_0 run as the equal Q8_0 rows);
 # 11: BF16 (v_dot2 over the bf16-rounded activation, ggml's vec_dot_bf16)
@@ -364,3 +396,45 @@ def test_mmq_equals_single_token_matvec(device, qtype, k, rows, nt):
         want = g / (1.0 + np.exp(-g)) * u
         err = float(np.abs(y[t] - want).max())
         assert err <= 1e-5 * float(np.abs(want).max()) + 1e-6, (t, err)
+
+
+_FUSION_SCRIPT = r"""
+import hashlib, sys
+import numpy as np
+sys.path.insert(0, sys.argv[2])
+import miotts_amd as m
+dev = m.Device(0)
+g = m.Llm(dev, sys.argv[1], 512)
+prompt = np.array([256, 257, 65, 258, 257, 300, 301], np.int32)
+toks = g.generate(prompt, 80, 0.8, 5, allow=(m.SYNTH_SPEECH0, m.SYNTH_SPEECH0 + 12800), check_interval=16)
+h = hashlib.sha256(toks.tobytes())
+for pos in (3, 70, 129):
+    h.update(g.eval(int(toks[0]), pos).tobytes())
+print(g.step_kinds().count(11), g.step_kinds().count(10), h.hexdigest())
+"""
+
+
+@pytest.mark.parametrize("preset", [2, 3])
+def test_fused_attention_launches_bit_identical(synth_llm_path, tmp_path, preset):
+    """The attention block as one launch (k_layer_att, layers >= 1), attention + O as one
+    launch (k_att_o) and the three separate launches run the same arithmetic: 80 free-run
+    tokens and the logits of three later evaluations are bit-identical across
+    MIO_LAYER_ATT / MIO_ATT_FUSE_O (each variant is a fresh process: the switches are read once)."""
+    import os
+    import subprocess
+    import sys
+    path = synth_llm_path(preset)
+    script = tmp_path / "fusion.py"
+    script.write_text(_FUSION_SCRIPT)
+    pkg = os.path.dirname(os.path.dirname(m.__file__))
+    outs = {}
+    for name, env in (("layer_att", {}), ("att_o", {"MIO_LAYER_ATT": "0"}),
+                      ("separate", {"MIO_ATT_FUSE_O": "0"})):
+        p = subprocess.run([sys.executable, str(script), path, pkg], capture_output=True, text=True, timeout=240,
+                           env=dict(os.environ, **env))
+        assert p.returncode == 0, p.stderr[-2000:]
+        outs[name] = p.stdout.split()
+    assert int(outs["layer_att"][0]) > 0 and int(outs["att_o"][0]) == 0 and int(outs["att_o"][1]) > 0
+    assert int(outs["separate"][0]) == int(outs["separate"][1]) == 0
+    print(outs)
+    assert outs["layer_att"][2] == outs["att_o"][2] == outs["separate"][2], outs
