@@ -796,6 +796,39 @@ __device__ __forceinline__ v4f slot16_sum(const float *red) {
 // KP: the launch is Q8_0 with K % 256 == 0 and (1) K <= 2048 or (2) K > 2048 (host-checked),
 // so only that pair path is compiled into it: the generic kernel (KP 0) carries three Q8_0
 // paths, and its size alone cost the 2.6B gate|up launch 19.2 vs 14.4 us
+// In-launch quantization producer (launch_mmq_q): workgroup t quantizes token t's input with
+// k_bt_quant's arithmetic into an LDS record laid out as the global one, copies it out with
+// 16-B write-through stores, drains them and adds 1 to each of the 8 counter shards. Workgroup
+// 0 also zeroes the other counter set (the next fused launch's).
+template <int AK, int QNP, int QM>
+__device__ __forceinline__ void mmq_quant_producer(const MmqArgs &a, const MmqQuant &q, char *lds) {
+    const int t = blockIdx.x;
+    if (blockIdx.x == 0 && threadIdx.x < 8)
+        __hip_atomic_store((__attribute__((address_space(1))) int *)(q.other + 64 * threadIdx.x), 0, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    Smem st = carve(lds + act_bytes(a.K), a.K);
+    st.a = carve_t(lds, a.K, 0).a;
+    XRegs<QNP> xr;
+    load_x(q.src + (size_t)t * a.K, QM == 0 ? q.norm_w : nullptr, a.K, xr);
+    if constexpr (QM == 0)
+        rmsnorm_quant(xr, a.K, q.eps, AK, st);
+    else
+        plain_quant(xr, a.K, AK, st);
+    const int n16 = (int)(act_bytes(a.K) / 16);
+    const auto dst = rsrc(a.act + (size_t)t * a.act_stride, (uint32_t)act_bytes(a.K));
+    for (int i = threadIdx.x; i < n16; i += MMQ_NT) {
+        const uint4 v = reinterpret_cast<const uint4 *>(lds)[i];
+        u32x4 u;
+        u.x = v.x, u.y = v.y, u.z = v.z, u.w = v.w;
+        __builtin_amdgcn_raw_buffer_store_b128(u, dst, i * 16, 0, 16);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x < 8)
+        __hip_atomic_fetch_add((__attribute__((address_space(1))) int *)(q.cnt + 64 * threadIdx.x), 1,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // QNP > 0 (k_mmq16q): the first a.nt workgroups are quantization producers (MmqQuant, XRegs
 // of QNP passes, QM = its mode), the tiles follow and wait before their activation reads.
 template <int T0, int T1, int T2, int MODE, int KP = 0, int QNP = 0, int QM = 0>
@@ -805,35 +838,7 @@ __global__ __launch_bounds__(MMQ_NT) void k_mmq16(MmqSeg s0, MmqSeg s1, MmqSeg s
     constexpr bool QF = QNP > 0;
     if constexpr (QF) {
         if ((int)blockIdx.x < a.nt) {
-            // producer: k_bt_quant's arithmetic into an LDS record laid out as the global one,
-            // then copied write-through (16-B sc1 stores), drained, and signalled
-            const int t = blockIdx.x;
-            const int ak = T0 == 8 ? 0 : 1;
-            if (blockIdx.x == 0 && threadIdx.x < 8) {
-                __hip_atomic_store((__attribute__((address_space(1))) int *)(q.other + 64 * threadIdx.x), 0,
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            Smem st = carve(lds + act_bytes(a.K), a.K);
-            st.a = carve_t(lds, a.K, 0).a;
-            XRegs<QNP> xr;
-            load_x(q.src + (size_t)t * a.K, QM == 0 ? q.norm_w : nullptr, a.K, xr);
-            if constexpr (QM == 0)
-                rmsnorm_quant(xr, a.K, q.eps, ak, st);
-            else
-                plain_quant(xr, a.K, ak, st);
-            const int n16 = (int)(act_bytes(a.K) / 16);
-            const auto dst = rsrc(a.act + (size_t)t * a.act_stride, (uint32_t)act_bytes(a.K));
-            for (int i = threadIdx.x; i < n16; i += MMQ_NT) {
-                const uint4 v = reinterpret_cast<const uint4 *>(lds)[i];
-                u32x4 u;
-                u.x = v.x, u.y = v.y, u.z = v.z, u.w = v.w;
-                __builtin_amdgcn_raw_buffer_store_b128(u, dst, i * 16, 0, 16);
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-            if (threadIdx.x < 8)
-                __hip_atomic_fetch_add((__attribute__((address_space(1))) int *)(q.cnt + 64 * threadIdx.x), 1,
-                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            mmq_quant_producer<T0 == 8 ? 0 : 1, QNP, QM>(a, q, lds);
             return;
         }
     }
@@ -922,6 +927,92 @@ __global__ __launch_bounds__(MMQ_NT) void k_mmq16(MmqSeg s0, MmqSeg s1, MmqSeg s
     }
 }
 
+
+// Q8_0 one-pass pairs (K % 256 == 0, K <= 2048), one matrix (W, or W | U for SwiGLU): each
+// workgroup walks tiles blockIdx, + G, + 2G ... with the next tile's weights in flight while it
+// reduces the current one (ping-pong register sets, no copies), and loads the activations and
+// their scales ONCE. With 672 tiles (the 2.6B gate|up) the plain grid runs 1.3 rounds of two
+// workgroups per CU; here one workgroup per CU streams its 2-3 tiles back to back. Per tile the
+// arithmetic is k_mmq16's (q80p_acc, tree8, slot16_sum, the same epilogue): bit-identical.
+// QNP > 0: the first a.nt workgroups are the in-launch quantization producers.
+template <int MODE, int QNP, int QM>
+__global__ __launch_bounds__(MMQ_NT) void k_mmq16_loop(MmqSeg s0, MmqArgs a, MmqQuant q, int n_tiles) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    constexpr int NV = MODE == MMQ_SWIGLU ? 2 : 1;
+    constexpr bool QF = QNP > 0;
+    const int nq = QF ? a.nt : 0;
+    if constexpr (QF) {
+        if ((int)blockIdx.x < nq) {
+            mmq_quant_producer<0, QNP, QM>(a, q, lds);
+            return;
+        }
+    }
+    float *red = reinterpret_cast<float *>(lds);  // [NV][8 waves][64][4]
+    float *da = red + NV * MMQ_NT * 4;           // [groups][16 tokens]
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int k = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int G = (int)gridDim.x - nq;
+    int tile = (int)blockIdx.x - nq;
+    if (tile >= n_tiles) return;
+    const int nb = a.K >> 5;
+    auto row_of = [&](int ti) { return min(ti * RT16 + (lane & 15), s0.w.rows - 1); };
+    Q80Pass wA, uA, wB, uB;
+    q80p_load(s0.w, row_of(tile), 0, k, wA);
+    if constexpr (NV == 2) q80p_load(a.w_up, row_of(tile), 0, k, uA);
+    if constexpr (QF) {
+        if (threadIdx.x == 0) wait_count(q.cnt + 64 * (blockIdx.x & 7), a.nt, q.flag);
+        asm volatile("s_barrier" ::: "memory");
+    }
+    const int8_t *aq = act16_codes(a, 0);
+    v4i x[4];
+    act_load(aq, a.K, 0, k, x);
+    stage_act16<8>(a, 0, a.K, da);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) swap_halves(x[i]);
+    // one tile: the next tile's loads (clamped to this tile at the end: L2 hits) go out first
+    auto step = [&](Q80Pass &cw, Q80Pass &cu, Q80Pass &nw, Q80Pass &nu) -> bool {
+        const int next = tile + G < n_tiles ? tile + G : tile;
+        q80p_load(s0.w, row_of(next), 0, k, nw);
+        if constexpr (NV == 2) q80p_load(a.w_up, row_of(next), 0, k, nu);
+        v4f acc[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[i] = v4f{};
+        q80p_acc(cw, x, 0, k, nb, da, acc);
+        slot16_store(tree8(acc), red);
+        if constexpr (NV == 2) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) acc[i] = v4f{};
+            q80p_acc(cu, x, 0, k, nb, da, acc);
+            slot16_store(tree8(acc), red + MMQ_NT * 4);
+        }
+        __syncthreads();
+        if (wave == 0) {
+            const v4f y = slot16_sum(red);
+            v4f u = {};
+            if constexpr (NV == 2) u = slot16_sum(red + MMQ_NT * 4);
+            const int orow = tile * RT16 + (lane & 15);
+            if (orow < s0.w.rows) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int t = tok16(lane, i);
+                    if (t >= a.nt) continue;
+                    float *o = a.out + (size_t)t * a.ld + s0.out_off + orow;
+                    if constexpr (MODE == MMQ_STORE) *o = y[i];
+                    else if constexpr (MODE == MMQ_RESID) *o = y[i] + *o;
+                    else *o = silu_f(y[i]) * u[i];
+                }
+            }
+        }
+        __syncthreads();  // red is rewritten by the next tile
+        if (next == tile) return false;
+        tile = next;
+        return true;
+    };
+    for (;;) {
+        if (!step(wA, uA, wB, uB)) break;
+        if (!step(wB, uB, wA, uA)) break;
+    }
+}
 }  // namespace
 
 size_t mmq_lds(int type, int K, int mode) {
@@ -947,6 +1038,22 @@ int mmq_tiles(int rows) { return (rows + RT - 1) / RT; }
 
 // types: {T0, T1, T2} (-1 = segment unused); mode MMQ_*.
 // 16 x 16 tiles (k_mmq16) for launches of at most 16 tokens; MIO_MMQ16=0: 32 x 32 tiles always
+// CUs of the current device (the tile-loop grids: one workgroup per CU), cached
+static int n_cu() {
+    static const int n = [] {
+        int dev = 0, v = 0;
+        hipGetDevice(&dev);
+        return hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0 ? v : 256;
+    }();
+    return n;
+}
+// MIO_MMQ_LOOP (default 1): Q8_0 one-pass launches with more 16-row tiles than CUs walk their
+// tiles in k_mmq16_loop (one workgroup per CU) instead of one workgroup per tile
+static bool mmq_loop_on() {
+    static const bool on = !(getenv("MIO_MMQ_LOOP") && getenv("MIO_MMQ_LOOP")[0] == '0');
+    return on;
+}
+
 bool mmq16_on(int nt) {
     static const bool on = !(getenv("MIO_MMQ16") && getenv("MIO_MMQ16")[0] == '0');
     return on && nt <= TT16;
@@ -971,6 +1078,18 @@ void launch_mmq(const MmqSeg *seg, const int *types, int nseg, int mode, const M
         if (t16) {
             const bool q8 = A == 8 && (B < 0 || B == 8) && (C < 0 || C == 8) && a.K % 256 == 0;
             const int kp = q8 ? (a.K <= 2048 ? 1 : 2) : 0;
+            if constexpr (A == 8 && B < 0) {
+                if (kp == 1 && tiles > n_cu() && mmq_loop_on()) {
+                    auto kl = [&](auto kern) {
+                        if (lds > 64 * 1024) allow_lds_mmq(reinterpret_cast<const void *>(kern));
+                        hipLaunchKernelGGL(kern, dim3(n_cu()), dim3(MMQ_NT), lds, s, sg[0], a, MmqQuant{}, tiles);
+                    };
+                    if (mode == MMQ_STORE) kl(k_mmq16_loop<MMQ_STORE, 0, 0>);
+                    else if (mode == MMQ_RESID) kl(k_mmq16_loop<MMQ_RESID, 0, 0>);
+                    else kl(k_mmq16_loop<MMQ_SWIGLU, 0, 0>);
+                    return;
+                }
+            }
             auto kpl = [&]<int M>() {
                 if (kp == 1) launch(k_mmq16<A, B, C, M, 1>);
                 else if (kp == 2) launch(k_mmq16<A, B, C, M, 2>);
@@ -1032,7 +1151,16 @@ bool launch_mmq_q(const MmqSeg *seg, const int *types, int nseg, int mode, const
     }
     if (mode == MMQ_SWIGLU && nseg == 1 && q.mode == 0 && np == 1) {
         if (types[0] == 12) return go(k_mmq16<12, -1, -1, MMQ_SWIGLU, 0, 1, 0>);
-        if (types[0] == 8 && a.K % 256 == 0 && a.K <= 2048) return go(k_mmq16<8, -1, -1, MMQ_SWIGLU, 1, 1, 0>);
+        if (types[0] == 8 && a.K % 256 == 0 && a.K <= 2048) {
+            const int nl = n_cu() - a.nt;  // the producers keep CUs of their own
+            if (tiles > nl && nl > 0 && mmq_loop_on()) {
+                auto kern = k_mmq16_loop<MMQ_SWIGLU, 1, 0>;
+                if (lds > 64 * 1024) allow_lds_mmq(reinterpret_cast<const void *>(kern));
+                hipLaunchKernelGGL(kern, dim3(a.nt + nl), dim3(MMQ_NT), lds, s, sg[0], a, q, tiles);
+                return true;
+            }
+            return go(k_mmq16<8, -1, -1, MMQ_SWIGLU, 1, 1, 0>);
+        }
     }
     if (mode == MMQ_RESID && nseg == 1 && q.mode == 1 && np == 3) {
         if (types[0] == 12) return go(k_mmq16<12, -1, -1, MMQ_RESID, 0, 3, 1>);
