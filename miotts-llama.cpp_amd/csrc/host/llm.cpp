@@ -293,12 +293,19 @@ int check_handoff(mio_hip_llm *m) {
 
 // MIO_LAYER_ATT (default 1): layers >= 1 run their whole attention block as one launch
 // (k_layer_att, which = 11) where it is instantiated; 0 keeps attn_in + the k_att_o launch.
+// MIO_LAYER_ATT: unset = measured policy, "0" = never, "1" = wherever instantiated. The policy
+// leaves the hd 64 / 3-query-head shape (0.1B) on attn_in + k_att_o: its q|k|v hand-off inside
+// the launch costs more than the boundary it removes (C2 93.0x fused vs 97.5x, and 86.8-89.1x
+// vs 97.4x with 4 polls in flight; 1.7B Q4_K_M 54.27x vs 53.8x, 2.6B 35.43x vs 35.16x, 1.7B BF16
+// even: profiles/r05_layer_att_policy.txt).
 bool fuse_layer_att(const mio_hip_llm *m, int il) {
-    static const bool env = [] {
+    static const int env = [] {
         const char *e = getenv("MIO_LAYER_ATT");
-        return !(e && *e == '0');
+        return e && *e == '0' ? 0 : (e && *e == '1' ? 1 : -1);
     }();
-    return env && il > 0 && fuse_att_o(m) && mio::layer_att_supported(m->dims, m->layers[il]);
+    if (env == 0 || il == 0 || !fuse_att_o(m) || !mio::layer_att_supported(m->dims, m->layers[il])) return false;
+    const mio::LlmDims &d = m->dims;
+    return env == 1 || !(d.hd == 64 && d.n_head == 3 * d.n_kv);
 }
 
 int layer_kinds(const mio_hip_llm *m, int il, int *w) {

@@ -428,7 +428,7 @@ def test_fused_attention_launches_bit_identical(synth_llm_path, tmp_path, preset
     script.write_text(_FUSION_SCRIPT)
     pkg = os.path.dirname(os.path.dirname(m.__file__))
     outs = {}
-    for name, env in (("layer_att", {}), ("att_o", {"MIO_LAYER_ATT": "0"}),
+    for name, env in (("layer_att", {"MIO_LAYER_ATT": "1"}), ("att_o", {"MIO_LAYER_ATT": "0"}),
                       ("separate", {"MIO_ATT_FUSE_O": "0"})):
         p = subprocess.run([sys.executable, str(script), path, pkg], capture_output=True, text=True, timeout=240,
                            env=dict(os.environ, **env))
