@@ -62,10 +62,10 @@ void launch_rownorm(const float *x, float *y, int M, int D, float eps, int mode,
 // xa = f16(silu(GroupNorm(x) * gamma + beta)) over [L][C], G groups of C/G channels
 // (C % 8 == 0, C <= 1024, G <= 64, 64 % (C/G) == 0). Five launches on stream s.
 struct GnScratch {
-    double *part;        // kGnPartDoubles: [P <= 256][G] slice sums
+    double *part;        // kGnPartDoubles: [2][P <= 256][64] slice sums (pass 1, pass 2)
     float2 *stat;        // [64] (mean, rstd)
 };
-constexpr int kGnPartDoubles = 256 * 64;
+constexpr int kGnPartDoubles = 2 * 256 * 64;
 void launch_groupnorm_apply(const float *x, int L, int C, int G, float eps, const float *gamma,
                             const float *beta, GnScratch gs, _Float16 *xa, hipStream_t s);
 // Banded (|i-j| <= window/2) RoPE attention, head_dim 64, q|k|v packed per row (ld = 3*D).

@@ -660,6 +660,160 @@ __global__ __launch_bounds__(1024) void gn_fused_kernel(const float *x, int L, i
     }
 }
 
+// ---------------------------------------------------------------- group norm, three launches
+// The sliced statistics without the two single-workgroup finals: every workgroup of the
+// launch after a partial pass reduces the P <= 128 slice sums itself (the same fixed order as
+// gn_final_kernel: 32 lanes per group, lane s takes slices s, s + 32, .., then a 5-level xor
+// tree), so the redundant copies agree bit for bit. gn_stat2 = means + pass-2 partials (its
+// workgroup 0 also stores the means); gn_apply3 = rstd + the f16 operand, 16 channels per
+// thread. Both issue their x loads before the reduction. 3 launches per GroupNorm instead of
+// 5 (sliced), ~128-256 workgroups each instead of gn_fused's one per group (32 on 256 CUs,
+// three dependent passes over a group strided through memory).
+constexpr int GN3_PMAX = 128;
+
+// out[g] (LDS) = sum over the P slice partials of group g, g < G (GI * 8 >= G, 256 threads)
+template <int GI>
+__device__ __forceinline__ void gn_reduce(const double *part, int P, int G, double *out) {
+    const int t = threadIdx.x, s32 = t & 31;
+    double v[GI][GN3_PMAX / 32];
+#pragma unroll
+    for (int k = 0; k < GI; ++k) {
+        const int g = k * 8 + (t >> 5), gg = g < G ? g : 0;
+#pragma unroll
+        for (int i = 0; i < GN3_PMAX / 32; ++i) {
+            const int q = s32 + 32 * i;
+            v[k][i] = part[(long)(q < P ? q : 0) * G + gg];
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < GI; ++k) {
+        const int g = k * 8 + (t >> 5);
+        double sum = 0.0;
+#pragma unroll
+        for (int i = 0; i < GN3_PMAX / 32; ++i)
+            if (s32 + 32 * i < P) sum += v[k][i];
+#pragma unroll
+        for (int o = 1; o < 32; o <<= 1) sum += __shfl_xor(sum, o);
+        if (s32 == 0 && g < G) out[g] = sum;
+    }
+    __syncthreads();
+}
+
+template <int NJ, int GI>
+__global__ __launch_bounds__(256) void gn_stat2_kernel(const float *x, int L, int C, int G, int cpg, int rows, long n,
+                                                       const double *part1, double *part2, float2 *stat) {
+    __shared__ double red[64];
+    __shared__ double wsum[4][64];
+    const int p = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int r0 = p * rows, r1 = min(L, r0 + rows);
+    double acc[NJ];
+    float mean[NJ];
+    bool ok[NJ];
+    int ch[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+        ok[j] = j * 64 + lane < C;
+        ch[j] = ok[j] ? j * 64 + lane : 0;
+        acc[j] = 0.0;
+    }
+    // the wave's first two rows are in flight while the slice sums are reduced (a row past
+    // r1 reads row r0, in range, and is not added)
+    float pre[2][NJ];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const int r = r0 + wave + 4 * k;
+        const float *xr = x + (long)(r < r1 ? r : r0) * C;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) pre[k][j] = xr[ch[j]];
+    }
+    gn_reduce<GI>(part1, gridDim.x, G, red);
+    if (p == 0 && threadIdx.x < G) stat[threadIdx.x].x = (float)(red[threadIdx.x] / (double)n);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) mean[j] = (float)(red[ch[j] / cpg] / (double)n);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        if (r0 + wave + 4 * k >= r1) break;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const float d = pre[k][j] - mean[j];
+            acc[j] += ok[j] ? (double)(d * d) : 0.0;
+        }
+    }
+#pragma unroll 2
+    for (int r = r0 + wave + 8; r < r1; r += 4) {
+        const float *xr = x + (long)r * C;
+        float v[NJ];
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) v[j] = xr[ch[j]];
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const float d = v[j] - mean[j];
+            acc[j] += ok[j] ? (double)(d * d) : 0.0;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+        double sm = acc[j];
+        for (int o = 1; o < cpg; o <<= 1) sm += __shfl_xor(sm, o);
+        if (lane % cpg == 0 && ok[j]) wsum[wave][(j * 64 + lane) / cpg] = sm;
+    }
+    __syncthreads();
+    for (int g = threadIdx.x; g < G; g += 256)
+        part2[(long)p * G + g] = ((wsum[0][g] + wsum[1][g]) + wsum[2][g]) + wsum[3][g];
+}
+
+template <int GI>
+__global__ __launch_bounds__(256) void gn_apply3_kernel(const float *x, int L, int C, int G, int cpg, int P, long n,
+                                                        float eps, const double *part2, const float2 *stat,
+                                                        const float *gamma, const float *beta, _Float16 *xa) {
+    __shared__ double red[64];
+    __shared__ float2 st[64];
+    // two 8-channel vectors per thread (grid = ceil(n8 / 512)); their x, gamma and beta are
+    // in flight while the pass-2 sums are reduced (an index past the end reads vector 0)
+    const long n8 = (long)L * C / 8;
+    long e8[2];
+    float4 u[2][2], gm[2][2], bt[2][2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        e8[k] = (long)blockIdx.x * 512 + 256 * k + threadIdx.x;
+        const long e = e8[k] < n8 ? e8[k] : 0;
+        const int c0 = (int)((e * 8) % C);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            u[k][h] = *reinterpret_cast<const float4 *>(x + e * 8 + 4 * h);
+            gm[k][h] = *reinterpret_cast<const float4 *>(gamma + c0 + 4 * h);
+            bt[k][h] = *reinterpret_cast<const float4 *>(beta + c0 + 4 * h);
+        }
+    }
+    gn_reduce<GI>(part2, P, G, red);
+    if (threadIdx.x < G) {
+        const float variance = (float)(red[threadIdx.x] / (double)n);
+        st[threadIdx.x] = make_float2(stat[threadIdx.x].x, 1.0f / sqrtf(variance + eps));
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        if (e8[k] >= n8) break;
+        const int c0 = (int)((e8[k] * 8) % C);
+        const float t[8] = {u[k][0].x, u[k][0].y, u[k][0].z, u[k][0].w, u[k][1].x, u[k][1].y, u[k][1].z, u[k][1].w};
+        const float ga[8] = {gm[k][0].x, gm[k][0].y, gm[k][0].z, gm[k][0].w,
+                             gm[k][1].x, gm[k][1].y, gm[k][1].z, gm[k][1].w};
+        const float be[8] = {bt[k][0].x, bt[k][0].y, bt[k][0].z, bt[k][0].w,
+                             bt[k][1].x, bt[k][1].y, bt[k][1].z, bt[k][1].w};
+        f16x8 o;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const float2 ms = st[(c0 + q) / cpg];
+            float y = t[q] - ms.x;
+            y = y * ms.y;
+            y = y * ga[q];
+            y = y + be[q];
+            o[q] = (_Float16)silu_f(y);
+        }
+        *reinterpret_cast<f16x8 *>(xa + e8[k] * 8) = o;
+    }
+}
+
 // xa[l][c] = f16(silu((x - mean) * rstd * gamma + beta)), 8 channels per thread.
 __global__ __launch_bounds__(256) void gn_apply_kernel(const float *x, int L, int C, int G, int cpg,
                                                        const float2 *stat, const float *gamma,
@@ -906,10 +1060,43 @@ void launch_rownorm(const float *x, float *y, int M, int D, float eps, int mode,
 void launch_groupnorm_apply(const float *x, int L, int C, int G, float eps, const float *gamma,
                             const float *beta, GnScratch gs, _Float16 *xa, hipStream_t s) {
     const int cpg = C / G;
-    // one launch when the group is whole float4 quads (cpg = 4, 8, 16, 32, 64: cpg | 64);
-    // MIO_GN_SLICED=1 keeps the sliced five-launch path (A/B)
-    static const bool sliced = getenv("MIO_GN_SLICED") && getenv("MIO_GN_SLICED")[0] == '1';
-    if (!sliced && cpg % 4 == 0 && (cpg & (cpg - 1)) == 0 && (long)L * (cpg / 4) < (1L << 30)) {
+    // MIO_GN=3 (default): three launches, every workgroup reducing the slice sums itself;
+    // MIO_GN=1: one workgroup per group (gn_fused_kernel) when the group is whole float4 quads
+    // (cpg = 4, 8, 16, 32, 64: cpg | 64); MIO_GN=5 (or 1 otherwise): the sliced five launches
+    static const int mode = getenv("MIO_GN") ? atoi(getenv("MIO_GN")) : 3;
+    const long n = (long)L * cpg;
+    if (mode == 3) {
+        int rows = 4;
+        if ((L + rows - 1) / rows > GN3_PMAX) rows = (L + GN3_PMAX - 1) / GN3_PMAX;
+        const int P = (L + rows - 1) / rows;
+        double *part1 = gs.part, *part2 = gs.part + GN_PMAX * 64;
+        const int nj = (C + 63) / 64;
+        const long n8 = (long)L * C / 8;
+        const unsigned ga = (unsigned)((n8 + 511) / 512);
+        auto go = [&](auto gi) {
+            constexpr int GI = decltype(gi)::value;
+            switch (nj) {
+#define G3(J)                                                                                                      \
+    case J:                                                                                                        \
+        hipLaunchKernelGGL((gn_partial_kernel<1, J>), dim3(P), dim3(256), 0, s, x, L, C, G, cpg, rows,             \
+                           (const float2 *)gs.stat, part1);                                                        \
+        hipLaunchKernelGGL((gn_stat2_kernel<J, GI>), dim3(P), dim3(256), 0, s, x, L, C, G, cpg, rows, n, part1,     \
+                           part2, gs.stat);                                                                        \
+        break;
+                G3(1) G3(2) G3(3) G3(4) G3(5) G3(6) G3(7) G3(8) G3(9) G3(10) G3(11) G3(12) G3(13) G3(14) G3(15) G3(16)
+#undef G3
+                default: return;  // C <= 1024 (codec.cpp refuses larger)
+            }
+            hipLaunchKernelGGL((gn_apply3_kernel<GI>), dim3(ga), dim3(256), 0, s, x, L, C, G, cpg, P, n, eps, part2,
+                               (const float2 *)gs.stat, gamma, beta, xa);
+        };
+        if (G <= 32)
+            go(std::integral_constant<int, 4>{});
+        else
+            go(std::integral_constant<int, 8>{});
+        return;
+    }
+    if (mode == 1 && cpg % 4 == 0 && (cpg & (cpg - 1)) == 0 && (long)L * (cpg / 4) < (1L << 30)) {
         int qsh = 0;
         while ((4 << qsh) < cpg) ++qsh;
         hipLaunchKernelGGL(gn_fused_kernel, dim3(G), dim3(1024), 0, s, x, L, C, cpg, qsh, eps, gamma, beta, xa);
@@ -918,7 +1105,6 @@ void launch_groupnorm_apply(const float *x, int L, int C, int G, float eps, cons
     int rows = 4;
     if ((L + rows - 1) / rows > GN_PMAX) rows = (L + GN_PMAX - 1) / GN_PMAX;
     const int P = (L + rows - 1) / rows;
-    const long n = (long)L * cpg;
     auto partial = [&](auto pass) {
         constexpr int PS = decltype(pass)::value;
         switch ((C + 63) / 64) {
