@@ -1149,6 +1149,10 @@ bool launch_mmq_q(const MmqSeg *seg, const int *types, int nseg, int mode, const
         if (types[2] == 12) return go(k_mmq16<12, 12, 12, MMQ_STORE, 0, 1, 0>);
         if (types[2] == 14) return go(k_mmq16<12, 12, 14, MMQ_STORE, 0, 1, 0>);
     }
+    // Q8_0 q|k|v (one pass, K <= 2048) when MIO_BT_FQ=0 takes it off the dot4 in-launch path
+    if (mode == MMQ_STORE && nseg == 3 && q.mode == 0 && np == 1 && types[0] == 8 && types[1] == 8 && types[2] == 8 &&
+        a.K % 256 == 0 && a.K <= 2048)
+        return go(k_mmq16<8, 8, 8, MMQ_STORE, 1, 1, 0>);
     if (mode == MMQ_SWIGLU && nseg == 1 && q.mode == 0 && np == 1) {
         if (types[0] == 12) return go(k_mmq16<12, -1, -1, MMQ_SWIGLU, 0, 1, 0>);
         if (types[0] == 8 && a.K % 256 == 0 && a.K <= 2048) {

@@ -903,6 +903,86 @@ __global__ __launch_bounds__(MT) void k_pf_ffn_down(LlmDims d, QMat down, Prefil
     });
 }
 
+// The batched decode's down on the dot4 engine with the h quantization in the launch (no
+// k_bt_quant_split launch in front; MIO_BT_QF). Workgroups [0, npr) are producers, one per
+// (token t, 2048-element chunk c) as k_bt_quant_split's grid: the chunk is quantized into an
+// LDS image of t's record with k_bt_quant_split's arithmetic (the same bits), its code, scale
+// and (Q8_K) bsum ranges are copied out with 16-B write-through stores, drained, and each
+// producer adds 1 to the 8 counter shards (workgroup 0 first zeroes the other set, the next
+// fused launch's). The matvec workgroups follow: residual and first weight group issued, one
+// lane waits for npr on its shard, then the records are copied to LDS (no workgroup of the
+// launch reads them before every producer has stored: the lines come from past the L2s).
+// Deadlock-free by dispatch order (producers first, they never wait).
+__device__ __forceinline__ void down_quant_producer(const float *src, int K, int kq, int nch, char *act,
+                                                    const MmqQuant &q, char *lds) {
+    const int t = blockIdx.x / nch, c = blockIdx.x - t * nch;
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (blockIdx.x == 0 && threadIdx.x < 8)
+        __hip_atomic_store((__attribute__((address_space(1))) int *)(q.other + 64 * threadIdx.x), 0, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    const ActL a = carve_t(lds, K, 0).a;
+    if (c * 2048 + wave * 256 < K) {  // wave-uniform
+        const float4 x = *reinterpret_cast<const float4 *>(src + (size_t)t * K + c * 2048 + 4 * (int)threadIdx.x);
+        const float v[4] = {x.x, x.y, x.z, x.w};
+        if (kq)
+            q8k_store(v, abs_max4(v), c * 8 + wave, a);
+        else
+            q80_store(v, c * 64 + wave * 8 + (lane >> 3), true, a);
+    }
+    __syncthreads();
+    // the chunk's ranges of the record: codes [2048 c, +2048), Q8_0 scales [64 c, +64) or Q8_K
+    // scales [8 c, +8) and bsums [128 c, +128); a partial last chunk copies its whole 256s only
+    const int nsb = min(8, (K - c * 2048) >> 8);
+    const int nq = nsb * 16, nd = kq ? (nsb * 4 + 15) / 16 : nsb * 2, nb = kq ? nsb * 2 : 0;
+    const auto dst = rsrc(act + (size_t)t * act_bytes(K), (uint32_t)act_bytes(K));
+    const int i = threadIdx.x;
+    uint32_t off = 0xFFFFFFFFu;
+    if (i < nq)
+        off = c * 2048 + 16 * i;
+    else if (i < nq + nd)
+        off = K + (kq ? c * 32 : c * 256) + 16 * (i - nq);
+    else if (i < nq + nd + nb)
+        off = K + (K / 32 + 8) * 4 + c * 256 + 16 * (i - nq - nd);
+    if (off != 0xFFFFFFFFu) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(lds + off);
+        u32x4 u;
+        u.x = v.x, u.y = v.y, u.z = v.z, u.w = v.w;
+        __builtin_amdgcn_raw_buffer_store_b128(u, dst, off, 0, 16);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x < 8)
+        __hip_atomic_fetch_add((__attribute__((address_space(1))) int *)(q.cnt + 64 * threadIdx.x), 1,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int NP, int T>
+__global__ __launch_bounds__(MT) void k_pf_ffn_down_q(LlmDims d, QMat down, PrefillBuffers pb, int nt, int rpw,
+                                                      MmqQuant q, int nch) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int K = down.k, E = d.n_embd, KR = rec_k(K, T), npr = nt * nch;
+    if ((int)blockIdx.x < npr) {
+        down_quant_producer(q.src, K, T != 8, nch, pb.act, q, smem);
+        return;
+    }
+    int lo, hi;
+    wave_range(down.rows, lo, hi, (int)blockIdx.x - npr, matvec_grid_n(d.n_wg, down.rows));
+    const Resid rr = load_resid_b(pb.x, E, lo, hi, nt, rpw);
+    Frag ga[CfgB<T, NP, 1>::U], gb[CfgB<T, NP, 1>::U];
+    load_first_b<T, NP, 1>(down, down, lo, hi, ga, gb);
+    if (threadIdx.x == 0) wait_count(q.cnt + 64 * (blockIdx.x & 7), npr, q.flag);
+    asm volatile("s_barrier" ::: "memory");
+    ActPre<NP> ap;
+    act_issue<NP>(pb.act, KR, nt, ap);
+    float *res = resid_lds(smem, KR, nt, rpw);
+    store_resid_b(rr, res, nt, rpw);
+    act_store<NP>(ap, pb.act, KR, smem, nt);
+    stream_rows_b<T, NP, 1>(down, down, lo, hi, ga, gb, smem, nt, [&](int row, int t, float v, float) {
+        const float r = res[t * rpw + row - lo];
+        pb.x[(size_t)t * E + row] = v + r;
+    });
+}
+
 __global__ __launch_bounds__(ST) void k_pf_embed(LlmDims d, QMat emb, PrefillBuffers pb, int p0) {
     const int t = blockIdx.x;
     embed_row(emb, pb.tokens[p0 + t], d.n_embd, pb.x + (size_t)t * d.n_embd);
@@ -1190,15 +1270,6 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
     // dot4 engine, instead of behind a k_bt_quant launch (and, for q|k|v, on the matrix cores).
     // 8-stream steps (graph; profiles/r04_fq_ab.txt): 2.6B Q8_0 2.354 ms with attn_in only,
     // 2.362 both, 2.488 neither or ffn_in only; 1.7B Q4_K_M 1.837 / 1.881 / 1.843 / 1.891
-    // default: attn_in in-launch for Q8_0 (its gate|up runs on the matrix cores, above), none for
-    // the K-quants (every matvec on the matrix cores)
-    static const int fq2_env = getenv("MIO_BT_FQ") ? atoi(getenv("MIO_BT_FQ")) : -1;
-    auto fq2 = [&](int kind, int type) {
-        const bool q8_pair = d.n_embd % 256 == 0 && d.n_embd <= 2048;
-        const bool on = fq2_env >= 0 ? ((fq2_env >> kind) & 1) != 0 : (type == 8 && (kind == 0 || !q8_pair));
-        return !mmq && nt <= MW && pick_np(d.n_embd) == 1 && on && type != 30;
-    };
-    static const bool att_q_env = !(getenv("MIO_ATT_Q") && getenv("MIO_ATT_Q")[0] == '0');
     // MIO_BT_ATT=0: the batched decode step uses k_pf_rope + k_pf_attention (A/B)
     static const bool bt_att = !(getenv("MIO_BT_ATT") && getenv("MIO_BT_ATT")[0] == '0');
     decode = decode && bt_att;
@@ -1207,6 +1278,20 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
     // launch; the counter sets alternate per fused launch (k_bt_sample zeroes both at the end of
     // each step)
     static const bool qf_env = !(getenv("MIO_BT_QF") && getenv("MIO_BT_QF")[0] == '0');
+    // MIO_BT_DQ=0: the dot4 down keeps its k_bt_quant_split launch (A/B)
+    static const bool dq_env = !(getenv("MIO_BT_DQ") && getenv("MIO_BT_DQ")[0] == '0');
+    // default: the Q8_0 q|k|v in-launch on dot4 only where the matrix cores cannot quantize in
+    // the launch themselves (r05: C4 169.0-169.3x with q|k|v on k_mmq16 + producers vs
+    // 161.8-162.2x on dot4, profiles/r05_c4_qkv_mfma_ab.txt); none for the K-quants (every
+    // matvec on the matrix cores)
+    static const int fq2_env = getenv("MIO_BT_FQ") ? atoi(getenv("MIO_BT_FQ")) : -1;
+    const bool qkv_qf = decode && qf_env && pb.qcnt && d.n_embd % 256 == 0 && d.n_embd <= 2048;
+    auto fq2 = [&](int kind, int type) {
+        const bool q8_pair = d.n_embd % 256 == 0 && d.n_embd <= 2048;
+        const bool on = fq2_env >= 0 ? ((fq2_env >> kind) & 1) != 0 : (type == 8 && (kind == 0 ? !qkv_qf : !q8_pair));
+        return !mmq && nt <= MW && pick_np(d.n_embd) == 1 && on && type != 30;
+    };
+    static const bool att_q_env = !(getenv("MIO_ATT_Q") && getenv("MIO_ATT_Q")[0] == '0');
     int qi = 0;
     auto fused_q = [&](const MmqSeg *sg, const int *ty, int nseg, int mode, const MmqArgs &a, const float *src,
                        const float *nw, int qmode) {
@@ -1365,10 +1450,27 @@ void launch_layers(const LlmDims &d, const LayerW *layers, int n_layer, _Float16
         const MmqSeg sg3{L.down, mmq_tiles(L.down.rows), 0};
         const MmqArgs a3{pb.act, act_bytes(L.down.k), L.down.k, nt, pb.x, d.n_embd, {}};
         const bool q3 = mq3 && fused_q(&sg3, &L.down.type, 1, MMQ_RESID, a3, pb.h, nullptr, 1);
-        if (!q3) launch_quant(d, 1, pb.h, L.down.k, nullptr, akind(L.down.type), pb, nt, s);
+        // the dot4 down quantizing h in the launch (Q8_0 / Q8_K, every token in one launch)
+        const int KD = L.down.k, akd = akind(L.down.type);
+        const bool q3d = !mq3 && decode && qf_env && pb.qcnt && dq_env && KD % 256 == 0 && akd != 2 &&
+                         tokens_per_launch(rec_k(KD, L.down.type), nt,
+                                           rows_per_wave(L.down.rows, matvec_grid(d, L.down.rows))) >= nt;
+        if (!q3 && !q3d) launch_quant(d, 1, pb.h, L.down.k, nullptr, akind(L.down.type), pb, nt, s);
         if (q3) {
         } else if (mq3) {
             launch_mmq(&sg3, &L.down.type, 1, MMQ_RESID, a3, s);
+        } else if (q3d) {
+            const int grid = matvec_grid(d, L.down.rows), rpw = rows_per_wave(L.down.rows, grid);
+            const int KR = rec_k(KD, L.down.type), nch = (KD + 2047) / 2048;
+            const int set = qi & 1;
+            ++qi;
+            const MmqQuant q{pb.h, nullptr, 1, d.eps, pb.qcnt + 512 * set, pb.qcnt + 512 * (1 - set), pb.qcnt + kQcntFlag};
+            const size_t lds = std::max(pf_lds_bytes(KR, nt, rpw), act_bytes(KD));
+            dispatch_nt<true>(KD, L.down.type, [&]<int NP, int T>() {
+                allow_lds(k_pf_ffn_down_q<NP, T>);
+                hipLaunchKernelGGL((k_pf_ffn_down_q<NP, T>), dim3(nt * nch + grid), dim3(MT), lds, s, d, L.down, pb, nt,
+                                   rpw, q, nch);
+            });
         } else {
             const int grid = matvec_grid(d, L.down.rows), rpw = rows_per_wave(L.down.rows, grid);
             const int KR = rec_k(L.down.k, L.down.type);
