@@ -1051,6 +1051,52 @@ __global__ __launch_bounds__(MT) void k_bt_lm_head(LlmDims d, const float *norm_
     }
 }
 
+// The batched lm_head's sampling partials from logits already in bb.logits ([t][rows], the
+// int8 matrix-core lm_head, MIO_BT_LM_MMQ): workgroup b of nblk takes rows [R b / nblk,
+// R (b + 1) / nblk) and writes, per stream, the Gumbel-max over its allowed rows as
+// k_bt_lm_head does (largest value, lowest row on ties: a total order, so k_bt_sample's
+// reduction picks the same token whatever the partition).
+__global__ __launch_bounds__(MT) void k_bt_gumbel(int R, BatchBuffers bb, int nt) {
+    // one wave per stream (t = wave, wave + 8, ..): its row loads go out 12 per lane at a time
+    // and it reduces with shuffles alone (no workgroup barrier between streams)
+    constexpr int U = 12;
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int r0 = (int)((long)R * blockIdx.x / gridDim.x), r1 = (int)((long)R * (blockIdx.x + 1) / gridDim.x);
+    for (int t = wave; t < nt; t += MW) {
+        const SampleCfg sc = bb.cfg[t];
+        const int step = bb.st[t].step;
+        const uint64_t seed = ((uint64_t)sc.seed_hi << 32) | sc.seed_lo;
+        const int lo = max(r0, sc.lo), hi = min(r1, sc.hi);
+        const float *lg = bb.logits + (size_t)t * R;
+        float best = -INFINITY;
+        int bi = INT_MAX;
+        for (int base = lo; base < hi; base += 64 * U) {
+            float v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) v[u] = lg[min(base + lane + 64 * u, hi - 1)];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int row = base + lane + 64 * u;
+                if (row < hi) {
+                    const float g = sc.temp > 0.0f ? v[u] / sc.temp + gumbel(seed, step, row) : v[u];
+                    if (g > best || (g == best && row < bi)) best = g, bi = row;
+                }
+            }
+        }
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            const float ov = __shfl_xor(best, o);
+            const int oi = __shfl_xor(bi, o);
+            if (ov > best || (ov == best && oi < bi)) best = ov, bi = oi;
+        }
+        if (lane == 0) {
+            float *o = bb.smp + ((size_t)t * gridDim.x + blockIdx.x) * 2;
+            o[0] = best;
+            o[1] = __int_as_float(bi);
+        }
+    }
+}
+
 // One workgroup per stream b: the lm_head partials -> the sampled token (k_sample's
 // selection rule), the token ring, end-token flag, the next embedding into pb.x[b], and the
 // state advance. A stream whose step budget (cfg.max_steps) is spent, or that sampled an end
@@ -1525,6 +1571,19 @@ void launch_batch_step(const LlmDims &d, const LayerW *layers, int n_layer, _Flo
     launch_layers(d, layers, n_layer, kcache, vcache, pb, B, d.max_splits, true, s);
     launch_quant(d, 0, pb.x, d.n_embd, out_norm, akind(lm.type), pb, B, s);
     const int nblk = matvec_grid(d, d.n_vocab);  // the batched lm_head keeps one workgroup per CU
+    // the logits on the int8 matrix cores (launch_mmq, the dot engine's values bit for bit),
+    // then the sampling partials from them (k_bt_gumbel): 8 streams 1.7B 217.0-217.5x vs
+    // 214.5-215.0x with k_bt_lm_head (dot4, partials fused), C4 179.5-179.6 vs 177.3-177.5x
+    // (profiles/r05_bt_lm_mmq_ab.txt). MIO_BT_LM_MMQ=0: k_bt_lm_head
+    static const bool lm_mmq = !(getenv("MIO_BT_LM_MMQ") && getenv("MIO_BT_LM_MMQ")[0] == '0');
+    if (lm_mmq && lm.type != 30) {
+        const MmqSeg sg{lm, mmq_tiles(lm.rows), 0};
+        launch_mmq(&sg, &lm.type, 1, MMQ_STORE,
+                   MmqArgs{pb.act, act_bytes(d.n_embd), d.n_embd, B, bb.logits, lm.rows, {}}, s);
+        hipLaunchKernelGGL(k_bt_gumbel, dim3(nblk), dim3(MT), 0, s, lm.rows, bb, B);
+        hipLaunchKernelGGL(k_bt_sample, dim3(B), dim3(ST), 0, s, d, tok_embd, nblk, pb, bb);
+        return;
+    }
     dispatch_nt<true>(d.n_embd, lm.type, [&]<int NP, int T>() {
         allow_lds(k_bt_lm_head<NP, T>);
         hipLaunchKernelGGL((k_bt_lm_head<NP, T>), dim3(nblk), dim3(MT), batch_lm_head_lds(d, B, T), s, d, out_norm, lm,
