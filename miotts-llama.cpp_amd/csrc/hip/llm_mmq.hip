@@ -544,30 +544,39 @@ __device__ __forceinline__ v4f sb16_q4k(const uint8_t *qrow, const uint8_t *hrow
 // load per lane each; after the swaps every lane holds 8 values l in {0-7, 16-23, 8-15, 24-31}
 // of its group g, so sub-block 8 n + 2 g4 lies in groups 0, 2 and the next one in groups 1, 3:
 // two 16x16x32 MFMAs per q-group, each on one sub-block's lanes (the others zero).
-__device__ __forceinline__ v4f sb16_q6k(const QMat &W, int row, int s, const int8_t *aq, const float *da_lds) {
+// the weight loads of superblock s of `row` (sb16_q6k's), kept apart so a tile loop can hold
+// the next tile's in flight (k_mmq16_loop_q6)
+struct Q6Pass {
+    uint4 scr;
+    v4i ql[2], qh;
+    uint16_t d;
+};
+__device__ __forceinline__ void q6p_load(const QMat &W, int row, int s, Q6Pass &p) {
     const int lane = threadIdx.x & 63, g = lane >> 4;
-    const bool first = (g & 1) == 0;  // groups 0, 2: the q-group's first sub-block
     const int nsb = W.k >> 8;
     const uint8_t *qlrow = W.p0 + (size_t)row * (W.k / 2);
     const uint8_t *qhrow = W.p1 + (size_t)row * (W.k / 4);
     const int8_t *screw = (const int8_t *)W.p2 + (size_t)row * (W.k / 16);
     const uint16_t *drow = (const uint16_t *)W.p3 + (size_t)row * nsb;
     // split-layout scales: pair p2 = 4n + r -> {scales[8n + r], scales[8n + r + 4]}
-    const uint4 scr = *reinterpret_cast<const uint4 *>(screw + (size_t)s * 16);
+    p.scr = *reinterpret_cast<const uint4 *>(screw + (size_t)s * 16);
+#pragma unroll
+    for (int n = 0; n < 2; ++n) p.ql[n] = *reinterpret_cast<const v4i *>(qlrow + (size_t)s * 128 + 64 * n + 16 * g);
+    p.qh = *reinterpret_cast<const v4i *>(qhrow + (size_t)s * 64 + 16 * g);
+    p.d = drow[s];
+}
+// x: the superblock's activation codes of this lane, already swap_halves'd
+__device__ __forceinline__ v4f q6p_val(Q6Pass p, const v4i (&x)[4], int s, const float *da_lds) {
+    const int lane = threadIdx.x & 63, g = lane >> 4;
+    const bool first = (g & 1) == 0;  // groups 0, 2: the q-group's first sub-block
     int8_t sc[16];
-    __builtin_memcpy(sc, &scr, 16);
-    v4i ql[2], qh, x[4];
-#pragma unroll
-    for (int n = 0; n < 2; ++n) ql[n] = *reinterpret_cast<const v4i *>(qlrow + (size_t)s * 128 + 64 * n + 16 * g);
-    qh = *reinterpret_cast<const v4i *>(qhrow + (size_t)s * 64 + 16 * g);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) x[i] = *reinterpret_cast<const v4i *>(aq + s * 256 + 64 * i + 16 * g);
-    const float dw = h2f(drow[s]);
+    __builtin_memcpy(sc, &p.scr, 16);
+    v4i (&ql)[2] = p.ql;
+    v4i &qh = p.qh;
+    const float dw = h2f(p.d);
     swap_halves(ql[0]);
     swap_halves(ql[1]);
     swap_halves(qh);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) swap_halves(x[i]);
     v4i isum = {};
 #pragma unroll
     for (int n = 0; n < 2; ++n) {
@@ -603,6 +612,18 @@ __device__ __forceinline__ v4f sb16_q6k(const QMat &W, int row, int s, const int
         v[i] = d * (float)isum[i];
     }
     return v;
+}
+
+__device__ __forceinline__ v4f sb16_q6k(const QMat &W, int row, int s, const int8_t *aq, const float *da_lds) {
+    const int g = (threadIdx.x & 63) >> 4;
+    Q6Pass p;
+    q6p_load(W, row, s, p);
+    v4i x[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) x[i] = *reinterpret_cast<const v4i *>(aq + s * 256 + 64 * i + 16 * g);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) swap_halves(x[i]);
+    return q6p_val(p, x, s, da_lds);
 }
 
 template <int T>
@@ -1013,6 +1034,68 @@ __global__ __launch_bounds__(MMQ_NT) void k_mmq16_loop(MmqSeg s0, MmqArgs a, Mmq
         if (!step(wB, uB, wA, uA)) break;
     }
 }
+
+// Q6_K, K <= 2048 (one superblock per wave), one matrix: k_mmq16_loop's walk for the K-quant
+// the batched lm_head uses (10296 16-row tiles of 164736 rows): the activation codes (this
+// wave's superblock k of every tile) and their scales are loaded once per workgroup, and the
+// next tile's weights (q6p_load) are in flight while the current one is reduced. Per tile the
+// arithmetic is k_mmq16's slot16_kq (q6p_val, the 0 + v pass sum, slot16_sum, the same
+// epilogue): bit-identical.
+template <int MODE>
+__global__ __launch_bounds__(MMQ_NT) void k_mmq16_loop_q6(MmqSeg s0, MmqArgs a, int n_tiles) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    static_assert(MODE != MMQ_SWIGLU, "one matrix");
+    float *red = reinterpret_cast<float *>(lds);  // [8 waves][64][4]
+    float *da = red + MMQ_NT * 4;                // [superblocks][16 tokens]
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
+    const int k = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int G = (int)gridDim.x;
+    int tile = (int)blockIdx.x;
+    if (tile >= n_tiles) return;
+    const bool live = k < (a.K >> 8);  // wave-uniform: this wave's superblock exists
+    const int sb = live ? k : 0;
+    auto row_of = [&](int ti) { return min(ti * RT16 + (lane & 15), s0.w.rows - 1); };
+    Q6Pass pA, pB;
+    q6p_load(s0.w, row_of(tile), sb, pA);
+    const int8_t *aq = stage_act16<14>(a, 0, a.K, da);
+    v4i x[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) x[i] = *reinterpret_cast<const v4i *>(aq + sb * 256 + 64 * i + 16 * g);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) swap_halves(x[i]);
+    auto step = [&](Q6Pass &cur, Q6Pass &nxt) -> bool {
+        const int next = tile + G < n_tiles ? tile + G : tile;
+        q6p_load(s0.w, row_of(next), sb, nxt);
+        v4f acc = {};
+        v4f v = {};
+        if (live) v = q6p_val(cur, x, sb, da);
+        acc = acc + v;
+        slot16_store(acc, red);
+        __syncthreads();
+        if (wave == 0) {
+            const v4f y = slot16_sum(red);
+            const int orow = tile * RT16 + (lane & 15);
+            if (orow < s0.w.rows) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int t = tok16(lane, i);
+                    if (t >= a.nt) continue;
+                    float *o = a.out + (size_t)t * a.ld + s0.out_off + orow;
+                    if constexpr (MODE == MMQ_STORE) *o = y[i];
+                    else *o = y[i] + *o;
+                }
+            }
+        }
+        __syncthreads();  // red is rewritten by the next tile
+        if (next == tile) return false;
+        tile = next;
+        return true;
+    };
+    for (;;) {
+        if (!step(pA, pB)) break;
+        if (!step(pB, pA)) break;
+    }
+}
 }  // namespace
 
 size_t mmq_lds(int type, int K, int mode) {
@@ -1078,6 +1161,16 @@ void launch_mmq(const MmqSeg *seg, const int *types, int nseg, int mode, const M
         if (t16) {
             const bool q8 = A == 8 && (B < 0 || B == 8) && (C < 0 || C == 8) && a.K % 256 == 0;
             const int kp = q8 ? (a.K <= 2048 ? 1 : 2) : 0;
+            if constexpr (A == 14 && B < 0) {
+                // MIO_MMQ_LOOP_Q6=0: one workgroup per tile (A/B)
+                static const bool q6_loop = !(getenv("MIO_MMQ_LOOP_Q6") && getenv("MIO_MMQ_LOOP_Q6")[0] == '0');
+                if (mode != MMQ_SWIGLU && a.K % 256 == 0 && a.K <= 2048 && tiles > n_cu() && mmq_loop_on() && q6_loop) {
+                    auto kern = mode == MMQ_STORE ? k_mmq16_loop_q6<MMQ_STORE> : k_mmq16_loop_q6<MMQ_RESID>;
+                    if (lds > 64 * 1024) allow_lds_mmq(reinterpret_cast<const void *>(kern));
+                    hipLaunchKernelGGL(kern, dim3(n_cu()), dim3(MMQ_NT), lds, s, sg[0], a, tiles);
+                    return;
+                }
+            }
             if constexpr (A == 8 && B < 0) {
                 if (kp == 1 && tiles > n_cu() && mmq_loop_on()) {
                     auto kl = [&](auto kern) {
