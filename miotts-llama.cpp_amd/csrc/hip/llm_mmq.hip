@@ -492,19 +492,23 @@ __device__ __forceinline__ long hi8(const v4i &x) { return (long)(uint32_t)x.z |
 // in the Q8_0 pair path (swap_halves): the 32-B nibble runs of sub-block pairs c, c + 1 are
 // one 16-B load per lane, the 64 activation bytes of sub-blocks 2c, 2c + 1 another; after the
 // swaps the low / high halves hold one run / one sub-block each in the same K order.
-__device__ __forceinline__ v4f sb16_q4k(const uint8_t *qrow, const uint8_t *hrow, int s, const int8_t *aq,
-                                        const float *da_lds) {
-    const int lane = threadIdx.x & 63, g = lane >> 4;
-    const uint4 hd = *reinterpret_cast<const uint4 *>(hrow + (size_t)s * 16);
-    v4i w[2], x[4];
+struct Q4Pass {
+    uint4 hd;
+    v4i w[2];
+};
+__device__ __forceinline__ void q4p_load(const uint8_t *qrow, const uint8_t *hrow, int s, Q4Pass &p) {
+    const int g = (threadIdx.x & 63) >> 4;
+    p.hd = *reinterpret_cast<const uint4 *>(hrow + (size_t)s * 16);
 #pragma unroll
-    for (int i = 0; i < 2; ++i) w[i] = *reinterpret_cast<const v4i *>(qrow + (size_t)s * 128 + 64 * i + 16 * g);
-#pragma unroll
-    for (int c = 0; c < 4; ++c) x[c] = *reinterpret_cast<const v4i *>(aq + s * 256 + 64 * c + 16 * g);
+    for (int i = 0; i < 2; ++i) p.w[i] = *reinterpret_cast<const v4i *>(qrow + (size_t)s * 128 + 64 * i + 16 * g);
+}
+// x: the superblock's activation codes of this lane, already swap_halves'd
+__device__ __forceinline__ v4f q4p_val(Q4Pass p, const v4i (&x)[4], int s, const float *da_lds) {
+    const int lane = threadIdx.x & 63;
+    const uint4 hd = p.hd;
+    v4i (&w)[2] = p.w;
 #pragma unroll
     for (int i = 0; i < 2; ++i) swap_halves(w[i]);
-#pragma unroll
-    for (int c = 0; c < 4; ++c) swap_halves(x[c]);
     v4i isum = {}, imin = {};
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
@@ -534,6 +538,22 @@ __device__ __forceinline__ v4f sb16_q4k(const uint8_t *qrow, const uint8_t *hrow
         v[i] = xx;
     }
     return v;
+}
+// this lane's activation codes of superblock s, swap_halves'd
+__device__ __forceinline__ void kq_act(const int8_t *aq, int s, v4i (&x)[4]) {
+    const int g = (threadIdx.x & 63) >> 4;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) x[c] = *reinterpret_cast<const v4i *>(aq + s * 256 + 64 * c + 16 * g);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) swap_halves(x[c]);
+}
+__device__ __forceinline__ v4f sb16_q4k(const uint8_t *qrow, const uint8_t *hrow, int s, const int8_t *aq,
+                                        const float *da_lds) {
+    Q4Pass p;
+    q4p_load(qrow, hrow, s, p);
+    v4i x[4];
+    kq_act(aq, s, x);
+    return q4p_val(p, x, s, da_lds);
 }
 
 // Q6_K superblock s: v = d * sum_j sc_j * dot_j over its 16 sub-blocks of 16 (ggml
@@ -615,14 +635,10 @@ __device__ __forceinline__ v4f q6p_val(Q6Pass p, const v4i (&x)[4], int s, const
 }
 
 __device__ __forceinline__ v4f sb16_q6k(const QMat &W, int row, int s, const int8_t *aq, const float *da_lds) {
-    const int g = (threadIdx.x & 63) >> 4;
     Q6Pass p;
     q6p_load(W, row, s, p);
     v4i x[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) x[i] = *reinterpret_cast<const v4i *>(aq + s * 256 + 64 * i + 16 * g);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) swap_halves(x[i]);
+    kq_act(aq, s, x);
     return q6p_val(p, x, s, da_lds);
 }
 
