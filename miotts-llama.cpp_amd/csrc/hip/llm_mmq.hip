@@ -30,6 +30,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <mutex>
+#include <type_traits>
 #include <utility>
 #include <vector>
 
@@ -1051,45 +1052,83 @@ __global__ __launch_bounds__(MMQ_NT) void k_mmq16_loop(MmqSeg s0, MmqArgs a, Mmq
     }
 }
 
-// Q6_K, K <= 2048 (one superblock per wave), one matrix: k_mmq16_loop's walk for the K-quant
-// the batched lm_head uses (10296 16-row tiles of 164736 rows): the activation codes (this
-// wave's superblock k of every tile) and their scales are loaded once per workgroup, and the
-// next tile's weights (q6p_load) are in flight while the current one is reduced. Per tile the
-// arithmetic is k_mmq16's slot16_kq (q6p_val, the 0 + v pass sum, slot16_sum, the same
-// epilogue): bit-identical.
-template <int MODE>
-__global__ __launch_bounds__(MMQ_NT) void k_mmq16_loop_q6(MmqSeg s0, MmqArgs a, int n_tiles) {
+// K-quants (T 12 = Q4_K, 14 = Q6_K), K <= 2048 (one superblock per wave): k_mmq16_loop's walk
+// (the batched lm_head: 10296 16-row Q6_K tiles; the 1.7B gate|up: 384 Q4_K tile pairs). The
+// activation codes (this wave's superblock k of every tile) and their scales are loaded once
+// per workgroup, the next tile's weights (q4p_load / q6p_load) are in flight while the current
+// one is reduced. Per tile the arithmetic is k_mmq16's slot16_kq (the 0 + v pass sum,
+// slot16_sum, the same epilogue): bit-identical. QNP > 0: the first a.nt workgroups are the
+// in-launch quantization producers (as k_mmq16_loop).
+template <int T>
+using KqPass = std::conditional_t<T == 12, Q4Pass, Q6Pass>;
+template <int T>
+__device__ __forceinline__ void kqp_load(const QMat &W, int row, int s, KqPass<T> &p) {
+    if constexpr (T == 12)
+        q4p_load(W.p0 + (size_t)row * (W.k / 2), W.p1 + (size_t)row * (W.k >> 8) * 16, s, p);
+    else
+        q6p_load(W, row, s, p);
+}
+template <int T>
+__device__ __forceinline__ v4f kqp_val(const KqPass<T> &p, const v4i (&x)[4], int s, const float *da) {
+    if constexpr (T == 12)
+        return q4p_val(p, x, s, da);
+    else
+        return q6p_val(p, x, s, da);
+}
+
+template <int T, int MODE, int QNP, int QM>
+__global__ __launch_bounds__(MMQ_NT) void k_mmq16_loop_kq(MmqSeg s0, MmqArgs a, MmqQuant q, int n_tiles) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
-    static_assert(MODE != MMQ_SWIGLU, "one matrix");
-    float *red = reinterpret_cast<float *>(lds);  // [8 waves][64][4]
-    float *da = red + MMQ_NT * 4;                // [superblocks][16 tokens]
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
+    constexpr int NV = MODE == MMQ_SWIGLU ? 2 : 1;
+    constexpr bool QF = QNP > 0;
+    const int nq = QF ? a.nt : 0;
+    if constexpr (QF) {
+        if ((int)blockIdx.x < nq) {
+            mmq_quant_producer<1, QNP, QM>(a, q, lds);
+            return;
+        }
+    }
+    float *red = reinterpret_cast<float *>(lds);  // [NV][8 waves][64][4]
+    float *da = red + NV * MMQ_NT * 4;           // [superblocks][16 tokens]
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int k = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int G = (int)gridDim.x;
-    int tile = (int)blockIdx.x;
+    const int G = (int)gridDim.x - nq;
+    int tile = (int)blockIdx.x - nq;
     if (tile >= n_tiles) return;
     const bool live = k < (a.K >> 8);  // wave-uniform: this wave's superblock exists
     const int sb = live ? k : 0;
     auto row_of = [&](int ti) { return min(ti * RT16 + (lane & 15), s0.w.rows - 1); };
-    Q6Pass pA, pB;
-    q6p_load(s0.w, row_of(tile), sb, pA);
-    const int8_t *aq = stage_act16<14>(a, 0, a.K, da);
+    KqPass<T> wA, uA, wB, uB;
+    kqp_load<T>(s0.w, row_of(tile), sb, wA);
+    if constexpr (NV == 2) kqp_load<T>(a.w_up, row_of(tile), sb, uA);
+    if constexpr (QF) {
+        if (threadIdx.x == 0) wait_count(q.cnt + 64 * (blockIdx.x & 7), a.nt, q.flag);
+        asm volatile("s_barrier" ::: "memory");
+    }
+    const int8_t *aq = stage_act16<T>(a, 0, a.K, da);
     v4i x[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) x[i] = *reinterpret_cast<const v4i *>(aq + sb * 256 + 64 * i + 16 * g);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) swap_halves(x[i]);
-    auto step = [&](Q6Pass &cur, Q6Pass &nxt) -> bool {
+    kq_act(aq, sb, x);
+    auto step = [&](KqPass<T> &cw, KqPass<T> &cu, KqPass<T> &nw, KqPass<T> &nu) -> bool {
         const int next = tile + G < n_tiles ? tile + G : tile;
-        q6p_load(s0.w, row_of(next), sb, nxt);
-        v4f acc = {};
-        v4f v = {};
-        if (live) v = q6p_val(cur, x, sb, da);
-        acc = acc + v;
-        slot16_store(acc, red);
+        kqp_load<T>(s0.w, row_of(next), sb, nw);
+        if constexpr (NV == 2) kqp_load<T>(a.w_up, row_of(next), sb, nu);
+        {
+            v4f acc = {}, v = {};
+            if (live) v = kqp_val<T>(cw, x, sb, da);
+            acc = acc + v;
+            slot16_store(acc, red);
+        }
+        if constexpr (NV == 2) {
+            v4f acc = {}, v = {};
+            if (live) v = kqp_val<T>(cu, x, sb, da);
+            acc = acc + v;
+            slot16_store(acc, red + MMQ_NT * 4);
+        }
         __syncthreads();
         if (wave == 0) {
             const v4f y = slot16_sum(red);
+            v4f u = {};
+            if constexpr (NV == 2) u = slot16_sum(red + MMQ_NT * 4);
             const int orow = tile * RT16 + (lane & 15);
             if (orow < s0.w.rows) {
 #pragma unroll
@@ -1098,7 +1137,8 @@ __global__ __launch_bounds__(MMQ_NT) void k_mmq16_loop_q6(MmqSeg s0, MmqArgs a, 
                     if (t >= a.nt) continue;
                     float *o = a.out + (size_t)t * a.ld + s0.out_off + orow;
                     if constexpr (MODE == MMQ_STORE) *o = y[i];
-                    else *o = y[i] + *o;
+                    else if constexpr (MODE == MMQ_RESID) *o = y[i] + *o;
+                    else *o = silu_f(y[i]) * u[i];
                 }
             }
         }
@@ -1108,8 +1148,8 @@ __global__ __launch_bounds__(MMQ_NT) void k_mmq16_loop_q6(MmqSeg s0, MmqArgs a, 
         return true;
     };
     for (;;) {
-        if (!step(pA, pB)) break;
-        if (!step(pB, pA)) break;
+        if (!step(wA, uA, wB, uB)) break;
+        if (!step(wB, uB, wA, uA)) break;
     }
 }
 }  // namespace
@@ -1153,6 +1193,14 @@ static bool mmq_loop_on() {
     return on;
 }
 
+// MIO_MMQ_LOOP_KQ (bits, default 3): K-quant (Q4_K / Q6_K, K <= 2048) matmuls of more 16-row
+// tiles than CUs walk their tiles in k_mmq16_loop_kq: bit 0 without in-launch quantization
+// (the batched lm_head), bit 1 with it (the batched gate|up)
+static int kq_loop_mask() {
+    static const int m = getenv("MIO_MMQ_LOOP_KQ") ? atoi(getenv("MIO_MMQ_LOOP_KQ")) : 3;
+    return m;
+}
+
 bool mmq16_on(int nt) {
     static const bool on = !(getenv("MIO_MMQ16") && getenv("MIO_MMQ16")[0] == '0');
     return on && nt <= TT16;
@@ -1177,13 +1225,15 @@ void launch_mmq(const MmqSeg *seg, const int *types, int nseg, int mode, const M
         if (t16) {
             const bool q8 = A == 8 && (B < 0 || B == 8) && (C < 0 || C == 8) && a.K % 256 == 0;
             const int kp = q8 ? (a.K <= 2048 ? 1 : 2) : 0;
-            if constexpr (A == 14 && B < 0) {
-                // MIO_MMQ_LOOP_Q6=0: one workgroup per tile (A/B)
-                static const bool q6_loop = !(getenv("MIO_MMQ_LOOP_Q6") && getenv("MIO_MMQ_LOOP_Q6")[0] == '0');
-                if (mode != MMQ_SWIGLU && a.K % 256 == 0 && a.K <= 2048 && tiles > n_cu() && mmq_loop_on() && q6_loop) {
-                    auto kern = mode == MMQ_STORE ? k_mmq16_loop_q6<MMQ_STORE> : k_mmq16_loop_q6<MMQ_RESID>;
-                    if (lds > 64 * 1024) allow_lds_mmq(reinterpret_cast<const void *>(kern));
-                    hipLaunchKernelGGL(kern, dim3(n_cu()), dim3(MMQ_NT), lds, s, sg[0], a, tiles);
+            if constexpr ((A == 12 || A == 14) && B < 0) {
+                if (a.K % 256 == 0 && a.K <= 2048 && tiles > n_cu() && mmq_loop_on() && (kq_loop_mask() & 1)) {
+                    auto kl = [&](auto kern) {
+                        if (lds > 64 * 1024) allow_lds_mmq(reinterpret_cast<const void *>(kern));
+                        hipLaunchKernelGGL(kern, dim3(n_cu()), dim3(MMQ_NT), lds, s, sg[0], a, MmqQuant{}, tiles);
+                    };
+                    if (mode == MMQ_STORE) kl(k_mmq16_loop_kq<A, MMQ_STORE, 0, 0>);
+                    else if (mode == MMQ_RESID) kl(k_mmq16_loop_kq<A, MMQ_RESID, 0, 0>);
+                    else kl(k_mmq16_loop_kq<A, MMQ_SWIGLU, 0, 0>);
                     return;
                 }
             }
@@ -1263,7 +1313,16 @@ bool launch_mmq_q(const MmqSeg *seg, const int *types, int nseg, int mode, const
         a.K % 256 == 0 && a.K <= 2048)
         return go(k_mmq16<8, 8, 8, MMQ_STORE, 1, 1, 0>);
     if (mode == MMQ_SWIGLU && nseg == 1 && q.mode == 0 && np == 1) {
-        if (types[0] == 12) return go(k_mmq16<12, -1, -1, MMQ_SWIGLU, 0, 1, 0>);
+        if (types[0] == 12) {
+            const int nl = n_cu() - a.nt;  // the producers keep CUs of their own
+            if (a.K % 256 == 0 && a.K <= 2048 && tiles > nl && nl > 0 && mmq_loop_on() && (kq_loop_mask() & 2)) {
+                auto kern = k_mmq16_loop_kq<12, MMQ_SWIGLU, 1, 0>;
+                if (lds > 64 * 1024) allow_lds_mmq(reinterpret_cast<const void *>(kern));
+                hipLaunchKernelGGL(kern, dim3(a.nt + nl), dim3(MMQ_NT), lds, s, sg[0], a, q, tiles);
+                return true;
+            }
+            return go(k_mmq16<12, -1, -1, MMQ_SWIGLU, 0, 1, 0>);
+        }
         if (types[0] == 8 && a.K % 256 == 0 && a.K <= 2048) {
             const int nl = n_cu() - a.nt;  // the producers keep CUs of their own
             if (tiles > nl && nl > 0 && mmq_loop_on()) {
