@@ -41,6 +41,7 @@ struct MmqQuant {
     int *cnt;
     int *other;
     int *flag;
+    int early = 0;  // set by launch_mmq_q: K-quant tiles issue their weight loads before the wait
 };
 
 int mmq_tiles(int rows);

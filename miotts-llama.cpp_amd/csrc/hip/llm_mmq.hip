@@ -26,6 +26,7 @@
 // tools/micro/mfma_i8_probe.hip).
 #include "llm_device.h"
 #include "llm_mmq.h"
+#include "llm_quant_producer.h"
 
 #include <algorithm>
 #include <cstdlib>
@@ -867,6 +868,23 @@ __device__ __forceinline__ void mmq_quant_producer(const MmqArgs &a, const MmqQu
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+template <int T>
+using KqPass = std::conditional_t<T == 12, Q4Pass, Q6Pass>;
+template <int T>
+__device__ __forceinline__ void kqp_load(const QMat &W, int row, int s, KqPass<T> &p) {
+    if constexpr (T == 12)
+        q4p_load(W.p0 + (size_t)row * (W.k / 2), W.p1 + (size_t)row * (W.k >> 8) * 16, s, p);
+    else
+        q6p_load(W, row, s, p);
+}
+template <int T>
+__device__ __forceinline__ v4f kqp_val(const KqPass<T> &p, const v4i (&x)[4], int s, const float *da) {
+    if constexpr (T == 12)
+        return q4p_val(p, x, s, da);
+    else
+        return q6p_val(p, x, s, da);
+}
+
 // QNP > 0 (k_mmq16q): the first a.nt workgroups are quantization producers (MmqQuant, XRegs
 // of QNP passes, QM = its mode), the tiles follow and wait before their activation reads.
 template <int T0, int T1, int T2, int MODE, int KP = 0, int QNP = 0, int QM = 0>
@@ -874,9 +892,19 @@ __global__ __launch_bounds__(MMQ_NT) void k_mmq16(MmqSeg s0, MmqSeg s1, MmqSeg s
     extern __shared__ __attribute__((aligned(16))) char lds[];
     constexpr int NV = MODE == MMQ_SWIGLU ? 2 : 1;
     constexpr bool QF = QNP > 0;
+    // plain rows (QM 1, the down's h) are quantized by one producer per (token, 2048-element
+    // chunk) (chunk_quant_producer); RMSNorm rows by one per token
+    // (q.mode 2 = plain rows one producer per token: MIO_BT_QCHUNK=0, A/B)
+    static_assert(QM != 1 || MMQ_NT == 512, "chunk_quant_producer covers 2048 elements with 512 threads");
+    const bool chunked = QM == 1 && q.mode == 1;
+    const int nq = !QF ? 0 : (chunked ? a.nt * ((a.K + 2047) / 2048) : a.nt);
     if constexpr (QF) {
-        if ((int)blockIdx.x < a.nt) {
-            mmq_quant_producer<T0 == 8 ? 0 : 1, QNP, QM>(a, q, lds);
+        if ((int)blockIdx.x < nq) {
+            if (chunked)
+                chunk_quant_producer(q.src, a.K, T0 != 8, (a.K + 2047) / 2048, const_cast<char *>(a.act), q.cnt,
+                                     q.other, lds);
+            else
+                mmq_quant_producer<T0 == 8 ? 0 : 1, QNP, QM>(a, q, lds);
             return;
         }
     }
@@ -884,11 +912,11 @@ __global__ __launch_bounds__(MMQ_NT) void k_mmq16(MmqSeg s0, MmqSeg s1, MmqSeg s
     float *da = red + NV * MMQ_NT * 4;           // [groups][16 tokens]
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int t0 = blockIdx.y * TT16;
-    int tile_id = (int)blockIdx.x - (QF ? a.nt : 0);
+    int tile_id = (int)blockIdx.x - nq;
     // the producers' records are complete: one lane waits, the barrier releases the others
     auto wait_act = [&]() {
         if constexpr (QF) {
-            if (threadIdx.x == 0) wait_count(q.cnt + 64 * (blockIdx.x & 7), a.nt, q.flag);
+            if (threadIdx.x == 0) wait_count(q.cnt + 64 * (blockIdx.x & 7), nq, q.flag);
             asm volatile("s_barrier" ::: "memory");
         }
     };
@@ -930,11 +958,39 @@ __global__ __launch_bounds__(MMQ_NT) void k_mmq16(MmqSeg s0, MmqSeg s1, MmqSeg s
             slot16_store(y, red);
             if constexpr (NV == 2) slot16_store(u, red + MMQ_NT * 4);
         } else {
+            if constexpr (QF && NV == 1 && (T == 12 || T == 14)) {
+                // in-launch quantization: up to three passes' weights (K <= 6144, the 1.7B down)
+                // are in flight while the producers quantize; then slot16_kq's arithmetic
+                const int nsb = sg.w.k >> 8, np = (nsb + 7) / 8;
+                if (q.early && np <= 3) {
+                    KqPass<T> ps[3];
+#pragma unroll
+                    for (int p = 0; p < 3; ++p)
+                        if (p < np) kqp_load<T>(sg.w, row, min(p * 8 + k, nsb - 1), ps[p]);
+                    wait_act();
+                    const int8_t *aq = stage_act16<T>(a, t0, a.K, da);
+                    v4f acc = {};
+#pragma unroll
+                    for (int p = 0; p < 3; ++p) {
+                        if (p < np) {
+                            const int s = p * 8 + k;
+                            v4i x[4];
+                            kq_act(aq, min(s, nsb - 1), x);
+                            v4f v = {};
+                            if (s < nsb) v = kqp_val<T>(ps[p], x, s, da);
+                            acc = acc + v;  // the decode lane's pass accumulation (0 + v0 + v1 ...)
+                        }
+                    }
+                    slot16_store(acc, red);
+                    goto reduce;
+                }
+            }
             wait_act();
             const int8_t *aq = stage_act16<T>(a, t0, a.K, da);
             slot16_store(slot16_val<T>(sg.w, row, k, aq, da), red);
             if constexpr (NV == 2) slot16_store(slot16_val<T>(a.w_up, row, k, aq, da), red + MMQ_NT * 4);
         }
+    reduce:
         __syncthreads();
         if (wave != 0) return;
         const v4f y = slot16_sum(red);
@@ -1059,23 +1115,6 @@ __global__ __launch_bounds__(MMQ_NT) void k_mmq16_loop(MmqSeg s0, MmqArgs a, Mmq
 // one is reduced. Per tile the arithmetic is k_mmq16's slot16_kq (the 0 + v pass sum,
 // slot16_sum, the same epilogue): bit-identical. QNP > 0: the first a.nt workgroups are the
 // in-launch quantization producers (as k_mmq16_loop).
-template <int T>
-using KqPass = std::conditional_t<T == 12, Q4Pass, Q6Pass>;
-template <int T>
-__device__ __forceinline__ void kqp_load(const QMat &W, int row, int s, KqPass<T> &p) {
-    if constexpr (T == 12)
-        q4p_load(W.p0 + (size_t)row * (W.k / 2), W.p1 + (size_t)row * (W.k >> 8) * 16, s, p);
-    else
-        q6p_load(W, row, s, p);
-}
-template <int T>
-__device__ __forceinline__ v4f kqp_val(const KqPass<T> &p, const v4i (&x)[4], int s, const float *da) {
-    if constexpr (T == 12)
-        return q4p_val(p, x, s, da);
-    else
-        return q6p_val(p, x, s, da);
-}
-
 template <int T, int MODE, int QNP, int QM>
 __global__ __launch_bounds__(MMQ_NT) void k_mmq16_loop_kq(MmqSeg s0, MmqArgs a, MmqQuant q, int n_tiles) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -1297,10 +1336,18 @@ bool launch_mmq_q(const MmqSeg *seg, const int *types, int nseg, int mode, const
                                 (size_t)(types[i] == 8 ? a.K / 32 : a.K / 256) * TT16 * sizeof(float));
     }
     lds = std::max(lds, act_bytes(a.K) + smem_bytes(a.K));  // the producers' record + scratch
-    const dim3 grid(a.nt + tiles);
+    // k_mmq16's producer count: per (token, 2048-element chunk) for plain rows (q.mode 1)
+    static const bool qchunk = !(getenv("MIO_BT_QCHUNK") && getenv("MIO_BT_QCHUNK")[0] == '0');
+    MmqQuant qq = q;
+    if (q.mode == 1 && !qchunk) qq.mode = 2;
+    // MIO_KQ_EARLY=0: K-quant tiles issue their weight loads after the producers' wait (A/B)
+    static const bool early = !(getenv("MIO_KQ_EARLY") && getenv("MIO_KQ_EARLY")[0] == '0');
+    qq.early = early ? 1 : 0;
+    const int nq = qq.mode == 1 ? a.nt * ((a.K + 2047) / 2048) : a.nt;
+    const dim3 grid(nq + tiles);
     auto go = [&](auto kern) {
         if (lds > 64 * 1024) allow_lds_mmq(reinterpret_cast<const void *>(kern));
-        hipLaunchKernelGGL(kern, grid, dim3(MMQ_NT), lds, s, sg[0], sg[1], sg[2], a, q);
+        hipLaunchKernelGGL(kern, grid, dim3(MMQ_NT), lds, s, sg[0], sg[1], sg[2], a, qq);
         return true;
     };
     const int np = pick_np(a.K);

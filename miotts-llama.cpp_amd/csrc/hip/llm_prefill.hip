@@ -22,6 +22,7 @@
 // bit (tests/test_llm_gpu.py::test_batched_prefill_matches_sequential).
 #include "llm_device.h"
 #include "llm_mmq.h"
+#include "llm_quant_producer.h"
 
 #include <mutex>
 #include <utility>
@@ -913,56 +914,13 @@ __global__ __launch_bounds__(MT) void k_pf_ffn_down(LlmDims d, QMat down, Prefil
 // lane waits for npr on its shard, then the records are copied to LDS (no workgroup of the
 // launch reads them before every producer has stored: the lines come from past the L2s).
 // Deadlock-free by dispatch order (producers first, they never wait).
-__device__ __forceinline__ void down_quant_producer(const float *src, int K, int kq, int nch, char *act,
-                                                    const MmqQuant &q, char *lds) {
-    const int t = blockIdx.x / nch, c = blockIdx.x - t * nch;
-    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (blockIdx.x == 0 && threadIdx.x < 8)
-        __hip_atomic_store((__attribute__((address_space(1))) int *)(q.other + 64 * threadIdx.x), 0, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    const ActL a = carve_t(lds, K, 0).a;
-    if (c * 2048 + wave * 256 < K) {  // wave-uniform
-        const float4 x = *reinterpret_cast<const float4 *>(src + (size_t)t * K + c * 2048 + 4 * (int)threadIdx.x);
-        const float v[4] = {x.x, x.y, x.z, x.w};
-        if (kq)
-            q8k_store(v, abs_max4(v), c * 8 + wave, a);
-        else
-            q80_store(v, c * 64 + wave * 8 + (lane >> 3), true, a);
-    }
-    __syncthreads();
-    // the chunk's ranges of the record: codes [2048 c, +2048), Q8_0 scales [64 c, +64) or Q8_K
-    // scales [8 c, +8) and bsums [128 c, +128); a partial last chunk copies its whole 256s only
-    const int nsb = min(8, (K - c * 2048) >> 8);
-    const int nq = nsb * 16, nd = kq ? (nsb * 4 + 15) / 16 : nsb * 2, nb = kq ? nsb * 2 : 0;
-    const auto dst = rsrc(act + (size_t)t * act_bytes(K), (uint32_t)act_bytes(K));
-    const int i = threadIdx.x;
-    uint32_t off = 0xFFFFFFFFu;
-    if (i < nq)
-        off = c * 2048 + 16 * i;
-    else if (i < nq + nd)
-        off = K + (kq ? c * 32 : c * 256) + 16 * (i - nq);
-    else if (i < nq + nd + nb)
-        off = K + (K / 32 + 8) * 4 + c * 256 + 16 * (i - nq - nd);
-    if (off != 0xFFFFFFFFu) {
-        const uint4 v = *reinterpret_cast<const uint4 *>(lds + off);
-        u32x4 u;
-        u.x = v.x, u.y = v.y, u.z = v.z, u.w = v.w;
-        __builtin_amdgcn_raw_buffer_store_b128(u, dst, off, 0, 16);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x < 8)
-        __hip_atomic_fetch_add((__attribute__((address_space(1))) int *)(q.cnt + 64 * threadIdx.x), 1,
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 template <int NP, int T>
 __global__ __launch_bounds__(MT) void k_pf_ffn_down_q(LlmDims d, QMat down, PrefillBuffers pb, int nt, int rpw,
                                                       MmqQuant q, int nch) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int K = down.k, E = d.n_embd, KR = rec_k(K, T), npr = nt * nch;
     if ((int)blockIdx.x < npr) {
-        down_quant_producer(q.src, K, T != 8, nch, pb.act, q, smem);
+        chunk_quant_producer(q.src, K, T != 8, nch, pb.act, q.cnt, q.other, smem);
         return;
     }
     int lo, hi;
