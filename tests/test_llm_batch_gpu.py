@@ -134,3 +134,50 @@ def test_batch_c4_2p6b_q8_b8(device, synth_llm_path):
         ref = g.generate(prompts[b], 48, 0.8, seeds[b], allow=ALLOW)
         assert np.array_equal(got[b], ref), b
     g.close()
+
+
+_ENGINE_SCRIPT = r"""
+import hashlib, sys
+import numpy as np
+sys.path.insert(0, sys.argv[2])
+import miotts_amd as m
+dev = m.Device(0)
+g = m.Llm(dev, sys.argv[1], 512)
+rng = np.random.default_rng(7)
+prompts = [list(rng.integers(0, 256, int(n))) for n in (5, 1, 17, 9, 30, 3, 12, 8)]
+got = g.generate_batch(prompts, 24, 0.8, [900 + b for b in range(8)],
+                       allow=(m.SYNTH_SPEECH0, m.SYNTH_SPEECH0 + 12800))
+h = hashlib.sha256()
+for t in got:
+    h.update(np.asarray(t, np.int32).tobytes())
+print(h.hexdigest())
+"""
+
+
+@pytest.mark.parametrize("preset,variants", [
+    (3, [{"MIO_BT_LM_MMQ": "0"}, {"MIO_MMQ_LOOP_KQ": "0"}, {"MIO_KQ_EARLY": "0"}, {"MIO_BT_QCHUNK": "0"}]),
+    (4, [{"MIO_BT_DQ": "0"}, {"MIO_BT_FQ": "1"}, {"MIO_BT_LM_MMQ": "0"}, {"MIO_MMQ_LOOP": "0"}]),
+])
+def test_batch_engine_switches_bit_identical(synth_llm_path, tmp_path, preset, variants):
+    """The round-5 batched-step engines run the arithmetic of the ones they replace: 8 streams x
+    24 tokens are identical with each switched back (a fresh process per variant; the switches
+    are read once). 1.7B Q4_K_M: the lm_head on the matrix cores vs k_bt_lm_head's dot4, the
+    K-quant tile loops vs one workgroup per tile, weight loads before vs after the in-launch
+    producers' wait, chunked vs per-token producers. 2.6B Q8_0: the dot4 down quantizing h in
+    its launch vs behind k_bt_quant_split, q|k|v on the matrix cores vs the dot4 in-launch path,
+    the lm_head engines, the Q8_0 tile loops."""
+    import os
+    import subprocess
+    import sys
+    path = synth_llm_path(preset)
+    script = tmp_path / "engines.py"
+    script.write_text(_ENGINE_SCRIPT)
+    pkg = os.path.dirname(os.path.dirname(m.__file__))
+    outs = []
+    for env in [{}] + variants:
+        p = subprocess.run([sys.executable, str(script), path, pkg], capture_output=True, text=True, timeout=240,
+                           env=dict(os.environ, **env))
+        assert p.returncode == 0, (env, p.stderr[-2000:])
+        outs.append((env, p.stdout.strip()))
+    print(outs)
+    assert all(o == outs[0][1] for _, o in outs), outs
