@@ -567,7 +567,7 @@ __device__ __forceinline__ v4f sb16_q4k(const uint8_t *qrow, const uint8_t *hrow
 // of its group g, so sub-block 8 n + 2 g4 lies in groups 0, 2 and the next one in groups 1, 3:
 // two 16x16x32 MFMAs per q-group, each on one sub-block's lanes (the others zero).
 // the weight loads of superblock s of `row` (sb16_q6k's), kept apart so a tile loop can hold
-// the next tile's in flight (k_mmq16_loop_q6)
+// the next tile's in flight (k_mmq16_loop_kq)
 struct Q6Pass {
     uint4 scr;
     v4i ql[2], qh;
