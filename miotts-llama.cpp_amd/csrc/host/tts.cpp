@@ -524,7 +524,10 @@ bool TestToSpeech::synthesize_batch_to_files(const VoiceModel &voice, const std:
         if (mio_hip_llm_generate_batch(I.llm, prompts.data(), lens.data(), B, max_tokens, temp, seeds.data(),
                                        sp.allow_lo, sp.allow_hi, sp.eos0, sp.eos1, 32, toks.data(),
                                        n_out.data()) != MIO_OK) {
-            // a model the batched engine does not take: one utterance at a time
+            // a model the batched engine does not take (or a failed hand-off): one utterance
+            // at a time, said on stderr so the fallback is visible
+            fprintf(stderr, "TestToSpeech: batched decode unavailable (%s); decoding one utterance at a time\n",
+                    mio_hip_last_error());
             for (int b = 0; b < B; ++b)
                 if (!synthesize_to_file(voice, texts[g0 + b], output_paths[g0 + b], options)) return false;
             continue;
