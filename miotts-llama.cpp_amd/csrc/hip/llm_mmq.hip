@@ -918,6 +918,9 @@ __global__ __launch_bounds__(MMQ_NT) void k_mmq16(MmqSeg s0, MmqSeg s1, MmqSeg s
         if constexpr (QF) {
             if (threadIdx.x == 0) wait_count(q.cnt + 64 * (blockIdx.x & 7), nq, q.flag);
             asm volatile("s_barrier" ::: "memory");
+            // agent-scope acquire: this XCD's L2 drops lines of the records cached before the
+            // producers' write-through stores (a stale act line was seen once in a few CLI runs)
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         }
     };
     auto run = [&]<int T>(const MmqSeg &sg, int ti) {
@@ -1056,6 +1059,9 @@ __global__ __launch_bounds__(MMQ_NT) void k_mmq16_loop(MmqSeg s0, MmqArgs a, Mmq
     if constexpr (QF) {
         if (threadIdx.x == 0) wait_count(q.cnt + 64 * (blockIdx.x & 7), a.nt, q.flag);
         asm volatile("s_barrier" ::: "memory");
+        // agent-scope acquire: this XCD's L2 drops lines of the records cached before the
+        // producers' write-through stores (a stale act line was seen once in a few CLI runs)
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     }
     const int8_t *aq = act16_codes(a, 0);
     v4i x[4];
@@ -1143,6 +1149,9 @@ __global__ __launch_bounds__(MMQ_NT) void k_mmq16_loop_kq(MmqSeg s0, MmqArgs a, 
     if constexpr (QF) {
         if (threadIdx.x == 0) wait_count(q.cnt + 64 * (blockIdx.x & 7), a.nt, q.flag);
         asm volatile("s_barrier" ::: "memory");
+        // agent-scope acquire: this XCD's L2 drops lines of the records cached before the
+        // producers' write-through stores (a stale act line was seen once in a few CLI runs)
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     }
     const int8_t *aq = stage_act16<T>(a, 0, a.K, da);
     v4i x[4];

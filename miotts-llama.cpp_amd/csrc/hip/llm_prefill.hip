@@ -930,6 +930,9 @@ __global__ __launch_bounds__(MT) void k_pf_ffn_down_q(LlmDims d, QMat down, Pref
     load_first_b<T, NP, 1>(down, down, lo, hi, ga, gb);
     if (threadIdx.x == 0) wait_count(q.cnt + 64 * (blockIdx.x & 7), npr, q.flag);
     asm volatile("s_barrier" ::: "memory");
+    // agent-scope acquire: this XCD's L2 drops lines of the records cached before the
+    // producers' write-through stores (a stale act line was seen once in a few CLI runs)
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     ActPre<NP> ap;
     act_issue<NP>(pb.act, KR, nt, ap);
     float *res = resid_lds(smem, KR, nt, rpw);
