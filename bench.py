@@ -48,7 +48,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 ROOF_POS = 400  # decode position of the roofline timeline / kernel timings (and of the PMC run)
 KERNEL_NAMES = {0: "k_attn_in", 1: "k_attention", 2: "k_attn_out", 3: "k_ffn_in", 4: "k_ffn_down",
                 6: "k_lm_head", 8: "k_conv_in", 9: "k_conv_out", 10: "k_att_o", 11: "k_layer_att"}
-PRESETS = {2: "MioTTS-0.1B Q8_0", 3: "MioTTS-1.7B Q4_K_M", 4: "MioTTS-2.6B Q8_0", 12: "MioTTS-1.7B BF16"}
+PRESETS = {2: "MioTTS-0.1B Q8_0", 3: "MioTTS-1.7B Q4_K_M", 4: "MioTTS-2.6B Q8_0",
+           6: "MioTTS-2.6B Q8_0 (LFM2 shape: 22 short-conv + 8 attention layers)", 12: "MioTTS-1.7B BF16"}
 PROMPT = "こんにちは、今日はいい天気ですね。"  # README.md:83, SURVEY 8(d)
 
 

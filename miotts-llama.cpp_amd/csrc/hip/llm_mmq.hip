@@ -541,15 +541,41 @@ __device__ __forceinline__ v4f q4p_val(Q4Pass p, const v4i (&x)[4], int s, const
     }
     return v;
 }
+// A lane's activation record in the launches whose own producer workgroups wrote it (in-launch
+// quantization, QNP > 0): the wave-uniform record base plus this lane's token offset, read with
+// 16-B / 4-B sc1 buffer loads (L1 bypassed). The producers store every record byte sc1, drain
+// them and add to 8 counter replicas behind a workgroup barrier; the consumer polls one replica
+// and releases its waves with a barrier: MI355X_MICROARCH's replica-counter hand-off, whose
+// loads must ALL be sc1 loads (plain loads after a relaxed poll may return a stale L1 line;
+// round 5's repair was an agent-scope acquire per workgroup, an L1 invalidate that also waited
+// for the early weight loads: 8 streams 240 -> 140x). Records an earlier launch wrote stay
+// plain pointers (the kernel boundary orders them).
+struct ActSc1 {
+    const char *base;
+    uint32_t off;
+};
+__device__ __forceinline__ v4i ld_act16(const int8_t *p, int o) { return *reinterpret_cast<const v4i *>(p + o); }
+__device__ __forceinline__ v4i ld_act16(const ActSc1 &p, int o) {
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rsrc(p.base, 0x7FFFFFF0u), p.off + (uint32_t)o, 0, 16);
+    return v4i{(int)v.x, (int)v.y, (int)v.z, (int)v.w};
+}
+__device__ __forceinline__ float ld_scale(const char *base, size_t off, bool sc1) {
+    if (sc1)
+        return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc(base, 0x7FFFFFF0u), (uint32_t)off, 0, 16));
+    return *reinterpret_cast<const float *>(base + off);
+}
+
 // this lane's activation codes of superblock s, swap_halves'd
-__device__ __forceinline__ void kq_act(const int8_t *aq, int s, v4i (&x)[4]) {
+template <class AP>
+__device__ __forceinline__ void kq_act(const AP &aq, int s, v4i (&x)[4]) {
     const int g = (threadIdx.x & 63) >> 4;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) x[c] = *reinterpret_cast<const v4i *>(aq + s * 256 + 64 * c + 16 * g);
+    for (int c = 0; c < 4; ++c) x[c] = ld_act16(aq, s * 256 + 64 * c + 16 * g);
 #pragma unroll
     for (int c = 0; c < 4; ++c) swap_halves(x[c]);
 }
-__device__ __forceinline__ v4f sb16_q4k(const uint8_t *qrow, const uint8_t *hrow, int s, const int8_t *aq,
+template <class AP>
+__device__ __forceinline__ v4f sb16_q4k(const uint8_t *qrow, const uint8_t *hrow, int s, const AP &aq,
                                         const float *da_lds) {
     Q4Pass p;
     q4p_load(qrow, hrow, s, p);
@@ -636,7 +662,8 @@ __device__ __forceinline__ v4f q6p_val(Q6Pass p, const v4i (&x)[4], int s, const
     return v;
 }
 
-__device__ __forceinline__ v4f sb16_q6k(const QMat &W, int row, int s, const int8_t *aq, const float *da_lds) {
+template <class AP>
+__device__ __forceinline__ v4f sb16_q6k(const QMat &W, int row, int s, const AP &aq, const float *da_lds) {
     Q6Pass p;
     q6p_load(W, row, s, p);
     v4i x[4];
@@ -644,8 +671,8 @@ __device__ __forceinline__ v4f sb16_q6k(const QMat &W, int row, int s, const int
     return q6p_val(p, x, s, da_lds);
 }
 
-template <int T>
-__device__ v4f slot16_kq(const QMat &W, int row, int k, const int8_t *aq, const float *da_lds) {
+template <int T, class AP>
+__device__ v4f slot16_kq(const QMat &W, int row, int k, const AP &aq, const float *da_lds) {
     const int nsb = W.k >> 8, NP = (nsb + 7) / 8;
     v4f acc = {};
     for (int p = 0; p < NP; ++p) {
@@ -720,11 +747,12 @@ __device__ __forceinline__ void q80p_load(const QMat &W, int row, int p, int k, 
     for (int i = 0; i < 4; ++i) q.w[i] = *reinterpret_cast<const v4i *>(qrow + (size_t)(b0 + 2 * i) * 32 + 16 * g);
     q.ds = *reinterpret_cast<const v4i *>((const uint16_t *)W.p1 + (size_t)row * nb + b0);
 }
-__device__ __forceinline__ void act_load(const int8_t *aq, int K, int p, int k, v4i (&a)[4]) {
+template <class AP>
+__device__ __forceinline__ void act_load(const AP &aq, int K, int p, int k, v4i (&a)[4]) {
     const int g = (threadIdx.x & 63) >> 4;
     const int b0 = min(p * 64 + 8 * k, (K >> 5) - 8);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) a[i] = *reinterpret_cast<const v4i *>(aq + (b0 + 2 * i) * 32 + 16 * g);
+    for (int i = 0; i < 4; ++i) a[i] = ld_act16(aq, (b0 + 2 * i) * 32 + 16 * g);
 }
 // the 8 slots' values of one pass added to acc (a: the pass's activations, already swapped)
 __device__ __forceinline__ void q80p_acc(Q80Pass &q, const v4i (&a)[4], int p, int k, int nb, const float *da_lds,
@@ -760,8 +788,8 @@ __device__ __forceinline__ v4f tree8(const v4f (&acc)[8]) {
     return t.result;
 }
 // NV matrices (W, then U) over the same activations, one pass at a time
-template <int NV>
-__device__ __forceinline__ void slot16_q80p(const QMat &W, const QMat &U, int row, int k, const int8_t *aq,
+template <int NV, class AP>
+__device__ __forceinline__ void slot16_q80p(const QMat &W, const QMat &U, int row, int k, const AP &aq,
                                             const float *da_lds, v4f &y, v4f &u) {
     const int nb = W.k >> 5, NP = (nb + 63) / 64;
     v4f aw[8], au[8];
@@ -782,32 +810,42 @@ __device__ __forceinline__ void slot16_q80p(const QMat &W, const QMat &U, int ro
     if constexpr (NV == 2) u = tree8(au);
 }
 
-template <int T>
-__device__ __forceinline__ v4f slot16_val(const QMat &W, int row, int k, const int8_t *aq, const float *da_lds) {
-    if constexpr (T == 8) return slot16_q80(W, row, k, aq, da_lds);
-    else return slot16_kq<T>(W, row, k, aq, da_lds);
+template <int T, class AP>
+__device__ __forceinline__ v4f slot16_val(const QMat &W, int row, int k, const AP &aq, const float *da_lds) {
+    if constexpr (T == 8) {
+        // the 8-B Q8_0 path (K % 256 != 0) never runs in an in-launch-quantization launch
+        // (launch_mmq_q takes K % 256 == 0 only)
+        if constexpr (std::is_same_v<AP, ActSc1>) return v4f{};
+        else return slot16_q80(W, row, k, aq, da_lds);
+    } else {
+        return slot16_kq<T>(W, row, k, aq, da_lds);
+    }
+}
+
+// this lane's token's codes (A operand: token lane & 15; no loads); SC: the producers of this
+// launch wrote them (ActSc1, sc1 loads)
+template <bool SC>
+__device__ __forceinline__ auto act16_codes(const MmqArgs &a, int t0) {
+    const int t = min(t0 + (threadIdx.x & 15), a.nt - 1);
+    if constexpr (SC)
+        return ActSc1{a.act, (uint32_t)((size_t)t * a.act_stride)};
+    else
+        return reinterpret_cast<const int8_t *>(a.act + (size_t)t * a.act_stride);
 }
 
 // activation scales of the tile's 16 tokens -> LDS [group][token]; returns this lane's
 // token's codes (A operand: token lane & 15)
-template <int T>
-__device__ __forceinline__ const int8_t *stage_act16(const MmqArgs &a, int t0, int K, float *da_lds) {
+template <int T, bool SC = false>
+__device__ __forceinline__ auto stage_act16(const MmqArgs &a, int t0, int K, float *da_lds) {
     const int ng = T == 8 ? K >> 5 : K >> 8;
     const size_t ab = a.act_stride;
     // token-major walk: consecutive threads read consecutive scales of one record
     for (int e = threadIdx.x; e < ng * TT16; e += MMQ_NT) {
         const int tt = e / ng, g = e - tt * ng, t = min(t0 + tt, a.nt - 1);
-        da_lds[g * TT16 + tt] = reinterpret_cast<const float *>(a.act + (size_t)t * ab + K)[g];
+        da_lds[g * TT16 + tt] = ld_scale(a.act, (size_t)t * ab + K + 4 * (size_t)g, SC);
     }
     __syncthreads();
-    const int t = min(t0 + (threadIdx.x & 15), a.nt - 1);
-    return reinterpret_cast<const int8_t *>(a.act + (size_t)t * ab);
-}
-
-// this lane's token's codes (A operand: token lane & 15; no loads)
-__device__ __forceinline__ const int8_t *act16_codes(const MmqArgs &a, int t0) {
-    const int t = min(t0 + (threadIdx.x & 15), a.nt - 1);
-    return reinterpret_cast<const int8_t *>(a.act + (size_t)t * a.act_stride);
+    return act16_codes<SC>(a, t0);
 }
 
 __device__ __forceinline__ void slot16_store(const v4f &mine, float *red) {
@@ -913,14 +951,12 @@ __global__ __launch_bounds__(MMQ_NT) void k_mmq16(MmqSeg s0, MmqSeg s1, MmqSeg s
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int t0 = blockIdx.y * TT16;
     int tile_id = (int)blockIdx.x - nq;
-    // the producers' records are complete: one lane waits, the barrier releases the others
+    // the producers' records are complete: one lane waits, the barrier releases the others; every
+    // record load after it is an sc1 load (ActSc1, stage_act16<T, QF>)
     auto wait_act = [&]() {
         if constexpr (QF) {
             if (threadIdx.x == 0) wait_count(q.cnt + 64 * (blockIdx.x & 7), nq, q.flag);
             asm volatile("s_barrier" ::: "memory");
-            // agent-scope acquire: this XCD's L2 drops lines of the records cached before the
-            // producers' write-through stores (a stale act line was seen once in a few CLI runs)
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         }
     };
     auto run = [&]<int T>(const MmqSeg &sg, int ti) {
@@ -929,7 +965,7 @@ __global__ __launch_bounds__(MMQ_NT) void k_mmq16(MmqSeg s0, MmqSeg s1, MmqSeg s
         // them with a partial EXEC)
         const int k = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
         if (T == 8 && (KP != 0 || a.K % 256 == 0)) {
-            const int8_t *aq = act16_codes(a, t0);
+            const auto aq = act16_codes<QF>(a, t0);
             v4f y = {}, u = {};
             if (KP == 1 || (KP == 0 && a.K <= 2048)) {
                 // one pass: every weight / activation / scale load goes out before the
@@ -941,7 +977,7 @@ __global__ __launch_bounds__(MMQ_NT) void k_mmq16(MmqSeg s0, MmqSeg s1, MmqSeg s
                 if constexpr (NV == 2) q80p_load(a.w_up, row, 0, k, qu);
                 wait_act();
                 act_load(aq, a.K, 0, k, x);
-                stage_act16<8>(a, t0, a.K, da);
+                stage_act16<8, QF>(a, t0, a.K, da);
 #pragma unroll
                 for (int i = 0; i < 4; ++i) swap_halves(x[i]);
                 v4f aw[8], au[8];
@@ -955,7 +991,7 @@ __global__ __launch_bounds__(MMQ_NT) void k_mmq16(MmqSeg s0, MmqSeg s1, MmqSeg s
                 }
             } else {
                 wait_act();
-                stage_act16<8>(a, t0, a.K, da);
+                stage_act16<8, QF>(a, t0, a.K, da);
                 slot16_q80p<NV>(sg.w, a.w_up, row, k, aq, da, y, u);
             }
             slot16_store(y, red);
@@ -971,7 +1007,7 @@ __global__ __launch_bounds__(MMQ_NT) void k_mmq16(MmqSeg s0, MmqSeg s1, MmqSeg s
                     for (int p = 0; p < 3; ++p)
                         if (p < np) kqp_load<T>(sg.w, row, min(p * 8 + k, nsb - 1), ps[p]);
                     wait_act();
-                    const int8_t *aq = stage_act16<T>(a, t0, a.K, da);
+                    const auto aq = stage_act16<T, QF>(a, t0, a.K, da);
                     v4f acc = {};
 #pragma unroll
                     for (int p = 0; p < 3; ++p) {
@@ -989,7 +1025,7 @@ __global__ __launch_bounds__(MMQ_NT) void k_mmq16(MmqSeg s0, MmqSeg s1, MmqSeg s
                 }
             }
             wait_act();
-            const int8_t *aq = stage_act16<T>(a, t0, a.K, da);
+            const auto aq = stage_act16<T, QF>(a, t0, a.K, da);
             slot16_store(slot16_val<T>(sg.w, row, k, aq, da), red);
             if constexpr (NV == 2) slot16_store(slot16_val<T>(a.w_up, row, k, aq, da), red + MMQ_NT * 4);
         }
@@ -1056,17 +1092,14 @@ __global__ __launch_bounds__(MMQ_NT) void k_mmq16_loop(MmqSeg s0, MmqArgs a, Mmq
     Q80Pass wA, uA, wB, uB;
     q80p_load(s0.w, row_of(tile), 0, k, wA);
     if constexpr (NV == 2) q80p_load(a.w_up, row_of(tile), 0, k, uA);
-    if constexpr (QF) {
+    if constexpr (QF) {  // the records' loads below are sc1 (ActSc1)
         if (threadIdx.x == 0) wait_count(q.cnt + 64 * (blockIdx.x & 7), a.nt, q.flag);
         asm volatile("s_barrier" ::: "memory");
-        // agent-scope acquire: this XCD's L2 drops lines of the records cached before the
-        // producers' write-through stores (a stale act line was seen once in a few CLI runs)
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     }
-    const int8_t *aq = act16_codes(a, 0);
+    const auto aq = act16_codes<QF>(a, 0);
     v4i x[4];
     act_load(aq, a.K, 0, k, x);
-    stage_act16<8>(a, 0, a.K, da);
+    stage_act16<8, QF>(a, 0, a.K, da);
 #pragma unroll
     for (int i = 0; i < 4; ++i) swap_halves(x[i]);
     // one tile: the next tile's loads (clamped to this tile at the end: L2 hits) go out first
@@ -1146,14 +1179,11 @@ __global__ __launch_bounds__(MMQ_NT) void k_mmq16_loop_kq(MmqSeg s0, MmqArgs a, 
     KqPass<T> wA, uA, wB, uB;
     kqp_load<T>(s0.w, row_of(tile), sb, wA);
     if constexpr (NV == 2) kqp_load<T>(a.w_up, row_of(tile), sb, uA);
-    if constexpr (QF) {
+    if constexpr (QF) {  // the records' loads below are sc1 (ActSc1)
         if (threadIdx.x == 0) wait_count(q.cnt + 64 * (blockIdx.x & 7), a.nt, q.flag);
         asm volatile("s_barrier" ::: "memory");
-        // agent-scope acquire: this XCD's L2 drops lines of the records cached before the
-        // producers' write-through stores (a stale act line was seen once in a few CLI runs)
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     }
-    const int8_t *aq = stage_act16<T>(a, 0, a.K, da);
+    const auto aq = stage_act16<T, QF>(a, 0, a.K, da);
     v4i x[4];
     kq_act(aq, sb, x);
     auto step = [&](KqPass<T> &cw, KqPass<T> &cu, KqPass<T> &nw, KqPass<T> &nu) -> bool {

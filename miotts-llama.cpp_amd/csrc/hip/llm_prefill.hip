@@ -387,14 +387,24 @@ struct ActPre {
     static constexpr int CP = NP == 1 ? 6 : (NP == 3 ? 10 : 14);
     uint4 v[CP];
 };
-template <int NP>
+// 16-B granule i of the records; SC: written by producer workgroups of this launch, so read
+// with an sc1 load (llm_mmq.hip ActSc1 explains the hand-off)
+template <bool SC>
+__device__ __forceinline__ uint4 act_granule(const char *act, int i) {
+    if constexpr (SC) {
+        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rsrc(act, 0x7FFFFFF0u), (uint32_t)i * 16u, 0, 16);
+        return make_uint4(v.x, v.y, v.z, v.w);
+    } else {
+        return reinterpret_cast<const uint4 *>(act)[i];
+    }
+}
+template <int NP, bool SC = false>
 __device__ __forceinline__ void act_issue(const char *act, int K, int nt, ActPre<NP> &ap) {
     const int n16 = (int)(act_bytes(K) * nt / 16);
-    const uint4 *src = reinterpret_cast<const uint4 *>(act);
 #pragma unroll
-    for (int u = 0; u < ActPre<NP>::CP; ++u) ap.v[u] = src[min((int)threadIdx.x + u * MT, n16 - 1)];
+    for (int u = 0; u < ActPre<NP>::CP; ++u) ap.v[u] = act_granule<SC>(act, min((int)threadIdx.x + u * MT, n16 - 1));
 }
-template <int NP>
+template <int NP, bool SC = false>
 __device__ __forceinline__ void act_store(const ActPre<NP> &ap, const char *act, int K, char *smem, int nt) {
     const int n16 = (int)(act_bytes(K) * nt / 16);
     uint4 *dst = reinterpret_cast<uint4 *>(smem + act_base(K));
@@ -403,8 +413,7 @@ __device__ __forceinline__ void act_store(const ActPre<NP> &ap, const char *act,
         const int i = (int)threadIdx.x + u * MT;
         if (i < n16) dst[i] = ap.v[u];
     }
-    const uint4 *src = reinterpret_cast<const uint4 *>(act);
-    for (int i = (int)threadIdx.x + ActPre<NP>::CP * MT; i < n16; i += MT) dst[i] = src[i];
+    for (int i = (int)threadIdx.x + ActPre<NP>::CP * MT; i < n16; i += MT) dst[i] = act_granule<SC>(act, i);
     lds_barrier();
 }
 
@@ -911,8 +920,8 @@ __global__ __launch_bounds__(MT) void k_pf_ffn_down(LlmDims d, QMat down, Prefil
 // and (Q8_K) bsum ranges are copied out with 16-B write-through stores, drained, and each
 // producer adds 1 to the 8 counter shards (workgroup 0 first zeroes the other set, the next
 // fused launch's). The matvec workgroups follow: residual and first weight group issued, one
-// lane waits for npr on its shard, then the records are copied to LDS (no workgroup of the
-// launch reads them before every producer has stored: the lines come from past the L2s).
+// lane waits for npr on its shard, then the records are copied to LDS with sc1 loads (the
+// replica-counter hand-off of llm_mmq.hip ActSc1: no plain load of a record this launch wrote).
 // Deadlock-free by dispatch order (producers first, they never wait).
 template <int NP, int T>
 __global__ __launch_bounds__(MT) void k_pf_ffn_down_q(LlmDims d, QMat down, PrefillBuffers pb, int nt, int rpw,
@@ -930,14 +939,11 @@ __global__ __launch_bounds__(MT) void k_pf_ffn_down_q(LlmDims d, QMat down, Pref
     load_first_b<T, NP, 1>(down, down, lo, hi, ga, gb);
     if (threadIdx.x == 0) wait_count(q.cnt + 64 * (blockIdx.x & 7), npr, q.flag);
     asm volatile("s_barrier" ::: "memory");
-    // agent-scope acquire: this XCD's L2 drops lines of the records cached before the
-    // producers' write-through stores (a stale act line was seen once in a few CLI runs)
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     ActPre<NP> ap;
-    act_issue<NP>(pb.act, KR, nt, ap);
+    act_issue<NP, true>(pb.act, KR, nt, ap);
     float *res = resid_lds(smem, KR, nt, rpw);
     store_resid_b(rr, res, nt, rpw);
-    act_store<NP>(ap, pb.act, KR, smem, nt);
+    act_store<NP, true>(ap, pb.act, KR, smem, nt);
     stream_rows_b<T, NP, 1>(down, down, lo, hi, ga, gb, smem, nt, [&](int row, int t, float v, float) {
         const float r = res[t * rpw + row - lo];
         pb.x[(size_t)t * E + row] = v + r;
@@ -1108,7 +1114,7 @@ __global__ __launch_bounds__(ST) void k_bt_sample(LlmDims d, QMat emb, int nblk,
     if (live) embed_row(emb, tok, d.n_embd, pb.x + (size_t)t * d.n_embd);
     if (tid == 0 && live) {
         sc.out_tokens[step] = tok;
-        if (tok == sc.eos0 || tok == sc.eos1) st->done = 1;
+        if (tok == sc.eos0 || tok == sc.eos1) st->done = 1, signal_host_done(sc);
         st->token = tok;
         // a stream ending at a full context stays frozen on its last cache row
         st->pos = min(st->pos + 1, d.n_ctx - 1);

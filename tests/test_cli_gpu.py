@@ -35,6 +35,9 @@ def run(args, timeout=300):
     p = subprocess.run([os.path.join(BIN, args[0])] + [str(a) for a in args[1:]], capture_output=True, text=True,
                        timeout=timeout)
     assert p.returncode == 0, f"{args[0]} rc={p.returncode}\n{p.stdout}\n{p.stderr[-2000:]}"
+    # a fallback the product takes must not pass a test silently (tts.cpp: a batched decode that
+    # fails - a refused model or a timed-out hand-off - decodes one utterance at a time)
+    assert "batched decode unavailable" not in p.stderr, p.stderr[-2000:]
     return p.stdout
 
 

@@ -136,6 +136,34 @@ def test_batch_c4_2p6b_q8_b8(device, synth_llm_path):
     g.close()
 
 
+CLI_PROMPTS = ["テストです。", "こんにちは。", "今日はいい天気ですね。"]
+
+
+def test_batch_cli_prompt_set_repeated(device, llm_files):
+    """Regression for round 5's intermittent `miotts --batch` mismatch (the third, longest
+    prompt's WAV differed from its single run in 1 of 3 CLI runs; the batched step's in-launch
+    quantization consumers read their producers' act records with plain loads). The exact CLI
+    workload through the C-ABI: the three prompts in the chat template, tokenized as
+    TestToSpeech::prompt_tokens does (tts.cpp:258-266), preset 1, n_ctx 2048, 40 speech-only
+    tokens at the config temperature 0.8 with the single run's seed 42 for every stream, polls
+    every 32 steps. Repeated 12 times (the first run of a fresh batch width captures its graphs,
+    the later ones replay them): every stream equals its single-stream decode every time."""
+    path = llm_files[1]
+    tok = m.Tokenizer(path)
+    prompts = [tok.tokenize("<|startoftext|><|im_start|>user\n" + m.normalize_text(p) +
+                            "<|im_end|>\n<|im_start|>assistant\n", True, True) for p in CLI_PROMPTS]
+    assert len(prompts[2]) > len(prompts[0]) > 8
+    g = m.Llm(device, path, 2048)
+    refs = [g.generate(p, 40, 0.8, 42, allow=ALLOW, check_interval=32) for p in prompts]
+    assert all(len(r) == 40 for r in refs)
+    bad = []
+    for rep in range(12):
+        got = g.generate_batch(prompts, 40, 0.8, [42, 42, 42], allow=ALLOW, check_interval=32)
+        bad += [(rep, b, int(np.argmax(got[b] != refs[b]))) for b in range(3) if not np.array_equal(got[b], refs[b])]
+    assert not bad, f"(repeat, stream, first differing token): {bad}"
+    g.close()
+
+
 _ENGINE_SCRIPT = r"""
 import hashlib, sys
 import numpy as np

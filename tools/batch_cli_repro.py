@@ -9,7 +9,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "miotts-llama.cpp_amd", "python"))
 import miotts_amd as m  # noqa: E402
 
-d = "/tmp/r05cli2"
+d = "/tmp/batch_cli_repro"
 os.makedirs(d, exist_ok=True)
 llm = m.synth_llm(d + "/llm1.gguf", 1, 1)
 codec = m.synth_codec(d + "/codec.gguf", 0, 1)
