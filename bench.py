@@ -47,7 +47,7 @@ sys.path.insert(0, os.path.join(REPO, "miotts-llama.cpp_amd", "python"))
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 ROOF_POS = 400  # decode position of the roofline timeline / kernel timings (and of the PMC run)
 KERNEL_NAMES = {0: "k_attn_in", 1: "k_attention", 2: "k_attn_out", 3: "k_ffn_in", 4: "k_ffn_down",
-                6: "k_lm_head", 8: "k_conv_in", 9: "k_conv_out", 10: "k_att_o", 11: "k_layer_att"}
+                6: "k_lm_head", 8: "k_conv_in", 9: "k_conv_out", 10: "k_att_o", 11: "k_layer_att", 12: "k_ffn"}
 PRESETS = {2: "MioTTS-0.1B Q8_0", 3: "MioTTS-1.7B Q4_K_M", 4: "MioTTS-2.6B Q8_0",
            6: "MioTTS-2.6B Q8_0 (LFM2 shape: 22 short-conv + 8 attention layers)", 12: "MioTTS-1.7B BF16"}
 PROMPT = "こんにちは、今日はいい天気ですね。"  # README.md:83, SURVEY 8(d)
@@ -208,7 +208,8 @@ def eos_tail(llm, prompt, tokens_per_step_us):
     """Cost of the decode steps queued past an end token (test-to-speech.cpp:168-170 breaks
     before the next llama_decode): an EOS-ending run (1 in 4 allowed ids is the end token,
     temperature 2), then mio_hip_llm_tail: steps issued after the end token and the GPU time of
-    the whole check intervals queued behind the poll that found it."""
+    the step graphs queued after the one that sampled it (the host stops issuing graphs when the
+    sampler's mapped host word says so)."""
     import miotts_amd as m
     for seed in range(11, 40):
         toks = llm.generate(prompt, 400, 2.0, seed, allow=(m.SYNTH_EOT, m.SYNTH_SPEECH0 + 3),
@@ -217,7 +218,10 @@ def eos_tail(llm, prompt, tokens_per_step_us):
         if timed:
             break
     r = {"tokens_before_eos": len(toks), "steps_after_eos": wasted, "timed_steps": timed,
-         "timed_ms": round(ms, 3), "check_interval": 32}
+         "timed_ms": round(ms, 3), "stop": "end-token host word, step graphs of 8, 2 queued ahead"}
+    if timed:
+        # every post-EOS step, at the timed steps' cost: the whole tail's GPU time
+        r["tail_ms_est"] = round(ms / timed * wasted, 3)
     if timed:
         r["us_per_step_after_eos"] = round(ms * 1e3 / timed, 2)
         r["us_per_step_decoding"] = round(tokens_per_step_us, 2)

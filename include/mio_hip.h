@@ -144,9 +144,11 @@ int mio_hip_llm_prefill(mio_hip_llm *m, const int32_t *tokens, int n_tokens, flo
 int mio_hip_llm_logits(mio_hip_llm *m, float *logits);
 /* run_llm (test-to-speech.cpp:94-199): prefill prompt[n_prompt], then up to max_tokens
  * sampled tokens with temperature + seeded sampling restricted to ids [allow_lo, allow_hi)
- * (-1 = whole vocab); stops at eos0/eos1 (checked every check_interval tokens on the host,
- * the end token itself is not returned). Sampling is on the device (Gumbel-max over a
- * counter-based hash of (seed, step, id)); temperature <= 0 is greedy. */
+ * (-1 = whole vocab); stops at eos0/eos1 (the end token itself is not returned). Sampling is
+ * on the device (Gumbel-max over a counter-based hash of (seed, step, id)); temperature <= 0 is
+ * greedy. The sampler stores the end token's flag to a mapped host word, and the host stops
+ * issuing step graphs (8 steps each, at most 2 queued ahead) once it is set; check_interval is
+ * accepted for ABI compatibility and no longer paces the stop (round 6). */
 int mio_hip_llm_generate(mio_hip_llm *m, const int32_t *prompt, int n_prompt, int max_tokens,
                          float temperature, uint64_t seed, int32_t allow_lo, int32_t allow_hi,
                          int32_t eos0, int32_t eos1, int32_t check_interval,
@@ -171,8 +173,9 @@ int mio_hip_llm_eval_layers(mio_hip_llm *m, int32_t token, int pos, float *x_lay
 int mio_hip_llm_kv_rows(mio_hip_llm *m, int il, int n_pos, uint16_t *k, uint16_t *v);
 
 /* Live timing of one decode-step kernel (which: 0 attn_in, 1 attention, 2 attn_out,
- * 3 ffn_in, 4 ffn_down, 8 conv_in, 9 conv_out of the first layer at or after n_layer/2 that
- * has it; 6 lm_head): `iters` back-to-back launches on
+ * 3 ffn_in, 4 ffn_down, 8 conv_in, 9 conv_out, 10 attention + O, 11 the attention block,
+ * 12 the FFN pair, of the first layer at or after n_layer/2 that has it; 6 lm_head): `iters`
+ * back-to-back launches on
  * the runner's stream between HIP events (state/buffers of the last generate/eval).
  * *avg_ms = mean duration; *bytes = algorithmic HBM bytes per launch (attention: K/V rows of
  * positions <= the decode state's pos, q|k|v, chunk partials). */
@@ -190,8 +193,8 @@ int mio_hip_llm_trace_kernel(mio_hip_llm *m, int which, uint64_t *out);
  * Advances the decode state. */
 int mio_hip_llm_timeline(mio_hip_llm *m, uint64_t *out, int max_launches, int *n_launches);
 /* The launches of one decode step in order, as the `which` of mio_hip_llm_time_kernel: per
- * layer 0 attn_in, 1 attention, 2 attn_out, or for an lfm2 short-conv layer 8 conv_in, 9 conv_out; then 3 ffn_in, 4
- * ffn_down; last 6 lm_head. *n = the count; kinds may be null (count only), else it needs
+ * layer 0 attn_in, 1 attention, 2 attn_out (or 10 / 11: fused), or for an lfm2 short-conv
+ * layer 8 conv_in, 9 conv_out; then 3 ffn_in, 4 ffn_down (or 12: fused); last 6 lm_head. *n = the count; kinds may be null (count only), else it needs
  * cap >= *n entries. */
 int mio_hip_llm_step_kinds(const mio_hip_llm *m, int *kinds, int cap, int *n);
 /* lfm2 short-conv state of layer il: [4][n_embd] floats, slot p & 3 = the B*X row of position
@@ -201,17 +204,16 @@ int mio_hip_llm_conv_ring(mio_hip_llm *m, int il, float *ring, int set);
  * asynchronous copies into the HBM weight arena (double-buffered). */
 int mio_hip_llm_load_ms(const mio_hip_llm *m, double *ms);
 /* Decode steps (one sampled token each) issued since the last generate began, look-ahead
- * included: generate keeps one check interval queued ahead of its end-token poll, so a run
- * that stops at an end token after n_out tokens issued *steps - n_out - 1 steps for nothing
- * (the rest of the end token's interval plus one more: < 2 * check_interval; 0 when it stops
- * at max_tokens). */
+ * included: generate keeps up to 2 step graphs queued ahead of the GPU, so a run that stops at
+ * an end token after n_out tokens issued *steps - n_out - 1 steps for nothing (the rest of the
+ * end token's graph plus at most one more: <= 15; 0 when it stops at max_tokens). */
 int mio_hip_llm_steps_issued(const mio_hip_llm *m, int *steps);
 /* Cost of those steps after the last mio_hip_llm_generate that stopped at an end token
  * (test-to-speech.cpp:168-170 decodes nothing after it): every decode launch after the end
  * token returns at entry (StepState.done), so such a step costs about its launch boundaries.
  * *steps = steps issued after the end token's step (0 when the run stopped at max_tokens);
- * *timed_steps / *timed_ms = the whole check intervals queued behind the poll that found it and
- * their GPU time (HIP events; 0 when none was queued). */
+ * *timed_steps / *timed_ms = the step graphs queued after the one that sampled the end token
+ * and their GPU time (HIP events; 0 when none was queued). */
 int mio_hip_llm_tail(const mio_hip_llm *m, int *steps, int *timed_steps, float *timed_ms);
 /* Allocates now the device memory decodes of up to n_codes codes need (workspace, RoPE
  * table, incremental prenet cache), as miocodec_load's graph-allocator reserve

@@ -28,6 +28,9 @@ __global__ __launch_bounds__(MT) void k_attn_in(LlmDims d, const float *norm_w, 
     const Smem s = carve(smem, K);
     MIO_TRACE(b, 0);
     MIO_TL_BEGIN(b);
+    if (blockIdx.x == 2 && MIO_TIDX < 2 * kFfnShards)  // the previous k_ffn's h counters (kernel boundary ordered)
+        __hip_atomic_store((__attribute__((address_space(1))) int *)(b.att_cnt + kFfnOff + kFfnStride * MIO_TIDX), 0,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     int pend = 0, step = 0;
     if constexpr (FS) {
         // after an end token every decode launch returns at entry (test-to-speech.cpp:168-170
@@ -56,7 +59,7 @@ __global__ __launch_bounds__(MT) void k_attn_in(LlmDims d, const float *norm_w, 
                     }
                     if (MIO_TIDX == 0) {
                         if (step < sc.max_steps) sc.out_tokens[step] = tok;
-                        if (tok == sc.eos0 || tok == sc.eos1) b.st->done = 1;
+                        if (tok == sc.eos0 || tok == sc.eos1) b.st->done = 1, signal_host_done(sc);
                         b.st->token = tok;
                     }
                 }

@@ -1056,6 +1056,12 @@ __device__ __forceinline__ uint32_t done_issue(const B &b) {
     return __builtin_amdgcn_raw_buffer_load_b32(rsrc(&b.st->done, 4), 0, 0, 0);
 }
 __device__ __forceinline__ bool done_now(uint32_t v) { return __builtin_amdgcn_readfirstlane(v) != 0; }
+// An end token was sampled: besides StepState.done (which the step's own launches read), one
+// system-scope vector store to the host's mapped word, so the host stops enqueuing steps
+// without a blocking poll (once per utterance, over PCIe)
+__device__ __forceinline__ void signal_host_done(const SampleCfg &sc) {
+    if (sc.host_done) __hip_atomic_store(sc.host_done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 // The pending sample's token: Gumbel-max winner (ties -> lowest id) over the lm_head
 // workgroups' partials {smp[2i] value, smp[2i+1] id bits}, sc.lo when no id was allowed, the
@@ -1157,14 +1163,22 @@ __device__ __forceinline__ void st4_sc1(float *base, uint32_t off, float4 v) {
 }
 // One lane waits until the agent-scope counter *c reaches target (relaxed loads, s_sleep
 // between polls: MI355X_MICROARCH "polling-cost"). Bounded: after ~2^16 polls (tens of ms) it
-// gives up and raises *flag, so a lost signal ends the launch instead of hanging the GPU.
+// gives up and raises *flag, so a lost signal ends the launch instead of hanging the GPU. Once
+// the flag is up (an earlier wait of this run gave up: the run is already an error), every
+// further wait returns after at most 1024 polls instead of spinning its full bound: a broken
+// hand-off costs one bound per run, not one per launch (round 5 saw a 180-s stall that a
+// per-launch timeout across a 40-step batch would explain).
+// Hand-off rule for every caller: the bytes the signallers published are read with sc1 loads
+// only (buffer / global loads with aux 16), never plain loads (MI355X_MICROARCH, replica row).
 __device__ __forceinline__ void wait_count(int *c, int target, int *flag) {
     auto *p = (__attribute__((address_space(1))) int *)c;
+    auto *f = (__attribute__((address_space(1))) int *)flag;
     for (int it = 0; it < (1 << 16); ++it) {
         if (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) return;
+        if ((it & 1023) == 1023 && __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
         __builtin_amdgcn_s_sleep(1);
     }
-    __hip_atomic_store((__attribute__((address_space(1))) int *)flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(f, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ float4 ld4_sc1(const float *base, uint32_t off) {
     const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rsrc(base, 0x7FFFFFF0u), off, 0, 16);
@@ -1182,6 +1196,9 @@ __device__ __forceinline__ float2 ld2_sc1(const float *base, uint32_t off) {
 // the sums unchanged (only real chunks are loaded: every vector load instruction costs the
 // CU's address path the same, used or not). The float order does not depend on which
 // workgroup merges, so every path's outputs are the same bits.
+// (r06 A/B: issuing the next batch's loads before merging the current one doubles the
+// batch registers; k_layer_att went from 65 to 136-160 VGPRs, its roles no longer co-reside,
+// and the step lost 9 %: not kept.)
 __device__ __forceinline__ float4 merge_out4(const float *part, uint32_t head, int nch, int rec, int hd, int dd) {
     float M = -INFINITY, L = 0.0f;
     float4 O = make_float4(0.f, 0.f, 0.f, 0.f);

@@ -62,6 +62,7 @@ struct SampleCfg {
     int n_force;
     int *out_tokens;     // [max_steps] sampled/forced next token per step
     int max_steps;
+    int *host_done;      // mapped host word set to 1 with StepState.done (null: none)
 };
 
 // lfm2 gated short conv: kernel width (shortconv.l_cache) and the ring of bx values kept per
@@ -202,6 +203,8 @@ bool att_o_supported(int hd, int G);
 // the whole attention block of layer L as one launch (llm_layer_att.hip, which = 11) exists for
 // its shapes and weight types
 bool layer_att_supported(const LlmDims &d, const LayerW &L);
+// the FFN pair of layer L as one launch (k_ffn, which = 12) exists for its weight types
+bool ffn_fused_supported(const LlmDims &d, const LayerW &L);
 void launch_layer_att(const LlmDims &d, const LayerW &L, _Float16 *kc, _Float16 *vc, const LlmBuffers &b, bool dg,
                       hipStream_t s);
 // k_att_o's merge counters in LlmBuffers.att_cnt: kRdyShards words kRdyStride ints (256 B)
@@ -212,7 +215,15 @@ void launch_layer_att(const LlmDims &d, const LayerW &L, _Float16 *kc, _Float16 
 constexpr int kRdyOff = 64, kRdyShards = 8, kRdyStride = 64;
 constexpr int kRdyFlag = kRdyOff + kRdyShards * kRdyStride;
 constexpr int kQkvOff = kRdyFlag + 64, kQkvStride = 64, kQkvMax = 64;
-constexpr int kAttCntInts = kQkvOff + kQkvStride * kQkvMax;
+// Then the fused FFN launch's h counters (k_ffn, which = 12), two levels, every word kFfnStride
+// ints apart: kFfnShards arrival shards (gate|up workgroup b adds 1 to shard b % 8: <= 32 adds
+// per word at 256 producers; the price list's fan-in on one word is 3.6-4.5 us), then
+// kFfnShards ready replicas (the producer whose shard add returns the shard's last count adds 1
+// to every replica; a down workgroup polls replica b % 8 until all shards are in: <= 32 pollers
+// per word). Zeroed by the launch after k_ffn (the next layer's attn_in / layer_att, lm_head).
+constexpr int kFfnOff = kQkvOff + kQkvStride * kQkvMax, kFfnShards = 8, kFfnStride = 64;
+constexpr int kFfnRdy = kFfnOff + kFfnShards * kFfnStride;
+constexpr int kAttCntInts = kFfnRdy + kFfnShards * kFfnStride;
 int pick_np(int K);
 size_t matvec_lds(int K);
 // units (row passes) of the busiest wave of a matvec over `rows` rows on `grid` workgroups,

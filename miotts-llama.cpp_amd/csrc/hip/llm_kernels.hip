@@ -201,6 +201,146 @@ __global__ __launch_bounds__(MT) void k_ffn_down(LlmDims d, QMat down, LlmBuffer
     MIO_TRACE(b, 15);
 }
 
+// The FFN pair of a layer as ONE launch (which = 12, MIO_FFN_FUSE): two workgroup roles of
+// one grid.
+//   [0, GI)        k_ffn_in's body (RMSNorm + quant -> gate|up matvec + SwiGLU), the h rows
+//                  stored write-through (sc1); every storing wave drains its stores
+//                  (vmcnt(0)), a workgroup barrier, then ONE lane adds 1 to shard blockIdx % 8
+//                  of the h counter (b.att_cnt + kFfnOff); the shard's last arriver adds 1 to
+//                  each of the 8 ready replicas (kFfnRdy)
+//   [GI, GI + GD)  k_ffn_down's body: residual rows and the first weight group issued, one lane
+//                  waits until its ready replica (blockIdx % 8) counts every shard, a barrier
+//                  releases the waves, h is loaded with sc1 loads, quantized, streamed, x += .
+// MI355X_MICROARCH hand-off rows 1-2 (sharded arrivals, replicated ready word, every load of the
+// handed-off bytes sc1; a first version polled all 8 arrival shards from every down workgroup:
+// 256 pollers per word, the step 12 % slower);
+// the boundary it removes costs ~1.5-2.1 us plus the down's first-load latency, which now
+// overlaps the gate|up stream. Producers never wait and precede every consumer, so in-order
+// dispatch makes progress whatever the residency. The consumers write x only after every
+// producer has signalled, i.e. after every producer's read of x. Arithmetic = the two
+// launches' (bit-identical). The counter is zeroed by the next launch (attn_in / layer_att /
+// lm_head), the timeout flag is k_att_o's (kRdyFlag).
+template <int NP, int T, int SU, int NPD, int TD, int SUD, bool DG>
+__global__ __launch_bounds__(MT) void k_ffn(LlmDims d, const float *norm_w, QMat gate, QMat up, QMat down,
+                                            LlmBuffers b, int adv, int GI) {
+    constexpr bool kDiag = DG;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    MIO_TRACE(b, 0);
+    MIO_TL_BEGIN(b);
+    const uint32_t dn = done_issue(b);
+    if ((int)blockIdx.x < GI) {
+        const int K = d.n_embd;
+        const Smem s = carve(smem, K);
+        XRegs<NP> xr;
+        load_x(b.x, norm_w, K, xr);
+        x_gate();
+        if (blockIdx.x == 0 && MIO_TIDX < kRdyShards)
+            __hip_atomic_store((__attribute__((address_space(1))) int *)(b.att_cnt + kRdyOff + kRdyStride * MIO_TIDX),
+                               0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (blockIdx.x == 1 && MIO_TIDX < d.n_kv)
+            __hip_atomic_store((__attribute__((address_space(1))) int *)(b.att_cnt + kQkvOff + kQkvStride * MIO_TIDX),
+                               0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        int lo, hi;
+        wave_range(gate.rows, lo, hi, blockIdx.x, GI);
+        Frag ga[Cfg<NP, SU>::U], gb[Cfg<NP, SU>::U];
+        load_first<T, NP, 2, SU>(gate, up, lo, hi, ga, gb);
+        x_after_weights(xr);
+        if (done_now(dn)) {  // layer 0 still folds the end token's step (the host counts it)
+            if (adv && blockIdx.x == 0 && MIO_TIDX == 0) advance_state(b.st, d);
+            return;
+        }
+        MIO_TL_MARK1(b);
+        rmsnorm_quant(xr, K, d.eps, akind(T), s, MIO_TL_DIAGSLOT(b));
+        MIO_TL_MARK(b, 2);
+        stream_rows<T, NP, 2, SU>(gate, up, lo, hi, ga, gb, s.a, [&](int row, float g, float u) {
+            if ((threadIdx.x & 63) == 0) st1_sc1(b.h, (uint32_t)row * 4u, silu_f(g) * u);
+        });
+        if (adv && blockIdx.x == 0 && MIO_TIDX == 0) advance_state(b.st, d);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (MIO_TIDX < 64) {
+            int last = 0;
+            if (MIO_TIDX == 0) {
+                const int sh = blockIdx.x & (kFfnShards - 1), n_sh = (GI - sh + kFfnShards - 1) / kFfnShards;
+                last = __hip_atomic_fetch_add((__attribute__((address_space(1))) int *)(b.att_cnt + kFfnOff + kFfnStride * sh),
+                                              1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == n_sh - 1;
+            }
+            // the shard's last arriver: its add returned after every other add of the shard, each
+            // made after that workgroup's h stores had drained; one instruction, 8 lanes
+            if (__builtin_amdgcn_readfirstlane(last) && MIO_TIDX < kFfnShards)
+                __hip_atomic_fetch_add((__attribute__((address_space(1))) int *)(b.att_cnt + kFfnRdy + kFfnStride * MIO_TIDX),
+                                       1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    } else {
+        const int K = down.k;
+        const Smem s = carve(smem, K);
+        const int GD = (int)gridDim.x - GI, ob = (int)blockIdx.x - GI;
+        int lo, hi;
+        wave_range(down.rows, lo, hi, ob, GD);
+        const float xres = load_resid(b.x, lo, hi);
+        Frag ga[Cfg<NPD, SUD>::U], gb[Cfg<NPD, SUD>::U];
+        load_first<TD, NPD, 1, SUD>(down, down, lo, hi, ga, gb);
+        if (done_now(dn)) return;  // the producers return too: nobody signals, nobody waits
+        if (MIO_TIDX == 0)
+            wait_count(b.att_cnt + kFfnRdy + kFfnStride * (blockIdx.x & (kFfnShards - 1)), min(GI, kFfnShards),
+                       b.att_cnt + kRdyFlag);
+        asm volatile("s_barrier" ::: "memory");
+        MIO_TL_MARK(b, 3);
+        XRegs<NPD> xr;
+        load_x<NPD, 16>(b.h, nullptr, K, xr);
+        x_after_weights(xr);
+        MIO_TL_MARK1(b);
+        plain_quant(xr, K, akind(TD), s, MIO_TL_DIAGSLOT(b));
+        MIO_TL_MARK(b, 2);
+        stream_rows<TD, NPD, 1, SUD>(down, down, lo, hi, ga, gb, s.a, [&](int row, float v, float) {
+            const float r = lane_value(xres, row - lo);
+            if ((threadIdx.x & 63) == 0) b.x[row] = v + r;
+        });
+    }
+    MIO_TL_END(b);
+    MIO_TRACE(b, 15);
+}
+
+// the instantiated (np, gate|up type, su, down np, down type, down su): 1.7B Q4_K_M (down Q4_K
+// or Q6_K) and BF16, 0.1B Q8_0, 2.6B Q8_0 (and LFM2-2.6B), the tiny test presets' shapes
+#define MIO_FFN_SHAPES(X) \
+    X(1, 12, 6, 3, 12, 3)  \
+    X(1, 12, 6, 3, 14, 3)  \
+    X(1, 30, 6, 3, 30, 3)  \
+    X(1, 8, 2, 1, 8, 1)    \
+    X(1, 8, 0, 6, 8, 0)
+
+struct FfnShape {
+    int np, t, su, npd, td, sud, GI, GD;
+};
+FfnShape ffn_shape(const LlmDims &d, const LayerW &L) {
+    FfnShape f{};
+    f.GI = matvec_grid(d, L.gate.rows), f.GD = matvec_grid(d, L.down.rows);
+    f.np = pick_np(d.n_embd), f.t = L.gate.type;
+    f.su = pick_su(max_wave_units(L.gate.rows, f.GI, f.np, 2), f.np);
+    f.npd = pick_np(L.down.k), f.td = L.down.type;
+    f.sud = pick_su(max_wave_units(L.down.rows, f.GD, f.npd, 1), f.npd);
+    return f;
+}
+
+template <bool DG>
+bool launch_ffn(const LlmDims &d, const LayerW &L, const LlmBuffers &b, int adv, hipStream_t st, bool dry) {
+    if (L.up.type != L.gate.type) return false;
+    const FfnShape f = ffn_shape(d, L);
+    const size_t lds = std::max(smem_bytes(d.n_embd), smem_bytes(L.down.k));
+    bool found = false;
+#define MIO_FFN_CASE(NP, T, SU, NPD, TD, SUD)                                                                     \
+    if (!found && f.np == NP && f.t == T && f.su == SU && f.npd == NPD && f.td == TD && f.sud == SUD) {          \
+        found = true;                                                                                            \
+        if (!dry)                                                                                                \
+            hipLaunchKernelGGL((k_ffn<NP, T, SU, NPD, TD, SUD, DG>), dim3(f.GI + f.GD), dim3(MT), lds, st, d,       \
+                               L.ffn_norm, L.gate, L.up, L.down, b, adv, f.GI);                                  \
+    }
+    MIO_FFN_SHAPES(MIO_FFN_CASE)
+#undef MIO_FFN_CASE
+    return found;
+}
+
 // final RMSNorm (once per CU) + logits + per-workgroup Gumbel-max partial. A wave's rows
 // (<= 128) are parked one per lane (two registers) and the noise is drawn for 64 rows at
 // a time after the stream.
@@ -213,6 +353,9 @@ __global__ __launch_bounds__(MT) void k_lm_head(LlmDims d, const float *norm_w, 
     const int K = d.n_embd;
     MIO_TRACE(b, 0);
     MIO_TL_BEGIN(b);
+    if (blockIdx.x == 2 && MIO_TIDX < 2 * kFfnShards)  // the previous k_ffn's h counters (kernel boundary ordered)
+        __hip_atomic_store((__attribute__((address_space(1))) int *)(b.att_cnt + kFfnOff + kFfnStride * MIO_TIDX), 0,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const Smem s = carve(smem, K);
     XRegs<NP> xr;
     load_x(b.x, norm_w, K, xr);
@@ -374,7 +517,7 @@ __global__ __launch_bounds__(ST) void k_sample(LlmDims d, QMat emb, int nblk, Ll
     MIO_TRACE(b, 15);
     if (MIO_TIDX == 0) {
         if (step < sc.max_steps) sc.out_tokens[step] = tok;
-        if (tok == sc.eos0 || tok == sc.eos1) st->done = 1;
+        if (tok == sc.eos0 || tok == sc.eos1) st->done = 1, signal_host_done(sc);
         st->token = tok;
         // a full context ends generation (host-side step budget); the state never points
         // past the cache, so later diagnostic launches stay in bounds
@@ -398,6 +541,9 @@ static_assert(MW == 8, "matvec_grid_n assumes 8 waves per workgroup");
 // (hd, G) of the fused launch: 1.7B qwen3 (128, 2), 0.1B (64, 3), 2.6B (64, 4); other shapes
 // keep the two launches
 bool att_o_supported(int hd, int G) { return (hd == 128 && G == 2) || (hd == 64 && (G == 3 || G == 4)); }
+bool ffn_fused_supported(const LlmDims &d, const LayerW &L) {
+    return launch_ffn<false>(d, L, LlmBuffers{}, 0, nullptr, true);
+}
 
 int matvec_grid(const LlmDims &d, int rows) { return matvec_grid_n(d.n_wg, rows); }
 
@@ -520,6 +666,9 @@ void launch_step_kernel(int which, const LlmDims &d, const LayerW *layers, int i
             });
             break;
         }
+        case 12:  // the FFN pair in one launch (k_ffn)
+            launch_ffn<DG>(d, layers[il], b, il == 0 ? 1 : 0, s, false);
+            break;
         case 8: {  // lfm2 conv_in: RMSNorm + in_proj as the attn_in launch (B | C rows, X rows)
             const LayerW &L = layers[il];
             const int n = d.n_embd;

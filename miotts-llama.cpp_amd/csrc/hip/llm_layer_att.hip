@@ -95,6 +95,9 @@ __global__ __launch_bounds__(MT) void k_layer_att(LlmDims d, const float *norm_w
     constexpr bool kDiag = DG;
     MIO_TRACE(b, 0);
     MIO_TL_BEGIN(b);
+    if (blockIdx.x == 2 && MIO_TIDX < 2 * kFfnShards)  // the previous k_ffn's h counters (kernel boundary ordered)
+        __hip_atomic_store((__attribute__((address_space(1))) int *)(b.att_cnt + kFfnOff + kFfnStride * MIO_TIDX), 0,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int bid = blockIdx.x;
     if (bid < GW) {
         qkv_producer<NP, TQ, TV, SU, HD, G, DG>(d, norm_w, wq, wk, wv, g_qk, GW, b);

@@ -92,6 +92,13 @@ struct mio_hip_llm {
     // time of the whole intervals queued behind that snapshot
     int eos_snap = -1, tail_steps = 0, tail_timed_steps = 0;
     float tail_ms = 0.0f;
+    // end-token words the samplers store to host memory (pinned, mapped: [0] the single-stream
+    // decode, [1 + b] batched stream b), so the host stops enqueuing steps without a blocking
+    // poll; and one event per step graph of the running generate (flow control: at most
+    // kRunDepth graphs queued ahead of the GPU; the tail timing)
+    int *host_done = nullptr, *host_done_dev = nullptr;
+    std::vector<hipEvent_t> run_ev;
+    int run_base = 0, run_graphs = 0;  // steps issued before the first graph; graphs issued
 
     ~mio_hip_llm() {
         if (d) hipSetDevice(d->dev);
@@ -103,6 +110,8 @@ struct mio_hip_llm {
         for (void *p : bt.allocs) hipFree(p);
         for (void *p : allocs) hipFree(p);
         stager_free(stager);
+        if (host_done) hipHostFree(host_done);
+        for (hipEvent_t e : run_ev) hipEventDestroy(e);
         for (Snap &sn : snaps) {
             if (sn.ev) hipEventDestroy(sn.ev);
             if (sn.st) hipHostFree(sn.st);
@@ -277,15 +286,18 @@ bool fuse_att_o(const mio_hip_llm *m) {
 
 // k_att_o's bounded wait (wait_count) raises att_cnt[kRdyFlag] if a merge signal never came:
 // reported as an error instead of silently using stale attention outputs.
+bool fuse_ffn(const mio_hip_llm *m, int il);
 int check_handoff(mio_hip_llm *m) {
-    if (!fuse_att_o(m)) return MIO_OK;
+    bool any = fuse_att_o(m);
+    for (int il = 0; il < m->n_layer && !any; ++il) any = fuse_ffn(m, il);
+    if (!any) return MIO_OK;
     int flag = 0;
     int *f = m->buf.att_cnt + mio::kRdyFlag;
     MIO_HIP_CHECK(hipMemcpyAsync(&flag, f, sizeof(int), hipMemcpyDeviceToHost, m->d->stream));
     MIO_HIP_CHECK(hipStreamSynchronize(m->d->stream));
     if (flag) {
         MIO_HIP_CHECK(hipMemsetAsync(f, 0, sizeof(int), m->d->stream));
-        mio::set_error("llm decode: the attention -> O hand-off wait timed out");
+        mio::set_error("llm decode: an in-launch hand-off wait (attention -> O, or gate|up -> down) timed out");
         return MIO_ERR_HIP;
     }
     return MIO_OK;
@@ -308,6 +320,13 @@ bool fuse_layer_att(const mio_hip_llm *m, int il) {
     return env == 1 || !(d.hd == 64 && d.n_head == 3 * d.n_kv);
 }
 
+// MIO_FFN_FUSE (default 1): the FFN pair of a layer as one launch (k_ffn, which = 12) where it
+// is instantiated (ffn_fused_supported); 0 keeps k_ffn_in + k_ffn_down (A/B).
+bool fuse_ffn(const mio_hip_llm *m, int il) {
+    static const bool env = !(getenv("MIO_FFN_FUSE") && getenv("MIO_FFN_FUSE")[0] == '0');
+    return env && mio::ffn_fused_supported(m->dims, m->layers[il]);
+}
+
 int layer_kinds(const mio_hip_llm *m, int il, int *w) {
     int n = 0;
     if (m->layers[il].conv) {
@@ -319,7 +338,10 @@ int layer_kinds(const mio_hip_llm *m, int il, int *w) {
     } else {
         w[n++] = 0, w[n++] = 1, w[n++] = 2;
     }
-    w[n++] = 3, w[n++] = 4;
+    if (fuse_ffn(m, il))
+        w[n++] = 12;
+    else
+        w[n++] = 3, w[n++] = 4;
     return n;
 }
 
@@ -539,6 +561,8 @@ int llm_begin(mio_hip_llm *m, const int32_t *prompt, int n_prompt, int max_new, 
     c.eos0 = sp.eos0, c.eos1 = sp.eos1;
     c.force = m->d_force, c.n_force = m->max_steps;
     c.out_tokens = m->d_tokens, c.max_steps = m->max_steps;
+    __atomic_store_n(m->host_done, 0, __ATOMIC_SEQ_CST);  // the cfg copy below is stream-ordered behind it
+    c.host_done = m->host_done_dev;
     if ((rc = put_cfg(m, c)) || (rc = ensure_graph(m))) return rc;
     m->n_prompt = n_prompt;
     m->max_new = max_new;
@@ -572,6 +596,48 @@ int llm_run(mio_hip_llm *m, int n_steps) {
         for (const int gs = graph_steps(); n >= gs; n -= gs) MIO_HIP_CHECK(hipGraphLaunch(m->graph_n, m->d->stream));
         for (; n > 0; --n) MIO_HIP_CHECK(hipGraphLaunch(m->graph, m->d->stream));
     }
+    if ((rc = flush_sample(m))) return rc;
+    return snap_push(m);
+}
+
+int llm_graph_steps() { return graph_steps(); }
+
+// Steps until the end: graphs of graph_steps() steps, at most kRunDepth queued ahead of the GPU
+// (the host waits for the event of the graph kRunDepth back, while the next one still runs),
+// and none issued once the sampler has stored the end token's host word. After an end token the
+// rest of its graph and at most kRunDepth - 1 more run (returning at entry), instead of the
+// rest of a 32-step poll interval and one more interval. Then the flush sampler + a snapshot
+// (llm_poll collects the tokens).
+int llm_run_to_end(mio_hip_llm *m) {
+    constexpr int kRunDepth = 2;
+    int rc = mio::bind(m->d);
+    if (rc) return rc;
+    static const bool eager = getenv("MIO_NO_GRAPH") && getenv("MIO_NO_GRAPH")[0] == '1';
+    const int gs = graph_steps();
+    m->run_base = m->steps_issued;
+    int k = 0;
+    while (m->steps_issued < m->steps_total) {
+        if (k >= kRunDepth) MIO_HIP_CHECK(hipEventSynchronize(m->run_ev[k - kRunDepth]));
+        if (__atomic_load_n(m->host_done, __ATOMIC_ACQUIRE)) break;
+        const int n = std::min(gs, m->steps_total - m->steps_issued);
+        if (eager) {
+            for (int i = 0; i < n; ++i)
+                if ((rc = issue_step(m))) return rc;
+        } else if (n == gs) {
+            MIO_HIP_CHECK(hipGraphLaunch(m->graph_n, m->d->stream));
+        } else {
+            for (int i = 0; i < n; ++i) MIO_HIP_CHECK(hipGraphLaunch(m->graph, m->d->stream));
+        }
+        m->steps_issued += n;
+        if ((int)m->run_ev.size() <= k) {
+            hipEvent_t e = nullptr;
+            MIO_HIP_CHECK(hipEventCreate(&e));
+            m->run_ev.push_back(e);
+        }
+        MIO_HIP_CHECK(hipEventRecord(m->run_ev[k], m->d->stream));
+        ++k;
+    }
+    m->run_graphs = k;
     if ((rc = flush_sample(m))) return rc;
     return snap_push(m);
 }
@@ -863,6 +929,13 @@ extern "C" int mio_hip_llm_load(mio_hip_device *d, const char *path, int n_ctx, 
             mio::set_error("llm_load: pinned host buffers / events failed");
             return fail(MIO_ERR_OOM);
         }
+    if (hipHostMalloc((void **)&m->host_done, 64 * sizeof(int), hipHostMallocMapped | hipHostMallocCoherent) !=
+            hipSuccess ||
+        hipHostGetDevicePointer((void **)&m->host_done_dev, m->host_done, 0) != hipSuccess) {
+        mio::set_error("llm_load: mapped host end-token words failed");
+        return fail(MIO_ERR_OOM);
+    }
+    std::memset(m->host_done, 0, 64 * sizeof(int));
     want(m->d_tokens, m->max_steps);
     want(m->d_force, m->max_steps);
     want(m->d_prompt, n_ctx);
@@ -1084,32 +1157,24 @@ extern "C" int mio_hip_llm_generate(mio_hip_llm *m, const int32_t *prompt, int n
     sp.eos0 = eos0, sp.eos1 = eos1;
     int rc = mio::llm_begin(m, prompt, n_prompt, max_tokens, sp);
     if (rc) return rc;
-    const int total = n_prompt - 1 + max_tokens;
-    if (check_interval <= 0) check_interval = total;
+    (void)check_interval;  // the end token reaches the host through its mapped word (r06)
     std::vector<int32_t> toks;
     bool done = false;
-    // (llm_begin prefilled the prompt) check every `check_interval` generated tokens (the
-    // streaming cadence, test-to-speech.cpp:499,608) for an end token. The next interval is
-    // enqueued before the previous one is checked: the GPU never waits for the host; after
-    // an end token the rest of its interval and one more run for nothing (their tokens are
-    // dropped; mio_hip_llm_steps_issued counts them).
     m->eos_snap = -1, m->tail_steps = 0, m->tail_timed_steps = 0, m->tail_ms = 0.0f;
-    if ((rc = mio::llm_run(m, check_interval))) return rc;
-    while (!done) {
-        if (m->steps_issued < m->steps_total && (rc = mio::llm_run(m, check_interval))) return rc;
-        if ((rc = mio::llm_poll(m, toks, &done))) return rc;
-    }
+    if ((rc = mio::llm_run_to_end(m))) return rc;
+    if ((rc = mio::llm_poll(m, toks, &done))) return rc;
     if (m->eos_snap >= 0) {
-        // steps after the end token's: they return at entry (StepState.done); the whole
-        // intervals queued behind the snapshot that found it are timed by its event and the
-        // last one's
-        m->tail_steps = m->steps_issued - (n_prompt - 1) - (int)toks.size() - 1;
-        if (m->snap_n > 0) {
-            const auto &a = m->snaps[m->eos_snap];
-            const auto &z = m->snaps[(m->snap_head + m->snap_n - 1) % mio_hip_llm::kSnaps];
-            MIO_HIP_CHECK(hipEventSynchronize(z.ev));
-            MIO_HIP_CHECK(hipEventElapsedTime(&m->tail_ms, a.ev, z.ev));
-            m->tail_timed_steps = z.issued - a.issued;
+        // steps after the end token's: they return at entry (StepState.done). The end token is
+        // sampled by step e + 1 (inside its layer-0 launch, or the flush after the last graph);
+        // the graphs queued after the one holding that step are timed by their events
+        const int e1 = (n_prompt - 1) + (int)toks.size() + 1;
+        m->tail_steps = m->steps_issued - e1;
+        const int gs = mio::llm_graph_steps();
+        const int g = (e1 - 1 - m->run_base) / gs;  // step numbers are 0-based: e1 - 1 is step e + 1
+        if (g >= 0 && g + 1 < m->run_graphs) {
+            MIO_HIP_CHECK(hipEventSynchronize(m->run_ev[m->run_graphs - 1]));
+            MIO_HIP_CHECK(hipEventElapsedTime(&m->tail_ms, m->run_ev[g], m->run_ev[m->run_graphs - 1]));
+            m->tail_timed_steps = m->steps_issued - std::min(m->steps_total, m->run_base + (g + 1) * gs);
         }
     }
     if ((rc = check_handoff(m))) return rc;
@@ -1292,6 +1357,8 @@ extern "C" int mio_hip_llm_generate_batch(mio_hip_llm *m, const int32_t *prompts
         c.eos0 = eos0, c.eos1 = eos1;
         c.force = nullptr, c.n_force = 0;
         c.out_tokens = bt.tokens + (size_t)b * D.n_ctx;
+        c.host_done = m->host_done_dev + 1 + b;
+        __atomic_store_n(m->host_done + 1 + b, 0, __ATOMIC_SEQ_CST);
         // as llm_begin: a full context ends the stream after n_ctx - len + 1 tokens
         c.max_steps = P + std::min(max_tokens, D.n_ctx - prompt_lens[b] + 1);
     }
@@ -1299,18 +1366,33 @@ extern "C" int mio_hip_llm_generate_batch(mio_hip_llm *m, const int32_t *prompts
     MIO_HIP_CHECK(hipMemcpyAsync(bt.cfg, cf.data(), B * sizeof(mio::SampleCfg), hipMemcpyHostToDevice, s));
     mio::launch_batch_embed(D, m->tok, batch_pb(m), batch_bb(m), B, s);
     MIO_HIP_CHECK(hipGetLastError());
-    if (check_interval <= 0) check_interval = max_tokens;
-    std::vector<mio::StepState> hs(B);
-    for (int done = 0; done < max_tokens;) {
-        const int n = std::min(check_interval, max_tokens - done);
-        if ((rc = run_batch(m, n))) return rc;
-        done += n;
-        MIO_HIP_CHECK(hipMemcpyAsync(hs.data(), bt.st, B * sizeof(mio::StepState), hipMemcpyDeviceToHost, s));
-        MIO_HIP_CHECK(hipStreamSynchronize(s));
+    // graphs of graph_steps() steps, at most 2 queued ahead of the GPU; none issued once every
+    // stream has stored its end token's host word or spent its step budget (check_interval no
+    // longer paces this: r06)
+    (void)check_interval;
+    std::vector<int> budget(B);
+    for (int b = 0; b < B; ++b) budget[b] = std::min(max_tokens, D.n_ctx - prompt_lens[b] + 1);
+    constexpr int kRunDepth = 2;
+    const int gs = graph_steps();
+    for (int issued = 0, k = 0; issued < max_tokens; ++k) {
+        if (k >= kRunDepth) MIO_HIP_CHECK(hipEventSynchronize(m->run_ev[k - kRunDepth]));
         bool all = true;
-        for (int b = 0; b < B; ++b) all = all && hs[b].done;
+        for (int b = 0; b < B && all; ++b)
+            all = issued >= budget[b] || __atomic_load_n(m->host_done + 1 + b, __ATOMIC_ACQUIRE);
         if (all) break;
+        const int n = std::min(gs, max_tokens - issued);
+        if ((rc = run_batch(m, n))) return rc;
+        issued += n;
+        if ((int)m->run_ev.size() <= k) {
+            hipEvent_t e = nullptr;
+            MIO_HIP_CHECK(hipEventCreate(&e));
+            m->run_ev.push_back(e);
+        }
+        MIO_HIP_CHECK(hipEventRecord(m->run_ev[k], s));
     }
+    std::vector<mio::StepState> hs(B);
+    MIO_HIP_CHECK(hipMemcpyAsync(hs.data(), bt.st, B * sizeof(mio::StepState), hipMemcpyDeviceToHost, s));
+    MIO_HIP_CHECK(hipStreamSynchronize(s));
     std::vector<int32_t> ring(max_tokens);
     for (int b = 0; b < B; ++b) {
         const int P = prompt_lens[b] - 1;
@@ -1379,8 +1461,9 @@ static int kernel_layer(const mio_hip_llm *m, int which) {
     for (int i = 0; i < m->n_layer; ++i) {
         const int il = (m->n_layer / 2 + i) % m->n_layer;
         const bool conv = m->layers[il].conv != 0;
-        if (which == 11 ? !conv && fuse_layer_att(m, il)
-                        : (which <= 2 || which == 10 ? !conv : (which >= 8 ? conv : true)))
+        if (which == 11   ? !conv && fuse_layer_att(m, il)
+            : which == 12 ? fuse_ffn(m, il)
+                          : (which <= 2 || which == 10 ? !conv : (which >= 8 ? conv : true)))
             return il;
     }
     return -1;
@@ -1428,9 +1511,10 @@ struct DiagStateGuard {
 extern "C" int mio_hip_llm_time_kernel(mio_hip_llm *m, int which, int iters, float *avg_ms, uint64_t *bytes) {
     MIO_REQUIRE(m && avg_ms && bytes && iters > 0 && m->graph, MIO_ERR_INVALID,
                 "llm_time_kernel: run generate/eval first");
-    MIO_REQUIRE(which >= 0 && which <= 11 && which != 5 && which != 7, MIO_ERR_INVALID,
+    MIO_REQUIRE(which >= 0 && which <= 12 && which != 5 && which != 7, MIO_ERR_INVALID,
                 "llm_time_kernel: which %d", which);
-    MIO_REQUIRE(which < 10 || fuse_att_o(m), MIO_ERR_INVALID, "llm_time_kernel: no fused attention launch");
+    MIO_REQUIRE(which < 10 || which == 12 || fuse_att_o(m), MIO_ERR_INVALID,
+                "llm_time_kernel: no fused attention launch");
     const int il = kernel_layer(m, which);
     MIO_REQUIRE(il >= 0, MIO_ERR_INVALID, "llm_time_kernel: the model has no layer with kernel %d", which);
     int rc = mio::bind(m->d);
@@ -1466,6 +1550,11 @@ extern "C" int mio_hip_llm_time_kernel(mio_hip_llm *m, int which, int iters, flo
             break;
         case 3: b = qbytes(L.gate) + qbytes(L.up) + 4ull * (D.n_embd * 2 + D.n_ff); break;
         case 4: b = qbytes(L.down) + 4ull * (D.n_ff + 2 * D.n_embd); break;
+        // h written and read back by the down workgroups: counted once each way
+        case 12:
+            b = qbytes(L.gate) + qbytes(L.up) + 4ull * (D.n_embd * 2 + D.n_ff) + qbytes(L.down) +
+                4ull * (D.n_ff + 2 * D.n_embd);
+            break;
         case 6: b = qbytes(m->lm) + 4ull * D.n_vocab; break;
         case 8: b = qbytes(L.in_proj) + 4ull * D.n_embd * 4; break;
         // B | C | X in, taps, the two window rows, this position's bx (one workgroup), x in / out

@@ -27,6 +27,10 @@ struct SamplingParams {
 int llm_begin(mio_hip_llm *m, const int32_t *prompt, int n_prompt, int max_new,
               const SamplingParams &sp);
 int llm_run(mio_hip_llm *m, int n_steps);
+// Every remaining step, stopping (at step-graph granularity) once the device has flagged an
+// end token to the host; then the flush sampler and a snapshot for llm_poll.
+int llm_run_to_end(mio_hip_llm *m);
+int llm_graph_steps();
 // Copies generated tokens [0, *n_out) and reports whether an end token was sampled.
 int llm_poll(mio_hip_llm *m, std::vector<int32_t> &out, bool *done);
 LlmInfo llm_info(const mio_hip_llm *m);

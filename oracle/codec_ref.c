@@ -470,8 +470,11 @@ static void resnet_block(const mo_codec *c, const char *prefix, float *x, int L,
 
 /* Runs the decoder up to `stop_stage` (see mio_oracle.h) and copies that stage's
  * activation into out. Returns 0 on success. */
-int mo_codec_decode_stage(mo_codec *c, const int *codes, int T, const float *emb, int stop_stage,
-                          float *out, int *out_rows, int *out_cols) {
+/* start_stage > 0 (teacher forcing, tests only): the stages from start_stage on run on `in`, the
+ * output of stage start_stage - 1 (its rows x cols as mo_codec_decode_stage returns them), in
+ * place of the stages before it; codes still give T. */
+static int decode_stages(mo_codec *c, const int *codes, int T, const float *emb, int start_stage, const float *in,
+                         int stop_stage, float *out, int *out_rows, int *out_cols) {
     if (T <= 0) return -1;
     for (int i = 0; i < T; i++)
         if (codes[i] < 0 || codes[i] >= c->n_codes) return -2;
@@ -513,6 +516,42 @@ int mo_codec_decode_stage(mo_codec *c, const int *codes, int T, const float *emb
         stage++;                                                                   \
     } while (0)
 
+    int L = S, C = Dd, s_up0 = 0;
+    if (start_stage > 0) {
+        /* shape of stage start_stage - 1's output, then jump to stage start_stage */
+        if (start_stage > mo_codec_n_stages(c) - 1) goto finish;
+        int r = T, cc = Dp;
+        if (start_stage >= 2) r = T, cc = Dd;
+        if (start_stage >= 3) r = S, cc = Dd;
+        if (start_stage >= 7) {
+            s_up0 = start_stage - 6;
+            if (s_up0 > c->up_stages) s_up0 = c->up_stages;
+            for (int s = 0; s < s_up0; s++) {
+                const int K = c->kernels[s], fac = c->factors[s], trim = (K - fac) / 2;
+                snprintf(n, sizeof n, "wave_upsampler.up.%d.weight", s);
+                L = (L - 1) * fac + K - 2 * (trim > 0 ? trim : 0);
+                C = WN(c, n, 1);
+            }
+            r = L, cc = C;
+        }
+        memcpy(x, in, sizeof(float) * (size_t)r * cc);
+        stage = start_stage;
+        switch (start_stage) {
+            case 1: goto st_prenet;
+            case 2: goto st_upsample;
+            case 3: goto st_prior;
+            case 4: goto st_decoder;
+            case 5: goto st_post;
+            default: break;
+        }
+        if (start_stage == 7 + c->up_stages) {
+            memcpy(h, in, sizeof(float) * (size_t)L * Dd);
+            goto st_head;
+        }
+        if (start_stage == 6 + c->up_stages) goto st_outproj;
+        goto st_up;
+    }
+
     /* 1. token embedding (:599-600) */
     {
         const float *emb_tbl = W(c, "token_embd");
@@ -521,6 +560,7 @@ int mo_codec_decode_stage(mo_codec *c, const int *codes, int T, const float *emb
     DONE(x, T, Dp);
 
     /* 2. prenet (:604-618) */
+st_prenet:
     {
         const int H = c->pre_heads, hd = Dp / H;
         for (int i = 0; i < c->pre_layers; i++) {
@@ -549,12 +589,14 @@ int mo_codec_decode_stage(mo_codec *c, const int *codes, int T, const float *emb
     DONE(x, T, Dd);
 
     /* 3. wave_upsample ConvT k=2 s=2 (:622-626) */
+st_upsample:
     conv_transpose1d(x, T, Dd, WR(c, "wave_upsample.weight"), WN(c, "wave_upsample.weight", 0), Dd,
                      2, 0, W(c, "wave_upsample.bias"), h);
     memcpy(x, h, sizeof(float) * (size_t)S * Dd);
     DONE(x, S, Dd);
 
     /* 4. wave_prior ResNets (:629-637) */
+st_prior:
     for (int blk = 0; blk < c->res_blocks; blk++) {
         char p[64];
         snprintf(p, sizeof p, "wave_prior.%d.", blk);
@@ -563,6 +605,7 @@ int mo_codec_decode_stage(mo_codec *c, const int *codes, int T, const float *emb
     DONE(x, S, Dd);
 
     /* 5. AdaLN-Zero decoder (:640-660) */
+st_decoder:
     {
         const int H = c->dec_heads, hd = Dd / H, A = c->adaln;
         float *se = (float *)malloc(sizeof(float) * A);
@@ -609,6 +652,7 @@ int mo_codec_decode_stage(mo_codec *c, const int *codes, int T, const float *emb
     DONE(x, S, Dd);
 
     /* 6. wave_post ResNets (:663-672) */
+st_post:
     for (int blk = 0; blk < c->res_blocks; blk++) {
         char p[64];
         snprintf(p, sizeof p, "wave_post.%d.", blk);
@@ -617,8 +661,8 @@ int mo_codec_decode_stage(mo_codec *c, const int *codes, int T, const float *emb
     DONE(x, S, Dd);
 
     /* 7. upsampler stages (:677-708) */
-    int L = S, C = Dd;
-    for (int s = 0; s < c->up_stages; s++) {
+st_up:
+    for (int s = s_up0; s < c->up_stages; s++) {
         const int fac = c->factors[s], K = c->kernels[s], trim = (K - fac) / 2;
         snprintf(n, sizeof n, "wave_upsampler.up.%d.weight", s);
         const int Cout = WN(c, n, 1);
@@ -639,12 +683,14 @@ int mo_codec_decode_stage(mo_codec *c, const int *codes, int T, const float *emb
     }
 
     /* 8. out_proj + out_snake (:711-725) */
+st_outproj:
     linear(x, L, C, WR(c, "wave_upsampler.out_proj.weight"), W(c, "wave_upsampler.out_proj.bias"), Dd, h);
     snake_rows(h, L, Dd, W(c, "wave_upsampler.out_snake.alpha"), W(c, "wave_upsampler.out_snake.beta"),
                is_f16(c, "wave_upsampler.out_snake.alpha"), is_f16(c, "wave_upsampler.out_snake.beta"));
     DONE(h, L, Dd);
 
     /* 9. iSTFT head (:728-737) + interleave (:801-808) */
+st_head:
     {
         const int nf = c->n_freq;
         linear(h, L, Dd, WR(c, "istft_head.out.weight"), W(c, "istft_head.out.bias"), c->head_out, a);
@@ -670,6 +716,17 @@ finish:
 }
 
 int mo_codec_n_stages(const mo_codec *c) { return 8 + c->up_stages; }
+
+int mo_codec_decode_stage(mo_codec *c, const int *codes, int T, const float *emb, int stop_stage, float *out,
+                          int *out_rows, int *out_cols) {
+    return decode_stages(c, codes, T, emb, 0, NULL, stop_stage, out, out_rows, out_cols);
+}
+
+int mo_codec_stage_from(mo_codec *c, const int *codes, int T, const float *emb, int start_stage, const float *in,
+                        int stop_stage, float *out, int *out_rows, int *out_cols) {
+    if (start_stage < 1 || stop_stage < start_stage) return -4;
+    return decode_stages(c, codes, T, emb, start_stage, in, stop_stage, out, out_rows, out_cols);
+}
 
 /* Full decode -> spectrogram [S_final][n_freq][2]; returns S_final or < 0 on error. */
 int mo_codec_decode(mo_codec *c, const int *codes, int T, const float *emb, float *spec) {

@@ -44,6 +44,10 @@ int mo_codec_n_stages(const mo_codec *c);
 int mo_codec_decode_stage(mo_codec *c, const int *codes, int T, const float *emb, int stop_stage,
                           float *out, int *out_rows, int *out_cols);
 int mo_codec_decode(mo_codec *c, const int *codes, int T, const float *emb, float *spec);
+/* Teacher forcing (tests): stages start_stage .. stop_stage run on `in`, the output of stage
+ * start_stage - 1 (e.g. the GPU's), instead of on the oracle's own earlier stages. */
+int mo_codec_stage_from(mo_codec *c, const int *codes, int T, const float *emb, int start_stage, const float *in,
+                        int stop_stage, float *out, int *out_rows, int *out_cols);
 float mo_f16_round(float f);
 
 /* ---- streaming emission (test-to-speech.cpp:367-417,496-571), stream_ref.c ---- */

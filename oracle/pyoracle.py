@@ -139,6 +139,24 @@ class Codec:
             raise RuntimeError(f"oracle stage {stage} failed: {rc}")
         return out[: r.value * c.value].reshape(r.value, c.value)
 
+    def stage_from(self, codes, emb, start: int, x_in, stop: int, max_elems: int) -> np.ndarray:
+        """Teacher forcing: stages start .. stop run on x_in (the output of stage start - 1,
+        e.g. the GPU's) instead of on the oracle's own earlier stages."""
+        codes = np.ascontiguousarray(codes, dtype=np.int32)
+        emb = np.ascontiguousarray(emb, dtype=np.float32)
+        x_in = np.ascontiguousarray(x_in, dtype=np.float32)
+        out = np.zeros(max_elems, np.float32)
+        r, c = ctypes.c_int(0), ctypes.c_int(0)
+        o = oracle()
+        o.mo_codec_stage_from.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
+                                          ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int),
+                                          ctypes.POINTER(ctypes.c_int)]
+        rc = o.mo_codec_stage_from(self.h, codes.ctypes.data, len(codes), emb.ctypes.data, start, x_in.ctypes.data,
+                                   stop, out.ctypes.data, ctypes.byref(r), ctypes.byref(c))
+        if rc != 0:
+            raise RuntimeError(f"oracle stages {start}..{stop} failed: {rc}")
+        return out[: r.value * c.value].reshape(r.value, c.value)
+
     def decode_pcm(self, codes, emb) -> np.ndarray:
         spec = self.decode(codes, emb)
         return istft(spec, self.n_fft, self.n_fft, self.hop_length)

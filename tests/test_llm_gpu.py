@@ -132,10 +132,11 @@ def test_generate_stops_at_eos(device, llm_files):
     toks = g.generate(prompt, 200, 2.0, 7, allow=(m.SYNTH_EOT, m.SYNTH_SPEECH0 + 3),
                       eos=(m.SYNTH_EOT, m.SYNTH_IM_END), check_interval=20)
     assert len(toks) < 200 and (toks != m.SYNTH_EOT).all()
-    # steps past the end token: the rest of its check interval plus the one interval queued
-    # ahead of the poll that found it
+    # steps past the end token: the sampler stores it to the host's mapped word, the host stops
+    # issuing step graphs (8 steps each, at most 2 queued ahead): the rest of the end token's
+    # graph plus at most one more
     wasted = g.steps_issued() - len(toks) - 1
-    assert 0 <= wasted < 2 * 20, wasted
+    assert 0 <= wasted <= 2 * 8 - 1, wasted
     assert g.tail()[0] == wasted
     # a run that stops at max_tokens issues exactly max_tokens steps
     toks = g.generate(prompt, 50, 0.8, 7, allow=(m.SYNTH_SPEECH0, m.SYNTH_SPEECH0 + 3), check_interval=20)
@@ -154,7 +155,10 @@ def test_steps_after_eos_return_at_entry(device, synth_llm_path, preset):
                       eos=(m.SYNTH_EOT, m.SYNTH_IM_END), check_interval=20)
     assert len(toks) < 20, len(toks)  # 1 in 4 allowed ids ends the run
     wasted, timed, ms = g.tail()
-    assert wasted == g.steps_issued() - len(toks) - 1 and timed == 20, (wasted, timed)
+    # timed: the step graphs queued after the one that sampled the end token (0 or 8 steps)
+    assert wasted == g.steps_issued() - len(toks) - 1 and wasted <= 15 and timed in (0, 8), (wasted, timed)
+    if not timed:
+        pytest.skip("the host saw the end token before queueing another graph: no step to time")
     us_per_launch = ms * 1e3 / timed / len(g.step_kinds())
     print(f"preset {preset}: {wasted} steps after the end token, {ms * 1e3 / timed:.1f} us per step "
           f"({us_per_launch:.2f} us per launch)")
@@ -410,16 +414,17 @@ toks = g.generate(prompt, 80, 0.8, 5, allow=(m.SYNTH_SPEECH0, m.SYNTH_SPEECH0 + 
 h = hashlib.sha256(toks.tobytes())
 for pos in (3, 70, 129):
     h.update(g.eval(int(toks[0]), pos).tobytes())
-print(g.step_kinds().count(11), g.step_kinds().count(10), h.hexdigest())
+print(g.step_kinds().count(11), g.step_kinds().count(10), g.step_kinds().count(12), h.hexdigest())
 """
 
 
-@pytest.mark.parametrize("preset", [2, 3])
+@pytest.mark.parametrize("preset", [2, 3, 4])
 def test_fused_attention_launches_bit_identical(synth_llm_path, tmp_path, preset):
     """The attention block as one launch (k_layer_att, layers >= 1), attention + O as one
-    launch (k_att_o) and the three separate launches run the same arithmetic: 80 free-run
-    tokens and the logits of three later evaluations are bit-identical across
-    MIO_LAYER_ATT / MIO_ATT_FUSE_O (each variant is a fresh process: the switches are read once)."""
+    launch (k_att_o) and the three separate launches run the same arithmetic, and so do the
+    FFN pair as one launch (k_ffn, r06) and k_ffn_in + k_ffn_down: 80 free-run tokens and the
+    logits of three later evaluations are bit-identical across MIO_LAYER_ATT / MIO_ATT_FUSE_O /
+    MIO_FFN_FUSE (each variant is a fresh process: the switches are read once)."""
     import os
     import subprocess
     import sys
@@ -429,12 +434,13 @@ def test_fused_attention_launches_bit_identical(synth_llm_path, tmp_path, preset
     pkg = os.path.dirname(os.path.dirname(m.__file__))
     outs = {}
     for name, env in (("layer_att", {"MIO_LAYER_ATT": "1"}), ("att_o", {"MIO_LAYER_ATT": "0"}),
-                      ("separate", {"MIO_ATT_FUSE_O": "0"})):
+                      ("separate", {"MIO_ATT_FUSE_O": "0", "MIO_FFN_FUSE": "0"})):
         p = subprocess.run([sys.executable, str(script), path, pkg], capture_output=True, text=True, timeout=240,
                            env=dict(os.environ, **env))
         assert p.returncode == 0, p.stderr[-2000:]
         outs[name] = p.stdout.split()
     assert int(outs["layer_att"][0]) > 0 and int(outs["att_o"][0]) == 0 and int(outs["att_o"][1]) > 0
-    assert int(outs["separate"][0]) == int(outs["separate"][1]) == 0
+    assert int(outs["separate"][0]) == int(outs["separate"][1]) == int(outs["separate"][2]) == 0
+    assert int(outs["layer_att"][2]) > 0  # the FFN pairs ran fused
     print(outs)
-    assert outs["layer_att"][2] == outs["att_o"][2] == outs["separate"][2], outs
+    assert outs["layer_att"][3] == outs["att_o"][3] == outs["separate"][3], outs
