@@ -25,7 +25,7 @@ llm.generate([256, 257, 65, 258, 257], a.pos, 0.8, 1, allow=(m.SYNTH_SPEECH0, m.
 t = llm.timeline()
 nl = t.shape[0]
 KN = {0: "attn_in", 1: "attention", 2: "attn_out", 3: "ffn_in", 4: "ffn_down", 6: "lm_head", 8: "conv_in",
-      9: "conv_out", 10: "att_o", 11: "layer_att"}
+      9: "conv_out", 10: "att_o", 11: "layer_att", 12: "ffn"}
 names = [KN[k] for k in llm.step_kinds()]
 s0 = np.nanmin(t[:, :, 0], axis=1)
 s1 = np.nanmax(t[:, :, 0], axis=1)
@@ -42,14 +42,14 @@ gap = np.r_[0.0, s0[1:] - e1[:-1]]
 print(f"step wall {e1[-1] - s0[0]:.1f} us over {nl} launches; kernel time {dur.sum():.1f} us, "
       f"gaps {gap[1:].sum():.1f} us (mean {gap[1:].mean():.2f}, min {gap[1:].min():.2f}, max {gap[1:].max():.2f})")
 print("  kernel      dur    gap-before  start-spread  end-spread  median-wg   wg:->m1  m1->m2  m2->end  last-m2")
-for k in ["attn_in", "attention", "attn_out", "ffn_in", "ffn_down", "lm_head"]:
+for k in ["attn_in", "attention", "attn_out", "layer_att", "ffn_in", "ffn_down", "ffn", "lm_head"]:
     idx = [i for i, n in enumerate(names) if n == k]
     print(f"  {k:10s} {dur[idx].mean():6.2f} {gap[idx].mean():8.2f} {(s1 - s0)[idx].mean():12.2f} "
           f"{(e1 - e0)[idx].mean():11.2f} {wd[idx].mean():10.2f} {np.nanmean(ph1[idx]):9.2f} "
           f"{np.nanmean(ph2[idx]):7.2f} {np.nanmean(ph3[idx]):8.2f} {np.nanmean(m2[idx]):8.2f}")
 # every recorded mark (1-6) and the end, as median offsets from the workgroup's own start
 print("  kernel      " + " ".join(f"{'m' + str(k):>6s}" for k in range(1, 7)) + "    end   (us after workgroup start)")
-for k in ["attn_in", "attention", "attn_out", "ffn_in", "ffn_down", "lm_head"]:
+for k in ["attn_in", "attention", "attn_out", "layer_att", "ffn_in", "ffn_down", "ffn", "lm_head"]:
     idx = [i for i, n in enumerate(names) if n == k]
     cols = []
     for j in list(range(1, 7)) + [7]:
@@ -101,3 +101,27 @@ if il:
     print(f"  layer_att mergers ({int(mg[0].sum())}): ticket {med(T[:, :, 5] - base, mg):.2f}, outputs written "
           f"{med(T[:, :, 6] - base, mg):.2f}, end {med(T[:, :, 7] - base, mg):.2f}; chunk compute done (m2->end "
           f"of non-mergers) {med(T[:, :, 7] - base, isA & ~mg):.2f} (last {lastv(T[:, :, 7] - base, isA & ~mg):.2f})")
+# the FFN pair in one launch: gate|up producers (no mark 3), down workgroups (mark 3 = their
+# wait for h is over, mark 1 = h loaded, mark 2 = h quantized)
+jf = [i for i, n in enumerate(names) if n == "ffn"]
+if jf:
+    T = t[jf]
+    base = s0[jf][:, None]
+    isD = np.isfinite(T[:, :, 3])
+    isP = np.isfinite(T[:, :, 7]) & ~isD
+
+    def med(x, msk):
+        return float(np.nanmedian(np.where(msk, x, np.nan)))
+
+    def lastv(x, msk):
+        return float(np.nanmedian(np.nanmax(np.where(msk, x, np.nan), axis=1)))
+
+    def firstv(x, msk):
+        return -lastv(-x, msk)
+    print(f"  ffn: {int(isP[0].sum())} gate|up producers: start {med(T[:, :, 0] - base, isP):.2f} (last "
+          f"{lastv(T[:, :, 0] - base, isP):.2f}), quantized {med(T[:, :, 2] - base, isP):.2f}, end "
+          f"{med(T[:, :, 7] - base, isP):.2f} (last {lastv(T[:, :, 7] - base, isP):.2f}); {int(isD[0].sum())} down: "
+          f"start {med(T[:, :, 0] - base, isD):.2f} (last {lastv(T[:, :, 0] - base, isD):.2f}), wait done "
+          f"{med(T[:, :, 3] - base, isD):.2f} (first {firstv(T[:, :, 3] - base, isD):.2f}), h in "
+          f"{med(T[:, :, 1] - base, isD):.2f}, quantized {med(T[:, :, 2] - base, isD):.2f}, end "
+          f"{med(T[:, :, 7] - base, isD):.2f} (last {lastv(T[:, :, 7] - base, isD):.2f}) us after the launch's first start")
