@@ -47,7 +47,7 @@ sys.path.insert(0, os.path.join(REPO, "miotts-llama.cpp_amd", "python"))
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 ROOF_POS = 400  # decode position of the roofline timeline / kernel timings (and of the PMC run)
 KERNEL_NAMES = {0: "k_attn_in", 1: "k_attention", 2: "k_attn_out", 3: "k_ffn_in", 4: "k_ffn_down",
-                6: "k_lm_head", 8: "k_conv_in", 9: "k_conv_out", 10: "k_att_o", 11: "k_layer_att", 12: "k_ffn"}
+                6: "k_lm_head", 8: "k_conv_in", 9: "k_conv_out", 10: "k_att_o", 11: "k_layer_att", 12: "k_ffn", 13: "k_layer"}
 PRESETS = {2: "MioTTS-0.1B Q8_0", 3: "MioTTS-1.7B Q4_K_M", 4: "MioTTS-2.6B Q8_0",
            6: "MioTTS-2.6B Q8_0 (LFM2 shape: 22 short-conv + 8 attention layers)", 12: "MioTTS-1.7B BF16"}
 PROMPT = "こんにちは、今日はいい天気ですね。"  # README.md:83, SURVEY 8(d)
@@ -320,7 +320,7 @@ def roofline(llm, preset):
     step = llm.step_kinds()
     assert len(step) == nl, (len(step), nl)
     names = [KERNEL_NAMES[k] for k in step]
-    fused = 10 in step or 11 in step
+    fused = 10 in step or 11 in step or 13 in step
     dur = np.nanmax(tl[:, :, 7], axis=1) - np.nanmin(tl[:, :, 0], axis=1)
     step_wall_us = float(np.nanmax(tl[-1, :, 7]) - np.nanmin(tl[0, :, 0]))
     per_kernel = {}
@@ -360,8 +360,9 @@ def roofline(llm, preset):
             "note": ("timeline, events and attention bytes at decode position ~400 (as the PMC run)"
                      + ("; k_att_o = attention + O projection in one launch (layer 0; bytes: K/V rows, q|k|v, "
                         "chunk records, W_o, x), k_layer_att = RMSNorm + q|k|v + attention + O in one launch "
-                        "(layers >= 1; + W_q|k|v); their event times exclude the counter reset a step's k_ffn_in "
-                        "does" if fused else ""))}
+                        "(layers >= 1; + W_q|k|v), k_layer = k_layer_att + the FFN pair in one launch (layers >= 1; "
+                        "+ W_gate|up, W_down, h); their event times exclude the counter reset a step's next "
+                        "launch does" if fused else ""))}
 
 
 F32_MFMA_PEAK_TFS = 157.3  # MI355X_MICROARCH.md: f32 matrix (and vector) peak, exact f32

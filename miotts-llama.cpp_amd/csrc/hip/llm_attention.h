@@ -155,7 +155,42 @@ __device__ __forceinline__ bool attention_wg(const LlmDims &d, const float *q_no
 // order: every producer has a lower workgroup index than every consumer and never waits, so
 // it is dispatched (and finishes) whatever the residency. The counter is zeroed by the next
 // launch, k_ffn_in (kernel boundary ordered), and by reset_tickets.
-template <int NP, int T, int SU, bool DG>
+// Two-level arrival counter of an in-launch hand-off with n signalling workgroups (r = the
+// signaller's index among them; first wave, after every wave's stores drained and a workgroup
+// barrier): one add to arrival shard r % 8 (<= n / 8 adds per word); the workgroup whose add
+// returns its shard's last count adds 1 to each of the 8 ready replicas (one instruction, 8
+// lanes), where a consumer polls replica r' % 8 until min(n, 8) (MI355X_MICROARCH hand-off
+// rows 1-2; k_ffn's h counter).
+__device__ __forceinline__ void signal_two_level(int *arr, int *rdy, int r, int n) {
+    if (MIO_TIDX < 64) {
+        int last = 0;
+        if (MIO_TIDX == 0) {
+            const int sh = r & (kFfnShards - 1), n_sh = (n - sh + kFfnShards - 1) / kFfnShards;
+            last = __hip_atomic_fetch_add((__attribute__((address_space(1))) int *)(arr + kFfnStride * sh), 1,
+                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == n_sh - 1;
+        }
+        if (__builtin_amdgcn_readfirstlane(last) && MIO_TIDX < kFfnShards)
+            __hip_atomic_fetch_add((__attribute__((address_space(1))) int *)(rdy + kFfnStride * MIO_TIDX), 1,
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+__device__ __forceinline__ void wait_two_level(int *rdy, int r, int n, int *flag) {
+    if (MIO_TIDX == 0) wait_count(rdy + kFfnStride * (r & (kFfnShards - 1)), min(n, kFfnShards), flag);
+    asm volatile("s_barrier" ::: "memory");
+}
+
+// residual rows [lo, hi) of this wave, lane i holding x[lo + i], by sc1 loads (x was stored
+// write-through by other workgroups of the launch); lanes past hi read 0 (out of range)
+__device__ __forceinline__ float load_resid_sc1(const float *x, int lo, int hi) {
+    const int lane = threadIdx.x & 63;
+    return __uint_as_float(
+        __builtin_amdgcn_raw_buffer_load_b32(rsrc(x, (uint32_t)hi * 4u), (uint32_t)(lo + lane) * 4u, 0, 16));
+}
+
+// XS (the whole-layer launch, k_layer): the x rows are stored write-through and, once every
+// wave's stores drained, the workgroup signals the two-level x counter (kXOff / kXRdy of
+// b.att_cnt) for the launch's gate|up workgroups
+template <int NP, int T, int SU, bool DG, bool XS = false>
 __device__ __forceinline__ void o_consumer(const LlmDims &d, const QMat &wo, const LlmBuffers &b, int ob, int no) {
     constexpr bool kDiag = DG;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -178,8 +213,19 @@ __device__ __forceinline__ void o_consumer(const LlmDims &d, const QMat &wo, con
     MIO_TL_MARK(b, 2);
     stream_rows<T, NP, 1, SU, MIO_SMALL_AUX>(wo, wo, lo, hi, ga, gb, s.a, [&](int row, float v, float) {
         const float r = lane_value(xres, row - lo);
-        if ((threadIdx.x & 63) == 0) b.x[row] = v + r;
+        if ((threadIdx.x & 63) == 0) {
+            if constexpr (XS)
+                st1_sc1(b.x, (uint32_t)row * 4u, v + r);
+            else
+                b.x[row] = v + r;
+        }
     });
+    if constexpr (XS) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        MIO_TL_MARK(b, 6);  // x rows written through
+        signal_two_level(b.att_cnt + kXOff, b.att_cnt + kXRdy, ob, no);
+    }
 }
 
 }  // namespace

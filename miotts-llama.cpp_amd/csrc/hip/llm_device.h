@@ -41,7 +41,7 @@ constexpr bool kDiag = true;
 // mark 1, mark 2, diagnostic marks 3-6, end}, s_memrealtime ticks (100 MHz), plain stores to
 // slot [seq][wg][8] (wg < 512). Marks: matvec kernels 1 = weight loads issued, 2 = activations quantized;
 // attention 1 = K/V loads issued, 2 = heads prepared; sampler 1 = token chosen.
-#define MIO_TL_SLOT(bufs) ((bufs).tl + 8 * ((size_t)(bufs).seq * 1024 + ((blockIdx.x + blockIdx.y * gridDim.x) & 1023)))
+#define MIO_TL_SLOT(bufs) ((bufs).tl + 8 * ((size_t)(bufs).seq * kTlSlots + ((blockIdx.x + blockIdx.y * gridDim.x) & (kTlSlots - 1))))
 #define MIO_TL_AT(bufs, k)                                                                      \
     do {                                                                                        \
         if (kDiag && (bufs).tl && MIO_TIDX == 0) MIO_TL_SLOT(bufs)[k] = __builtin_amdgcn_s_memrealtime(); \

@@ -15,6 +15,8 @@ namespace mio {
 #define MIO_ATT_CHUNK 64
 #endif
 constexpr int kAttChunk = MIO_ATT_CHUNK;
+// step timeline (diagnostic): workgroup slots per launch (k_layer grids reach ~1,300)
+constexpr int kTlSlots = 2048;
 static_assert(kAttChunk == 32 || kAttChunk == 64 || kAttChunk == 128, "attention chunk");
 
 // One quantized matrix in the split layout (csrc/host/quant.h), rows x k.
@@ -181,7 +183,8 @@ void launch_batch_embed(const LlmDims &d, const QMat &tok_embd, const PrefillBuf
 // Launch one kernel of a decode step (which: 0 attn_in, 1 attention, 2 attn_out, 3 ffn_in,
 // 4 ffn_down of layer il; 6 lm_head, 7 sampler; lfm2 short-conv layers: 8 conv_in, 9
 // conv_out in place of 0..2; 10 attention + O (k_att_o, for 1 + 2), 11 the whole attention
-// block (k_layer_att, for 0 + 1 + 2)) on stream s.
+// block (k_layer_att, for 0 + 1 + 2), 12 the FFN pair (k_ffn, for 3 + 4), 13 the whole layer
+// (k_layer, for 11 + 12)) on stream s.
 void launch_step_kernel(int which, const LlmDims &d, const LayerW *layers, int il, _Float16 *kcache,
                         _Float16 *vcache, const float *out_norm, const QMat &lm, const QMat &tok_embd,
                         const LlmBuffers &b, hipStream_t s);
@@ -207,6 +210,14 @@ bool layer_att_supported(const LlmDims &d, const LayerW &L);
 bool ffn_fused_supported(const LlmDims &d, const LayerW &L);
 void launch_layer_att(const LlmDims &d, const LayerW &L, _Float16 *kc, _Float16 *vc, const LlmBuffers &b, bool dg,
                       hipStream_t s);
+// the whole decoder layer L (attention block + FFN pair) as one launch (k_layer, which = 13)
+// exists for its shapes and weight types; launch_layer runs it for layer il (counter set il & 1)
+bool layer_fused_supported(const LlmDims &d, const LayerW &L);
+void launch_layer(const LlmDims &d, const LayerW &L, int il, _Float16 *kc, _Float16 *vc, const LlmBuffers &b,
+                  bool dg, hipStream_t s);
+// MIO_LAYER_GATE (k_layer): 1 = the FFN workgroups issue their weights only once their kv head's
+// q|k|v rows are in (the producers' stream goes first), 0 = at dispatch
+int layer_ffn_gate();
 // k_att_o's merge counters in LlmBuffers.att_cnt: kRdyShards words kRdyStride ints (256 B)
 // apart from int kRdyOff on (one per XCD: an O workgroup polls shard blockIdx % 8, so no word
 // has more than 1/8 of the pollers; MI355X_MICROARCH "dequeue": one word saturates near 88
@@ -223,7 +234,16 @@ constexpr int kQkvOff = kRdyFlag + 64, kQkvStride = 64, kQkvMax = 64;
 // per word). Zeroed by the launch after k_ffn (the next layer's attn_in / layer_att, lm_head).
 constexpr int kFfnOff = kQkvOff + kQkvStride * kQkvMax, kFfnShards = 8, kFfnStride = 64;
 constexpr int kFfnRdy = kFfnOff + kFfnShards * kFfnStride;
-constexpr int kAttCntInts = kFfnRdy + kFfnShards * kFfnStride;
+// The whole-layer launch (k_layer, which = 13) hands the O projection's x rows to its gate|up
+// workgroups through one more two-level counter (arrival shards kXOff, ready replicas kXRdy),
+// laid out after the counters above. k_layer runs with LlmBuffers.att_cnt pointing at counter
+// SET il & 1 (kLaySet ints each, from kLayOff on; every offset above is the same inside a set):
+// each k_layer zeroes the other set at entry (used by the previous k_layer: kernel boundary), so
+// no counter of a set is reset while a launch may still poll it; lm_head zeroes both.
+constexpr int kXOff = kFfnRdy + kFfnShards * kFfnStride, kXRdy = kXOff + kFfnShards * kFfnStride;
+constexpr int kLaySet = kXRdy + kFfnShards * kFfnStride;
+constexpr int kLayOff = kLaySet;  // the plain counters occupy [0, kLaySet) too
+constexpr int kAttCntInts = kLayOff + 2 * kLaySet;
 int pick_np(int K);
 size_t matvec_lds(int K);
 // units (row passes) of the busiest wave of a matvec over `rows` rows on `grid` workgroups,

@@ -126,6 +126,20 @@ __device__ __forceinline__ void advance_state(StepState *st, const LlmDims &d) {
     st->pending = 0;
 }
 
+// Both k_layer counter sets (every counter but the timeout flag; the chunk tickets reset
+// themselves): lm_head, after the step's last k_layer (kernel boundary ordered).
+__device__ __forceinline__ void zero_layer_sets(int *cnt) {
+    constexpr int n = kRdyShards + kQkvMax + 4 * kFfnShards;
+    for (int i = MIO_TIDX; i < 2 * n; i += MT) {
+        const int j = i % n;
+        const int o = j < kRdyShards ? kRdyOff + kRdyStride * j
+                    : j < kRdyShards + kQkvMax ? kQkvOff + kQkvStride * (j - kRdyShards)
+                                               : kFfnOff + kFfnStride * (j - kRdyShards - kQkvMax);
+        __hip_atomic_store((__attribute__((address_space(1))) int *)(cnt + kLayOff + (i / n) * kLaySet + o), 0,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 template <int NP, int T, int SU, bool DG>
 __global__ __launch_bounds__(MT) void k_ffn_in(LlmDims d, const float *norm_w, QMat gate, QMat up,
                                                LlmBuffers b, int adv) {
@@ -356,6 +370,7 @@ __global__ __launch_bounds__(MT) void k_lm_head(LlmDims d, const float *norm_w, 
     if (blockIdx.x == 2 && MIO_TIDX < 2 * kFfnShards)  // the previous k_ffn's h counters (kernel boundary ordered)
         __hip_atomic_store((__attribute__((address_space(1))) int *)(b.att_cnt + kFfnOff + kFfnStride * MIO_TIDX), 0,
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (blockIdx.x == 3) zero_layer_sets(b.att_cnt);  // the k_layer counter sets (the last layer's is in use)
     const Smem s = carve(smem, K);
     XRegs<NP> xr;
     load_x(b.x, norm_w, K, xr);
@@ -668,6 +683,9 @@ void launch_step_kernel(int which, const LlmDims &d, const LayerW *layers, int i
         }
         case 12:  // the FFN pair in one launch (k_ffn)
             launch_ffn<DG>(d, layers[il], b, il == 0 ? 1 : 0, s, false);
+            break;
+        case 13:  // the whole layer in one launch (k_layer, layers >= 1)
+            launch_layer(d, layers[il], il, kcache + il * layer_kv, vcache + il * layer_kv, b, DG, s);
             break;
         case 8: {  // lfm2 conv_in: RMSNorm + in_proj as the attn_in launch (B | C rows, X rows)
             const LayerW &L = layers[il];

@@ -292,11 +292,16 @@ int check_handoff(mio_hip_llm *m) {
     for (int il = 0; il < m->n_layer && !any; ++il) any = fuse_ffn(m, il);
     if (!any) return MIO_OK;
     int flag = 0;
-    int *f = m->buf.att_cnt + mio::kRdyFlag;
-    MIO_HIP_CHECK(hipMemcpyAsync(&flag, f, sizeof(int), hipMemcpyDeviceToHost, m->d->stream));
+    // the plain counters' flag and the two k_layer counter sets' (each set has its own)
+    int *f[3] = {m->buf.att_cnt + mio::kRdyFlag, m->buf.att_cnt + mio::kLayOff + mio::kRdyFlag,
+                 m->buf.att_cnt + mio::kLayOff + mio::kLaySet + mio::kRdyFlag};
+    int fl[3] = {0, 0, 0};
+    for (int i = 0; i < 3; ++i)
+        MIO_HIP_CHECK(hipMemcpyAsync(&fl[i], f[i], sizeof(int), hipMemcpyDeviceToHost, m->d->stream));
     MIO_HIP_CHECK(hipStreamSynchronize(m->d->stream));
+    flag = fl[0] | fl[1] | fl[2];
     if (flag) {
-        MIO_HIP_CHECK(hipMemsetAsync(f, 0, sizeof(int), m->d->stream));
+        for (int i = 0; i < 3; ++i) MIO_HIP_CHECK(hipMemsetAsync(f[i], 0, sizeof(int), m->d->stream));
         mio::set_error("llm decode: an in-launch hand-off wait (attention -> O, or gate|up -> down) timed out");
         return MIO_ERR_HIP;
     }
@@ -327,8 +332,22 @@ bool fuse_ffn(const mio_hip_llm *m, int il) {
     return env && mio::ffn_fused_supported(m->dims, m->layers[il]);
 }
 
+// MIO_LAYER_FUSE (default 0, A/B): 1 = a layer whose attention block runs as k_layer_att and
+// whose FFN pair runs as k_ffn runs both as ONE launch (k_layer, which = 13) where that is
+// instantiated (layer_fused_supported). Bit-identical, but slower on the box (r06, 1.7B Q4_K_M:
+// 0.800-0.812 vs 0.726-0.729 ms per token, profiles/r06/layer_fuse_ab.txt): the in-launch x and
+// h hand-offs cost what the boundaries did, and the FFN weight burst slows the attention chain.
+bool fuse_layer(const mio_hip_llm *m, int il) {
+    static const bool env = getenv("MIO_LAYER_FUSE") && getenv("MIO_LAYER_FUSE")[0] == '1';
+    return env && fuse_layer_att(m, il) && fuse_ffn(m, il) && mio::layer_fused_supported(m->dims, m->layers[il]);
+}
+
 int layer_kinds(const mio_hip_llm *m, int il, int *w) {
     int n = 0;
+    if (!m->layers[il].conv && fuse_layer(m, il)) {
+        w[n++] = 13;
+        return n;
+    }
     if (m->layers[il].conv) {
         w[n++] = 8, w[n++] = 9;
     } else if (fuse_layer_att(m, il)) {
@@ -1463,6 +1482,7 @@ static int kernel_layer(const mio_hip_llm *m, int which) {
         const bool conv = m->layers[il].conv != 0;
         if (which == 11   ? !conv && fuse_layer_att(m, il)
             : which == 12 ? fuse_ffn(m, il)
+            : which == 13 ? !conv && fuse_layer(m, il)
                           : (which <= 2 || which == 10 ? !conv : (which >= 8 ? conv : true)))
             return il;
     }
@@ -1511,7 +1531,7 @@ struct DiagStateGuard {
 extern "C" int mio_hip_llm_time_kernel(mio_hip_llm *m, int which, int iters, float *avg_ms, uint64_t *bytes) {
     MIO_REQUIRE(m && avg_ms && bytes && iters > 0 && m->graph, MIO_ERR_INVALID,
                 "llm_time_kernel: run generate/eval first");
-    MIO_REQUIRE(which >= 0 && which <= 12 && which != 5 && which != 7, MIO_ERR_INVALID,
+    MIO_REQUIRE(which >= 0 && which <= 13 && which != 5 && which != 7, MIO_ERR_INVALID,
                 "llm_time_kernel: which %d", which);
     MIO_REQUIRE(which < 10 || which == 12 || fuse_att_o(m), MIO_ERR_INVALID,
                 "llm_time_kernel: no fused attention launch");
@@ -1550,6 +1570,13 @@ extern "C" int mio_hip_llm_time_kernel(mio_hip_llm *m, int which, int iters, flo
             break;
         case 3: b = qbytes(L.gate) + qbytes(L.up) + 4ull * (D.n_embd * 2 + D.n_ff); break;
         case 4: b = qbytes(L.down) + 4ull * (D.n_ff + 2 * D.n_embd); break;
+        // the whole layer: k_layer_att's bytes + k_ffn's (x handed over in-launch: counted once
+        // each way like q|k|v and h)
+        case 13:
+            b = qbytes(L.wq) + qbytes(L.wk) + qbytes(L.wv) + 4ull * D.n_embd + att_bytes + qbytes(L.wo) +
+                4ull * D.n_head * D.hd + 4ull * D.n_embd * 2 + qbytes(L.gate) + qbytes(L.up) +
+                4ull * (D.n_embd * 2 + D.n_ff) + qbytes(L.down) + 4ull * (D.n_ff + 2 * D.n_embd);
+            break;
         // h written and read back by the down workgroups: counted once each way
         case 12:
             b = qbytes(L.gate) + qbytes(L.up) + 4ull * (D.n_embd * 2 + D.n_ff) + qbytes(L.down) +
@@ -1602,7 +1629,7 @@ extern "C" int mio_hip_llm_time_kernel(mio_hip_llm *m, int which, int iters, flo
 // checkpoints 0 and 15 in out[16] / out[31]. Diagnostic only.
 extern "C" int mio_hip_llm_trace_kernel(mio_hip_llm *m, int which, uint64_t *out) {
     MIO_REQUIRE(m && out && m->graph, MIO_ERR_INVALID, "llm_trace_kernel: run generate/eval first");
-    MIO_REQUIRE(which >= 0 && which <= 11 && which != 5, MIO_ERR_INVALID, "llm_trace_kernel: which %d", which);
+    MIO_REQUIRE(which >= 0 && which <= 13 && which != 5, MIO_ERR_INVALID, "llm_trace_kernel: which %d", which);
     MIO_REQUIRE(which < 10 || fuse_att_o(m), MIO_ERR_INVALID, "llm_trace_kernel: no fused attention launch");
     const int il = kernel_layer(m, which);
     MIO_REQUIRE(il >= 0, MIO_ERR_INVALID, "llm_trace_kernel: the model has no layer with kernel %d", which);
@@ -1650,7 +1677,7 @@ extern "C" int mio_hip_llm_timeline(mio_hip_llm *m, uint64_t *out, int max_launc
     const int nl = (int)step_kinds(m).size();
     MIO_REQUIRE(max_launches >= nl, MIO_ERR_INVALID, "llm_timeline: need %d launch slots", nl);
     hipStream_t s = m->d->stream;
-    const size_t nslot = (size_t)nl * 1024 * 8;  // MIO_TL_SLOT: 1024 workgroup slots per launch
+    const size_t nslot = (size_t)nl * mio::kTlSlots * 8;  // MIO_TL_SLOT: kTlSlots workgroup slots per launch
     unsigned long long *tl = nullptr;
     MIO_HIP_CHECK(hipMalloc(&tl, sizeof(unsigned long long) * nslot));
     hipGraph_t g = nullptr;

@@ -503,10 +503,11 @@ class Llm:
         """Per-launch, per-workgroup [start, marks 1-6, end] (us from the step start, NaN =
         absent) of one graph-replayed step (diagnostic, mio_hip_llm_timeline; advances the
         decode state). Marks: see MIO_TL_MARK in csrc/hip/llm_device.h."""
-        out = np.zeros(512 * 1024 * 8, np.uint64)
+        slots = 2048  # kTlSlots (csrc/hip/llm_kernels.h): workgroup slots per launch
+        out = np.zeros(256 * slots * 8, np.uint64)
         n = ctypes.c_int(0)
-        check(lib().mio_hip_llm_timeline(self.h, _ptr(out), 512, ctypes.byref(n)))
-        t = out[: n.value * 8192].astype(np.float64).reshape(n.value, 1024, 8)
+        check(lib().mio_hip_llm_timeline(self.h, _ptr(out), 256, ctypes.byref(n)))
+        t = out[: n.value * slots * 8].astype(np.float64).reshape(n.value, slots, 8)
         t[t == 0] = np.nan
         return (t - np.nanmin(t[0, :, 0])) * 0.01
 

@@ -414,17 +414,19 @@ toks = g.generate(prompt, 80, 0.8, 5, allow=(m.SYNTH_SPEECH0, m.SYNTH_SPEECH0 + 
 h = hashlib.sha256(toks.tobytes())
 for pos in (3, 70, 129):
     h.update(g.eval(int(toks[0]), pos).tobytes())
-print(g.step_kinds().count(11), g.step_kinds().count(10), g.step_kinds().count(12), h.hexdigest())
+k = g.step_kinds()
+print(k.count(11), k.count(10), k.count(12), k.count(13), h.hexdigest())
 """
 
 
 @pytest.mark.parametrize("preset", [2, 3, 4])
 def test_fused_attention_launches_bit_identical(synth_llm_path, tmp_path, preset):
-    """The attention block as one launch (k_layer_att, layers >= 1), attention + O as one
-    launch (k_att_o) and the three separate launches run the same arithmetic, and so do the
-    FFN pair as one launch (k_ffn, r06) and k_ffn_in + k_ffn_down: 80 free-run tokens and the
-    logits of three later evaluations are bit-identical across MIO_LAYER_ATT / MIO_ATT_FUSE_O /
-    MIO_FFN_FUSE (each variant is a fresh process: the switches are read once)."""
+    """The whole layer as one launch (k_layer, layers >= 1, r06, opt-in), the attention block as one
+    launch (k_layer_att) + the FFN pair as one launch (k_ffn), attention + O as one launch
+    (k_att_o) and the separate launches run the same arithmetic: 80 free-run tokens and the
+    logits of three later evaluations are bit-identical across MIO_LAYER_FUSE / MIO_LAYER_GATE /
+    MIO_LAYER_ATT / MIO_ATT_FUSE_O / MIO_FFN_FUSE (each variant is a fresh process: the switches
+    are read once). k_layer is instantiated for the 1.7B Q4_K_M shapes (preset 3)."""
     import os
     import subprocess
     import sys
@@ -433,14 +435,21 @@ def test_fused_attention_launches_bit_identical(synth_llm_path, tmp_path, preset
     script.write_text(_FUSION_SCRIPT)
     pkg = os.path.dirname(os.path.dirname(m.__file__))
     outs = {}
-    for name, env in (("layer_att", {"MIO_LAYER_ATT": "1"}), ("att_o", {"MIO_LAYER_ATT": "0"}),
+    for name, env in (("layer", {"MIO_LAYER_FUSE": "1"}), ("layer_gate", {"MIO_LAYER_FUSE": "1", "MIO_LAYER_GATE": "2"}),
+                      ("layer_att", {"MIO_LAYER_FUSE": "0", "MIO_LAYER_ATT": "1"}),
+                      ("att_o", {"MIO_LAYER_FUSE": "0", "MIO_LAYER_ATT": "0"}),
                       ("separate", {"MIO_ATT_FUSE_O": "0", "MIO_FFN_FUSE": "0"})):
         p = subprocess.run([sys.executable, str(script), path, pkg], capture_output=True, text=True, timeout=240,
                            env=dict(os.environ, **env))
         assert p.returncode == 0, p.stderr[-2000:]
         outs[name] = p.stdout.split()
-    assert int(outs["layer_att"][0]) > 0 and int(outs["att_o"][0]) == 0 and int(outs["att_o"][1]) > 0
-    assert int(outs["separate"][0]) == int(outs["separate"][1]) == int(outs["separate"][2]) == 0
-    assert int(outs["layer_att"][2]) > 0  # the FFN pairs ran fused
     print(outs)
-    assert outs["layer_att"][3] == outs["att_o"][3] == outs["separate"][3], outs
+    if preset == 3:
+        assert int(outs["layer"][3]) == 27 and int(outs["layer_gate"][3]) == 27  # layers 1..27 as k_layer
+    assert int(outs["layer_att"][0]) > 0 and int(outs["layer_att"][3]) == 0
+    assert int(outs["att_o"][0]) == 0 and int(outs["att_o"][1]) > 0
+    assert int(outs["separate"][0]) == int(outs["separate"][1]) == int(outs["separate"][2]) == 0
+    assert int(outs["separate"][3]) == 0
+    assert int(outs["layer_att"][2]) > 0  # the FFN pairs ran fused
+    digests = {k: v[4] for k, v in outs.items()}
+    assert len(set(digests.values())) == 1, digests

@@ -25,7 +25,7 @@ llm.generate([256, 257, 65, 258, 257], a.pos, 0.8, 1, allow=(m.SYNTH_SPEECH0, m.
 t = llm.timeline()
 nl = t.shape[0]
 KN = {0: "attn_in", 1: "attention", 2: "attn_out", 3: "ffn_in", 4: "ffn_down", 6: "lm_head", 8: "conv_in",
-      9: "conv_out", 10: "att_o", 11: "layer_att", 12: "ffn"}
+      9: "conv_out", 10: "att_o", 11: "layer_att", 12: "ffn", 13: "layer"}
 names = [KN[k] for k in llm.step_kinds()]
 s0 = np.nanmin(t[:, :, 0], axis=1)
 s1 = np.nanmax(t[:, :, 0], axis=1)
@@ -42,14 +42,14 @@ gap = np.r_[0.0, s0[1:] - e1[:-1]]
 print(f"step wall {e1[-1] - s0[0]:.1f} us over {nl} launches; kernel time {dur.sum():.1f} us, "
       f"gaps {gap[1:].sum():.1f} us (mean {gap[1:].mean():.2f}, min {gap[1:].min():.2f}, max {gap[1:].max():.2f})")
 print("  kernel      dur    gap-before  start-spread  end-spread  median-wg   wg:->m1  m1->m2  m2->end  last-m2")
-for k in ["attn_in", "attention", "attn_out", "layer_att", "ffn_in", "ffn_down", "ffn", "lm_head"]:
+for k in ["attn_in", "attention", "attn_out", "layer_att", "ffn_in", "ffn_down", "ffn", "layer", "lm_head"]:
     idx = [i for i, n in enumerate(names) if n == k]
     print(f"  {k:10s} {dur[idx].mean():6.2f} {gap[idx].mean():8.2f} {(s1 - s0)[idx].mean():12.2f} "
           f"{(e1 - e0)[idx].mean():11.2f} {wd[idx].mean():10.2f} {np.nanmean(ph1[idx]):9.2f} "
           f"{np.nanmean(ph2[idx]):7.2f} {np.nanmean(ph3[idx]):8.2f} {np.nanmean(m2[idx]):8.2f}")
 # every recorded mark (1-6) and the end, as median offsets from the workgroup's own start
 print("  kernel      " + " ".join(f"{'m' + str(k):>6s}" for k in range(1, 7)) + "    end   (us after workgroup start)")
-for k in ["attn_in", "attention", "attn_out", "layer_att", "ffn_in", "ffn_down", "ffn", "lm_head"]:
+for k in ["attn_in", "attention", "attn_out", "layer_att", "ffn_in", "ffn_down", "ffn", "layer", "lm_head"]:
     idx = [i for i, n in enumerate(names) if n == k]
     cols = []
     for j in list(range(1, 7)) + [7]:
@@ -125,3 +125,41 @@ if jf:
           f"{med(T[:, :, 3] - base, isD):.2f} (first {firstv(T[:, :, 3] - base, isD):.2f}), h in "
           f"{med(T[:, :, 1] - base, isD):.2f}, quantized {med(T[:, :, 2] - base, isD):.2f}, end "
           f"{med(T[:, :, 7] - base, isD):.2f} (last {lastv(T[:, :, 7] - base, isD):.2f}) us after the launch's first start")
+# the whole layer in one launch (k_layer): roles by workgroup slot (1.7B: GW = no = GI = GD = 256
+# workgroups; the attention chunks are the slots with mark 4 = K/V staged)
+jl = [i for i, n in enumerate(names) if n == "layer"]
+if jl:
+    T = t[jl]
+    base = s0[jl][:, None]
+    n_act = int(np.isfinite(T[0, :, 4]).sum())
+    GW = NO = GI = GD = int(os.environ.get("TL_ROLE_WG", 256))
+    j = np.arange(T.shape[1])[None, :].repeat(T.shape[0], 0)
+    isP = j < GW
+    isA = (j >= GW) & (j < GW + n_act)
+    isO = (j >= GW + n_act) & (j < GW + n_act + NO)
+    isF = (j >= GW + n_act + NO) & (j < GW + n_act + NO + GI)
+    isD = (j >= GW + n_act + NO + GI) & (j < GW + n_act + NO + GI + GD)
+
+    def med(x, msk):
+        return float(np.nanmedian(np.where(msk, x, np.nan)))
+
+    def lastv(x, msk):
+        return float(np.nanmedian(np.nanmax(np.where(msk, x, np.nan), axis=1)))
+
+    def firstv(x, msk):
+        return -lastv(-x, msk)
+    R = T - base[:, :, None]
+    mg = isA & np.isfinite(T[:, :, 5])
+    print(f"  layer: producers end {med(R[:, :, 7], isP):.2f} (last {lastv(R[:, :, 7], isP):.2f}); {n_act} attention: "
+          f"q|k|v ready {med(R[:, :, 3], isA):.2f}, end {med(R[:, :, 7], isA):.2f}; mergers ticket "
+          f"{med(R[:, :, 5], mg):.2f}, outputs written {med(R[:, :, 6], mg):.2f}")
+    print(f"  layer: O start {med(R[:, :, 0], isO):.2f} (last {lastv(R[:, :, 0], isO):.2f}), wait done "
+          f"{med(R[:, :, 3], isO):.2f}, x written {med(R[:, :, 6], isO):.2f} (last {lastv(R[:, :, 6], isO):.2f}), end "
+          f"{med(R[:, :, 7], isO):.2f}")
+    print(f"  layer: gate|up start {med(R[:, :, 0], isF):.2f} (last {lastv(R[:, :, 0], isF):.2f}), x wait done "
+          f"{med(R[:, :, 3], isF):.2f} (first {firstv(R[:, :, 3], isF):.2f}), x in {med(R[:, :, 1], isF):.2f}, "
+          f"quantized {med(R[:, :, 2], isF):.2f}, end {med(R[:, :, 7], isF):.2f} (last {lastv(R[:, :, 7], isF):.2f})")
+    print(f"  layer: down start {med(R[:, :, 0], isD):.2f} (last {lastv(R[:, :, 0], isD):.2f}), h wait done "
+          f"{med(R[:, :, 3], isD):.2f} (first {firstv(R[:, :, 3], isD):.2f}), h in {med(R[:, :, 1], isD):.2f}, "
+          f"quantized {med(R[:, :, 2], isD):.2f}, end {med(R[:, :, 7], isD):.2f} (last {lastv(R[:, :, 7], isD):.2f}) "
+          f"us after the launch's first start")
