@@ -60,7 +60,7 @@ if not os.path.exists(vp):
 dev = m.Device(0)
 c = m.Codec(dev, cp)
 emb = m.read_voice(vp)
-codes = (np.arange(700) * 7919) % 12800
+codes = (np.arange(int(os.environ.get("CODEC_T", 700))) * 7919) % 12800
 for _ in range(2):
     c.decode_pcm(codes, emb)
 print("codec ms", c.last_timings())
