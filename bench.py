@@ -247,27 +247,26 @@ def batched_line(a, llm, codec, dev, prompt, allow, d_emb, d_pcm):
 
 
 def make_batch_step(tokens, B, llm, codec, dev, prompt, allow, d_emb, d_pcm):
-    """One step of B utterances decoded together, then each through codec + iSTFT (PCM left
-    in HBM). step(seed_base, _) -> (audio samples, llm seconds)."""
+    """One step of B utterances decoded together, then their codec + iSTFT decodes run
+    concurrently (mio_hip_codec_decode_pcm_batch: up to 3 streams, each with its own workspace;
+    PCM left in HBM). step(seed_base, _) -> (audio samples, llm seconds, codec+iSTFT ms, 0)."""
     import numpy as np
     import miotts_amd as m
+    d_outs = [dev.empty((tokens * codec.samples_per_token,), np.float32) for _ in range(B)]
 
     def step(seed_base, _record):
         seeds = [utterance_seed(0, seed_base + b) for b in range(B)]
         t0 = time.perf_counter()
         outs = llm.generate_batch([prompt] * B, tokens, 0.8, seeds, allow=allow, check_interval=64)
         t1 = time.perf_counter()
-        samples, codec_ms, istft_ms = 0, 0.0, 0.0
         for toks in outs:
             if len(toks) != tokens:
                 raise RuntimeError("batched utterance ended early")
-            d_codes = dev.upload((toks - m.SYNTH_SPEECH0).astype(np.int32))
-            samples += codec.decode_pcm_device(d_codes, len(toks), d_emb, d_pcm)
-            c_ms, i_ms = codec.last_timings()
-            codec_ms += c_ms
-            istft_ms += i_ms
+        d_codes = [dev.upload((toks - m.SYNTH_SPEECH0).astype(np.int32)) for toks in outs]
+        lens = codec.decode_pcm_batch_device(d_codes, [len(t) for t in outs], d_emb, d_outs)
+        c_ms, _ = codec.last_timings()
         dev.sync()
-        return samples, t1 - t0, codec_ms, istft_ms
+        return sum(lens), t1 - t0, c_ms, 0.0
 
     return step
 

@@ -114,6 +114,15 @@ int mio_hip_codec_decode(mio_hip_codec *c, const int32_t *codes, int n_codes,
 int mio_hip_codec_decode_pcm(mio_hip_codec *c, const int32_t *codes, int n_codes,
                              const float *global_emb, float *out_pcm, int *out_len,
                              unsigned flags, void *stream);
+/* B independent utterances (test-to-speech.cpp:264-287 per utterance), each through codec +
+ * fused iSTFT into out_pcm[b] (*out_len[b] samples): the decodes run on up to
+ * MIO_CODEC_STREAMS (default 3) streams at once, each with its own workspace, so one decode's
+ * small GEMM grids and row kernels leave the CUs to the others; every utterance's arithmetic is
+ * mio_hip_codec_decode_pcm's (same kernels, same tiling: bit-identical PCM). Joined on `stream`
+ * before return. Flags as mio_hip_codec_decode_pcm (no MIO_CODEC_INCREMENTAL). */
+int mio_hip_codec_decode_pcm_batch(mio_hip_codec *c, const int32_t *const *codes, const int *n_codes, int B,
+                                   const float *global_emb, float *const *out_pcm, int *out_len,
+                                   unsigned flags, void *stream);
 /* Debug/parity: run up to `stage` and copy that activation to host `out` (stage list as
  * in oracle/mio_oracle.h: 0 embed .. 7+U spectrogram). rows/cols receive its shape. */
 int mio_hip_codec_decode_stage(mio_hip_codec *c, const int32_t *codes, int n_codes,

@@ -78,6 +78,12 @@ struct mio_hip_codec {
     int rope_cap = 0;
     char *ws = nullptr;
     size_t ws_cap = 0;
+    // mio_hip_codec_decode_pcm_batch: lane k >= 1 decodes on stream xs[k - 1] in workspace
+    // xws[k - 1] (lane 0: the caller's stream and ws), joined through xev
+    std::vector<hipStream_t> xs;
+    std::vector<hipEvent_t> xev;
+    std::vector<char *> xws;
+    std::vector<size_t> xws_cap;
     mio_hip_istft *ist = nullptr;
     std::vector<void *> allocs;
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
@@ -97,6 +103,10 @@ struct mio_hip_codec {
         for (void *p : allocs) hipFree(p);
         if (rope) hipFree(rope);
         if (ws) hipFree(ws);
+        for (char *p : xws)
+            if (p) hipFree(p);
+        for (auto e : xev) hipEventDestroy(e);
+        for (auto q : xs) hipStreamDestroy(q);
         if (pc) hipFree(pc);
         if (ist) mio_hip_istft_destroy(ist);
         for (auto e : ev)
@@ -278,7 +288,9 @@ struct Ws {
     int Lf;
 };
 
-int plan_ws(mio_hip_codec *c, int T, Ws &w, bool alloc, size_t *bytes = nullptr) {
+int plan_ws(mio_hip_codec *c, int T, Ws &w, bool alloc, size_t *bytes = nullptr, int lane = 0) {
+    char *&ws = lane ? c->xws[lane - 1] : c->ws;
+    size_t &ws_cap = lane ? c->xws_cap[lane - 1] : c->ws_cap;
     const int S = 2 * T;
     size_t off = 0;
     std::vector<size_t> sizes;
@@ -328,7 +340,7 @@ int plan_ws(mio_hip_codec *c, int T, Ws &w, bool alloc, size_t *bytes = nullptr)
     float *codes_f = nullptr;
     F(&codes_f, (size_t)T);
     if (bytes) *bytes = off;
-    if (alloc && off > c->ws_cap) {
+    if (alloc && off > ws_cap) {
         // sized for at least 1024 codes: streaming re-decodes grow T every call, and each
         // re-allocation (hipFree) would wait for whatever else runs on the device
         size_t want = off;
@@ -336,16 +348,16 @@ int plan_ws(mio_hip_codec *c, int T, Ws &w, bool alloc, size_t *bytes = nullptr)
             Ws big;
             plan_ws(c, 1024, big, false, &want);
         }
-        if (c->ws) hipFree(c->ws);
-        c->ws = nullptr;
-        c->ws_cap = 0;
-        if (hipMalloc(&c->ws, want) != hipSuccess) {
+        if (ws) hipFree(ws);
+        ws = nullptr;
+        ws_cap = 0;
+        if (hipMalloc(&ws, want) != hipSuccess) {
             mio::set_error("miocodec: workspace of %zu bytes failed", want);
             return MIO_ERR_OOM;
         }
-        c->ws_cap = want;
+        ws_cap = want;
     }
-    for (auto &s : slots) *s.first = (float *)(c->ws + s.second);
+    for (auto &s : slots) *s.first = (float *)(ws + s.second);
     w.codes = (int *)codes_f;
     w.gns.part = (double *)gnp_f;
     w.gns.stat = (float2 *)gns_f;
@@ -877,6 +889,79 @@ extern "C" int mio_hip_codec_decode_pcm(mio_hip_codec *c, const int32_t *codes, 
         MIO_HIP_CHECK(hipMemcpyAsync(out_pcm, w.pcm, (size_t)len * 4, hipMemcpyDeviceToHost, s));
         MIO_HIP_CHECK(hipStreamSynchronize(s));
     }
+    return MIO_OK;
+}
+
+// Concurrent decodes of independent utterances (header: mio_hip_codec_decode_pcm_batch). Every
+// lane's workspace and the RoPE table are sized before the first kernel is issued, so no
+// hipFree runs while another lane's kernels read a buffer.
+extern "C" int mio_hip_codec_decode_pcm_batch(mio_hip_codec *c, const int32_t *const *codes, const int *n_codes,
+                                              int B, const float *emb, float *const *out_pcm, int *out_len,
+                                              unsigned flags, void *stream) {
+    MIO_REQUIRE(c && codes && n_codes && emb && out_pcm && B > 0, MIO_ERR_INVALID, "codec_decode_pcm_batch: bad args");
+    MIO_REQUIRE(!(flags & MIO_CODEC_INCREMENTAL), MIO_ERR_INVALID, "codec_decode_pcm_batch: no incremental decodes");
+    for (int b = 0; b < B; ++b)
+        MIO_REQUIRE(codes[b] && out_pcm[b] && n_codes[b] > 0, MIO_ERR_INVALID, "codec_decode_pcm_batch: utterance %d", b);
+    int rc = mio::bind(c->d);
+    if (rc) return rc;
+    hipStream_t s = mio::pick_stream(c->d, stream);
+    static const int kLanes = [] {
+        const char *e = getenv("MIO_CODEC_STREAMS");
+        const int v = e ? atoi(e) : 3;  // 8 x 700 codes: 23.1 / 17.8 / 16.9 / 18.8 ms at 1-4 (r06)
+        return v < 1 ? 1 : (v > 8 ? 8 : v);
+    }();
+    const int NS = std::min(B, kLanes);
+    if (!c->ev[0])
+        for (auto &e : c->ev) MIO_HIP_CHECK(hipEventCreate(&e));
+    while ((int)c->xs.size() < NS - 1) {
+        hipStream_t q = nullptr;
+        hipEvent_t e = nullptr;
+        MIO_HIP_CHECK(hipStreamCreateWithFlags(&q, hipStreamNonBlocking));
+        MIO_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        c->xs.push_back(q), c->xev.push_back(e), c->xws.push_back(nullptr), c->xws_cap.push_back(0);
+    }
+    // size every lane for its longest utterance first (allocations wait for the device)
+    for (int k = 0; k < NS; ++k) {
+        int tmax = 0;
+        for (int b = k; b < B; b += NS) tmax = std::max(tmax, n_codes[b]);
+        Ws w;
+        if ((rc = plan_ws(c, tmax, w, true, nullptr, k))) return rc;
+    }
+    MIO_HIP_CHECK(hipEventRecord(c->ev[0], s));
+    for (int k = 1; k < NS; ++k) MIO_HIP_CHECK(hipStreamWaitEvent(c->xs[k - 1], c->ev[0], 0));
+    double flops = 0.0;
+    for (int b = 0; b < B; ++b) {
+        const int k = b % NS;
+        hipStream_t ls = k ? c->xs[k - 1] : s;
+        Ws w;
+        if ((rc = plan_ws(c, n_codes[b], w, false, nullptr, k))) return rc;
+        if ((rc = prepare_inputs(c, w, codes[b], n_codes[b], emb, flags, ls))) return rc;
+        const float *buf = nullptr;
+        int r = 0, cc = 0;
+        t_flops = 0.0;
+        if ((rc = run_decode(c, w, ls, 1 << 20, &buf, &r, &cc))) return rc;
+        flops += t_flops;
+        int len = 0;
+        if ((rc = mio_hip_istft_out_len(c->ist, w.Lf, c->hop, &len))) return rc;
+        if (flags & MIO_OUT_DEVICE) {
+            if ((rc = mio_istft_launch_device(c->ist, w.spec, w.Lf, c->hop, out_pcm[b], ls))) return rc;
+        } else {
+            if ((rc = mio_istft_launch_device(c->ist, w.spec, w.Lf, c->hop, w.pcm, ls))) return rc;
+            MIO_HIP_CHECK(hipMemcpyAsync(out_pcm[b], w.pcm, (size_t)len * 4, hipMemcpyDeviceToHost, ls));
+        }
+        if (out_len) out_len[b] = len;
+    }
+    for (int k = 1; k < NS; ++k) {
+        MIO_HIP_CHECK(hipEventRecord(c->xev[k - 1], c->xs[k - 1]));
+        MIO_HIP_CHECK(hipStreamWaitEvent(s, c->xev[k - 1], 0));
+    }
+    MIO_HIP_CHECK(hipGetLastError());
+    // last_timings: codec = the whole batch (decodes and iSTFTs overlap), iSTFT 0
+    MIO_HIP_CHECK(hipEventRecord(c->ev[1], s));
+    MIO_HIP_CHECK(hipEventRecord(c->ev[2], s));
+    c->timed = true;
+    c->last_flops = flops;
+    if (!(flags & MIO_OUT_DEVICE)) MIO_HIP_CHECK(hipStreamSynchronize(s));
     return MIO_OK;
 }
 

@@ -100,6 +100,7 @@ def _declare(L: ctypes.CDLL) -> None:
                                          ctypes.c_uint, _vp]),
         "mio_hip_codec_decode_pcm": (c_int, [_vp, _vp, c_int, _vp, _vp, ctypes.POINTER(c_int),
                                              ctypes.c_uint, _vp]),
+        "mio_hip_codec_decode_pcm_batch": (c_int, [_vp, _vp, _vp, c_int, _vp, _vp, _vp, ctypes.c_uint, _vp]),
         "mio_hip_codec_decode_stage": (c_int, [_vp, _vp, c_int, _vp, c_int, _vp,
                                                ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),
         "mio_synth_codec_gguf": (c_int, [ctypes.c_char_p, c_int, ctypes.c_uint64]),
@@ -394,6 +395,29 @@ class Codec:
                                              ctypes.byref(n), MIO_IN_DEVICE | MIO_OUT_DEVICE,
                                              stream or None))
         return n.value
+
+    def decode_pcm_batch_device(self, codes, n_codes, emb: DeviceArray, outs, stream: int = 0):
+        """B utterances at once (mio_hip_codec_decode_pcm_batch): codes[b] / outs[b] are
+        DeviceArrays, n_codes[b] their lengths; returns the PCM lengths."""
+        B = len(codes)
+        cp = (ctypes.c_void_p * B)(*[c.ptr for c in codes])
+        op = (ctypes.c_void_p * B)(*[o.ptr for o in outs])
+        nc = (ctypes.c_int * B)(*[int(n) for n in n_codes])
+        ln = (ctypes.c_int * B)()
+        check(lib().mio_hip_codec_decode_pcm_batch(self.h, ctypes.cast(cp, _vp), ctypes.cast(nc, _vp), B, emb.ptr,
+                                                   ctypes.cast(op, _vp), ctypes.cast(ln, _vp),
+                                                   MIO_IN_DEVICE | MIO_OUT_DEVICE, stream or None))
+        return [int(x) for x in ln]
+
+    def decode_pcm_batch(self, codes, emb):
+        """Host convenience of decode_pcm_batch_device: list of code arrays -> list of PCM."""
+        dev = self.dev
+        d_codes = [dev.upload(np.ascontiguousarray(c, np.int32)) for c in codes]
+        d_emb = dev.upload(np.ascontiguousarray(emb, np.float32))
+        outs = [dev.empty((len(c) * self.samples_per_token + self.n_fft,), np.float32) for c in codes]
+        lens = self.decode_pcm_batch_device(d_codes, [len(c) for c in codes], d_emb, outs)
+        dev.sync()
+        return [o.numpy()[:n] for o, n in zip(outs, lens)]
 
     def last_timings(self):
         ms = np.zeros(2, np.float32)

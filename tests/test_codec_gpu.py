@@ -106,6 +106,21 @@ def test_codec_device_buffers_and_repeat(device, files, emb):
     assert np.array_equal(a, b)  # deterministic: same kernels, same order
 
 
+def test_codec_batch_equals_single(device, files, emb):
+    """mio_hip_codec_decode_pcm_batch (the batched bench line and batch synthesis): ragged
+    utterances decoded concurrently on up to 4 streams, each lane in its own workspace and
+    reused for a second utterance, give each utterance's single-decode PCM bit for bit (same
+    kernels, same tiling; test-to-speech.cpp:264-287 runs every utterance on its own)."""
+    gc = m.Codec(device, files["full"])
+    rng = np.random.default_rng(5)
+    lens = [33, 7, 120, 60, 2, 95]
+    codes = [rng.integers(0, 12800, n).astype(np.int32) for n in lens]
+    got = gc.decode_pcm_batch(codes, emb)
+    for c, g in zip(codes, got):
+        want = gc.decode_pcm(c, emb)
+        assert g.shape == want.shape and np.array_equal(g, want), len(c)
+
+
 def test_codec_rejects_bad_codes(device, files, emb):
     gc = m.Codec(device, files["tiny"])
     with pytest.raises(m.HipError):
