@@ -87,6 +87,47 @@ bool is_punct(uint32_t cp) { return in_sorted(kPunctRanges, kPunctRanges_n, cp);
 bool is_nl(uint32_t cp) { return cp == '\r' || cp == '\n'; }
 uint32_t lower_ascii(uint32_t cp) { return cp >= 'A' && cp <= 'Z' ? cp + 32 : cp; }
 
+// WPM classes (unicode_ranges.h): Cc / Cf / Co / Cs, the first code point of the canonical
+// decomposition, the one-to-one lowercase mapping, CJK ideographs (BERT's _is_chinese_char)
+bool is_control(uint32_t cp) { return in_sorted(kOtherRanges, kOtherRanges_n, cp); }
+uint32_t nfd_first(uint32_t cp) {
+    size_t lo = 0, hi = kNfdFirst_n;
+    while (lo < hi) {
+        const size_t mid = (lo + hi) / 2;
+        if (cp < kNfdFirst[mid].a)
+            hi = mid;
+        else if (cp > kNfdFirst[mid].b)
+            lo = mid + 1;
+        else
+            return kNfdFirst[mid].v;
+    }
+    return cp;
+}
+uint32_t to_lower(uint32_t cp) {
+    if (cp < 0x80) return lower_ascii(cp);
+    size_t lo = 0, hi = kLowerPairs_n;
+    while (lo < hi) {
+        const size_t mid = (lo + hi) / 2;
+        if (cp < kLowerPairs[mid].a)
+            hi = mid;
+        else if (cp > kLowerPairs[mid].a)
+            lo = mid + 1;
+        else
+            return kLowerPairs[mid].b;
+    }
+    return cp;
+}
+bool is_cjk(uint32_t cp) {
+    return (cp >= 0x4E00 && cp <= 0x9FFF) || (cp >= 0x3400 && cp <= 0x4DBF) || (cp >= 0x20000 && cp <= 0x2A6DF) ||
+           (cp >= 0x2A700 && cp <= 0x2B73F) || (cp >= 0x2B740 && cp <= 0x2B81F) || (cp >= 0x2B820 && cp <= 0x2CEAF) ||
+           (cp >= 0xF900 && cp <= 0xFAFF) || (cp >= 0x2F800 && cp <= 0x2FA1F);
+}
+// ASCII symbols (general category S*: $ + < = > ^ ` | ~)
+bool is_ascii_symbol(uint32_t cp) {
+    return cp == '$' || cp == '+' || cp == '<' || cp == '=' || cp == '>' || cp == '^' || cp == '`' || cp == '|' ||
+           cp == '~';
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------ load
@@ -94,8 +135,9 @@ bool BpeTokenizer::load(const GgufFile &g) {
     const std::string model = g.get_str("tokenizer.ggml.model");
     const GgufValue *tv = g.get("tokenizer.ggml.tokens");
     if (model == "llama" && tv && !tv->arr_s.empty()) return load_spm(g);
+    if (model == "bert" && tv && !tv->arr_s.empty()) return load_wpm(g);
     if (model != "gpt2" || !tv || tv->arr_s.empty()) {
-        set_error("tokenizer: GGUF has no gpt2 (byte-level BPE) or llama (SPM) vocabulary (model '%s')",
+        set_error("tokenizer: GGUF has no gpt2 (byte-level BPE), llama (SPM) or bert (WPM) vocabulary (model '%s')",
                   model.c_str());
         return false;
     }
@@ -157,18 +199,12 @@ bool BpeTokenizer::load(const GgufFile &g) {
     return true;
 }
 
-// SPM (tokenizer.ggml.model "llama"): tokens, scores, types; llama.cpp's defaults for this
-// vocabulary type: BOS added, EOS not, a space prefix on the first fragment
-bool BpeTokenizer::load_spm(const GgufFile &g) {
-    spm_ = true;
+void BpeTokenizer::load_vocab(const GgufFile &g) {
     tokens_ = g.get("tokenizer.ggml.tokens")->arr_s;
     const size_t n = tokens_.size();
     types_.assign(n, 1);
     if (const GgufValue *tt = g.get("tokenizer.ggml.token_type"))
         for (size_t i = 0; i < tt->arr_i.size() && i < n; ++i) types_[i] = (int32_t)tt->arr_i[i];
-    scores_.assign(n, 0.0f);
-    if (const GgufValue *sc = g.get("tokenizer.ggml.scores"))
-        for (size_t i = 0; i < sc->arr_f.size() && i < n; ++i) scores_[i] = (float)sc->arr_f[i];
     id_.reserve(n * 2);
     for (size_t i = 0; i < n; ++i) id_.emplace(tokens_[i], (int32_t)i);
     std::set<size_t, std::greater<size_t>> lens;
@@ -178,6 +214,17 @@ bool BpeTokenizer::load_spm(const GgufFile &g) {
             lens.insert(tokens_[i].size());
         }
     special_lens_.assign(lens.begin(), lens.end());
+}
+
+// SPM (tokenizer.ggml.model "llama"): tokens, scores, types; llama.cpp's defaults for this
+// vocabulary type: BOS added, EOS not, a space prefix on the first fragment
+bool BpeTokenizer::load_spm(const GgufFile &g) {
+    spm_ = true;
+    load_vocab(g);
+    const size_t n = tokens_.size();
+    scores_.assign(n, 0.0f);
+    if (const GgufValue *sc = g.get("tokenizer.ggml.scores"))
+        for (size_t i = 0; i < sc->arr_f.size() && i < n; ++i) scores_[i] = (float)sc->arr_f[i];
     eos_ = (int32_t)g.get_int("tokenizer.ggml.eos_token_id", -1);
     bos_ = (int32_t)g.get_int("tokenizer.ggml.bos_token_id", -1);
     unk_ = (int32_t)g.get_int("tokenizer.ggml.unknown_token_id", -1);
@@ -200,6 +247,79 @@ bool BpeTokenizer::load_spm(const GgufFile &g) {
         return false;
     }
     return true;
+}
+
+// WPM (tokenizer.ggml.model "bert"): llama.cpp's defaults for this vocabulary type are the
+// BERT ids [CLS] 101 (BOS), [UNK] 100, [SEP] 102, with BOS and SEP added around the text
+bool BpeTokenizer::load_wpm(const GgufFile &g) {
+    wpm_ = true;
+    load_vocab(g);
+    const int32_t n = (int32_t)tokens_.size();
+    bos_ = (int32_t)g.get_int("tokenizer.ggml.bos_token_id", 101);
+    eos_ = (int32_t)g.get_int("tokenizer.ggml.eos_token_id", -1);
+    unk_ = (int32_t)g.get_int("tokenizer.ggml.unknown_token_id", 100);
+    sep_ = (int32_t)g.get_int("tokenizer.ggml.seperator_token_id", 102);  // the GGUF key's spelling
+    const GgufValue *ab = g.get("tokenizer.ggml.add_bos_token");
+    add_bos_ = ab ? ab->u != 0 : true;
+    const GgufValue *ae = g.get("tokenizer.ggml.add_eos_token");
+    add_eos_ = ae ? ae->u != 0 : false;
+    const GgufValue *as = g.get("tokenizer.ggml.add_sep_token");
+    add_sep_ = as ? as->u != 0 : true;
+    for (const std::string &t : tokens_) max_tok_len_ = std::max(max_tok_len_, t.size());
+    if (bos_ >= n || eos_ >= n || unk_ >= n || sep_ >= n || unk_ < 0) {
+        set_error("tokenizer: WPM special token id out of range");
+        return false;
+    }
+    return true;
+}
+
+// ------------------------------------------------------------------ WPM
+void BpeTokenizer::wpm(const std::string &text, std::vector<int32_t> &out) const {
+    std::vector<std::string> words;
+    std::string word;
+    auto end_word = [&]() {
+        if (!word.empty()) words.push_back(word);
+        word.clear();
+    };
+    for (size_t i = 0; i < text.size();) {
+        size_t l = 1;
+        const uint32_t cp = nfd_first(utf8_decode(text, i, &l));
+        i += l;
+        if (is_space(cp)) {
+            end_word();
+            continue;
+        }
+        if (cp == 0 || cp == 0xFFFD || is_control(cp)) continue;
+        const std::string c = utf8_encode(to_lower(cp));
+        if (is_punct(cp) || is_ascii_symbol(cp) || is_cjk(cp)) {
+            end_word();
+            words.push_back(c);
+        } else {
+            word += c;
+        }
+    }
+    end_word();
+    for (const std::string &w : words) {
+        const std::string s = "\xe2\x96\x81" + w;  // U+2581: a word-initial token
+        const size_t first = out.size();
+        bool ok = true;
+        for (size_t i = 0; i < s.size() && ok;) {
+            ok = false;
+            for (size_t j = std::min(s.size(), i + max_tok_len_); j > i; --j) {
+                const auto it = id_.find(s.substr(i, j - i));
+                if (it != id_.end()) {
+                    out.push_back(it->second);
+                    i = j;
+                    ok = true;
+                    break;
+                }
+            }
+        }
+        if (!ok) {  // an unmatched position: the whole word is UNK
+            out.resize(first);
+            out.push_back(unk_);
+        }
+    }
 }
 
 // ------------------------------------------------------------------ SPM
@@ -491,7 +611,9 @@ std::vector<int32_t> BpeTokenizer::tokenize(const std::string &text, bool add_sp
     bool prev_special = true;  // SPM: the space prefix goes on a fragment that opens the text or follows a special
     auto flush = [&]() {
         if (run.empty()) return;
-        if (spm_) {
+        if (wpm_) {
+            wpm(run, out);
+        } else if (spm_) {
             std::string t = add_space_prefix_ && prev_special ? " " + run : run;
             std::string e;
             for (char c : t) {
@@ -531,7 +653,8 @@ std::vector<int32_t> BpeTokenizer::tokenize(const std::string &text, bool add_sp
         }
     }
     flush();
-    if (spm_ && add_special && add_eos_ && eos_ >= 0) out.push_back(eos_);
+    if ((spm_ || wpm_) && add_special && add_eos_ && eos_ >= 0) out.push_back(eos_);
+    if (wpm_ && add_special && add_sep_ && sep_ >= 0) out.push_back(sep_);
     return out;
 }
 
@@ -539,7 +662,7 @@ std::string BpeTokenizer::piece(int32_t id) const {
     if (id < 0 || id >= (int32_t)tokens_.size()) return "";
     const std::string &t = tokens_[id];
     if (types_[id] == 3 || types_[id] == 4) return t;  // special: rendered as text
-    if (spm_) {
+    if (spm_ || wpm_) {
         // llama_token_to_piece(special = true): UNKNOWN as its text, NORMAL with U+2581 -> ' ',
         // BYTE "<0xXX>" -> the byte, other types (UNUSED) nothing
         if (types_[id] == 2) return t;

@@ -25,6 +25,17 @@
 // token become their <0xXX> byte tokens. BOS is added by default (add_bos_token), EOS when
 // add_eos_token. Pieces: U+2581 -> ' ', byte tokens -> the byte. Checked id for id against
 // the `sentencepiece` package's BPE encoder on trained vocabularies (tests/test_tokenizer_spm.py).
+//
+// WPM vocabularies (tokenizer.ggml.model == "bert": WordPiece, llama.cpp's llm_tokenizer_wpm,
+// restated): specials split as above; a fragment's code points are mapped to the first code
+// point of their canonical decomposition (accents of precomposed letters drop) and lowercased;
+// whitespace ends a word, control / format characters and U+FFFD are dropped, and punctuation,
+// ASCII symbols and CJK ideographs become words of their own; each word, prefixed with U+2581,
+// is split greedily into the longest vocabulary tokens (convert_hf_to_gguf writes a BERT
+// vocabulary's word-initial tokens with that prefix and "##" continuations without it), and a
+// word with an unmatched position becomes one UNK. [CLS] (BOS) opens and [SEP] closes the text
+// by default. Checked id for id against HuggingFace `tokenizers`' BERT WordPiece
+// (tests/test_tokenizer_wpm.py).
 #pragma once
 
 #include <cstdint>
@@ -54,6 +65,10 @@ private:
     void bpe(const std::string &piece, std::vector<int32_t> &out) const;
     void spm(const std::string &text, std::vector<int32_t> &out) const;
     bool load_spm(const GgufFile &g);
+    void wpm(const std::string &text, std::vector<int32_t> &out) const;
+    bool load_wpm(const GgufFile &g);
+    // tokens, types, id map, special tokens (shared by the SPM / WPM loaders)
+    void load_vocab(const GgufFile &g);
     void pretokenize(const std::string &text, std::vector<std::string> &pieces) const;
 
     std::vector<std::string> tokens_;
@@ -68,6 +83,10 @@ private:
     bool add_bos_ = false, add_eos_ = false;
     // SPM vocabularies
     bool spm_ = false, add_space_prefix_ = true;
+    // WPM vocabularies: [SEP] after the text (add_sep), longest token in bytes
+    bool wpm_ = false, add_sep_ = true;
+    int32_t sep_ = -1;
+    size_t max_tok_len_ = 0;
     std::vector<float> scores_;
     int32_t byte_tok_[256];
     // pre-tokenizer family (llama.cpp LLAMA_VOCAB_PRE_TYPE_*): the regex sequence of step 2
