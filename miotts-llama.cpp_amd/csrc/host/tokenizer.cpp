@@ -2,7 +2,10 @@
 #include "tokenizer.h"
 
 #include <algorithm>
+#include <cfloat>
 #include <climits>
+#include <cmath>
+#include <cstring>
 #include <functional>
 #include <queue>
 #include <set>
@@ -136,9 +139,10 @@ bool BpeTokenizer::load(const GgufFile &g) {
     const GgufValue *tv = g.get("tokenizer.ggml.tokens");
     if (model == "llama" && tv && !tv->arr_s.empty()) return load_spm(g);
     if (model == "bert" && tv && !tv->arr_s.empty()) return load_wpm(g);
+    if (model == "t5" && tv && !tv->arr_s.empty()) return load_ugm(g);
     if (model != "gpt2" || !tv || tv->arr_s.empty()) {
-        set_error("tokenizer: GGUF has no gpt2 (byte-level BPE), llama (SPM) or bert (WPM) vocabulary (model '%s')",
-                  model.c_str());
+        set_error("tokenizer: GGUF has no gpt2 (byte-level BPE), llama (SPM), bert (WPM) or t5 (UGM) vocabulary "
+                  "(model '%s')", model.c_str());
         return false;
     }
     tokens_ = tv->arr_s;
@@ -320,6 +324,174 @@ void BpeTokenizer::wpm(const std::string &text, std::vector<int32_t> &out) const
             out.push_back(unk_);
         }
     }
+}
+
+// UGM (tokenizer.ggml.model "t5"): llama.cpp's defaults for this vocabulary type are the T5
+// ids (pad 0, EOS 1, UNK 2, no BOS), EOS added after the text, a space prefix, whitespace
+// escaped to U+2581 and not merged unless tokenizer.ggml.remove_extra_whitespaces
+bool BpeTokenizer::load_ugm(const GgufFile &g) {
+    ugm_ = true;
+    load_vocab(g);
+    const size_t n = tokens_.size();
+    scores_.assign(n, 0.0f);
+    if (const GgufValue *sc = g.get("tokenizer.ggml.scores"))
+        for (size_t i = 0; i < sc->arr_f.size() && i < n; ++i) scores_[i] = (float)sc->arr_f[i];
+    bos_ = (int32_t)g.get_int("tokenizer.ggml.bos_token_id", -1);
+    eos_ = (int32_t)g.get_int("tokenizer.ggml.eos_token_id", 1);
+    unk_ = (int32_t)g.get_int("tokenizer.ggml.unknown_token_id", 2);
+    auto flag = [&](const char *k, bool def) {
+        const GgufValue *v = g.get(k);
+        return v ? v->u != 0 : def;
+    };
+    add_bos_ = flag("tokenizer.ggml.add_bos_token", false);
+    add_eos_ = flag("tokenizer.ggml.add_eos_token", true);
+    add_space_prefix_ = flag("tokenizer.ggml.add_space_prefix", true);
+    remove_extra_ws_ = flag("tokenizer.ggml.remove_extra_whitespaces", false);
+    if (bos_ >= (int32_t)n || eos_ >= (int32_t)n || unk_ >= (int32_t)n || unk_ < 0) {
+        set_error("tokenizer: UGM special token id out of range");
+        return false;
+    }
+    // the character map: u32 size of the double array, its units, then the NUL-terminated
+    // replacement strings the leaves index
+    if (const GgufValue *cm = g.get("tokenizer.ggml.precompiled_charsmap"); cm && !cm->arr_i.empty()) {
+        std::string b(cm->arr_i.size(), '\0');
+        for (size_t i = 0; i < b.size(); ++i) b[i] = (char)(uint8_t)cm->arr_i[i];
+        uint32_t xs = 0;
+        if (b.size() < 4 || (std::memcpy(&xs, b.data(), 4), xs % 4) || xs > b.size() - 4) {
+            set_error("tokenizer: malformed precompiled_charsmap");
+            return false;
+        }
+        xcda_.resize(xs / 4);
+        std::memcpy(xcda_.data(), b.data() + 4, xs);
+        repl_ = b.substr(4 + xs);
+    }
+    float min_score = INFINITY;
+    std::set<size_t, std::greater<size_t>> ulens;
+    for (size_t i = 0; i < n; ++i) {
+        const int32_t t = types_[i];
+        if (t == 1) min_score = std::min(min_score, scores_[i]);
+        if (t == 1 || t == 4 || t == 5) ugm_tok_.emplace(tokens_[i], (int32_t)i);  // NORMAL, USER_DEFINED, UNUSED
+        if (t == 4 && !tokens_[i].empty()) {
+            user_def_.emplace(tokens_[i], (int32_t)i);
+            ulens.insert(tokens_[i].size());
+        }
+        max_tok_len_ = std::max(max_tok_len_, tokens_[i].size());
+    }
+    user_def_lens_.assign(ulens.begin(), ulens.end());
+    unk_score_ = (std::isfinite(min_score) ? min_score : 0.0f) - 10.0f;
+    return true;
+}
+
+// ------------------------------------------------------------------ UGM
+// One normalization step at byte i: a user-defined token is kept as it is; else the longest
+// input prefix in the character map's double array (Darts-clone units: BASE = unit >> 10 shifted
+// left by 8 when bit 9 is set, LCHECK = label | bit 31, LEAF = bit 8, a leaf child's VALUE =
+// unit & 0x7FFFFFFF, the replacement's offset); else one UTF-8 character as it is (an invalid
+// byte: U+FFFD)
+std::pair<std::string, size_t> BpeTokenizer::ugm_prefix(const std::string &text, size_t i) const {
+    for (size_t l : user_def_lens_)
+        if (l <= text.size() - i && user_def_.count(text.substr(i, l))) return {text.substr(i, l), l};
+    size_t best = 0, off = 0;
+    if (!xcda_.empty()) {
+        auto unit = [&](size_t k) { return k < xcda_.size() ? xcda_[k] : 0u; };
+        auto base = [&](uint32_t u) { return (u >> 10) << ((u & (1u << 9)) >> 6); };
+        size_t node = base(unit(0));
+        for (size_t p = i; p < text.size(); ++p) {
+            const uint8_t c = (uint8_t)text[p];
+            if (c == 0) break;
+            node ^= c;
+            const uint32_t u = unit(node);
+            if ((u & ((1u << 31) | 0xFFu)) != c) break;
+            const bool leaf = (u >> 8) & 1;
+            node ^= base(u);
+            if (leaf) {
+                best = p - i + 1;
+                off = unit(node) & ((1u << 31) - 1);
+            }
+        }
+    }
+    if (best > 0 && off < repl_.size()) return {std::string(repl_.c_str() + off), best};
+    // a valid UTF-8 sequence is kept, anything else is one byte -> U+FFFD
+    const uint8_t c = (uint8_t)text[i];
+    const size_t l = c < 0x80 ? 1 : (c >> 5) == 6 ? 2 : (c >> 4) == 14 ? 3 : (c >> 3) == 30 ? 4 : 0;
+    bool ok = l > 0 && i + l <= text.size();
+    for (size_t k = 1; ok && k < l; ++k) ok = ((uint8_t)text[i + k] >> 6) == 2;
+    if (!ok) return {"\xef\xbf\xbd", 1};
+    return {text.substr(i, l), l};
+}
+
+std::string BpeTokenizer::ugm_normalize(const std::string &text) const {
+    const std::string space = escape_ws_ ? "\xe2\x96\x81" : " ";
+    const bool prepend = !ws_suffix_ && add_space_prefix_, append = ws_suffix_ && add_space_prefix_;
+    const bool merge = remove_extra_ws_;
+    bool prepended = false, non_ws = false;
+    std::string o;
+    for (size_t i = 0; i < text.size();) {
+        const auto r = ugm_prefix(text, i);
+        for (char c : r.first) {
+            if (c != ' ') {
+                if (!non_ws) {
+                    non_ws = true;
+                    if ((prepend && !prepended) || merge) {
+                        o += space;
+                        prepended = true;
+                    }
+                }
+                o += c;
+            } else {
+                non_ws = false;
+                if (!merge) o += space;
+            }
+        }
+        i += r.second;
+    }
+    if (append) o += space;
+    return o;
+}
+
+// Viterbi over the normalized bytes: best[e] = the best segmentation of [0, e) (score sums in
+// double, kept as float), every token starting at a code point boundary; a code point no token
+// covers alone may be UNK at unk_score_; backtracked, with runs of UNK merged into one
+void BpeTokenizer::ugm(const std::string &text, std::vector<int32_t> &out) const {
+    const std::string s = ugm_normalize(text);
+    const size_t n = s.size();
+    if (n == 0) return;
+    struct Best {
+        int32_t id;
+        size_t from;
+        float score;
+    };
+    std::vector<Best> best(n + 1, {unk_, 0, -FLT_MAX});
+    best[0] = {unk_, 0, 0.0f};
+    for (size_t i = 0; i < n;) {
+        const uint8_t c = (uint8_t)s[i];
+        const size_t cl = std::min(n - i, (size_t)(c < 0x80 ? 1 : (c >> 5) == 6 ? 2 : (c >> 4) == 14 ? 3 : (c >> 3) == 30 ? 4 : 1));
+        bool single = false;
+        const Best cur = best[i];
+        for (size_t l = 1; l <= std::min(max_tok_len_, n - i); ++l) {
+            const auto it = ugm_tok_.find(s.substr(i, l));
+            if (it == ugm_tok_.end()) continue;
+            if (l == cl) single = true;
+            const double sc = (double)cur.score + (types_[it->second] == 4 ? 0.0 : (double)scores_[it->second]);
+            if (sc > best[i + l].score) best[i + l] = {it->second, i, (float)sc};
+        }
+        if (!single) {
+            const double sc = (double)cur.score + (double)unk_score_;
+            if (sc > best[i + cl].score) best[i + cl] = {unk_, i, (float)sc};
+        }
+        i += cl;
+    }
+    std::vector<int32_t> rev;
+    bool prev_unk = false;
+    for (size_t e = n;;) {
+        const Best &b = best[e];
+        const bool is_unk = b.id == unk_;
+        if (!(prev_unk && is_unk)) rev.push_back(b.id);
+        if (b.from == 0) break;
+        prev_unk = is_unk;
+        e = b.from;
+    }
+    out.insert(out.end(), rev.rbegin(), rev.rend());
 }
 
 // ------------------------------------------------------------------ SPM
@@ -613,6 +785,8 @@ std::vector<int32_t> BpeTokenizer::tokenize(const std::string &text, bool add_sp
         if (run.empty()) return;
         if (wpm_) {
             wpm(run, out);
+        } else if (ugm_) {
+            ugm(run, out);
         } else if (spm_) {
             std::string t = add_space_prefix_ && prev_special ? " " + run : run;
             std::string e;
@@ -653,7 +827,7 @@ std::vector<int32_t> BpeTokenizer::tokenize(const std::string &text, bool add_sp
         }
     }
     flush();
-    if ((spm_ || wpm_) && add_special && add_eos_ && eos_ >= 0) out.push_back(eos_);
+    if ((spm_ || wpm_ || ugm_) && add_special && add_eos_ && eos_ >= 0) out.push_back(eos_);
     if (wpm_ && add_special && add_sep_ && sep_ >= 0) out.push_back(sep_);
     return out;
 }
@@ -662,7 +836,7 @@ std::string BpeTokenizer::piece(int32_t id) const {
     if (id < 0 || id >= (int32_t)tokens_.size()) return "";
     const std::string &t = tokens_[id];
     if (types_[id] == 3 || types_[id] == 4) return t;  // special: rendered as text
-    if (spm_ || wpm_) {
+    if (spm_ || wpm_ || ugm_) {
         // llama_token_to_piece(special = true): UNKNOWN as its text, NORMAL with U+2581 -> ' ',
         // BYTE "<0xXX>" -> the byte, other types (UNUSED) nothing
         if (types_[id] == 2) return t;

@@ -36,6 +36,18 @@
 // word with an unmatched position becomes one UNK. [CLS] (BOS) opens and [SEP] closes the text
 // by default. Checked id for id against HuggingFace `tokenizers`' BERT WordPiece
 // (tests/test_tokenizer_wpm.py).
+//
+// UGM vocabularies (tokenizer.ggml.model == "t5": SentencePiece Unigram, llama.cpp's
+// llm_tokenizer_ugm, restated): a fragment is normalized with the precompiled character map
+// (tokenizer.ggml.precompiled_charsmap: sentencepiece's XOR-compressed double-array trie of
+// input prefixes and their replacements, longest prefix first; user-defined tokens are kept as
+// they are; invalid UTF-8 becomes U+FFFD), spaces become U+2581 with a prefix space
+// (add_space_prefix) and runs merged (remove_extra_whitespaces); then the Viterbi best
+// segmentation by summed token scores (user-defined tokens score 0; a code point no token
+// covers is UNK at the lowest score - 10), consecutive UNKs merged. EOS added by default.
+// Checked id for id against the `sentencepiece` package's Unigram encoder on vocabularies
+// trained with its nmt_nfkc character map and with identity normalization
+// (tests/test_tokenizer_ugm.py).
 #pragma once
 
 #include <cstdint>
@@ -67,6 +79,11 @@ private:
     bool load_spm(const GgufFile &g);
     void wpm(const std::string &text, std::vector<int32_t> &out) const;
     bool load_wpm(const GgufFile &g);
+    void ugm(const std::string &text, std::vector<int32_t> &out) const;
+    bool load_ugm(const GgufFile &g);
+    std::string ugm_normalize(const std::string &text) const;
+    // one normalization step at byte i: the replacement and the input bytes it consumes
+    std::pair<std::string, size_t> ugm_prefix(const std::string &text, size_t i) const;
     // tokens, types, id map, special tokens (shared by the SPM / WPM loaders)
     void load_vocab(const GgufFile &g);
     void pretokenize(const std::string &text, std::vector<std::string> &pieces) const;
@@ -87,6 +104,15 @@ private:
     bool wpm_ = false, add_sep_ = true;
     int32_t sep_ = -1;
     size_t max_tok_len_ = 0;
+    // UGM vocabularies: the character map (double-array units, replacement strings), the
+    // matchable tokens (NORMAL, USER_DEFINED, UNUSED) and user-defined lengths, UNK's score
+    bool ugm_ = false, remove_extra_ws_ = false, escape_ws_ = true, ws_suffix_ = false;
+    std::vector<uint32_t> xcda_;
+    std::string repl_;
+    std::unordered_map<std::string, int32_t> ugm_tok_;
+    std::unordered_map<std::string, int32_t> user_def_;
+    std::vector<size_t> user_def_lens_;  // descending
+    float unk_score_ = 0.0f;
     std::vector<float> scores_;
     int32_t byte_tok_[256];
     // pre-tokenizer family (llama.cpp LLAMA_VOCAB_PRE_TYPE_*): the regex sequence of step 2

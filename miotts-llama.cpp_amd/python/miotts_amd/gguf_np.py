@@ -105,7 +105,8 @@ class GGUFReader:
 
 def write_kv_gguf(path: str, kv: Dict[str, Any]) -> None:
     """Minimal GGUF v3 writer (metadata only, no tensors) for tokenizer tests.
-    Values: str, bool, int (u32), float (f32), list[str], list[int] (i32), list[float] (f32)."""
+    Values: str, bool, int (u32), float (f32), list[str], list[int] (i32), list[float] (f32),
+    bytes (an array of u8, e.g. tokenizer.ggml.precompiled_charsmap)."""
     def s(x: str) -> bytes:
         b = x.encode("utf-8")
         return struct.pack("<Q", len(b)) + b
@@ -121,6 +122,8 @@ def write_kv_gguf(path: str, kv: Dict[str, Any]) -> None:
             out += struct.pack("<If", 6, v)
         elif isinstance(v, str):
             out += struct.pack("<I", 8) + s(v)
+        elif isinstance(v, (bytes, bytearray)):
+            out += struct.pack("<IIQ", 9, 0, len(v)) + bytes(v)
         elif isinstance(v, list) and (not v or isinstance(v[0], str)):
             out += struct.pack("<IIQ", 9, 8, len(v)) + b"".join(s(x) for x in v)
         elif isinstance(v, list) and isinstance(v[0], float):
