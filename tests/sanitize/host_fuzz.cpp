@@ -96,7 +96,7 @@ static bool exercise(const std::string &path, bool expect_ok) {
     }
     mio::BpeTokenizer tk;
     if (tk.load(g)) {
-        const char *texts[] = {"", "hello world", "こんにちは、今日はいい天気ですね。",
+        const char *texts[] = {"", "hello world", "こんにちは、今日はいい天気ですね。", "ＡＢＣ①ｶﾞ Café naïve [SEP]",
                                "<|im_start|>user\n12345 it's<|im_end|>\n", "\xff\xfe\x80 broken \xe3\x81",
                                "   \r\n\t  tabs and  spaces  "};
         for (const char *s : texts)
@@ -111,7 +111,8 @@ static bool exercise(const std::string &path, bool expect_ok) {
     return true;
 }
 
-// usage: host_fuzz DIR [quick|full]  (quick: the CPU suite's budget, one LLM, fewer mutations)
+// usage: host_fuzz DIR [quick|full] [GGUF...]  (quick: the CPU suite's budget, one LLM, fewer
+// mutations; further GGUFs, e.g. tokenizer-only WPM / UGM vocabularies, are fuzzed the same way)
 int main(int argc, char **argv) {
     const std::string dir = argc > 1 ? argv[1] : "/tmp";
     const bool quick = argc > 2 && std::string(argv[2]) == "quick";
@@ -135,6 +136,7 @@ int main(int argc, char **argv) {
         if (!mio::synth_write_voice(v, 7)) std::exit(4);
         files.push_back(v);
     }
+    for (int a = 3; a < argc; ++a) files.push_back(argv[a]);
     std::mt19937_64 rng(1234);
     const std::string mut = dir + "/mut.gguf";
     for (const auto &f : files) {
@@ -143,7 +145,8 @@ int main(int argc, char **argv) {
         const std::vector<uint8_t> b = read_file(f);
         mio::GgufFile g;
         g.open(f);
-        const size_t hdr = g.data_offset();
+        // a file without tensors ends inside the alignment padding its data offset counts
+        const size_t hdr = std::min<size_t>(g.data_offset(), b.size());
         // the tensor-info records close the header (name, n_dims, ne[], type, offset each);
         // the KV section before them is dominated by the vocabulary strings
         size_t ti = 0;
