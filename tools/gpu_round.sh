@@ -2,7 +2,8 @@
 # bench under rocprofv3 kernel trace + stats (graph replays crash rocprofiler-sdk 7.2's
 # queue intercept), and the two PMC passes at decode position ~400.
 # With "configs" as the third argument, also smoke() and the BASELINE config lines C2 (0.1B
-# Q8_0), C4 (2.6B Q8_0, 8 utterances per GPU) and C5 (stream benchmark, 3 runs).
+# Q8_0), C4 (2.6B Q8_0, 8 utterances per GPU; the plain-attention stand-in and the LFM2-2.6B shape)
+# and C5 (stream benchmark, 3 runs).
 # Outputs under gpurun_out/$TAG/.   usage: bash tools/gpu_round.sh TAG [skip-tests|tests] [configs]
 set -e
 tag=${1:-run}
@@ -24,6 +25,7 @@ if [ "$3" = "configs" ]; then
   timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $out/smoke.txt 2>&1
   timeout -k 10 400 python -u bench.py --preset 2 --no-cpu-baseline > $out/c2.json 2> $out/c2.err
   timeout -k 10 400 python -u bench.py --preset 4 --utts-per-gpu 8 --no-cpu-baseline --batch 0 > $out/c4.json 2> $out/c4.err
+  timeout -k 10 400 python -u bench.py --preset 6 --utts-per-gpu 8 --no-cpu-baseline --batch 0 > $out/c4_lfm2.json 2> $out/c4_lfm2.err
   AB_K=3 timeout -k 10 400 python -u tools/stream_ab.py > $out/c5.json 2> $out/c5.err
 fi
 echo done

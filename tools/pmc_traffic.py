@@ -18,7 +18,7 @@ import re
 import sys
 from collections import defaultdict
 
-KERNELS = ["k_attn_in", "k_attention", "k_attn_out", "k_att_o", "k_layer_att", "k_ffn_in", "k_ffn_down", "k_lm_head", "k_sample"]
+KERNELS = ["k_attn_in", "k_attention", "k_attn_out", "k_att_o", "k_layer_att", "k_ffn", "k_ffn_in", "k_ffn_down", "k_lm_head", "k_sample"]
 
 
 def base(name):
