@@ -32,6 +32,10 @@ tools/pmc_traffic.py). step_* = all bytes of one decode step over the step's gra
 cpu_baseline: the C oracle (oracle/, "port") on rank 0 at N=1 only, timed on a bounded
 sample (decode steps at positions spread over 0..700 + codec/iSTFT of a few codes) and
 extrapolated to one utterance, at the box's thread share and at 4 threads.
+baseline_configs (N=1, after everything else; --no-configs skips): the other BASELINE configs,
+each in a child process with its own timed region at short K — C2 (0.1B Q8_0), C4 per GPU on
+the 2.6B Q8_0 stand-in and on the LFM2-2.6B shape (8 utterances decoded together), and C5 (the
+miotts-stream-benchmark CLI's own clock); never part of `value`.
 """
 import argparse
 import json
@@ -72,6 +76,8 @@ def parse_args(argv=None):
     p.add_argument("--batch", type=int, default=8,
                    help="also time B utterances decoded together per GPU (N=1 only; 0 = skip)")
     p.add_argument("--no-roofline", action="store_true")
+    p.add_argument("--no-configs", action="store_true",
+                   help="skip the other BASELINE config lines (C2, C4 on both 2.6B shapes, C5) a default N=1 run adds")
     p.add_argument("--launcher-selftest", action="store_true",
                    help="tests only: the launcher + timed region with a CPU sleep as the utterance, no GPU; "
                         "prints a 'launcher self-test' line, never the metric")
@@ -269,6 +275,47 @@ def make_batch_step(tokens, B, llm, codec, dev, prompt, allow, d_emb, d_pcm):
         return sum(lens), t1 - t0, c_ms, 0.0
 
     return step
+
+
+def baseline_configs(a, llm_path, codec_path, voice_path):
+    """The other BASELINE.json configs, each in a child process after the timed region (N=1,
+    rank 0): C2 (0.1B Q8_0, one utterance per step), C4 per GPU (2.6B Q8_0, 8 utterances decoded
+    together; the plain-attention stand-in and the LFM2-2.6B shape), and C5 (the streaming
+    benchmark CLI, miotts-stream-benchmark, 1.7B Q4_K_M, 700 tokens: test-to-speech.cpp:435-614).
+    Each is this script's own timed region (or the CLI's own clock) at short K; a failure is
+    recorded in its entry and never touches the headline line."""
+    import re
+    import subprocess
+    res = {}
+    me, py = os.path.abspath(__file__), sys.executable
+    common = ["--no-cpu-baseline", "--batch", "0", "--no-roofline", "--no-configs", "--workdir", a.workdir,
+              "--tokens", str(a.tokens)]
+    runs = {"C2_0p1b_q8_single": ["--preset", "2", "--steps", "3", "--warmup", "1"],
+            "C4_2p6b_q8_8_per_gpu": ["--preset", "4", "--utts-per-gpu", "8", "--steps", "1", "--warmup", "1"],
+            "C4_2p6b_lfm2_8_per_gpu": ["--preset", "6", "--utts-per-gpu", "8", "--steps", "1", "--warmup", "1"]}
+    for name, args in runs.items():
+        t0 = time.perf_counter()
+        try:
+            p = subprocess.run([py, me] + args + common, capture_output=True, text=True, timeout=400)
+            line = json.loads(p.stdout.strip().splitlines()[-1])
+            res[name] = {"value": line["value"], "unit": line["unit"], "ms_per_step": line["ms_per_step"],
+                         "steps": line["steps"], "config": line["config"], "stage_ms": line.get("stage_ms"),
+                         "child_wall_s": round(time.perf_counter() - t0, 1)}
+        except Exception as e:  # noqa: BLE001 - reported, the headline line stands
+            res[name] = {"error": repr(e)[:400]}
+    t0 = time.perf_counter()
+    try:
+        exe = os.path.join(REPO, "miotts-llama.cpp_amd", "build", "miotts-stream-benchmark")
+        p = subprocess.run([exe, "-m", llm_path, "-c", codec_path, "-v", voice_path, "-p", PROMPT, "--max-tokens",
+                            str(a.tokens), "--speech-only", "--ignore-eos"], capture_output=True, text=True, timeout=300)
+        kv = {k: float(v) for k, v in re.findall(r"^stream_bench\.([\w.]+)=([-\d.eE+]+)", p.stdout, re.M)}
+        res["C5_stream_1p7b"] = {"value": round(kv["x_realtime"], 3), "unit": "x realtime (audio s / wall s)",
+                                 "stream_bench": kv, "child_wall_s": round(time.perf_counter() - t0, 1),
+                                 "config": {"workload": "miotts-stream-benchmark, 1.7B Q4_K_M synthetic, "
+                                                        f"{a.tokens} speech tokens, 20-token checks"}}
+    except Exception as e:  # noqa: BLE001
+        res["C5_stream_1p7b"] = {"error": repr(e)[:400]}
+    return res
 
 
 def utterance_seed(rank: int, index: int) -> int:
@@ -570,6 +617,8 @@ def main():
                                                      a.cpu_codes // 2, a.tokens, 4)
         if not a.no_cpu_c1:
             out["cpu_baseline_c1"] = cpu_baseline_c1(a.workdir, a.tokens, share)
+    if rank == 0 and world == 1 and B == 1 and not a.no_configs:
+        out["baseline_configs"] = baseline_configs(a, llm_path, codec_path, voice_path)
     if rank == 0:
         print(json.dumps(out, ensure_ascii=False), flush=True)
     if dist is not None:
