@@ -231,6 +231,9 @@ struct TestToSpeech::Impl {
     // PCM of the last decode in HBM (f32) and its PCM16 image (synthesize_to_file)
     void *d_pcm = nullptr, *d_pcm16 = nullptr;
     size_t pcm_cap = 0, pcm16_cap = 0;
+    // batch synthesis: one f32 PCM buffer per utterance of a group (concurrent codec decodes)
+    std::vector<void *> d_pcmb;
+    std::vector<size_t> pcmb_cap;
     // streaming decodes run on their own stream, beside the LLM's next check interval
     hipStream_t cstream = nullptr;
 
@@ -239,6 +242,8 @@ struct TestToSpeech::Impl {
         if (llm) mio_hip_llm_free(llm);
         if (dev && d_pcm) mio_hip_free(dev, d_pcm);
         if (dev && d_pcm16) mio_hip_free(dev, d_pcm16);
+        for (void *p : d_pcmb)
+            if (dev && p) mio_hip_free(dev, p);
         miocodec_free(codec);
     }
 
@@ -485,7 +490,8 @@ bool TestToSpeech::synthesize_to_file(const VoiceModel &voice, const std::string
 }
 
 // Batched synthesis (extension): prompts in groups of up to 16 through the batched decode
-// engine, then codec + iSTFT + the PCM epilogue per utterance as synthesize_to_file does it.
+// engine, the group's codec + iSTFT decodes concurrently, then the PCM epilogue per utterance as
+// synthesize_to_file does it.
 // Every stream uses synthesize_to_file's seed, so each file has the bytes a single call writes
 // (mio_hip_llm_generate_batch's streams equal mio_hip_llm_generate of their prompts).
 bool TestToSpeech::synthesize_batch_to_files(const VoiceModel &voice, const std::vector<std::string> &texts,
@@ -532,17 +538,45 @@ bool TestToSpeech::synthesize_batch_to_files(const VoiceModel &voice, const std:
                 if (!synthesize_to_file(voice, texts[g0 + b], output_paths[g0 + b], options)) return false;
             continue;
         }
+        // every stream's codes decoded concurrently (mio_hip_codec_decode_pcm_batch: the same
+        // kernels per utterance, so the PCM is a single decode's), then synthesize_to_file's
+        // epilogue (peak normalisation + PCM16 on the device, WAV) per utterance
+        std::vector<std::vector<int32_t>> codes((size_t)B);
         for (int b = 0; b < B; ++b) {
             std::string text;
             for (int i = 0; i < n_out[b]; ++i) text += I.tok.piece(toks[(size_t)b * max_tokens + i]);
-            if (!synthesize_to_file(voice, text, output_paths[g0 + b], [&] {
-                    Options o = options;
-                    o.skip_llm = true;
-                    return o;
-                }())) {
+            const std::vector<int> c = parse_speech_tokens(text);
+            if (c.empty()) {
+                fprintf(stderr, "TestToSpeech: no speech codes parsed from text\n");
                 fprintf(stderr, "TestToSpeech: utterance %zu failed\n", g0 + b);
                 return false;
             }
+            codes[b].assign(c.begin(), c.end());
+        }
+        I.d_pcmb.resize(std::max(I.d_pcmb.size(), (size_t)B), nullptr);
+        I.pcmb_cap.resize(I.d_pcmb.size(), 0);
+        std::vector<const int32_t *> cp((size_t)B);
+        std::vector<float *> op((size_t)B);
+        std::vector<int> nc((size_t)B), len((size_t)B);
+        for (int b = 0; b < B; ++b) {
+            if (!I.ensure(I.d_pcmb[b], I.pcmb_cap[b], codes[b].size() * I.spt * sizeof(float) + 64)) return false;
+            cp[b] = codes[b].data(), op[b] = (float *)I.d_pcmb[b], nc[b] = (int)codes[b].size();
+        }
+        if (mio_hip_codec_decode_pcm_batch(I.codec->codec, cp.data(), nc.data(), B, voice.embedding().data(), op.data(),
+                                           len.data(), MIO_OUT_DEVICE, nullptr) != MIO_OK) {
+            fprintf(stderr, "TestToSpeech: codec decode failed: %s\n", mio_hip_last_error());
+            return false;
+        }
+        for (int b = 0; b < B; ++b) {
+            std::vector<int16_t> pcm16((size_t)len[b]);
+            if (!I.ensure(I.d_pcm16, I.pcm16_cap, (size_t)len[b] * 2 + 64) ||
+                mio_hip_pcm_finish(I.dev, op[b], len[b], options.apply_peak_normalization ? 1 : 0,
+                                   (int16_t *)I.d_pcm16, nullptr, nullptr) != MIO_OK ||
+                (len[b] && mio_hip_memcpy_d2h(I.dev, pcm16.data(), I.d_pcm16, (size_t)len[b] * 2) != MIO_OK)) {
+                fprintf(stderr, "TestToSpeech: PCM epilogue failed: %s\n", mio_hip_last_error());
+                return false;
+            }
+            if (!mio::wav_write_pcm16(output_paths[g0 + b], pcm16.data(), pcm16.size(), sample_rate())) return false;
         }
     }
     return true;
