@@ -923,6 +923,11 @@ __device__ __forceinline__ v4f kqp_val(const KqPass<T> &p, const v4i (&x)[4], in
         return q6p_val(p, x, s, da);
 }
 
+// MIO_MMQ_XPRE (A/B builds; default 1): k_mmq16's residual epilogue adds values loaded at the
+// tile's start instead of loading them behind the reduction
+#ifndef MIO_MMQ_XPRE
+#define MIO_MMQ_XPRE 1
+#endif
 // QNP > 0 (k_mmq16q): the first a.nt workgroups are quantization producers (MmqQuant, XRegs
 // of QNP passes, QM = its mode), the tiles follow and wait before their activation reads.
 template <int T0, int T1, int T2, int MODE, int KP = 0, int QNP = 0, int QM = 0>
@@ -961,6 +966,19 @@ __global__ __launch_bounds__(MMQ_NT) void k_mmq16(MmqSeg s0, MmqSeg s1, MmqSeg s
     };
     auto run = [&]<int T>(const MmqSeg &sg, int ti) {
         const int row0 = ti * RT16, row = min(row0 + (lane & 15), sg.w.rows - 1);
+        // MMQ_RESID: the residual values wave 0's epilogue adds, loaded before anything else
+        // (the launch before this one wrote them; read at the end they were a dependent
+        // round trip behind the reduction)
+        float xres[4] = {0.f, 0.f, 0.f, 0.f};
+        if constexpr (MODE == MMQ_RESID && MIO_MMQ_XPRE) {
+            if (wave == 0 && row0 + (lane & 15) < sg.w.rows) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int t = t0 + tok16(lane, i);
+                    if (t < a.nt) xres[i] = a.out[(size_t)t * a.ld + sg.out_off + row0 + (lane & 15)];
+                }
+            }
+        }
         // the slot index must be wave-uniform (divergent branches around the MFMAs would run
         // them with a partial EXEC)
         const int k = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1043,7 +1061,7 @@ __global__ __launch_bounds__(MMQ_NT) void k_mmq16(MmqSeg s0, MmqSeg s1, MmqSeg s
             if (t >= a.nt) continue;
             float *o = a.out + (size_t)t * a.ld + sg.out_off + orow;
             if constexpr (MODE == MMQ_STORE) *o = y[i];
-            else if constexpr (MODE == MMQ_RESID) *o = y[i] + *o;
+            else if constexpr (MODE == MMQ_RESID) *o = y[i] + (MIO_MMQ_XPRE ? xres[i] : *o);
             else *o = silu_f(y[i]) * u[i];
         }
     };
