@@ -565,12 +565,17 @@ __device__ __forceinline__ float ld_scale(const char *base, size_t off, bool sc1
     return *reinterpret_cast<const float *>(base + off);
 }
 
-// this lane's activation codes of superblock s, swap_halves'd
+// this lane's activation codes of superblock s (kq_act_ld: the loads alone, so a caller can
+// issue them ahead of the scales' staging round trip; kq_act: loaded and swap_halves'd)
 template <class AP>
-__device__ __forceinline__ void kq_act(const AP &aq, int s, v4i (&x)[4]) {
+__device__ __forceinline__ void kq_act_ld(const AP &aq, int s, v4i (&x)[4]) {
     const int g = (threadIdx.x & 63) >> 4;
 #pragma unroll
     for (int c = 0; c < 4; ++c) x[c] = ld_act16(aq, s * 256 + 64 * c + 16 * g);
+}
+template <class AP>
+__device__ __forceinline__ void kq_act(const AP &aq, int s, v4i (&x)[4]) {
+    kq_act_ld(aq, s, x);
 #pragma unroll
     for (int c = 0; c < 4; ++c) swap_halves(x[c]);
 }
@@ -928,6 +933,23 @@ __device__ __forceinline__ v4f kqp_val(const KqPass<T> &p, const v4i (&x)[4], in
 #ifndef MIO_MMQ_XPRE
 #define MIO_MMQ_XPRE 1
 #endif
+// MIO_LOOP_D (A/B builds; default 4): tiles whose weights a tile-walking workgroup
+// (k_mmq16_loop, k_mmq16_loop_kq) holds: D - 1 in flight while one is reduced (2 = the
+// ping-pong of rounds 4-5; 4 holds every tile of the 1.7B / 2.6B gate|up walks, <= 4 per
+// workgroup, before the producers' wait)
+#ifndef MIO_LOOP_D
+#define MIO_LOOP_D 4
+#endif
+// MIO_LOOP_DQ8: the same for the Q8_0 walk (k_mmq16_loop), 3 (the 2.6B gate|up's <= 3 tiles per
+// workgroup; 4 Q8_0 W | U sets exceed 256 VGPRs)
+#ifndef MIO_LOOP_DQ8
+#define MIO_LOOP_DQ8 3
+#endif
+// MIO_MMQ_ACT1 (A/B builds; default 1): the K-quant tiles issue their weights, then their
+// activation codes, then the scales' staging (one activation round trip instead of two)
+#ifndef MIO_MMQ_ACT1
+#define MIO_MMQ_ACT1 1
+#endif
 // QNP > 0 (k_mmq16q): the first a.nt workgroups are quantization producers (MmqQuant, XRegs
 // of QNP passes, QM = its mode), the tiles follow and wait before their activation reads.
 template <int T0, int T1, int T2, int MODE, int KP = 0, int QNP = 0, int QM = 0>
@@ -1015,24 +1037,47 @@ __global__ __launch_bounds__(MMQ_NT) void k_mmq16(MmqSeg s0, MmqSeg s1, MmqSeg s
             slot16_store(y, red);
             if constexpr (NV == 2) slot16_store(u, red + MMQ_NT * 4);
         } else {
-            if constexpr (QF && NV == 1 && (T == 12 || T == 14)) {
-                // in-launch quantization: up to three passes' weights (K <= 6144, the 1.7B down)
-                // are in flight while the producers quantize; then slot16_kq's arithmetic
+            if constexpr (NV == 1 && (T == 12 || T == 14) && (QF || MIO_MMQ_ACT1)) {
+                // up to three passes' weights (K <= 6144, the 1.7B down) are in flight before
+                // the activations are read (with in-launch quantization: while the producers
+                // quantize); then slot16_kq's arithmetic. MIO_MMQ_ACT1: the activation codes of
+                // every pass are issued before the scales' staging, so codes and scales arrive
+                // in one round trip (and the launches without producers, the O, take this path
+                // too)
+                // register sets for NPX passes: 3 for the plain-row down (K <= 6144), one
+                // elsewhere (K <= 2048: the q|k|v launch must stay at <= 128 VGPRs, two
+                // workgroups per CU, for its 256 tiles + producers); longer K: the generic path
+                constexpr int NPX = QF && QM == 1 ? 3 : 1;
                 const int nsb = sg.w.k >> 8, np = (nsb + 7) / 8;
-                if (q.early && np <= 3) {
-                    KqPass<T> ps[3];
+                if ((!QF || q.early) && np <= NPX) {
+                    KqPass<T> ps[NPX];
 #pragma unroll
-                    for (int p = 0; p < 3; ++p)
+                    for (int p = 0; p < NPX; ++p)
                         if (p < np) kqp_load<T>(sg.w, row, min(p * 8 + k, nsb - 1), ps[p]);
                     wait_act();
+#if MIO_MMQ_ACT1
+                    const auto aq = act16_codes<QF>(a, t0);
+                    v4i xs[NPX][4];
+#pragma unroll
+                    for (int p = 0; p < NPX; ++p)
+                        if (p < np) kq_act_ld(aq, min(p * 8 + k, nsb - 1), xs[p]);
+                    stage_act16<T, QF>(a, t0, a.K, da);
+#else
                     const auto aq = stage_act16<T, QF>(a, t0, a.K, da);
+#endif
                     v4f acc = {};
 #pragma unroll
-                    for (int p = 0; p < 3; ++p) {
+                    for (int p = 0; p < NPX; ++p) {
                         if (p < np) {
                             const int s = p * 8 + k;
+#if MIO_MMQ_ACT1
+                            v4i(&x)[4] = xs[p];
+#pragma unroll
+                            for (int c = 0; c < 4; ++c) swap_halves(x[c]);
+#else
                             v4i x[4];
                             kq_act(aq, min(s, nsb - 1), x);
+#endif
                             v4f v = {};
                             if (s < nsb) v = kqp_val<T>(ps[p], x, s, da);
                             acc = acc + v;  // the decode lane's pass accumulation (0 + v0 + v1 ...)
@@ -1107,9 +1152,17 @@ __global__ __launch_bounds__(MMQ_NT) void k_mmq16_loop(MmqSeg s0, MmqArgs a, Mmq
     if (tile >= n_tiles) return;
     const int nb = a.K >> 5;
     auto row_of = [&](int ti) { return min(ti * RT16 + (lane & 15), s0.w.rows - 1); };
-    Q80Pass wA, uA, wB, uB;
-    q80p_load(s0.w, row_of(tile), 0, k, wA);
-    if constexpr (NV == 2) q80p_load(a.w_up, row_of(tile), 0, k, uA);
+    // ring of D tiles' weights: D - 1 tiles in flight while one is reduced
+    constexpr int D = MIO_LOOP_DQ8;
+    Q80Pass w[D], u[D];
+#pragma unroll
+    for (int d = 0; d < D - 1; ++d) {
+        const int ti = tile + d * G;
+        if (ti < n_tiles) {
+            q80p_load(s0.w, row_of(ti), 0, k, w[d]);
+            if constexpr (NV == 2) q80p_load(a.w_up, row_of(ti), 0, k, u[d]);
+        }
+    }
     if constexpr (QF) {  // the records' loads below are sc1 (ActSc1)
         if (threadIdx.x == 0) wait_count(q.cnt + 64 * (blockIdx.x & 7), a.nt, q.flag);
         asm volatile("s_barrier" ::: "memory");
@@ -1120,11 +1173,14 @@ __global__ __launch_bounds__(MMQ_NT) void k_mmq16_loop(MmqSeg s0, MmqArgs a, Mmq
     stage_act16<8, QF>(a, 0, a.K, da);
 #pragma unroll
     for (int i = 0; i < 4; ++i) swap_halves(x[i]);
-    // one tile: the next tile's loads (clamped to this tile at the end: L2 hits) go out first
+    // one tile: the loads of the tile D - 1 ahead go out first, into the set the previous
+    // tile freed
     auto step = [&](Q80Pass &cw, Q80Pass &cu, Q80Pass &nw, Q80Pass &nu) -> bool {
-        const int next = tile + G < n_tiles ? tile + G : tile;
-        q80p_load(s0.w, row_of(next), 0, k, nw);
-        if constexpr (NV == 2) q80p_load(a.w_up, row_of(next), 0, k, nu);
+        const int ahead = tile + (D - 1) * G;
+        if (ahead < n_tiles) {
+            q80p_load(s0.w, row_of(ahead), 0, k, nw);
+            if constexpr (NV == 2) q80p_load(a.w_up, row_of(ahead), 0, k, nu);
+        }
         v4f acc[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) acc[i] = v4f{};
@@ -1155,13 +1211,14 @@ __global__ __launch_bounds__(MMQ_NT) void k_mmq16_loop(MmqSeg s0, MmqArgs a, Mmq
             }
         }
         __syncthreads();  // red is rewritten by the next tile
-        if (next == tile) return false;
-        tile = next;
+        if (tile + G >= n_tiles) return false;
+        tile += G;
         return true;
     };
     for (;;) {
-        if (!step(wA, uA, wB, uB)) break;
-        if (!step(wB, uB, wA, uA)) break;
+#pragma unroll
+        for (int d = 0; d < D; ++d)
+            if (!step(w[d], u[d], w[(d + D - 1) % D], u[(d + D - 1) % D])) return;
     }
 }
 
@@ -1194,20 +1251,38 @@ __global__ __launch_bounds__(MMQ_NT) void k_mmq16_loop_kq(MmqSeg s0, MmqArgs a, 
     const bool live = k < (a.K >> 8);  // wave-uniform: this wave's superblock exists
     const int sb = live ? k : 0;
     auto row_of = [&](int ti) { return min(ti * RT16 + (lane & 15), s0.w.rows - 1); };
-    KqPass<T> wA, uA, wB, uB;
-    kqp_load<T>(s0.w, row_of(tile), sb, wA);
-    if constexpr (NV == 2) kqp_load<T>(a.w_up, row_of(tile), sb, uA);
+    // ring of D tiles' weights: D - 1 tiles in flight while one is reduced
+    constexpr int D = MIO_LOOP_D;
+    KqPass<T> w[D], u[D];
+#pragma unroll
+    for (int d = 0; d < D - 1; ++d) {
+        const int ti = tile + d * G;
+        if (ti < n_tiles) {
+            kqp_load<T>(s0.w, row_of(ti), sb, w[d]);
+            if constexpr (NV == 2) kqp_load<T>(a.w_up, row_of(ti), sb, u[d]);
+        }
+    }
     if constexpr (QF) {  // the records' loads below are sc1 (ActSc1)
         if (threadIdx.x == 0) wait_count(q.cnt + 64 * (blockIdx.x & 7), a.nt, q.flag);
         asm volatile("s_barrier" ::: "memory");
     }
-    const auto aq = stage_act16<T, QF>(a, 0, a.K, da);
     v4i x[4];
+#if MIO_MMQ_ACT1
+    // codes issued ahead of the scales' staging: one round trip for both
+    kq_act_ld(act16_codes<QF>(a, 0), sb, x);
+    stage_act16<T, QF>(a, 0, a.K, da);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) swap_halves(x[c]);
+#else
+    const auto aq = stage_act16<T, QF>(a, 0, a.K, da);
     kq_act(aq, sb, x);
+#endif
     auto step = [&](KqPass<T> &cw, KqPass<T> &cu, KqPass<T> &nw, KqPass<T> &nu) -> bool {
-        const int next = tile + G < n_tiles ? tile + G : tile;
-        kqp_load<T>(s0.w, row_of(next), sb, nw);
-        if constexpr (NV == 2) kqp_load<T>(a.w_up, row_of(next), sb, nu);
+        const int ahead = tile + (D - 1) * G;
+        if (ahead < n_tiles) {
+            kqp_load<T>(s0.w, row_of(ahead), sb, nw);
+            if constexpr (NV == 2) kqp_load<T>(a.w_up, row_of(ahead), sb, nu);
+        }
         {
             v4f acc = {}, v = {};
             if (live) v = kqp_val<T>(cw, x, sb, da);
@@ -1239,13 +1314,14 @@ __global__ __launch_bounds__(MMQ_NT) void k_mmq16_loop_kq(MmqSeg s0, MmqArgs a, 
             }
         }
         __syncthreads();  // red is rewritten by the next tile
-        if (next == tile) return false;
-        tile = next;
+        if (tile + G >= n_tiles) return false;
+        tile += G;
         return true;
     };
     for (;;) {
-        if (!step(wA, uA, wB, uB)) break;
-        if (!step(wB, uB, wA, uA)) break;
+#pragma unroll
+        for (int d = 0; d < D; ++d)
+            if (!step(w[d], u[d], w[(d + D - 1) % D], u[(d + D - 1) % D])) return;
     }
 }
 }  // namespace
