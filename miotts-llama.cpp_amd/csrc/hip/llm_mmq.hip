@@ -1229,7 +1229,11 @@ __global__ __launch_bounds__(MMQ_NT) void k_mmq16_loop(MmqSeg s0, MmqArgs a, Mmq
 // one is reduced. Per tile the arithmetic is k_mmq16's slot16_kq (the 0 + v pass sum,
 // slot16_sum, the same epilogue): bit-identical. QNP > 0: the first a.nt workgroups are the
 // in-launch quantization producers (as k_mmq16_loop).
-template <int T, int MODE, int QNP, int QM>
+// IQ (QNP 0, RMSNorm rows, nt <= 8, K <= 2048): no producer workgroups; every walking
+// workgroup RMSNorm-quantizes the nt token rows itself, one wave per token (xpre_issue before
+// its weight loads, xpre_quant into LDS records: k_bt_quant's bits), and reads the records from
+// LDS; workgroup 0 zeroes the other counter set as a producer would.
+template <int T, int MODE, int QNP, int QM, bool IQ = false>
 __global__ __launch_bounds__(MMQ_NT) void k_mmq16_loop_kq(MmqSeg s0, MmqArgs a, MmqQuant q, int n_tiles) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     constexpr int NV = MODE == MMQ_SWIGLU ? 2 : 1;
@@ -1251,6 +1255,15 @@ __global__ __launch_bounds__(MMQ_NT) void k_mmq16_loop_kq(MmqSeg s0, MmqArgs a, 
     const bool live = k < (a.K >> 8);  // wave-uniform: this wave's superblock exists
     const int sb = live ? k : 0;
     auto row_of = [&](int ti) { return min(ti * RT16 + (lane & 15), s0.w.rows - 1); };
+    static_assert(!IQ || (QNP == 0 && NV == 2), "in-prologue quantization: the gate|up walk");
+    char *rec = reinterpret_cast<char *>(da + (a.K >> 8) * TT16);  // IQ: the nt records
+    XPre xp;
+    if constexpr (IQ) {
+        if (blockIdx.x == 0 && threadIdx.x < 8)
+            __hip_atomic_store((__attribute__((address_space(1))) int *)(q.other + 64 * threadIdx.x), 0,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        xpre_issue(q.src, q.norm_w, a.K, a.nt, xp);
+    }
     // ring of D tiles' weights: D - 1 tiles in flight while one is reduced
     constexpr int D = MIO_LOOP_D;
     KqPass<T> w[D], u[D];
@@ -1266,15 +1279,20 @@ __global__ __launch_bounds__(MMQ_NT) void k_mmq16_loop_kq(MmqSeg s0, MmqArgs a, 
         if (threadIdx.x == 0) wait_count(q.cnt + 64 * (blockIdx.x & 7), a.nt, q.flag);
         asm volatile("s_barrier" ::: "memory");
     }
+    MmqArgs al = a;
+    if constexpr (IQ) {
+        xpre_quant(xp, a.K, q.eps, true, rec, a.nt);
+        al.act = rec, al.act_stride = act_bytes(a.K);
+    }
     v4i x[4];
 #if MIO_MMQ_ACT1
     // codes issued ahead of the scales' staging: one round trip for both
-    kq_act_ld(act16_codes<QF>(a, 0), sb, x);
-    stage_act16<T, QF>(a, 0, a.K, da);
+    kq_act_ld(act16_codes<QF>(al, 0), sb, x);
+    stage_act16<T, QF>(al, 0, a.K, da);
 #pragma unroll
     for (int c = 0; c < 4; ++c) swap_halves(x[c]);
 #else
-    const auto aq = stage_act16<T, QF>(a, 0, a.K, da);
+    const auto aq = stage_act16<T, QF>(al, 0, a.K, da);
     kq_act(aq, sb, x);
 #endif
     auto step = [&](KqPass<T> &cw, KqPass<T> &cu, KqPass<T> &nw, KqPass<T> &nu) -> bool {
@@ -1494,6 +1512,20 @@ bool launch_mmq_q(const MmqSeg *seg, const int *types, int nseg, int mode, const
         return go(k_mmq16<8, 8, 8, MMQ_STORE, 1, 1, 0>);
     if (mode == MMQ_SWIGLU && nseg == 1 && q.mode == 0 && np == 1) {
         if (types[0] == 12) {
+            // MIO_BT_IQ=1 (opt-in): the walk quantizes its <= 8 tokens in its own prologue instead
+            // of behind producer workgroups. Bit-exact, but 8 streams 1.7B 1.366 vs 1.252 ms per
+            // step (profiles/r06/bt_iq_ab.txt): one wave per token quantizing 8 superblocks in a
+            // row is a longer chain than the producers' hop
+            static const bool iq = getenv("MIO_BT_IQ") && getenv("MIO_BT_IQ")[0] == '1';
+            if (iq && a.nt <= 8 && a.K % 256 == 0 && a.K <= 2048 && tiles > n_cu() && mmq_loop_on() &&
+                (kq_loop_mask() & 2)) {
+                auto kern = k_mmq16_loop_kq<12, MMQ_SWIGLU, 0, 0, true>;
+                const size_t l = (size_t)2 * MMQ_NT * 4 * sizeof(float) + (size_t)(a.K / 256) * TT16 * sizeof(float) +
+                                 (size_t)a.nt * act_bytes(a.K);
+                if (l > 64 * 1024) allow_lds_mmq(reinterpret_cast<const void *>(kern));
+                hipLaunchKernelGGL(kern, dim3(n_cu()), dim3(MMQ_NT), l, s, sg[0], a, q, tiles);
+                return true;
+            }
             const int nl = n_cu() - a.nt;  // the producers keep CUs of their own
             if (a.K % 256 == 0 && a.K <= 2048 && tiles > nl && nl > 0 && mmq_loop_on() && (kq_loop_mask() & 2)) {
                 auto kern = k_mmq16_loop_kq<12, MMQ_SWIGLU, 1, 0>;

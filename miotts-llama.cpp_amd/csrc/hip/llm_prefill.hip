@@ -417,81 +417,8 @@ __device__ __forceinline__ void act_store(const ActPre<NP> &ap, const char *act,
     lds_barrier();
 }
 
-// In-launch RMSNorm + quantization with the inputs loaded AHEAD of the weights (batched
-// decode, K <= 2048, nt <= 8 tokens: wave t quantizes token t). The token row and the norm
-// weights sit in registers (lane l, register vw: elements
-// vw * 256 + 4 l .. +3, i.e. superblock vw / Q8_0 blocks 8 vw .. 8 vw + 7), issued before the
-// first weight group, so the quantization waits only for them (in-order vmcnt) and never
-// re-reads the row. The arithmetic is the workgroup prologue's (rmsnorm_quant), replayed by one
-// wave: the sum of squares accumulates per virtual thread tid = 64 vw + lane over its elements
-// (tid + i MT) * 4 in order, each virtual wave reduces by the same DPP tree (wave_sum_d) and
-// the 8 partial sums add in wave order as block_sum does; each superblock / block is quantized
-// by q8k_store / q80_store as any wave of the workgroup would, so the records equal
-// k_bt_quant's bit for bit. Saves the k_bt_quant launch in front of the matvec.
-struct XPre {
-    float4 x[MW], w[MW];
-};
-__device__ __forceinline__ void xpre_issue(const float *src, const float *norm_w, int K, int nt, XPre &xp) {
-    const int lane = threadIdx.x & 63;
-    const int t = min((int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6), nt - 1);
-    const float *x = src + (size_t)t * K;
-#pragma unroll
-    for (int vw = 0; vw < MW; ++vw) {
-        const int e = min(vw * 256 + 4 * lane, K - 4);
-        xp.x[vw] = ld4(x + e);
-        xp.w[vw] = ld4(norm_w + e);
-    }
-}
-__device__ __forceinline__ void xpre_quant(const XPre &xp, int K, float eps, bool kq, char *smem, int nt) {
-    const int lane = threadIdx.x & 63;
-    const int t = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (t < nt) {
-        const ActL a = carve_t(smem, K, t).a;
-        double tot = 0.0;
-#pragma unroll
-        for (int vw = 0; vw < MW; ++vw) {
-            const int e = vw * 256 + 4 * lane;
-            const float4 v = xp.x[vw];
-            double acc = 0.0;
-            if (e < K) {
-                acc += (double)(v.x * v.x);
-                acc += (double)(v.y * v.y);
-                acc += (double)(v.z * v.z);
-                acc += (double)(v.w * v.w);
-            }
-            tot += wave_sum_d(acc);
-        }
-        const float scale = rms_scale(tot, K, eps);
-        auto val4 = [&](int vw, float (&v)[4]) {
-            const float4 xv = xp.x[vw], w = xp.w[vw];
-            float q;
-            q = xv.x * scale, v[0] = q * w.x;
-            q = xv.y * scale, v[1] = q * w.y;
-            q = xv.z * scale, v[2] = q * w.z;
-            q = xv.w * scale, v[3] = q * w.w;
-        };
-        if (kq) {
-#pragma unroll
-            for (int b = 0; b < MW; ++b)
-                if (b < K / 256) {
-                    float v[4];
-                    val4(b, v);
-                    q8k_store(v, abs_max4(v), b, a);
-                }
-        } else {
-            const int nb = K / 32;
-#pragma unroll
-            for (int m = 0; m < MW; ++m)
-                if (8 * m < nb) {
-                    const int b = 8 * m + (lane >> 3);
-                    float v[4];
-                    val4(m, v);
-                    q80_store(v, b, b < nb, a);
-                }
-        }
-    }
-    lds_barrier();
-}
+// XPre / xpre_issue / xpre_quant (the in-launch RMSNorm + quantization of up to 8 tokens by
+// one wave each): llm_quant_producer.h
 
 // One workgroup per token t: MODE 0 RMSNorm(src[t]) * norm_w, 1 src[t] as is (the attention
 // output pb.att, h); quantized (Q8_K / Q8_0) into the token's act record.

@@ -183,7 +183,8 @@ print(h.hexdigest())
 
 
 @pytest.mark.parametrize("preset,variants", [
-    (3, [{"MIO_BT_LM_MMQ": "0"}, {"MIO_MMQ_LOOP_KQ": "0"}, {"MIO_KQ_EARLY": "0"}, {"MIO_BT_QCHUNK": "0"}]),
+    (3, [{"MIO_BT_LM_MMQ": "0"}, {"MIO_MMQ_LOOP_KQ": "0"}, {"MIO_KQ_EARLY": "0"}, {"MIO_BT_QCHUNK": "0"},
+         {"MIO_BT_IQ": "1"}]),
     (4, [{"MIO_BT_DQ": "0"}, {"MIO_BT_FQ": "1"}, {"MIO_BT_LM_MMQ": "0"}, {"MIO_MMQ_LOOP": "0"}]),
 ])
 def test_batch_engine_switches_bit_identical(synth_llm_path, tmp_path, preset, variants):
@@ -191,7 +192,8 @@ def test_batch_engine_switches_bit_identical(synth_llm_path, tmp_path, preset, v
     24 tokens are identical with each switched back (a fresh process per variant; the switches
     are read once). 1.7B Q4_K_M: the lm_head on the matrix cores vs k_bt_lm_head's dot4, the
     K-quant tile loops vs one workgroup per tile, weight loads before vs after the in-launch
-    producers' wait, chunked vs per-token producers. 2.6B Q8_0: the dot4 down quantizing h in
+    producers' wait, chunked vs per-token producers, the gate|up walk quantizing its tokens in
+    its own prologue (r06, opt-in MIO_BT_IQ=1) vs producer workgroups. 2.6B Q8_0: the dot4 down quantizing h in
     its launch vs behind k_bt_quant_split, q|k|v on the matrix cores vs the dot4 in-launch path,
     the lm_head engines, the Q8_0 tile loops."""
     import os
