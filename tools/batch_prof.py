@@ -18,7 +18,7 @@ if not os.path.exists(path):
     m.synth_llm(path + ".tmp", preset, 1)
     os.replace(path + ".tmp", path)
 dev = m.Device(0)
-llm = m.Llm(dev, path, 2048)
+llm = m.Llm(dev, path, int(os.environ.get("AB_NCTX", 2048)))
 allow = (m.SYNTH_SPEECH0, m.SYNTH_SPEECH0 + 12800)
 prompt = [256, 257] + list(b"user\nhello") + [258, 257]
 llm.generate_batch([prompt] * B, 8, 0.8, list(range(B)), allow=allow)

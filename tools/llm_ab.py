@@ -17,7 +17,7 @@ K = int(os.environ.get("AB_K", 3))
 wd = os.environ.get("MIOTTS_BENCH_DIR", "/tmp/miotts_bench")
 llm_path, _, _ = bench.ensure_files(wd, preset, 0, lambda: None)
 dev = m.Device(0)
-llm = m.Llm(dev, llm_path, 2048)
+llm = m.Llm(dev, llm_path, int(os.environ.get("AB_NCTX", 2048)))
 prompt = bench.prompt_tokens(bench.PROMPT)
 allow = (m.SYNTH_SPEECH0, m.SYNTH_SPEECH0 + 12800)
 CI = int(os.environ.get("AB_CI", 20))
