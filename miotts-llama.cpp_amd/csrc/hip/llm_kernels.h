@@ -185,6 +185,8 @@ void launch_batch_embed(const LlmDims &d, const QMat &tok_embd, const PrefillBuf
 // conv_out in place of 0..2; 10 attention + O (k_att_o, for 1 + 2), 11 the whole attention
 // block (k_layer_att, for 0 + 1 + 2), 12 the FFN pair (k_ffn, for 3 + 4), 13 the whole layer
 // (k_layer, for 11 + 12)) on stream s.
+// an empty one-workgroup launch (the timing reference of mio_hip_llm_time_kernel)
+void launch_nop(hipStream_t s);
 void launch_step_kernel(int which, const LlmDims &d, const LayerW *layers, int il, _Float16 *kcache,
                         _Float16 *vcache, const float *out_norm, const QMat &lm, const QMat &tok_embd,
                         const LlmBuffers &b, hipStream_t s);

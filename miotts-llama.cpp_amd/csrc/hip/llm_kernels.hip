@@ -580,6 +580,11 @@ int lm_head_blocks(const LlmDims &d) { const LlmDims l = lm_dims(d); return matv
 size_t matvec_lds(int K) { return smem_bytes(K); }
 
 
+// An empty one-workgroup launch: the reference of mio_hip_llm_time_kernel's launch timing (what
+// a launch costs the stream besides its own work)
+__global__ void k_nop() {}
+void launch_nop(hipStream_t s) { hipLaunchKernelGGL(k_nop, dim3(1), dim3(64), 0, s); }
+
 void launch_embed_token(const LlmDims &d, const QMat &tok_embd, const LlmBuffers &b, hipStream_t s) {
     hipLaunchKernelGGL(k_embed, dim3(1), dim3(ST), 0, s, d, tok_embd, b);
 }

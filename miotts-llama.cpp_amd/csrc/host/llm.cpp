@@ -1523,7 +1523,8 @@ struct DiagStateGuard {
 
 // Live timing of one kernel of the decode step (bench.py roofline): launches kernel
 // `which` (0 attn_in, 1 attention, 2 attn_out, 3 ffn_in, 4 ffn_down, 6 lm_head, 8 conv_in,
-// 9 conv_out) of layer kernel_layer() `iters` times on the runner's stream between HIP events, with the buffers and
+// 9 conv_out, 10-13 the fused launches) of layer kernel_layer() `iters` times on the runner's
+// stream between HIP events (MIO_TK_MODE below), with the buffers and
 // device state left by the last generate/eval. Returns the mean duration and the
 // algorithmic HBM bytes of one launch (weights of the matrices it streams + activations;
 // attention: F16 K and V rows of positions 0..pos (the row at pos is written, the rest
@@ -1591,32 +1592,67 @@ extern "C" int mio_hip_llm_time_kernel(mio_hip_llm *m, int which, int iters, flo
     MIO_HIP_CHECK(hipEventCreate(&e0));
     MIO_HIP_CHECK(hipEventCreate(&e1));
     hipStream_t s = m->d->stream;
-    // k_att_o's merge counter is zeroed by the k_ffn_in that follows it in a step: here a
-    // memset does it before every launch, and a loop of the memsets alone is subtracted
+    // The fused launches' hand-off counters are zeroed by the launch after them in a step: here
+    // a memset does it before every launch. MIO_TK_MODE (default 1): how the iters launches are
+    // timed with HIP events.
+    //   0: issued eagerly, minus an eager loop of the memsets alone (rounds 4-6; the host issues
+    //      a memset + launch pair in about the GPU time of one, so both loops are partly
+    //      host-paced: k_layer_att's figure moved 11.7-14.9 us between runs of one tree);
+    //   1: both loops captured as hipGraphs and replayed (GPU-paced, +-0.3 % between reps):
+    //      k_layer_att 12.1 us vs the eager rocprof mean 12.65 of a real step, k_ffn 10.65 vs
+    //      10.9, lm_head 46-48 vs 47.2 (profiles/r06/time_kernel_modes.txt);
+    //   2: as 1, with the reference loop launching an empty one-workgroup kernel (launch_nop)
+    //      after each memset: per launch = the kernel minus an empty launch (1.5-2 us below the
+    //      rocprof durations, which count a launch's dispatch).
+    static const int tk_mode = getenv("MIO_TK_MODE") ? atoi(getenv("MIO_TK_MODE")) : 1;
+    const bool fused = which >= 10;
     int *rdy = m->buf.att_cnt + mio::kRdyOff;
     const size_t rdy_bytes = (size_t)(mio::kAttCntInts - mio::kRdyOff) * sizeof(int);
-    auto launch = [&](bool fused, bool reset_only) {
+    // ref: 0 = the kernel itself, 1 = nothing (memset only), 2 = the empty launch
+    auto launch = [&](int ref) {
         if (fused) MIO_HIP_CHECK(hipMemsetAsync(rdy, 0, rdy_bytes, s));
-        if (!reset_only)
+        if (ref == 0)
             mio::launch_step_kernel(which, D, m->layers.data(), il, m->kc, m->vc, m->out_norm, m->lm, m->tok, m->buf,
                                     s);
+        else if (ref == 2)
+            mio::launch_nop(s);
         return MIO_OK;
     };
-    auto timed = [&](bool reset_only, float &ms) {
+    auto timed = [&](int ref, float &ms) {
+        hipGraphExec_t ge = nullptr;
+        if (tk_mode >= 1) {
+            hipGraph_t g = nullptr;
+            MIO_HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+            int rc = MIO_OK;
+            for (int i = 0; i < iters && rc == MIO_OK; ++i) rc = launch(ref);
+            const hipError_t ec = hipStreamEndCapture(s, &g);
+            if (rc) return rc;
+            MIO_HIP_CHECK(ec);
+            const hipError_t ei = hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
+            hipGraphDestroy(g);
+            MIO_HIP_CHECK(ei);
+            MIO_HIP_CHECK(hipGraphLaunch(ge, s));  // warm replay
+        }
         MIO_HIP_CHECK(hipEventRecord(e0, s));
-        for (int i = 0; i < iters; ++i)
-            if (int rc = launch(which >= 10, reset_only)) return rc;
+        if (ge) {
+            MIO_HIP_CHECK(hipGraphLaunch(ge, s));
+        } else {
+            for (int i = 0; i < iters; ++i)
+                if (int rc = launch(ref)) return rc;
+        }
         MIO_HIP_CHECK(hipEventRecord(e1, s));
         MIO_HIP_CHECK(hipEventSynchronize(e1));
         MIO_HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+        if (ge) hipGraphExecDestroy(ge);
         return MIO_OK;
     };
-    if (int rc = launch(which >= 10, false)) return rc;  // warm
-    float ms = 0, ms_reset = 0;
-    if (int rc = timed(false, ms)) return rc;
-    if (which >= 10) {
-        if (int rc = timed(true, ms_reset)) return rc;
-        ms = std::max(0.0f, ms - ms_reset);
+    if (int rc = launch(0)) return rc;  // warm
+    float ms = 0, ms_ref = 0;
+    if (int rc = timed(0, ms)) return rc;
+    const int ref = tk_mode == 2 ? 2 : (fused ? 1 : -1);
+    if (ref > 0) {
+        if (int rc = timed(ref, ms_ref)) return rc;
+        ms = std::max(0.0f, ms - ms_ref);
     }
     hipEventDestroy(e0), hipEventDestroy(e1);
     *avg_ms = ms / iters;

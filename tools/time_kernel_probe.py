@@ -21,7 +21,11 @@ dev = m.Device(0)
 llm = m.Llm(dev, path, 2048)
 allow = (m.SYNTH_SPEECH0, m.SYNTH_SPEECH0 + 12800)
 prompt = [256, 257] + list(b"user\nhello") + [258, 257]
+for _ in range(int(os.environ.get("PROBE_HEAVY", 0))):  # the bench's timed region before
+    llm.generate(prompt, 700, 0.8, 42, allow=allow)
 llm.generate(prompt, 400, 0.8, 42, allow=allow)
+if os.environ.get("PROBE_TL") == "1":  # bench.roofline takes the step timeline first
+    llm.timeline()
 for w in which:
     for r in range(int(os.environ.get("PROBE_REPS", 4))):
         ms, by = llm.time_kernel(w, 40)
