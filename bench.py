@@ -23,8 +23,10 @@ roofline: the decode-step kernel with the largest in-graph time per token (step 
 mio_hip_llm_timeline, after the timed region at decode position ~400 = the utterance's mean
 position and the PMC run's): achieved = its algorithmic bytes per launch (GGUF bytes of the matrices it streams +
 activations; attention: the F16 K/V rows of positions <= pos + q/k/v in + partial records
-out, mio_hip_llm_time_kernel) / its mean launch duration from HIP events around 40
-back-to-back launches on the runner's stream; peak = 8 TB/s HBM3E. `frac_in_graph` = the
+out, mio_hip_llm_time_kernel) / its mean launch duration from HIP events around a replayed
+graph of 40 back-to-back launches on the runner's stream (the fused launches: each behind a
+memset of their hand-off counters, minus a replayed graph of the memsets alone; GPU-paced,
+within 4 % of the eager rocprof means, profiles/r06/time_kernel_modes.txt); peak = 8 TB/s HBM3E. `frac_in_graph` = the
 same bytes over the in-graph span (first workgroup start -> last workgroup end,
 s_memrealtime; the timeline replays the diagnostic kernel instantiations). traffic = the same kernel's HBM bytes per launch
 from rocprofv3 PMC (FETCH_SIZE x 2 on gfx950 + WRITE_SIZE, profiles/pmc_traffic.json,
